@@ -1,0 +1,220 @@
+"""Benchmark: Resample + SumRange on UInt16 volumes, BASELINE.json's headline metric.
+
+One step = the metric pipeline on device-resident synthetic data:
+    Resample(R, S, Linear)      S = 512^3 UInt16  ->  R = 1024^3 UInt16
+    SumRange(D, R, B, 0, dims)  B, D = 1024^3 UInt16
+per GPU.  With N GPUs (torchrun, one process per GPU, RCCL) the volumes are Z-slab
+partitioned: global dst = 1024 x 1024 x (1024*N), source 512 x 512 x (512*N); every rank
+owns one 1024^3 dst slab and its 512^3 source slab (weak scaling; at N=8 the global dst has
+the voxel count of the 2048^3 config).  The exact z index table keeps every rank's reads in
+its own source slab for this ratio and format, so no plane crosses ranks (the exchange plan
+is still computed and executed -- it is empty).
+
+value = dst voxels of all ranks / wall time per step (Gvoxels/s).  roofline: the dominant
+kernel (SumRange: 6 B/voxel algorithmic) timed with HIP events on the compute stream.
+cpu_baseline: the oracle restatement (port, 1 thread) on a bounded sample of the same pipeline.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0   # MI355X spec (MI355X_MICROARCH.md: HBM3E 8.0 TB/s)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--dst", type=int, default=1024, help="per-GPU dst cube edge (source = dst/2)")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-dst", type=int, default=512, help="dst edge of the CPU-baseline sample")
+    return p.parse_args()
+
+
+def cpu_baseline(dst_edge):
+    """Oracle (C restatement of the reference serial path, 1 thread) on the same pipeline at
+    dst_edge^3; returns Gvoxels/s of dst voxels."""
+    import numpy as np
+    from oracle import binding as ob
+
+    s = dst_edge // 2
+    src = ob.Volume(ob.synth_codes((s, s, s), 5, 0x5EED), 5)
+    b = ob.Volume(ob.synth_codes((dst_edge,) * 3, 5, 0x5EED + 1), 5)
+    r = ob.Volume.zeros((dst_edge,) * 3, 5)
+    d = ob.Volume.zeros((dst_edge,) * 3, 5)
+    t0 = time.perf_counter()
+    ob.resample(r, src, 1)
+    ob.arith_range("Sum", d, r, b, (0, 0, 0), (dst_edge,) * 3)
+    dt = time.perf_counter() - t0
+    del np
+    return dst_edge ** 3 / dt / 1e9, dt
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import volkit_amd.volkit as vkt
+    from volkit_amd import slab
+    from volkit_amd._lib import lib, HipVolumeView_t
+    import ctypes as C
+
+    if lib.vktHipSetDevice(local) != 0:
+        raise RuntimeError(vkt.last_error())
+    # one stream for our kernels and torch's (events, RCCL) -> no cross-stream hazards
+    lib.vktHipSetComputeStream(C.c_void_p(torch.cuda.current_stream().cuda_stream))
+
+    ep = vkt.GetThreadExecutionPolicy()
+    ep.device = vkt.ExecutionPolicy.Device_GPU
+    vkt.SetThreadExecutionPolicy(ep)
+
+    E = args.dst
+    S = E // 2
+    UINT16, LINEAR = vkt.DataFormat_UInt16, vkt.FilterMode_Linear
+    dst_gdz, src_gdz = E * world, S * world
+    plan = slab.plan_resample(dst_gdz, src_gdz, world, rank, LINEAR, chain=False)
+    ls0, ls1 = plan.local_src
+    dz0, dz1 = plan.dst
+
+    # device-resident volumes (allocated on HBM directly: GPU policy at construction)
+    Sv = vkt.StructuredVolume(S, S, ls1 - ls0, UINT16)
+    Rv = vkt.StructuredVolume(E, E, dz1 - dz0, UINT16)
+    Bv = vkt.StructuredVolume(E, E, dz1 - dz0, UINT16)
+    Dv = vkt.StructuredVolume(E, E, dz1 - dz0, UINT16)
+    for k, v in enumerate((Sv, Bv)):
+        assert vkt.Synthesize(v, 0x5EED + k + 1000 * rank) == 0, vkt.last_error()
+    sview, rview, bview, dview = Sv.hip_view(), Rv.hip_view(), Bv.hip_view(), Dv.hip_view()
+    first = _lib_vec(0, 0, 0)
+    last = _lib_vec(E, E, dz1 - dz0)
+    plane_bytes = S * S * 2
+
+    def planes(g0, g1):
+        return slab.device_tensor(sview.data + (g0 - ls0) * plane_bytes, (g1 - g0) * plane_bytes)
+
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    t_res, t_sum = [], []
+
+    def step(timed):
+        if plan.recvs or plan.sends:
+            slab.exchange_planes(plan, planes)
+        if timed:
+            ev[0].record()
+        e1 = lib.vktHipResampleSlab(rview, sview, LINEAR, dst_gdz, dz0, src_gdz, ls0)
+        if timed:
+            ev[1].record()
+        e2 = lib.vktHipArithmeticRange(0, dview, rview, bview, first, last, _lib_vec(0, 0, 0))
+        if timed:
+            ev[2].record()
+        if e1 or e2:
+            raise RuntimeError(vkt.last_error())
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+        # per-step kernel times are read after the loop (events stay valid)
+        t_res.append((ev[0], ev[1]))
+        t_sum.append((ev[1], ev[2]))
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    res_ms = sum(a.elapsed_time(b) for a, b in t_res) / len(t_res)
+    sum_ms = sum(a.elapsed_time(b) for a, b in t_sum) / len(t_sum)
+    ms_per_step = elapsed * 1e3 / args.steps
+    vox_rank = E * E * (dz1 - dz0)
+    total_vox = E * E * dst_gdz
+    value = total_vox / (ms_per_step / 1e3) / 1e9
+
+    # algorithmic bytes per launch: SumRange 6 B/voxel; Resample
+    # N_src*2 + N_dst*2
+    sum_bytes = 6 * vox_rank
+    res_bytes = 2 * S * S * (ls1 - ls0) + 2 * vox_rank
+    pipe_bytes = sum_bytes + res_bytes
+    traffic = None
+    tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(tf):
+        try:
+            traffic = json.load(open(tf)).get("SumRange_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    out = {
+        "metric": "Gvoxels/s + achieved HBM GB/s, Resample+SumRange 1024^3 UInt16",
+        "value": round(value, 3),
+        "unit": "Gvoxels/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u16",
+        "data": "synthetic (splitmix64 codes, device-resident)",
+        "config": {
+            "workload": f"Resample {S}^3->{E}^3 UInt16 Linear + SumRange {E}^3 UInt16 per GPU",
+            "global_dst": [E, E, dst_gdz], "global_src": [S, S, src_gdz],
+            "parallelism": f"zslab{world}", "halo_planes_per_rank": plan.halo_planes,
+        },
+        "pipeline_hbm_gbs": round(pipe_bytes * world / (ms_per_step / 1e3) / 1e9, 1),
+        "kernels_ms": {"Resample": round(res_ms, 4), "SumRange": round(sum_ms, 4)},
+        "roofline": {
+            "kernel": "SumRange (arithmetic pointwise, UInt16)",
+            "bound": "hbm",
+            "achieved": round(sum_bytes / (sum_ms / 1e3) / 1e9, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(sum_bytes / (sum_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "resample_achieved": round(res_bytes / (res_ms / 1e3) / 1e9, 1),
+            "pipeline_frac": round(pipe_bytes / ((res_ms + sum_ms) / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+        },
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        gv, dt = cpu_baseline(args.cpu_dst)
+        out["cpu_baseline"] = {
+            "value": round(gv, 5), "unit": "Gvoxels/s", "cores": 1, "kind": "port",
+            "sample": f"oracle restatement of the reference serial path, Resample {args.cpu_dst // 2}^3->"
+                      f"{args.cpu_dst}^3 UInt16 Linear + SumRange {args.cpu_dst}^3, {dt:.1f} s, 1 thread of "
+                      f"{os.cpu_count()} host CPUs",
+        }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def _lib_vec(x, y, z):
+    from volkit_amd._lib import Vec3i_t
+    return Vec3i_t(x, y, z)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,386 @@
+// volkit.hpp -- C++ API of the MI355X-native volkit StructuredVolume core path.
+//
+// Source-compatible with the reference's include/cpp/vkt/*.hpp for the hot path:
+// same namespace, class names, overload sets, default arguments and member order
+// of ManagedBuffer / StructuredVolume (reference include/cpp/vkt/ManagedBuffer.hpp:50-56,
+// include/cpp/vkt/StructuredVolume.hpp:118-128).  Per-name forwarding headers in
+// include/cpp/vkt/ include this file, so `#include <vkt/StructuredVolume.hpp>` works.
+//
+// What differs by design (MI355X-first):
+//  * ManagedBuffer::migrate() moves bytes with hipMemcpyAsync on a side copy stream,
+//    ordered against the compute stream with events (volkit_amd/csrc/runtime/Memory.cpp).
+//  * The per-thread policy is thread_local (race-free; same observable semantics as the
+//    reference's unlocked global map, src/vkt/ExecutionPolicy.cpp:17).
+//  * Algorithms dispatched under Device::GPU run hand-written gfx950 kernels and return
+//    InvalidValue (instead of silently doing nothing) when a launch or allocation fails.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+
+#ifndef VKTAPI
+#define VKTAPI __attribute__((visibility("default")))
+#endif
+
+namespace vkt
+{
+    //--- common.hpp (reference include/cpp/vkt/common.hpp:10-68) --------------------------
+    typedef uint8_t Bool;
+    static constexpr Bool False = 0;
+    static constexpr Bool True = 1;
+
+    enum Error
+    {
+        InvalidValue = -1,
+        NoError = 0,
+        InvalidDataSource = 1,
+        ReadError = 2,
+        WriteError = 3,
+    };
+
+    enum class ColorFormat
+    {
+        Unspecified, R8, RG8, RGB8, RGBA8, R16UI, RG16UI, RGB16UI, RGBA16UI,
+        R32UI, RG32UI, RGB32UI, RGBA32UI, R32F, RG32F, RGB32F, RGBA32F, Count,
+    };
+
+    enum class DataFormat
+    {
+        Unspecified, Int8, Int16, Int32, UInt8, UInt16, UInt32, Float32, Count,
+    };
+
+    enum class OpenMode { Read, Write, ReadWrite };
+
+    //--- linalg.hpp (reference include/cpp/vkt/linalg.hpp) -------------------------------
+    struct Vec2f { float x, y; };
+    struct Vec3f { float x, y, z; };
+    struct Vec4f { float x, y, z, w; };
+    struct Vec2i { int x, y; };
+    struct Vec3i { int x, y, z; };
+    struct Vec4i { int x, y, z, w; };
+    struct Box2f { Vec2f min, max; };
+    struct Box3f { Vec3f min, max; };
+    struct Box2i { Vec2i min, max; };
+    struct Box3i { Vec3i min, max; };
+    struct Mat3f { Vec3f col0, col1, col2; };
+    struct Mat4f { Vec4f col0, col1, col2, col3; };
+    enum class Axis { X, Y, Z };
+
+    inline bool operator==(Vec2f const& a, Vec2f const& b) { return a.x == b.x && a.y == b.y; }
+    inline bool operator!=(Vec2f const& a, Vec2f const& b) { return !(a == b); }
+    inline bool operator==(Vec3i const& a, Vec3i const& b) { return a.x == b.x && a.y == b.y && a.z == b.z; }
+    inline bool operator!=(Vec3i const& a, Vec3i const& b) { return !(a == b); }
+
+    class StructuredVolume;
+
+    //--- ExecutionPolicy.hpp (reference include/cpp/vkt/ExecutionPolicy.hpp:47-102) -------
+    struct ExecutionPolicy
+    {
+        enum class Device { CPU, GPU, Unspecified };
+        enum class HostAPI { Serial, OpenMP, Auto };
+        // DeviceAPI::CUDA keeps value 0 for source/ABI compatibility and means "the GPU
+        // backend", which is HIP on this build; HIP is an alias of the same value.
+        enum class DeviceAPI { CUDA, Auto, HIP = CUDA };
+
+        Device device = Device::CPU;
+        HostAPI hostApi = HostAPI::Serial;
+        DeviceAPI deviceApi = DeviceAPI::CUDA;
+        Bool printPerformance = False;
+    };
+
+    VKTAPI void SetThreadExecutionPolicy(ExecutionPolicy policy);
+    VKTAPI ExecutionPolicy GetThreadExecutionPolicy();
+
+    //--- ManagedResource.hpp (reference include/cpp/vkt/ManagedResource.hpp:12-19) -------
+    typedef void* ManagedResource;
+    typedef uint32_t ResourceHandle;
+    VKTAPI ResourceHandle RegisterManagedResource(ManagedResource resource);
+    VKTAPI void UnregisterManagedResource(ResourceHandle handle);
+    VKTAPI ManagedResource GetManagedResource(ResourceHandle handle);
+
+    //--- Memory.hpp (reference include/cpp/vkt/Memory.hpp:15-30) -------------------------
+    enum class CopyKind { HostToHost, HostToDevice, DeviceToHost, DeviceToDevice };
+    VKTAPI void Allocate(void** ptr, std::size_t size);
+    VKTAPI void Free(void* ptr);
+    VKTAPI void Memcpy(void* dst, void const* src, std::size_t size, CopyKind ck);
+    VKTAPI void MemsetRange(void* dst, void const* src, std::size_t dstSize, std::size_t srcSize);
+
+    namespace detail
+    {
+        // Moves a buffer between address spaces when the thread's device differs from
+        // `last`; returns the new pointer.  Implemented in csrc/runtime/Memory.cpp.
+        VKTAPI void* MigrateBuffer(void* data, std::size_t bytes, ExecutionPolicy& last);
+        // Frees `data` under `owner`'s device (host free or hipFree).
+        VKTAPI void FreeOn(void* data, ExecutionPolicy const& owner);
+        VKTAPI void* AllocateOn(std::size_t bytes, ExecutionPolicy const& owner);
+        VKTAPI void CopyOn(void* dst, void const* src, std::size_t bytes, ExecutionPolicy const& owner);
+    }
+
+    //--- ManagedBuffer<T> (reference include/cpp/vkt/ManagedBuffer.hpp:21-276) -----------
+    // Deferred migration: data lives where it was last allocated/migrated; the next access
+    // under a different thread device moves it.  Moves copy-then-free like the reference
+    // (ManagedBuffer.hpp:91-107) so a moved-from buffer is empty, not aliased.
+    template <typename T>
+    class ManagedBuffer
+    {
+    public:
+        typedef T value_type;
+
+        ManagedBuffer(std::size_t size = 0) : data_(nullptr), size_(size)
+        {
+            allocate(size);
+            resourceHandle_ = RegisterManagedResource(this);
+        }
+
+        ManagedBuffer(ManagedBuffer& rhs)
+            : data_(nullptr), size_(rhs.size_), lastAllocationPolicy_(rhs.lastAllocationPolicy_)
+        {
+            rhs.migrate();
+            allocate(rhs.size_);
+            copy(rhs);
+            resourceHandle_ = RegisterManagedResource(this);
+        }
+
+        ManagedBuffer(ManagedBuffer&& rhs)
+            : data_(nullptr), size_(rhs.size_), lastAllocationPolicy_(rhs.lastAllocationPolicy_)
+        {
+            rhs.migrate();
+            allocate(rhs.size_);
+            copy(rhs);
+            resourceHandle_ = RegisterManagedResource(this);
+            rhs.release();
+        }
+
+        virtual ~ManagedBuffer()
+        {
+            UnregisterManagedResource(resourceHandle_);
+            deallocate();
+        }
+
+        ManagedBuffer& operator=(ManagedBuffer& rhs)
+        {
+            if (&rhs != this)
+            {
+                rhs.migrate();
+                deallocate();
+                size_ = rhs.size_;
+                allocate(rhs.size_);
+                copy(rhs);
+            }
+            return *this;
+        }
+
+        ManagedBuffer& operator=(ManagedBuffer&& rhs)
+        {
+            if (&rhs != this)
+            {
+                rhs.migrate();
+                deallocate();
+                size_ = rhs.size_;
+                allocate(rhs.size_);
+                copy(rhs);
+                rhs.release();
+            }
+            return *this;
+        }
+
+        ResourceHandle getResourceHandle() const { return resourceHandle_; }
+
+        //! If the thread's device changed since the last allocation, move the bytes there.
+        void migrate()
+        {
+            data_ = static_cast<T*>(detail::MigrateBuffer(data_, size_ * sizeof(T), lastAllocationPolicy_));
+        }
+
+    protected:
+        void allocate(std::size_t size)
+        {
+            lastAllocationPolicy_ = GetThreadExecutionPolicy();
+            size_ = size;
+            data_ = static_cast<T*>(detail::AllocateOn(size_ * sizeof(T), lastAllocationPolicy_));
+        }
+
+        void deallocate()
+        {
+            detail::FreeOn(data_, lastAllocationPolicy_);
+            data_ = nullptr;
+            lastAllocationPolicy_ = GetThreadExecutionPolicy();
+        }
+
+        void resize(std::size_t size)
+        {
+            migrate();
+            T* fresh = static_cast<T*>(detail::AllocateOn(size * sizeof(T), lastAllocationPolicy_));
+            std::size_t keep = (size < size_ ? size : size_) * sizeof(T);
+            if (keep > 0)
+                detail::CopyOn(fresh, data_, keep, lastAllocationPolicy_);
+            detail::FreeOn(data_, lastAllocationPolicy_);
+            data_ = fresh;
+            size_ = size;
+        }
+
+        void fill(T& value)
+        {
+            migrate();
+            MemsetRange(data_, &value, size_ * sizeof(T), sizeof(T));
+        }
+
+        void fill(T const& value) { fill(const_cast<T&>(value)); }
+
+        void copy(ManagedBuffer& rhs)
+        {
+            rhs.migrate();
+            std::size_t n = (size_ < rhs.size_ ? size_ : rhs.size_) * sizeof(T);
+            if (n > 0)
+                detail::CopyOn(data_, rhs.data_, n, lastAllocationPolicy_);
+        }
+
+        T* data_ = nullptr;
+        std::size_t size_ = 0;
+
+    private:
+        void release()
+        {
+            detail::FreeOn(data_, lastAllocationPolicy_);
+            data_ = nullptr;
+            size_ = 0;
+        }
+
+        ExecutionPolicy lastAllocationPolicy_ = {};
+        ResourceHandle resourceHandle_ = ResourceHandle(-1);
+    };
+
+    //--- StructuredVolume (reference include/cpp/vkt/StructuredVolume.hpp:34-132) ---------
+    // Dense x-fastest voxel array: byte offset of (x,y,z) = ((z*dimY + y)*dimX + x) * bpv.
+    class VKTAPI StructuredVolume : public ManagedBuffer<uint8_t>
+    {
+    public:
+        constexpr static uint8_t GetMaxBytesPerVoxel() { return 8; }
+
+        StructuredVolume();
+        StructuredVolume(int32_t dimX, int32_t dimY, int32_t dimZ, DataFormat dataFormat,
+                         float distX = 1.f, float distY = 1.f, float distZ = 1.f,
+                         float mappingLo = 0.f, float mappingHi = 1.f);
+        StructuredVolume(StructuredVolume& rhs) = default;
+        StructuredVolume(StructuredVolume&& rhs) = default;
+        StructuredVolume& operator=(StructuredVolume& rhs) = default;
+        StructuredVolume& operator=(StructuredVolume&& rhs) = default;
+
+        void setDims(int32_t dimX, int32_t dimY, int32_t dimZ);
+        void getDims(int32_t& dimX, int32_t& dimY, int32_t& dimZ);
+        void setDims(Vec3i dims);
+        Vec3i getDims() const;
+
+        void setDataFormat(DataFormat dataFormat);
+        DataFormat getDataFormat() const;
+
+        void setDist(float distX, float distY, float distZ);
+        void getDist(float& distX, float& distY, float& distZ);
+        void setDist(Vec3f dist);
+        Vec3f getDist() const;
+
+        void setVoxelMapping(float lo, float hi);
+        void getVoxelMapping(float& lo, float& hi);
+        void setVoxelMapping(Vec2f mapping);
+        Vec2f getVoxelMapping() const;
+
+        Box3f getDomainBounds() const;
+        Box3f getObjectBounds() const;
+
+        //! Raw pointer in the address space of the calling thread's device (migrates first)
+        uint8_t* getData();
+
+        // Host accessors.  Under the GPU policy the reference dereferences a device
+        // pointer on the host; here they move the single voxel with a synchronous copy.
+        void setValue(int32_t x, int32_t y, int32_t z, float value);
+        void getValue(int32_t x, int32_t y, int32_t z, float& value);
+        float getValue(int32_t x, int32_t y, int32_t z);
+        void setValue(Vec3i index, float value);
+        void getValue(Vec3i index, float& value);
+        float getValue(Vec3i index);
+        void setBytes(int32_t x, int32_t y, int32_t z, uint8_t const* data);
+        void getBytes(int32_t x, int32_t y, int32_t z, uint8_t* data);
+        void setBytes(Vec3i index, uint8_t const* data);
+        void getBytes(Vec3i index, uint8_t* data);
+
+        uint8_t getBytesPerVoxel() const;
+        std::size_t getSizeInBytes() const;
+
+    private:
+        Vec3i dims_;
+        DataFormat dataFormat_;
+        Vec3f dist_;
+        Vec2f voxelMapping_;
+        Vec3f haloSize_;
+
+        std::size_t linearIndex(int32_t x, int32_t y, int32_t z) const;
+        std::size_t linearIndex(Vec3i index) const;
+    };
+
+    //--- Voxel.hpp (reference include/cpp/vkt/Voxel.hpp:15-39) ---------------------------
+    struct VoxelView
+    {
+        uint8_t* bytes;
+        DataFormat dataFormat;
+        float mappingLo;
+        float mappingHi;
+    };
+    VKTAPI Error MapVoxel(uint8_t* dst, float value, DataFormat dataFormat, float mappingLo, float mappingHi);
+    VKTAPI Error UnmapVoxel(float& value, uint8_t const* src, DataFormat dataFormat, float mappingLo, float mappingHi);
+
+    //--- Fill.hpp (reference include/cpp/vkt/Fill.hpp:16-50, SV overloads) ---------------
+    VKTAPI Error Fill(StructuredVolume& volume, float value);
+    VKTAPI Error FillRange(StructuredVolume& volume, int32_t firstX, int32_t firstY, int32_t firstZ,
+                           int32_t lastX, int32_t lastY, int32_t lastZ, float value);
+    VKTAPI Error FillRange(StructuredVolume& volume, Vec3i first, Vec3i last, float value);
+
+    //--- Copy.hpp (reference include/cpp/vkt/Copy.hpp:14-37) ------------------------------
+    VKTAPI Error Copy(StructuredVolume& dst, StructuredVolume& src);
+    VKTAPI Error CopyRange(StructuredVolume& dst, StructuredVolume& src, int32_t firstX, int32_t firstY,
+                           int32_t firstZ, int32_t lastX, int32_t lastY, int32_t lastZ,
+                           int32_t dstOffsetX = 0, int32_t dstOffsetY = 0, int32_t dstOffsetZ = 0);
+    VKTAPI Error CopyRange(StructuredVolume& dst, StructuredVolume& src, Vec3i first, Vec3i last,
+                           Vec3i dstOffset = {0, 0, 0});
+
+    //--- Arithmetic.hpp (reference include/cpp/vkt/Arithmetic.hpp:31-299) ----------------
+#define VKT_DECLARE_ARITHMETIC_CPP_(NAME)                                                          \
+    VKTAPI Error NAME(StructuredVolume& dest, StructuredVolume& source1, StructuredVolume& source2); \
+    VKTAPI Error NAME##Range(StructuredVolume& dest, StructuredVolume& source1,                    \
+                             StructuredVolume& source2, int32_t firstX, int32_t firstY,            \
+                             int32_t firstZ, int32_t lastX, int32_t lastY, int32_t lastZ,          \
+                             int32_t dstOffsetX = 0, int32_t dstOffsetY = 0,                       \
+                             int32_t dstOffsetZ = 0);                                              \
+    VKTAPI Error NAME##Range(StructuredVolume& dest, StructuredVolume& source1,                    \
+                             StructuredVolume& source2, Vec3i first, Vec3i last,                   \
+                             Vec3i dstOffset = {0, 0, 0});
+    VKT_DECLARE_ARITHMETIC_CPP_(Sum)
+    VKT_DECLARE_ARITHMETIC_CPP_(Diff)
+    VKT_DECLARE_ARITHMETIC_CPP_(Prod)
+    VKT_DECLARE_ARITHMETIC_CPP_(Quot)
+    VKT_DECLARE_ARITHMETIC_CPP_(AbsDiff)
+    VKT_DECLARE_ARITHMETIC_CPP_(SafeSum)
+    VKT_DECLARE_ARITHMETIC_CPP_(SafeDiff)
+    VKT_DECLARE_ARITHMETIC_CPP_(SafeProd)
+    VKT_DECLARE_ARITHMETIC_CPP_(SafeQuot)
+    VKT_DECLARE_ARITHMETIC_CPP_(SafeAbsDiff)
+#undef VKT_DECLARE_ARITHMETIC_CPP_
+
+    //--- Transform.hpp (reference include/cpp/vkt/Transform.hpp:16-62) --------------------
+    typedef void (*TransformUnaryOp)(int32_t x, int32_t y, int32_t z, VoxelView voxel);
+    typedef void (*TransformBinaryOp)(int32_t x1, int32_t y1, int32_t z1, VoxelView voxel1, VoxelView voxel2);
+    VKTAPI Error Transform(StructuredVolume& volume, TransformUnaryOp unaryOp);
+    VKTAPI Error Transform(StructuredVolume& volume1, StructuredVolume& volume2, TransformBinaryOp binaryOp);
+    VKTAPI Error TransformRange(StructuredVolume& volume, int32_t firstX, int32_t firstY, int32_t firstZ,
+                                int32_t lastX, int32_t lastY, int32_t lastZ, TransformUnaryOp unaryOp);
+    VKTAPI Error TransformRange(StructuredVolume& volume, Vec3i first, Vec3i last, TransformUnaryOp unaryOp);
+    VKTAPI Error TransformRange(StructuredVolume& volume1, StructuredVolume& volume2, int32_t firstX,
+                                int32_t firstY, int32_t firstZ, int32_t lastX, int32_t lastY, int32_t lastZ,
+                                TransformBinaryOp binaryOp);
+    VKTAPI Error TransformRange(StructuredVolume& volume1, StructuredVolume& volume2, Vec3i first, Vec3i last,
+                                TransformBinaryOp binaryOp);
+
+    //--- Resample.hpp (reference include/cpp/vkt/Resample.hpp:14-31, SV->SV) ------------
+    enum class FilterMode { Nearest, Linear };
+    VKTAPI Error Resample(StructuredVolume& dst, StructuredVolume& src, FilterMode fm);
+
+} // vkt

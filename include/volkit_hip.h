@@ -1,0 +1,130 @@
+/*
+ * volkit_hip.h -- the HIP/gfx950 backend seam, as a plain C ABI.
+ *
+ * The reference plugs its GPU backend in by name pasting: VKT_LEGACY_CALL__(FUNC, ...)
+ * calls FUNC##_cuda(...) when the thread policy says Device::GPU
+ * (reference src/vkt/Callable.hpp:82-113).  Each vktHip* entry point below replaces
+ * one of those _cuda functions; it takes a plain voxel-array view (pointer + dims +
+ * format + mapping, the fields of the reference's kernel argument
+ * StructuredVolumeView, src/vkt/StructuredVolumeView.hpp:221-225) instead of C++
+ * objects, so it can be bound from C, ctypes, cgo or JNI without C++ types.
+ *
+ * All pointers in a view are DEVICE pointers (hipMalloc'ed, or any pointer valid on
+ * the current HIP device).  Work is enqueued on the backend's compute stream
+ * (vktHipGetComputeStream) and is NOT waited for unless async execution is switched
+ * off (vktHipSetAsyncExecution(0)); errors are returned, never ignored (the reference
+ * drops them, src/vkt/macros.hpp:10).  Out-of-bounds ranges are rejected with
+ * vktInvalidValue before any launch (in the reference they are undefined behaviour).
+ */
+#ifndef VOLKIT_HIP_H
+#define VOLKIT_HIP_H
+
+#include "volkit_c.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Kernel-argument view of one structured volume (reference StructuredVolumeView). */
+typedef struct {
+    uint8_t* data;       /* device pointer to dense x-fastest voxels */
+    int32_t dimX, dimY, dimZ;
+    int32_t dataFormat;  /* vktDataFormat value */
+    float mappingLo, mappingHi;
+} vktHipVolumeView_t;
+
+/* Arithmetic operator codes: order of reference src/vkt/Arithmetic_serial.hpp:47-258. */
+typedef enum {
+    vktHipOpSum, vktHipOpDiff, vktHipOpProd, vktHipOpQuot, vktHipOpAbsDiff,
+    vktHipOpSafeSum, vktHipOpSafeDiff, vktHipOpSafeProd, vktHipOpSafeQuot, vktHipOpSafeAbsDiff,
+    vktHipOpCount
+} vktHipArithmeticOp;
+
+/* ---- runtime / context (design intent of reference include/c/vkt/CudaContext.h:17-65,
+ *      which is declared there but never defined) ----------------------------------- */
+VKTAPI vktError vktHipSetDevice(int32_t device);        /* before first GPU use */
+VKTAPI vktError vktHipGetDevice(int32_t* device);
+VKTAPI vktError vktHipSetAsyncExecution(int32_t async);  /* 0: every call synchronises */
+VKTAPI vktError vktHipGetAsyncExecution(int32_t* async);
+/* Replace the compute stream (e.g. with torch.cuda.current_stream().cuda_stream);
+ * NULL restores the backend's own blocking stream. */
+VKTAPI vktError vktHipSetComputeStream(void* hipStream);
+VKTAPI vktError vktHipGetComputeStream(void** hipStream);
+VKTAPI vktError vktHipGetCopyStream(void** hipStream);
+VKTAPI vktError vktHipSynchronize(void);
+/* Last HIP error string seen by the backend (thread-local), "" if none. */
+VKTAPI const char* vktHipGetLastErrorString(void);
+/* Milliseconds of the most recent kernel launched by the calling thread, measured with
+ * hipEvents on the compute stream when timing is enabled (vktHipSetKernelTiming(1));
+ * this is how printPerformance is implemented. */
+VKTAPI vktError vktHipSetKernelTiming(int32_t enable);
+VKTAPI vktError vktHipGetLastKernelMs(float* ms);
+
+/* ---- memory: replaces Allocate_cuda/Free_cuda/MemsetRange_cuda
+ *      (reference src/vkt/Memory_cuda.hpp:16-31) and the cudaMemcpy of src/vkt/Memory.cpp:40-75 */
+VKTAPI vktError vktHipAllocate(void** ptr, size_t size);
+VKTAPI vktError vktHipFree(void* ptr);
+VKTAPI vktError vktHipMemcpy(void* dst, void const* src, size_t size, vktCopyKind ck);
+/* Repeat the `patternSize`-byte host pattern over `dstSize` device bytes (no device
+ * allocation per call, 64-bit grid; reference truncates at 2^32 elements, Memory_cuda.cu:40). */
+VKTAPI vktError vktHipMemsetRange(void* dst, void const* pattern, size_t dstSize, size_t patternSize);
+
+/* ---- algorithms (first/last/dstOffset are voxel coordinates, ranges half-open) ---- */
+
+/* replaces FillRange_cuda (reference src/vkt/Fill_cuda.hpp:13, Fill_cuda.cu:22-55);
+ * semantics of FillRange_serial (src/vkt/Fill_serial.hpp:20-26). */
+VKTAPI vktError vktHipFillRange(vktHipVolumeView_t volume, vktVec3i_t first, vktVec3i_t last, float value);
+
+/* replaces CopyRange_cuda (reference src/vkt/Copy_cuda.hpp:11-17); semantics of
+ * CopyRange_serial (src/vkt/Copy_serial.hpp:13-82): source index clamped to the
+ * source dims, dst index = x - first + dstOffset, bytewise iff format and mapping match. */
+VKTAPI vktError vktHipCopyRange(vktHipVolumeView_t dst, vktHipVolumeView_t src,
+                                vktVec3i_t first, vktVec3i_t last, vktVec3i_t dstOffset);
+
+/* replaces {Sum,...,SafeAbsDiff}Range_cuda (reference src/vkt/Arithmetic_cuda.hpp:10-98);
+ * semantics of ArithmeticOp (src/vkt/Arithmetic_serial.hpp:15-45): sources read at the
+ * absolute x, dest written at x + dstOffset, Safe* clamps to the dest mapping. */
+VKTAPI vktError vktHipArithmeticRange(vktHipArithmeticOp op, vktHipVolumeView_t dest,
+                                      vktHipVolumeView_t source1, vktHipVolumeView_t source2,
+                                      vktVec3i_t first, vktVec3i_t last, vktVec3i_t dstOffset);
+
+/* replaces Resample_cuda (reference src/vkt/Resample_cuda.hpp:12-17); semantics of
+ * Resample_serial (src/vkt/Resample_serial.hpp:26-71), including the same-dims
+ * conversion branch that the CUDA path lacks. */
+VKTAPI vktError vktHipResample(vktHipVolumeView_t dst, vktHipVolumeView_t src, vktFilterMode fm);
+
+/* Z-slab Resample for multi-GPU partitions (no reference counterpart):
+ * `dst` holds global dst planes [dstZ0, dstZ0 + dst.dimZ) of a volume whose global depth
+ * is dstGlobalDimZ; `src` holds global source planes [srcZ0, srcZ0 + src.dimZ) of a
+ * volume of global depth srcGlobalDimZ.  X/Y dims are global.  The planes the exact
+ * index table asks for (vktHipResampleSlabSourceRange) must be inside `src`. */
+VKTAPI vktError vktHipResampleSlab(vktHipVolumeView_t dst, vktHipVolumeView_t src, vktFilterMode fm,
+                                   int32_t dstGlobalDimZ, int32_t dstZ0,
+                                   int32_t srcGlobalDimZ, int32_t srcZ0);
+/* Source planes [*srcZBegin, *srcZEnd) that dst planes [dstZ0, dstZ1) read, for the
+ * given filter and formats (Linear with a non-integer-exact source reads the clamped
+ * z+1 neighbour plane too). */
+VKTAPI vktError vktHipResampleSlabSourceRange(int32_t dstGlobalDimZ, int32_t dstZ0, int32_t dstZ1,
+                                              int32_t srcGlobalDimZ, vktFilterMode fm,
+                                              int32_t needsNeighbours,
+                                              int32_t* srcZBegin, int32_t* srcZEnd);
+
+/* replaces TransformRange_cuda (reference src/vkt/Transform_cuda.hpp:12-30, an empty
+ * stub there): host callbacks cannot run on the GPU, so the range is staged to host,
+ * transformed in the serial order, and written back. */
+VKTAPI vktError vktHipTransformRange1(vktHipVolumeView_t volume, vktVec3i_t first, vktVec3i_t last,
+                                      vktTransformUnaryOp unaryOp);
+VKTAPI vktError vktHipTransformRange2(vktHipVolumeView_t volume1, vktHipVolumeView_t volume2,
+                                      vktVec3i_t first, vktVec3i_t last, vktVec3i_t volume2Offset,
+                                      vktTransformBinaryOp binaryOp);
+
+/* Synthetic benchmark/test input: byte i of the volume = byte (i % 8) of
+ * splitmix64(seed + (i / 8)) -- counter-based, so the oracle reproduces it exactly
+ * (oracle/vkt_oracle.c: vkt_oracle_synth). */
+VKTAPI vktError vktHipSynthesize(vktHipVolumeView_t volume, uint64_t seed);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* VOLKIT_HIP_H */

@@ -1,0 +1,144 @@
+"""TEST INFRASTRUCTURE ONLY -- numpy/ctypes binding of oracle/liboracle.so, the CPU
+restatement of the reference serial path (oracle/vkt_oracle.c).
+
+Imported only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg, always as
+the checker / CPU baseline, never as the thing measured or shipped.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "liboracle.so")
+
+CODE_DTYPE = {1: np.uint8, 2: np.uint16, 3: np.uint32, 4: np.uint8, 5: np.uint16, 6: np.uint32, 7: np.uint32}
+BPV = {1: 1, 2: 2, 3: 4, 4: 1, 5: 2, 6: 4, 7: 4}
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return LIB_PATH
+
+
+if not os.path.exists(LIB_PATH):
+    build()
+
+_lib = C.CDLL(LIB_PATH)
+_i3 = C.c_int32 * 3
+
+
+class _Vol(C.Structure):
+    _fields_ = [("data", C.POINTER(C.c_uint8)), ("dims", C.c_int32 * 3), ("fmt", C.c_int32),
+                ("lo", C.c_float), ("hi", C.c_float), ("nbytes", C.c_size_t)]
+
+
+_lib.vko_map.argtypes = [C.POINTER(C.c_uint8), C.c_float, C.c_int32, C.c_float, C.c_float]
+_lib.vko_unmap.argtypes = [C.POINTER(C.c_float), C.POINTER(C.c_uint8), C.c_int32, C.c_float, C.c_float]
+_lib.vko_fill_range.argtypes = [C.POINTER(_Vol), _i3, _i3, C.c_float]
+_lib.vko_copy_range.argtypes = [C.POINTER(_Vol), C.POINTER(_Vol), _i3, _i3, _i3]
+_lib.vko_arith_range.argtypes = [C.c_int32, C.POINTER(_Vol), C.POINTER(_Vol), C.POINTER(_Vol), _i3, _i3, _i3]
+_lib.vko_resample.argtypes = [C.POINTER(_Vol), C.POINTER(_Vol), C.c_int32]
+_lib.vko_resample_slab.argtypes = [C.POINTER(_Vol), C.POINTER(_Vol), C.c_int32, C.c_int32, C.c_int32,
+                                   C.c_int32, C.c_int32]
+_lib.vko_splitmix64.restype = C.c_uint64
+_lib.vko_splitmix64.argtypes = [C.c_uint64]
+_lib.vko_synth.argtypes = [C.POINTER(C.c_uint8), C.c_size_t, C.c_uint64]
+
+UNARY = C.CFUNCTYPE(None, C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_uint8), C.c_int32, C.c_float, C.c_float)
+BINARY = C.CFUNCTYPE(None, C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_uint8), C.c_int32, C.c_float, C.c_float,
+                     C.POINTER(C.c_uint8), C.c_int32, C.c_float, C.c_float)
+_lib.vko_transform_range1.argtypes = [C.POINTER(_Vol), _i3, _i3, UNARY]
+_lib.vko_transform_range2.argtypes = [C.POINTER(_Vol), C.POINTER(_Vol), _i3, _i3, _i3, BINARY]
+
+OPS = ["Sum", "Diff", "Prod", "Quot", "AbsDiff", "SafeSum", "SafeDiff", "SafeProd", "SafeQuot", "SafeAbsDiff"]
+
+
+class Volume:
+    """A host volume: `codes` is a (z, y, x) array of raw stored codes."""
+
+    def __init__(self, codes: np.ndarray, fmt: int, lo: float = 0.0, hi: float = 1.0):
+        self.fmt = int(fmt)
+        self.codes = np.ascontiguousarray(codes, dtype=CODE_DTYPE[self.fmt])
+        self.lo, self.hi = float(lo), float(hi)
+        z, y, x = self.codes.shape
+        self._s = _Vol(self.codes.ctypes.data_as(C.POINTER(C.c_uint8)), _i3(x, y, z), self.fmt, self.lo, self.hi,
+                       self.codes.nbytes)
+
+    @classmethod
+    def zeros(cls, dims, fmt, lo=0.0, hi=1.0, fill_byte=0):
+        x, y, z = dims
+        codes = np.empty((z, y, x), dtype=CODE_DTYPE[fmt])
+        codes.view(np.uint8)[...] = fill_byte
+        return cls(codes, fmt, lo, hi)
+
+    @property
+    def dims(self):
+        z, y, x = self.codes.shape
+        return (x, y, z)
+
+    @property
+    def ref(self):
+        return C.byref(self._s)
+
+
+def map_voxel(value: float, fmt: int, lo: float = 0.0, hi: float = 1.0) -> bytes:
+    buf = (C.c_uint8 * 8)()
+    _lib.vko_map(buf, value, fmt, lo, hi)
+    return bytes(buf[: BPV.get(fmt, 0)])
+
+
+def unmap_voxel(data: bytes, fmt: int, lo: float = 0.0, hi: float = 1.0) -> float:
+    buf = (C.c_uint8 * 8)(*bytes(data)[:8])
+    v = C.c_float(0.0)
+    _lib.vko_unmap(C.byref(v), buf, fmt, lo, hi)
+    return v.value
+
+
+def fill_range(v: Volume, first, last, value: float) -> None:
+    _lib.vko_fill_range(v.ref, _i3(*first), _i3(*last), value)
+
+
+def copy_range(dst: Volume, src: Volume, first, last, off=(0, 0, 0)) -> None:
+    _lib.vko_copy_range(dst.ref, src.ref, _i3(*first), _i3(*last), _i3(*off))
+
+
+def arith_range(op, dst: Volume, s1: Volume, s2: Volume, first, last, off=(0, 0, 0)) -> None:
+    code = OPS.index(op) if isinstance(op, str) else int(op)
+    _lib.vko_arith_range(code, dst.ref, s1.ref, s2.ref, _i3(*first), _i3(*last), _i3(*off))
+
+
+def resample(dst: Volume, src: Volume, filter_mode: int) -> None:
+    _lib.vko_resample(dst.ref, src.ref, filter_mode)
+
+
+def resample_slab(dst: Volume, src: Volume, filter_mode: int, dst_gdz: int, dst_z0: int, src_gdz: int,
+                  src_z0: int) -> None:
+    _lib.vko_resample_slab(dst.ref, src.ref, filter_mode, dst_gdz, dst_z0, src_gdz, src_z0)
+
+
+def transform_range1(v: Volume, first, last, fn) -> None:
+    cb = UNARY(lambda x, y, z, b, f, lo, hi: fn(x, y, z, b, f, lo, hi))
+    _lib.vko_transform_range1(v.ref, _i3(*first), _i3(*last), cb)
+
+
+def transform_range2(v1: Volume, v2: Volume, first, last, off, fn) -> None:
+    cb = BINARY(lambda x, y, z, b1, f1, lo1, hi1, b2, f2, lo2, hi2: fn(x, y, z, b1, b2))
+    _lib.vko_transform_range2(v1.ref, v2.ref, _i3(*first), _i3(*last), _i3(*off), cb)
+
+
+def synth(nbytes: int, seed: int) -> np.ndarray:
+    """Same bytes as vktHipSynthesize: byte i = byte i%8 of splitmix64(seed + i//8)."""
+    out = np.empty(nbytes, dtype=np.uint8)
+    if nbytes:
+        _lib.vko_synth(out.ctypes.data_as(C.POINTER(C.c_uint8)), nbytes, C.c_uint64(seed))
+    return out
+
+
+def synth_codes(dims, fmt, seed) -> np.ndarray:
+    x, y, z = dims
+    b = synth(x * y * z * BPV[fmt], seed)
+    return b.view(CODE_DTYPE[fmt]).reshape(z, y, x)

@@ -1,0 +1,367 @@
+/*
+ * vkt_oracle.c -- TEST INFRASTRUCTURE ONLY: CPU restatement of the volkit reference's
+ * serial StructuredVolume path (see vkt_oracle.h for the pinning status).
+ *
+ * Structure deliberately follows the reference: per-voxel accessors (get_value /
+ * set_value / get_bytes / set_bytes, reference src/vkt/StructuredVolume.cpp:155-296)
+ * driven by z->y->x loops with `!=` bounds (src/vkt/for_each.hpp:23-39), so that the
+ * timed CPU baseline keeps the reference's loop order and per-voxel call structure.
+ * The reference's migrate()/policy-lookup overhead per access is NOT reproduced.
+ *
+ * Build: gcc -O2 -fPIC -shared -ffp-contract=off (oracle/Makefile); no -march, like the
+ * reference's CMake build (which sets no flags).
+ */
+#include "vkt_oracle.h"
+
+#include <math.h>
+#include <string.h>
+
+/* ---- helpers: src/vkt/linalg.hpp:18-41 ------------------------------------------ */
+static float r_min(float a, float b) { return b < a ? b : a; }
+static float r_max(float a, float b) { return a < b ? b : a; }
+static float r_clamp(float x, float lo, float hi) { return r_max(lo, r_min(x, hi)); }
+static int32_t i_clamp(int32_t x, int32_t lo, int32_t hi)
+{
+    int32_t m = hi < x ? hi : x; /* clamp = max(lo, min(x, hi)) */
+    return lo < m ? m : lo;
+}
+static float r_lerp(float a, float b, float t) { return (1.0f - t) * a + t * b; }
+
+/* x86 cvttss2si semantics, as the reference's float->int16/int8 assignments compile
+ * (SURVEY.md Appendix A.1). */
+static int32_t cvtt_i32(float f)
+{
+    return (f >= -2147483648.0f && f < 2147483648.0f) ? (int32_t)f : INT32_MIN;
+}
+static int64_t cvtt_i64(float f)
+{
+    return (f >= -9223372036854775808.0f && f < 9223372036854775808.0f) ? (int64_t)f : INT64_MIN;
+}
+
+/* src/vkt/DataFormatInfo.hpp:34-47 */
+uint32_t vko_bytes_per_voxel(int32_t fmt)
+{
+    switch (fmt) {
+    case 1: case 4: return 1;
+    case 2: case 5: return 2;
+    case 3: case 6: case 7: return 4;
+    default: return 255;
+    }
+}
+
+/* MapVoxelImpl, src/vkt/VoxelMapping.hpp:15-95 (little endian). */
+void vko_map(uint8_t* dst, float value, int32_t fmt, float lo, float hi)
+{
+    value -= lo;
+    value /= hi - lo;
+    switch (fmt) {
+    case 2: { /* Int16, :28-38 */
+        uint32_t c = (uint32_t)cvtt_i32(value * 65535.999f - 32767.f);
+        dst[0] = (uint8_t)c;
+        dst[1] = (uint8_t)(c >> 8);
+        break;
+    }
+    case 4: /* UInt8, :41-46 */
+        dst[0] = (uint8_t)cvtt_i32(value * 255.999f);
+        break;
+    case 5: { /* UInt16, :48-59 */
+        uint32_t c = (uint32_t)cvtt_i32(value * 65535.999f);
+        dst[0] = (uint8_t)c;
+        dst[1] = (uint8_t)(c >> 8);
+        break;
+    }
+    case 6: { /* UInt32, :62-76 */
+        uint32_t c = (uint32_t)(uint64_t)cvtt_i64(value * 4294967295.999f);
+        dst[0] = (uint8_t)c;
+        dst[1] = (uint8_t)(c >> 8);
+        dst[2] = (uint8_t)(c >> 16);
+        dst[3] = (uint8_t)(c >> 24);
+        break;
+    }
+    case 7: { /* Float32, :79-94 */
+        uint32_t c;
+        memcpy(&c, &value, 4);
+        dst[0] = (uint8_t)c;
+        dst[1] = (uint8_t)(c >> 8);
+        dst[2] = (uint8_t)(c >> 16);
+        dst[3] = (uint8_t)(c >> 24);
+        break;
+    }
+    default: /* Int8, Int32, Unspecified: no case in the reference switch */
+        break;
+    }
+}
+
+/* UnmapVoxelImpl, src/vkt/VoxelMapping.hpp:98-177 (little endian); leaves *value
+ * untouched for formats without a case. */
+void vko_unmap(float* value, const uint8_t* src, int32_t fmt, float lo, float hi)
+{
+    switch (fmt) {
+    case 2: { /* :107-119 */
+        int16_t iv = (int16_t)(uint16_t)(src[0] | (src[1] << 8));
+        float f = (float)iv;
+        *value = r_lerp(lo, hi, (f + 32767.f) / 65535.999f);
+        break;
+    }
+    case 4: /* :122-127 */
+        *value = r_lerp(lo, hi, (float)src[0] / 255.999f);
+        break;
+    case 5: { /* :130-142 */
+        uint16_t iv = (uint16_t)(src[0] | (src[1] << 8));
+        *value = r_lerp(lo, hi, (float)iv / 65535.999f);
+        break;
+    }
+    case 6: { /* :145-160 */
+        uint32_t iv = (uint32_t)src[0] | ((uint32_t)src[1] << 8) | ((uint32_t)src[2] << 16) |
+                      ((uint32_t)src[3] << 24);
+        *value = r_lerp(lo, hi, (float)iv / 4294967295.999f);
+        break;
+    }
+    case 7: { /* :163-175 */
+        uint32_t iv = (uint32_t)src[0] | ((uint32_t)src[1] << 8) | ((uint32_t)src[2] << 16) |
+                      ((uint32_t)src[3] << 24);
+        memcpy(value, &iv, 4);
+        break;
+    }
+    default:
+        break;
+    }
+}
+
+/* ---- per-voxel accessors: src/vkt/StructuredVolume.cpp:155-317 -------------------- */
+static size_t lin_index(const vko_volume* v, int32_t x, int32_t y, int32_t z)
+{
+    size_t idx = (size_t)z * (size_t)v->dims[0] * (size_t)v->dims[1] + (size_t)y * (size_t)v->dims[0] + (size_t)x;
+    return idx * vko_bytes_per_voxel(v->fmt);
+}
+
+static float get_value(const vko_volume* v, int32_t x, int32_t y, int32_t z)
+{
+    float value = 0.f; /* StructuredVolume.cpp:196 */
+    vko_unmap(&value, v->data + lin_index(v, x, y, z), v->fmt, v->lo, v->hi);
+    return value;
+}
+
+static void set_value(vko_volume* v, int32_t x, int32_t y, int32_t z, float value)
+{
+    vko_map(v->data + lin_index(v, x, y, z), value, v->fmt, v->lo, v->hi);
+}
+
+static void get_bytes(const vko_volume* v, int32_t x, int32_t y, int32_t z, uint8_t* out)
+{
+    uint32_t bpv = vko_bytes_per_voxel(v->fmt);
+    size_t idx = lin_index(v, x, y, z);
+    for (uint32_t i = 0; i < bpv; ++i)
+        out[i] = v->data[idx + i];
+}
+
+static void set_bytes(vko_volume* v, int32_t x, int32_t y, int32_t z, const uint8_t* in)
+{
+    uint32_t bpv = vko_bytes_per_voxel(v->fmt);
+    size_t idx = lin_index(v, x, y, z);
+    for (uint32_t i = 0; i < bpv; ++i)
+        v->data[idx + i] = in[i];
+}
+
+/* Flat-index read used by sampleLinear's unclamped hi.x neighbour
+ * (src/vkt/StructuredVolumeView.hpp:93-107): the reference reads one voxel past the
+ * end of the buffer there (undefined); both this oracle and the HIP kernel clamp that
+ * single read to the last voxel. */
+static float get_value_flat(const vko_volume* v, size_t voxel)
+{
+    uint32_t bpv = vko_bytes_per_voxel(v->fmt);
+    size_t nvox = v->nbytes / bpv;
+    if (voxel >= nvox)
+        voxel = nvox - 1;
+    float value = 0.f;
+    vko_unmap(&value, v->data + voxel * bpv, v->fmt, v->lo, v->hi);
+    return value;
+}
+
+/* ---- FillRange_serial, src/vkt/Fill_serial.hpp:20-26 ----------------------------- */
+void vko_fill_range(vko_volume* v, const int32_t first[3], const int32_t last[3], float value)
+{
+    for (int32_t z = first[2]; z != last[2]; ++z)
+        for (int32_t y = first[1]; y != last[1]; ++y)
+            for (int32_t x = first[0]; x != last[0]; ++x)
+                set_value(v, x, y, z, value);
+}
+
+/* ---- CopyRange_serial, src/vkt/Copy_serial.hpp:13-82 ----------------------------- */
+void vko_copy_range(vko_volume* dst, vko_volume* src, const int32_t first[3], const int32_t last[3],
+                    const int32_t off[3])
+{
+    int bytewise = dst->fmt == src->fmt && dst->lo == src->lo && dst->hi == src->hi; /* :21-22 */
+    uint8_t voxel[8];
+    for (int32_t z = first[2]; z != last[2]; ++z)
+        for (int32_t y = first[1]; y != last[1]; ++y)
+            for (int32_t x = first[0]; x != last[0]; ++x) {
+                int32_t sx = i_clamp(x, 0, src->dims[0] - 1);
+                int32_t sy = i_clamp(y, 0, src->dims[1] - 1);
+                int32_t sz = i_clamp(z, 0, src->dims[2] - 1);
+                int32_t dx = x - first[0] + off[0];
+                int32_t dy = y - first[1] + off[1];
+                int32_t dz = z - first[2] + off[2];
+                /* the reference repeats this per byte of the voxel (:34,:63); idempotent */
+                if (bytewise) {
+                    get_bytes(src, sx, sy, sz, voxel);
+                    set_bytes(dst, dx, dy, dz, voxel);
+                } else {
+                    set_value(dst, dx, dy, dz, get_value(src, sx, sy, sz));
+                }
+            }
+}
+
+/* ---- ArithmeticOp + lambdas, src/vkt/Arithmetic_serial.hpp:15-258 ---------------- */
+static float apply_op(int32_t op, float f1, float f2, float lo, float hi)
+{
+    switch (op) {
+    case 0: return f1 + f2;                                /* :63 */
+    case 1: return f1 - f2;                                /* :83 */
+    case 2: return f1 * f2;                                /* :103 */
+    case 3: return f1 / f2;                                /* :123 */
+    case 4: return fabsf(f1 - f2);                         /* :143 */
+    case 5: return r_clamp(f1 + f2, lo, hi);               /* :156-166 */
+    case 6: return r_clamp(f1 - f2, lo, hi);
+    case 7: return r_clamp(f1 * f2, lo, hi);
+    case 8: return r_clamp(f1 / f2, lo, hi);
+    case 9: return r_clamp(fabsf(f1 - f2), lo, hi);
+    default: return 0.f;
+    }
+}
+
+void vko_arith_range(int32_t op, vko_volume* dst, vko_volume* s1, vko_volume* s2, const int32_t first[3],
+                     const int32_t last[3], const int32_t off[3])
+{
+    float lo = dst->lo, hi = dst->hi;
+    for (int32_t z = first[2]; z != last[2]; ++z)
+        for (int32_t y = first[1]; y != last[1]; ++y)
+            for (int32_t x = first[0]; x != last[0]; ++x) {
+                float v1 = get_value(s1, x, y, z);
+                float v2 = get_value(s2, x, y, z);
+                set_value(dst, x + off[0], y + off[1], z + off[2], apply_op(op, v1, v2, lo, hi));
+            }
+}
+
+/* ---- Resample_serial (SV->SV), src/vkt/Resample_serial.hpp:26-71 ----------------- */
+static int32_t src_index(int32_t d, int32_t dd, int32_t sd)
+{
+    /* :60-62 then the implicit int32 conversion of sampleLinear's parameters (:65) or
+     * the explicit (int32_t) cast (:67): f32 divide, f32 multiply, truncate. */
+    float s = (float)d / (float)dd * (float)sd;
+    return (int32_t)s;
+}
+
+/* sampleLinear(int32_t,int32_t,int32_t), src/vkt/StructuredVolumeView.hpp:80-119, with
+ * z given in slab-local planes (local = global - src_z0). */
+static float sample_linear(const vko_volume* src, int32_t x, int32_t y, int32_t zg, int32_t src_gdz,
+                           int32_t src_z0)
+{
+    float xf1 = x - 0.f, yf1 = y - 0.f, zf1 = zg - 0.f;
+    float xf2 = x + 1.f, yf2 = y + 1.f, zf2 = zg + 1.f;
+    int32_t lox = (int32_t)xf1, loy = (int32_t)yf1, loz = (int32_t)zf1;
+    int32_t hix = (int32_t)xf2, hiy = (int32_t)yf2, hiz = (int32_t)zf2;
+    lox = i_clamp(lox, 0, src->dims[0] - 1); /* :93-99: lo.x, lo.y, hi.y, hi.z only */
+    loy = i_clamp(loy, 0, src->dims[1] - 1);
+    hiy = i_clamp(hiy, 0, src->dims[1] - 1);
+    hiz = i_clamp(hiz, 0, src_gdz - 1);
+    float fx = xf1 - lox, fy = yf1 - loy, fz = zf1 - loz;
+    size_t dx = (size_t)src->dims[0], plane = dx * (size_t)src->dims[1];
+    size_t zl0 = (size_t)(loz - src_z0), zl1 = (size_t)(hiz - src_z0);
+#define FLAT(X, Y, Z) get_value_flat(src, (Z) * plane + (size_t)(Y) * dx + (size_t)(X))
+    float v0 = FLAT(lox, loy, zl0), v1 = FLAT(hix, loy, zl0);
+    float v2 = FLAT(lox, hiy, zl0), v3 = FLAT(hix, hiy, zl0);
+    float v4 = FLAT(lox, loy, zl1), v5 = FLAT(hix, loy, zl1);
+    float v6 = FLAT(lox, hiy, zl1), v7 = FLAT(hix, hiy, zl1);
+#undef FLAT
+    return r_lerp(r_lerp(r_lerp(v0, v1, fx), r_lerp(v2, v3, fx), fy),
+                  r_lerp(r_lerp(v4, v5, fx), r_lerp(v6, v7, fx), fy), fz);
+}
+
+void vko_resample_slab(vko_volume* dst, vko_volume* src, int32_t filter, int32_t dst_gdz, int32_t dst_z0,
+                       int32_t src_gdz, int32_t src_z0)
+{
+    int32_t ddx = dst->dims[0], ddy = dst->dims[1];
+    int32_t sdx = src->dims[0], sdy = src->dims[1];
+    if (ddx == sdx && ddy == sdy && dst_gdz == src_gdz) {
+        /* same-dims branch, :32-48: per-voxel re-encode, no index math */
+        for (int32_t z = 0; z != dst->dims[2]; ++z)
+            for (int32_t y = 0; y != ddy; ++y)
+                for (int32_t x = 0; x != ddx; ++x)
+                    set_value(dst, x, y, z, get_value(src, x, y, z + dst_z0 - src_z0));
+        return;
+    }
+    for (int32_t z = 0; z != dst->dims[2]; ++z) {
+        int32_t sz = src_index(z + dst_z0, dst_gdz, src_gdz);
+        for (int32_t y = 0; y != ddy; ++y) {
+            int32_t sy = src_index(y, ddy, sdy);
+            for (int32_t x = 0; x != ddx; ++x) {
+                int32_t sx = src_index(x, ddx, sdx);
+                float value;
+                if (filter == 1)
+                    value = sample_linear(src, sx, sy, sz, src_gdz, src_z0);
+                else
+                    value = get_value(src, sx, sy, sz - src_z0);
+                set_value(dst, x, y, z, value);
+            }
+        }
+    }
+}
+
+void vko_resample(vko_volume* dst, vko_volume* src, int32_t filter)
+{
+    vko_resample_slab(dst, src, filter, dst->dims[2], 0, src->dims[2], 0);
+}
+
+/* ---- TransformRange_serial, src/vkt/Transform_serial.hpp:15-101 ------------------ */
+void vko_transform_range1(vko_volume* v, const int32_t first[3], const int32_t last[3], vko_unary_op op)
+{
+    for (int32_t z = first[2]; z != last[2]; ++z)
+        for (int32_t y = first[1]; y != last[1]; ++y)
+            for (int32_t x = first[0]; x != last[0]; ++x) {
+                uint8_t bytes[8];
+                memset(bytes, 0, sizeof(bytes));
+                get_bytes(v, x, y, z, bytes);
+                op(x, y, z, bytes, v->fmt, v->lo, v->hi);
+                set_bytes(v, x, y, z, bytes);
+            }
+}
+
+void vko_transform_range2(vko_volume* v1, vko_volume* v2, const int32_t first[3], const int32_t last[3],
+                          const int32_t off[3], vko_binary_op op)
+{
+    for (int32_t z = first[2]; z != last[2]; ++z)
+        for (int32_t y = first[1]; y != last[1]; ++y)
+            for (int32_t x = first[0]; x != last[0]; ++x) {
+                uint8_t b1[8], b2[8];
+                memset(b1, 0, sizeof(b1));
+                memset(b2, 0, sizeof(b2));
+                get_bytes(v1, x, y, z, b1);
+                get_bytes(v2, x + off[0], y + off[1], z + off[2], b2);
+                op(x, y, z, b1, v1->fmt, v1->lo, v1->hi, b2, v2->fmt, v2->lo, v2->hi);
+                set_bytes(v1, x, y, z, b1);
+                set_bytes(v2, x + off[0], y + off[1], z + off[2], b2);
+            }
+}
+
+/* ---- synthetic input -------------------------------------------------------------- */
+uint64_t vko_splitmix64(uint64_t x)
+{
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+void vko_synth(uint8_t* data, size_t nbytes, uint64_t seed)
+{
+    size_t words = nbytes / 8;
+    for (size_t w = 0; w < words; ++w) {
+        uint64_t r = vko_splitmix64(seed + w);
+        memcpy(data + 8 * w, &r, 8);
+    }
+    if (nbytes % 8) {
+        uint64_t r = vko_splitmix64(seed + words);
+        memcpy(data + 8 * words, &r, nbytes % 8);
+    }
+}

@@ -1,0 +1,264 @@
+"""Parity of the HIP/gfx950 path (through the public C ABI) with the CPU oracle on seeded
+inputs: every op, data format and mapping of the hot path, ragged dims, ranges that need
+clamping, offsets, and the reference's numeric traps.  Integer outputs must be bit-exact;
+Float32 outputs are bit-exact too except that any NaN matches any NaN (payload bits of NaNs
+produced by x86 SSE and gfx950 VALU arithmetic are not compared -- see DESIGN.md §3).
+"""
+import numpy as np
+import pytest
+
+from backends import CODE_DTYPE, GpuBackend, OracleBackend, codes_of
+
+pytestmark = pytest.mark.gpu
+
+MAPPINGS = [(0.0, 1.0), (-1.0, 3.0), (0.25, 7.5)]
+INT_FMTS = [4, 5, 2, 6]        # UInt8, UInt16, Int16, UInt32
+ALL_FMTS = INT_FMTS + [7, 1, 3]  # + Float32, Int8, Int32 (no-write/zero-read formats)
+OPS = ["Sum", "Diff", "Prod", "Quot", "AbsDiff", "SafeSum", "SafeDiff", "SafeProd", "SafeQuot", "SafeAbsDiff"]
+
+
+@pytest.fixture(scope="module")
+def g():
+    return GpuBackend()
+
+
+@pytest.fixture(scope="module")
+def o():
+    return OracleBackend()
+
+
+def rand_codes(rng, fmt, shape, floats="mixed"):
+    dt = CODE_DTYPE[fmt]
+    if fmt == 7:
+        if floats == "bits":
+            return rng.integers(0, 2**32, size=shape, dtype=np.uint64).astype(np.uint32)
+        vals = rng.uniform(-0.5, 1.5, size=shape).astype(np.float32)
+        flat = vals.reshape(-1)
+        specials = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 1e-40, -1e-40, 3e38, 1.0], dtype=np.float32)
+        idx = rng.choice(flat.size, size=min(flat.size, 2 * len(specials)), replace=False)
+        flat[idx] = np.resize(specials, idx.size)
+        return vals.view(np.uint32)
+    info = np.iinfo(dt)
+    return rng.integers(0, int(info.max) + 1, size=shape, dtype=np.uint64).astype(dt)
+
+
+def assert_codes_equal(out, ref, fmt, what=""):
+    if fmt == 7:
+        fo, fr = out.view(np.float32), ref.view(np.float32)
+        nan_o, nan_r = np.isnan(fo), np.isnan(fr)
+        bad = (nan_o != nan_r) | (~nan_r & (out != ref))
+    else:
+        bad = out != ref
+    n = int(np.count_nonzero(bad))
+    if n:
+        i = tuple(np.argwhere(bad)[0])
+        raise AssertionError(f"{what}: {n} mismatching voxels, first at zyx={i}: gpu={out[i]!r} ref={ref[i]!r}")
+
+
+# ---- Fill -----------------------------------------------------------------------------
+@pytest.mark.parametrize("fmt", ALL_FMTS)
+@pytest.mark.parametrize("mapping", MAPPINGS[:2])
+def test_fill_range(g, o, fmt, mapping):
+    rng = np.random.default_rng(fmt)
+    dims = (37, 23, 11)
+    init = rand_codes(rng, fmt, (11, 23, 37))
+    for value in (0.0, 0.1, 0.5, 1.0, 1.5, -0.25):
+        for first, last in (((0, 0, 0), dims), ((3, 2, 1), (30, 20, 9)), ((5, 5, 5), (6, 6, 6)), ((4, 4, 4), (4, 9, 9))):
+            out = g.fill_range(fmt, mapping, dims, init.copy(), first, last, value)
+            ref = o.fill_range(fmt, mapping, dims, init.copy(), first, last, value)
+            assert_codes_equal(out, ref, fmt, f"fill fmt={fmt} v={value} {first}->{last}")
+
+
+# ---- Copy -----------------------------------------------------------------------------
+@pytest.mark.parametrize("sfmt,dfmt", [(4, 4), (5, 5), (7, 7), (5, 4), (4, 7), (7, 5), (2, 6)])
+def test_copy_range(g, o, sfmt, dfmt):
+    rng = np.random.default_rng(11 * sfmt + dfmt)
+    src = rand_codes(rng, sfmt, (20, 24, 32))      # dims (32, 24, 20)
+    for smap, dmap in (((0.0, 1.0), (0.0, 1.0)), ((0.0, 1.0), (-1.0, 3.0))):
+        for first, last, off in (((0, 0, 0), (32, 24, 20), (0, 0, 0)),        # whole, vector path
+                                 ((10, 10, 10), (34, 34, 34), (0, 0, 0)),     # CoreAlgorithms.c: clamps
+                                 ((-3, -2, -1), (8, 9, 5), (2, 1, 3)),        # negative first: clamps
+                                 ((8, 0, 4), (24, 24, 12), (0, 0, 0))):       # partial rows, aligned
+            n = [l - f for f, l in zip(first, last)]
+            dd = (max(n[0] + off[0], 24), max(n[1] + off[1], 24), max(n[2] + off[2], 24))
+            init = rand_codes(rng, dfmt, (dd[2], dd[1], dd[0]))
+            out = g.copy_range(dfmt, dmap, dd, init.copy(), sfmt, smap, src, first, last, off)
+            ref = o.copy_range(dfmt, dmap, dd, init.copy(), sfmt, smap, src, first, last, off)
+            assert_codes_equal(out, ref, dfmt, f"copy {sfmt}->{dfmt} {smap}->{dmap} {first}->{last}+{off}")
+
+
+# ---- Arithmetic -------------------------------------------------------------------------
+@pytest.mark.parametrize("op", OPS)
+@pytest.mark.parametrize("fmt", [4, 5, 7, 2, 6])
+def test_arithmetic_same_format(g, o, op, fmt):
+    rng = np.random.default_rng(hash((op, fmt)) % 2**32)
+    for mapping in MAPPINGS:
+        maps = [mapping] * 3
+        a = rand_codes(rng, fmt, (16, 16, 16))
+        b = rand_codes(rng, fmt, (16, 16, 16))
+        # whole volume (vector path)
+        d0 = rand_codes(rng, fmt, (16, 16, 16))
+        out = g.arith(op, [fmt] * 3, maps, a, b, d0.copy(), (0, 0, 0), (16, 16, 16), (0, 0, 0))
+        ref = o.arith(op, [fmt] * 3, maps, a, b, d0.copy(), (0, 0, 0), (16, 16, 16), (0, 0, 0))
+        assert_codes_equal(out, ref, fmt, f"{op} fmt={fmt} map={mapping} whole")
+        # SURVEY Appendix C range case: first=(3,2,1) last=(13,11,9) off=(1,0,2) into a 20^3 dst of 0x5A
+        dinit = np.empty((20, 20, 20), dtype=CODE_DTYPE[fmt])
+        dinit.view(np.uint8)[...] = 0x5A
+        out = g.arith(op, [fmt] * 3, maps, a, b, dinit.copy(), (3, 2, 1), (13, 11, 9), (1, 0, 2))
+        ref = o.arith(op, [fmt] * 3, maps, a, b, dinit.copy(), (3, 2, 1), (13, 11, 9), (1, 0, 2))
+        assert_codes_equal(out, ref, fmt, f"{op} fmt={fmt} map={mapping} range")
+
+
+@pytest.mark.parametrize("op", ["Sum", "SafeDiff", "Quot"])
+def test_arithmetic_mixed_formats(g, o, op):
+    rng = np.random.default_rng(99)
+    for fd, f1, f2 in ((4, 5, 7), (7, 4, 5), (5, 2, 4), (6, 7, 5), (1, 5, 5), (5, 3, 4)):
+        maps = [(-1.0, 3.0), (0.0, 1.0), (0.25, 7.5)]
+        a = rand_codes(rng, f1, (9, 10, 17))
+        b = rand_codes(rng, f2, (9, 10, 17))
+        d = rand_codes(rng, fd, (9, 10, 17))
+        out = g.arith(op, [fd, f1, f2], maps, a, b, d.copy(), (1, 2, 0), (17, 10, 9), (0, 0, 0))
+        ref = o.arith(op, [fd, f1, f2], maps, a, b, d.copy(), (1, 2, 0), (17, 10, 9), (0, 0, 0))
+        assert_codes_equal(out, ref, fd, f"{op} {f1},{f2}->{fd}")
+
+
+def test_arithmetic_ragged_whole_volume(g, o):
+    # odd dims: collapsed single row with a scalar tail
+    rng = np.random.default_rng(5)
+    for fmt in (4, 5, 7):
+        a = rand_codes(rng, fmt, (11, 23, 37))
+        b = rand_codes(rng, fmt, (11, 23, 37))
+        d = rand_codes(rng, fmt, (11, 23, 37))
+        out = g.arith("SafeSum", [fmt] * 3, [(0.0, 1.0)] * 3, a, b, d.copy(), (0, 0, 0), (37, 23, 11), (0, 0, 0))
+        ref = o.arith("SafeSum", [fmt] * 3, [(0.0, 1.0)] * 3, a, b, d.copy(), (0, 0, 0), (37, 23, 11), (0, 0, 0))
+        assert_codes_equal(out, ref, fmt, f"ragged fmt={fmt}")
+
+
+def test_arithmetic_float_bit_patterns(g, o):
+    # every float bit pattern class, including NaN payloads, denormals and infinities
+    rng = np.random.default_rng(17)
+    a = rand_codes(rng, 7, (8, 16, 64), floats="bits")
+    b = rand_codes(rng, 7, (8, 16, 64), floats="bits")
+    for op in OPS:
+        for mapping in ((0.0, 1.0), (-1.0, 3.0)):
+            d = np.zeros((8, 16, 64), np.uint32)
+            out = g.arith(op, [7] * 3, [mapping] * 3, a, b, d.copy(), (0, 0, 0), (64, 16, 8), (0, 0, 0))
+            ref = o.arith(op, [7] * 3, [mapping] * 3, a, b, d.copy(), (0, 0, 0), (64, 16, 8), (0, 0, 0))
+            assert_codes_equal(out, ref, 7, f"{op} f32 bits {mapping}")
+
+
+# ---- Resample -------------------------------------------------------------------------
+RESAMPLE_PAIRS = [((10, 1, 1), (7, 1, 1)), ((4, 4, 4), (8, 8, 8)), ((16, 16, 16), (32, 32, 32)),
+                  ((37, 23, 11), (64, 40, 19)), ((64, 37, 9), (37, 64, 5)), ((22, 22, 22), (22, 22, 22)),
+                  ((33, 33, 33), (16, 16, 16)), ((32, 16, 8), (64, 32, 16)), ((24, 8, 8), (96, 8, 4)),
+                  ((10, 9, 8), (7, 6, 5)), ((5, 7, 3), (13, 19, 11))]
+FORMAT_PAIRS = [(4, 4), (5, 5), (7, 7), (4, 7), (7, 5), (5, 4), (2, 2)]
+
+
+@pytest.mark.parametrize("src_dims,dst_dims", RESAMPLE_PAIRS)
+@pytest.mark.parametrize("sfmt,dfmt", FORMAT_PAIRS)
+def test_resample(g, o, src_dims, dst_dims, sfmt, dfmt):
+    rng = np.random.default_rng(abs(hash((src_dims, dst_dims, sfmt, dfmt))) % 2**32)
+    src = rand_codes(rng, sfmt, src_dims[::-1])
+    for smap, dmap in (((0.0, 1.0), (0.0, 1.0)), ((-1.0, 3.0), (0.0, 1.0))):
+        for fm in (0, 1):
+            out = g.resample(dfmt, dmap, dst_dims, sfmt, smap, src, fm)
+            ref = o.resample(dfmt, dmap, dst_dims, sfmt, smap, src, fm)
+            assert_codes_equal(out, ref, dfmt, f"resample {src_dims}->{dst_dims} {sfmt}->{dfmt} fm={fm} {smap}")
+
+
+def test_resample_float_bit_patterns(g, o):
+    rng = np.random.default_rng(23)
+    src = rand_codes(rng, 7, (6, 10, 16), floats="bits")
+    for fm in (0, 1):
+        out = g.resample(7, (0.0, 1.0), (32, 20, 12), 7, (0.0, 1.0), src, fm)
+        ref = o.resample(7, (0.0, 1.0), (32, 20, 12), 7, (0.0, 1.0), src, fm)
+        assert_codes_equal(out, ref, 7, f"f32 bits fm={fm}")
+
+
+# ---- Transform -------------------------------------------------------------------------
+def test_transform_examples(g):
+    """Unary checkerboard of reference src/examples/Arithmetic.cpp:8-21 and binary OR of
+    src/examples/CoreAlgorithms.c:20-24, through the C ABI with the GPU policy."""
+    vkt = g.vkt
+    n = 32
+
+    def checker(level):
+        def op(x, y, z, v):
+            x, y, z = x >> level, y >> level, z >> level
+            li = z * 32 * 32 + y * 32 + x
+            v.bytes[0] = 128 if ((y % 2 == z % 2 and li % 2 == 0) or (y % 2 != z % 2 and li % 2 == 1)) else 0
+        return op
+
+    v1 = g.volume(np.zeros((n, n, n), np.uint8), 4, (0.0, 1.0))
+    g._run(lambda: vkt.Transform(v1, checker(3)))
+    got = v1.to_numpy()
+    z, y, x = np.meshgrid(np.arange(n), np.arange(n), np.arange(n), indexing="ij")
+    xs, ys, zs = x >> 3, y >> 3, z >> 3
+    li = zs * 1024 + ys * 32 + xs
+    exp = np.where(((ys % 2 == zs % 2) & (li % 2 == 0)) | ((ys % 2 != zs % 2) & (li % 2 == 1)), 128, 0)
+    np.testing.assert_array_equal(got, exp.astype(np.uint8))
+
+    a = g.volume(np.random.default_rng(1).integers(0, 256, (8, 8, 8), dtype=np.uint8), 4, (0.0, 1.0))
+    b = g.volume(np.random.default_rng(2).integers(0, 256, (8, 8, 8), dtype=np.uint8), 4, (0.0, 1.0))
+    ea = a.to_numpy() | b.to_numpy()
+
+    def orop(x, y, z, v1, v2):
+        v1.bytes[0] |= v2.bytes[0]
+        v2.bytes[0] = v1.bytes[0]
+
+    g._run(lambda: vkt.Transform(a, b, orop))
+    np.testing.assert_array_equal(a.to_numpy(), ea)
+    np.testing.assert_array_equal(b.to_numpy(), ea)
+
+    # range form: diagonal marker of CoreAlgorithms.c:14-18
+    c = g.volume(np.zeros((24, 24, 24), np.uint8), 4, (0.0, 1.0))
+
+    def diag(x, y, z, v):
+        if x == y and y == z:
+            v.bytes[0] = 0xFF
+
+    g._run(lambda: vkt.TransformRange(c, 2, 2, 2, 22, 22, 22, diag))
+    got = c.to_numpy()
+    exp = np.zeros((24, 24, 24), np.uint8)
+    for i in range(2, 22):
+        exp[i, i, i] = 0xFF
+    np.testing.assert_array_equal(got, exp)
+
+
+# ---- runtime semantics -------------------------------------------------------------------
+def test_deferred_migration_roundtrip(g):
+    """README flow: data written on the CPU, op on the GPU, read back on the CPU."""
+    vkt = g.vkt
+    v = g.volume(np.zeros((4, 5, 6), np.uint16), 5, (0.0, 1.0))
+    v.setValue(1, 2, 3, 0.5)                      # host accessor, CPU policy
+    g._gpu()
+    assert v.getValue(1, 2, 3) == 0.5             # host accessor under GPU policy (1-voxel copy)
+    v.setValue(0, 0, 0, 0.25)
+    assert vkt.FillRange(v, 2, 0, 0, 4, 1, 1, 0.75) == vkt.NoError
+    g._cpu()
+    arr = v.to_numpy()
+    assert arr[3, 2, 1] == 32768 and arr[0, 0, 0] == 16384
+    assert arr[0, 0, 2] == arr[0, 0, 3] == int(0.75 * 65536)
+
+
+def test_errors_are_returned_not_ignored(g):
+    vkt = g.vkt
+    v = g.volume(np.zeros((4, 4, 4), np.uint8), 4, (0.0, 1.0))
+    g._gpu()
+    try:
+        assert vkt.FillRange(v, 0, 0, 0, 5, 4, 4, 0.5) == vkt.InvalidValue   # out of bounds
+        assert "outside" in vkt.last_error()
+        assert vkt.FillRange(v, 2, 2, 2, 1, 1, 1, 0.5) == vkt.NoError        # empty range
+    finally:
+        g._cpu()
+
+
+def test_copy_constructor_on_gpu(g):
+    vkt = g.vkt
+    v = g.volume(np.arange(64, dtype=np.uint8).reshape(4, 4, 4), 4, (0.0, 1.0))
+    g._gpu()
+    v.migrate()
+    w = vkt.StructuredVolume.CreateCopy(v)
+    g._cpu()
+    np.testing.assert_array_equal(w.to_numpy(), np.arange(64, dtype=np.uint8).reshape(4, 4, 4))

@@ -1,0 +1,170 @@
+"""ctypes binding of libvolkit.so (the C ABI declared in include/volkit_c.h and
+include/volkit_hip.h).
+
+The library is built in-tree (``python -c "import __graft_entry__ as g; g.build()"`` or
+``make -C volkit_amd/csrc``) and loaded from ``volkit_amd/lib/libvolkit.so``.  There is no
+fallback: if the shared library is missing, importing :mod:`volkit_amd` raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("VOLKIT_LIB", os.path.join(_HERE, "lib", "libvolkit.so"))
+
+
+class VolkitLibraryMissing(ImportError):
+    pass
+
+
+if not os.path.exists(LIB_PATH):
+    raise VolkitLibraryMissing(
+        f"libvolkit.so not found at {LIB_PATH}: build it with `make -C volkit_amd/csrc` "
+        "(the HIP/gfx950 backend has no CPU fallback)")
+
+lib = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+
+# ---- C types -----------------------------------------------------------------------------
+c_vol = C.c_void_p            # vktStructuredVolume (opaque handle)
+c_err = C.c_int               # vktError
+i32, u32, u64, f32 = C.c_int32, C.c_uint32, C.c_uint64, C.c_float
+P = C.POINTER
+
+
+class Vec3i_t(C.Structure):
+    _fields_ = [("x", C.c_int), ("y", C.c_int), ("z", C.c_int)]
+
+
+class Vec3f_t(C.Structure):
+    _fields_ = [("x", C.c_float), ("y", C.c_float), ("z", C.c_float)]
+
+
+class Vec2f_t(C.Structure):
+    _fields_ = [("x", C.c_float), ("y", C.c_float)]
+
+
+class Box3f_t(C.Structure):
+    _fields_ = [("min", Vec3f_t), ("max", Vec3f_t)]
+
+
+class ExecutionPolicy_t(C.Structure):
+    _fields_ = [("device", C.c_int), ("hostApi", C.c_int), ("deviceApi", C.c_int),
+                ("printPerformance", C.c_uint8)]
+
+
+class VoxelView_t(C.Structure):
+    _fields_ = [("bytes", P(C.c_uint8)), ("dataFormat", C.c_int), ("mappingLo", C.c_float),
+                ("mappingHi", C.c_float)]
+
+
+class HipVolumeView_t(C.Structure):
+    _fields_ = [("data", C.c_void_p), ("dimX", i32), ("dimY", i32), ("dimZ", i32),
+                ("dataFormat", i32), ("mappingLo", f32), ("mappingHi", f32)]
+
+
+UnaryOp = C.CFUNCTYPE(None, i32, i32, i32, VoxelView_t)
+BinaryOp = C.CFUNCTYPE(None, i32, i32, i32, VoxelView_t, VoxelView_t)
+
+ARITH_OPS = ["Sum", "Diff", "Prod", "Quot", "AbsDiff",
+             "SafeSum", "SafeDiff", "SafeProd", "SafeQuot", "SafeAbsDiff"]
+
+_R9 = [i32] * 9
+
+# name -> (restype, argtypes)
+SIGNATURES = {
+    # ExecutionPolicy.h
+    "vktSetThreadExecutionPolicy": (None, [ExecutionPolicy_t]),
+    "vktGetThreadExecutionPolicy": (ExecutionPolicy_t, []),
+    # ManagedResource.h
+    "vktRegisterManagedResource": (u32, [C.c_void_p]),
+    "vktUnregisterManagedResource": (None, [u32]),
+    "vktGetManagedResource": (C.c_void_p, [u32]),
+    # Memory.h
+    "vktAllocate": (None, [P(C.c_void_p), C.c_size_t]),
+    "vktFree": (None, [C.c_void_p]),
+    "vktMemcpy": (None, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]),
+    # Voxel.h
+    "vktMapVoxel": (c_err, [P(C.c_uint8), f32, C.c_int, f32, f32]),
+    "vktUnmapVoxel": (c_err, [P(C.c_float), P(C.c_uint8), C.c_int, f32, f32]),
+    # StructuredVolume.h
+    "vktStructuredVolumeGetMaxBytesPerVoxel": (C.c_uint8, []),
+    "vktStructuredVolumeCreate": (None, [P(c_vol), i32, i32, i32, C.c_int, f32, f32, f32, f32, f32]),
+    "vktStructuredVolumeCreateCopy": (None, [P(c_vol), c_vol]),
+    "vktStructuredVolumeDestroy": (None, [c_vol]),
+    "vktStructuredVolumeSetDims3i": (None, [c_vol, i32, i32, i32]),
+    "vktStructuredVolumeGetDims3i": (None, [c_vol, P(i32), P(i32), P(i32)]),
+    "vktStructuredVolumeSetDims3iv": (None, [c_vol, Vec3i_t]),
+    "vktStructuredVolumeGetDims3iv": (Vec3i_t, [c_vol]),
+    "vktStructuredVolumeSetDataFormat": (None, [c_vol, C.c_int]),
+    "vktStructuredVolumeGetDataFormat": (C.c_int, [c_vol]),
+    "vktStructuredVolumeSetDist3f": (None, [c_vol, f32, f32, f32]),
+    "vktStructuredVolumeGetDist3f": (None, [c_vol, P(f32), P(f32), P(f32)]),
+    "vktStructuredVolumeSetDist3fv": (None, [c_vol, Vec3f_t]),
+    "vktStructuredVolumeGetDist3fv": (Vec3f_t, [c_vol]),
+    "vktStructuredVolumeSetVoxelMapping2f": (None, [c_vol, f32, f32]),
+    "vktStructuredVolumeGetVoxelMapping2f": (None, [c_vol, P(f32), P(f32)]),
+    "vktStructuredVolumeSetVoxelMapping2fv": (None, [c_vol, Vec2f_t]),
+    "vktStructuredVolumeGetVoxelMapping2fv": (Vec2f_t, [c_vol]),
+    "vktStructuredVolumeGetDomainBounds": (Box3f_t, [c_vol]),
+    "vktStructuredVolumeGetObjectBounds": (Box3f_t, [c_vol]),
+    "vktStructuredVolumeGetData": (C.c_void_p, [c_vol]),
+    "vktStructuredVolumeSetValue": (None, [c_vol, i32, i32, i32, f32]),
+    "vktStructuredVolumeGetValue": (None, [c_vol, i32, i32, i32, P(f32)]),
+    "vktStructuredVolumeSetBytes": (None, [c_vol, i32, i32, i32, P(C.c_uint8)]),
+    "vktStructuredVolumeGetBytes": (None, [c_vol, i32, i32, i32, P(C.c_uint8)]),
+    "vktStructuredVolumeGetSizeInBytes": (C.c_size_t, [c_vol]),
+    "vktStructuredVolumeGetResourceHandle": (u32, [c_vol]),
+    "vktStructuredVolumeMigrate": (None, [c_vol]),
+    # Fill.h / Copy.h
+    "vktFillSV": (c_err, [c_vol, f32]),
+    "vktFillRangeSV": (c_err, [c_vol, i32, i32, i32, i32, i32, i32, f32]),
+    "vktCopySV": (c_err, [c_vol, c_vol]),
+    "vktCopyRangeSV": (c_err, [c_vol, c_vol] + _R9),
+    # Transform.h
+    "vktTransformSV1": (c_err, [c_vol, UnaryOp]),
+    "vktTransformSV2": (c_err, [c_vol, c_vol, BinaryOp]),
+    "vktTransformRangeSV1": (c_err, [c_vol, i32, i32, i32, i32, i32, i32, UnaryOp]),
+    "vktTransformRangeSV2": (c_err, [c_vol, c_vol] + _R9 + [BinaryOp]),
+    # Resample (C entry point added by this library)
+    "vktResampleSV": (c_err, [c_vol, c_vol, C.c_int]),
+    # volkit_hip.h runtime
+    "vktHipSetDevice": (c_err, [i32]),
+    "vktHipGetDevice": (c_err, [P(i32)]),
+    "vktHipSetAsyncExecution": (c_err, [i32]),
+    "vktHipGetAsyncExecution": (c_err, [P(i32)]),
+    "vktHipSetComputeStream": (c_err, [C.c_void_p]),
+    "vktHipGetComputeStream": (c_err, [P(C.c_void_p)]),
+    "vktHipGetCopyStream": (c_err, [P(C.c_void_p)]),
+    "vktHipSynchronize": (c_err, []),
+    "vktHipGetLastErrorString": (C.c_char_p, []),
+    "vktHipSetKernelTiming": (c_err, [i32]),
+    "vktHipGetLastKernelMs": (c_err, [P(f32)]),
+    "vktHipAllocate": (c_err, [P(C.c_void_p), C.c_size_t]),
+    "vktHipFree": (c_err, [C.c_void_p]),
+    "vktHipMemcpy": (c_err, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]),
+    "vktHipMemsetRange": (c_err, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_size_t]),
+    # volkit_hip.h algorithms
+    "vktHipFillRange": (c_err, [HipVolumeView_t, Vec3i_t, Vec3i_t, f32]),
+    "vktHipCopyRange": (c_err, [HipVolumeView_t, HipVolumeView_t, Vec3i_t, Vec3i_t, Vec3i_t]),
+    "vktHipArithmeticRange": (c_err, [C.c_int, HipVolumeView_t, HipVolumeView_t, HipVolumeView_t,
+                                      Vec3i_t, Vec3i_t, Vec3i_t]),
+    "vktHipResample": (c_err, [HipVolumeView_t, HipVolumeView_t, C.c_int]),
+    "vktHipResampleSlab": (c_err, [HipVolumeView_t, HipVolumeView_t, C.c_int, i32, i32, i32, i32]),
+    "vktHipResampleSlabSourceRange": (c_err, [i32, i32, i32, i32, C.c_int, i32, P(i32), P(i32)]),
+    "vktHipTransformRange1": (c_err, [HipVolumeView_t, Vec3i_t, Vec3i_t, UnaryOp]),
+    "vktHipTransformRange2": (c_err, [HipVolumeView_t, HipVolumeView_t, Vec3i_t, Vec3i_t, Vec3i_t, BinaryOp]),
+    "vktHipSynthesize": (c_err, [HipVolumeView_t, u64]),
+}
+for _op in ARITH_OPS:
+    SIGNATURES[f"vkt{_op}SV"] = (c_err, [c_vol, c_vol, c_vol])
+    SIGNATURES[f"vkt{_op}RangeSV"] = (c_err, [c_vol, c_vol, c_vol] + _R9)
+
+for _name, (_res, _args) in SIGNATURES.items():
+    _fn = getattr(lib, _name)   # AttributeError here = a declared symbol is not exported
+    _fn.restype = _res
+    _fn.argtypes = _args
+
+
+def last_error() -> str:
+    return lib.vktHipGetLastErrorString().decode(errors="replace")

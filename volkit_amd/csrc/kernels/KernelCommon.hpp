@@ -1,0 +1,147 @@
+// KernelCommon.hpp -- device-side helpers shared by the gfx950 kernels.
+//
+// All kernels are bandwidth-bound byte/integer/f32 streams (no MFMA): they are written for
+// 64-lane waves, 16-byte-per-lane coalesced accesses where alignment allows, grid-stride
+// loops sized to fill 256 CUs, and nontemporal stores for outputs that are not re-read.
+#pragma once
+
+#include <cstdint>
+#include <hip/hip_runtime.h>
+
+#include "../common/Codec.hpp"
+
+namespace vkt
+{
+namespace hipk
+{
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+    constexpr int kBlock = 256;          // 4 waves of 64
+    constexpr int kNumCUs = 256;         // MI355X: 8 XCDs x 32 CUs
+
+    // Grid for a grid-stride streaming kernel: enough workgroups for ~8 per CU, never more
+    // than the work needs.
+    inline unsigned streamingGrid(uint64_t items, unsigned itemsPerBlock, unsigned maxBlocksPerCU = 8)
+    {
+        uint64_t need = (items + itemsPerBlock - 1) / itemsPerBlock;
+        uint64_t cap = static_cast<uint64_t>(kNumCUs) * maxBlocksPerCU;
+        if (need < 1)
+            need = 1;
+        return static_cast<unsigned>(need < cap ? need : cap);
+    }
+
+    // ---- scalar code access -----------------------------------------------------------
+    template <int BPV>
+    __device__ __forceinline__ uint32_t loadCode(uint8_t const* base, uint64_t voxel)
+    {
+        if constexpr (BPV == 1)
+            return base[voxel];
+        else if constexpr (BPV == 2)
+            return reinterpret_cast<uint16_t const*>(base)[voxel];
+        else
+            return reinterpret_cast<uint32_t const*>(base)[voxel];
+    }
+
+    template <int BPV>
+    __device__ __forceinline__ void storeCode(uint8_t* base, uint64_t voxel, uint32_t code)
+    {
+        if constexpr (BPV == 1)
+            base[voxel] = static_cast<uint8_t>(code);
+        else if constexpr (BPV == 2)
+            reinterpret_cast<uint16_t*>(base)[voxel] = static_cast<uint16_t>(code);
+        else
+            reinterpret_cast<uint32_t*>(base)[voxel] = code;
+    }
+
+    // Runtime bytes-per-voxel versions (wave-uniform branch).
+    __device__ __forceinline__ uint32_t loadCodeDyn(uint8_t const* base, uint64_t voxel, uint32_t bpv)
+    {
+        return bpv == 1 ? loadCode<1>(base, voxel) : bpv == 2 ? loadCode<2>(base, voxel) : loadCode<4>(base, voxel);
+    }
+
+    __device__ __forceinline__ void storeCodeDyn(uint8_t* base, uint64_t voxel, uint32_t bpv, uint32_t code)
+    {
+        if (bpv == 1)
+            storeCode<1>(base, voxel, code);
+        else if (bpv == 2)
+            storeCode<2>(base, voxel, code);
+        else
+            storeCode<4>(base, voxel, code);
+    }
+
+    // ---- 8 consecutive codes per lane ------------------------------------------------
+    // BPV 1: one 8-byte load; BPV 2: one 16-byte load; BPV 4: two 16-byte loads.
+    template <int BPV>
+    __device__ __forceinline__ void load8(uint8_t const* base, uint64_t voxel, uint32_t (&c)[8])
+    {
+        if constexpr (BPV == 1)
+        {
+            u32x2 v = *reinterpret_cast<u32x2 const*>(base + voxel);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+            {
+                c[i] = (v.x >> (8 * i)) & 0xFFu;
+                c[4 + i] = (v.y >> (8 * i)) & 0xFFu;
+            }
+        }
+        else if constexpr (BPV == 2)
+        {
+            u32x4 v = *reinterpret_cast<u32x4 const*>(base + 2 * voxel);
+            c[0] = v.x & 0xFFFFu; c[1] = v.x >> 16;
+            c[2] = v.y & 0xFFFFu; c[3] = v.y >> 16;
+            c[4] = v.z & 0xFFFFu; c[5] = v.z >> 16;
+            c[6] = v.w & 0xFFFFu; c[7] = v.w >> 16;
+        }
+        else
+        {
+            u32x4 a = *reinterpret_cast<u32x4 const*>(base + 4 * voxel);
+            u32x4 b = *reinterpret_cast<u32x4 const*>(base + 4 * voxel + 16);
+            c[0] = a.x; c[1] = a.y; c[2] = a.z; c[3] = a.w;
+            c[4] = b.x; c[5] = b.y; c[6] = b.z; c[7] = b.w;
+        }
+    }
+
+    template <int BPV, bool NT>
+    __device__ __forceinline__ void store8(uint8_t* base, uint64_t voxel, uint32_t const (&c)[8])
+    {
+        if constexpr (BPV == 1)
+        {
+            u32x2 v;
+            v.x = c[0] | c[1] << 8 | c[2] << 16 | c[3] << 24;
+            v.y = c[4] | c[5] << 8 | c[6] << 16 | c[7] << 24;
+            u32x2* p = reinterpret_cast<u32x2*>(base + voxel);
+            if constexpr (NT) __builtin_nontemporal_store(v, p); else *p = v;
+        }
+        else if constexpr (BPV == 2)
+        {
+            u32x4 v;
+            v.x = c[0] | c[1] << 16; v.y = c[2] | c[3] << 16;
+            v.z = c[4] | c[5] << 16; v.w = c[6] | c[7] << 16;
+            u32x4* p = reinterpret_cast<u32x4*>(base + 2 * voxel);
+            if constexpr (NT) __builtin_nontemporal_store(v, p); else *p = v;
+        }
+        else
+        {
+            u32x4 a, b;
+            a.x = c[0]; a.y = c[1]; a.z = c[2]; a.w = c[3];
+            b.x = c[4]; b.y = c[5]; b.z = c[6]; b.w = c[7];
+            u32x4* p = reinterpret_cast<u32x4*>(base + 4 * voxel);
+            if constexpr (NT) { __builtin_nontemporal_store(a, p); __builtin_nontemporal_store(b, p + 1); }
+            else { p[0] = a; p[1] = b; }
+        }
+    }
+
+    // XCD-aware block order (guide §5.5 T1): hardware deals workgroups round-robin over the
+    // 8 XCDs, so block b and b+8 share an L2.  Remap so each XCD walks one contiguous band of
+    // logical blocks -- neighbouring rows then hit the same L2.  Speed only, never correctness.
+    __device__ __forceinline__ uint32_t xcdSwizzle(uint32_t b, uint32_t nblocks)
+    {
+        uint32_t per = nblocks / 8u;
+        if (per == 0u || b >= per * 8u)
+            return b;
+        return (b % 8u) * per + b / 8u;
+    }
+
+} // hipk
+} // vkt

@@ -1,0 +1,485 @@
+// Pointwise.hip -- gfx950 kernels and backend entry points for FillRange, CopyRange, the
+// ten arithmetic ops, format conversion, MemsetRange and the synthetic-input generator.
+//
+// Replaces the reference's FillRange_cuda (src/vkt/Fill_cuda.cu:22-55, which is never
+// reached for SV because Call() has no GPU branch, src/vkt/Callable.cpp:53-66),
+// CopyRange_cuda (src/vkt/Copy_cuda.cu:12-111), ArithmeticOp_kernel x10
+// (src/vkt/Arithmetic_cuda.cu:12-296) and MemsetRange_cuda (src/vkt/Memory_cuda.cu:15-49).
+// Semantics follow the SERIAL path, not the CUDA path:
+// arithmetic writes dst[x + dstOffset] at absolute x; CopyRange clamps source indices.
+//
+// Roofline: every op here is HBM-bound.  Algorithmic bytes per voxel of the range:
+// Fill b_dst; Copy b_src + b_dst; arithmetic b_s1 + b_s2 + b_dst (6 B for UInt16).
+
+#include "Pointwise.hpp"
+#include "../runtime/Runtime.hpp"
+#include "volkit_hip.h"
+
+#include <cstring>
+
+namespace vkt
+{
+namespace hipk
+{
+    using codec::MapParams;
+
+    // ---- functors ------------------------------------------------------------------
+    struct FillF
+    {
+        uint32_t code;
+        __device__ __forceinline__ uint32_t operator()(uint32_t, uint32_t) const { return code; }
+    };
+
+    struct PassF
+    {
+        __device__ __forceinline__ uint32_t operator()(uint32_t a, uint32_t) const { return a; }
+    };
+
+    // dst = map_dst(unmap_src(code))  (CopyRange by value, Copy_serial.hpp:69-70;
+    // Resample same-dims branch, Resample_serial.hpp:32-48)
+    template <int FS, int FD>
+    struct ConvertF
+    {
+        int32_t fs, fd;
+        float slo, shi;
+        MapParams dm;
+        __device__ __forceinline__ uint32_t operator()(uint32_t a, uint32_t) const
+        {
+            float v = codec::decode(a, FS == kDyn ? fs : FS, slo, shi);
+            bool w;
+            return codec::encode(v, FD == kDyn ? fd : FD, dm, w);
+        }
+    };
+
+    // The ten lambdas of reference src/vkt/Arithmetic_serial.hpp:63-258.
+    template <int OP>
+    __device__ __forceinline__ float applyOp(float a, float b, float lo, float hi)
+    {
+        if constexpr (OP == vktHipOpSum) return a + b;
+        else if constexpr (OP == vktHipOpDiff) return a - b;
+        else if constexpr (OP == vktHipOpProd) return a * b;
+        else if constexpr (OP == vktHipOpQuot) return a / b;
+        else if constexpr (OP == vktHipOpAbsDiff) return fabsf(a - b);
+        else if constexpr (OP == vktHipOpSafeSum) return codec::clampRef(a + b, lo, hi);
+        else if constexpr (OP == vktHipOpSafeDiff) return codec::clampRef(a - b, lo, hi);
+        else if constexpr (OP == vktHipOpSafeProd) return codec::clampRef(a * b, lo, hi);
+        else if constexpr (OP == vktHipOpSafeQuot) return codec::clampRef(a / b, lo, hi);
+        else return codec::clampRef(fabsf(a - b), lo, hi);
+    }
+
+    template <int OP, int FS1, int FS2, int FD>
+    struct ArithF
+    {
+        int32_t fs1, fs2, fd;
+        float lo1, hi1, lo2, hi2;
+        MapParams dm;
+        __device__ __forceinline__ uint32_t operator()(uint32_t a, uint32_t b) const
+        {
+            float v1 = codec::decode(a, FS1 == kDyn ? fs1 : FS1, lo1, hi1);
+            float v2 = codec::decode(b, FS2 == kDyn ? fs2 : FS2, lo2, hi2);
+            float r = applyOp<OP>(v1, v2, dm.lo, dm.hi);
+            bool w;
+            return codec::encode(r, FD == kDyn ? fd : FD, dm, w);
+        }
+    };
+
+    // ---- planning --------------------------------------------------------------------
+    PwPlan planPointwise(int ns, Operand d, Operand s1, Operand s2, int64_t nx, int64_t ny, int64_t nz)
+    {
+        PwPlan p;
+        p.d = d;
+        p.s1 = s1;
+        p.s2 = s2;
+        p.g.nx = nx;
+        p.g.ny = ny;
+        p.g.nz = nz;
+        Operand* ops[3] = {&p.d, &p.s1, &p.s2};
+        int nops = ns + 1;
+
+        bool vec = true;
+        uint32_t bpv = p.d.bpv;
+        for (int i = 0; i < nops; ++i)
+        {
+            Operand& o = *ops[i];
+            int64_t dx = o.dims[0], dy = o.dims[1];
+            o.base = (static_cast<int64_t>(o.origin[2]) * dy + o.origin[1]) * dx + o.origin[0];
+            o.sy = dx;
+            o.sz = dx * dy;
+            if (o.clamp || o.bpv != bpv)
+                vec = false;
+        }
+
+        // collapse rows that are contiguous in every operand
+        int64_t vnx = nx, vny = ny, vnz = nz;
+        bool mergeY = vny > 1;
+        for (int i = 0; i < nops && mergeY; ++i)
+            mergeY = ops[i]->sy == vnx;
+        if (mergeY)
+        {
+            vnx *= vny;
+            vny = 1;
+        }
+        if (vny == 1 && vnz > 1)
+        {
+            bool mergeZ = true;
+            for (int i = 0; i < nops && mergeZ; ++i)
+                mergeZ = ops[i]->sz == vnx;
+            if (mergeZ)
+            {
+                vnx *= vnz;
+                vnz = 1;
+            }
+        }
+        p.g.vnx = vnx;
+        p.g.vny = vny;
+        p.g.vnz = vnz;
+        p.g.vnx8 = vnx & ~int64_t(7);
+
+        // 8-voxel chunks must start aligned in every operand
+        uint64_t needAlign = bpv == 1 ? 8u : 16u;
+        for (int i = 0; i < nops && vec; ++i)
+        {
+            Operand const& o = *ops[i];
+            if ((reinterpret_cast<uintptr_t>(o.data) % needAlign) != 0 || (o.base & 7) != 0)
+                vec = false;
+            if (vny > 1 && (o.sy & 7) != 0)
+                vec = false;
+            if (vnz > 1 && (o.sz & 7) != 0)
+                vec = false;
+        }
+        if (!(bpv == 1 || bpv == 2 || bpv == 4))
+            vec = false;
+        p.vec = vec;
+        p.bpv = bpv;
+        return p;
+    }
+
+    // ---- validation helpers ------------------------------------------------------------
+    bool validView(vktHipVolumeView_t const& v)
+    {
+        if (v.dimX < 0 || v.dimY < 0 || v.dimZ < 0)
+            return false;
+        uint32_t b = codec::bytesPerVoxel(v.dataFormat);
+        if (b == 255u)
+            return false;
+        if (v.data == nullptr && static_cast<int64_t>(v.dimX) * v.dimY * v.dimZ > 0)
+            return false;
+        return true;
+    }
+
+    uint64_t viewBytes(vktHipVolumeView_t const& v)
+    {
+        return static_cast<uint64_t>(v.dimX) * static_cast<uint64_t>(v.dimY) * static_cast<uint64_t>(v.dimZ) *
+               codec::bytesPerVoxel(v.dataFormat);
+    }
+
+    bool boxInside(vktHipVolumeView_t const& v, vktVec3i_t o, int64_t nx, int64_t ny, int64_t nz)
+    {
+        return o.x >= 0 && o.y >= 0 && o.z >= 0 && o.x + nx <= v.dimX && o.y + ny <= v.dimY && o.z + nz <= v.dimZ;
+    }
+
+    bool overlaps(vktHipVolumeView_t const& a, vktHipVolumeView_t const& b)
+    {
+        uintptr_t a0 = reinterpret_cast<uintptr_t>(a.data), a1 = a0 + viewBytes(a);
+        uintptr_t b0 = reinterpret_cast<uintptr_t>(b.data), b1 = b0 + viewBytes(b);
+        return a0 < b1 && b0 < a1;
+    }
+
+    Operand makeOperand(vktHipVolumeView_t const& v, vktVec3i_t origin, bool clamp)
+    {
+        Operand o{};
+        o.data = v.data;
+        o.dims[0] = v.dimX;
+        o.dims[1] = v.dimY;
+        o.dims[2] = v.dimZ;
+        o.origin[0] = origin.x;
+        o.origin[1] = origin.y;
+        o.origin[2] = origin.z;
+        o.clamp = clamp ? 1 : 0;
+        o.fmt = v.dataFormat;
+        o.bpv = codec::bytesPerVoxel(v.dataFormat);
+        o.lo = v.mappingLo;
+        o.hi = v.mappingHi;
+        return o;
+    }
+
+    // Formats whose encode writes nothing (reference MapVoxelImpl switch has no case).
+    bool encodeWrites(int32_t fmt)
+    {
+        return fmt == codec::FmtInt16 || fmt == codec::FmtUInt8 || fmt == codec::FmtUInt16 ||
+               fmt == codec::FmtUInt32 || fmt == codec::FmtFloat32;
+    }
+
+    template <int NS, class F>
+    vktError launchByBpv(PwPlan const& p, F const& f, hipStream_t s)
+    {
+        switch (p.bpv)
+        {
+        case 1: return launchPointwise<NS, 1>(p, f, s);
+        case 2: return launchPointwise<NS, 2>(p, f, s);
+        case 4: return launchPointwise<NS, 4>(p, f, s);
+        default: return launchPointwise<NS, 0>(p, f, s);
+        }
+    }
+
+    // ---- conversion (shared with Resample's same-dims branch) ---------------------------
+    vktError convertBox(vktHipVolumeView_t dst, vktHipVolumeView_t src, vktVec3i_t srcOrigin, bool clampSrc,
+                        vktVec3i_t dstOrigin, int64_t nx, int64_t ny, int64_t nz)
+    {
+        hipStream_t s = rt::computeStream();
+        Operand od = makeOperand(dst, dstOrigin, false);
+        Operand os = makeOperand(src, srcOrigin, clampSrc);
+        PwPlan p = planPointwise(1, od, os, os, nx, ny, nz);
+        MapParams dm = codec::makeMapParams(dst.mappingLo, dst.mappingHi);
+        int32_t fs = src.dataFormat, fd = dst.dataFormat;
+        if (p.vec && fs == fd)
+        {
+            if (fs == codec::FmtUInt8)
+                return launchPointwise<1, 1>(p, ConvertF<codec::FmtUInt8, codec::FmtUInt8>{fs, fd, src.mappingLo, src.mappingHi, dm}, s);
+            if (fs == codec::FmtUInt16)
+                return launchPointwise<1, 2>(p, ConvertF<codec::FmtUInt16, codec::FmtUInt16>{fs, fd, src.mappingLo, src.mappingHi, dm}, s);
+            if (fs == codec::FmtFloat32)
+                return launchPointwise<1, 4>(p, ConvertF<codec::FmtFloat32, codec::FmtFloat32>{fs, fd, src.mappingLo, src.mappingHi, dm}, s);
+        }
+        return launchByBpv<1>(p, ConvertF<kDyn, kDyn>{fs, fd, src.mappingLo, src.mappingHi, dm}, s);
+    }
+
+    // ---- arithmetic dispatch ---------------------------------------------------------
+    template <int OP>
+    vktError arithmetic(PwPlan const& p, vktHipVolumeView_t const& d, vktHipVolumeView_t const& a,
+                        vktHipVolumeView_t const& b, hipStream_t s)
+    {
+        MapParams dm = codec::makeMapParams(d.mappingLo, d.mappingHi);
+        int32_t f1 = a.dataFormat, f2 = b.dataFormat, fd = d.dataFormat;
+        if (p.vec && f1 == f2 && f1 == fd)
+        {
+            if (fd == codec::FmtUInt16)
+                return launchPointwise<2, 2>(
+                    p, ArithF<OP, codec::FmtUInt16, codec::FmtUInt16, codec::FmtUInt16>{
+                           f1, f2, fd, a.mappingLo, a.mappingHi, b.mappingLo, b.mappingHi, dm}, s);
+            if (fd == codec::FmtUInt8)
+                return launchPointwise<2, 1>(
+                    p, ArithF<OP, codec::FmtUInt8, codec::FmtUInt8, codec::FmtUInt8>{
+                           f1, f2, fd, a.mappingLo, a.mappingHi, b.mappingLo, b.mappingHi, dm}, s);
+            if (fd == codec::FmtFloat32)
+                return launchPointwise<2, 4>(
+                    p, ArithF<OP, codec::FmtFloat32, codec::FmtFloat32, codec::FmtFloat32>{
+                           f1, f2, fd, a.mappingLo, a.mappingHi, b.mappingLo, b.mappingHi, dm}, s);
+        }
+        return launchByBpv<2>(p, ArithF<OP, kDyn, kDyn, kDyn>{f1, f2, fd, a.mappingLo, a.mappingHi, b.mappingLo,
+                                                               b.mappingHi, dm}, s);
+    }
+
+    // ---- MemsetRange ---------------------------------------------------------------
+    struct Pattern256
+    {
+        uint8_t bytes[256];
+    };
+
+    __global__ __launch_bounds__(kBlock) void memsetVec16Kernel(u32x4* dst, uint64_t n16, u32x4 pattern)
+    {
+        uint64_t const stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+        for (uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; i < n16; i += stride)
+            __builtin_nontemporal_store(pattern, dst + i);
+    }
+
+    __global__ __launch_bounds__(kBlock) void memsetBytesKernel(uint8_t* dst, uint64_t begin, uint64_t nbytes,
+                                                                uint32_t psize, Pattern256 pat,
+                                                                uint8_t const* bigPattern)
+    {
+        uint64_t const stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+        for (uint64_t i = begin + blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; i < nbytes; i += stride)
+        {
+            uint32_t k = static_cast<uint32_t>(i % psize);
+            dst[i] = bigPattern != nullptr ? bigPattern[k] : pat.bytes[k];
+        }
+    }
+
+    vktError memsetRange(void* dst, void const* pattern, std::size_t dstSize, std::size_t patternSize)
+    {
+        if (patternSize == 0 || dstSize < patternSize)
+            return vktNoError;
+        if (dst == nullptr || pattern == nullptr)
+            return rt::fail("MemsetRange: null pointer");
+        hipStream_t s = rt::computeStream();
+        uint64_t nbytes = (dstSize / patternSize) * patternSize;   // whole patterns only
+        uint8_t const* pb = static_cast<uint8_t const*>(pattern);
+        uint64_t head = 0;
+        if (16 % patternSize == 0 && reinterpret_cast<uintptr_t>(dst) % 16 == 0)
+        {
+            uint8_t v16[16];
+            for (int i = 0; i < 16; ++i)
+                v16[i] = pb[i % patternSize];
+            u32x4 pv;
+            std::memcpy(&pv, v16, 16);
+            uint64_t n16 = nbytes / 16;
+            if (n16 > 0)
+                hipLaunchKernelGGL(memsetVec16Kernel, dim3(streamingGrid(n16, kBlock)), dim3(kBlock), 0, s,
+                                   static_cast<u32x4*>(dst), n16, pv);
+            head = n16 * 16;
+        }
+        if (head < nbytes)
+        {
+            Pattern256 pat{};
+            uint8_t* big = nullptr;
+            if (patternSize <= sizeof(pat.bytes))
+                std::memcpy(pat.bytes, pb, patternSize);
+            else
+            {
+                VKT_HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&big), patternSize, s));
+                VKT_HIP_TRY(hipMemcpyAsync(big, pb, patternSize, hipMemcpyHostToDevice, s));
+                VKT_HIP_TRY(hipStreamSynchronize(s));   // pageable source must be consumed
+            }
+            hipLaunchKernelGGL(memsetBytesKernel, dim3(streamingGrid(nbytes - head, kBlock)), dim3(kBlock), 0, s,
+                               static_cast<uint8_t*>(dst), head, nbytes, static_cast<uint32_t>(patternSize), pat,
+                               big);
+            if (big != nullptr)
+                VKT_HIP_TRY(hipFreeAsync(big, s));
+        }
+        return rt::finishLaunch("MemsetRange");
+    }
+
+    // ---- synthetic input -------------------------------------------------------------
+    __device__ __forceinline__ uint64_t splitmix64(uint64_t x)
+    {
+        x += 0x9E3779B97F4A7C15ull;
+        x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+        x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+        return x ^ (x >> 31);
+    }
+
+    __global__ __launch_bounds__(kBlock) void synthKernel(uint8_t* data, uint64_t nbytes, uint64_t seed)
+    {
+        uint64_t const stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+        uint64_t const words = nbytes / 8;
+        for (uint64_t w = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; w <= words; w += stride)
+        {
+            uint64_t r = splitmix64(seed + w);
+            if (w < words)
+                __builtin_nontemporal_store(r, reinterpret_cast<uint64_t*>(data) + w);
+            else
+                for (uint64_t b = 0; b < nbytes % 8; ++b)
+                    data[8 * w + b] = static_cast<uint8_t>(r >> (8 * b));
+        }
+    }
+
+} // hipk
+} // vkt
+
+using namespace vkt;
+using namespace vkt::hipk;
+
+extern "C" {
+
+vktError vktHipFillRange(vktHipVolumeView_t volume, vktVec3i_t first, vktVec3i_t last, float value)
+{
+    if (!validView(volume))
+        return rt::fail("vktHipFillRange: invalid volume view");
+    int64_t nx = int64_t(last.x) - first.x, ny = int64_t(last.y) - first.y, nz = int64_t(last.z) - first.z;
+    if (nx <= 0 || ny <= 0 || nz <= 0)
+        return vktNoError;
+    if (!boxInside(volume, first, nx, ny, nz))
+        return rt::fail("vktHipFillRange: range outside the volume");
+    if (!encodeWrites(volume.dataFormat))
+        return vktNoError;   // reference MapVoxelImpl writes nothing for Int8/Int32
+    bool w;
+    uint32_t code = codec::encode(value, volume.dataFormat, codec::makeMapParams(volume.mappingLo, volume.mappingHi), w);
+    Operand od = makeOperand(volume, first, false);
+    PwPlan p = planPointwise(0, od, od, od, nx, ny, nz);
+    vktError e = launchByBpv<0>(p, FillF{code}, rt::computeStream());
+    return e != vktNoError ? e : rt::finishLaunch("FillRange_hip");
+}
+
+vktError vktHipCopyRange(vktHipVolumeView_t dst, vktHipVolumeView_t src, vktVec3i_t first, vktVec3i_t last,
+                         vktVec3i_t dstOffset)
+{
+    if (!validView(dst) || !validView(src))
+        return rt::fail("vktHipCopyRange: invalid volume view");
+    int64_t nx = int64_t(last.x) - first.x, ny = int64_t(last.y) - first.y, nz = int64_t(last.z) - first.z;
+    if (nx <= 0 || ny <= 0 || nz <= 0)
+        return vktNoError;
+    if (src.dimX <= 0 || src.dimY <= 0 || src.dimZ <= 0)
+        return rt::fail("vktHipCopyRange: empty source volume");
+    if (!boxInside(dst, dstOffset, nx, ny, nz))
+        return rt::fail("vktHipCopyRange: destination range outside the volume");
+    bool clamp = !boxInside(src, first, nx, ny, nz);
+    if (overlaps(dst, src) && !(dst.data == src.data && first.x == dstOffset.x && first.y == dstOffset.y &&
+                                first.z == dstOffset.z && !clamp))
+        return rt::fail("vktHipCopyRange: overlapping source and destination are not supported");
+    bool bytewise = dst.dataFormat == src.dataFormat && dst.mappingLo == src.mappingLo &&
+                    dst.mappingHi == src.mappingHi;   // Copy_serial.hpp:21-22
+    hipStream_t s = rt::computeStream();
+    vktError e;
+    if (bytewise)
+    {
+        Operand od = makeOperand(dst, dstOffset, false);
+        Operand os = makeOperand(src, first, clamp);
+        PwPlan p = planPointwise(1, od, os, os, nx, ny, nz);
+        e = launchByBpv<1>(p, PassF{}, s);
+    }
+    else
+    {
+        if (!encodeWrites(dst.dataFormat))
+            return vktNoError;
+        e = convertBox(dst, src, first, clamp, dstOffset, nx, ny, nz);
+    }
+    return e != vktNoError ? e : rt::finishLaunch("CopyRange_hip");
+}
+
+vktError vktHipArithmeticRange(vktHipArithmeticOp op, vktHipVolumeView_t dest, vktHipVolumeView_t source1,
+                               vktHipVolumeView_t source2, vktVec3i_t first, vktVec3i_t last, vktVec3i_t dstOffset)
+{
+    if (!validView(dest) || !validView(source1) || !validView(source2))
+        return rt::fail("vktHipArithmeticRange: invalid volume view");
+    if (op < 0 || op >= vktHipOpCount)
+        return rt::fail("vktHipArithmeticRange: unknown op");
+    int64_t nx = int64_t(last.x) - first.x, ny = int64_t(last.y) - first.y, nz = int64_t(last.z) - first.z;
+    if (nx <= 0 || ny <= 0 || nz <= 0)
+        return vktNoError;
+    vktVec3i_t dOrigin{first.x + dstOffset.x, first.y + dstOffset.y, first.z + dstOffset.z};
+    if (!boxInside(source1, first, nx, ny, nz) || !boxInside(source2, first, nx, ny, nz) ||
+        !boxInside(dest, dOrigin, nx, ny, nz))
+        return rt::fail("vktHipArithmeticRange: range outside a volume");
+    bool shifted = dstOffset.x != 0 || dstOffset.y != 0 || dstOffset.z != 0;
+    if (shifted && (overlaps(dest, source1) || overlaps(dest, source2)))
+        return rt::fail("vktHipArithmeticRange: dest aliases a source with a non-zero dstOffset");
+    if (!encodeWrites(dest.dataFormat))
+        return vktNoError;
+    Operand od = makeOperand(dest, dOrigin, false);
+    Operand o1 = makeOperand(source1, first, false);
+    Operand o2 = makeOperand(source2, first, false);
+    PwPlan p = planPointwise(2, od, o1, o2, nx, ny, nz);
+    hipStream_t s = rt::computeStream();
+    vktError e = vktNoError;
+    switch (op)
+    {
+    case vktHipOpSum: e = arithmetic<vktHipOpSum>(p, dest, source1, source2, s); break;
+    case vktHipOpDiff: e = arithmetic<vktHipOpDiff>(p, dest, source1, source2, s); break;
+    case vktHipOpProd: e = arithmetic<vktHipOpProd>(p, dest, source1, source2, s); break;
+    case vktHipOpQuot: e = arithmetic<vktHipOpQuot>(p, dest, source1, source2, s); break;
+    case vktHipOpAbsDiff: e = arithmetic<vktHipOpAbsDiff>(p, dest, source1, source2, s); break;
+    case vktHipOpSafeSum: e = arithmetic<vktHipOpSafeSum>(p, dest, source1, source2, s); break;
+    case vktHipOpSafeDiff: e = arithmetic<vktHipOpSafeDiff>(p, dest, source1, source2, s); break;
+    case vktHipOpSafeProd: e = arithmetic<vktHipOpSafeProd>(p, dest, source1, source2, s); break;
+    case vktHipOpSafeQuot: e = arithmetic<vktHipOpSafeQuot>(p, dest, source1, source2, s); break;
+    case vktHipOpSafeAbsDiff: e = arithmetic<vktHipOpSafeAbsDiff>(p, dest, source1, source2, s); break;
+    default: break;
+    }
+    return e != vktNoError ? e : rt::finishLaunch("ArithmeticRange_hip");
+}
+
+vktError vktHipSynthesize(vktHipVolumeView_t volume, uint64_t seed)
+{
+    if (!validView(volume))
+        return rt::fail("vktHipSynthesize: invalid volume view");
+    uint64_t nbytes = viewBytes(volume);
+    if (nbytes == 0)
+        return vktNoError;
+    if (reinterpret_cast<uintptr_t>(volume.data) % 8 != 0)
+        return rt::fail("vktHipSynthesize: data must be 8-byte aligned");
+    hipLaunchKernelGGL(synthKernel, dim3(streamingGrid(nbytes / 8 + 1, kBlock)), dim3(kBlock), 0,
+                       rt::computeStream(), volume.data, nbytes, seed);
+    return rt::finishLaunch("Synthesize_hip");
+}
+
+} // extern "C"

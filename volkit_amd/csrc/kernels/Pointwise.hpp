@@ -1,0 +1,183 @@
+// Pointwise.hpp -- the pointwise streaming engine behind Fill, Copy, Arithmetic and the
+// same-dims branch of Resample.
+//
+// Iteration space: a box of extent (nx, ny, nz) voxels.  Every operand maps box voxel
+// (i, j, k) to its own voxel origin + (i, j, k) (optionally clamped to its dims, as
+// CopyRange_serial clamps its source, reference src/vkt/Copy_serial.hpp:38-40).
+//
+// Two device paths, chosen on the host:
+//  * vector path: the box is collapsed (rows that are contiguous in every operand merge
+//    into longer rows, whole-volume ops become one row of dimX*dimY*dimZ voxels), every
+//    lane moves 8 consecutive voxels per operand with 8/16/32-byte loads and a nontemporal
+//    store; rows whose length is not a multiple of 8 finish with a scalar tail.
+//  * scalar path: one voxel per lane-iteration with full 3-D coordinates (clamping,
+//    unaligned operands, mixed voxel sizes).
+#pragma once
+
+#include "KernelCommon.hpp"
+#include "volkit_c.h"
+
+namespace vkt
+{
+namespace hipk
+{
+    struct Operand
+    {
+        uint8_t* data;
+        // vector path (after collapsing): voxel index = base + k*sz + j*sy + i
+        int64_t base;
+        int64_t sy;
+        int64_t sz;
+        // scalar path
+        int32_t dims[3];
+        int32_t origin[3];
+        int32_t clamp;
+        int32_t fmt;
+        uint32_t bpv;
+        float lo;
+        float hi;
+    };
+
+    struct Geom
+    {
+        int64_t nx, ny, nz;      // raw extents (scalar path)
+        int64_t vnx, vny, vnz;   // collapsed extents (vector path)
+        int64_t vnx8;            // vnx rounded down to a multiple of 8
+    };
+
+    // Sentinel for "format known only at run time".
+    constexpr int kDyn = -1;
+
+    // ---- operand index helpers ----------------------------------------------------------
+    __device__ __forceinline__ int32_t clampRefI(int32_t x, int32_t lo, int32_t hi)
+    {
+        int32_t m = hi < x ? hi : x;   // reference clamp = max(lo, min(x, hi)), linalg.hpp:38-41
+        return lo < m ? m : lo;
+    }
+
+    __device__ __forceinline__ uint64_t scalarIndex(Operand const& o, int64_t i, int64_t j, int64_t k)
+    {
+        int32_t x = o.origin[0] + static_cast<int32_t>(i);
+        int32_t y = o.origin[1] + static_cast<int32_t>(j);
+        int32_t z = o.origin[2] + static_cast<int32_t>(k);
+        if (o.clamp)
+        {
+            x = clampRefI(x, 0, o.dims[0] - 1);
+            y = clampRefI(y, 0, o.dims[1] - 1);
+            z = clampRefI(z, 0, o.dims[2] - 1);
+        }
+        return (static_cast<uint64_t>(z) * static_cast<uint64_t>(o.dims[1]) + static_cast<uint64_t>(y)) *
+                   static_cast<uint64_t>(o.dims[0]) + static_cast<uint64_t>(x);
+    }
+
+    // ---- kernels ---------------------------------------------------------------------
+    // F: functor `uint32_t operator()(uint32_t code1, uint32_t code2) const` -> dst code.
+    template <int NS, int BPV, class F>
+    __global__ __launch_bounds__(kBlock) void pointwiseVecKernel(Operand d, Operand s1, Operand s2, Geom g, F f)
+    {
+        uint64_t const tid = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
+        uint64_t const stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+        uint64_t const cpr = static_cast<uint64_t>(g.vnx8) >> 3;          // chunks per row
+        uint64_t const rows = static_cast<uint64_t>(g.vny) * static_cast<uint64_t>(g.vnz);
+        uint64_t const items = cpr * rows;
+        uint64_t const ny = static_cast<uint64_t>(g.vny);
+
+        for (uint64_t it = tid; it < items; it += stride)
+        {
+            uint64_t r = 0, c = it;
+            if (rows > 1)
+            {
+                r = it / cpr;
+                c = it - r * cpr;
+            }
+            uint64_t j = r % ny, k = r / ny;
+            uint64_t x = c << 3;
+            uint32_t a[8], b[8], o[8];
+            if constexpr (NS >= 1)
+                load8<BPV>(s1.data, s1.base + k * s1.sz + j * s1.sy + x, a);
+            if constexpr (NS >= 2)
+                load8<BPV>(s2.data, s2.base + k * s2.sz + j * s2.sy + x, b);
+#pragma unroll
+            for (int v = 0; v < 8; ++v)
+                o[v] = f(NS >= 1 ? a[v] : 0u, NS >= 2 ? b[v] : 0u);
+            store8<BPV, true>(d.data, d.base + k * d.sz + j * d.sy + x, o);
+        }
+
+        // scalar tail of every row: voxels [vnx8, vnx)
+        uint64_t const tailLen = static_cast<uint64_t>(g.vnx - g.vnx8);
+        if (tailLen == 0)
+            return;
+        uint64_t const tailItems = tailLen * rows;
+        for (uint64_t it = tid; it < tailItems; it += stride)
+        {
+            uint64_t r = it / tailLen;
+            uint64_t x = static_cast<uint64_t>(g.vnx8) + (it - r * tailLen);
+            uint64_t j = r % ny, k = r / ny;
+            uint32_t a = 0, b = 0;
+            if constexpr (NS >= 1)
+                a = loadCode<BPV>(s1.data, s1.base + k * s1.sz + j * s1.sy + x);
+            if constexpr (NS >= 2)
+                b = loadCode<BPV>(s2.data, s2.base + k * s2.sz + j * s2.sy + x);
+            storeCode<BPV>(d.data, d.base + k * d.sz + j * d.sy + x, f(a, b));
+        }
+    }
+
+    template <int NS, class F>
+    __global__ __launch_bounds__(kBlock) void pointwiseScalarKernel(Operand d, Operand s1, Operand s2, Geom g, F f)
+    {
+        uint64_t const tid = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
+        uint64_t const stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+        uint64_t const nx = static_cast<uint64_t>(g.nx), ny = static_cast<uint64_t>(g.ny);
+        uint64_t const total = nx * ny * static_cast<uint64_t>(g.nz);
+        for (uint64_t l = tid; l < total; l += stride)
+        {
+            uint64_t i = l % nx;
+            uint64_t t = l / nx;
+            uint64_t j = t % ny;
+            uint64_t k = t / ny;
+            uint32_t a = 0, b = 0;
+            if constexpr (NS >= 1)
+                a = loadCodeDyn(s1.data, scalarIndex(s1, i, j, k), s1.bpv);
+            if constexpr (NS >= 2)
+                b = loadCodeDyn(s2.data, scalarIndex(s2, i, j, k), s2.bpv);
+            storeCodeDyn(d.data, scalarIndex(d, i, j, k), d.bpv, f(a, b));
+        }
+    }
+
+    // ---- host-side planning (Pointwise.hip) -----------------------------------------
+    struct PwPlan
+    {
+        Operand d, s1, s2;
+        Geom g;
+        bool vec;        // vector path eligible (aligned, unclamped, uniform voxel size)
+        uint32_t bpv;    // common bytes per voxel when vec
+    };
+
+    // Builds the plan for `ns` sources over a box of extent n (all > 0).
+    PwPlan planPointwise(int ns, Operand d, Operand s1, Operand s2, int64_t nx, int64_t ny, int64_t nz);
+
+    // Launch the plan with functor f: vector kernel if eligible and BPV matches, else scalar.
+    template <int NS, int BPV, class F>
+    vktError launchPointwise(PwPlan const& p, F const& f, hipStream_t stream)
+    {
+        if constexpr (BPV != 0)
+        {
+            if (p.vec && p.bpv == BPV)
+            {
+                uint64_t items = static_cast<uint64_t>(p.g.vny) * static_cast<uint64_t>(p.g.vnz) *
+                                 static_cast<uint64_t>(p.g.vnx8 / 8 + (p.g.vnx - p.g.vnx8));
+                unsigned grid = streamingGrid(items, kBlock);
+                hipLaunchKernelGGL((pointwiseVecKernel<NS, BPV, F>), dim3(grid), dim3(kBlock), 0, stream,
+                                   p.d, p.s1, p.s2, p.g, f);
+                return vktNoError;
+            }
+        }
+        uint64_t total = static_cast<uint64_t>(p.g.nx) * static_cast<uint64_t>(p.g.ny) * static_cast<uint64_t>(p.g.nz);
+        unsigned grid = streamingGrid(total, kBlock);
+        hipLaunchKernelGGL((pointwiseScalarKernel<NS, F>), dim3(grid), dim3(kBlock), 0, stream, p.d, p.s1, p.s2,
+                           p.g, f);
+        return vktNoError;
+    }
+
+} // hipk
+} // vkt

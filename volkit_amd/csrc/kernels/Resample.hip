@@ -1,0 +1,549 @@
+// Resample.hip -- SV->SV Resample on gfx950 (replaces Resample_cuda,
+// reference src/vkt/Resample_cuda.cu:19-43; semantics of Resample_serial,
+// src/vkt/Resample_serial.hpp:26-71).
+//
+// Semantics restated:
+//  * dst.dims == src.dims: per-voxel re-encode dst[i] = map_dst(unmap_src(src[i])), no index
+//    math (serial branch :32-48, absent from the CUDA path) -> the pointwise convert kernel.
+//  * otherwise, per axis, s = (int32)( (float)d / (float)Dd * (float)Ds ) -- computed ONCE on
+//    the host into exact index tables; Nearest reads src[s]; "Linear" calls
+//    sampleLinear(int,int,int) whose fractions are all 0, i.e. lerp chains v000 + 0*v100 ...
+//    over the neighbours (hi.x = the next voxel in memory, unclamped; hi.y, hi.z clamped),
+//    so for finite neighbours and an integer destination it equals Nearest exactly, while a
+//    non-finite neighbour turns the result into NaN and -0 may become +0.
+//
+// MI355X design (source-row-centric): the y and z index tables are monotone, so every
+// source row (sy, sz) that is read at all feeds a rectangle of destination rows
+// [y0,y1) x [z0,z1).  One wave owns one source row: it reads the row once from HBM,
+// converts each source voxel once, replicates along x in registers (integer x ratio) and
+// streams the result into every destination row of its rectangle with 16-byte nontemporal
+// stores.  HBM traffic is therefore N_src*b_src + N_dst*b_dst, the algorithmic minimum.
+// General ratios use a gather through the exact x table; the float "Linear" chain reads its
+// neighbours through the same tables (L2/MALL-resident rows).
+
+#include "KernelCommon.hpp"
+#include "../runtime/Runtime.hpp"
+#include "volkit_hip.h"
+
+#include <cmath>
+#include <map>
+#include <mutex>
+#include <tuple>
+#include <vector>
+
+namespace vkt
+{
+namespace hipk
+{
+    using codec::MapParams;
+
+    vktError convertBox(vktHipVolumeView_t dst, vktHipVolumeView_t src, vktVec3i_t srcOrigin, bool clampSrc,
+                        vktVec3i_t dstOrigin, int64_t nx, int64_t ny, int64_t nz);
+    bool validView(vktHipVolumeView_t const& v);
+    bool encodeWrites(int32_t fmt);
+    bool overlaps(vktHipVolumeView_t const& a, vktHipVolumeView_t const& b);
+
+    // Exact reference index formula (Resample_serial.hpp:60-62 + int32 truncation).
+    inline int32_t srcIndex(int32_t d, int32_t dd, int32_t sd)
+    {
+        volatile float q = static_cast<float>(d) / static_cast<float>(dd);
+        volatile float s = q * static_cast<float>(sd);
+        return static_cast<int32_t>(s);
+    }
+
+    // One run: destination rows [d0, d1) all read source row `s`.
+    struct Run
+    {
+        int32_t s, d0, d1;
+    };
+
+    struct ResampleArgs
+    {
+        uint8_t* dst;
+        uint8_t const* src;
+        int32_t ddx, ddy;          // dst dims x, y (dst slab depth implied by runs)
+        int32_t sdx, sdy, sdz;     // src dims of the LOCAL source buffer
+        int32_t srcZ0;             // global z of local plane 0
+        int32_t srcGlobalDz;       // global source depth (hi.z clamp)
+        int32_t dstZ0;             // global z of dst plane 0
+        int32_t nRunsY, nRunsZ;
+        Run const* runsY;          // device
+        Run const* runsZ;          // device (s in GLOBAL source planes, d in GLOBAL dst planes)
+        int32_t const* xtab;       // device, ddx entries (gather/chain paths)
+        int32_t k;                 // integer x ratio (replication path)
+        int32_t fs, fd;
+        float slo, shi;
+        MapParams dm;
+        uint64_t srcVoxels;        // voxels in the local source buffer (flat-read clamp)
+        int32_t srcIsGlobalEnd;    // local buffer ends at the global end (clamp there)
+    };
+
+    template <int FS, int FD>
+    __device__ __forceinline__ uint32_t convertCode(uint32_t c, ResampleArgs const& a)
+    {
+        float v = codec::decode(c, FS == -1 ? a.fs : FS, a.slo, a.shi);
+        bool w;
+        return codec::encode(v, FD == -1 ? a.fd : FD, a.dm, w);
+    }
+
+    __device__ __forceinline__ uint64_t dstRowIndex(ResampleArgs const& a, int32_t yd, int32_t zdGlobal)
+    {
+        return (static_cast<uint64_t>(zdGlobal - a.dstZ0) * static_cast<uint64_t>(a.ddy) + static_cast<uint64_t>(yd)) *
+               static_cast<uint64_t>(a.ddx);
+    }
+
+    __device__ __forceinline__ uint64_t srcRowIndex(ResampleArgs const& a, int32_t ys, int32_t zsGlobal)
+    {
+        return (static_cast<uint64_t>(zsGlobal - a.srcZ0) * static_cast<uint64_t>(a.sdy) + static_cast<uint64_t>(ys)) *
+               static_cast<uint64_t>(a.sdx);
+    }
+
+    // ---- integer-ratio replication path --------------------------------------------
+    // Wave-per-source-row.  K = dst voxels per source voxel along x (1, 2 or 4); BPV is the
+    // common voxel size; CONV = re-encode each source voxel (false when the code mapping is
+    // the identity, verified on the host over every code).
+    template <int BPV, int K, bool CONV, int FS, int FD>
+    __global__ __launch_bounds__(kBlock) void resampleRepKernel(ResampleArgs a)
+    {
+        int const lane = threadIdx.x & 63;
+        uint32_t const wavesPerBlock = blockDim.x >> 6;
+        uint32_t const wave = xcdSwizzle(blockIdx.x, gridDim.x) * wavesPerBlock + (threadIdx.x >> 6);
+        uint32_t const totalWaves = gridDim.x * wavesPerBlock;
+        uint32_t const tasks = static_cast<uint32_t>(a.nRunsY) * static_cast<uint32_t>(a.nRunsZ);
+        int32_t const chunks = a.sdx >> 3;   // 8 source voxels per lane-chunk
+
+        for (uint32_t t = wave; t < tasks; t += totalWaves)
+        {
+            Run const ry = a.runsY[t % static_cast<uint32_t>(a.nRunsY)];
+            Run const rz = a.runsZ[t / static_cast<uint32_t>(a.nRunsY)];
+            uint64_t const srow = srcRowIndex(a, ry.s, rz.s);
+            for (int32_t c = lane; c < chunks; c += 64)
+            {
+                uint32_t code[8];
+                load8<BPV>(a.src, srow + (static_cast<uint64_t>(c) << 3), code);
+                if constexpr (CONV)
+                {
+#pragma unroll
+                    for (int v = 0; v < 8; ++v)
+                        code[v] = convertCode<FS, FD>(code[v], a);
+                }
+                // dst voxels [8K*c, 8K*c + 8K): group g holds dst voxels 8g..8g+7 of the chunk
+                uint32_t grp[K][8];
+#pragma unroll
+                for (int g = 0; g < K; ++g)
+#pragma unroll
+                    for (int i = 0; i < 8; ++i)
+                        grp[g][i] = code[(8 * g + i) / K];
+                uint64_t const dx0 = static_cast<uint64_t>(c) * 8u * K;
+                for (int32_t zd = rz.d0; zd < rz.d1; ++zd)
+                    for (int32_t yd = ry.d0; yd < ry.d1; ++yd)
+                    {
+                        uint64_t drow = dstRowIndex(a, yd, zd) + dx0;
+#pragma unroll
+                        for (int g = 0; g < K; ++g)
+                            store8<BPV, true>(a.dst, drow + 8u * g, grp[g]);
+                    }
+            }
+        }
+    }
+
+    // ---- general gather path (any ratio, any formats, Nearest semantics) -------------
+    // Wave-per-source-row again; lanes walk the destination x range and gather through the
+    // exact x table (the source row stays in L1/L2 while the wave reads it).
+    __global__ __launch_bounds__(kBlock) void resampleGatherKernel(ResampleArgs a, int32_t conv)
+    {
+        int const lane = threadIdx.x & 63;
+        uint32_t const wavesPerBlock = blockDim.x >> 6;
+        uint32_t const wave = xcdSwizzle(blockIdx.x, gridDim.x) * wavesPerBlock + (threadIdx.x >> 6);
+        uint32_t const totalWaves = gridDim.x * wavesPerBlock;
+        uint32_t const tasks = static_cast<uint32_t>(a.nRunsY) * static_cast<uint32_t>(a.nRunsZ);
+        uint32_t const bs = codec::bytesPerVoxel(a.fs), bd = codec::bytesPerVoxel(a.fd);
+
+        for (uint32_t t = wave; t < tasks; t += totalWaves)
+        {
+            Run const ry = a.runsY[t % static_cast<uint32_t>(a.nRunsY)];
+            Run const rz = a.runsZ[t / static_cast<uint32_t>(a.nRunsY)];
+            uint64_t const srow = srcRowIndex(a, ry.s, rz.s);
+            for (int32_t x = lane; x < a.ddx; x += 64)
+            {
+                uint32_t c = loadCodeDyn(a.src, srow + static_cast<uint64_t>(a.xtab[x]), bs);
+                if (conv)
+                    c = convertCode<-1, -1>(c, a);
+                for (int32_t zd = rz.d0; zd < rz.d1; ++zd)
+                    for (int32_t yd = ry.d0; yd < ry.d1; ++yd)
+                        storeCodeDyn(a.dst, dstRowIndex(a, yd, zd) + static_cast<uint64_t>(x), bd, c);
+            }
+        }
+    }
+
+    // ---- "Linear" with float semantics: the exact sampleLinear lerp chain -------------
+    // Value depends only on the source position, so it is evaluated per destination voxel
+    // from the 8 neighbours (StructuredVolumeView.hpp:80-119): lo = (sx,sy,sz); hi.x reads
+    // the next voxel in memory (unclamped in the reference); hi.y, hi.z are clamped.
+    __device__ __forceinline__ float flatValue(ResampleArgs const& a, uint64_t voxel, uint32_t bs)
+    {
+        if (voxel >= a.srcVoxels)
+            voxel = a.srcVoxels - 1;   // reference reads past the buffer end (UB); clamp
+        return codec::decode(loadCodeDyn(a.src, voxel, bs), a.fs, a.slo, a.shi);
+    }
+
+    __global__ __launch_bounds__(kBlock) void resampleChainKernel(ResampleArgs a)
+    {
+        int const lane = threadIdx.x & 63;
+        uint32_t const wavesPerBlock = blockDim.x >> 6;
+        uint32_t const wave = xcdSwizzle(blockIdx.x, gridDim.x) * wavesPerBlock + (threadIdx.x >> 6);
+        uint32_t const totalWaves = gridDim.x * wavesPerBlock;
+        uint32_t const tasks = static_cast<uint32_t>(a.nRunsY) * static_cast<uint32_t>(a.nRunsZ);
+        uint32_t const bs = codec::bytesPerVoxel(a.fs), bd = codec::bytesPerVoxel(a.fd);
+
+        for (uint32_t t = wave; t < tasks; t += totalWaves)
+        {
+            Run const ry = a.runsY[t % static_cast<uint32_t>(a.nRunsY)];
+            Run const rz = a.runsZ[t / static_cast<uint32_t>(a.nRunsY)];
+            int32_t const hy = ry.s + 1 < a.sdy ? ry.s + 1 : a.sdy - 1;
+            int32_t const hz = rz.s + 1 < a.srcGlobalDz ? rz.s + 1 : a.srcGlobalDz - 1;
+            uint64_t const r00 = srcRowIndex(a, ry.s, rz.s), r10 = srcRowIndex(a, hy, rz.s);
+            uint64_t const r01 = srcRowIndex(a, ry.s, hz), r11 = srcRowIndex(a, hy, hz);
+            for (int32_t x = lane; x < a.ddx; x += 64)
+            {
+                uint64_t const sx = static_cast<uint64_t>(a.xtab[x]);
+                float v0 = flatValue(a, r00 + sx, bs), v1 = flatValue(a, r00 + sx + 1, bs);
+                float v2 = flatValue(a, r10 + sx, bs), v3 = flatValue(a, r10 + sx + 1, bs);
+                float v4 = flatValue(a, r01 + sx, bs), v5 = flatValue(a, r01 + sx + 1, bs);
+                float v6 = flatValue(a, r11 + sx, bs), v7 = flatValue(a, r11 + sx + 1, bs);
+                float const f = 0.f;   // xf1 - lo.x etc.: lo is never clamped, so every fraction is 0
+                float value = codec::lerp(codec::lerp(codec::lerp(v0, v1, f), codec::lerp(v2, v3, f), f),
+                                          codec::lerp(codec::lerp(v4, v5, f), codec::lerp(v6, v7, f), f), f);
+                bool w;
+                uint32_t c = codec::encode(value, a.fd, a.dm, w);
+                for (int32_t zd = rz.d0; zd < rz.d1; ++zd)
+                    for (int32_t yd = ry.d0; yd < ry.d1; ++yd)
+                        storeCodeDyn(a.dst, dstRowIndex(a, yd, zd) + static_cast<uint64_t>(x), bd, c);
+            }
+        }
+    }
+
+    // ---- host planning -------------------------------------------------------------
+    std::vector<Run> buildRuns(int32_t dstBegin, int32_t dstEnd, int32_t dd, int32_t sd)
+    {
+        std::vector<Run> runs;
+        for (int32_t d = dstBegin; d < dstEnd; ++d)
+        {
+            int32_t s = srcIndex(d, dd, sd);
+            if (!runs.empty() && runs.back().s == s)
+                runs.back().d1 = d + 1;
+            else
+                runs.push_back(Run{s, d, d + 1});
+        }
+        return runs;
+    }
+
+    // Device copies of the per-geometry tables, cached for the life of the process (a
+    // benchmark or pipeline resamples the same geometry repeatedly; uploading per call would
+    // put a pageable H2D copy in every step).
+    struct TableKey
+    {
+        int32_t v[9];
+        bool operator<(TableKey const& o) const
+        {
+            for (int i = 0; i < 9; ++i)
+                if (v[i] != o.v[i])
+                    return v[i] < o.v[i];
+            return false;
+        }
+    };
+
+    struct Tables
+    {
+        int32_t* dev = nullptr;
+        int32_t nRunsY = 0, nRunsZ = 0;
+        int32_t k = 0;            // integer x ratio, 0 if none
+        int32_t minSz = 0, maxSz = 0;
+        Run const* runsY = nullptr;
+        Run const* runsZ = nullptr;
+        int32_t const* xtab = nullptr;
+    };
+
+    vktError getTables(int32_t ddx, int32_t ddy, int32_t dgz, int32_t dz0, int32_t dnz, int32_t sdx, int32_t sdy,
+                       int32_t sgz, Tables& out)
+    {
+        static std::mutex m;
+        static std::map<std::pair<int, TableKey>, Tables> cache;
+        TableKey key{{ddx, ddy, dgz, dz0, dnz, sdx, sdy, sgz, 0}};
+        int dev = rt::device();
+        std::lock_guard<std::mutex> lock(m);
+        auto it = cache.find({dev, key});
+        if (it != cache.end())
+        {
+            out = it->second;
+            return vktNoError;
+        }
+        std::vector<Run> ry = buildRuns(0, ddy, ddy, sdy);
+        std::vector<Run> rz = buildRuns(dz0, dz0 + dnz, dgz, sgz);
+        std::vector<int32_t> xt(static_cast<size_t>(ddx));
+        bool rep = ddx % sdx == 0;
+        int32_t k = rep ? ddx / sdx : 0;
+        for (int32_t x = 0; x < ddx; ++x)
+        {
+            xt[x] = srcIndex(x, ddx, sdx);
+            if (rep && xt[x] != x / k)
+                rep = false;
+        }
+        for (Run const& r : ry)
+            if (r.s < 0 || r.s >= sdy)
+                return rt::fail("Resample: y index table leaves the source (reference would read out of bounds)");
+        for (int32_t s : xt)
+            if (s < 0 || s >= sdx)
+                return rt::fail("Resample: x index table leaves the source (reference would read out of bounds)");
+        for (Run const& r : rz)
+            if (r.s < 0 || r.s >= sgz)
+                return rt::fail("Resample: z index table leaves the source (reference would read out of bounds)");
+        Tables t;
+        t.nRunsY = static_cast<int32_t>(ry.size());
+        t.nRunsZ = static_cast<int32_t>(rz.size());
+        t.k = rep ? k : 0;
+        t.minSz = rz.empty() ? 0 : rz.front().s;
+        t.maxSz = rz.empty() ? -1 : rz.back().s;
+        size_t words = 3 * ry.size() + 3 * rz.size() + xt.size();
+        std::vector<int32_t> host;
+        host.reserve(words);
+        for (Run const& r : ry) host.insert(host.end(), {r.s, r.d0, r.d1});
+        for (Run const& r : rz) host.insert(host.end(), {r.s, r.d0, r.d1});
+        host.insert(host.end(), xt.begin(), xt.end());
+        VKT_HIP_TRY(hipMalloc(&t.dev, words * sizeof(int32_t) + 16));
+        VKT_HIP_TRY(hipMemcpy(t.dev, host.data(), words * sizeof(int32_t), hipMemcpyHostToDevice));
+        t.runsY = reinterpret_cast<Run const*>(t.dev);
+        t.runsZ = reinterpret_cast<Run const*>(t.dev + 3 * ry.size());
+        t.xtab = t.dev + 3 * ry.size() + 3 * rz.size();
+        cache[{dev, key}] = t;
+        out = t;
+        return vktNoError;
+    }
+
+    // Is map_dst(unmap_src(c)) == c for every code c?  (only <=16-bit formats are enumerable)
+    bool identityConversionUncached(int32_t fs, float slo, float shi, int32_t fd, float dlo, float dhi)
+    {
+        if (fs != fd)
+            return false;
+        uint32_t n;
+        if (fs == codec::FmtUInt8)
+            n = 256;
+        else if (fs == codec::FmtUInt16 || fs == codec::FmtInt16)
+            n = 65536;
+        else
+            return false;
+        MapParams dm = codec::makeMapParams(dlo, dhi);
+        for (uint32_t c = 0; c < n; ++c)
+        {
+            bool w;
+            if (codec::encode(codec::decode(c, fs, slo, shi), fd, dm, w) != c)
+                return false;
+        }
+        return true;
+    }
+
+    // Are all unmapped source values finite, so that Linear's 0*neighbour terms vanish?
+    bool allSourceValuesFiniteUncached(int32_t fs, float lo, float hi)
+    {
+        if (fs == codec::FmtUInt8 || fs == codec::FmtUInt16 || fs == codec::FmtInt16)
+        {
+            uint32_t n = fs == codec::FmtUInt8 ? 256u : 65536u;
+            for (uint32_t c = 0; c < n; ++c)
+                if (!std::isfinite(codec::decode(c, fs, lo, hi)))
+                    return false;
+            return true;
+        }
+        if (fs == codec::FmtUInt32)
+            return std::isfinite(lo) && std::isfinite(hi) && std::fabs(lo) <= 1e38f && std::fabs(hi) <= 1e38f;
+        if (fs == codec::FmtInt8 || fs == codec::FmtInt32)
+            return true;   // unmap leaves 0.f
+        return false;      // Float32: raw bits, anything goes
+    }
+
+    // Both properties are enumerations over up to 65536 codes (~ms); cache them per mapping.
+    struct ConvProps
+    {
+        bool identity;
+        bool finite;
+    };
+
+    ConvProps conversionProperties(int32_t fs, float slo, float shi, int32_t fd, float dlo, float dhi)
+    {
+        static std::mutex m;
+        static std::map<std::tuple<int32_t, uint32_t, uint32_t, int32_t, uint32_t, uint32_t>, ConvProps> cache;
+        auto key = std::make_tuple(fs, codec::floatToBits(slo), codec::floatToBits(shi), fd, codec::floatToBits(dlo),
+                                   codec::floatToBits(dhi));
+        std::lock_guard<std::mutex> lock(m);
+        auto it = cache.find(key);
+        if (it != cache.end())
+            return it->second;
+        ConvProps p{identityConversionUncached(fs, slo, shi, fd, dlo, dhi), allSourceValuesFiniteUncached(fs, slo, shi)};
+        cache[key] = p;
+        return p;
+    }
+
+    vktError resampleSlab(vktHipVolumeView_t dst, vktHipVolumeView_t src, vktFilterMode fm, int32_t dgz, int32_t dz0,
+                          int32_t sgz, int32_t sz0)
+    {
+        if (!validView(dst) || !validView(src))
+            return rt::fail("Resample_hip: invalid volume view");
+        if (fm != vktFilterModeNearest && fm != vktFilterModeLinear)
+            return rt::fail("Resample_hip: unknown filter mode");
+        if (dst.dimX == 0 || dst.dimY == 0 || dst.dimZ == 0)
+            return vktNoError;
+        if (src.dimX <= 0 || src.dimY <= 0 || src.dimZ <= 0)
+            return rt::fail("Resample_hip: empty source");
+        if (dz0 < 0 || dz0 + dst.dimZ > dgz || sz0 < 0 || sz0 + src.dimZ > sgz)
+            return rt::fail("Resample_hip: slab outside the global volume");
+        if (overlaps(dst, src) && dst.data != src.data)
+            return rt::fail("Resample_hip: partially overlapping source and destination");
+        if (!encodeWrites(dst.dataFormat))
+            return vktNoError;
+
+        hipStream_t s = rt::computeStream();
+        // same-dims branch (Resample_serial.hpp:32-48)
+        if (dst.dimX == src.dimX && dst.dimY == src.dimY && dgz == sgz)
+        {
+            if (dz0 < sz0 || dz0 + dst.dimZ > sz0 + src.dimZ)
+                return rt::fail("Resample_hip: source slab does not hold the planes this dst slab reads");
+            if (dst.data == src.data && dz0 != sz0)
+                return rt::fail("Resample_hip: in-place same-dims resample needs aligned slabs");
+            vktError e = convertBox(dst, src, vktVec3i_t{0, 0, dz0 - sz0}, false, vktVec3i_t{0, 0, 0}, dst.dimX,
+                                    dst.dimY, dst.dimZ);
+            return e != vktNoError ? e : rt::finishLaunch("Resample_hip(same dims)");
+        }
+        if (dst.data == src.data)
+            return rt::fail("Resample_hip: in-place resample with different dims");
+
+        Tables t;
+        vktError e = getTables(dst.dimX, dst.dimY, dgz, dz0, dst.dimZ, src.dimX, src.dimY, sgz, t);
+        if (e != vktNoError)
+            return e;
+
+        ConvProps const props = conversionProperties(src.dataFormat, src.mappingLo, src.mappingHi, dst.dataFormat,
+                                                     dst.mappingLo, dst.mappingHi);
+        bool const identity = props.identity;
+        bool const chain = fm == vktFilterModeLinear && (dst.dataFormat == codec::FmtFloat32 || !props.finite);
+        // planes this dst slab reads: for the chain also the clamped z+1 neighbour plane and
+        // the first voxel of the plane after it (hi.x of that plane's last voxel)
+        int32_t needLo = t.minSz, needHi = t.maxSz;
+        if (chain)
+            needHi = needHi + 2 < sgz ? needHi + 2 : sgz - 1;
+        if (needLo < sz0 || needHi >= sz0 + src.dimZ)
+            return rt::fail("Resample_hip: source slab does not hold the planes this dst slab reads");
+
+        ResampleArgs a{};
+        a.dst = dst.data;
+        a.src = src.data;
+        a.ddx = dst.dimX;
+        a.ddy = dst.dimY;
+        a.sdx = src.dimX;
+        a.sdy = src.dimY;
+        a.sdz = src.dimZ;
+        a.srcZ0 = sz0;
+        a.srcGlobalDz = sgz;
+        a.dstZ0 = dz0;
+        a.nRunsY = t.nRunsY;
+        a.nRunsZ = t.nRunsZ;
+        a.runsY = t.runsY;
+        a.runsZ = t.runsZ;
+        a.xtab = t.xtab;
+        a.k = t.k;
+        a.fs = src.dataFormat;
+        a.fd = dst.dataFormat;
+        a.slo = src.mappingLo;
+        a.shi = src.mappingHi;
+        a.dm = codec::makeMapParams(dst.mappingLo, dst.mappingHi);
+        a.srcVoxels = static_cast<uint64_t>(src.dimX) * src.dimY * src.dimZ;
+        a.srcIsGlobalEnd = sz0 + src.dimZ == sgz;
+
+        uint64_t tasks = static_cast<uint64_t>(t.nRunsY) * static_cast<uint64_t>(t.nRunsZ);
+        if (tasks >= (1ull << 32))
+            return rt::fail("Resample_hip: too many source rows");
+        unsigned grid = streamingGrid(tasks, kBlock / 64);
+
+        if (chain)
+        {
+            hipLaunchKernelGGL(resampleChainKernel, dim3(grid), dim3(kBlock), 0, s, a);
+            return rt::finishLaunch("Resample_hip(linear chain)");
+        }
+
+        uint32_t const bs = codec::bytesPerVoxel(src.dataFormat), bd = codec::bytesPerVoxel(dst.dataFormat);
+        bool const aligned = reinterpret_cast<uintptr_t>(src.data) % 16 == 0 &&
+                             reinterpret_cast<uintptr_t>(dst.data) % 16 == 0 && src.dimX % 8 == 0;
+        if (t.k >= 1 && t.k <= 4 && t.k != 3 && aligned && bs == bd)
+        {
+#define VKT_REP_LAUNCH(BPV, K, CONV, FS, FD)                                                               \
+    hipLaunchKernelGGL((resampleRepKernel<BPV, K, CONV, FS, FD>), dim3(grid), dim3(kBlock), 0, s, a)
+#define VKT_REP_BY_K(BPV, CONV, FS, FD)                                                                    \
+    do {                                                                                                   \
+        if (t.k == 1) VKT_REP_LAUNCH(BPV, 1, CONV, FS, FD);                                                \
+        else if (t.k == 2) VKT_REP_LAUNCH(BPV, 2, CONV, FS, FD);                                           \
+        else VKT_REP_LAUNCH(BPV, 4, CONV, FS, FD);                                                         \
+    } while (0)
+            if (identity)
+            {
+                if (bs == 1) VKT_REP_BY_K(1, false, -1, -1);
+                else if (bs == 2) VKT_REP_BY_K(2, false, -1, -1);
+                else VKT_REP_BY_K(4, false, -1, -1);
+            }
+            else if (src.dataFormat == codec::FmtUInt16 && dst.dataFormat == codec::FmtUInt16)
+                VKT_REP_BY_K(2, true, codec::FmtUInt16, codec::FmtUInt16);
+            else if (src.dataFormat == codec::FmtUInt8 && dst.dataFormat == codec::FmtUInt8)
+                VKT_REP_BY_K(1, true, codec::FmtUInt8, codec::FmtUInt8);
+            else if (bs == 1) VKT_REP_BY_K(1, true, -1, -1);
+            else if (bs == 2) VKT_REP_BY_K(2, true, -1, -1);
+            else VKT_REP_BY_K(4, true, -1, -1);
+#undef VKT_REP_BY_K
+#undef VKT_REP_LAUNCH
+            return rt::finishLaunch("Resample_hip(replicate)");
+        }
+        hipLaunchKernelGGL(resampleGatherKernel, dim3(grid), dim3(kBlock), 0, s, a, identity ? 0 : 1);
+        return rt::finishLaunch("Resample_hip(gather)");
+    }
+
+} // hipk
+} // vkt
+
+using namespace vkt;
+
+extern "C" {
+
+vktError vktHipResample(vktHipVolumeView_t dst, vktHipVolumeView_t src, vktFilterMode fm)
+{
+    return hipk::resampleSlab(dst, src, fm, dst.dimZ, 0, src.dimZ, 0);
+}
+
+vktError vktHipResampleSlab(vktHipVolumeView_t dst, vktHipVolumeView_t src, vktFilterMode fm, int32_t dstGlobalDimZ,
+                            int32_t dstZ0, int32_t srcGlobalDimZ, int32_t srcZ0)
+{
+    return hipk::resampleSlab(dst, src, fm, dstGlobalDimZ, dstZ0, srcGlobalDimZ, srcZ0);
+}
+
+vktError vktHipResampleSlabSourceRange(int32_t dstGlobalDimZ, int32_t dstZ0, int32_t dstZ1, int32_t srcGlobalDimZ,
+                                       vktFilterMode fm, int32_t needsNeighbours, int32_t* srcZBegin,
+                                       int32_t* srcZEnd)
+{
+    if (srcZBegin == nullptr || srcZEnd == nullptr)
+        return rt::fail("vktHipResampleSlabSourceRange: null pointer");
+    if (dstZ1 <= dstZ0)
+    {
+        *srcZBegin = *srcZEnd = 0;
+        return vktNoError;
+    }
+    if (dstGlobalDimZ == srcGlobalDimZ)   // same-dims branch maps plane to plane
+    {
+        *srcZBegin = dstZ0;
+        *srcZEnd = dstZ1;
+        return vktNoError;
+    }
+    int32_t lo = hipk::srcIndex(dstZ0, dstGlobalDimZ, srcGlobalDimZ);
+    int32_t hi = hipk::srcIndex(dstZ1 - 1, dstGlobalDimZ, srcGlobalDimZ);
+    if (fm == vktFilterModeLinear && needsNeighbours)
+        hi = hi + 2 < srcGlobalDimZ ? hi + 2 : srcGlobalDimZ - 1;
+    *srcZBegin = lo;
+    *srcZEnd = hi + 1;
+    return vktNoError;
+}
+
+} // extern "C"

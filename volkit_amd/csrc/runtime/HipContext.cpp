@@ -1,0 +1,256 @@
+// HipContext.cpp -- process-wide HIP context: device, compute/copy streams, errors, timing.
+//
+// Realises the design intent of the reference's declared-but-undefined CUDA context API
+// (reference include/c/vkt/CudaContext.h:17-65: async execution flag, compute and copy
+// stream ids) as the vktHip* runtime functions of include/volkit_hip.h.
+
+#include "Runtime.hpp"
+#include "volkit_hip.h"
+
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <iostream>
+#include <mutex>
+
+namespace vkt
+{
+namespace rt
+{
+    namespace
+    {
+        struct Context
+        {
+            std::mutex mutex;
+            bool initialised = false;
+            int device = -1;              // requested device, -1 = current at first use
+            hipStream_t ownCompute = nullptr;
+            hipStream_t userCompute = nullptr;
+            bool userStreamSet = false;
+            hipStream_t copy = nullptr;
+            std::atomic<int> async{1};
+            std::atomic<int> timing{0};
+        };
+
+        Context& ctx()
+        {
+            static Context* c = new Context;   // intentionally leaked: no teardown-order issues
+            return *c;
+        }
+
+        thread_local std::string tlsLastError;
+        thread_local float tlsLastKernelMs = 0.f;
+
+        int logLevelFromEnv()
+        {
+            char const* s = std::getenv("VKT_LOG_LEVEL");
+            if (s == nullptr)
+                return 2;
+            return std::atoi(s);
+        }
+
+        void initLocked(Context& c)
+        {
+            if (c.initialised)
+                return;
+            if (c.device >= 0)
+                (void)hipSetDevice(c.device);
+            else
+                (void)hipGetDevice(&c.device);
+            // Blocking streams: they synchronise with the NULL stream, so user code that
+            // hipMemcpy's from getData() pointers sees finished kernels, exactly as with the
+            // reference's legacy-default-stream launches.
+            (void)hipStreamCreateWithFlags(&c.ownCompute, hipStreamDefault);
+            (void)hipStreamCreateWithFlags(&c.copy, hipStreamDefault);
+            c.initialised = true;
+        }
+    } // namespace
+
+    LogStream::~LogStream()
+    {
+        static int const threshold = logLevelFromEnv();
+        if (static_cast<int>(level_) > threshold)
+            return;
+        static char const* const tag[] = {"\033[1;31m[volkit error]\033[0m ", "\033[1;33m[volkit warning]\033[0m ",
+                                          "[volkit] "};
+        std::string msg = tag[static_cast<int>(level_)] + stream_.str() + "\n";
+        std::fwrite(msg.data(), 1, msg.size(), stdout);
+        std::fflush(stdout);
+    }
+
+    hipStream_t computeStream()
+    {
+        Context& c = ctx();
+        std::lock_guard<std::mutex> lock(c.mutex);
+        initLocked(c);
+        return c.userStreamSet ? c.userCompute : c.ownCompute;
+    }
+
+    hipStream_t copyStream()
+    {
+        Context& c = ctx();
+        std::lock_guard<std::mutex> lock(c.mutex);
+        initLocked(c);
+        return c.copy;
+    }
+
+    bool asyncExecution() { return ctx().async.load() != 0; }
+
+    int device()
+    {
+        Context& c = ctx();
+        std::lock_guard<std::mutex> lock(c.mutex);
+        initLocked(c);
+        return c.device;
+    }
+
+    void setLastError(std::string const& msg) { tlsLastError = msg; }
+
+    vktError check(hipError_t err, char const* what)
+    {
+        if (err == hipSuccess)
+            return vktNoError;
+        std::string msg = std::string(what) + ": " + hipGetErrorString(err);
+        setLastError(msg);
+        VKT_LOG(LogLevel::Error) << msg;
+        return vktInvalidValue;
+    }
+
+    vktError fail(char const* what)
+    {
+        setLastError(what);
+        VKT_LOG(LogLevel::Error) << what;
+        return vktInvalidValue;
+    }
+
+    vktError finishLaunch(char const* what)
+    {
+        vktError e = check(hipGetLastError(), what);
+        if (e != vktNoError)
+            return e;
+        if (!asyncExecution())
+            return check(hipStreamSynchronize(computeStream()), what);
+        return vktNoError;
+    }
+
+    bool kernelTimingEnabled() { return ctx().timing.load() != 0; }
+
+    ScopedKernelTimer::ScopedKernelTimer(char const* name, bool log)
+        : name_(name), active_(log || kernelTimingEnabled()), log_(log)
+    {
+        if (!active_)
+            return;
+        hipStream_t s = computeStream();
+        if (hipEventCreate(&start_) != hipSuccess || hipEventCreate(&stop_) != hipSuccess)
+        {
+            active_ = false;
+            return;
+        }
+        (void)hipEventRecord(start_, s);
+    }
+
+    ScopedKernelTimer::~ScopedKernelTimer()
+    {
+        if (!active_)
+            return;
+        (void)hipEventRecord(stop_, computeStream());
+        (void)hipEventSynchronize(stop_);
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, start_, stop_);
+        tlsLastKernelMs = ms;
+        (void)hipEventDestroy(start_);
+        (void)hipEventDestroy(stop_);
+        if (log_)
+            VKT_LOG(LogLevel::Info) << "Device: GPU (HIP, gfx950), algorithm: " << name_
+                                    << ", time elapsed: " << ms * 1e-3f << " sec.";
+    }
+
+} // rt
+} // vkt
+
+using namespace vkt;
+
+extern "C" {
+
+vktError vktHipSetDevice(int32_t dev)
+{
+    rt::Context& c = rt::ctx();
+    std::lock_guard<std::mutex> lock(c.mutex);
+    if (c.initialised && c.device != dev)
+        return rt::fail("vktHipSetDevice: the HIP context is already initialised on another device");
+    c.device = dev;
+    return rt::check(hipSetDevice(dev), "hipSetDevice");
+}
+
+vktError vktHipGetDevice(int32_t* dev)
+{
+    if (dev == nullptr)
+        return rt::fail("vktHipGetDevice: null pointer");
+    *dev = rt::device();
+    return vktNoError;
+}
+
+vktError vktHipSetAsyncExecution(int32_t async)
+{
+    rt::ctx().async.store(async != 0);
+    return vktNoError;
+}
+
+vktError vktHipGetAsyncExecution(int32_t* async)
+{
+    if (async == nullptr)
+        return rt::fail("vktHipGetAsyncExecution: null pointer");
+    *async = rt::ctx().async.load();
+    return vktNoError;
+}
+
+vktError vktHipSetComputeStream(void* stream)
+{
+    rt::Context& c = rt::ctx();
+    std::lock_guard<std::mutex> lock(c.mutex);
+    rt::initLocked(c);
+    c.userCompute = static_cast<hipStream_t>(stream);
+    c.userStreamSet = stream != nullptr;
+    return vktNoError;
+}
+
+vktError vktHipGetComputeStream(void** stream)
+{
+    if (stream == nullptr)
+        return rt::fail("vktHipGetComputeStream: null pointer");
+    *stream = rt::computeStream();
+    return vktNoError;
+}
+
+vktError vktHipGetCopyStream(void** stream)
+{
+    if (stream == nullptr)
+        return rt::fail("vktHipGetCopyStream: null pointer");
+    *stream = rt::copyStream();
+    return vktNoError;
+}
+
+vktError vktHipSynchronize(void)
+{
+    VKT_HIP_TRY(hipStreamSynchronize(rt::computeStream()));
+    VKT_HIP_TRY(hipStreamSynchronize(rt::copyStream()));
+    return vktNoError;
+}
+
+const char* vktHipGetLastErrorString(void) { return rt::tlsLastError.c_str(); }
+
+vktError vktHipSetKernelTiming(int32_t enable)
+{
+    rt::ctx().timing.store(enable != 0);
+    return vktNoError;
+}
+
+vktError vktHipGetLastKernelMs(float* ms)
+{
+    if (ms == nullptr)
+        return rt::fail("vktHipGetLastKernelMs: null pointer");
+    *ms = rt::tlsLastKernelMs;
+    return vktNoError;
+}
+
+} // extern "C"

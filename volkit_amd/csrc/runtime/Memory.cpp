@@ -1,0 +1,209 @@
+// Memory.cpp -- allocation, copies and deferred migration on HIP.
+//
+// Reference: Allocate/Free/Memcpy/MemsetRange dispatch on the thread policy
+// (src/vkt/Memory.cpp:30-80) to malloc/free/memcpy or cudaMalloc/cudaFree/synchronous
+// cudaMemcpy (src/vkt/Memory_cuda.hpp:16-24), and ManagedBuffer::migrate
+// (include/cpp/vkt/ManagedBuffer.hpp:168-198) allocates on the new device, copies, and frees
+// under the old policy.
+//
+// MI355X design: host<->device traffic goes through a side copy stream.  The copy stream
+// first waits (event) for everything already queued on the compute stream, so a D2H
+// migration after GPU kernels sees their results; an H2D copy is followed by an event the
+// compute stream waits on.  Host-facing copies return only when the bytes have landed (the
+// reference's cudaMemcpy contract: the caller may free or read host memory right after).
+// Device-to-device copies stay on the compute stream, ordered with the kernels.
+
+#include "Runtime.hpp"
+#include "volkit_hip.h"
+
+#include <cstdlib>
+#include <cstring>
+
+namespace vkt
+{
+namespace hipk
+{
+    // Pattern fill kernel launcher (kernels/Memset.hip).
+    vktError memsetRange(void* dst, void const* pattern, std::size_t dstSize, std::size_t patternSize);
+}
+
+namespace
+{
+    bool onGpu(ExecutionPolicy const& p) { return p.device == ExecutionPolicy::Device::GPU; }
+
+    // Copy stream waits for the compute stream's current tail.
+    vktError copyStreamAfterCompute()
+    {
+        hipEvent_t ev;
+        VKT_HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        vktError e = rt::check(hipEventRecord(ev, rt::computeStream()), "hipEventRecord(compute)");
+        if (e == vktNoError)
+            e = rt::check(hipStreamWaitEvent(rt::copyStream(), ev, 0), "hipStreamWaitEvent(copy)");
+        (void)hipEventDestroy(ev);
+        return e;
+    }
+
+    // Compute stream waits for the copy stream's current tail.
+    vktError computeStreamAfterCopy()
+    {
+        hipEvent_t ev;
+        VKT_HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        vktError e = rt::check(hipEventRecord(ev, rt::copyStream()), "hipEventRecord(copy)");
+        if (e == vktNoError)
+            e = rt::check(hipStreamWaitEvent(rt::computeStream(), ev, 0), "hipStreamWaitEvent(compute)");
+        (void)hipEventDestroy(ev);
+        return e;
+    }
+} // namespace
+
+namespace detail
+{
+    vktError memcpyHip(void* dst, void const* src, std::size_t size, CopyKind ck)
+    {
+        if (size == 0)
+            return vktNoError;
+        switch (ck)
+        {
+        case CopyKind::HostToHost:
+            std::memcpy(dst, src, size);
+            return vktNoError;
+        case CopyKind::DeviceToDevice:
+            VKT_HIP_TRY(hipMemcpyAsync(dst, src, size, hipMemcpyDeviceToDevice, rt::computeStream()));
+            return rt::finishLaunch("Memcpy(DeviceToDevice)");
+        case CopyKind::HostToDevice:
+        case CopyKind::DeviceToHost:
+        {
+            hipMemcpyKind kind = ck == CopyKind::HostToDevice ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost;
+            vktError e = copyStreamAfterCompute();
+            if (e != vktNoError)
+                return e;
+            VKT_HIP_TRY(hipMemcpyAsync(dst, src, size, kind, rt::copyStream()));
+            if (ck == CopyKind::HostToDevice)
+            {
+                e = computeStreamAfterCopy();
+                if (e != vktNoError)
+                    return e;
+            }
+            VKT_HIP_TRY(hipStreamSynchronize(rt::copyStream()));
+            return vktNoError;
+        }
+        }
+        return rt::fail("Memcpy: unknown CopyKind");
+    }
+
+    void* AllocateOn(std::size_t bytes, ExecutionPolicy const& owner)
+    {
+        if (bytes == 0)
+            return nullptr;
+        if (onGpu(owner))
+        {
+            (void)rt::device();   // bind the context's device before allocating
+            void* p = nullptr;
+            if (rt::check(hipMalloc(&p, bytes), "hipMalloc") != vktNoError)
+                return nullptr;
+            return p;
+        }
+        void* p = std::malloc(bytes);
+        if (p == nullptr)
+            rt::fail("Allocate: host malloc failed");
+        return p;
+    }
+
+    void FreeOn(void* data, ExecutionPolicy const& owner)
+    {
+        if (data == nullptr)
+            return;
+        if (onGpu(owner))
+            (void)rt::check(hipFree(data), "hipFree");
+        else
+            std::free(data);
+    }
+
+    void CopyOn(void* dst, void const* src, std::size_t bytes, ExecutionPolicy const& owner)
+    {
+        (void)memcpyHip(dst, src, bytes, onGpu(owner) ? CopyKind::DeviceToDevice : CopyKind::HostToHost);
+    }
+
+    void* MigrateBuffer(void* data, std::size_t bytes, ExecutionPolicy& last)
+    {
+        ExecutionPolicy ep = GetThreadExecutionPolicy();
+        if (ep.device == last.device)
+            return data;
+        void* fresh = AllocateOn(bytes, ep);
+        if (bytes > 0 && data != nullptr && fresh != nullptr)
+            (void)memcpyHip(fresh, data, bytes,
+                            onGpu(ep) ? CopyKind::HostToDevice : CopyKind::DeviceToHost);
+        FreeOn(data, last);
+        last = ep;
+        return fresh;
+    }
+} // detail
+
+void Allocate(void** ptr, std::size_t size)
+{
+    if (ptr != nullptr)
+        *ptr = detail::AllocateOn(size, GetThreadExecutionPolicy());
+}
+
+void Free(void* ptr) { detail::FreeOn(ptr, GetThreadExecutionPolicy()); }
+
+void Memcpy(void* dst, void const* src, std::size_t size, CopyKind ck) { (void)detail::memcpyHip(dst, src, size, ck); }
+
+void MemsetRange(void* dst, void const* src, std::size_t dstSize, std::size_t srcSize)
+{
+    if (onGpu(GetThreadExecutionPolicy()))
+    {
+        (void)hipk::memsetRange(dst, src, dstSize, srcSize);
+        return;
+    }
+    // Host-resident buffers (CPU policy): a plain pattern copy, as MemsetRange_serial
+    // (reference src/vkt/Memory_serial.hpp:24-37).  This is buffer housekeeping of
+    // ManagedBuffer::fill, not one of the StructuredVolume algorithms.
+    if (srcSize == 0)
+        return;
+    std::size_t n = dstSize / srcSize;
+    for (std::size_t i = 0; i < n; ++i)
+        std::memcpy(static_cast<char*>(dst) + i * srcSize, src, srcSize);
+}
+
+} // vkt
+
+extern "C" {
+
+void vktAllocate(void** ptr, size_t size) { vkt::Allocate(ptr, size); }
+
+void vktFree(void* ptr) { vkt::Free(ptr); }
+
+void vktMemcpy(void* dst, void const* src, size_t size, vktCopyKind ck)
+{
+    vkt::Memcpy(dst, src, size, static_cast<vkt::CopyKind>(ck));
+}
+
+vktError vktHipAllocate(void** ptr, size_t size)
+{
+    if (ptr == nullptr)
+        return vkt::rt::fail("vktHipAllocate: null pointer");
+    vkt::ExecutionPolicy gpu;
+    gpu.device = vkt::ExecutionPolicy::Device::GPU;
+    *ptr = vkt::detail::AllocateOn(size, gpu);
+    return (*ptr != nullptr || size == 0) ? vktNoError : vktInvalidValue;
+}
+
+vktError vktHipFree(void* ptr)
+{
+    if (ptr == nullptr)
+        return vktNoError;
+    return vkt::rt::check(hipFree(ptr), "hipFree");
+}
+
+vktError vktHipMemcpy(void* dst, void const* src, size_t size, vktCopyKind ck)
+{
+    return vkt::detail::memcpyHip(dst, src, size, static_cast<vkt::CopyKind>(ck));
+}
+
+vktError vktHipMemsetRange(void* dst, void const* pattern, size_t dstSize, size_t patternSize)
+{
+    return vkt::hipk::memsetRange(dst, pattern, dstSize, patternSize);
+}
+
+} // extern "C"

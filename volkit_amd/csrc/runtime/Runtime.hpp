@@ -1,0 +1,86 @@
+// Runtime.hpp -- internal runtime services of libvolkit (not installed).
+//
+// One HIP context per process (one process per GPU is the multi-GPU model): the device
+// chosen by vktHipSetDevice (default: the current HIP device at first use), a blocking
+// compute stream (ordered with the legacy NULL stream, like the reference's default-stream
+// launches), a side copy stream for migrate(), and error/timing bookkeeping.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <sstream>
+#include <string>
+
+#include "volkit_c.h"
+#include "volkit.hpp"
+
+namespace vkt
+{
+namespace rt
+{
+    enum class LogLevel { Error = 0, Warning = 1, Info = 2 };
+
+    // VKT_LOG equivalent (reference src/vkt/Logging.hpp:41): message is emitted when the
+    // temporary is destroyed; VKT_LOG_LEVEL=0/1/2 filters (default 2 = everything).
+    class LogStream
+    {
+    public:
+        explicit LogStream(LogLevel level) : level_(level) {}
+        ~LogStream();
+        std::ostream& stream() { return stream_; }
+
+    private:
+        std::ostringstream stream_;
+        LogLevel level_;
+    };
+
+    // Context accessors (created lazily, thread-safe).
+    hipStream_t computeStream();
+    hipStream_t copyStream();
+    bool asyncExecution();
+    int device();
+
+    // Error handling: record the message as the thread's last error, log it, return
+    // vktInvalidValue; vktNoError for hipSuccess.
+    vktError check(hipError_t err, char const* what);
+    vktError fail(char const* what);          // non-HIP failure (bad arguments)
+    void setLastError(std::string const& msg);
+
+    // Called by every backend entry point right after its launches: picks up launch
+    // errors and, if async execution is off, waits for the compute stream.
+    vktError finishLaunch(char const* what);
+
+    // printPerformance / vktHipGetLastKernelMs support: brackets a backend call with
+    // events on the compute stream.
+    class ScopedKernelTimer
+    {
+    public:
+        ScopedKernelTimer(char const* name, bool log);
+        ~ScopedKernelTimer();
+
+    private:
+        char const* name_;
+        bool active_;
+        bool log_;
+        hipEvent_t start_ = nullptr;
+        hipEvent_t stop_ = nullptr;
+    };
+
+    bool kernelTimingEnabled();
+
+} // rt
+
+namespace detail
+{
+    // Copy with the stream ordering described in runtime/Memory.cpp.
+    vktError memcpyHip(void* dst, void const* src, std::size_t size, CopyKind ck);
+}
+} // vkt
+
+#define VKT_LOG(LEVEL) ::vkt::rt::LogStream(LEVEL).stream()
+#define VKT_HIP_TRY(EXPR)                                                            \
+    do {                                                                             \
+        vktError vkt_err_ = ::vkt::rt::check((EXPR), #EXPR);                         \
+        if (vkt_err_ != vktNoError)                                                  \
+            return vkt_err_;                                                         \
+    } while (0)
