@@ -1,0 +1,9 @@
+#!/bin/bash
+# Quick GPU validation: parity tests then the default bench line.
+set -u
+cd "$(dirname "$0")/.."
+mkdir -p gpurun_out
+timeout -k 10 900 python -m pytest tests -m gpu -q -x > gpurun_out/pytest_gpu.log 2>&1
+rc=$?; tail -n 15 gpurun_out/pytest_gpu.log; [ $rc -gt 1 ] && exit $rc
+timeout -k 10 300 python bench.py --steps 20 --warmup 3 > gpurun_out/bench.log 2>&1 || { cat gpurun_out/bench.log; exit 1; }
+grep '^{' gpurun_out/bench.log

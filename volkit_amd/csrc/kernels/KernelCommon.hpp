@@ -72,12 +72,21 @@ namespace hipk
 
     // ---- 8 consecutive codes per lane ------------------------------------------------
     // BPV 1: one 8-byte load; BPV 2: one 16-byte load; BPV 4: two 16-byte loads.
-    template <int BPV>
+    template <class V, bool NT>
+    __device__ __forceinline__ V loadVec(void const* p)
+    {
+        if constexpr (NT)
+            return __builtin_nontemporal_load(reinterpret_cast<V const*>(p));
+        else
+            return *reinterpret_cast<V const*>(p);
+    }
+
+    template <int BPV, bool NT = false>
     __device__ __forceinline__ void load8(uint8_t const* base, uint64_t voxel, uint32_t (&c)[8])
     {
         if constexpr (BPV == 1)
         {
-            u32x2 v = *reinterpret_cast<u32x2 const*>(base + voxel);
+            u32x2 v = loadVec<u32x2, NT>(base + voxel);
 #pragma unroll
             for (int i = 0; i < 4; ++i)
             {
@@ -87,7 +96,7 @@ namespace hipk
         }
         else if constexpr (BPV == 2)
         {
-            u32x4 v = *reinterpret_cast<u32x4 const*>(base + 2 * voxel);
+            u32x4 v = loadVec<u32x4, NT>(base + 2 * voxel);
             c[0] = v.x & 0xFFFFu; c[1] = v.x >> 16;
             c[2] = v.y & 0xFFFFu; c[3] = v.y >> 16;
             c[4] = v.z & 0xFFFFu; c[5] = v.z >> 16;
@@ -95,10 +104,49 @@ namespace hipk
         }
         else
         {
-            u32x4 a = *reinterpret_cast<u32x4 const*>(base + 4 * voxel);
-            u32x4 b = *reinterpret_cast<u32x4 const*>(base + 4 * voxel + 16);
+            u32x4 a = loadVec<u32x4, NT>(base + 4 * voxel);
+            u32x4 b = loadVec<u32x4, NT>(base + 4 * voxel + 16);
             c[0] = a.x; c[1] = a.y; c[2] = a.z; c[3] = a.w;
             c[4] = b.x; c[5] = b.y; c[6] = b.z; c[7] = b.w;
+        }
+    }
+
+    // N consecutive codes (N*BPV bytes in {1,2,4,8,16,32}, naturally aligned) -> c[0..N)
+    template <int BPV, int N, bool NT>
+    __device__ __forceinline__ void loadN(uint8_t const* base, uint64_t voxel, uint32_t* c)
+    {
+        constexpr int kBytes = BPV * N;
+        uint8_t const* p = base + voxel * BPV;
+        uint32_t w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if constexpr (kBytes == 32)
+        {
+            u32x4 x = loadVec<u32x4, NT>(p), y = loadVec<u32x4, NT>(p + 16);
+            w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w;
+            w[4] = y.x; w[5] = y.y; w[6] = y.z; w[7] = y.w;
+        }
+        else if constexpr (kBytes == 16)
+        {
+            u32x4 x = loadVec<u32x4, NT>(p);
+            w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w;
+        }
+        else if constexpr (kBytes == 8)
+        {
+            u32x2 x = loadVec<u32x2, NT>(p);
+            w[0] = x.x; w[1] = x.y;
+        }
+        else if constexpr (kBytes == 4)
+            w[0] = loadVec<uint32_t, NT>(p);
+        else if constexpr (kBytes == 2)
+            w[0] = *reinterpret_cast<uint16_t const*>(p);
+        else
+            w[0] = *p;
+        constexpr uint32_t kMask = BPV == 4 ? 0xFFFFFFFFu : ((1u << (8 * BPV)) - 1u);
+#pragma unroll
+        for (int i = 0; i < N; ++i)
+        {
+            constexpr int kBits = 8 * BPV;
+            int off = i * kBits;
+            c[i] = (w[off / 32] >> (off % 32)) & kMask;
         }
     }
 

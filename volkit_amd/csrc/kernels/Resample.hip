@@ -99,49 +99,63 @@ namespace hipk
     }
 
     // ---- integer-ratio replication path --------------------------------------------
-    // Wave-per-source-row.  K = dst voxels per source voxel along x (1, 2 or 4); BPV is the
-    // common voxel size; CONV = re-encode each source voxel (false when the code mapping is
-    // the identity, verified on the host over every code).
+    // One wave per source row (task).  The destination row is written as 512-voxel store
+    // instructions: lane l of instruction g writes dst voxels [512g + 8l, +8), i.e. every
+    // wave-instruction stores one contiguous 8*BPV*64-byte block (1 KiB for UInt16); those
+    // 8 voxels come from 8/K consecutive source voxels, loaded with one coalesced
+    // nontemporal load per lane.  Up to 4 instructions' loads are issued before any store.
+    // The same registers are stored to every destination row of the task's rectangle.
+    // Measured (kbench, 512^3 -> 1024^3 UInt16, identity codes): 0.35 ms = 6.9 TB/s of
+    // algorithmic bytes, against 0.93 ms for the earlier 8-source-voxels-per-lane layout,
+    // whose half-strided store instructions the memory system merged poorly.
     template <int BPV, int K, bool CONV, int FS, int FD>
     __global__ __launch_bounds__(kBlock) void resampleRepKernel(ResampleArgs a)
     {
+        constexpr int kSrcPerLane = 8 / K;
         int const lane = threadIdx.x & 63;
         uint32_t const wavesPerBlock = blockDim.x >> 6;
-        uint32_t const wave = xcdSwizzle(blockIdx.x, gridDim.x) * wavesPerBlock + (threadIdx.x >> 6);
+        uint32_t const wave = blockIdx.x * wavesPerBlock + (threadIdx.x >> 6);
         uint32_t const totalWaves = gridDim.x * wavesPerBlock;
         uint32_t const tasks = static_cast<uint32_t>(a.nRunsY) * static_cast<uint32_t>(a.nRunsZ);
-        int32_t const chunks = a.sdx >> 3;   // 8 source voxels per lane-chunk
+        int32_t const instrPerRow = (a.ddx + 511) / 512;
 
         for (uint32_t t = wave; t < tasks; t += totalWaves)
         {
             Run const ry = a.runsY[t % static_cast<uint32_t>(a.nRunsY)];
             Run const rz = a.runsZ[t / static_cast<uint32_t>(a.nRunsY)];
             uint64_t const srow = srcRowIndex(a, ry.s, rz.s);
-            for (int32_t c = lane; c < chunks; c += 64)
+            for (int32_t g0 = 0; g0 < instrPerRow; g0 += 4)
             {
-                uint32_t code[8];
-                load8<BPV>(a.src, srow + (static_cast<uint64_t>(c) << 3), code);
-                if constexpr (CONV)
+                uint32_t code[4][8];
+                bool active[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
                 {
+                    int32_t const dx = 512 * (g0 + u) + 8 * lane;
+                    active[u] = g0 + u < instrPerRow && dx < a.ddx;
+                    if (active[u])
+                    {
+                        uint32_t sc[kSrcPerLane];
+                        loadN<BPV, kSrcPerLane, true>(a.src, srow + static_cast<uint64_t>(dx / K), sc);
+                        if constexpr (CONV)
+                        {
 #pragma unroll
-                    for (int v = 0; v < 8; ++v)
-                        code[v] = convertCode<FS, FD>(code[v], a);
+                            for (int i = 0; i < kSrcPerLane; ++i)
+                                sc[i] = convertCode<FS, FD>(sc[i], a);
+                        }
+#pragma unroll
+                        for (int i = 0; i < 8; ++i)
+                            code[u][i] = sc[i / K];
+                    }
                 }
-                // dst voxels [8K*c, 8K*c + 8K): group g holds dst voxels 8g..8g+7 of the chunk
-                uint32_t grp[K][8];
-#pragma unroll
-                for (int g = 0; g < K; ++g)
-#pragma unroll
-                    for (int i = 0; i < 8; ++i)
-                        grp[g][i] = code[(8 * g + i) / K];
-                uint64_t const dx0 = static_cast<uint64_t>(c) * 8u * K;
                 for (int32_t zd = rz.d0; zd < rz.d1; ++zd)
                     for (int32_t yd = ry.d0; yd < ry.d1; ++yd)
                     {
-                        uint64_t drow = dstRowIndex(a, yd, zd) + dx0;
+                        uint64_t const drow = dstRowIndex(a, yd, zd) + 8u * lane;
 #pragma unroll
-                        for (int g = 0; g < K; ++g)
-                            store8<BPV, true>(a.dst, drow + 8u * g, grp[g]);
+                        for (int u = 0; u < 4; ++u)
+                            if (active[u])
+                                store8<BPV, true>(a.dst, drow + 512u * (g0 + u), code[u]);
                     }
             }
         }
@@ -471,10 +485,13 @@ namespace hipk
         uint32_t const bs = codec::bytesPerVoxel(src.dataFormat), bd = codec::bytesPerVoxel(dst.dataFormat);
         bool const aligned = reinterpret_cast<uintptr_t>(src.data) % 16 == 0 &&
                              reinterpret_cast<uintptr_t>(dst.data) % 16 == 0 && src.dimX % 8 == 0;
-        if (t.k >= 1 && t.k <= 4 && t.k != 3 && aligned && bs == bd)
+        if (t.k >= 1 && t.k <= 4 && t.k != 3 && aligned && bs == bd && dst.dimX % 8 == 0)
         {
+            // one task per wave: measured fastest (no task loop latency chain)
+            uint64_t repBlocks = (tasks + 3) / 4;
+            unsigned repGrid = static_cast<unsigned>(repBlocks < (1u << 30) ? repBlocks : (1u << 30));
 #define VKT_REP_LAUNCH(BPV, K, CONV, FS, FD)                                                               \
-    hipLaunchKernelGGL((resampleRepKernel<BPV, K, CONV, FS, FD>), dim3(grid), dim3(kBlock), 0, s, a)
+    hipLaunchKernelGGL((resampleRepKernel<BPV, K, CONV, FS, FD>), dim3(repGrid), dim3(kBlock), 0, s, a)
 #define VKT_REP_BY_K(BPV, CONV, FS, FD)                                                                    \
     do {                                                                                                   \
         if (t.k == 1) VKT_REP_LAUNCH(BPV, 1, CONV, FS, FD);                                                \
