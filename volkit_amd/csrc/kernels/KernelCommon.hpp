@@ -72,10 +72,13 @@ namespace hipk
 
     // ---- 8 consecutive codes per lane ------------------------------------------------
     // BPV 1: one 8-byte load; BPV 2: one 16-byte load; BPV 4: two 16-byte loads.
+    // Nontemporal only for 16-byte vectors: narrower nt/sc1 loads run at 0.54-0.70x the
+    // 16-byte rate on gfx950 (MI355X_MICROARCH.md, inter-workgroup visibility table), and a
+    // resample source read with 8-byte nt loads measured 0.44 ms vs 0.35 ms with plain loads.
     template <class V, bool NT>
     __device__ __forceinline__ V loadVec(void const* p)
     {
-        if constexpr (NT)
+        if constexpr (NT && sizeof(V) >= 16)
             return __builtin_nontemporal_load(reinterpret_cast<V const*>(p));
         else
             return *reinterpret_cast<V const*>(p);

@@ -78,6 +78,79 @@ namespace hipk
     // stores: every byte is touched once.
     constexpr int kUnroll = 4;
 
+    template <int NS, int BPV, bool FLAT, class F>
+    __device__ __forceinline__ void pointwiseVecItem(Operand const& d, Operand const& s1, Operand const& s2,
+                                                     uint64_t it, uint64_t cpr, uint64_t ny, uint64_t& o1,
+                                                     uint64_t& o2, uint64_t& od)
+    {
+        if constexpr (FLAT)
+        {
+            uint64_t x = it << 3;
+            o1 = s1.base + x;
+            o2 = s2.base + x;
+            od = d.base + x;
+        }
+        else
+        {
+            uint64_t r = it / cpr;
+            uint64_t x = (it - r * cpr) << 3;
+            uint64_t j = r % ny, k = r / ny;
+            o1 = s1.base + k * s1.sz + j * s1.sy + x;
+            o2 = s2.base + k * s2.sz + j * s2.sy + x;
+            od = d.base + k * d.sz + j * d.sy + x;
+        }
+    }
+
+    // One workgroup's span [beg, end) of 8-voxel items.  The main loop is branch-free so that
+    // the compiler keeps all kUnroll x NS loads in flight (a guard per item made hipcc wait
+    // vmcnt(0) after every item); the remainder loop handles the last partial quantum.
+    template <int NS, int BPV, bool FLAT, class F>
+    __device__ __forceinline__ void pointwiseVecSpan(Operand const& d, Operand const& s1, Operand const& s2,
+                                                     uint64_t beg, uint64_t end, uint64_t cpr, uint64_t ny, F const& f)
+    {
+        constexpr uint64_t kQ = static_cast<uint64_t>(kBlock) * kUnroll;
+        uint64_t it = beg + threadIdx.x;
+        for (; it + (kUnroll - 1) * static_cast<uint64_t>(kBlock) < end; it += kQ)
+        {
+            uint32_t a[kUnroll][8], b[kUnroll][8];
+            uint64_t od[kUnroll];
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u)
+            {
+                uint64_t o1, o2;
+                pointwiseVecItem<NS, BPV, FLAT, F>(d, s1, s2, it + static_cast<uint64_t>(u) * kBlock, cpr, ny, o1,
+                                                   o2, od[u]);
+                if constexpr (NS >= 1)
+                    load8<BPV, true>(s1.data, o1, a[u]);
+                if constexpr (NS >= 2)
+                    load8<BPV, true>(s2.data, o2, b[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u)
+            {
+                uint32_t o[8];
+#pragma unroll
+                for (int v = 0; v < 8; ++v)
+                    o[v] = f(NS >= 1 ? a[u][v] : 0u, NS >= 2 ? b[u][v] : 0u);
+                store8<BPV, true>(d.data, od[u], o);
+            }
+        }
+        for (; it < end; it += kBlock)
+        {
+            uint32_t a[8], b[8], o[8];
+            uint64_t o1, o2, od;
+            pointwiseVecItem<NS, BPV, FLAT, F>(d, s1, s2, it, cpr, ny, o1, o2, od);
+            if constexpr (NS >= 1)
+                load8<BPV, true>(s1.data, o1, a);
+            if constexpr (NS >= 2)
+                load8<BPV, true>(s2.data, o2, b);
+#pragma unroll
+            for (int v = 0; v < 8; ++v)
+                o[v] = f(NS >= 1 ? a[v] : 0u, NS >= 2 ? b[v] : 0u);
+            store8<BPV, true>(d.data, od, o);
+        }
+    }
+
     template <int NS, int BPV, class F>
     __global__ __launch_bounds__(kBlock) void pointwiseVecKernel(Operand d, Operand s1, Operand s2, Geom g, F f)
     {
@@ -90,52 +163,12 @@ namespace hipk
         per = (per + kSpanQuantum - 1) / kSpanQuantum * kSpanQuantum;
         uint64_t const beg = blockIdx.x * per;
         uint64_t const end = beg + per < items ? beg + per : items;
-
-        auto offsets = [&](uint64_t it, uint64_t& o1, uint64_t& o2, uint64_t& od) {
-            uint64_t r = 0, c = it;
-            if (rows > 1)
-            {
-                r = it / cpr;
-                c = it - r * cpr;
-            }
-            uint64_t j = r % ny, k = r / ny;
-            uint64_t x = c << 3;
-            o1 = s1.base + k * s1.sz + j * s1.sy + x;
-            o2 = s2.base + k * s2.sz + j * s2.sy + x;
-            od = d.base + k * d.sz + j * d.sy + x;
-        };
-
-        for (uint64_t it = beg + threadIdx.x; it < end; it += kSpanQuantum)
+        if (beg < end)
         {
-            uint32_t a[kUnroll][8], b[kUnroll][8];
-            uint64_t od[kUnroll];
-#pragma unroll
-            for (int u = 0; u < kUnroll; ++u)
-            {
-                uint64_t i = it + static_cast<uint64_t>(u) * kBlock;
-                if (i < end)
-                {
-                    uint64_t o1, o2;
-                    offsets(i, o1, o2, od[u]);
-                    if constexpr (NS >= 1)
-                        load8<BPV, true>(s1.data, o1, a[u]);
-                    if constexpr (NS >= 2)
-                        load8<BPV, true>(s2.data, o2, b[u]);
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < kUnroll; ++u)
-            {
-                uint64_t i = it + static_cast<uint64_t>(u) * kBlock;
-                if (i < end)
-                {
-                    uint32_t o[8];
-#pragma unroll
-                    for (int v = 0; v < 8; ++v)
-                        o[v] = f(NS >= 1 ? a[u][v] : 0u, NS >= 2 ? b[u][v] : 0u);
-                    store8<BPV, true>(d.data, od[u], o);
-                }
-            }
+            if (rows == 1)
+                pointwiseVecSpan<NS, BPV, true>(d, s1, s2, beg, end, cpr, ny, f);
+            else
+                pointwiseVecSpan<NS, BPV, false>(d, s1, s2, beg, end, cpr, ny, f);
         }
 
         // scalar tail of every row: voxels [vnx8, vnx)

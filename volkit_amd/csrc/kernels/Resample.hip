@@ -69,6 +69,11 @@ namespace hipk
         int32_t nRunsY, nRunsZ;
         Run const* runsY;          // device
         Run const* runsZ;          // device (s in GLOBAL source planes, d in GLOBAL dst planes)
+        // Affine run generators (exact integer ratios, verified against the tables on the
+        // host): run i = {s0 + sa*i, d0 + da*i, d0 + da*i + dl}; avoids a dependent table load
+        // at the start of every task.
+        int32_t affY, saY, daY, dlY, s0Y, d0Y;
+        int32_t affZ, saZ, daZ, dlZ, s0Z, d0Z;
         int32_t const* xtab;       // device, ddx entries (gather/chain paths)
         int32_t k;                 // integer x ratio (replication path)
         int32_t fs, fd;
@@ -77,6 +82,26 @@ namespace hipk
         uint64_t srcVoxels;        // voxels in the local source buffer (flat-read clamp)
         int32_t srcIsGlobalEnd;    // local buffer ends at the global end (clamp there)
     };
+
+    __device__ __forceinline__ Run runY(ResampleArgs const& a, uint32_t i)
+    {
+        if (a.affY)
+        {
+            int32_t d0 = a.d0Y + a.daY * static_cast<int32_t>(i);
+            return Run{a.s0Y + a.saY * static_cast<int32_t>(i), d0, d0 + a.dlY};
+        }
+        return a.runsY[i];
+    }
+
+    __device__ __forceinline__ Run runZ(ResampleArgs const& a, uint32_t i)
+    {
+        if (a.affZ)
+        {
+            int32_t d0 = a.d0Z + a.daZ * static_cast<int32_t>(i);
+            return Run{a.s0Z + a.saZ * static_cast<int32_t>(i), d0, d0 + a.dlZ};
+        }
+        return a.runsZ[i];
+    }
 
     template <int FS, int FD>
     __device__ __forceinline__ uint32_t convertCode(uint32_t c, ResampleArgs const& a)
@@ -108,52 +133,54 @@ namespace hipk
     // Measured (kbench, 512^3 -> 1024^3 UInt16, identity codes): 0.35 ms = 6.9 TB/s of
     // algorithmic bytes, against 0.93 ms for the earlier 8-source-voxels-per-lane layout,
     // whose half-strided store instructions the memory system merged poorly.
-    template <int BPV, int K, bool CONV, int FS, int FD>
+    template <int BPV, int K, bool CONV, int FS, int FD, int NSLOT>
     __global__ __launch_bounds__(kBlock) void resampleRepKernel(ResampleArgs a)
     {
         constexpr int kSrcPerLane = 8 / K;
         int const lane = threadIdx.x & 63;
         uint32_t const wavesPerBlock = blockDim.x >> 6;
-        uint32_t const wave = blockIdx.x * wavesPerBlock + (threadIdx.x >> 6);
+        // wave-uniform task index in SGPRs (scalar loads of the run tables)
+        uint32_t const wave = __builtin_amdgcn_readfirstlane(xcdSwizzle(blockIdx.x, gridDim.x) * wavesPerBlock +
+                                                             (threadIdx.x >> 6));
         uint32_t const totalWaves = gridDim.x * wavesPerBlock;
         uint32_t const tasks = static_cast<uint32_t>(a.nRunsY) * static_cast<uint32_t>(a.nRunsZ);
         int32_t const instrPerRow = (a.ddx + 511) / 512;
 
         for (uint32_t t = wave; t < tasks; t += totalWaves)
         {
-            Run const ry = a.runsY[t % static_cast<uint32_t>(a.nRunsY)];
-            Run const rz = a.runsZ[t / static_cast<uint32_t>(a.nRunsY)];
+            Run const ry = runY(a, t % static_cast<uint32_t>(a.nRunsY));
+            Run const rz = runZ(a, t / static_cast<uint32_t>(a.nRunsY));
             uint64_t const srow = srcRowIndex(a, ry.s, rz.s);
-            for (int32_t g0 = 0; g0 < instrPerRow; g0 += 4)
+            for (int32_t g0 = 0; g0 < instrPerRow; g0 += NSLOT)
             {
-                uint32_t code[4][8];
-                bool active[4];
+                uint32_t code[NSLOT][8];
+                bool active[NSLOT];
+                // loads are unconditional (clamped into the row) so all stay in flight;
+                // only the stores are predicated
 #pragma unroll
-                for (int u = 0; u < 4; ++u)
+                for (int u = 0; u < NSLOT; ++u)
                 {
-                    int32_t const dx = 512 * (g0 + u) + 8 * lane;
+                    int32_t dx = 512 * (g0 + u) + 8 * lane;
                     active[u] = g0 + u < instrPerRow && dx < a.ddx;
-                    if (active[u])
+                    dx = dx < a.ddx ? dx : a.ddx - 8;
+                    uint32_t sc[kSrcPerLane];
+                    loadN<BPV, kSrcPerLane, true>(a.src, srow + static_cast<uint64_t>(dx / K), sc);
+                    if constexpr (CONV)
                     {
-                        uint32_t sc[kSrcPerLane];
-                        loadN<BPV, kSrcPerLane, true>(a.src, srow + static_cast<uint64_t>(dx / K), sc);
-                        if constexpr (CONV)
-                        {
 #pragma unroll
-                            for (int i = 0; i < kSrcPerLane; ++i)
-                                sc[i] = convertCode<FS, FD>(sc[i], a);
-                        }
-#pragma unroll
-                        for (int i = 0; i < 8; ++i)
-                            code[u][i] = sc[i / K];
+                        for (int i = 0; i < kSrcPerLane; ++i)
+                            sc[i] = convertCode<FS, FD>(sc[i], a);
                     }
+#pragma unroll
+                    for (int i = 0; i < 8; ++i)
+                        code[u][i] = sc[i / K];
                 }
                 for (int32_t zd = rz.d0; zd < rz.d1; ++zd)
                     for (int32_t yd = ry.d0; yd < ry.d1; ++yd)
                     {
                         uint64_t const drow = dstRowIndex(a, yd, zd) + 8u * lane;
 #pragma unroll
-                        for (int u = 0; u < 4; ++u)
+                        for (int u = 0; u < NSLOT; ++u)
                             if (active[u])
                                 store8<BPV, true>(a.dst, drow + 512u * (g0 + u), code[u]);
                     }
@@ -175,8 +202,8 @@ namespace hipk
 
         for (uint32_t t = wave; t < tasks; t += totalWaves)
         {
-            Run const ry = a.runsY[t % static_cast<uint32_t>(a.nRunsY)];
-            Run const rz = a.runsZ[t / static_cast<uint32_t>(a.nRunsY)];
+            Run const ry = runY(a, t % static_cast<uint32_t>(a.nRunsY));
+            Run const rz = runZ(a, t / static_cast<uint32_t>(a.nRunsY));
             uint64_t const srow = srcRowIndex(a, ry.s, rz.s);
             for (int32_t x = lane; x < a.ddx; x += 64)
             {
@@ -212,8 +239,8 @@ namespace hipk
 
         for (uint32_t t = wave; t < tasks; t += totalWaves)
         {
-            Run const ry = a.runsY[t % static_cast<uint32_t>(a.nRunsY)];
-            Run const rz = a.runsZ[t / static_cast<uint32_t>(a.nRunsY)];
+            Run const ry = runY(a, t % static_cast<uint32_t>(a.nRunsY));
+            Run const rz = runZ(a, t / static_cast<uint32_t>(a.nRunsY));
             int32_t const hy = ry.s + 1 < a.sdy ? ry.s + 1 : a.sdy - 1;
             int32_t const hz = rz.s + 1 < a.srcGlobalDz ? rz.s + 1 : a.srcGlobalDz - 1;
             uint64_t const r00 = srcRowIndex(a, ry.s, rz.s), r10 = srcRowIndex(a, hy, rz.s);
@@ -276,7 +303,31 @@ namespace hipk
         Run const* runsY = nullptr;
         Run const* runsZ = nullptr;
         int32_t const* xtab = nullptr;
+        int32_t aff[2][6] = {{0, 0, 0, 0, 0, 0}, {0, 0, 0, 0, 0, 0}};   // {aff, sa, da, dl, s0, d0}
     };
+
+    // Do the runs follow {s0 + sa*i, d0 + da*i, +dl}?  (exact integer up/down-sampling)
+    void affineOf(std::vector<Run> const& runs, int32_t (&out)[6])
+    {
+        out[0] = 0;
+        if (runs.empty())
+            return;
+        int32_t s0 = runs[0].s, d0 = runs[0].d0, dl = runs[0].d1 - runs[0].d0;
+        int32_t sa = runs.size() > 1 ? runs[1].s - runs[0].s : 1;
+        int32_t da = runs.size() > 1 ? runs[1].d0 - runs[0].d0 : dl;
+        for (size_t i = 0; i < runs.size(); ++i)
+        {
+            int32_t ii = static_cast<int32_t>(i);
+            if (runs[i].s != s0 + sa * ii || runs[i].d0 != d0 + da * ii || runs[i].d1 != d0 + da * ii + dl)
+                return;
+        }
+        out[0] = 1;
+        out[1] = sa;
+        out[2] = da;
+        out[3] = dl;
+        out[4] = s0;
+        out[5] = d0;
+    }
 
     vktError getTables(int32_t ddx, int32_t ddy, int32_t dgz, int32_t dz0, int32_t dnz, int32_t sdx, int32_t sdy,
                        int32_t sgz, Tables& out)
@@ -316,6 +367,8 @@ namespace hipk
         t.nRunsY = static_cast<int32_t>(ry.size());
         t.nRunsZ = static_cast<int32_t>(rz.size());
         t.k = rep ? k : 0;
+        affineOf(ry, t.aff[0]);
+        affineOf(rz, t.aff[1]);
         t.minSz = rz.empty() ? 0 : rz.front().s;
         t.maxSz = rz.empty() ? -1 : rz.back().s;
         size_t words = 3 * ry.size() + 3 * rz.size() + xt.size();
@@ -462,6 +515,10 @@ namespace hipk
         a.runsY = t.runsY;
         a.runsZ = t.runsZ;
         a.xtab = t.xtab;
+        a.affY = t.aff[0][0]; a.saY = t.aff[0][1]; a.daY = t.aff[0][2]; a.dlY = t.aff[0][3];
+        a.s0Y = t.aff[0][4]; a.d0Y = t.aff[0][5];
+        a.affZ = t.aff[1][0]; a.saZ = t.aff[1][1]; a.daZ = t.aff[1][2]; a.dlZ = t.aff[1][3];
+        a.s0Z = t.aff[1][4]; a.d0Z = t.aff[1][5];
         a.k = t.k;
         a.fs = src.dataFormat;
         a.fd = dst.dataFormat;
@@ -490,8 +547,16 @@ namespace hipk
             // one task per wave: measured fastest (no task loop latency chain)
             uint64_t repBlocks = (tasks + 3) / 4;
             unsigned repGrid = static_cast<unsigned>(repBlocks < (1u << 30) ? repBlocks : (1u << 30));
+            int32_t const instrPerRow = (dst.dimX + 511) / 512;
 #define VKT_REP_LAUNCH(BPV, K, CONV, FS, FD)                                                               \
-    hipLaunchKernelGGL((resampleRepKernel<BPV, K, CONV, FS, FD>), dim3(repGrid), dim3(kBlock), 0, s, a)
+    do {                                                                                                   \
+        if (instrPerRow == 1)                                                                              \
+            hipLaunchKernelGGL((resampleRepKernel<BPV, K, CONV, FS, FD, 1>), dim3(repGrid), dim3(kBlock), 0, s, a); \
+        else if (instrPerRow == 2)                                                                         \
+            hipLaunchKernelGGL((resampleRepKernel<BPV, K, CONV, FS, FD, 2>), dim3(repGrid), dim3(kBlock), 0, s, a); \
+        else                                                                                               \
+            hipLaunchKernelGGL((resampleRepKernel<BPV, K, CONV, FS, FD, 4>), dim3(repGrid), dim3(kBlock), 0, s, a); \
+    } while (0)
 #define VKT_REP_BY_K(BPV, CONV, FS, FD)                                                                    \
     do {                                                                                                   \
         if (t.k == 1) VKT_REP_LAUNCH(BPV, 1, CONV, FS, FD);                                                \
