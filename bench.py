@@ -75,8 +75,12 @@ def main():
 
     if lib.vktHipSetDevice(local) != 0:
         raise RuntimeError(vkt.last_error())
-    # one stream for our kernels and torch's (events, RCCL) -> no cross-stream hazards
-    lib.vktHipSetComputeStream(C.c_void_p(torch.cuda.current_stream().cuda_stream))
+    # One dedicated (non-NULL) stream for our kernels and for torch's events / RCCL calls:
+    # torch's default stream is the legacy NULL stream, which would serialise against the
+    # backend's blocking stream at every event record.
+    stream = torch.cuda.Stream()
+    lib.vktHipSetComputeStream(C.c_void_p(stream.cuda_stream))
+    torch.cuda.set_stream(stream)
 
     ep = vkt.GetThreadExecutionPolicy()
     ep.device = vkt.ExecutionPolicy.Device_GPU
