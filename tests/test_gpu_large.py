@@ -1,0 +1,189 @@
+"""GPU tests at BASELINE.json sizes and for the Z-slab path, through the backend C ABI
+(include/volkit_hip.h) on device-resident volumes.
+
+* full-size parity where the oracle finishes in seconds (512^3 UInt16 arithmetic, config 2);
+* size-independent properties at the metric sizes: 2x Resample of integer (and finite,
+  non-negative float) data is exact replication; Sum with a zero volume is the identity for
+  every UInt16 code; Fill writes one code everywhere; Copy reproduces its source;
+* Z-slab resample: P slabs of a global volume, each resampled from its local planes (owned +
+  exchanged halo, per volkit_amd.slab's plan), equal the whole-volume oracle resample.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from oracle import binding as ob
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def hip():
+    import torch
+    assert torch.cuda.is_available()
+    from volkit_amd import _lib
+    return _lib
+
+
+class DevVol:
+    """A device allocation + backend view."""
+
+    def __init__(self, L, dims, fmt, lo=0.0, hi=1.0):
+        self.L = L
+        self.dims, self.fmt = tuple(dims), fmt
+        x, y, z = dims
+        self.nbytes = x * y * z * ob.BPV[fmt]
+        p = C.c_void_p()
+        assert L.lib.vktHipAllocate(C.byref(p), self.nbytes) == 0, L.last_error()
+        self.ptr = p.value
+        self.view = L.HipVolumeView_t(self.ptr, x, y, z, fmt, lo, hi)
+
+    def upload(self, codes):
+        a = np.ascontiguousarray(codes)
+        assert a.nbytes == self.nbytes
+        assert self.L.lib.vktHipMemcpy(self.ptr, a.ctypes.data, a.nbytes, 1) == 0
+
+    def download(self):
+        x, y, z = self.dims
+        out = np.empty((z, y, x), dtype=ob.CODE_DTYPE[self.fmt])
+        assert self.L.lib.vktHipMemcpy(out.ctypes.data, self.ptr, self.nbytes, 2) == 0
+        return out
+
+    def synth(self, seed):
+        assert self.L.lib.vktHipSynthesize(self.view, C.c_uint64(seed)) == 0
+
+    def free(self):
+        if self.ptr:
+            self.L.lib.vktHipFree(C.c_void_p(self.ptr))
+            self.ptr = None
+
+
+def v3(x, y, z, L):
+    return L.Vec3i_t(x, y, z)
+
+
+def test_config2_arith_512_full_parity(hip):
+    """512^3 UInt16 SafeSum / SafeDiff / SumRange (BASELINE config 2), bit-exact vs oracle."""
+    n = 512
+    A, B, D = (DevVol(hip, (n, n, n), 5) for _ in range(3))
+    A.synth(0x5EED)
+    B.synth(0x5EED + 1)
+    a, b = A.download(), B.download()
+    np.testing.assert_array_equal(a.view(np.uint8).reshape(-1)[:64], ob.synth(64, 0x5EED))   # same generator
+    for op, code in (("SafeSum", 5), ("SafeDiff", 6), ("Sum", 0)):
+        assert hip.lib.vktHipArithmeticRange(code, D.view, A.view, B.view, v3(0, 0, 0, hip), v3(n, n, n, hip),
+                                             v3(0, 0, 0, hip)) == 0
+        got = D.download()
+        ref = ob.Volume.zeros((n, n, n), 5)
+        ob.arith_range(op, ref, ob.Volume(a, 5), ob.Volume(b, 5), (0, 0, 0), (n, n, n))
+        np.testing.assert_array_equal(got, ref.codes, err_msg=op)
+    for v in (A, B, D):
+        v.free()
+
+
+def test_metric_pipeline_1024_properties(hip):
+    """Resample 512^3 -> 1024^3 UInt16 Linear + SumRange 1024^3: the exact index table for
+    this ratio is x//2, and Linear == Nearest for integer data, so R must be the 2x2x2
+    replication of S; SumRange(R, 0) must return R (every code round-trips);
+    SumRange(R, B) is checked plane-sampled against the oracle."""
+    s, e = 512, 1024
+    S = DevVol(hip, (s, s, s), 5)
+    R, B, D = (DevVol(hip, (e, e, e), 5) for _ in range(3))
+    S.synth(7)
+    B.synth(8)
+    assert hip.lib.vktHipResample(R.view, S.view, 1) == 0
+    src = S.download()
+    r = R.download()
+    for dz in (0, 1):
+        for dy in (0, 1):
+            for dx in (0, 1):
+                np.testing.assert_array_equal(r[dz::2, dy::2, dx::2], src)
+    del src
+    Z = DevVol(hip, (e, e, e), 5)
+    assert hip.lib.vktHipFillRange(Z.view, v3(0, 0, 0, hip), v3(e, e, e, hip), C.c_float(0.0)) == 0
+    assert hip.lib.vktHipArithmeticRange(0, D.view, R.view, Z.view, v3(0, 0, 0, hip), v3(e, e, e, hip),
+                                         v3(0, 0, 0, hip)) == 0
+    np.testing.assert_array_equal(D.download(), r)
+    assert hip.lib.vktHipArithmeticRange(0, D.view, R.view, B.view, v3(0, 0, 0, hip), v3(e, e, e, hip),
+                                         v3(0, 0, 0, hip)) == 0
+    d, b = D.download(), B.download()
+    for z in (0, 1, 511, 1023):
+        ref = ob.Volume.zeros((e, e, 1), 5)
+        ob.arith_range("Sum", ref, ob.Volume(r[z:z + 1], 5), ob.Volume(b[z:z + 1], 5), (0, 0, 0), (e, e, 1))
+        np.testing.assert_array_equal(d[z:z + 1], ref.codes, err_msg=f"plane {z}")
+    for v in (S, R, B, D, Z):
+        v.free()
+
+
+def test_float_resample_replication_512_to_1024(hip):
+    """Config-3 kernel at half size: finite non-negative Float32 data -> Linear == Nearest ==
+    replication (bitwise)."""
+    s, e = 512, 1024
+    rng = np.random.default_rng(3)
+    S = DevVol(hip, (s, s, s), 7)
+    R = DevVol(hip, (e, e, e), 7)
+    src = rng.random((s, s, s), dtype=np.float32)
+    S.upload(src.view(np.uint32))
+    assert hip.lib.vktHipResample(R.view, S.view, 1) == 0
+    r = R.download()
+    for dz in (0, 1):
+        for dy in (0, 1):
+            for dx in (0, 1):
+                np.testing.assert_array_equal(r[dz::2, dy::2, dx::2], src.view(np.uint32))
+    S.free()
+    R.free()
+
+
+def test_fill_and_copy_1024(hip):
+    e = 1024
+    V, W = DevVol(hip, (e, e, e), 5), DevVol(hip, (e, e, e), 5)
+    assert hip.lib.vktHipFillRange(V.view, v3(0, 0, 0, hip), v3(e, e, e, hip), C.c_float(0.1)) == 0
+    code = int.from_bytes(ob.map_voxel(0.1, 5), "little")
+    v = V.download()
+    assert (v == code).all()
+    V.synth(99)
+    assert hip.lib.vktHipCopyRange(W.view, V.view, v3(0, 0, 0, hip), v3(e, e, e, hip), v3(0, 0, 0, hip)) == 0
+    np.testing.assert_array_equal(W.download(), V.download())
+    V.free()
+    W.free()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("fmt,fm", [(5, 1), (7, 1), (4, 0)])
+@pytest.mark.parametrize("sdims,ddims", [((64, 48, 40), (128, 96, 80)), ((37, 23, 29), (64, 40, 53)),
+                                         ((32, 32, 64), (16, 16, 21))])
+def test_zslab_resample_matches_whole_volume(hip, world, fmt, fm, sdims, ddims):
+    from volkit_amd import slab
+    rng = np.random.default_rng(world * 100 + fmt)
+    sx, sy, sz = sdims
+    dx, dy, dz = ddims
+    if fmt == 7:
+        g = rng.uniform(-1, 2, (sz, sy, sx)).astype(np.float32)
+        g.reshape(-1)[::131] = np.nan
+        glob = g.view(np.uint32)
+    else:
+        glob = rng.integers(0, 2 ** (8 * ob.BPV[fmt]), (sz, sy, sx), dtype=np.uint64).astype(ob.CODE_DTYPE[fmt])
+    ref = ob.Volume.zeros(ddims, fmt)
+    ob.resample(ref, ob.Volume(glob, fmt), fm)
+    chain = fm == 1 and fmt == 7
+    for rank in range(world):
+        plan = slab.plan_resample(dz, sz, world, rank, fm, chain)
+        d0, d1 = plan.dst
+        if d1 <= d0:
+            continue
+        l0, l1 = plan.local_src
+        Sl = DevVol(hip, (sx, sy, l1 - l0), fmt)
+        Sl.upload(glob[l0:l1])          # owned planes + the halo the exchange would deliver
+        Dl = DevVol(hip, (dx, dy, d1 - d0), fmt)
+        assert slab.resample_slab(Dl.view, Sl.view, fm, plan) == 0, hip.last_error()
+        got = Dl.download()
+        exp = ref.codes[d0:d1]
+        if fmt == 7:
+            fg, fe = got.view(np.float32), exp.view(np.float32)
+            np.testing.assert_array_equal(np.isnan(fg), np.isnan(fe))
+            np.testing.assert_array_equal(got[~np.isnan(fe)], exp[~np.isnan(fe)])
+        else:
+            np.testing.assert_array_equal(got, exp)
+        Sl.free()
+        Dl.free()
