@@ -262,3 +262,34 @@ def test_copy_constructor_on_gpu(g):
     w = vkt.StructuredVolume.CreateCopy(v)
     g._cpu()
     np.testing.assert_array_equal(w.to_numpy(), np.arange(64, dtype=np.uint8).reshape(4, 4, 4))
+
+
+# ---- paths added for performance: common-phase heads, vector gather, row chain ---------
+@pytest.mark.parametrize("fmt", [4, 5, 7])
+def test_arithmetic_subbox_phases(g, o, fmt):
+    """Sub-boxes whose rows start off an 8-voxel boundary: same phase in every operand
+    (vector middle + scalar head/tail) and different phases (scalar path)."""
+    rng = np.random.default_rng(fmt + 40)
+    a = rand_codes(rng, fmt, (40, 50, 96))
+    b = rand_codes(rng, fmt, (40, 50, 96))
+    d = rand_codes(rng, fmt, (40, 50, 96))
+    for first, last, off in (((5, 3, 2), (91, 47, 39), (0, 0, 0)), ((1, 0, 0), (96, 50, 40), (0, 0, 0)),
+                             ((13, 7, 3), (80, 40, 30), (3, 2, 1)), ((8, 1, 1), (16, 49, 39), (0, 0, 0)),
+                             ((7, 0, 0), (9, 50, 40), (0, 0, 0))):
+        for op in ("SafeSum", "Diff"):
+            out = g.arith(op, [fmt] * 3, [(0.0, 1.0)] * 3, a, b, d.copy(), first, last, off)
+            ref = o.arith(op, [fmt] * 3, [(0.0, 1.0)] * 3, a, b, d.copy(), first, last, off)
+            assert_codes_equal(out, ref, fmt, f"{op} fmt={fmt} {first}->{last}+{off}")
+
+
+@pytest.mark.parametrize("sfmt,dfmt", [(5, 5), (4, 4), (7, 7), (7, 5), (5, 7)])
+def test_resample_vector_gather_and_row_chain(g, o, sfmt, dfmt):
+    rng = np.random.default_rng(sfmt * 10 + dfmt)
+    for sd, dd in (((96, 20, 12), (64, 24, 16)), ((40, 24, 10), (128, 16, 20)), ((64, 32, 8), (256, 64, 16)),
+                   ((256, 8, 4), (512, 16, 8)), ((100, 10, 5), (400, 20, 10))):
+        src = rand_codes(rng, sfmt, sd[::-1])
+        for smap, dmap in (((0.0, 1.0), (0.0, 1.0)), ((0.0, 1.0), (-1.0, 3.0))):
+            for fm in (0, 1):
+                out = g.resample(dfmt, dmap, dd, sfmt, smap, src, fm)
+                ref = o.resample(dfmt, dmap, dd, sfmt, smap, src, fm)
+                assert_codes_equal(out, ref, dfmt, f"resample {sd}->{dd} {sfmt}->{dfmt} fm={fm} {smap}->{dmap}")

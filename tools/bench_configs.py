@@ -1,0 +1,130 @@
+"""Secondary BASELINE.json configs on one GPU (development/reporting tool; bench.py is the
+driver's contract).  Prints one JSON line per case with kernel time (HIP events on the
+backend's compute stream, median of N) and algorithmic GB/s.
+
+  python tools/bench_configs.py [--reps 10] [--big]
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+from volkit_amd import _lib  # noqa: E402
+from volkit_amd._lib import lib, HipVolumeView_t, Vec3i_t  # noqa: E402
+
+BPV = {4: 1, 5: 2, 7: 4, 2: 2, 6: 4}
+
+
+def alloc(dims, fmt, lo=0.0, hi=1.0, seed=None):
+    x, y, z = dims
+    p = C.c_void_p()
+    n = x * y * z * BPV[fmt]
+    if lib.vktHipAllocate(C.byref(p), n) != 0:
+        raise RuntimeError(_lib.last_error())
+    v = HipVolumeView_t(p.value, x, y, z, fmt, lo, hi)
+    if seed is not None:
+        lib.vktHipSynthesize(v, C.c_uint64(seed))
+    return v
+
+
+def free(*vs):
+    for v in vs:
+        lib.vktHipFree(C.c_void_p(v.data))
+
+
+def timed(fn, reps):
+    s = torch.cuda.current_stream()
+    fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        if fn() != 0:
+            raise RuntimeError(_lib.last_error())
+        b.record()
+        b.synchronize()
+        ts.append(a.elapsed_time(b))
+    ts.sort()
+    del s
+    return ts[len(ts) // 2]
+
+
+def report(name, ms, nbytes, voxels):
+    print(json.dumps({"case": name, "ms": round(ms, 4), "GB/s": round(nbytes / ms / 1e6, 1),
+                      "frac_of_8TBs": round(nbytes / ms / 1e6 / 8000, 4),
+                      "Gvox/s": round(voxels / ms / 1e6, 2)}), flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--big", action="store_true", help="include 2048^3 cases (~50 GB of HBM)")
+    args = ap.parse_args()
+    torch.cuda.set_device(0)
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    lib.vktHipSetComputeStream(C.c_void_p(stream.cuda_stream))
+    o = Vec3i_t(0, 0, 0)
+    R = args.reps
+
+    # config 2: 512^3 UInt16 SafeSum / SafeDiff / SumRange
+    n = 512
+    A, B, D = alloc((n,) * 3, 5, seed=1), alloc((n,) * 3, 5, seed=2), alloc((n,) * 3, 5)
+    last = Vec3i_t(n, n, n)
+    for name, op in (("SafeSum", 5), ("SafeDiff", 6), ("SumRange", 0)):
+        ms = timed(lambda: lib.vktHipArithmeticRange(op, D, A, B, o, last, o), R)
+        report(f"config2 {name} 512^3 UInt16", ms, 6 * n ** 3, n ** 3)
+    free(A, B, D)
+
+    # config 3: 1024^3 Float32 -> 2048^3 Linear (lerp-chain kernel) and Nearest (replication)
+    s, e = 1024, 2048
+    S = alloc((s,) * 3, 7, seed=3)
+    Rv = alloc((e,) * 3, 7)
+    for fm, lab in ((1, "Linear"), (0, "Nearest")):
+        ms = timed(lambda: lib.vktHipResample(Rv, S, fm), max(3, R // 3))
+        report(f"config3 Resample 1024^3->2048^3 Float32 {lab}", ms, 4 * s ** 3 + 4 * e ** 3, e ** 3)
+    free(S, Rv)
+
+    # metric kernels at 1024^3 and some extra ops
+    s, e = 512, 1024
+    S, Rv, B, D = alloc((s,) * 3, 5, seed=4), alloc((e,) * 3, 5), alloc((e,) * 3, 5, seed=5), alloc((e,) * 3, 5)
+    lastE = Vec3i_t(e, e, e)
+    report("metric Resample 512^3->1024^3 UInt16 Linear",
+           timed(lambda: lib.vktHipResample(Rv, S, 1), R), 2 * s ** 3 + 2 * e ** 3, e ** 3)
+    report("metric SumRange 1024^3 UInt16", timed(lambda: lib.vktHipArithmeticRange(0, D, Rv, B, o, lastE, o), R),
+           6 * e ** 3, e ** 3)
+    report("FillRange 1024^3 UInt16", timed(lambda: lib.vktHipFillRange(D, o, lastE, C.c_float(0.3)), R), 2 * e ** 3,
+           e ** 3)
+    report("Copy 1024^3 UInt16", timed(lambda: lib.vktHipCopyRange(D, B, o, lastE, o), R), 4 * e ** 3, e ** 3)
+    Dm = HipVolumeView_t(D.data, e, e, e, 5, -1.0, 3.0)
+    report("Copy 1024^3 UInt16 remap [0,1]->[-1,3]", timed(lambda: lib.vktHipCopyRange(Dm, B, o, lastE, o), R),
+           4 * e ** 3, e ** 3)
+    sub0, sub1 = Vec3i_t(100, 100, 100), Vec3i_t(900, 900, 900)
+    report("SafeSumRange 800^3 sub-box of 1024^3", timed(lambda: lib.vktHipArithmeticRange(5, D, Rv, B, sub0, sub1, o),
+                                                          R), 6 * 800 ** 3, 800 ** 3)
+    D1000 = alloc((1000, 1000, 1000), 5)
+    report("Resample 1024^3->1000^3 UInt16 Nearest (gather)", timed(lambda: lib.vktHipResample(D1000, Rv, 0), R),
+           2 * 1000 ** 3 + 2 * e ** 3, 1000 ** 3)
+    free(S, Rv, B, D, D1000)
+
+    if args.big:
+        s, e = 1024, 2048
+        S, Rv, B, D = alloc((s,) * 3, 5, seed=6), alloc((e,) * 3, 5), alloc((e,) * 3, 5, seed=7), alloc((e,) * 3, 5)
+        lastE = Vec3i_t(e, e, e)
+        ms_r = timed(lambda: lib.vktHipResample(Rv, S, 1), 3)
+        ms_s = timed(lambda: lib.vktHipArithmeticRange(0, D, Rv, B, o, lastE, o), 3)
+        report("config4 (1 GPU, strong) Resample 1024^3->2048^3 UInt16", ms_r, 2 * s ** 3 + 2 * e ** 3, e ** 3)
+        report("config4 (1 GPU, strong) SumRange 2048^3 UInt16", ms_s, 6 * e ** 3, e ** 3)
+        report("config4 (1 GPU, strong) pipeline", ms_r + ms_s, 2 * s ** 3 + 8 * e ** 3, e ** 3)
+        free(S, Rv, B, D)
+
+
+if __name__ == "__main__":
+    main()

@@ -31,6 +31,33 @@ namespace hipk
         return static_cast<unsigned>(need < cap ? need : cap);
     }
 
+    // Division by a run-time constant for 32-bit operands: q = (umulhi(n, m) + n) >> l with
+    // l = ceil(log2 d), m = floor(2^32 (2^l - d) / d) + 1 (exact for every 32-bit n).  Replaces
+    // the ~40-instruction 64-bit divide in per-item index decomposition.
+    struct FastDiv
+    {
+        uint32_t d, m, l;
+    };
+
+    inline FastDiv makeFastDiv(uint32_t d)
+    {
+        FastDiv f{d, 0u, 0u};
+        if (d == 0)
+            return f;
+        uint32_t l = 0;
+        while ((1ull << l) < d)
+            ++l;
+        f.l = l;
+        f.m = static_cast<uint32_t>(((1ull << 32) * ((1ull << l) - d)) / d + 1);
+        return f;
+    }
+
+    __device__ __forceinline__ uint32_t fdiv(uint32_t n, FastDiv const& f)
+    {
+        uint64_t hi = __umulhi(n, f.m);
+        return static_cast<uint32_t>((hi + n) >> f.l);
+    }
+
     // ---- scalar code access -----------------------------------------------------------
     template <int BPV>
     __device__ __forceinline__ uint32_t loadCode(uint8_t const* base, uint64_t voxel)
@@ -181,6 +208,33 @@ namespace hipk
             if constexpr (NT) { __builtin_nontemporal_store(a, p); __builtin_nontemporal_store(b, p + 1); }
             else { p[0] = a; p[1] = b; }
         }
+    }
+
+    // 16 bytes of codes per lane (V = 16 / BPV voxels), nontemporal: the store layout of
+    // every streaming writer -- lane l of a wave-instruction writes bytes [16l, 16l + 16) of
+    // one contiguous KiB.
+    template <int BPV>
+    __device__ __forceinline__ void store16(uint8_t* base, uint64_t voxel, uint32_t const* c)
+    {
+        u32x4 v;
+        if constexpr (BPV == 1)
+        {
+            uint32_t w[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                w[i] = c[4 * i] | c[4 * i + 1] << 8 | c[4 * i + 2] << 16 | c[4 * i + 3] << 24;
+            v.x = w[0]; v.y = w[1]; v.z = w[2]; v.w = w[3];
+        }
+        else if constexpr (BPV == 2)
+        {
+            v.x = c[0] | c[1] << 16; v.y = c[2] | c[3] << 16;
+            v.z = c[4] | c[5] << 16; v.w = c[6] | c[7] << 16;
+        }
+        else
+        {
+            v.x = c[0]; v.y = c[1]; v.z = c[2]; v.w = c[3];
+        }
+        __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(base + voxel * BPV));
     }
 
     // XCD-aware block order (guide §5.5 T1): hardware deals workgroups round-robin over the

@@ -133,14 +133,31 @@ namespace hipk
         p.g.vnx = vnx;
         p.g.vny = vny;
         p.g.vnz = vnz;
-        p.g.vnx8 = vnx & ~int64_t(7);
+        // common misalignment phase of the row starts: a scalar head of (8 - phase) % 8 voxels
+        // brings every operand to an 8-voxel boundary at the same x
+        int64_t const phase = ops[0]->base & 7;
+        for (int i = 1; i < nops; ++i)
+            if ((ops[i]->base & 7) != phase)
+                vec = false;
+        int64_t head = (8 - phase) & 7;
+        if (head > vnx)
+            head = vnx;
+        p.g.vhead = head;
+        p.g.vnx8 = head + ((vnx - head) & ~int64_t(7));
+        uint64_t const vecItems = static_cast<uint64_t>((p.g.vnx8 - head) / 8) * static_cast<uint64_t>(vny) * vnz;
+        uint64_t const total = static_cast<uint64_t>(nx) * ny * nz;
+        p.g.fast32 = vecItems < (1ull << 32) && total < (1ull << 32) ? 1 : 0;
+        p.g.divCpr = makeFastDiv(static_cast<uint32_t>((p.g.vnx8 - head) / 8 > 0 ? (p.g.vnx8 - head) / 8 : 1));
+        p.g.divVny = makeFastDiv(static_cast<uint32_t>(vny));
+        p.g.divNx = makeFastDiv(static_cast<uint32_t>(nx));
+        p.g.divNy = makeFastDiv(static_cast<uint32_t>(ny));
 
         // 8-voxel chunks must start aligned in every operand
         uint64_t needAlign = bpv == 1 ? 8u : 16u;
         for (int i = 0; i < nops && vec; ++i)
         {
             Operand const& o = *ops[i];
-            if ((reinterpret_cast<uintptr_t>(o.data) % needAlign) != 0 || (o.base & 7) != 0)
+            if ((reinterpret_cast<uintptr_t>(o.data) % needAlign) != 0)
                 vec = false;
             if (vny > 1 && (o.sy & 7) != 0)
                 vec = false;

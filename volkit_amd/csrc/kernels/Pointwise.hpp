@@ -42,7 +42,11 @@ namespace hipk
     {
         int64_t nx, ny, nz;      // raw extents (scalar path)
         int64_t vnx, vny, vnz;   // collapsed extents (vector path)
-        int64_t vnx8;            // vnx rounded down to a multiple of 8
+        int64_t vnx8;            // end of the 8-aligned middle of each row: vhead + 8 * chunks
+        int64_t vhead;           // scalar head voxels per row (common misalignment phase)
+        int32_t fast32;          // all index arithmetic fits 32 bits -> magic-number division
+        FastDiv divCpr, divVny;  // vector path: items -> (row, chunk), row -> (j, k)
+        FastDiv divNx, divNy;    // scalar path: voxel -> (i, j, k)
     };
 
     // Sentinel for "format known only at run time".
@@ -78,23 +82,39 @@ namespace hipk
     // stores: every byte is touched once.
     constexpr int kUnroll = 4;
 
-    template <int NS, int BPV, bool FLAT, class F>
+    // MODE 0: one collapsed row; 1: rows, 32-bit magic division; 2: rows, 64-bit division.
+    template <int NS, int BPV, int MODE, class F>
     __device__ __forceinline__ void pointwiseVecItem(Operand const& d, Operand const& s1, Operand const& s2,
-                                                     uint64_t it, uint64_t cpr, uint64_t ny, uint64_t& o1,
-                                                     uint64_t& o2, uint64_t& od)
+                                                     Geom const& g, uint64_t it, uint64_t& o1, uint64_t& o2,
+                                                     uint64_t& od)
     {
-        if constexpr (FLAT)
+        if constexpr (MODE == 0)
         {
-            uint64_t x = it << 3;
+            uint64_t x = static_cast<uint64_t>(g.vhead) + (it << 3);
             o1 = s1.base + x;
             o2 = s2.base + x;
             od = d.base + x;
         }
         else
         {
-            uint64_t r = it / cpr;
-            uint64_t x = (it - r * cpr) << 3;
-            uint64_t j = r % ny, k = r / ny;
+            uint64_t j, k, x;
+            if constexpr (MODE == 1)
+            {
+                uint32_t r = fdiv(static_cast<uint32_t>(it), g.divCpr);
+                x = static_cast<uint64_t>(g.vhead) +
+                    (static_cast<uint64_t>(static_cast<uint32_t>(it) - r * g.divCpr.d) << 3);
+                uint32_t kk = fdiv(r, g.divVny);
+                k = kk;
+                j = r - kk * g.divVny.d;
+            }
+            else
+            {
+                uint64_t const cpr = static_cast<uint64_t>(g.vnx8 - g.vhead) >> 3, ny = static_cast<uint64_t>(g.vny);
+                uint64_t r = it / cpr;
+                x = static_cast<uint64_t>(g.vhead) + ((it - r * cpr) << 3);
+                j = r % ny;
+                k = r / ny;
+            }
             o1 = s1.base + k * s1.sz + j * s1.sy + x;
             o2 = s2.base + k * s2.sz + j * s2.sy + x;
             od = d.base + k * d.sz + j * d.sy + x;
@@ -104,9 +124,9 @@ namespace hipk
     // One workgroup's span [beg, end) of 8-voxel items.  The main loop is branch-free so that
     // the compiler keeps all kUnroll x NS loads in flight (a guard per item made hipcc wait
     // vmcnt(0) after every item); the remainder loop handles the last partial quantum.
-    template <int NS, int BPV, bool FLAT, class F>
+    template <int NS, int BPV, int MODE, class F>
     __device__ __forceinline__ void pointwiseVecSpan(Operand const& d, Operand const& s1, Operand const& s2,
-                                                     uint64_t beg, uint64_t end, uint64_t cpr, uint64_t ny, F const& f)
+                                                     Geom const& g, uint64_t beg, uint64_t end, F const& f)
     {
         constexpr uint64_t kQ = static_cast<uint64_t>(kBlock) * kUnroll;
         uint64_t it = beg + threadIdx.x;
@@ -118,8 +138,8 @@ namespace hipk
             for (int u = 0; u < kUnroll; ++u)
             {
                 uint64_t o1, o2;
-                pointwiseVecItem<NS, BPV, FLAT, F>(d, s1, s2, it + static_cast<uint64_t>(u) * kBlock, cpr, ny, o1,
-                                                   o2, od[u]);
+                pointwiseVecItem<NS, BPV, MODE, F>(d, s1, s2, g, it + static_cast<uint64_t>(u) * kBlock, o1, o2,
+                                                   od[u]);
                 if constexpr (NS >= 1)
                     load8<BPV, true>(s1.data, o1, a[u]);
                 if constexpr (NS >= 2)
@@ -139,7 +159,7 @@ namespace hipk
         {
             uint32_t a[8], b[8], o[8];
             uint64_t o1, o2, od;
-            pointwiseVecItem<NS, BPV, FLAT, F>(d, s1, s2, it, cpr, ny, o1, o2, od);
+            pointwiseVecItem<NS, BPV, MODE, F>(d, s1, s2, g, it, o1, o2, od);
             if constexpr (NS >= 1)
                 load8<BPV, true>(s1.data, o1, a);
             if constexpr (NS >= 2)
@@ -159,7 +179,7 @@ namespace hipk
     template <int NS, int BPV, class F>
     __global__ __launch_bounds__(kBlock) void pointwiseVecKernel(Operand d, Operand s1, Operand s2, Geom g, F f)
     {
-        uint64_t const cpr = static_cast<uint64_t>(g.vnx8) >> 3;          // chunks per row
+        uint64_t const cpr = static_cast<uint64_t>(g.vnx8 - g.vhead) >> 3;   // chunks per row
         uint64_t const rows = static_cast<uint64_t>(g.vny) * static_cast<uint64_t>(g.vnz);
         uint64_t const items = cpr * rows;
         uint64_t const ny = static_cast<uint64_t>(g.vny);
@@ -169,13 +189,16 @@ namespace hipk
             uint64_t const beg = q * kQ;
             uint64_t const end = beg + kQ < items ? beg + kQ : items;
             if (rows == 1)
-                pointwiseVecSpan<NS, BPV, true>(d, s1, s2, beg, end, cpr, ny, f);
+                pointwiseVecSpan<NS, BPV, 0>(d, s1, s2, g, beg, end, f);
+            else if (g.fast32)
+                pointwiseVecSpan<NS, BPV, 1>(d, s1, s2, g, beg, end, f);
             else
-                pointwiseVecSpan<NS, BPV, false>(d, s1, s2, beg, end, cpr, ny, f);
+                pointwiseVecSpan<NS, BPV, 2>(d, s1, s2, g, beg, end, f);
         }
 
-        // scalar tail of every row: voxels [vnx8, vnx)
-        uint64_t const tailLen = static_cast<uint64_t>(g.vnx - g.vnx8);
+        // scalar edges of every row: head [0, vhead) and tail [vnx8, vnx)
+        uint64_t const head = static_cast<uint64_t>(g.vhead);
+        uint64_t const tailLen = head + static_cast<uint64_t>(g.vnx - g.vnx8);
         if (tailLen == 0)
             return;
         uint64_t const tid = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
@@ -184,7 +207,8 @@ namespace hipk
         for (uint64_t it = tid; it < tailItems; it += stride)
         {
             uint64_t r = it / tailLen;
-            uint64_t x = static_cast<uint64_t>(g.vnx8) + (it - r * tailLen);
+            uint64_t e = it - r * tailLen;
+            uint64_t x = e < head ? e : static_cast<uint64_t>(g.vnx8) + (e - head);
             uint64_t j = r % ny, k = r / ny;
             uint32_t a = 0, b = 0;
             if constexpr (NS >= 1)
@@ -204,10 +228,22 @@ namespace hipk
         uint64_t const total = nx * ny * static_cast<uint64_t>(g.nz);
         for (uint64_t l = tid; l < total; l += stride)
         {
-            uint64_t i = l % nx;
-            uint64_t t = l / nx;
-            uint64_t j = t % ny;
-            uint64_t k = t / ny;
+            uint64_t i, j, k;
+            if (g.fast32)
+            {
+                uint32_t t = fdiv(static_cast<uint32_t>(l), g.divNx);
+                i = static_cast<uint32_t>(l) - t * g.divNx.d;
+                uint32_t kk = fdiv(t, g.divNy);
+                k = kk;
+                j = t - kk * g.divNy.d;
+            }
+            else
+            {
+                i = l % nx;
+                uint64_t t = l / nx;
+                j = t % ny;
+                k = t / ny;
+            }
             uint32_t a = 0, b = 0;
             if constexpr (NS >= 1)
                 a = loadCodeDyn(s1.data, scalarIndex(s1, i, j, k), s1.bpv);
@@ -238,8 +274,15 @@ namespace hipk
             if (p.vec && p.bpv == BPV)
             {
                 uint64_t items = static_cast<uint64_t>(p.g.vny) * static_cast<uint64_t>(p.g.vnz) *
-                                 static_cast<uint64_t>(p.g.vnx8 / 8 + (p.g.vnx - p.g.vnx8));
+                                 static_cast<uint64_t>((p.g.vnx8 - p.g.vhead) / 8);
                 uint64_t quanta = (items + kBlock * kUnroll - 1) / (kBlock * kUnroll);
+                // enough threads for the scalar row edges too (narrow boxes are all edge)
+                uint64_t edgeItems = static_cast<uint64_t>(p.g.vny) * static_cast<uint64_t>(p.g.vnz) *
+                                     static_cast<uint64_t>(p.g.vhead + (p.g.vnx - p.g.vnx8));
+                uint64_t edgeBlocks = (edgeItems + kBlock - 1) / kBlock;
+                edgeBlocks = edgeBlocks < 2048 ? edgeBlocks : 2048;
+                if (quanta < edgeBlocks)
+                    quanta = edgeBlocks;
                 unsigned grid = static_cast<unsigned>(quanta < (1u << 30) ? (quanta > 0 ? quanta : 1) : (1u << 30));
                 hipLaunchKernelGGL((pointwiseVecKernel<NS, BPV, F>), dim3(grid), dim3(kBlock), 0, stream,
                                    p.d, p.s1, p.s2, p.g, f);

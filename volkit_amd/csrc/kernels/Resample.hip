@@ -123,66 +123,111 @@ namespace hipk
                static_cast<uint64_t>(a.sdx);
     }
 
-    // ---- integer-ratio replication path --------------------------------------------
-    // One wave per source row (task).  The destination row is written as 512-voxel store
-    // instructions: lane l of instruction g writes dst voxels [512g + 8l, +8), i.e. every
-    // wave-instruction stores one contiguous 8*BPV*64-byte block (1 KiB for UInt16); those
-    // 8 voxels come from 8/K consecutive source voxels, loaded with one coalesced
-    // nontemporal load per lane.  Up to 4 instructions' loads are issued before any store.
-    // The same registers are stored to every destination row of the task's rectangle.
-    // Measured (kbench, 512^3 -> 1024^3 UInt16, identity codes): 0.35 ms = 6.9 TB/s of
-    // algorithmic bytes, against 0.93 ms for the earlier 8-source-voxels-per-lane layout,
-    // whose half-strided store instructions the memory system merged poorly.
-    template <int BPV, int K, bool CONV, int FS, int FD, int NSLOT>
-    __global__ __launch_bounds__(kBlock) void resampleRepKernel(ResampleArgs a)
+    // ---- integer-ratio row kernel (replication, conversion, and the Float32 lerp chain) ----
+    // One wave per source row (task).  Destination rows are written as wave-instructions of
+    // 64 lanes x 16 bytes: lane l of instruction g writes dst voxels [g*64V + V*l, +V) with
+    // V = 16 / BPVD, so every wave-store is one contiguous KiB.  Those V voxels come from
+    // N = V / K consecutive source voxels (one coalesced load per lane); each source voxel is
+    // decoded / converted / chained ONCE and replicated K times in registers, and the same
+    // registers are stored to every destination row of the task's rectangle.  Loads of all
+    // NSLOT instructions are issued unconditionally (clamped into the row) before any store.
+    // Measured (512^3 -> 1024^3 UInt16 identity): 0.35 ms = 6.9 TB/s; a half-strided store
+    // layout (2 x 16 B per lane) ran at 2.6 TB/s.
+    //
+    // MODE 0: identity codes (verified on the host for every code); MODE 1: convert each
+    // source code; MODE 2: "Linear" with float semantics -- the reference's sampleLinear
+    // chain lerp(lerp(lerp(v000,v100,0),lerp(v010,v110,0),0), lerp(...), 0) over the
+    // neighbours (x+1 = next voxel in memory, y+1 / z+1 clamped), evaluated per SOURCE voxel.
+    template <int BPVS, int BPVD, int K, int MODE, int FS, int FD, int NSLOT>
+    __global__ __launch_bounds__(kBlock) void resampleRowKernel(ResampleArgs a)
     {
-        constexpr int kSrcPerLane = 8 / K;
+        constexpr int V = 16 / BPVD;
+        constexpr int N = V / K;
+        constexpr int kInstr = 64 * V;
         int const lane = threadIdx.x & 63;
         uint32_t const wavesPerBlock = blockDim.x >> 6;
-        // wave-uniform task index in SGPRs (scalar loads of the run tables)
+        // wave-uniform task index in SGPRs
         uint32_t const wave = __builtin_amdgcn_readfirstlane(xcdSwizzle(blockIdx.x, gridDim.x) * wavesPerBlock +
                                                              (threadIdx.x >> 6));
         uint32_t const totalWaves = gridDim.x * wavesPerBlock;
         uint32_t const tasks = static_cast<uint32_t>(a.nRunsY) * static_cast<uint32_t>(a.nRunsZ);
-        int32_t const instrPerRow = (a.ddx + 511) / 512;
+        int32_t const instrPerRow = (a.ddx + kInstr - 1) / kInstr;
 
         for (uint32_t t = wave; t < tasks; t += totalWaves)
         {
             Run const ry = runY(a, t % static_cast<uint32_t>(a.nRunsY));
             Run const rz = runZ(a, t / static_cast<uint32_t>(a.nRunsY));
-            uint64_t const srow = srcRowIndex(a, ry.s, rz.s);
+            uint64_t const r00 = srcRowIndex(a, ry.s, rz.s);
+            uint64_t r10 = 0, r01 = 0, r11 = 0;
+            if constexpr (MODE == 2)
+            {
+                int32_t const hy = ry.s + 1 < a.sdy ? ry.s + 1 : a.sdy - 1;
+                int32_t const hz = rz.s + 1 < a.srcGlobalDz ? rz.s + 1 : a.srcGlobalDz - 1;
+                r10 = srcRowIndex(a, hy, rz.s);
+                r01 = srcRowIndex(a, ry.s, hz);
+                r11 = srcRowIndex(a, hy, hz);
+            }
             for (int32_t g0 = 0; g0 < instrPerRow; g0 += NSLOT)
             {
-                uint32_t code[NSLOT][8];
+                uint32_t code[NSLOT][V];
                 bool active[NSLOT];
-                // loads are unconditional (clamped into the row) so all stay in flight;
-                // only the stores are predicated
 #pragma unroll
                 for (int u = 0; u < NSLOT; ++u)
                 {
-                    int32_t dx = 512 * (g0 + u) + 8 * lane;
+                    int32_t dx = kInstr * (g0 + u) + V * lane;
                     active[u] = g0 + u < instrPerRow && dx < a.ddx;
-                    dx = dx < a.ddx ? dx : a.ddx - 8;
-                    uint32_t sc[kSrcPerLane];
-                    loadN<BPV, kSrcPerLane, true>(a.src, srow + static_cast<uint64_t>(dx / K), sc);
-                    if constexpr (CONV)
+                    dx = dx < a.ddx ? dx : a.ddx - V;
+                    uint64_t const sx = static_cast<uint64_t>(dx / K);
+                    uint32_t sc[N];
+                    loadN<BPVS, N, true>(a.src, r00 + sx, sc);
+                    if constexpr (MODE == 1)
                     {
 #pragma unroll
-                        for (int i = 0; i < kSrcPerLane; ++i)
+                        for (int i = 0; i < N; ++i)
                             sc[i] = convertCode<FS, FD>(sc[i], a);
                     }
+                    else if constexpr (MODE == 2)
+                    {
+                        uint32_t c10[N], c01[N], c11[N];
+                        loadN<BPVS, N, true>(a.src, r10 + sx, c10);
+                        loadN<BPVS, N, true>(a.src, r01 + sx, c01);
+                        loadN<BPVS, N, true>(a.src, r11 + sx, c11);
+                        uint64_t const last = a.srcVoxels - 1;   // reference reads past the end: clamp
+                        auto flat = [&](uint64_t i) { return loadCode<BPVS>(a.src, i < last ? i : last); };
+                        uint32_t const e00 = flat(r00 + sx + N), e10 = flat(r10 + sx + N);
+                        uint32_t const e01 = flat(r01 + sx + N), e11 = flat(r11 + sx + N);
+                        int32_t const fs = FS == -1 ? a.fs : FS;
+                        auto dec = [&](uint32_t c) { return codec::decode(c, fs, a.slo, a.shi); };
+                        float const f = 0.f;   // every fraction of sampleLinear(int,int,int) is 0
+                        uint32_t out[N];
 #pragma unroll
-                    for (int i = 0; i < 8; ++i)
+                        for (int i = 0; i < N; ++i)
+                        {
+                            float v0 = dec(sc[i]), v1 = dec(i + 1 < N ? sc[i + 1] : e00);
+                            float v2 = dec(c10[i]), v3 = dec(i + 1 < N ? c10[i + 1] : e10);
+                            float v4 = dec(c01[i]), v5 = dec(i + 1 < N ? c01[i + 1] : e01);
+                            float v6 = dec(c11[i]), v7 = dec(i + 1 < N ? c11[i + 1] : e11);
+                            float value = codec::lerp(codec::lerp(codec::lerp(v0, v1, f), codec::lerp(v2, v3, f), f),
+                                                      codec::lerp(codec::lerp(v4, v5, f), codec::lerp(v6, v7, f), f), f);
+                            bool w;
+                            out[i] = codec::encode(value, FD == -1 ? a.fd : FD, a.dm, w);
+                        }
+#pragma unroll
+                        for (int i = 0; i < N; ++i)
+                            sc[i] = out[i];
+                    }
+#pragma unroll
+                    for (int i = 0; i < V; ++i)
                         code[u][i] = sc[i / K];
                 }
                 for (int32_t zd = rz.d0; zd < rz.d1; ++zd)
                     for (int32_t yd = ry.d0; yd < ry.d1; ++yd)
                     {
-                        uint64_t const drow = dstRowIndex(a, yd, zd) + 8u * lane;
+                        uint64_t const drow = dstRowIndex(a, yd, zd) + static_cast<uint64_t>(V) * lane;
 #pragma unroll
                         for (int u = 0; u < NSLOT; ++u)
                             if (active[u])
-                                store8<BPV, true>(a.dst, drow + 512u * (g0 + u), code[u]);
+                                store16<BPVD>(a.dst, drow + static_cast<uint64_t>(kInstr) * (g0 + u), code[u]);
                     }
             }
         }
@@ -213,6 +258,57 @@ namespace hipk
                 for (int32_t zd = rz.d0; zd < rz.d1; ++zd)
                     for (int32_t yd = ry.d0; yd < ry.d1; ++yd)
                         storeCodeDyn(a.dst, dstRowIndex(a, yd, zd) + static_cast<uint64_t>(x), bd, c);
+            }
+        }
+    }
+
+    // Vectorised gather: lane l handles V = 16 / BPVD consecutive destination voxels, reads
+    // their V exact x-table entries and V source codes (the row is L1/L2-resident while the
+    // wave sweeps it) and writes one 16-byte nontemporal store per destination row.
+    template <int BPVD, bool CONV>
+    __global__ __launch_bounds__(kBlock) void resampleGatherVecKernel(ResampleArgs a)
+    {
+        constexpr int V = 16 / BPVD;
+        int const lane = threadIdx.x & 63;
+        uint32_t const wavesPerBlock = blockDim.x >> 6;
+        uint32_t const wave = __builtin_amdgcn_readfirstlane(xcdSwizzle(blockIdx.x, gridDim.x) * wavesPerBlock +
+                                                             (threadIdx.x >> 6));
+        uint32_t const totalWaves = gridDim.x * wavesPerBlock;
+        uint32_t const tasks = static_cast<uint32_t>(a.nRunsY) * static_cast<uint32_t>(a.nRunsZ);
+        uint32_t const bs = codec::bytesPerVoxel(a.fs);
+
+        for (uint32_t t = wave; t < tasks; t += totalWaves)
+        {
+            Run const ry = runY(a, t % static_cast<uint32_t>(a.nRunsY));
+            Run const rz = runZ(a, t / static_cast<uint32_t>(a.nRunsY));
+            uint64_t const srow = srcRowIndex(a, ry.s, rz.s);
+            for (int32_t dx = V * lane; dx < a.ddx; dx += 64 * V)
+            {
+                int32_t xs[V];
+                if constexpr (V == 4)
+                {
+                    u32x4 q = *reinterpret_cast<u32x4 const*>(a.xtab + dx);
+                    xs[0] = q.x; xs[1] = q.y; xs[2] = q.z; xs[3] = q.w;
+                }
+                else
+                {
+#pragma unroll
+                    for (int i = 0; i < V; i += 4)
+                    {
+                        u32x4 q = *reinterpret_cast<u32x4 const*>(a.xtab + dx + i);
+                        xs[i] = q.x; xs[i + 1] = q.y; xs[i + 2] = q.z; xs[i + 3] = q.w;
+                    }
+                }
+                uint32_t code[V];
+#pragma unroll
+                for (int i = 0; i < V; ++i)
+                {
+                    uint32_t c = loadCodeDyn(a.src, srow + static_cast<uint64_t>(xs[i]), bs);
+                    code[i] = CONV ? convertCode<-1, -1>(c, a) : c;
+                }
+                for (int32_t zd = rz.d0; zd < rz.d1; ++zd)
+                    for (int32_t yd = ry.d0; yd < ry.d1; ++yd)
+                        store16<BPVD>(a.dst, dstRowIndex(a, yd, zd) + static_cast<uint64_t>(dx), code);
             }
         }
     }
@@ -371,17 +467,18 @@ namespace hipk
         affineOf(rz, t.aff[1]);
         t.minSz = rz.empty() ? 0 : rz.front().s;
         t.maxSz = rz.empty() ? -1 : rz.back().s;
-        size_t words = 3 * ry.size() + 3 * rz.size() + xt.size();
-        std::vector<int32_t> host;
-        host.reserve(words);
+        // layout: x table first (16-byte aligned for vector reads, padded to 4 entries), runs after
+        size_t xwords = (xt.size() + 3) / 4 * 4;
+        size_t words = xwords + 3 * ry.size() + 3 * rz.size();
+        std::vector<int32_t> host(xt.begin(), xt.end());
+        host.resize(xwords, 0);
         for (Run const& r : ry) host.insert(host.end(), {r.s, r.d0, r.d1});
         for (Run const& r : rz) host.insert(host.end(), {r.s, r.d0, r.d1});
-        host.insert(host.end(), xt.begin(), xt.end());
         VKT_HIP_TRY(hipMalloc(&t.dev, words * sizeof(int32_t) + 16));
         VKT_HIP_TRY(hipMemcpy(t.dev, host.data(), words * sizeof(int32_t), hipMemcpyHostToDevice));
-        t.runsY = reinterpret_cast<Run const*>(t.dev);
-        t.runsZ = reinterpret_cast<Run const*>(t.dev + 3 * ry.size());
-        t.xtab = t.dev + 3 * ry.size() + 3 * rz.size();
+        t.xtab = t.dev;
+        t.runsY = reinterpret_cast<Run const*>(t.dev + xwords);
+        t.runsZ = reinterpret_cast<Run const*>(t.dev + xwords + 3 * ry.size());
         cache[{dev, key}] = t;
         out = t;
         return vktNoError;
@@ -447,6 +544,80 @@ namespace hipk
         ConvProps p{identityConversionUncached(fs, slo, shi, fd, dlo, dhi), allSourceValuesFiniteUncached(fs, slo, shi)};
         cache[key] = p;
         return p;
+    }
+
+    // Picks and launches the row kernel instantiation; false = layout/ratio not covered.
+    template <int BPVS, int BPVD, int MODE, int FS, int FD>
+    void launchRowK(ResampleArgs const& a, int32_t k, unsigned grid, int32_t instrPerRow, hipStream_t s)
+    {
+#define VKT_ROW_NS(K)                                                                                        \
+    do {                                                                                                     \
+        if (instrPerRow == 1)                                                                                \
+            hipLaunchKernelGGL((resampleRowKernel<BPVS, BPVD, K, MODE, FS, FD, 1>), dim3(grid), dim3(kBlock), 0, s, a); \
+        else if (instrPerRow == 2)                                                                           \
+            hipLaunchKernelGGL((resampleRowKernel<BPVS, BPVD, K, MODE, FS, FD, 2>), dim3(grid), dim3(kBlock), 0, s, a); \
+        else                                                                                                 \
+            hipLaunchKernelGGL((resampleRowKernel<BPVS, BPVD, K, MODE, FS, FD, 4>), dim3(grid), dim3(kBlock), 0, s, a); \
+    } while (0)
+        if (k == 1)
+        {
+            if constexpr ((16 / BPVD) * BPVS <= 32)
+                VKT_ROW_NS(1);
+        }
+        else if (k == 2)
+            VKT_ROW_NS(2);
+        else
+            VKT_ROW_NS(4);
+#undef VKT_ROW_NS
+    }
+
+    bool launchRowKernel(ResampleArgs const& a, int32_t k, uint64_t tasks, uint32_t bs, uint32_t bd, bool identity,
+                         bool chain, vktHipVolumeView_t const& src, vktHipVolumeView_t const& dst, hipStream_t s)
+    {
+        if (!(k == 1 || k == 2 || k == 4))
+            return false;
+        uint32_t const v = 16 / bd;            // dst voxels per lane-store
+        uint32_t const n = v / k;              // source voxels per lane-load
+        if (bd > 4 || bs > 4 || dst.dimX % v != 0 || src.dimX % n != 0 || n * bs > 32 || (k == 1 && n * bs > 32))
+            return false;
+        if (reinterpret_cast<uintptr_t>(src.data) % 16 != 0 || reinterpret_cast<uintptr_t>(dst.data) % 16 != 0)
+            return false;
+        uint64_t blocks = (tasks + 3) / 4;     // one task per wave (measured fastest)
+        unsigned grid = static_cast<unsigned>(blocks < (1u << 30) ? blocks : (1u << 30));
+        int32_t const instrPerRow = static_cast<int32_t>((dst.dimX + 64 * v - 1) / (64 * v));
+        int32_t const fs = src.dataFormat, fd = dst.dataFormat;
+        if (chain)
+        {
+            if (fs != codec::FmtFloat32)
+                return false;   // non-finite integer mappings: per-dst-voxel chain kernel
+            if (bd == 4)
+                launchRowK<4, 4, 2, codec::FmtFloat32, -1>(a, k, grid, instrPerRow, s);
+            else if (bd == 2)
+                launchRowK<4, 2, 2, codec::FmtFloat32, -1>(a, k, grid, instrPerRow, s);
+            else
+            {
+                if (k == 1)
+                    return false;
+                launchRowK<4, 1, 2, codec::FmtFloat32, -1>(a, k, grid, instrPerRow, s);
+            }
+            return true;
+        }
+        if (bs != bd)
+            return false;
+        if (identity)
+        {
+            if (bs == 1) launchRowK<1, 1, 0, -1, -1>(a, k, grid, instrPerRow, s);
+            else if (bs == 2) launchRowK<2, 2, 0, -1, -1>(a, k, grid, instrPerRow, s);
+            else launchRowK<4, 4, 0, -1, -1>(a, k, grid, instrPerRow, s);
+        }
+        else if (fs == codec::FmtUInt16 && fd == codec::FmtUInt16)
+            launchRowK<2, 2, 1, codec::FmtUInt16, codec::FmtUInt16>(a, k, grid, instrPerRow, s);
+        else if (fs == codec::FmtUInt8 && fd == codec::FmtUInt8)
+            launchRowK<1, 1, 1, codec::FmtUInt8, codec::FmtUInt8>(a, k, grid, instrPerRow, s);
+        else if (bs == 1) launchRowK<1, 1, 1, -1, -1>(a, k, grid, instrPerRow, s);
+        else if (bs == 2) launchRowK<2, 2, 1, -1, -1>(a, k, grid, instrPerRow, s);
+        else launchRowK<4, 4, 1, -1, -1>(a, k, grid, instrPerRow, s);
+        return true;
     }
 
     vktError resampleSlab(vktHipVolumeView_t dst, vktHipVolumeView_t src, vktFilterMode fm, int32_t dgz, int32_t dz0,
@@ -533,52 +704,25 @@ namespace hipk
             return rt::fail("Resample_hip: too many source rows");
         unsigned grid = streamingGrid(tasks, kBlock / 64);
 
+        uint32_t const bs = codec::bytesPerVoxel(src.dataFormat), bd = codec::bytesPerVoxel(dst.dataFormat);
+        if (launchRowKernel(a, t.k, tasks, bs, bd, identity, chain, src, dst, s))
+            return rt::finishLaunch(chain ? "Resample_hip(row, linear chain)" : "Resample_hip(row)");
         if (chain)
         {
             hipLaunchKernelGGL(resampleChainKernel, dim3(grid), dim3(kBlock), 0, s, a);
-            return rt::finishLaunch("Resample_hip(linear chain)");
+            return rt::finishLaunch("Resample_hip(linear chain, gather)");
         }
-
-        uint32_t const bs = codec::bytesPerVoxel(src.dataFormat), bd = codec::bytesPerVoxel(dst.dataFormat);
-        bool const aligned = reinterpret_cast<uintptr_t>(src.data) % 16 == 0 &&
-                             reinterpret_cast<uintptr_t>(dst.data) % 16 == 0 && src.dimX % 8 == 0;
-        if (t.k >= 1 && t.k <= 4 && t.k != 3 && aligned && bs == bd && dst.dimX % 8 == 0)
+        uint32_t const v = bd <= 4 ? 16 / bd : 0;
+        if (v != 0 && dst.dimX % v == 0 && reinterpret_cast<uintptr_t>(dst.data) % 16 == 0)
         {
-            // one task per wave: measured fastest (no task loop latency chain)
-            uint64_t repBlocks = (tasks + 3) / 4;
-            unsigned repGrid = static_cast<unsigned>(repBlocks < (1u << 30) ? repBlocks : (1u << 30));
-            int32_t const instrPerRow = (dst.dimX + 511) / 512;
-#define VKT_REP_LAUNCH(BPV, K, CONV, FS, FD)                                                               \
-    do {                                                                                                   \
-        if (instrPerRow == 1)                                                                              \
-            hipLaunchKernelGGL((resampleRepKernel<BPV, K, CONV, FS, FD, 1>), dim3(repGrid), dim3(kBlock), 0, s, a); \
-        else if (instrPerRow == 2)                                                                         \
-            hipLaunchKernelGGL((resampleRepKernel<BPV, K, CONV, FS, FD, 2>), dim3(repGrid), dim3(kBlock), 0, s, a); \
-        else                                                                                               \
-            hipLaunchKernelGGL((resampleRepKernel<BPV, K, CONV, FS, FD, 4>), dim3(repGrid), dim3(kBlock), 0, s, a); \
-    } while (0)
-#define VKT_REP_BY_K(BPV, CONV, FS, FD)                                                                    \
-    do {                                                                                                   \
-        if (t.k == 1) VKT_REP_LAUNCH(BPV, 1, CONV, FS, FD);                                                \
-        else if (t.k == 2) VKT_REP_LAUNCH(BPV, 2, CONV, FS, FD);                                           \
-        else VKT_REP_LAUNCH(BPV, 4, CONV, FS, FD);                                                         \
-    } while (0)
-            if (identity)
-            {
-                if (bs == 1) VKT_REP_BY_K(1, false, -1, -1);
-                else if (bs == 2) VKT_REP_BY_K(2, false, -1, -1);
-                else VKT_REP_BY_K(4, false, -1, -1);
-            }
-            else if (src.dataFormat == codec::FmtUInt16 && dst.dataFormat == codec::FmtUInt16)
-                VKT_REP_BY_K(2, true, codec::FmtUInt16, codec::FmtUInt16);
-            else if (src.dataFormat == codec::FmtUInt8 && dst.dataFormat == codec::FmtUInt8)
-                VKT_REP_BY_K(1, true, codec::FmtUInt8, codec::FmtUInt8);
-            else if (bs == 1) VKT_REP_BY_K(1, true, -1, -1);
-            else if (bs == 2) VKT_REP_BY_K(2, true, -1, -1);
-            else VKT_REP_BY_K(4, true, -1, -1);
-#undef VKT_REP_BY_K
-#undef VKT_REP_LAUNCH
-            return rt::finishLaunch("Resample_hip(replicate)");
+            uint64_t blocks = (tasks + 3) / 4;   // one task per wave
+            unsigned g = static_cast<unsigned>(blocks < (1u << 30) ? blocks : (1u << 30));
+#define VKT_GV(B, C) hipLaunchKernelGGL((resampleGatherVecKernel<B, C>), dim3(g), dim3(kBlock), 0, s, a)
+            if (bd == 1) { if (identity) VKT_GV(1, false); else VKT_GV(1, true); }
+            else if (bd == 2) { if (identity) VKT_GV(2, false); else VKT_GV(2, true); }
+            else { if (identity) VKT_GV(4, false); else VKT_GV(4, true); }
+#undef VKT_GV
+            return rt::finishLaunch("Resample_hip(gather, vector)");
         }
         hipLaunchKernelGGL(resampleGatherKernel, dim3(grid), dim3(kBlock), 0, s, a, identity ? 0 : 1);
         return rt::finishLaunch("Resample_hip(gather)");
