@@ -34,6 +34,10 @@ def parse():
     p.add_argument("--dst", type=int, default=1024, help="per-GPU dst cube edge (source = dst/2)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-dst", type=int, default=512, help="dst edge of the CPU-baseline sample")
+    p.add_argument("--dist-backend", default="nccl",
+                   help="torch.distributed backend for N>1 (nccl = RCCL over xGMI; gloo only for rehearsal)")
+    p.add_argument("--rehearse-one-device", action="store_true",
+                   help="put every rank on device 0 (multi-rank rehearsal on a 1-GPU box, with --dist-backend gloo)")
     return p.parse_args()
 
 
@@ -64,9 +68,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.rehearse_one_device:
+        local = 0
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.dist_backend)
 
     import volkit_amd.volkit as vkt
     from volkit_amd import slab
@@ -145,7 +154,8 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        dev = "cuda" if args.dist_backend == "nccl" else "cpu"
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -165,7 +175,9 @@ def main():
     tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(tf):
         try:
-            traffic = json.load(open(tf)).get("SumRange_bytes_per_launch")
+            pm = json.load(open(tf))
+            if pm.get("bench_dst_edge") == E:   # only for the workload the counters were taken on
+                traffic = pm.get("SumRange_bytes_per_launch")
         except Exception:
             traffic = None
 

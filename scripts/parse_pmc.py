@@ -34,9 +34,11 @@ def short(name):
 
 def main():
     root = sys.argv[1]
+    dst_edge = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
     fetch = load(os.path.join(root, "fetch", "**", "*counter_collection.csv"), "FETCH_SIZE")
     write = load(os.path.join(root, "write", "**", "*counter_collection.csv"), "WRITE_SIZE")
-    out = {"note": "bytes per launch; FETCH_SIZE doubled per the gfx950 correction", "kernels": {}}
+    out = {"note": "bytes per launch; FETCH_SIZE doubled per the gfx950 correction",
+           "bench_dst_edge": dst_edge, "kernels": {}}
     for name in set(fetch) | set(write):
         f = fetch.get(name, [])
         w = write.get(name, [])

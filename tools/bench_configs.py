@@ -33,6 +33,13 @@ def alloc(dims, fmt, lo=0.0, hi=1.0, seed=None):
     return v
 
 
+def rng_fill(v, n):
+    """Float32 source of BASELINE config 3: uniform in [0, 1) (torch on the same device)."""
+    t = torch.rand(n, device="cuda", dtype=torch.float32)
+    lib.vktHipMemcpy(C.c_void_p(v.data), C.c_void_p(t.data_ptr()), n * 4, 3)
+    torch.cuda.synchronize()
+
+
 def free(*vs):
     for v in vs:
         lib.vktHipFree(C.c_void_p(v.data))
@@ -66,6 +73,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--big", action="store_true", help="include 2048^3 cases (~50 GB of HBM)")
+    ap.add_argument("--only", default="", help="run only cases whose group name contains this")
     args = ap.parse_args()
     torch.cuda.set_device(0)
     stream = torch.cuda.Stream()
@@ -74,23 +82,31 @@ def main():
     o = Vec3i_t(0, 0, 0)
     R = args.reps
 
+    want = lambda g: args.only in g   # noqa: E731
+
     # config 2: 512^3 UInt16 SafeSum / SafeDiff / SumRange
     n = 512
-    A, B, D = alloc((n,) * 3, 5, seed=1), alloc((n,) * 3, 5, seed=2), alloc((n,) * 3, 5)
-    last = Vec3i_t(n, n, n)
-    for name, op in (("SafeSum", 5), ("SafeDiff", 6), ("SumRange", 0)):
-        ms = timed(lambda: lib.vktHipArithmeticRange(op, D, A, B, o, last, o), R)
-        report(f"config2 {name} 512^3 UInt16", ms, 6 * n ** 3, n ** 3)
-    free(A, B, D)
-
+    if not want("config2"):
+        n = 0
+    if n:
+        A, B, D = alloc((n,) * 3, 5, seed=1), alloc((n,) * 3, 5, seed=2), alloc((n,) * 3, 5)
+        last = Vec3i_t(n, n, n)
+        for name, op in (("SafeSum", 5), ("SafeDiff", 6), ("SumRange", 0)):
+            ms = timed(lambda: lib.vktHipArithmeticRange(op, D, A, B, o, last, o), R)
+            report(f"config2 {name} 512^3 UInt16", ms, 6 * n ** 3, n ** 3)
+        free(A, B, D)
     # config 3: 1024^3 Float32 -> 2048^3 Linear (lerp-chain kernel) and Nearest (replication)
     s, e = 1024, 2048
-    S = alloc((s,) * 3, 7, seed=3)
-    Rv = alloc((e,) * 3, 7)
-    for fm, lab in ((1, "Linear"), (0, "Nearest")):
-        ms = timed(lambda: lib.vktHipResample(Rv, S, fm), max(3, R // 3))
-        report(f"config3 Resample 1024^3->2048^3 Float32 {lab}", ms, 4 * s ** 3 + 4 * e ** 3, e ** 3)
-    free(S, Rv)
+    if want("config3"):
+        S = alloc((s,) * 3, 7)
+        rng_fill(S, s ** 3)
+        Rv = alloc((e,) * 3, 7)
+        for fm, lab in ((1, "Linear"), (0, "Nearest")):
+            ms = timed(lambda: lib.vktHipResample(Rv, S, fm), max(3, R // 3))
+            report(f"config3 Resample 1024^3->2048^3 Float32 {lab}", ms, 4 * s ** 3 + 4 * e ** 3, e ** 3)
+        free(S, Rv)
+    if not want("metric"):
+        return
 
     # metric kernels at 1024^3 and some extra ops
     s, e = 512, 1024

@@ -26,6 +26,7 @@
 #include "volkit_hip.h"
 
 #include <cmath>
+#include <cstdlib>
 #include <map>
 #include <mutex>
 #include <tuple>
@@ -74,6 +75,7 @@ namespace hipk
         // at the start of every task.
         int32_t affY, saY, daY, dlY, s0Y, d0Y;
         int32_t affZ, saZ, daZ, dlZ, s0Z, d0Z;
+        int32_t band;              // chain task order: rows per band (0 = plain y-fastest order)
         int32_t const* xtab;       // device, ddx entries (gather/chain paths)
         int32_t k;                 // integer x ratio (replication path)
         int32_t fs, fd;
@@ -150,13 +152,34 @@ namespace hipk
         uint32_t const wave = __builtin_amdgcn_readfirstlane(xcdSwizzle(blockIdx.x, gridDim.x) * wavesPerBlock +
                                                              (threadIdx.x >> 6));
         uint32_t const totalWaves = gridDim.x * wavesPerBlock;
-        uint32_t const tasks = static_cast<uint32_t>(a.nRunsY) * static_cast<uint32_t>(a.nRunsZ);
         int32_t const instrPerRow = (a.ddx + kInstr - 1) / kInstr;
+        // Task order.  Replication/conversion: y fastest (the write stream sweeps each plane).
+        // Chain: bands of kBand source rows, then z, then y within the band -- the workgroup
+        // that handles plane sz+1 of a band runs right after the one for plane sz on the same
+        // XCD (xcdSwizzle), so the z+1 neighbour rows are still in L2 (otherwise they were
+        // evicted and re-read from HBM: 2x source traffic measured).
+        uint32_t const kBand = MODE == 2 ? static_cast<uint32_t>(a.band) : 0u;
+        uint32_t const nY = static_cast<uint32_t>(a.nRunsY), nZ = static_cast<uint32_t>(a.nRunsZ);
+        uint32_t const tasks = kBand ? (nY + kBand - 1) / kBand * kBand * nZ : nY * nZ;
 
         for (uint32_t t = wave; t < tasks; t += totalWaves)
         {
-            Run const ry = runY(a, t % static_cast<uint32_t>(a.nRunsY));
-            Run const rz = runZ(a, t / static_cast<uint32_t>(a.nRunsY));
+            uint32_t iy, iz;
+            if (kBand)
+            {
+                uint32_t const rest = t / kBand;
+                iz = rest % nZ;
+                iy = (rest / nZ) * kBand + t % kBand;
+                if (iy >= nY)
+                    continue;
+            }
+            else
+            {
+                iy = t % nY;
+                iz = t / nY;
+            }
+            Run const ry = runY(a, iy);
+            Run const rz = runZ(a, iz);
             uint64_t const r00 = srcRowIndex(a, ry.s, rz.s);
             uint64_t r10 = 0, r01 = 0, r11 = 0;
             if constexpr (MODE == 2)
@@ -192,10 +215,20 @@ namespace hipk
                         loadN<BPVS, N, true>(a.src, r10 + sx, c10);
                         loadN<BPVS, N, true>(a.src, r01 + sx, c01);
                         loadN<BPVS, N, true>(a.src, r11 + sx, c11);
-                        uint64_t const last = a.srcVoxels - 1;   // reference reads past the end: clamp
-                        auto flat = [&](uint64_t i) { return loadCode<BPVS>(a.src, i < last ? i : last); };
-                        uint32_t const e00 = flat(r00 + sx + N), e10 = flat(r10 + sx + N);
-                        uint32_t const e01 = flat(r01 + sx + N), e11 = flat(r11 + sx + N);
+                        // x+1 neighbour of the lane's last voxel = the next lane's first voxel:
+                        // wave64 shuffle; lane 63 and the row's last group (whose neighbour is
+                        // the next row's first voxel, or past the buffer end) read it directly.
+                        uint32_t e00 = __shfl_down(sc[0], 1), e10 = __shfl_down(c10[0], 1);
+                        uint32_t e01 = __shfl_down(c01[0], 1), e11 = __shfl_down(c11[0], 1);
+                        if (lane == 63 || dx + V >= a.ddx)
+                        {
+                            uint64_t const last = a.srcVoxels - 1;   // reference reads past the end: clamp
+                            auto flat = [&](uint64_t i) { return loadCode<BPVS>(a.src, i < last ? i : last); };
+                            e00 = flat(r00 + sx + N);
+                            e10 = flat(r10 + sx + N);
+                            e01 = flat(r01 + sx + N);
+                            e11 = flat(r11 + sx + N);
+                        }
                         int32_t const fs = FS == -1 ? a.fs : FS;
                         auto dec = [&](uint32_t c) { return codec::decode(c, fs, a.slo, a.shi); };
                         float const f = 0.f;   // every fraction of sampleLinear(int,int,int) is 0
@@ -582,7 +615,9 @@ namespace hipk
             return false;
         if (reinterpret_cast<uintptr_t>(src.data) % 16 != 0 || reinterpret_cast<uintptr_t>(dst.data) % 16 != 0)
             return false;
-        uint64_t blocks = (tasks + 3) / 4;     // one task per wave (measured fastest)
+        uint64_t const padded = chain && a.band ? (static_cast<uint64_t>(a.nRunsY) + a.band - 1) / a.band * a.band * a.nRunsZ
+                                                : tasks;
+        uint64_t blocks = (padded + 3) / 4;    // one task per wave (measured fastest)
         unsigned grid = static_cast<unsigned>(blocks < (1u << 30) ? blocks : (1u << 30));
         int32_t const instrPerRow = static_cast<int32_t>((dst.dimX + 64 * v - 1) / (64 * v));
         int32_t const fs = src.dataFormat, fd = dst.dataFormat;
@@ -691,6 +726,10 @@ namespace hipk
         a.affZ = t.aff[1][0]; a.saZ = t.aff[1][1]; a.daZ = t.aff[1][2]; a.dlZ = t.aff[1][3];
         a.s0Z = t.aff[1][4]; a.d0Z = t.aff[1][5];
         a.k = t.k;
+        {
+            // chain task order: bands of 8 rows (measured: equal time, 1.6x less HBM re-reading)
+            a.band = 8;
+        }
         a.fs = src.dataFormat;
         a.fd = dst.dataFormat;
         a.slo = src.mappingLo;
