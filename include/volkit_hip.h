@@ -65,6 +65,9 @@ VKTAPI vktError vktHipGetLastKernelMs(float* ms);
 VKTAPI vktError vktHipAllocate(void** ptr, size_t size);
 VKTAPI vktError vktHipFree(void* ptr);
 VKTAPI vktError vktHipMemcpy(void* dst, void const* src, size_t size, vktCopyKind ck);
+/* Host buffers allocated under the CPU policy from now on are page-locked (hipHostMalloc),
+ * so migrate() DMAs directly to/from them (default 0: malloc, as the reference). */
+VKTAPI vktError vktHipSetPinnedHostAllocation(int32_t enable);
 /* Repeat the `patternSize`-byte host pattern over `dstSize` device bytes (no device
  * allocation per call, 64-bit grid; reference truncates at 2^32 elements, Memory_cuda.cu:40). */
 VKTAPI vktError vktHipMemsetRange(void* dst, void const* pattern, size_t dstSize, size_t patternSize);

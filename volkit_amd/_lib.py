@@ -144,6 +144,7 @@ SIGNATURES = {
     "vktHipFree": (c_err, [C.c_void_p]),
     "vktHipMemcpy": (c_err, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]),
     "vktHipMemsetRange": (c_err, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_size_t]),
+    "vktHipSetPinnedHostAllocation": (c_err, [i32]),
     # volkit_hip.h algorithms
     "vktHipFillRange": (c_err, [HipVolumeView_t, Vec3i_t, Vec3i_t, f32]),
     "vktHipCopyRange": (c_err, [HipVolumeView_t, HipVolumeView_t, Vec3i_t, Vec3i_t, Vec3i_t]),

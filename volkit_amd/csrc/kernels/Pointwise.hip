@@ -11,7 +11,7 @@
 // Roofline: every op here is HBM-bound.  Algorithmic bytes per voxel of the range:
 // Fill b_dst; Copy b_src + b_dst; arithmetic b_s1 + b_s2 + b_dst (6 B for UInt16).
 
-#include "Pointwise.hpp"
+#include "PointwiseOps.hpp"
 #include "../runtime/Runtime.hpp"
 #include "volkit_hip.h"
 
@@ -21,68 +21,6 @@ namespace vkt
 {
 namespace hipk
 {
-    using codec::MapParams;
-
-    // ---- functors ------------------------------------------------------------------
-    struct FillF
-    {
-        uint32_t code;
-        __device__ __forceinline__ uint32_t operator()(uint32_t, uint32_t) const { return code; }
-    };
-
-    struct PassF
-    {
-        __device__ __forceinline__ uint32_t operator()(uint32_t a, uint32_t) const { return a; }
-    };
-
-    // dst = map_dst(unmap_src(code))  (CopyRange by value, Copy_serial.hpp:69-70;
-    // Resample same-dims branch, Resample_serial.hpp:32-48)
-    template <int FS, int FD>
-    struct ConvertF
-    {
-        int32_t fs, fd;
-        float slo, shi;
-        MapParams dm;
-        __device__ __forceinline__ uint32_t operator()(uint32_t a, uint32_t) const
-        {
-            float v = codec::decode(a, FS == kDyn ? fs : FS, slo, shi);
-            bool w;
-            return codec::encode(v, FD == kDyn ? fd : FD, dm, w);
-        }
-    };
-
-    // The ten lambdas of reference src/vkt/Arithmetic_serial.hpp:63-258.
-    template <int OP>
-    __device__ __forceinline__ float applyOp(float a, float b, float lo, float hi)
-    {
-        if constexpr (OP == vktHipOpSum) return a + b;
-        else if constexpr (OP == vktHipOpDiff) return a - b;
-        else if constexpr (OP == vktHipOpProd) return a * b;
-        else if constexpr (OP == vktHipOpQuot) return a / b;
-        else if constexpr (OP == vktHipOpAbsDiff) return fabsf(a - b);
-        else if constexpr (OP == vktHipOpSafeSum) return codec::clampRef(a + b, lo, hi);
-        else if constexpr (OP == vktHipOpSafeDiff) return codec::clampRef(a - b, lo, hi);
-        else if constexpr (OP == vktHipOpSafeProd) return codec::clampRef(a * b, lo, hi);
-        else if constexpr (OP == vktHipOpSafeQuot) return codec::clampRef(a / b, lo, hi);
-        else return codec::clampRef(fabsf(a - b), lo, hi);
-    }
-
-    template <int OP, int FS1, int FS2, int FD>
-    struct ArithF
-    {
-        int32_t fs1, fs2, fd;
-        float lo1, hi1, lo2, hi2;
-        MapParams dm;
-        __device__ __forceinline__ uint32_t operator()(uint32_t a, uint32_t b) const
-        {
-            float v1 = codec::decode(a, FS1 == kDyn ? fs1 : FS1, lo1, hi1);
-            float v2 = codec::decode(b, FS2 == kDyn ? fs2 : FS2, lo2, hi2);
-            float r = applyOp<OP>(v1, v2, dm.lo, dm.hi);
-            bool w;
-            return codec::encode(r, FD == kDyn ? fd : FD, dm, w);
-        }
-    };
-
     // ---- planning --------------------------------------------------------------------
     PwPlan planPointwise(int ns, Operand d, Operand s1, Operand s2, int64_t nx, int64_t ny, int64_t nz)
     {
@@ -227,18 +165,6 @@ namespace hipk
                fmt == codec::FmtUInt32 || fmt == codec::FmtFloat32;
     }
 
-    template <int NS, class F>
-    vktError launchByBpv(PwPlan const& p, F const& f, hipStream_t s)
-    {
-        switch (p.bpv)
-        {
-        case 1: return launchPointwise<NS, 1>(p, f, s);
-        case 2: return launchPointwise<NS, 2>(p, f, s);
-        case 4: return launchPointwise<NS, 4>(p, f, s);
-        default: return launchPointwise<NS, 0>(p, f, s);
-        }
-    }
-
     // ---- conversion (shared with Resample's same-dims branch) ---------------------------
     vktError convertBox(vktHipVolumeView_t dst, vktHipVolumeView_t src, vktVec3i_t srcOrigin, bool clampSrc,
                         vktVec3i_t dstOrigin, int64_t nx, int64_t ny, int64_t nz)
@@ -259,32 +185,6 @@ namespace hipk
                 return launchPointwise<1, 4>(p, ConvertF<codec::FmtFloat32, codec::FmtFloat32>{fs, fd, src.mappingLo, src.mappingHi, dm}, s);
         }
         return launchByBpv<1>(p, ConvertF<kDyn, kDyn>{fs, fd, src.mappingLo, src.mappingHi, dm}, s);
-    }
-
-    // ---- arithmetic dispatch ---------------------------------------------------------
-    template <int OP>
-    vktError arithmetic(PwPlan const& p, vktHipVolumeView_t const& d, vktHipVolumeView_t const& a,
-                        vktHipVolumeView_t const& b, hipStream_t s)
-    {
-        MapParams dm = codec::makeMapParams(d.mappingLo, d.mappingHi);
-        int32_t f1 = a.dataFormat, f2 = b.dataFormat, fd = d.dataFormat;
-        if (p.vec && f1 == f2 && f1 == fd)
-        {
-            if (fd == codec::FmtUInt16)
-                return launchPointwise<2, 2>(
-                    p, ArithF<OP, codec::FmtUInt16, codec::FmtUInt16, codec::FmtUInt16>{
-                           f1, f2, fd, a.mappingLo, a.mappingHi, b.mappingLo, b.mappingHi, dm}, s);
-            if (fd == codec::FmtUInt8)
-                return launchPointwise<2, 1>(
-                    p, ArithF<OP, codec::FmtUInt8, codec::FmtUInt8, codec::FmtUInt8>{
-                           f1, f2, fd, a.mappingLo, a.mappingHi, b.mappingLo, b.mappingHi, dm}, s);
-            if (fd == codec::FmtFloat32)
-                return launchPointwise<2, 4>(
-                    p, ArithF<OP, codec::FmtFloat32, codec::FmtFloat32, codec::FmtFloat32>{
-                           f1, f2, fd, a.mappingLo, a.mappingHi, b.mappingLo, b.mappingHi, dm}, s);
-        }
-        return launchByBpv<2>(p, ArithF<OP, kDyn, kDyn, kDyn>{f1, f2, fd, a.mappingLo, a.mappingHi, b.mappingLo,
-                                                               b.mappingHi, dm}, s);
     }
 
     // ---- MemsetRange ---------------------------------------------------------------
@@ -468,19 +368,13 @@ vktError vktHipArithmeticRange(vktHipArithmeticOp op, vktHipVolumeView_t dest, v
     PwPlan p = planPointwise(2, od, o1, o2, nx, ny, nz);
     hipStream_t s = rt::computeStream();
     vktError e = vktNoError;
-    switch (op)
+    switch (op / 2)
     {
-    case vktHipOpSum: e = arithmetic<vktHipOpSum>(p, dest, source1, source2, s); break;
-    case vktHipOpDiff: e = arithmetic<vktHipOpDiff>(p, dest, source1, source2, s); break;
-    case vktHipOpProd: e = arithmetic<vktHipOpProd>(p, dest, source1, source2, s); break;
-    case vktHipOpQuot: e = arithmetic<vktHipOpQuot>(p, dest, source1, source2, s); break;
-    case vktHipOpAbsDiff: e = arithmetic<vktHipOpAbsDiff>(p, dest, source1, source2, s); break;
-    case vktHipOpSafeSum: e = arithmetic<vktHipOpSafeSum>(p, dest, source1, source2, s); break;
-    case vktHipOpSafeDiff: e = arithmetic<vktHipOpSafeDiff>(p, dest, source1, source2, s); break;
-    case vktHipOpSafeProd: e = arithmetic<vktHipOpSafeProd>(p, dest, source1, source2, s); break;
-    case vktHipOpSafeQuot: e = arithmetic<vktHipOpSafeQuot>(p, dest, source1, source2, s); break;
-    case vktHipOpSafeAbsDiff: e = arithmetic<vktHipOpSafeAbsDiff>(p, dest, source1, source2, s); break;
-    default: break;
+    case 0: e = arithmeticPair0(op, p, dest, source1, source2, s); break;
+    case 1: e = arithmeticPair1(op, p, dest, source1, source2, s); break;
+    case 2: e = arithmeticPair2(op, p, dest, source1, source2, s); break;
+    case 3: e = arithmeticPair3(op, p, dest, source1, source2, s); break;
+    default: e = arithmeticPair4(op, p, dest, source1, source2, s); break;
     }
     return e != vktNoError ? e : rt::finishLaunch("ArithmeticRange_hip");
 }

@@ -1,0 +1,272 @@
+// ResampleRow.hpp -- shared types of the Resample kernels and the integer-ratio row kernel
+// template (instantiated per MODE in ResampleRow{0,1,2}.hip so that the ~100 instantiations
+// compile in parallel).  Semantics and design: kernels/Resample.hip header comment.
+#pragma once
+
+#include "KernelCommon.hpp"
+#include "volkit_c.h"
+
+namespace vkt
+{
+namespace hipk
+{
+    using codec::MapParams;
+
+    // Exact reference index formula (Resample_serial.hpp:60-62 + int32 truncation).
+    inline int32_t srcIndex(int32_t d, int32_t dd, int32_t sd)
+    {
+        volatile float q = static_cast<float>(d) / static_cast<float>(dd);
+        volatile float s = q * static_cast<float>(sd);
+        return static_cast<int32_t>(s);
+    }
+
+    // One run: destination rows [d0, d1) all read source row `s`.
+    struct Run
+    {
+        int32_t s, d0, d1;
+    };
+
+    struct ResampleArgs
+    {
+        uint8_t* dst;
+        uint8_t const* src;
+        int32_t ddx, ddy;          // dst dims x, y (dst slab depth implied by runs)
+        int32_t sdx, sdy, sdz;     // src dims of the LOCAL source buffer
+        int32_t srcZ0;             // global z of local plane 0
+        int32_t srcGlobalDz;       // global source depth (hi.z clamp)
+        int32_t dstZ0;             // global z of dst plane 0
+        int32_t nRunsY, nRunsZ;
+        Run const* runsY;          // device
+        Run const* runsZ;          // device (s in GLOBAL source planes, d in GLOBAL dst planes)
+        // Affine run generators (exact integer ratios, verified against the tables on the
+        // host): run i = {s0 + sa*i, d0 + da*i, d0 + da*i + dl}; avoids a dependent table load
+        // at the start of every task.
+        int32_t affY, saY, daY, dlY, s0Y, d0Y;
+        int32_t affZ, saZ, daZ, dlZ, s0Z, d0Z;
+        int32_t band;              // chain task order: rows per band (0 = plain y-fastest order)
+        int32_t const* xtab;       // device, ddx entries (gather/chain paths)
+        int32_t k;                 // integer x ratio (replication path)
+        int32_t fs, fd;
+        float slo, shi;
+        MapParams dm;
+        uint64_t srcVoxels;        // voxels in the local source buffer (flat-read clamp)
+        int32_t srcIsGlobalEnd;    // local buffer ends at the global end (clamp there)
+    };
+
+    __device__ __forceinline__ Run runY(ResampleArgs const& a, uint32_t i)
+    {
+        if (a.affY)
+        {
+            int32_t d0 = a.d0Y + a.daY * static_cast<int32_t>(i);
+            return Run{a.s0Y + a.saY * static_cast<int32_t>(i), d0, d0 + a.dlY};
+        }
+        return a.runsY[i];
+    }
+
+    __device__ __forceinline__ Run runZ(ResampleArgs const& a, uint32_t i)
+    {
+        if (a.affZ)
+        {
+            int32_t d0 = a.d0Z + a.daZ * static_cast<int32_t>(i);
+            return Run{a.s0Z + a.saZ * static_cast<int32_t>(i), d0, d0 + a.dlZ};
+        }
+        return a.runsZ[i];
+    }
+
+    template <int FS, int FD>
+    __device__ __forceinline__ uint32_t convertCode(uint32_t c, ResampleArgs const& a)
+    {
+        float v = codec::decode(c, FS == -1 ? a.fs : FS, a.slo, a.shi);
+        bool w;
+        return codec::encode(v, FD == -1 ? a.fd : FD, a.dm, w);
+    }
+
+    __device__ __forceinline__ uint64_t dstRowIndex(ResampleArgs const& a, int32_t yd, int32_t zdGlobal)
+    {
+        return (static_cast<uint64_t>(zdGlobal - a.dstZ0) * static_cast<uint64_t>(a.ddy) + static_cast<uint64_t>(yd)) *
+               static_cast<uint64_t>(a.ddx);
+    }
+
+    __device__ __forceinline__ uint64_t srcRowIndex(ResampleArgs const& a, int32_t ys, int32_t zsGlobal)
+    {
+        return (static_cast<uint64_t>(zsGlobal - a.srcZ0) * static_cast<uint64_t>(a.sdy) + static_cast<uint64_t>(ys)) *
+               static_cast<uint64_t>(a.sdx);
+    }
+
+    // ---- integer-ratio row kernel (replication, conversion, and the Float32 lerp chain) ----
+    // One wave per source row (task).  Destination rows are written as wave-instructions of
+    // 64 lanes x 16 bytes: lane l of instruction g writes dst voxels [g*64V + V*l, +V) with
+    // V = 16 / BPVD, so every wave-store is one contiguous KiB.  Those V voxels come from
+    // N = V / K consecutive source voxels (one coalesced load per lane); each source voxel is
+    // decoded / converted / chained ONCE and replicated K times in registers, and the same
+    // registers are stored to every destination row of the task's rectangle.  Loads of all
+    // NSLOT instructions are issued unconditionally (clamped into the row) before any store.
+    // Measured (512^3 -> 1024^3 UInt16 identity): 0.35 ms = 6.9 TB/s; a half-strided store
+    // layout (2 x 16 B per lane) ran at 2.6 TB/s.
+    //
+    // MODE 0: identity codes (verified on the host for every code); MODE 1: convert each
+    // source code; MODE 2: "Linear" with float semantics -- the reference's sampleLinear
+    // chain lerp(lerp(lerp(v000,v100,0),lerp(v010,v110,0),0), lerp(...), 0) over the
+    // neighbours (x+1 = next voxel in memory, y+1 / z+1 clamped), evaluated per SOURCE voxel.
+    template <int BPVS, int BPVD, int K, int MODE, int FS, int FD, int NSLOT>
+    __global__ __launch_bounds__(kBlock) void resampleRowKernel(ResampleArgs a)
+    {
+        constexpr int V = 16 / BPVD;
+        constexpr int N = V / K;
+        constexpr int kInstr = 64 * V;
+        int const lane = threadIdx.x & 63;
+        uint32_t const wavesPerBlock = blockDim.x >> 6;
+        // wave-uniform task index in SGPRs
+        uint32_t const wave = __builtin_amdgcn_readfirstlane(xcdSwizzle(blockIdx.x, gridDim.x) * wavesPerBlock +
+                                                             (threadIdx.x >> 6));
+        uint32_t const totalWaves = gridDim.x * wavesPerBlock;
+        int32_t const instrPerRow = (a.ddx + kInstr - 1) / kInstr;
+        // Task order.  Replication/conversion: y fastest (the write stream sweeps each plane).
+        // Chain: bands of kBand source rows, then z, then y within the band -- the workgroup
+        // that handles plane sz+1 of a band runs right after the one for plane sz on the same
+        // XCD (xcdSwizzle), so the z+1 neighbour rows are still in L2 (otherwise they were
+        // evicted and re-read from HBM: 2x source traffic measured).
+        uint32_t const kBand = MODE == 2 ? static_cast<uint32_t>(a.band) : 0u;
+        uint32_t const nY = static_cast<uint32_t>(a.nRunsY), nZ = static_cast<uint32_t>(a.nRunsZ);
+        uint32_t const tasks = kBand ? (nY + kBand - 1) / kBand * kBand * nZ : nY * nZ;
+
+        for (uint32_t t = wave; t < tasks; t += totalWaves)
+        {
+            uint32_t iy, iz;
+            if (kBand)
+            {
+                uint32_t const rest = t / kBand;
+                iz = rest % nZ;
+                iy = (rest / nZ) * kBand + t % kBand;
+                if (iy >= nY)
+                    continue;
+            }
+            else
+            {
+                iy = t % nY;
+                iz = t / nY;
+            }
+            Run const ry = runY(a, iy);
+            Run const rz = runZ(a, iz);
+            uint64_t const r00 = srcRowIndex(a, ry.s, rz.s);
+            uint64_t r10 = 0, r01 = 0, r11 = 0;
+            if constexpr (MODE == 2)
+            {
+                int32_t const hy = ry.s + 1 < a.sdy ? ry.s + 1 : a.sdy - 1;
+                int32_t const hz = rz.s + 1 < a.srcGlobalDz ? rz.s + 1 : a.srcGlobalDz - 1;
+                r10 = srcRowIndex(a, hy, rz.s);
+                r01 = srcRowIndex(a, ry.s, hz);
+                r11 = srcRowIndex(a, hy, hz);
+            }
+            for (int32_t g0 = 0; g0 < instrPerRow; g0 += NSLOT)
+            {
+                uint32_t code[NSLOT][V];
+                bool active[NSLOT];
+#pragma unroll
+                for (int u = 0; u < NSLOT; ++u)
+                {
+                    int32_t dx = kInstr * (g0 + u) + V * lane;
+                    active[u] = g0 + u < instrPerRow && dx < a.ddx;
+                    dx = dx < a.ddx ? dx : a.ddx - V;
+                    uint64_t const sx = static_cast<uint64_t>(dx / K);
+                    uint32_t sc[N];
+                    loadN<BPVS, N, true>(a.src, r00 + sx, sc);
+                    if constexpr (MODE == 1)
+                    {
+#pragma unroll
+                        for (int i = 0; i < N; ++i)
+                            sc[i] = convertCode<FS, FD>(sc[i], a);
+                    }
+                    else if constexpr (MODE == 2)
+                    {
+                        uint32_t c10[N], c01[N], c11[N];
+                        loadN<BPVS, N, true>(a.src, r10 + sx, c10);
+                        loadN<BPVS, N, true>(a.src, r01 + sx, c01);
+                        loadN<BPVS, N, true>(a.src, r11 + sx, c11);
+                        // x+1 neighbour of the lane's last voxel = the next lane's first voxel:
+                        // wave64 shuffle; lane 63 and the row's last group (whose neighbour is
+                        // the next row's first voxel, or past the buffer end) read it directly.
+                        uint32_t e00 = __shfl_down(sc[0], 1), e10 = __shfl_down(c10[0], 1);
+                        uint32_t e01 = __shfl_down(c01[0], 1), e11 = __shfl_down(c11[0], 1);
+                        if (lane == 63 || dx + V >= a.ddx)
+                        {
+                            uint64_t const last = a.srcVoxels - 1;   // reference reads past the end: clamp
+                            auto flat = [&](uint64_t i) { return loadCode<BPVS>(a.src, i < last ? i : last); };
+                            e00 = flat(r00 + sx + N);
+                            e10 = flat(r10 + sx + N);
+                            e01 = flat(r01 + sx + N);
+                            e11 = flat(r11 + sx + N);
+                        }
+                        int32_t const fs = FS == -1 ? a.fs : FS;
+                        auto dec = [&](uint32_t c) { return codec::decode(c, fs, a.slo, a.shi); };
+                        float const f = 0.f;   // every fraction of sampleLinear(int,int,int) is 0
+                        uint32_t out[N];
+#pragma unroll
+                        for (int i = 0; i < N; ++i)
+                        {
+                            float v0 = dec(sc[i]), v1 = dec(i + 1 < N ? sc[i + 1] : e00);
+                            float v2 = dec(c10[i]), v3 = dec(i + 1 < N ? c10[i + 1] : e10);
+                            float v4 = dec(c01[i]), v5 = dec(i + 1 < N ? c01[i + 1] : e01);
+                            float v6 = dec(c11[i]), v7 = dec(i + 1 < N ? c11[i + 1] : e11);
+                            float value = codec::lerp(codec::lerp(codec::lerp(v0, v1, f), codec::lerp(v2, v3, f), f),
+                                                      codec::lerp(codec::lerp(v4, v5, f), codec::lerp(v6, v7, f), f), f);
+                            bool w;
+                            out[i] = codec::encode(value, FD == -1 ? a.fd : FD, a.dm, w);
+                        }
+#pragma unroll
+                        for (int i = 0; i < N; ++i)
+                            sc[i] = out[i];
+                    }
+#pragma unroll
+                    for (int i = 0; i < V; ++i)
+                        code[u][i] = sc[i / K];
+                }
+                for (int32_t zd = rz.d0; zd < rz.d1; ++zd)
+                    for (int32_t yd = ry.d0; yd < ry.d1; ++yd)
+                    {
+                        uint64_t const drow = dstRowIndex(a, yd, zd) + static_cast<uint64_t>(V) * lane;
+#pragma unroll
+                        for (int u = 0; u < NSLOT; ++u)
+                            if (active[u])
+                                store16<BPVD>(a.dst, drow + static_cast<uint64_t>(kInstr) * (g0 + u), code[u]);
+                    }
+            }
+        }
+    }
+
+
+    // Row-kernel launchers, one translation unit per MODE (0 identity, 1 convert, 2 chain).
+    // k: integer x ratio; instrPerRow: 64-lane 16-byte store instructions per dst row.
+    void launchRowMode0(ResampleArgs const& a, int32_t k, uint32_t bpv, unsigned grid, int32_t instrPerRow,
+                        hipStream_t s);
+    void launchRowMode1(ResampleArgs const& a, int32_t k, uint32_t bpv, int32_t fs, int32_t fd, unsigned grid,
+                        int32_t instrPerRow, hipStream_t s);
+    void launchRowMode2(ResampleArgs const& a, int32_t k, uint32_t bpvd, unsigned grid, int32_t instrPerRow,
+                        hipStream_t s);
+
+    template <int BPVS, int BPVD, int MODE, int FS, int FD>
+    void launchRowK(ResampleArgs const& a, int32_t k, unsigned grid, int32_t instrPerRow, hipStream_t s)
+    {
+#define VKT_ROW_NS(K)                                                                                        \
+    do {                                                                                                     \
+        if (instrPerRow == 1)                                                                                \
+            hipLaunchKernelGGL((resampleRowKernel<BPVS, BPVD, K, MODE, FS, FD, 1>), dim3(grid), dim3(kBlock), 0, s, a); \
+        else if (instrPerRow == 2)                                                                           \
+            hipLaunchKernelGGL((resampleRowKernel<BPVS, BPVD, K, MODE, FS, FD, 2>), dim3(grid), dim3(kBlock), 0, s, a); \
+        else                                                                                                 \
+            hipLaunchKernelGGL((resampleRowKernel<BPVS, BPVD, K, MODE, FS, FD, 4>), dim3(grid), dim3(kBlock), 0, s, a); \
+    } while (0)
+        if (k == 1)
+        {
+            if constexpr ((16 / BPVD) * BPVS <= 32)
+                VKT_ROW_NS(1);
+        }
+        else if (k == 2)
+            VKT_ROW_NS(2);
+        else
+            VKT_ROW_NS(4);
+#undef VKT_ROW_NS
+    }
+
+} // hipk
+} // vkt

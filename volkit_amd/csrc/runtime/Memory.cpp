@@ -16,8 +16,11 @@
 #include "Runtime.hpp"
 #include "volkit_hip.h"
 
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
+#include <unordered_set>
 
 namespace vkt
 {
@@ -30,6 +33,16 @@ namespace hipk
 namespace
 {
     bool onGpu(ExecutionPolicy const& p) { return p.device == ExecutionPolicy::Device::GPU; }
+
+    // Optional pinned (page-locked) host allocations for CPU-policy buffers: migrations then
+    // DMA straight from/to the user's buffer instead of through HIP's pageable staging.
+    std::atomic<int> gPinnedHost{0};
+    std::mutex gPinnedMutex;
+    std::unordered_set<void*>& pinnedSet()
+    {
+        static auto* s = new std::unordered_set<void*>;
+        return *s;
+    }
 
     // Copy stream waits for the compute stream's current tail.
     vktError copyStreamAfterCompute()
@@ -103,6 +116,16 @@ namespace detail
                 return nullptr;
             return p;
         }
+        if (gPinnedHost.load())
+        {
+            void* p = nullptr;
+            if (rt::check(hipHostMalloc(&p, bytes, hipHostMallocDefault), "hipHostMalloc") == vktNoError)
+            {
+                std::lock_guard<std::mutex> lock(gPinnedMutex);
+                pinnedSet().insert(p);
+                return p;
+            }
+        }
         void* p = std::malloc(bytes);
         if (p == nullptr)
             rt::fail("Allocate: host malloc failed");
@@ -114,9 +137,21 @@ namespace detail
         if (data == nullptr)
             return;
         if (onGpu(owner))
+        {
             (void)rt::check(hipFree(data), "hipFree");
-        else
-            std::free(data);
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> lock(gPinnedMutex);
+            auto it = pinnedSet().find(data);
+            if (it != pinnedSet().end())
+            {
+                pinnedSet().erase(it);
+                (void)rt::check(hipHostFree(data), "hipHostFree");
+                return;
+            }
+        }
+        std::free(data);
     }
 
     void CopyOn(void* dst, void const* src, std::size_t bytes, ExecutionPolicy const& owner)
@@ -199,6 +234,12 @@ vktError vktHipFree(void* ptr)
 vktError vktHipMemcpy(void* dst, void const* src, size_t size, vktCopyKind ck)
 {
     return vkt::detail::memcpyHip(dst, src, size, static_cast<vkt::CopyKind>(ck));
+}
+
+vktError vktHipSetPinnedHostAllocation(int32_t enable)
+{
+    vkt::gPinnedHost.store(enable != 0);
+    return vktNoError;
 }
 
 vktError vktHipMemsetRange(void* dst, void const* pattern, size_t dstSize, size_t patternSize)
