@@ -33,7 +33,7 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--dst", type=int, default=1024, help="per-GPU dst cube edge (source = dst/2)")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-dst", type=int, default=512, help="dst edge of the CPU-baseline sample")
+    p.add_argument("--cpu-dst", type=int, default=768, help="dst edge of the CPU-baseline sample")
     p.add_argument("--dist-backend", default="nccl",
                    help="torch.distributed backend for N>1 (nccl = RCCL over xGMI; gloo only for rehearsal)")
     p.add_argument("--rehearse-one-device", action="store_true",
