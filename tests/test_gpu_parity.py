@@ -293,3 +293,31 @@ def test_resample_vector_gather_and_row_chain(g, o, sfmt, dfmt):
                 out = g.resample(dfmt, dmap, dd, sfmt, smap, src, fm)
                 ref = o.resample(dfmt, dmap, dd, sfmt, smap, src, fm)
                 assert_codes_equal(out, ref, dfmt, f"resample {sd}->{dd} {sfmt}->{dfmt} fm={fm} {smap}->{dmap}")
+
+
+@pytest.mark.parametrize("dfmt", [7, 5])
+def test_resample_chain_sparse_specials(g, o, dfmt):
+    """Float32 "Linear" with mostly finite data: clean source rows take the conversion path
+    (no neighbour reads), rows near a non-finite value or a -0 take the lerp chain.  Specials
+    sit where the chain's neighbourhood crosses rows: a row's first voxel (hi.x of the row
+    before), the y+1 / z+1 neighbour rows, the last voxel of the buffer (clamped hi.x)."""
+    rng = np.random.default_rng(99 + dfmt)
+    for sd, dd in (((64, 32, 8), (128, 64, 16)), ((64, 16, 6), (64, 32, 12)), ((32, 8, 4), (128, 32, 16))):
+        sx, sy, sz = sd
+        vals = rng.uniform(0.0, 1.0, size=(sz, sy, sx)).astype(np.float32)
+        cases = [
+            [],                                            # all clean
+            [((1, 3, 0), np.inf)],                         # first voxel of a row: hi.x of row (2,1)
+            [((2, 5, 7), -0.0)],                           # -0 as v000
+            [((sz - 1, sy - 1, sx - 1), np.nan)],          # last voxel: clamped hi.x read
+            [((0, 0, 5), -np.inf), ((sz - 1, 0, 0), np.nan), ((3, sy - 1, sx - 1), -0.0)],
+        ]
+        for specials in cases:
+            v = vals.copy()
+            for (z, y, x), val in specials:
+                v[z, y, x] = val
+            src = v.view(np.uint32)
+            for dmap in ((0.0, 1.0), (-1.0, 3.0)):
+                out = g.resample(dfmt, dmap, dd, 7, (0.0, 1.0), src, 1)
+                ref = o.resample(dfmt, dmap, dd, 7, (0.0, 1.0), src, 1)
+                assert_codes_equal(out, ref, dfmt, f"chain {sd}->{dd} specials={specials} dmap={dmap}")

@@ -29,6 +29,7 @@
 #include <cstdlib>
 #include <map>
 #include <mutex>
+#include <string>
 #include <tuple>
 #include <vector>
 
@@ -169,6 +170,63 @@ namespace hipk
         }
     }
 
+    // ---- Float32 "Linear": which source rows can make the chain differ from v000 ------
+    // One wave per local source row; byte r of `dirty` = the row holds a non-finite value or
+    // a -0 (chainSensitive).  One streaming read of the source (N_src * 4 bytes) lets the
+    // row kernel skip the three neighbour-row reads for every clean task.
+    template <bool VEC>
+    __global__ __launch_bounds__(kBlock) void rowDirtyKernel(uint8_t const* src, int32_t sdx, uint64_t rows,
+                                                             uint8_t* dirty)
+    {
+        int const lane = threadIdx.x & 63;
+        uint64_t const row = static_cast<uint64_t>(blockIdx.x) * (kBlock / 64) + (threadIdx.x >> 6);
+        if (row >= rows)
+            return;
+        uint32_t const* p = reinterpret_cast<uint32_t const*>(src) + row * static_cast<uint64_t>(sdx);
+        bool d = false;
+        if constexpr (VEC)
+        {
+            for (int32_t x = 4 * lane; x < sdx; x += 256)
+            {
+                u32x4 v = __builtin_nontemporal_load(reinterpret_cast<u32x4 const*>(p + x));
+                d = d || chainSensitive(v.x) || chainSensitive(v.y) || chainSensitive(v.z) || chainSensitive(v.w);
+            }
+        }
+        else
+        {
+            for (int32_t x = lane; x < sdx; x += 64)
+                d = d || chainSensitive(p[x]);
+        }
+        uint64_t const any = __ballot(d);
+        if (lane == 0)
+            dirty[row] = any != 0;
+    }
+
+    // rowChain[r] = OR of rowDirty over the rows the chain of row r's voxels reads:
+    // (y,z), (y+1,z), (y,z+1), (y+1,z+1) -- y+1 / z+1 clamped like sampleLinear -- and the
+    // row after each in memory (hi.x of the last voxel).  Indices are clamped into the local
+    // buffer; rows whose neighbourhood leaves it are never read by a task (slab precondition).
+    __global__ __launch_bounds__(kBlock) void rowChainKernel(uint8_t const* dirty, int32_t sdy, int32_t sdz,
+                                                            int32_t srcZ0, int32_t srcGlobalDz, uint8_t* chain)
+    {
+        uint64_t const rows = static_cast<uint64_t>(sdy) * static_cast<uint64_t>(sdz);
+        uint64_t const r = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+        if (r >= rows)
+            return;
+        int32_t const y = static_cast<int32_t>(r % static_cast<uint64_t>(sdy));
+        int32_t const zl = static_cast<int32_t>(r / static_cast<uint64_t>(sdy));
+        int32_t const hy = y + 1 < sdy ? y + 1 : sdy - 1;
+        int32_t const zg = srcZ0 + zl;
+        int32_t const hzl = (zg + 1 < srcGlobalDz ? zg + 1 : srcGlobalDz - 1) - srcZ0;
+        uint64_t const last = rows - 1;
+        auto at = [&](int32_t yy, int32_t zz) {
+            uint64_t i = static_cast<uint64_t>(zz) * static_cast<uint64_t>(sdy) + static_cast<uint64_t>(yy);
+            i = i < last ? i : last;
+            return dirty[i] | dirty[i < last ? i + 1 : last];
+        };
+        chain[r] = (at(y, zl) | at(hy, zl) | at(y, hzl) | at(hy, hzl)) != 0;
+    }
+
     // ---- host planning -------------------------------------------------------------
     std::vector<Run> buildRuns(int32_t dstBegin, int32_t dstEnd, int32_t dd, int32_t sd)
     {
@@ -208,6 +266,7 @@ namespace hipk
         Run const* runsY = nullptr;
         Run const* runsZ = nullptr;
         int32_t const* xtab = nullptr;
+        int32_t const* zsrc = nullptr;   // source plane of every local dst plane
         int32_t aff[2][6] = {{0, 0, 0, 0, 0, 0}, {0, 0, 0, 0, 0, 0}};   // {aff, sa, da, dl, s0, d0}
     };
 
@@ -278,16 +337,20 @@ namespace hipk
         t.maxSz = rz.empty() ? -1 : rz.back().s;
         // layout: x table first (16-byte aligned for vector reads, padded to 4 entries), runs after
         size_t xwords = (xt.size() + 3) / 4 * 4;
-        size_t words = xwords + 3 * ry.size() + 3 * rz.size();
+        size_t words = xwords + 3 * ry.size() + 3 * rz.size() + static_cast<size_t>(dnz);
         std::vector<int32_t> host(xt.begin(), xt.end());
         host.resize(xwords, 0);
         for (Run const& r : ry) host.insert(host.end(), {r.s, r.d0, r.d1});
         for (Run const& r : rz) host.insert(host.end(), {r.s, r.d0, r.d1});
+        for (Run const& r : rz)
+            for (int32_t d = r.d0; d < r.d1; ++d)
+                host.push_back(r.s);
         VKT_HIP_TRY(hipMalloc(&t.dev, words * sizeof(int32_t) + 16));
         VKT_HIP_TRY(hipMemcpy(t.dev, host.data(), words * sizeof(int32_t), hipMemcpyHostToDevice));
         t.xtab = t.dev;
         t.runsY = reinterpret_cast<Run const*>(t.dev + xwords);
         t.runsZ = reinterpret_cast<Run const*>(t.dev + xwords + 3 * ry.size());
+        t.zsrc = t.dev + xwords + 3 * ry.size() + 3 * rz.size();
         cache[{dev, key}] = t;
         out = t;
         return vktNoError;
@@ -375,7 +438,38 @@ namespace hipk
         {
             if (src.dataFormat != codec::FmtFloat32 || (bd == 1 && k == 1))
                 return false;   // per-dst-voxel chain kernel handles these
-            launchRowMode2(a, k, bd, grid, instrPerRow, s);
+            ResampleArgs b = a;
+            b.srcRows = static_cast<uint64_t>(src.dimY) * static_cast<uint64_t>(src.dimZ);
+            uint8_t* dirty = nullptr;
+            // stream-ordered pool allocation: no device-wide sync, freed behind the launch
+            // (rowDirty, then rowChain for the plane layout)
+            if (hipMallocAsync(reinterpret_cast<void**>(&dirty), 2 * b.srcRows, s) != hipSuccess)
+            {
+                (void)hipGetLastError();
+                dirty = nullptr;   // fall back to the chain for every task (still exact)
+            }
+            if (dirty)
+            {
+                unsigned const g = static_cast<unsigned>((b.srcRows + kBlock / 64 - 1) / (kBlock / 64));
+                bool const vec = src.dimX % 4 == 0;   // base is 16-B aligned (checked above)
+                if (vec)
+                    hipLaunchKernelGGL(rowDirtyKernel<true>, dim3(g), dim3(kBlock), 0, s, src.data, src.dimX, b.srcRows,
+                                       dirty);
+                else
+                    hipLaunchKernelGGL(rowDirtyKernel<false>, dim3(g), dim3(kBlock), 0, s, src.data, src.dimX,
+                                       b.srcRows, dirty);
+                b.rowDirty = dirty;
+                if (b.planeLayout)
+                {
+                    unsigned const gc = static_cast<unsigned>((b.srcRows + kBlock - 1) / kBlock);
+                    hipLaunchKernelGGL(rowChainKernel, dim3(gc), dim3(kBlock), 0, s, dirty, src.dimY, src.dimZ, a.srcZ0,
+                                       a.srcGlobalDz, dirty + b.srcRows);
+                    b.rowChain = dirty + b.srcRows;
+                }
+            }
+            launchRowMode2(b, k, bd, grid, instrPerRow, s);
+            if (dirty)
+                (void)hipFreeAsync(dirty, s);
             return true;
         }
         if (bs != bd)
@@ -458,6 +552,28 @@ namespace hipk
         a.affZ = t.aff[1][0]; a.saZ = t.aff[1][1]; a.daZ = t.aff[1][2]; a.dlZ = t.aff[1][3];
         a.s0Z = t.aff[1][4]; a.d0Z = t.aff[1][5];
         a.k = t.k;
+        a.zsrc = t.zsrc;
+        a.dnz = dst.dimZ;
+        {
+            static int const layout = [] {
+                char const* e = std::getenv("VKT_RESAMPLE_LAYOUT");   // A/B tuning knob
+                return e && std::string(e) == "row" ? 0 : 1;
+            }();
+            a.planeLayout = layout;
+        }
+        {
+            uint32_t const bdv = codec::bytesPerVoxel(dst.dataFormat);
+            uint32_t const vv = bdv <= 4 ? 16 / bdv : 1;
+            uint32_t const instr = static_cast<uint32_t>((static_cast<uint64_t>(dst.dimX) + 64 * vv - 1) / (64 * vv));
+            a.fdInstr = makeFastDiv(instr);
+            a.fdRunsY = makeFastDiv(static_cast<uint32_t>(t.nRunsY));
+            // plane layout computes the z run arithmetically only for contiguous affine runs
+            if (t.aff[1][0] && t.aff[1][2] != t.aff[1][3])
+                a.affZ = 0;
+            a.fdDaZ = makeFastDiv(static_cast<uint32_t>(a.affZ ? a.daZ : 1));
+            if (static_cast<uint64_t>(dst.dimZ) * static_cast<uint64_t>(t.nRunsY) * instr >= (1ull << 32))
+                a.planeLayout = 0;
+        }
         {
             // chain task order: bands of 8 rows (measured: equal time, 1.6x less HBM re-reading)
             a.band = 8;

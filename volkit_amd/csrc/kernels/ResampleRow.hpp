@@ -51,7 +51,29 @@ namespace hipk
         MapParams dm;
         uint64_t srcVoxels;        // voxels in the local source buffer (flat-read clamp)
         int32_t srcIsGlobalEnd;    // local buffer ends at the global end (clamp there)
+        // MODE 2 only: one byte per local source row, nonzero if the row holds a value that
+        // can make the lerp chain differ from its first term (non-finite, or -0); nullptr =
+        // evaluate the chain everywhere.  Built by rowDirtyKernel just before the launch.
+        uint8_t const* rowDirty;
+        uint64_t srcRows;          // local source rows (sdy * sdz)
+        // plane-linear layout (resamplePlaneKernel): source plane (global) of every local dst
+        // plane, and the dst slab depth
+        int32_t const* zsrc;       // device, dnz entries
+        int32_t dnz;
+        int32_t planeLayout;       // 1: resamplePlaneKernel, 0: resampleRowKernel
+        FastDiv fdInstr, fdRunsY, fdDaZ;   // task decomposition without integer division
+        // MODE 2, plane layout: one byte per local source row r, nonzero if the chain of a
+        // voxel in row r can differ from v000 (OR of rowDirty over the rows its chain reads);
+        // built from rowDirty by rowChainKernel.  nullptr = chain everywhere.
+        uint8_t const* rowChain;
     };
+
+    // A Float32 code that can make lerp(a, b, 0) = a + 0*b differ from a: b non-finite
+    // (0*b = NaN) or a == -0 (-0 + +0 = +0).
+    __device__ __forceinline__ bool chainSensitive(uint32_t bits)
+    {
+        return (bits & 0x7F800000u) == 0x7F800000u || bits == 0x80000000u;
+    }
 
     __device__ __forceinline__ Run runY(ResampleArgs const& a, uint32_t i)
     {
@@ -150,6 +172,7 @@ namespace hipk
             Run const rz = runZ(a, iz);
             uint64_t const r00 = srcRowIndex(a, ry.s, rz.s);
             uint64_t r10 = 0, r01 = 0, r11 = 0;
+            bool chainTask = false;   // wave-uniform
             if constexpr (MODE == 2)
             {
                 int32_t const hy = ry.s + 1 < a.sdy ? ry.s + 1 : a.sdy - 1;
@@ -157,6 +180,21 @@ namespace hipk
                 r10 = srcRowIndex(a, hy, rz.s);
                 r01 = srcRowIndex(a, ry.s, hz);
                 r11 = srcRowIndex(a, hy, hz);
+                chainTask = true;
+                if (a.rowDirty)
+                {
+                    // The chain of a voxel reads rows r00, r10, r01, r11 and, for the row's
+                    // last voxel, the first voxel of the row after each in memory (clamped to
+                    // the buffer's last voxel, i.e. its own row, at the end).  If none of
+                    // them holds a sensitive value, every 0*neighbour term is +-0 and the
+                    // chain returns v000 exactly: plain conversion, no neighbour reads.
+                    uint64_t const lastRow = a.srcRows - 1;
+                    uint64_t const sdx = static_cast<uint64_t>(a.sdx);
+                    uint32_t dirty = 0;
+                    for (uint64_t r : {r00 / sdx, r10 / sdx, r01 / sdx, r11 / sdx})
+                        dirty |= a.rowDirty[r] | a.rowDirty[r < lastRow ? r + 1 : lastRow];
+                    chainTask = __builtin_amdgcn_readfirstlane(dirty) != 0;
+                }
             }
             for (int32_t g0 = 0; g0 < instrPerRow; g0 += NSLOT)
             {
@@ -179,6 +217,14 @@ namespace hipk
                     }
                     else if constexpr (MODE == 2)
                     {
+                      if (!chainTask)
+                      {
+#pragma unroll
+                        for (int i = 0; i < N; ++i)
+                            sc[i] = convertCode<FS, FD>(sc[i], a);
+                      }
+                      else
+                      {
                         uint32_t c10[N], c01[N], c11[N];
                         loadN<BPVS, N, true>(a.src, r10 + sx, c10);
                         loadN<BPVS, N, true>(a.src, r01 + sx, c01);
@@ -216,6 +262,7 @@ namespace hipk
 #pragma unroll
                         for (int i = 0; i < N; ++i)
                             sc[i] = out[i];
+                      }
                     }
 #pragma unroll
                     for (int i = 0; i < V; ++i)
@@ -235,6 +282,126 @@ namespace hipk
     }
 
 
+    // ---- plane-linear variant: the write stream sweeps the destination in memory order ----
+    // One wave (and one 64-thread workgroup) per task = (dst plane, source-row run in y, one
+    // 64-lane store instruction of x): it loads the N = V/K source voxels per lane that feed
+    // its 64*V destination voxels, converts / chains them once, and stores the instruction
+    // into every dst row of the y run (K_y rows of ONE plane).  Tasks are numbered x-fastest,
+    // then y, then dst plane, so the grid writes memory in order; a source row is re-read by
+    // the tasks of each dst plane it feeds (from L2 / MALL, not HBM: the source plane is
+    // re-used within one dst plane's sweep).  Measured on 1024^3 -> 2048^3 Float32 (tools/
+    // kbench6): 5.9 ms vs 7.4 ms for the source-row-rectangle layout -- many short one-wave
+    // workgroups writing 2 KiB each keep more store streams in flight per channel than long
+    // waves writing 32 KiB into 4 rows of 2 planes.
+    template <int BPVS, int BPVD, int K, int MODE, int FS, int FD>
+    __global__ __launch_bounds__(64) void resamplePlaneKernel(ResampleArgs a)
+    {
+        constexpr int V = 16 / BPVD;
+        constexpr int N = V / K;
+        constexpr int kInstr = 64 * V;
+        int const lane = threadIdx.x & 63;
+        uint32_t const instrPerRow = a.fdInstr.d;
+        uint32_t const nY = a.fdRunsY.d;
+        // < 2^32 (checked on the host)
+        uint32_t const tasks = static_cast<uint32_t>(a.dnz) * nY * instrPerRow;
+        for (uint32_t t = blockIdx.x; t < tasks; t += gridDim.x)
+        {
+            // all task math is wave-uniform (scalar unit); no dependent table load before the
+            // source load when the z runs are affine
+            uint32_t const rest = fdiv(t, a.fdInstr);
+            uint32_t const g = t - rest * instrPerRow;
+            uint32_t const zlu = fdiv(rest, a.fdRunsY);
+            uint32_t const iy = rest - zlu * nY;
+            int32_t const zl = static_cast<int32_t>(zlu);           // local dst plane
+            Run const ry = runY(a, iy);
+            int32_t sz;                                             // global source plane
+            if (a.affZ)
+                sz = a.s0Z + a.saZ * static_cast<int32_t>(fdiv(static_cast<uint32_t>(a.dstZ0 + zl - a.d0Z), a.fdDaZ));
+            else
+                sz = a.zsrc[zl];
+            uint64_t const r00 = srcRowIndex(a, ry.s, sz);
+            int32_t dx = kInstr * static_cast<int32_t>(g) + V * lane;
+            bool const active = dx < a.ddx;
+            dx = active ? dx : a.ddx - V;
+            uint64_t const sx = static_cast<uint64_t>(dx / K);
+            uint32_t sc[N];
+            loadN<BPVS, N, true>(a.src, r00 + sx, sc);
+            if constexpr (MODE == 1)
+            {
+#pragma unroll
+                for (int i = 0; i < N; ++i)
+                    sc[i] = convertCode<FS, FD>(sc[i], a);
+            }
+            else if constexpr (MODE == 2)
+            {
+                int32_t const hy = ry.s + 1 < a.sdy ? ry.s + 1 : a.sdy - 1;
+                int32_t const hz = sz + 1 < a.srcGlobalDz ? sz + 1 : a.srcGlobalDz - 1;
+                uint64_t const r10 = srcRowIndex(a, hy, sz), r01 = srcRowIndex(a, ry.s, hz);
+                uint64_t const r11 = srcRowIndex(a, hy, hz);
+                bool chainTask = true;
+                if (a.rowChain)
+                {
+                    uint64_t const row = static_cast<uint64_t>(sz - a.srcZ0) * static_cast<uint64_t>(a.sdy) +
+                                         static_cast<uint64_t>(ry.s);
+                    chainTask = __builtin_amdgcn_readfirstlane(a.rowChain[row]) != 0;
+                }
+                if (!chainTask)
+                {
+#pragma unroll
+                    for (int i = 0; i < N; ++i)
+                        sc[i] = convertCode<FS, FD>(sc[i], a);
+                }
+                else
+                {
+                    uint32_t c10[N], c01[N], c11[N];
+                    loadN<BPVS, N, true>(a.src, r10 + sx, c10);
+                    loadN<BPVS, N, true>(a.src, r01 + sx, c01);
+                    loadN<BPVS, N, true>(a.src, r11 + sx, c11);
+                    uint32_t e00 = __shfl_down(sc[0], 1), e10 = __shfl_down(c10[0], 1);
+                    uint32_t e01 = __shfl_down(c01[0], 1), e11 = __shfl_down(c11[0], 1);
+                    if (lane == 63 || dx + V >= a.ddx)
+                    {
+                        uint64_t const last = a.srcVoxels - 1;   // reference reads past the end: clamp
+                        auto flat = [&](uint64_t i) { return loadCode<BPVS>(a.src, i < last ? i : last); };
+                        e00 = flat(r00 + sx + N);
+                        e10 = flat(r10 + sx + N);
+                        e01 = flat(r01 + sx + N);
+                        e11 = flat(r11 + sx + N);
+                    }
+                    int32_t const fs = FS == -1 ? a.fs : FS;
+                    auto dec = [&](uint32_t c) { return codec::decode(c, fs, a.slo, a.shi); };
+                    float const f = 0.f;   // every fraction of sampleLinear(int,int,int) is 0
+                    uint32_t out[N];
+#pragma unroll
+                    for (int i = 0; i < N; ++i)
+                    {
+                        float v0 = dec(sc[i]), v1 = dec(i + 1 < N ? sc[i + 1] : e00);
+                        float v2 = dec(c10[i]), v3 = dec(i + 1 < N ? c10[i + 1] : e10);
+                        float v4 = dec(c01[i]), v5 = dec(i + 1 < N ? c01[i + 1] : e01);
+                        float v6 = dec(c11[i]), v7 = dec(i + 1 < N ? c11[i + 1] : e11);
+                        float value = codec::lerp(codec::lerp(codec::lerp(v0, v1, f), codec::lerp(v2, v3, f), f),
+                                                  codec::lerp(codec::lerp(v4, v5, f), codec::lerp(v6, v7, f), f), f);
+                        bool w;
+                        out[i] = codec::encode(value, FD == -1 ? a.fd : FD, a.dm, w);
+                    }
+#pragma unroll
+                    for (int i = 0; i < N; ++i)
+                        sc[i] = out[i];
+                }
+            }
+            uint32_t code[V];
+#pragma unroll
+            for (int i = 0; i < V; ++i)
+                code[i] = sc[i / K];
+            if (active)
+            {
+                int32_t const zd = a.dstZ0 + zl;
+                for (int32_t yd = ry.d0; yd < ry.d1; ++yd)
+                    store16<BPVD>(a.dst, dstRowIndex(a, yd, zd) + static_cast<uint64_t>(dx), code);
+            }
+        }
+    }
+
     // Row-kernel launchers, one translation unit per MODE (0 identity, 1 convert, 2 chain).
     // k: integer x ratio; instrPerRow: 64-lane 16-byte store instructions per dst row.
     void launchRowMode0(ResampleArgs const& a, int32_t k, uint32_t bpv, unsigned grid, int32_t instrPerRow,
@@ -249,7 +416,13 @@ namespace hipk
     {
 #define VKT_ROW_NS(K)                                                                                        \
     do {                                                                                                     \
-        if (instrPerRow == 1)                                                                                \
+        if (a.planeLayout)                                                                                   \
+        {                                                                                                    \
+            uint64_t const tasks = static_cast<uint64_t>(a.dnz) * a.nRunsY * instrPerRow;                    \
+            unsigned const g = static_cast<unsigned>(tasks < (1u << 30) ? tasks : (1u << 30));               \
+            hipLaunchKernelGGL((resamplePlaneKernel<BPVS, BPVD, K, MODE, FS, FD>), dim3(g), dim3(64), 0, s, a); \
+        }                                                                                                    \
+        else if (instrPerRow == 1)                                                                                \
             hipLaunchKernelGGL((resampleRowKernel<BPVS, BPVD, K, MODE, FS, FD, 1>), dim3(grid), dim3(kBlock), 0, s, a); \
         else if (instrPerRow == 2)                                                                           \
             hipLaunchKernelGGL((resampleRowKernel<BPVS, BPVD, K, MODE, FS, FD, 2>), dim3(grid), dim3(kBlock), 0, s, a); \
