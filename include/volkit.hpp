@@ -17,6 +17,7 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <memory>
 
 #ifndef VKTAPI
 #define VKTAPI __attribute__((visibility("default")))
@@ -382,5 +383,114 @@ namespace vkt
     //--- Resample.hpp (reference include/cpp/vkt/Resample.hpp:14-31, SV->SV) ------------
     enum class FilterMode { Nearest, Linear };
     VKTAPI Error Resample(StructuredVolume& dst, StructuredVolume& src, FilterMode fm);
+
+    //--- Array3D<T> (reference include/cpp/vkt/Array3D.hpp:14-143) -------------------------
+    // Dense x-fastest 3-D array with the reference's interface.  Deviation by design: the
+    // element array itself lives on the HOST (it holds handles / small metadata), elements
+    // are constructed and destroyed properly, and copies are deep.  The reference derives it
+    // from ManagedBuffer<T>, which migrates the raw bytes of the elements -- for
+    // Array3D<StructuredVolume> that would move host objects to device memory and then
+    // dereference them on the host.  Each StructuredVolume element migrates its own voxels.
+    template <typename T>
+    class Array3D
+    {
+    public:
+        typedef T value_type;
+        typedef T* iterator;
+        typedef T const* const_iterator;
+
+        Array3D() = default;
+        explicit Array3D(Vec3i const& dims) { resize(dims); }
+        Array3D(Array3D& rhs) { *this = rhs; }
+        Array3D(Array3D&& rhs) noexcept : elems_(std::move(rhs.elems_)), dims_(rhs.dims_) { rhs.dims_ = {0, 0, 0}; }
+        ~Array3D() = default;
+
+        Array3D& operator=(Array3D& rhs)
+        {
+            if (&rhs != this)
+            {
+                resize(rhs.dims_);
+                for (std::size_t i = 0; i < numElements(); ++i)
+                    elems_[i] = rhs.elems_[i];
+            }
+            return *this;
+        }
+
+        Array3D& operator=(Array3D&& rhs) noexcept
+        {
+            if (&rhs != this)
+            {
+                elems_ = std::move(rhs.elems_);
+                dims_ = rhs.dims_;
+                rhs.dims_ = {0, 0, 0};
+            }
+            return *this;
+        }
+
+        //! Re-shape; existing elements are dropped (reference: ManagedBuffer::resize of raw bytes)
+        void resize(Vec3i const& dims)
+        {
+            std::size_t n = count(dims);
+            elems_.reset(n ? new T[n] : nullptr);
+            dims_ = dims;
+        }
+
+        void fill(T& value)
+        {
+            for (std::size_t i = 0; i < numElements(); ++i)
+                elems_[i] = value;
+        }
+        void fill(T const& value) { fill(const_cast<T&>(value)); }
+
+        iterator begin() { return data(); }
+        const_iterator begin() const { return data(); }
+        const_iterator cbegin() { return data(); }
+        iterator end() { return data() + numElements(); }
+        const_iterator end() const { return data() + numElements(); }
+        const_iterator cend() { return data() + numElements(); }
+
+        T& operator[](Vec3i const& index) { return elems_[linear(index)]; }
+        T const& operator[](Vec3i const& index) const { return elems_[linear(index)]; }
+
+        bool empty() const { return numElements() == 0; }
+        T* data() { return elems_.get(); }
+        T const* data() const { return elems_.get(); }
+        Vec3i dims() const { return dims_; }
+        std::size_t numElements() const { return count(dims_); }
+
+    private:
+        static std::size_t count(Vec3i const& d)
+        {
+            return d.x > 0 && d.y > 0 && d.z > 0
+                       ? static_cast<std::size_t>(d.x) * static_cast<std::size_t>(d.y) * static_cast<std::size_t>(d.z)
+                       : 0;
+        }
+        std::size_t linear(Vec3i const& i) const
+        {
+            return (static_cast<std::size_t>(i.z) * static_cast<std::size_t>(dims_.y) + static_cast<std::size_t>(i.y)) *
+                       static_cast<std::size_t>(dims_.x) +
+                   static_cast<std::size_t>(i.x);
+        }
+
+        std::unique_ptr<T[]> elems_;
+        Vec3i dims_ = {0, 0, 0};
+    };
+
+    //--- Decompose.hpp (reference include/cpp/vkt/Decompose.hpp:16-50) -------------------
+    // BrickDecomposeResize allocates the bricks (on the calling thread's device, like any
+    // StructuredVolume); BrickDecompose copies source ranges with halos into them -- one
+    // batched gfx950 launch for all bricks under the GPU policy.
+    VKTAPI Error BrickDecompose(Array3D<StructuredVolume>& dest, StructuredVolume& source, int32_t brickSizeX,
+                                int32_t brickSizeY, int32_t brickSizeZ, int32_t haloSizeNegX = 0,
+                                int32_t haloSizeNegY = 0, int32_t haloSizeNegZ = 0, int32_t haloSizePosX = 0,
+                                int32_t haloSizePosY = 0, int32_t haloSizePosZ = 0);
+    VKTAPI Error BrickDecompose(Array3D<StructuredVolume>& dest, StructuredVolume& source, Vec3i brickSize,
+                                Vec3i haloSizeNeg = {0, 0, 0}, Vec3i haloSizePos = {0, 0, 0});
+    VKTAPI Error BrickDecomposeResize(Array3D<StructuredVolume>& dest, StructuredVolume& source, int32_t brickSizeX,
+                                      int32_t brickSizeY, int32_t brickSizeZ, int32_t haloSizeNegX = 0,
+                                      int32_t haloSizeNegY = 0, int32_t haloSizeNegZ = 0, int32_t haloSizePosX = 0,
+                                      int32_t haloSizePosY = 0, int32_t haloSizePosZ = 0);
+    VKTAPI Error BrickDecomposeResize(Array3D<StructuredVolume>& dest, StructuredVolume& source, Vec3i brickSize,
+                                      Vec3i haloSizeNeg = {0, 0, 0}, Vec3i haloSizePos = {0, 0, 0});
 
 } // vkt

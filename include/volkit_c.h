@@ -216,6 +216,47 @@ VKTAPI vktError vktTransformRangeSV2(vktStructuredVolume volume1, vktStructuredV
 typedef enum { vktFilterModeNearest, vktFilterModeLinear } vktFilterMode;
 VKTAPI vktError vktResampleSV(vktStructuredVolume dst, vktStructuredVolume src, vktFilterMode fm);
 
+/* ---- Array3D.h for vktStructuredVolume (reference include/c/vkt/Array3D.h:18-237) ----
+ * The reference instantiates these as header-inline functions over a ManagedBuffer of
+ * handles; here they are exported functions over a host-resident handle array (see
+ * vkt::Array3D in volkit.hpp).  Ownership: Destroy also destroys every non-NULL volume
+ * handle the array holds (the reference leaks the bricks its examples create). */
+struct vktArray3D_vktStructuredVolume_impl;
+typedef struct vktArray3D_vktStructuredVolume_impl* vktArray3D_vktStructuredVolume;
+typedef vktStructuredVolume vktArray3D_vktStructuredVolume_ValueType;
+typedef vktStructuredVolume* vktArray3D_vktStructuredVolume_Iterator;
+typedef vktStructuredVolume const* vktArray3D_vktStructuredVolume_ConstIterator;
+VKTAPI void vktArray3D_vktStructuredVolume_CreateEmpty(vktArray3D_vktStructuredVolume* arr);
+VKTAPI void vktArray3D_vktStructuredVolume_Create(vktArray3D_vktStructuredVolume* arr, vktVec3i_t dims);
+VKTAPI void vktArray3D_vktStructuredVolume_CreateCopy(vktArray3D_vktStructuredVolume* arr,
+                                                      vktArray3D_vktStructuredVolume rhs);
+VKTAPI void vktArray3D_vktStructuredVolume_Destroy(vktArray3D_vktStructuredVolume arr);
+VKTAPI void vktArray3D_vktStructuredVolume_Resize(vktArray3D_vktStructuredVolume arr, vktVec3i_t dims);
+VKTAPI void vktArray3D_vktStructuredVolume_Fill(vktArray3D_vktStructuredVolume arr, vktStructuredVolume value);
+VKTAPI vktArray3D_vktStructuredVolume_Iterator vktArray3D_vktStructuredVolume_Begin(vktArray3D_vktStructuredVolume arr);
+VKTAPI vktArray3D_vktStructuredVolume_ConstIterator vktArray3D_vktStructuredVolume_CBegin(vktArray3D_vktStructuredVolume arr);
+VKTAPI vktArray3D_vktStructuredVolume_Iterator vktArray3D_vktStructuredVolume_End(vktArray3D_vktStructuredVolume arr);
+VKTAPI vktArray3D_vktStructuredVolume_ConstIterator vktArray3D_vktStructuredVolume_CEnd(vktArray3D_vktStructuredVolume arr);
+VKTAPI vktArray3D_vktStructuredVolume_ValueType* vktArray3D_vktStructuredVolume_Access(vktArray3D_vktStructuredVolume arr,
+                                                                                       vktVec3i_t index);
+VKTAPI vktArray3D_vktStructuredVolume_ValueType const* vktArray3D_vktStructuredVolume_CAccess(
+    vktArray3D_vktStructuredVolume arr, vktVec3i_t index);
+VKTAPI vktBool_t vktArray3D_vktStructuredVolume_Empty(vktArray3D_vktStructuredVolume arr);
+VKTAPI vktStructuredVolume* vktArray3D_vktStructuredVolume_Data(vktArray3D_vktStructuredVolume arr);
+VKTAPI vktStructuredVolume const* vktArray3D_vktStructuredVolume_CData(vktArray3D_vktStructuredVolume arr);
+VKTAPI vktVec3i_t vktArray3D_vktStructuredVolume_Dims(vktArray3D_vktStructuredVolume arr);
+VKTAPI size_t vktArray3D_vktStructuredVolume_NumElements(vktArray3D_vktStructuredVolume arr);
+
+/* ---- Decompose.h (reference include/c/vkt/Decompose.h:18-44) ------------- */
+VKTAPI vktError vktBrickDecomposeSV(vktArray3D_vktStructuredVolume decomp, vktStructuredVolume source,
+                                    int32_t brickSizeX, int32_t brickSizeY, int32_t brickSizeZ,
+                                    int32_t haloSizeNegX, int32_t haloSizeNegY, int32_t haloSizeNegZ,
+                                    int32_t haloSizePosX, int32_t haloSizePosY, int32_t haloSizePosZ);
+VKTAPI vktError vktBrickDecomposeResizeSV(vktArray3D_vktStructuredVolume decomp, vktStructuredVolume source,
+                                          int32_t brickSizeX, int32_t brickSizeY, int32_t brickSizeZ,
+                                          int32_t haloSizeNegX, int32_t haloSizeNegY, int32_t haloSizeNegZ,
+                                          int32_t haloSizePosX, int32_t haloSizePosY, int32_t haloSizePosZ);
+
 #ifdef __cplusplus
 }
 #endif

@@ -121,6 +121,21 @@ VKTAPI vktError vktHipTransformRange2(vktHipVolumeView_t volume1, vktHipVolumeVi
                                       vktVec3i_t first, vktVec3i_t last, vktVec3i_t volume2Offset,
                                       vktTransformBinaryOp binaryOp);
 
+/* One brick of a decomposition: CopyRange(brick, source, first, last, {0,0,0}). */
+typedef struct {
+    vktHipVolumeView_t brick;
+    vktVec3i_t first;   /* may be negative / past the source (halo): source reads clamp */
+    vktVec3i_t last;
+} vktHipBrickRange_t;
+
+/* replaces BrickDecompose_cuda (reference src/vkt/Decompose_cuda.cu:8-26, an empty stub);
+ * semantics of BrickDecompose_serial (src/vkt/Decompose_serial.hpp:15-46), i.e. one
+ * CopyRange per brick.  All bricks whose format and mapping equal the source's are copied
+ * by ONE batched kernel launch; the others go through the CopyRange conversion path.
+ * Every range is validated against its brick before anything is launched. */
+VKTAPI vktError vktHipBrickDecompose(vktHipVolumeView_t source, vktHipBrickRange_t const* bricks,
+                                     int32_t numBricks);
+
 /* Synthetic benchmark/test input: byte i of the volume = byte (i % 8) of
  * splitmix64(seed + (i / 8)) -- counter-based, so the oracle reproduces it exactly
  * (oracle/vkt_oracle.c: vkt_oracle_synth). */

@@ -142,3 +142,49 @@ def synth_codes(dims, fmt, seed) -> np.ndarray:
     x, y, z = dims
     b = synth(x * y * z * BPV[fmt], seed)
     return b.view(CODE_DTYPE[fmt]).reshape(z, y, x)
+
+
+# ---- BrickDecompose (reference src/vkt/Decompose.cpp:96-150 + Decompose_serial.hpp:15-46) ----
+def _div_up(a, b):
+    return (a + b - 1) // b
+
+
+def brick_layout(dims, brick, neg=(0, 0, 0), pos=(0, 0, 0)):
+    """BrickDecomposeResize (Decompose.cpp:103-147): {(x, y, z): brick dims incl. halos}."""
+    nb = [_div_up(d, b) for d, b in zip(dims, brick)]
+    ext = [n * b for n, b in zip(nb, brick)]
+    border = [b if d % b == 0 else b - e + d for d, b, e in zip(dims, brick, ext)]
+    out = {}
+    for z in range(nb[2]):
+        for y in range(nb[1]):
+            for x in range(nb[0]):
+                idx = (x, y, z)
+                size = [brick[a] if idx[a] < nb[a] - 1 else border[a] for a in range(3)]
+                out[idx] = tuple(neg[a] + size[a] + pos[a] for a in range(3))
+    return tuple(nb), out
+
+
+def brick_ranges(dims, num_bricks, brick, neg=(0, 0, 0), pos=(0, 0, 0)):
+    """Decompose_serial.hpp:24-44: {(x, y, z): (first, last)} of each brick's CopyRange."""
+    out = {}
+    for z in range(num_bricks[2]):
+        for y in range(num_bricks[1]):
+            for x in range(num_bricks[0]):
+                first = [x * brick[0], y * brick[1], z * brick[2]]
+                last = [min(first[a] + brick[a], dims[a]) for a in range(3)]
+                out[(x, y, z)] = (tuple(first[a] - neg[a] for a in range(3)),
+                                  tuple(last[a] + pos[a] for a in range(3)))
+    return out
+
+
+def brick_decompose(src: Volume, brick, neg=(0, 0, 0), pos=(0, 0, 0), init_byte=0):
+    """BrickDecomposeResize + BrickDecompose on the oracle: {(x, y, z): Volume}."""
+    nb, layout = brick_layout(src.dims, brick, neg, pos)
+    ranges = brick_ranges(src.dims, nb, brick, neg, pos)
+    out = {}
+    for idx, bdims in layout.items():
+        v = Volume.zeros(bdims, src.fmt, src.lo, src.hi, fill_byte=init_byte)
+        first, last = ranges[idx]
+        copy_range(v, src, first, last)
+        out[idx] = v
+    return out

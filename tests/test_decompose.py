@@ -1,0 +1,191 @@
+"""BrickDecompose / BrickDecomposeResize against the oracle restatement
+of reference src/vkt/Decompose.cpp:96-150 and src/vkt/Decompose_serial.hpp:15-46.
+
+CPU tests: the brick layout that BrickDecomposeResize allocates (host logic), the C Array3D
+handle API, and that the GPU backend refuses the CPU policy.  GPU tests: bit-exact brick
+contents (clamped halos at the volume border) for every voxel format, the reference example
+(src/examples/Decompose.c: 120x66x49 UInt8, 16^3 bricks, halo 1), the conversion path for a
+brick whose mapping differs from the source's, and argument validation.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from oracle import binding as ob
+
+vkt = pytest.importorskip("volkit_amd.volkit")
+from volkit_amd._lib import Vec3i_t, lib  # noqa: E402
+
+LAYOUTS = [
+    ((10, 9, 8), (4, 4, 4), (0, 0, 0), (0, 0, 0)),
+    ((10, 9, 8), (4, 4, 4), (1, 1, 1), (1, 1, 1)),
+    ((120, 66, 49), (16, 16, 16), (1, 1, 1), (1, 1, 1)),      # src/examples/Decompose.c
+    ((33, 17, 5), (8, 32, 2), (2, 0, 1), (0, 3, 0)),
+    ((64, 64, 64), (64, 64, 64), (0, 0, 0), (0, 0, 0)),
+    ((7, 5, 3), (1, 2, 3), (0, 1, 0), (1, 0, 2)),
+]
+
+
+def set_device(dev):
+    ep = vkt.GetThreadExecutionPolicy()
+    ep.device = dev
+    vkt.SetThreadExecutionPolicy(ep)
+
+
+@pytest.fixture
+def cpu():
+    set_device(vkt.ExecutionPolicy.Device_CPU)
+    yield
+    set_device(vkt.ExecutionPolicy.Device_CPU)
+
+
+@pytest.mark.parametrize("dims,brick,neg,pos", LAYOUTS)
+def test_resize_layout_matches_reference(cpu, dims, brick, neg, pos):
+    src = vkt.StructuredVolume(*dims, vkt.DataFormat_UInt16, 0.5, 1.0, 2.0, -1.0, 3.0)
+    arr = vkt.Array3D_StructuredVolume()
+    assert vkt.BrickDecomposeResize(arr, src, vkt.Vec3i(*brick), vkt.Vec3i(*neg), vkt.Vec3i(*pos)) == vkt.NoError
+    nb, layout = ob.brick_layout(dims, brick, neg, pos)
+    assert tuple(arr.dims()) == nb and len(arr) == len(layout)
+    for idx, bdims in layout.items():
+        b = arr[idx]
+        assert tuple(b.getDims()) == bdims, idx
+        assert b.getDataFormat() == vkt.DataFormat_UInt16
+        assert b.getDist() == (0.5, 1.0, 2.0)
+        m = b.getVoxelMapping()
+        assert (m.x, m.y) == (-1.0, 3.0)
+
+
+def test_c_array3d_api(cpu):
+    h = C.c_void_p()
+    lib.vktArray3D_vktStructuredVolume_Create(C.byref(h), Vec3i_t(2, 3, 4))
+    try:
+        assert lib.vktArray3D_vktStructuredVolume_NumElements(h) == 24
+        d = lib.vktArray3D_vktStructuredVolume_Dims(h)
+        assert (d.x, d.y, d.z) == (2, 3, 4)
+        assert not lib.vktArray3D_vktStructuredVolume_Empty(h)
+        begin = C.cast(lib.vktArray3D_vktStructuredVolume_Begin(h), C.c_void_p).value
+        end = C.cast(lib.vktArray3D_vktStructuredVolume_End(h), C.c_void_p).value
+        assert end - begin == 24 * C.sizeof(C.c_void_p)
+        slot = C.cast(lib.vktArray3D_vktStructuredVolume_Access(h, Vec3i_t(1, 2, 3)), C.c_void_p).value
+        assert slot - begin == (3 * 6 + 2 * 2 + 1) * C.sizeof(C.c_void_p)
+        lib.vktArray3D_vktStructuredVolume_Resize(h, Vec3i_t(0, 0, 0))
+        assert lib.vktArray3D_vktStructuredVolume_Empty(h)
+    finally:
+        lib.vktArray3D_vktStructuredVolume_Destroy(h)
+
+
+def test_cpu_policy_is_refused(cpu):
+    src = vkt.StructuredVolume(8, 8, 8, vkt.DataFormat_UInt8)
+    arr = vkt.Array3D_StructuredVolume()
+    assert vkt.BrickDecomposeResize(arr, src, vkt.Vec3i(4, 4, 4)) == vkt.NoError
+    assert vkt.BrickDecompose(arr, src, vkt.Vec3i(4, 4, 4)) == vkt.InvalidValue
+    assert "CPU execution policy" in vkt.last_error()
+
+
+def rand_codes(rng, fmt, shape):
+    if fmt == 7:
+        return rng.uniform(-2, 2, size=shape).astype(np.float32).view(np.uint32)
+    info = np.iinfo(ob.CODE_DTYPE[fmt])
+    return rng.integers(0, int(info.max) + 1, size=shape, dtype=np.uint64).astype(ob.CODE_DTYPE[fmt])
+
+
+def gpu_decompose(codes, fmt, mapping, brick, neg, pos, tweak=None):
+    """Source filled on the host, bricks allocated and decomposed under the GPU policy, read
+    back under the CPU policy (deferred migration)."""
+    z, y, x = codes.shape
+    set_device(vkt.ExecutionPolicy.Device_CPU)
+    src = vkt.StructuredVolume(x, y, z, fmt, 1.0, 1.0, 1.0, *mapping)
+    src.from_numpy(codes)
+    arr = vkt.Array3D_StructuredVolume()
+    set_device(vkt.ExecutionPolicy.Device_GPU)
+    try:
+        assert vkt.BrickDecomposeResize(arr, src, vkt.Vec3i(*brick), vkt.Vec3i(*neg), vkt.Vec3i(*pos)) == vkt.NoError
+        if tweak:
+            tweak(arr)
+        err = vkt.BrickDecompose(arr, src, vkt.Vec3i(*brick), vkt.Vec3i(*neg), vkt.Vec3i(*pos))
+    finally:
+        set_device(vkt.ExecutionPolicy.Device_CPU)
+    if err != vkt.NoError:
+        return err, None
+    d = arr.dims()
+    out = {(i, j, k): arr[(i, j, k)].to_numpy() for k in range(d.z) for j in range(d.y) for i in range(d.x)}
+    return err, out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fmt", [4, 5, 7, 6])
+@pytest.mark.parametrize("dims,brick,neg,pos", LAYOUTS)
+def test_brick_decompose_parity(fmt, dims, brick, neg, pos):
+    rng = np.random.default_rng(fmt * 100 + sum(dims))
+    codes = rand_codes(rng, fmt, dims[::-1])
+    err, got = gpu_decompose(codes, fmt, (0.0, 1.0), brick, neg, pos)
+    assert err == vkt.NoError, vkt.last_error()
+    ref = ob.brick_decompose(ob.Volume(codes, fmt), brick, neg, pos)
+    assert set(got) == set(ref)
+    for idx, v in ref.items():
+        np.testing.assert_array_equal(got[idx], v.codes, err_msg=f"brick {idx}")
+
+
+@pytest.mark.gpu
+def test_reference_example_decompose():
+    """src/examples/Decompose.c:16-88: Fill(.1) on 120x66x49 UInt8, 16^3 bricks with halo 1 --
+    every brick voxel (halos clamped at the border) holds the code of 0.1."""
+    codes = np.full((49, 66, 120), ob.map_voxel(0.1, 4)[0], dtype=np.uint8)
+    err, got = gpu_decompose(codes, 4, (0.0, 1.0), (16, 16, 16), (1, 1, 1), (1, 1, 1))
+    assert err == vkt.NoError
+    assert len(got) == 8 * 5 * 4
+    for idx, a in got.items():
+        assert (a == 25).all(), idx
+    assert got[(0, 0, 0)].shape == (18, 18, 18) and got[(7, 4, 3)].shape == (1 + 1 + 1, 2 + 2, 8 + 2)
+
+
+@pytest.mark.gpu
+def test_brick_with_other_mapping_converts():
+    """A brick whose mapping differs from the source's takes CopyRange's unmap->map path
+    (Copy_serial.hpp:21-22), the others stay bytewise in the batched launch."""
+    rng = np.random.default_rng(5)
+    codes = rand_codes(rng, 5, (12, 10, 9))
+
+    def tweak(arr):
+        arr[(1, 0, 1)].setVoxelMapping(-1.0, 3.0)
+
+    err, got = gpu_decompose(codes, 5, (0.0, 1.0), (5, 5, 5), (1, 0, 1), (0, 1, 1), tweak)
+    assert err == vkt.NoError, vkt.last_error()
+    src = ob.Volume(codes, 5)
+    nb, layout = ob.brick_layout(src.dims, (5, 5, 5), (1, 0, 1), (0, 1, 1))
+    ranges = ob.brick_ranges(src.dims, nb, (5, 5, 5), (1, 0, 1), (0, 1, 1))
+    for idx, bdims in layout.items():
+        lo, hi = (-1.0, 3.0) if idx == (1, 0, 1) else (0.0, 1.0)
+        ref = ob.Volume.zeros(bdims, 5, lo, hi)
+        ob.copy_range(ref, src, *ranges[idx])
+        np.testing.assert_array_equal(got[idx], ref.codes, err_msg=f"brick {idx}")
+
+
+@pytest.mark.gpu
+def test_brick_too_small_is_rejected_before_any_launch():
+    codes = np.arange(8 * 8 * 8, dtype=np.uint16).reshape(8, 8, 8)
+
+    def tweak(arr):
+        arr[(1, 1, 1)].setDims(2, 2, 2)
+
+    err, _ = gpu_decompose(codes, 5, (0.0, 1.0), (4, 4, 4), (0, 0, 0), (0, 0, 0), tweak)
+    assert err == vkt.InvalidValue
+    assert "smaller than its range" in vkt.last_error()
+
+
+@pytest.mark.gpu
+def test_repeated_decompositions_stay_exact():
+    """Back-to-back decompositions with changing formats / layouts (bricks and descriptor
+    tables re-allocated at recycled addresses): a stream-ordered-pool version of the table
+    upload was intermittently read stale here."""
+    rng = np.random.default_rng(0)
+    for it in range(40):
+        fmt = (4, 5, 7, 6)[it % 4]
+        dims, brick = ((10, 9, 8), (4, 4, 4)) if it % 3 else ((33, 17, 5), (8, 32, 2))
+        codes = rand_codes(rng, fmt, dims[::-1])
+        err, got = gpu_decompose(codes, fmt, (0.0, 1.0), brick, (1, 0, 1), (0, 1, 0))
+        assert err == vkt.NoError
+        ref = ob.brick_decompose(ob.Volume(codes, fmt), brick, (1, 0, 1), (0, 1, 0))
+        for idx, v in ref.items():
+            np.testing.assert_array_equal(got[idx], v.codes, err_msg=f"iteration {it} brick {idx}")

@@ -105,6 +105,27 @@ def main():
             ms = timed(lambda: lib.vktHipResample(Rv, S, fm), max(3, R // 3))
             report(f"config3 Resample 1024^3->2048^3 Float32 {lab}", ms, 4 * s ** 3 + 4 * e ** 3, e ** 3)
         free(S, Rv)
+    if want("decompose"):
+        # BrickDecompose: 1024^3 UInt16 into 64^3 bricks with a 1-voxel halo
+        import volkit_amd.volkit as vkt
+        ep = vkt.GetThreadExecutionPolicy()
+        ep.device = vkt.ExecutionPolicy.Device_GPU
+        vkt.SetThreadExecutionPolicy(ep)
+        n = 1024
+        for bs, halo in ((64, 1), (128, 0), (32, 1)):
+            V = vkt.StructuredVolume(n, n, n, vkt.DataFormat_UInt16)
+            vkt.Synthesize(V, 77)
+            arr = vkt.Array3D_StructuredVolume()
+            b3, h3 = vkt.Vec3i(bs, bs, bs), vkt.Vec3i(halo, halo, halo)
+            vkt.BrickDecomposeResize(arr, V, b3, h3, h3)
+            vox = sum(arr[(i, j, k)].getSizeInBytes() // 2 for k in range(arr.dims().z)
+                      for j in range(arr.dims().y) for i in range(arr.dims().x))
+            ms = timed(lambda: vkt.BrickDecompose(arr, V, b3, h3, h3), R)
+            report(f"decompose BrickDecompose 1024^3 UInt16 -> {bs}^3 bricks halo {halo} (incl. host planning)",
+                   ms, 4 * vox, vox)
+            del arr, V
+        ep.device = vkt.ExecutionPolicy.Device_CPU
+        vkt.SetThreadExecutionPolicy(ep)
     if not want("metric"):
         return
 

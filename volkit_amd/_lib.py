@@ -63,6 +63,12 @@ class HipVolumeView_t(C.Structure):
                 ("dataFormat", i32), ("mappingLo", f32), ("mappingHi", f32)]
 
 
+class HipBrickRange_t(C.Structure):
+    _fields_ = [("brick", HipVolumeView_t), ("first", Vec3i_t), ("last", Vec3i_t)]
+
+
+c_arr = C.c_void_p            # vktArray3D_vktStructuredVolume (opaque handle)
+
 UnaryOp = C.CFUNCTYPE(None, i32, i32, i32, VoxelView_t)
 BinaryOp = C.CFUNCTYPE(None, i32, i32, i32, VoxelView_t, VoxelView_t)
 
@@ -156,6 +162,27 @@ SIGNATURES = {
     "vktHipTransformRange1": (c_err, [HipVolumeView_t, Vec3i_t, Vec3i_t, UnaryOp]),
     "vktHipTransformRange2": (c_err, [HipVolumeView_t, HipVolumeView_t, Vec3i_t, Vec3i_t, Vec3i_t, BinaryOp]),
     "vktHipSynthesize": (c_err, [HipVolumeView_t, u64]),
+    "vktHipBrickDecompose": (c_err, [HipVolumeView_t, P(HipBrickRange_t), i32]),
+    # Array3D.h (vktStructuredVolume instantiation) / Decompose.h
+    "vktArray3D_vktStructuredVolume_CreateEmpty": (None, [P(c_arr)]),
+    "vktArray3D_vktStructuredVolume_Create": (None, [P(c_arr), Vec3i_t]),
+    "vktArray3D_vktStructuredVolume_CreateCopy": (None, [P(c_arr), c_arr]),
+    "vktArray3D_vktStructuredVolume_Destroy": (None, [c_arr]),
+    "vktArray3D_vktStructuredVolume_Resize": (None, [c_arr, Vec3i_t]),
+    "vktArray3D_vktStructuredVolume_Fill": (None, [c_arr, c_vol]),
+    "vktArray3D_vktStructuredVolume_Begin": (P(c_vol), [c_arr]),
+    "vktArray3D_vktStructuredVolume_CBegin": (P(c_vol), [c_arr]),
+    "vktArray3D_vktStructuredVolume_End": (P(c_vol), [c_arr]),
+    "vktArray3D_vktStructuredVolume_CEnd": (P(c_vol), [c_arr]),
+    "vktArray3D_vktStructuredVolume_Access": (P(c_vol), [c_arr, Vec3i_t]),
+    "vktArray3D_vktStructuredVolume_CAccess": (P(c_vol), [c_arr, Vec3i_t]),
+    "vktArray3D_vktStructuredVolume_Empty": (C.c_uint8, [c_arr]),
+    "vktArray3D_vktStructuredVolume_Data": (P(c_vol), [c_arr]),
+    "vktArray3D_vktStructuredVolume_CData": (P(c_vol), [c_arr]),
+    "vktArray3D_vktStructuredVolume_Dims": (Vec3i_t, [c_arr]),
+    "vktArray3D_vktStructuredVolume_NumElements": (C.c_size_t, [c_arr]),
+    "vktBrickDecomposeSV": (c_err, [c_arr, c_vol] + _R9),
+    "vktBrickDecomposeResizeSV": (c_err, [c_arr, c_vol] + _R9),
 }
 for _op in ARITH_OPS:
     SIGNATURES[f"vkt{_op}SV"] = (c_err, [c_vol, c_vol, c_vol])

@@ -1,0 +1,308 @@
+// Decompose.cpp -- BrickDecompose / BrickDecomposeResize front-ends and the C Array3D of
+// StructuredVolume handles.
+//
+// Reference: src/vkt/Decompose.cpp:26-260 (C++ and C front-ends), src/vkt/Decompose_serial.hpp:
+// 15-88 (the per-brick CopyRange loop), include/c/vkt/Array3D.h:18-237 (C array API).
+// Under the GPU policy the whole decomposition is one vktHipBrickDecompose call
+// (kernels/Decompose.hip); under the CPU policy it returns InvalidValue like every other
+// algorithm of this GPU backend.
+
+#include "../runtime/Runtime.hpp"
+#include "../StructuredVolume_impl.hpp"
+#include "volkit_hip.h"
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+namespace vkt
+{
+namespace
+{
+    int32_t divUp(int32_t a, int32_t b) { return (a + b - 1) / b; }
+
+    vktHipVolumeView_t brickView(StructuredVolume& v)
+    {
+        vktHipVolumeView_t out;
+        out.data = v.getData();
+        Vec3i d = v.getDims();
+        out.dimX = d.x;
+        out.dimY = d.y;
+        out.dimZ = d.z;
+        out.dataFormat = static_cast<int32_t>(v.getDataFormat());
+        Vec2f m = v.getVoxelMapping();
+        out.mappingLo = m.x;
+        out.mappingHi = m.y;
+        return out;
+    }
+
+    bool validBrickSize(Vec3i b) { return b.x > 0 && b.y > 0 && b.z > 0; }
+
+    // numBricks and the border brick size (reference Decompose.cpp:103-121)
+    void brickGrid(Vec3i dims, Vec3i brick, Vec3i& numBricks, Vec3i& border)
+    {
+        numBricks = {divUp(dims.x, brick.x), divUp(dims.y, brick.y), divUp(dims.z, brick.z)};
+        Vec3i ext{numBricks.x * brick.x, numBricks.y * brick.y, numBricks.z * brick.z};
+        border = {dims.x % brick.x == 0 ? brick.x : brick.x - ext.x + dims.x,
+                  dims.y % brick.y == 0 ? brick.y : brick.y - ext.y + dims.y,
+                  dims.z % brick.z == 0 ? brick.z : brick.z - ext.z + dims.z};
+    }
+
+    // The per-brick ranges of BrickDecompose_serial (Decompose_serial.hpp:24-44), then one
+    // backend call.  `brickAt(i)` returns the StructuredVolume of brick linear index i.
+    template <class BrickAt>
+    Error decompose(Vec3i arrDims, StructuredVolume& source, Vec3i brickSize, Vec3i haloNeg, Vec3i haloPos,
+                    BrickAt&& brickAt)
+    {
+        ExecutionPolicy ep = GetThreadExecutionPolicy();
+        if (ep.device != ExecutionPolicy::Device::GPU)
+        {
+            rt::setLastError("BrickDecompose_hip: CPU execution policy");
+            VKT_LOG(rt::LogLevel::Error) << "When calling algorithm: BrickDecompose_hip -- volkit-amd implements the "
+                                            "GPU (HIP/gfx950) backend only; set ExecutionPolicy::Device::GPU";
+            return InvalidValue;
+        }
+        if (!validBrickSize(brickSize))
+        {
+            rt::fail("BrickDecompose: brick size must be positive");
+            return InvalidValue;
+        }
+        rt::ScopedKernelTimer timer("BrickDecompose_hip", ep.printPerformance != False);
+        Vec3i const dims = source.getDims();
+        std::vector<vktHipBrickRange_t> ranges;
+        ranges.reserve(static_cast<size_t>(std::max(0, arrDims.x)) * std::max(0, arrDims.y) * std::max(0, arrDims.z));
+        size_t i = 0;
+        for (int32_t z = 0; z < arrDims.z; ++z)
+            for (int32_t y = 0; y < arrDims.y; ++y)
+                for (int32_t x = 0; x < arrDims.x; ++x, ++i)
+                {
+                    vktHipBrickRange_t r;
+                    vktVec3i_t first{x * brickSize.x, y * brickSize.y, z * brickSize.z};
+                    vktVec3i_t last{std::min(first.x + brickSize.x, dims.x), std::min(first.y + brickSize.y, dims.y),
+                                    std::min(first.z + brickSize.z, dims.z)};
+                    r.first = {first.x - haloNeg.x, first.y - haloNeg.y, first.z - haloNeg.z};
+                    r.last = {last.x + haloPos.x, last.y + haloPos.y, last.z + haloPos.z};
+                    r.brick = brickView(brickAt(i));
+                    ranges.push_back(r);
+                }
+        vktHipVolumeView_t src = brickView(source);
+        return static_cast<Error>(vktHipBrickDecompose(src, ranges.data(), static_cast<int32_t>(ranges.size())));
+    }
+} // namespace
+
+Error BrickDecompose(Array3D<StructuredVolume>& dest, StructuredVolume& source, int32_t bx, int32_t by, int32_t bz,
+                     int32_t nx, int32_t ny, int32_t nz, int32_t px, int32_t py, int32_t pz)
+{
+    return BrickDecompose(dest, source, Vec3i{bx, by, bz}, Vec3i{nx, ny, nz}, Vec3i{px, py, pz});
+}
+
+Error BrickDecompose(Array3D<StructuredVolume>& dest, StructuredVolume& source, Vec3i brickSize, Vec3i haloSizeNeg,
+                     Vec3i haloSizePos)
+{
+    StructuredVolume* bricks = dest.data();
+    return decompose(dest.dims(), source, brickSize, haloSizeNeg, haloSizePos,
+                     [&](size_t i) -> StructuredVolume& { return bricks[i]; });
+}
+
+Error BrickDecomposeResize(Array3D<StructuredVolume>& dest, StructuredVolume& source, int32_t bx, int32_t by,
+                           int32_t bz, int32_t nx, int32_t ny, int32_t nz, int32_t px, int32_t py, int32_t pz)
+{
+    return BrickDecomposeResize(dest, source, Vec3i{bx, by, bz}, Vec3i{nx, ny, nz}, Vec3i{px, py, pz});
+}
+
+// Reference Decompose.cpp:96-150: one brick per cell, border bricks cropped, halos added,
+// same format / dist / mapping as the source.  Allocation happens on the calling thread's
+// device (GPU policy: straight into HBM).
+Error BrickDecomposeResize(Array3D<StructuredVolume>& dest, StructuredVolume& source, Vec3i brickSize,
+                           Vec3i haloSizeNeg, Vec3i haloSizePos)
+{
+    if (!validBrickSize(brickSize))
+    {
+        rt::fail("BrickDecomposeResize: brick size must be positive");
+        return InvalidValue;
+    }
+    Vec3i numBricks, border;
+    brickGrid(source.getDims(), brickSize, numBricks, border);
+    dest = Array3D<StructuredVolume>(numBricks);
+    Vec3f dist = source.getDist();
+    Vec2f map = source.getVoxelMapping();
+    for (int32_t z = 0; z < numBricks.z; ++z)
+        for (int32_t y = 0; y < numBricks.y; ++y)
+            for (int32_t x = 0; x < numBricks.x; ++x)
+            {
+                Vec3i size{x < numBricks.x - 1 ? brickSize.x : border.x, y < numBricks.y - 1 ? brickSize.y : border.y,
+                           z < numBricks.z - 1 ? brickSize.z : border.z};
+                StructuredVolume brick(haloSizeNeg.x + size.x + haloSizePos.x, haloSizeNeg.y + size.y + haloSizePos.y,
+                                       haloSizeNeg.z + size.z + haloSizePos.z, source.getDataFormat(), dist.x, dist.y,
+                                       dist.z, map.x, map.y);
+                dest[Vec3i{x, y, z}] = std::move(brick);
+            }
+    return NoError;
+}
+
+} // vkt
+
+//--- C API ---------------------------------------------------------------------------------
+struct vktArray3D_vktStructuredVolume_impl
+{
+    std::vector<vktStructuredVolume> handles;
+    vktVec3i_t dims{0, 0, 0};
+};
+
+namespace
+{
+    size_t count(vktVec3i_t d)
+    {
+        return d.x > 0 && d.y > 0 && d.z > 0 ? static_cast<size_t>(d.x) * static_cast<size_t>(d.y) * static_cast<size_t>(d.z)
+                                             : 0;
+    }
+
+    size_t linear(vktArray3D_vktStructuredVolume arr, vktVec3i_t i)
+    {
+        return (static_cast<size_t>(i.z) * static_cast<size_t>(arr->dims.y) + static_cast<size_t>(i.y)) *
+                   static_cast<size_t>(arr->dims.x) +
+               static_cast<size_t>(i.x);
+    }
+} // namespace
+
+extern "C" {
+
+void vktArray3D_vktStructuredVolume_CreateEmpty(vktArray3D_vktStructuredVolume* arr)
+{
+    *arr = new vktArray3D_vktStructuredVolume_impl;
+}
+
+void vktArray3D_vktStructuredVolume_Create(vktArray3D_vktStructuredVolume* arr, vktVec3i_t dims)
+{
+    *arr = new vktArray3D_vktStructuredVolume_impl;
+    (*arr)->handles.assign(count(dims), nullptr);
+    (*arr)->dims = dims;
+}
+
+// Copies the handle values (shallow, like the reference's byte copy of the handle buffer).
+void vktArray3D_vktStructuredVolume_CreateCopy(vktArray3D_vktStructuredVolume* arr, vktArray3D_vktStructuredVolume rhs)
+{
+    *arr = new vktArray3D_vktStructuredVolume_impl(*rhs);
+}
+
+void vktArray3D_vktStructuredVolume_Destroy(vktArray3D_vktStructuredVolume arr)
+{
+    if (!arr)
+        return;
+    for (vktStructuredVolume h : arr->handles)
+        if (h)
+            vktStructuredVolumeDestroy(h);
+    delete arr;
+}
+
+// Keeps the handles of the first min(old, new) slots (reference: ManagedBuffer resize keeps
+// the leading bytes); new slots are NULL.
+void vktArray3D_vktStructuredVolume_Resize(vktArray3D_vktStructuredVolume arr, vktVec3i_t dims)
+{
+    arr->handles.resize(count(dims), nullptr);
+    arr->dims = dims;
+}
+
+void vktArray3D_vktStructuredVolume_Fill(vktArray3D_vktStructuredVolume arr, vktStructuredVolume value)
+{
+    std::fill(arr->handles.begin(), arr->handles.end(), value);
+}
+
+vktStructuredVolume* vktArray3D_vktStructuredVolume_Begin(vktArray3D_vktStructuredVolume arr)
+{
+    return arr->handles.data();
+}
+
+vktStructuredVolume const* vktArray3D_vktStructuredVolume_CBegin(vktArray3D_vktStructuredVolume arr)
+{
+    return arr->handles.data();
+}
+
+vktStructuredVolume* vktArray3D_vktStructuredVolume_End(vktArray3D_vktStructuredVolume arr)
+{
+    return arr->handles.data() + arr->handles.size();
+}
+
+vktStructuredVolume const* vktArray3D_vktStructuredVolume_CEnd(vktArray3D_vktStructuredVolume arr)
+{
+    return arr->handles.data() + arr->handles.size();
+}
+
+vktStructuredVolume* vktArray3D_vktStructuredVolume_Access(vktArray3D_vktStructuredVolume arr, vktVec3i_t index)
+{
+    return &arr->handles[linear(arr, index)];
+}
+
+vktStructuredVolume const* vktArray3D_vktStructuredVolume_CAccess(vktArray3D_vktStructuredVolume arr, vktVec3i_t index)
+{
+    return &arr->handles[linear(arr, index)];
+}
+
+vktBool_t vktArray3D_vktStructuredVolume_Empty(vktArray3D_vktStructuredVolume arr)
+{
+    return arr->handles.empty() ? VKT_TRUE : VKT_FALSE;
+}
+
+vktStructuredVolume* vktArray3D_vktStructuredVolume_Data(vktArray3D_vktStructuredVolume arr)
+{
+    return arr->handles.data();
+}
+
+vktStructuredVolume const* vktArray3D_vktStructuredVolume_CData(vktArray3D_vktStructuredVolume arr)
+{
+    return arr->handles.data();
+}
+
+vktVec3i_t vktArray3D_vktStructuredVolume_Dims(vktArray3D_vktStructuredVolume arr) { return arr->dims; }
+
+size_t vktArray3D_vktStructuredVolume_NumElements(vktArray3D_vktStructuredVolume arr) { return arr->handles.size(); }
+
+vktError vktBrickDecomposeSV(vktArray3D_vktStructuredVolume dest, vktStructuredVolume source, int32_t bx, int32_t by,
+                             int32_t bz, int32_t nx, int32_t ny, int32_t nz, int32_t px, int32_t py, int32_t pz)
+{
+    if (!dest || !source)
+        return vktInvalidValue;
+    for (vktStructuredVolume h : dest->handles)
+        if (!h)
+            return vkt::rt::fail("vktBrickDecomposeSV: the array holds an unallocated brick (call vktBrickDecomposeResizeSV)");
+    return static_cast<vktError>(vkt::decompose(vkt::Vec3i{dest->dims.x, dest->dims.y, dest->dims.z}, source->volume,
+                                                vkt::Vec3i{bx, by, bz}, vkt::Vec3i{nx, ny, nz}, vkt::Vec3i{px, py, pz},
+                                                [&](size_t i) -> vkt::StructuredVolume& {
+                                                    return dest->handles[i]->volume;
+                                                }));
+}
+
+// Reference Decompose.cpp:185-260; previously held handles are destroyed first (the
+// reference overwrites and leaks them).
+vktError vktBrickDecomposeResizeSV(vktArray3D_vktStructuredVolume dest, vktStructuredVolume source, int32_t bx,
+                                   int32_t by, int32_t bz, int32_t nx, int32_t ny, int32_t nz, int32_t px, int32_t py,
+                                   int32_t pz)
+{
+    if (!dest || !source)
+        return vktInvalidValue;
+    if (bx <= 0 || by <= 0 || bz <= 0)
+        return vkt::rt::fail("vktBrickDecomposeResizeSV: brick size must be positive");
+    vkt::Vec3i numBricks, border;
+    vkt::brickGrid(source->volume.getDims(), vkt::Vec3i{bx, by, bz}, numBricks, border);
+    for (vktStructuredVolume h : dest->handles)
+        if (h)
+            vktStructuredVolumeDestroy(h);
+    dest->handles.assign(count(vktVec3i_t{numBricks.x, numBricks.y, numBricks.z}), nullptr);
+    dest->dims = {numBricks.x, numBricks.y, numBricks.z};
+    vkt::Vec3f dist = source->volume.getDist();
+    vkt::Vec2f map = source->volume.getVoxelMapping();
+    for (int32_t z = 0; z < numBricks.z; ++z)
+        for (int32_t y = 0; y < numBricks.y; ++y)
+            for (int32_t x = 0; x < numBricks.x; ++x)
+            {
+                int32_t sx = x < numBricks.x - 1 ? bx : border.x, sy = y < numBricks.y - 1 ? by : border.y;
+                int32_t sz = z < numBricks.z - 1 ? bz : border.z;
+                vktStructuredVolumeCreate(vktArray3D_vktStructuredVolume_Access(dest, vktVec3i_t{x, y, z}), nx + sx + px,
+                                          ny + sy + py, nz + sz + pz,
+                                          static_cast<vktDataFormat>(source->volume.getDataFormat()), dist.x, dist.y,
+                                          dist.z, map.x, map.y);
+            }
+    return vktNoError;
+}
+
+} // extern "C"

@@ -440,14 +440,10 @@ namespace hipk
                 return false;   // per-dst-voxel chain kernel handles these
             ResampleArgs b = a;
             b.srcRows = static_cast<uint64_t>(src.dimY) * static_cast<uint64_t>(src.dimZ);
-            uint8_t* dirty = nullptr;
-            // stream-ordered pool allocation: no device-wide sync, freed behind the launch
-            // (rowDirty, then rowChain for the plane layout)
-            if (hipMallocAsync(reinterpret_cast<void**>(&dirty), 2 * b.srcRows, s) != hipSuccess)
-            {
-                (void)hipGetLastError();
-                dirty = nullptr;   // fall back to the chain for every task (still exact)
-            }
+            // rowDirty, then rowChain for the plane layout; without scratch every task takes
+            // the chain (still exact)
+            static rt::StreamScratch scratch;
+            uint8_t* dirty = static_cast<uint8_t*>(scratch.acquire(2 * b.srcRows, s));
             if (dirty)
             {
                 unsigned const g = static_cast<unsigned>((b.srcRows + kBlock / 64 - 1) / (kBlock / 64));
@@ -469,7 +465,7 @@ namespace hipk
             }
             launchRowMode2(b, k, bd, grid, instrPerRow, s);
             if (dirty)
-                (void)hipFreeAsync(dirty, s);
+                scratch.release(s);
             return true;
         }
         if (bs != bd)

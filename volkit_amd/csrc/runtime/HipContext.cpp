@@ -133,6 +133,46 @@ namespace rt
         return vktNoError;
     }
 
+    void* StreamScratch::acquire(std::size_t bytes, hipStream_t stream)
+    {
+        m_.lock();
+        if (pending_ && (stream != last_ || cap_ < bytes))   // growing frees the old buffer
+        {
+            (void)check(hipEventSynchronize(done_), "hipEventSynchronize(scratch)");
+            pending_ = false;
+        }
+        if (!done_ && check(hipEventCreateWithFlags(&done_, hipEventDisableTiming), "hipEventCreate") != vktNoError)
+        {
+            m_.unlock();
+            return nullptr;
+        }
+        if (cap_ < bytes)
+        {
+            if (p_)
+                (void)check(hipFree(p_), "hipFree(scratch)");
+            p_ = nullptr;
+            cap_ = 0;
+            if (check(hipMalloc(&p_, bytes), "hipMalloc(scratch)") != vktNoError)
+            {
+                p_ = nullptr;
+                m_.unlock();
+                return nullptr;
+            }
+            cap_ = bytes;
+        }
+        return p_;
+    }
+
+    void StreamScratch::release(hipStream_t stream)
+    {
+        if (check(hipEventRecord(done_, stream), "hipEventRecord(scratch)") == vktNoError)
+        {
+            pending_ = true;
+            last_ = stream;
+        }
+        m_.unlock();
+    }
+
     bool kernelTimingEnabled() { return ctx().timing.load() != 0; }
 
     ScopedKernelTimer::ScopedKernelTimer(char const* name, bool log)

@@ -8,6 +8,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <mutex>
 #include <sstream>
 #include <string>
 
@@ -67,6 +68,30 @@ namespace rt
     };
 
     bool kernelTimingEnabled();
+
+    // Device scratch for one backend call site, reused across calls (no per-call hipMalloc,
+    // and no stream-ordered pool: hipMallocAsync blocks filled by an H2D copy were
+    // intermittently seen stale by the next kernel on gfx950/ROCm 7.2 -- DESIGN.md §4.6).
+    // acquire(stream) hands the buffer out again right away when the previous user released
+    // it on the same stream (stream order protects it); after a stream switch it first waits
+    // (host) for the previous user's work.
+    class StreamScratch
+    {
+    public:
+        // Returns nullptr (and records the error) on allocation failure.  Holds the lock
+        // until release().
+        void* acquire(std::size_t bytes, hipStream_t stream);
+        // Records completion of the work that uses the buffer on `stream`, unlocks.
+        void release(hipStream_t stream);
+
+    private:
+        std::mutex m_;
+        void* p_ = nullptr;
+        std::size_t cap_ = 0;
+        hipEvent_t done_ = nullptr;
+        hipStream_t last_ = nullptr;
+        bool pending_ = false;
+    };
 
 } // rt
 

@@ -103,7 +103,9 @@ class StructuredVolume:
 
     def __init__(self, dimX: int = 0, dimY: int = 0, dimZ: int = 0, dataFormat: int = DataFormat_UInt8,
                  distX: float = 1.0, distY: float = 1.0, distZ: float = 1.0,
-                 mappingLo: float = 0.0, mappingHi: float = 1.0, *, _handle=None):
+                 mappingLo: float = 0.0, mappingHi: float = 1.0, *, _handle=None, _owner=None):
+        # _owner: a container that owns the handle (bricks of an Array3D); kept alive, never destroyed here
+        self._owner = _owner
         if _handle is not None:
             self._h = _handle
             return
@@ -120,7 +122,7 @@ class StructuredVolume:
 
     def __del__(self):
         h = getattr(self, "_h", None)
-        if h is not None and h.value:
+        if h is not None and h.value and getattr(self, "_owner", None) is None:
             lib.vktStructuredVolumeDestroy(h)
             self._h = None
 
@@ -373,6 +375,76 @@ def TransformRange(volume1: StructuredVolume, *args) -> int:
     f = [int(v) for v in _flatlen(rest)]
     cb = _lib.UnaryOp(lambda x, y, z, v: fn(x, y, z, VoxelView(v)))
     return lib.vktTransformRangeSV1(volume1.handle, *f, cb)
+
+
+# ---- Array3D.hpp / Decompose.hpp --------------------------------------------------------------
+class Array3D_StructuredVolume:
+    """SWIG's ``vkt.Array3D_StructuredVolume`` (reference src/vkt/volkit.i:88-100) over the C
+    array of volume handles.  ``decomp[vkt.Vec3i(x, y, z)]`` returns the brick; the array owns
+    the bricks that BrickDecomposeResize created."""
+
+    def __init__(self, dims=None):
+        h = C.c_void_p()
+        if dims is None:
+            lib.vktArray3D_vktStructuredVolume_CreateEmpty(C.byref(h))
+        else:
+            lib.vktArray3D_vktStructuredVolume_Create(C.byref(h), Vec3i_t(*_ints([dims], 3)))
+        self._h = h
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            lib.vktArray3D_vktStructuredVolume_Destroy(h)
+            self._h = None
+
+    @property
+    def handle(self):
+        return self._h
+
+    def dims(self) -> Vec3i:
+        d = lib.vktArray3D_vktStructuredVolume_Dims(self._h)
+        return Vec3i(d.x, d.y, d.z)
+
+    def numElements(self) -> int:
+        return lib.vktArray3D_vktStructuredVolume_NumElements(self._h)
+
+    def empty(self) -> bool:
+        return bool(lib.vktArray3D_vktStructuredVolume_Empty(self._h))
+
+    def __len__(self):
+        return self.numElements()
+
+    def __getitem__(self, index) -> StructuredVolume:
+        x, y, z = _ints([index], 3)
+        d = self.dims()
+        if not (0 <= x < d.x and 0 <= y < d.y and 0 <= z < d.z):
+            raise IndexError(f"brick index {(x, y, z)} outside {tuple(d)}")
+        slot = lib.vktArray3D_vktStructuredVolume_Access(self._h, Vec3i_t(x, y, z))
+        h = slot[0]
+        if not h:
+            raise IndexError("unallocated brick (call BrickDecomposeResize first)")
+        return StructuredVolume(_handle=C.c_void_p(h), _owner=self)   # borrowed: the array owns it
+
+
+def _decompose_args(fn, args):
+    f = [int(v) for v in _flatlen(args)]
+    if len(f) == 3:
+        f += [0] * 6
+    elif len(f) == 6:
+        f += [0] * 3
+    if len(f) != 9:
+        raise TypeError(f"{fn} expects brickSize[, haloSizeNeg[, haloSizePos]]")
+    return f
+
+
+def BrickDecompose(decomp: Array3D_StructuredVolume, volume: StructuredVolume, *args) -> int:
+    """vkt::BrickDecompose: one CopyRange per brick (with halos), one gfx950 launch."""
+    return lib.vktBrickDecomposeSV(decomp.handle, volume.handle, *_decompose_args("BrickDecompose", args))
+
+
+def BrickDecomposeResize(decomp: Array3D_StructuredVolume, volume: StructuredVolume, *args) -> int:
+    return lib.vktBrickDecomposeResizeSV(decomp.handle, volume.handle,
+                                         *_decompose_args("BrickDecomposeResize", args))
 
 
 # ---- backend utilities (include/volkit_hip.h) ----------------------------------------------
