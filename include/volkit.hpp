@@ -493,4 +493,40 @@ namespace vkt
     VKTAPI Error BrickDecomposeResize(Array3D<StructuredVolume>& dest, StructuredVolume& source, Vec3i brickSize,
                                       Vec3i haloSizeNeg = {0, 0, 0}, Vec3i haloSizePos = {0, 0, 0});
 
+    //--- Aggregates.hpp (reference include/cpp/vkt/Aggregates.hpp:14-42) -------------------
+    struct Aggregates
+    {
+        float min;
+        float max;
+        float mean;
+        float stddev;
+        float var;
+        float sum;
+        float prod;
+        Vec3i argmin;
+        Vec3i argmax;
+    };
+
+    VKTAPI Error ComputeAggregates(StructuredVolume& volume, Aggregates& aggregates);
+    VKTAPI Error ComputeAggregatesRange(StructuredVolume& volume, Aggregates& aggregates, int32_t firstX,
+                                        int32_t firstY, int32_t firstZ, int32_t lastX, int32_t lastY, int32_t lastZ);
+    VKTAPI Error ComputeAggregatesRange(StructuredVolume& volume, Aggregates& aggregates, Vec3i first, Vec3i last);
+
+    //--- Histogram.hpp (reference include/cpp/vkt/Histogram.hpp:14-42) --------------------
+    class VKTAPI Histogram : public ManagedBuffer<std::size_t>
+    {
+    public:
+        Histogram(std::size_t numBins);
+
+        std::size_t getNumBins() const;
+
+        //! Bin counts in the calling thread's address space (migrates first)
+        std::size_t* getBinCounts();
+    };
+
+    VKTAPI Error ComputeHistogram(StructuredVolume& volume, Histogram& histogram);
+    VKTAPI Error ComputeHistogramRange(StructuredVolume& volume, Histogram& histogram, int32_t firstX, int32_t firstY,
+                                       int32_t firstZ, int32_t lastX, int32_t lastY, int32_t lastZ);
+    VKTAPI Error ComputeHistogramRange(StructuredVolume& volume, Histogram& histogram, Vec3i first, Vec3i last);
+
 } // vkt

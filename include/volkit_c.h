@@ -257,6 +257,39 @@ VKTAPI vktError vktBrickDecomposeResizeSV(vktArray3D_vktStructuredVolume decomp,
                                           int32_t haloSizeNegX, int32_t haloSizeNegY, int32_t haloSizeNegZ,
                                           int32_t haloSizePosX, int32_t haloSizePosY, int32_t haloSizePosZ);
 
+/* ---- Aggregates.h (reference include/c/vkt/Aggregates.h:17-44) ---------- */
+typedef struct {
+    float min;
+    float max;
+    float mean;
+    float stddev;
+    float var;
+    float sum;
+    float prod;
+    vktVec3i_t argmin;
+    vktVec3i_t argmax;
+} vktAggregates_t;
+VKTAPI vktError vktComputeAggregatesSV(vktStructuredVolume volume, vktAggregates_t* aggregates);
+VKTAPI vktError vktComputeAggregatesRangeSV(vktStructuredVolume volume, vktAggregates_t* aggregates,
+                                            int32_t firstX, int32_t firstY, int32_t firstZ,
+                                            int32_t lastX, int32_t lastY, int32_t lastZ);
+
+/* ---- Histogram (C++-only in the reference, include/cpp/vkt/Histogram.hpp:14-42).
+ * C entry points added so that C, ctypes and cgo callers reach the same path: the
+ * handle wraps a vkt::Histogram (a ManagedBuffer of size_t bin counts, migrated with the
+ * thread policy like every ManagedBuffer). */
+struct vktHistogram_impl;
+typedef struct vktHistogram_impl* vktHistogram;
+VKTAPI void vktHistogramCreate(vktHistogram* histogram, size_t numBins);
+VKTAPI void vktHistogramDestroy(vktHistogram histogram);
+VKTAPI size_t vktHistogramGetNumBins(vktHistogram histogram);
+/* bin counts in the address space of the calling thread's device (migrates first) */
+VKTAPI size_t* vktHistogramGetBinCounts(vktHistogram histogram);
+VKTAPI vktError vktComputeHistogramSV(vktStructuredVolume volume, vktHistogram histogram);
+VKTAPI vktError vktComputeHistogramRangeSV(vktStructuredVolume volume, vktHistogram histogram,
+                                           int32_t firstX, int32_t firstY, int32_t firstZ,
+                                           int32_t lastX, int32_t lastY, int32_t lastZ);
+
 #ifdef __cplusplus
 }
 #endif

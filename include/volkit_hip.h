@@ -136,6 +136,46 @@ typedef struct {
 VKTAPI vktError vktHipBrickDecompose(vktHipVolumeView_t source, vktHipBrickRange_t const* bricks,
                                      int32_t numBricks);
 
+/* ---- reductions --------------------------------------------------
+ * replaces ComputeAggregatesRange_cuda (declared by reference src/vkt/Aggregates_cuda.hpp,
+ * never implemented); semantics of ComputeAggregatesRange_serial
+ * (src/vkt/Aggregates_serial.hpp:20-83): min/max/argmin/argmax bit-exact (first occurrence
+ * in z,y,x order), sum/prod/var accumulated in double from the reference's per-voxel float
+ * terms (within the serial path's own rounding error), mean and var divided by the voxel
+ * count of the WHOLE volume like the reference. */
+VKTAPI vktError vktHipAggregatesRange(vktHipVolumeView_t volume, vktVec3i_t first, vktVec3i_t last,
+                                      vktAggregates_t* aggregates);
+
+/* Partial aggregates, for combining Z-slabs of one volume across ranks (multi-GPU): pass 1
+ * fills min/max (with GLOBAL linear voxel indices: z + zGlobalOffset), sum, prod, count;
+ * pass 2 fills sumSq = sum of (v - mean)^2 with the reference's float difference and square.
+ * Combine partials of all slabs (vktHipAggregatePartialCombine, associative), derive the
+ * float mean of the whole volume (vktHipAggregatesMean), run pass 2, combine, then
+ * vktHipAggregatesFinish. */
+typedef struct {
+    double sum, prod, sumSq;
+    float minValue, maxValue;
+    uint64_t minIndex, maxIndex;   /* global linear index z*dimY*dimX + y*dimX + x; ~0 = none */
+    uint64_t count;
+} vktHipAggregatePartial_t;
+VKTAPI vktError vktHipAggregatePartialInit(vktHipAggregatePartial_t* partial);
+VKTAPI vktError vktHipAggregatePartialCombine(vktHipAggregatePartial_t* acc, vktHipAggregatePartial_t const* other);
+VKTAPI float vktHipAggregatesMean(vktHipAggregatePartial_t const* pass1, uint64_t numElems);
+VKTAPI vktError vktHipAggregatesPass(vktHipVolumeView_t volume, vktVec3i_t first, vktVec3i_t last,
+                                     int32_t zGlobalOffset, int32_t pass, float mean,
+                                     vktHipAggregatePartial_t* partial);
+VKTAPI vktError vktHipAggregatesFinish(vktHipAggregatePartial_t const* pass1, vktHipAggregatePartial_t const* pass2,
+                                       uint64_t numElems, int32_t dimX, int32_t dimY, vktAggregates_t* aggregates);
+
+/* replaces ComputeHistogramRange_cuda (reference src/vkt/Histogram_cuda.cu:45-76, which
+ * ignores `first`); semantics of ComputeHistogramRange_serial (src/vkt/Histogram_serial.hpp:
+ * 20-50): bins[(size_t)((v - lo) * ((float)numBins / (hi - lo)))]++ over the range.  `bins`
+ * is a DEVICE array of numBins uint64 counters; zeroed first unless `accumulate` (slab
+ * partial histograms summed in place / all-reduced).  Indices the reference would write out
+ * of bounds (v outside [lo, hi], NaN) are not counted. */
+VKTAPI vktError vktHipHistogramRange(vktHipVolumeView_t volume, vktVec3i_t first, vktVec3i_t last, uint64_t* bins,
+                                     uint64_t numBins, int32_t accumulate);
+
 /* Synthetic benchmark/test input: byte i of the volume = byte (i % 8) of
  * splitmix64(seed + (i / 8)) -- counter-based, so the oracle reproduces it exactly
  * (oracle/vkt_oracle.c: vkt_oracle_synth). */

@@ -48,6 +48,16 @@ _lib.vko_splitmix64.restype = C.c_uint64
 _lib.vko_splitmix64.argtypes = [C.c_uint64]
 _lib.vko_synth.argtypes = [C.POINTER(C.c_uint8), C.c_size_t, C.c_uint64]
 
+class Aggregates(C.Structure):
+    _fields_ = [("min", C.c_float), ("max", C.c_float), ("mean", C.c_float), ("stddev", C.c_float),
+                ("var", C.c_float), ("sum", C.c_float), ("prod", C.c_float), ("argmin", C.c_int32 * 3),
+                ("argmax", C.c_int32 * 3)]
+
+
+_lib.vko_aggregates_range.argtypes = [C.POINTER(_Vol), _i3, _i3, C.POINTER(Aggregates)]
+_lib.vko_histogram_range.restype = C.c_uint64
+_lib.vko_histogram_range.argtypes = [C.POINTER(_Vol), _i3, _i3, C.POINTER(C.c_uint64), C.c_uint64]
+
 UNARY = C.CFUNCTYPE(None, C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_uint8), C.c_int32, C.c_float, C.c_float)
 BINARY = C.CFUNCTYPE(None, C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_uint8), C.c_int32, C.c_float, C.c_float,
                      C.POINTER(C.c_uint8), C.c_int32, C.c_float, C.c_float)
@@ -188,3 +198,18 @@ def brick_decompose(src: Volume, brick, neg=(0, 0, 0), pos=(0, 0, 0), init_byte=
         copy_range(v, src, first, last)
         out[idx] = v
     return out
+
+
+# ---- reductions (reference Aggregates_serial.hpp:20-83, Histogram_serial.hpp:20-50) ----------
+def aggregates_range(v: Volume, first, last) -> Aggregates:
+    out = Aggregates()
+    _lib.vko_aggregates_range(v.ref, _i3(*first), _i3(*last), C.byref(out))
+    return out
+
+
+def histogram_range(v: Volume, first, last, num_bins: int):
+    """-> (bins as uint64 array, number of voxels the reference would count out of bounds)"""
+    bins = np.zeros(max(num_bins, 1), dtype=np.uint64)
+    skipped = _lib.vko_histogram_range(v.ref, _i3(*first), _i3(*last),
+                                       bins.ctypes.data_as(C.POINTER(C.c_uint64)), num_bins)
+    return bins[:num_bins], int(skipped)

@@ -13,6 +13,7 @@
  */
 #include "vkt_oracle.h"
 
+#include <float.h>
 #include <math.h>
 #include <string.h>
 
@@ -342,6 +343,69 @@ void vko_transform_range2(vko_volume* v1, vko_volume* v2, const int32_t first[3]
                 set_bytes(v1, x, y, z, b1);
                 set_bytes(v2, x + off[0], y + off[1], z + off[2], b2);
             }
+}
+
+/* ---- ComputeAggregatesRange_serial, src/vkt/Aggregates_serial.hpp:20-83 ---------- */
+void vko_aggregates_range(const vko_volume* v, const int32_t first[3], const int32_t last[3], vko_aggregates* a)
+{
+    memset(a, 0, sizeof(*a)); /* :27 */
+    a->min = FLT_MAX;         /* :29-31 */
+    a->max = -FLT_MAX;
+    a->prod = 1.f;
+    for (int32_t z = first[2]; z != last[2]; ++z)
+        for (int32_t y = first[1]; y != last[1]; ++y)
+            for (int32_t x = first[0]; x != last[0]; ++x) {
+                float val = get_value(v, x, y, z);
+                if (val < a->min) { /* :41-45 */
+                    a->min = val;
+                    a->argmin[0] = x; a->argmin[1] = y; a->argmin[2] = z;
+                }
+                if (val > a->max) { /* :47-51 */
+                    a->max = val;
+                    a->argmax[0] = x; a->argmax[1] = y; a->argmax[2] = z;
+                }
+                a->mean += val;     /* :53 */
+                a->sum += val;      /* :55 */
+                a->prod *= val;     /* :56 */
+            }
+    size_t num = (size_t)v->dims[0] * (size_t)v->dims[1] * (size_t)v->dims[2]; /* :61 */
+    a->mean = (float)(a->mean / (double)num);                                   /* :63 */
+    for (int32_t z = first[2]; z != last[2]; ++z)                                /* :68-80 */
+        for (int32_t y = first[1]; y != last[1]; ++y)
+            for (int32_t x = first[0]; x != last[0]; ++x) {
+                float val = get_value(v, x, y, z);
+                a->var += (val - a->mean) * (val - a->mean);
+            }
+    a->var = (float)(a->var / (double)num); /* :81 */
+    a->stddev = sqrtf(a->var);              /* :82 */
+}
+
+/* ---- ComputeHistogramRange_serial, src/vkt/Histogram_serial.hpp:20-50 ------------- */
+uint64_t vko_histogram_range(const vko_volume* v, const int32_t first[3], const int32_t last[3], uint64_t* bins,
+                             uint64_t num_bins)
+{
+    float lo = v->lo, hi = v->hi;
+    uint64_t skipped = 0;
+    float scale = (float)num_bins / (hi - lo); /* numBins / (hi - lo): size_t -> float */
+    memset(bins, 0, num_bins * sizeof(uint64_t));
+    for (int32_t z = first[2]; z != last[2]; ++z)
+        for (int32_t y = first[1]; y != last[1]; ++y)
+            for (int32_t x = first[0]; x != last[0]; ++x) {
+                float val = get_value(v, x, y, z);
+                float f = (val - lo) * scale;
+                /* (size_t)f: x86-64 truncation; (-1, 0) -> 0; the rest would index out of bounds */
+                if (!(f > -1.0f) || !(f < 9.2233720e18f)) {
+                    ++skipped;
+                    continue;
+                }
+                uint64_t bin = (uint64_t)(int64_t)f;
+                if (bin >= num_bins) {
+                    ++skipped;
+                    continue;
+                }
+                bins[bin]++;
+            }
+    return skipped;
 }
 
 /* ---- synthetic input -------------------------------------------------------------- */

@@ -56,6 +56,19 @@ void vko_transform_range1(vko_volume* v, const int32_t first[3], const int32_t l
 void vko_transform_range2(vko_volume* v1, vko_volume* v2, const int32_t first[3], const int32_t last[3],
                           const int32_t v2_offset[3], vko_binary_op op);
 
+/* ComputeAggregatesRange_serial, reference src/vkt/Aggregates_serial.hpp:20-83 (float
+ * accumulation in z->y->x order, mean/var divided by the WHOLE volume's voxel count). */
+typedef struct {
+    float min, max, mean, stddev, var, sum, prod;
+    int32_t argmin[3], argmax[3];
+} vko_aggregates;
+void vko_aggregates_range(const vko_volume* v, const int32_t first[3], const int32_t last[3], vko_aggregates* out);
+/* ComputeHistogramRange_serial, reference src/vkt/Histogram_serial.hpp:20-50.  Voxels whose
+ * bin index the reference would write out of bounds (UB) are not counted; their number is
+ * returned. */
+uint64_t vko_histogram_range(const vko_volume* v, const int32_t first[3], const int32_t last[3], uint64_t* bins,
+                             uint64_t num_bins);
+
 /* Synthetic input shared with the GPU generator (include/volkit_hip.h vktHipSynthesize). */
 uint64_t vko_splitmix64(uint64_t x);
 void vko_synth(uint8_t* data, size_t nbytes, uint64_t seed);

@@ -1,0 +1,287 @@
+"""ComputeAggregates / ComputeHistogram against the oracle restatement of
+reference src/vkt/Aggregates_serial.hpp:20-83 and src/vkt/Histogram_serial.hpp:20-50.
+
+Parity contract:
+  * histogram counts, min, max, argmin, argmax: bit-exact;
+  * sum, mean, var, stddev, prod: the reference accumulates floats serially, the GPU
+    accumulates the same per-voxel float terms in double and rounds once.  Tested bounds:
+      |gpu - exact| <= 1 ulp(exact) + 2^-24 * sum|terms| * 1e-6     (GPU is accurate)
+      |gpu - oracle| <= n * 2^-24 * sum|terms| + 1 ulp                (serial error bound)
+    where exact is a float64 sum of the same float32 terms.
+The oracle itself is pinned here against numpy's sequential float32 accumulation
+(np.add.accumulate is strictly left-to-right) and a float32 restatement of the bin formula.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from oracle import binding as ob
+
+vkt = pytest.importorskip("volkit_amd.volkit")
+from volkit_amd import _lib  # noqa: E402
+from volkit_amd._lib import lib  # noqa: E402
+
+F32 = np.float32
+EPS = 2.0 ** -24
+
+
+def values_of(codes, fmt, lo, hi):
+    """Unmapped float32 values of a code array through the oracle codec (vectorised for the
+    formats used here)."""
+    if fmt == 7:
+        return codes.view(np.float32)
+    flat = codes.reshape(-1)
+    uniq, inv = np.unique(flat, return_inverse=True)
+    vals = np.array([ob.unmap_voxel(int(c).to_bytes(ob.BPV[fmt], "little"), fmt, lo, hi) for c in uniq],
+                    dtype=np.float32)
+    return vals[inv].reshape(codes.shape)
+
+
+# ---- oracle pinning (CPU) -----------------------------------------------------------------
+def test_oracle_aggregates_follow_sequential_float32():
+    rng = np.random.default_rng(1)
+    codes = rng.integers(0, 65536, (6, 7, 9), dtype=np.uint16)
+    v = ob.Volume(codes, 5, -1.0, 3.0)
+    first, last = (1, 2, 0), (8, 7, 5)
+    a = ob.aggregates_range(v, first, last)
+    vals = values_of(codes, 5, -1.0, 3.0)[first[2]:last[2], first[1]:last[1], first[0]:last[0]].reshape(-1)
+    seq = np.add.accumulate(vals, dtype=np.float32)[-1]
+    assert a.sum == seq
+    n = codes.size
+    mean = F32(np.float64(seq) / n)
+    assert a.mean == mean
+    d = (vals - mean).astype(np.float32)
+    var_acc = np.add.accumulate((d * d).astype(np.float32), dtype=np.float32)[-1]
+    assert a.var == F32(np.float64(var_acc) / n)
+    assert a.prod == np.multiply.accumulate(vals, dtype=np.float32)[-1]
+    i = int(np.argmin(vals))   # first occurrence in z, y, x order
+    box = (last[0] - first[0], last[1] - first[1])
+    assert list(a.argmin) == [first[0] + i % box[0], first[1] + (i // box[0]) % box[1], first[2] + i // (box[0] * box[1])]
+
+
+def test_oracle_histogram_formula():
+    rng = np.random.default_rng(2)
+    vals = rng.uniform(-0.2, 1.2, (5, 6, 7)).astype(np.float32)
+    vals.reshape(-1)[:4] = [np.nan, np.inf, -0.0, 1.0]
+    v = ob.Volume(vals.view(np.uint32), 7, 0.0, 1.0)
+    bins, skipped = ob.histogram_range(v, (0, 0, 0), (7, 6, 5), 10)
+    f = (vals.reshape(-1) - F32(0.0)) * (F32(10) / (F32(1.0) - F32(0.0)))
+    ok = (f > -1) & (f < 10)
+    assert skipped == int((~ok).sum())
+    np.testing.assert_array_equal(bins, np.bincount(np.trunc(f[ok]).astype(np.int64), minlength=10))
+
+
+def test_cpu_policy_is_refused():
+    v = vkt.StructuredVolume(4, 4, 4, vkt.DataFormat_UInt8)
+    assert vkt.ComputeAggregates(v, vkt.Aggregates()) == vkt.InvalidValue
+    assert vkt.ComputeHistogram(v, vkt.Histogram(8)) == vkt.InvalidValue
+
+
+def test_partial_combine_is_associative_and_tie_breaks_on_index():
+    P = _lib.HipAggregatePartial_t
+
+    def part(mn, mi, mx, xi, s, n):
+        p = P()
+        lib.vktHipAggregatePartialInit(C.byref(p))
+        p.minValue, p.minIndex, p.maxValue, p.maxIndex, p.sum, p.count = mn, mi, mx, xi, s, n
+        p.prod = 2.0
+        return p
+
+    a, b, c = part(1.0, 50, 5.0, 7, 1.5, 3), part(1.0, 20, 5.0, 9, 2.5, 4), part(0.5, 90, 4.0, 1, -1.0, 5)
+    acc = P()
+    lib.vktHipAggregatePartialInit(C.byref(acc))
+    for p in (a, b):
+        lib.vktHipAggregatePartialCombine(C.byref(acc), C.byref(p))
+    assert (acc.minValue, acc.minIndex, acc.maxValue, acc.maxIndex) == (1.0, 20, 5.0, 7)
+    lib.vktHipAggregatePartialCombine(C.byref(acc), C.byref(c))
+    assert (acc.minValue, acc.minIndex, acc.sum, acc.count, acc.prod) == (0.5, 90, 3.0, 12, 8.0)
+    out = _lib.Aggregates_t()
+    lib.vktHipAggregatesFinish(C.byref(acc), C.byref(acc), 100, 10, 3, C.byref(out))
+    assert (out.argmin.x, out.argmin.y, out.argmin.z) == (0, 0, 3)    # 90 = 3*30 + 0*10 + 0
+    assert (out.argmax.x, out.argmax.y, out.argmax.z) == (7, 0, 0)
+
+
+# ---- GPU parity -----------------------------------------------------------------------------
+def set_device(dev):
+    ep = vkt.GetThreadExecutionPolicy()
+    ep.device = dev
+    vkt.SetThreadExecutionPolicy(ep)
+
+
+def gpu_volume(codes, fmt, lo, hi):
+    z, y, x = codes.shape
+    set_device(vkt.ExecutionPolicy.Device_CPU)
+    v = vkt.StructuredVolume(x, y, z, fmt, 1.0, 1.0, 1.0, lo, hi)
+    v.from_numpy(codes)
+    return v
+
+
+def gpu_aggregates(codes, fmt, lo, hi, first, last):
+    v = gpu_volume(codes, fmt, lo, hi)
+    a = vkt.Aggregates()
+    set_device(vkt.ExecutionPolicy.Device_GPU)
+    try:
+        err = vkt.ComputeAggregatesRange(v, a, *first, *last)
+    finally:
+        set_device(vkt.ExecutionPolicy.Device_CPU)
+    assert err == vkt.NoError, vkt.last_error()
+    return a
+
+
+def gpu_histogram(codes, fmt, lo, hi, first, last, nbins):
+    v = gpu_volume(codes, fmt, lo, hi)
+    h = vkt.Histogram(nbins)
+    set_device(vkt.ExecutionPolicy.Device_GPU)
+    try:
+        err = vkt.ComputeHistogramRange(v, h, *first, *last)
+    finally:
+        set_device(vkt.ExecutionPolicy.Device_CPU)
+    assert err == vkt.NoError, vkt.last_error()
+    return h.getBinCounts()    # migrates back under the CPU policy
+
+
+def rand_codes(rng, fmt, shape, specials=False):
+    if fmt == 7:
+        vals = rng.uniform(-1.5, 2.5, shape).astype(np.float32)
+        if specials:
+            flat = vals.reshape(-1)
+            k = min(12, flat.size)
+            idx = rng.choice(flat.size, k, replace=False)
+            flat[idx] = np.resize(np.array([np.nan, np.inf, -np.inf, -0.0, 3e38, -3e38], np.float32), k)
+        return vals.view(np.uint32)
+    info = np.iinfo(ob.CODE_DTYPE[fmt])
+    return rng.integers(0, int(info.max) + 1, shape, dtype=np.uint64).astype(ob.CODE_DTYPE[fmt])
+
+
+CASES = [
+    ((40, 30, 20), (0, 0, 0), (40, 30, 20)),
+    ((40, 30, 20), (3, 5, 2), (37, 29, 19)),
+    ((129, 3, 70), (1, 0, 10), (129, 3, 11)),
+    ((1, 1, 1), (0, 0, 0), (1, 1, 1)),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fmt", [4, 5, 2, 6, 7])
+@pytest.mark.parametrize("mapping", [(0.0, 1.0), (-1.0, 3.0)])
+@pytest.mark.parametrize("nbins", [1, 7, 256, 1000, 20000])
+def test_histogram_parity(fmt, mapping, nbins):
+    rng = np.random.default_rng(fmt * 7 + nbins)
+    for dims, first, last in CASES:
+        codes = rand_codes(rng, fmt, dims[::-1], specials=True)
+        got = gpu_histogram(codes, fmt, *mapping, first, last, nbins)
+        ref, _ = ob.histogram_range(ob.Volume(codes, fmt, *mapping), first, last, nbins)
+        np.testing.assert_array_equal(got, ref, err_msg=f"dims={dims} {first}->{last}")
+
+
+@pytest.mark.gpu
+def test_histogram_constant_volume_and_reference_example():
+    """Wave-uniform bins (one atomic per wave) and src/examples/Histogram.cpp's 256 bins."""
+    codes = np.full((33, 65, 130), 200, np.uint8)
+    got = gpu_histogram(codes, 4, 0.0, 1.0, (0, 0, 0), (130, 65, 33), 256)
+    ref, _ = ob.histogram_range(ob.Volume(codes, 4), (0, 0, 0), (130, 65, 33), 256)
+    np.testing.assert_array_equal(got, ref)
+    assert got.sum() == codes.size
+
+
+def check_float(name, gpu, oracle, exact, terms_abs_sum, n):
+    ulp = float(np.spacing(np.float32(abs(exact)))) if np.isfinite(exact) else 0.0
+    assert abs(gpu - exact) <= ulp + 1e-6 * EPS * terms_abs_sum, f"{name}: gpu {gpu} vs exact {exact}"
+    assert abs(gpu - oracle) <= n * EPS * terms_abs_sum + ulp, f"{name}: gpu {gpu} vs oracle {oracle}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fmt,mapping", [(4, (0.0, 1.0)), (5, (-1.0, 3.0)), (2, (0.0, 1.0)), (7, (0.0, 1.0)),
+                                         (6, (0.25, 7.5))])
+def test_aggregates_parity(fmt, mapping):
+    rng = np.random.default_rng(fmt)
+    for dims, first, last in CASES:
+        codes = rand_codes(rng, fmt, dims[::-1])
+        got = gpu_aggregates(codes, fmt, *mapping, first, last)
+        ref = ob.aggregates_range(ob.Volume(codes, fmt, *mapping), first, last)
+        what = f"fmt={fmt} dims={dims} {first}->{last}"
+        assert (got.min, got.max) == (ref.min, ref.max), what
+        assert tuple(got.argmin) == tuple(ref.argmin) and tuple(got.argmax) == tuple(ref.argmax), what
+        vals = values_of(codes, fmt, *mapping)[first[2]:last[2], first[1]:last[1], first[0]:last[0]].reshape(-1)
+        n, nall = vals.size, codes.size
+        exact_sum = float(np.sum(vals, dtype=np.float64))
+        abs_sum = float(np.sum(np.abs(vals), dtype=np.float64))
+        check_float("sum", got.sum, ref.sum, exact_sum, abs_sum, n)
+        assert got.mean == np.float32(np.float64(np.float32(got.sum)) / nall), what
+        d = (vals - np.float32(got.mean)).astype(np.float32)
+        d2 = (d * d).astype(np.float32)
+        exact_var = float(np.float32(np.float64(np.float32(np.sum(d2, dtype=np.float64))) / nall))
+        assert abs(got.var - exact_var) <= float(np.spacing(np.float32(exact_var))), what
+        assert abs(got.var - ref.var) <= n * EPS * 4 * (abs(ref.var) + 1e-30) + float(np.spacing(np.float32(ref.var)))
+        assert got.stddev == np.float32(np.sqrt(np.float32(got.var))), what
+
+
+@pytest.mark.gpu
+def test_aggregates_ties_specials_and_whole_volume_mean():
+    # duplicate minima / maxima: first occurrence in z, y, x order; NaN never min / max;
+    # +-inf: -inf < FLT_MAX and +inf > -FLT_MAX, so both qualify (the reference starts from
+    # +-FLT_MAX); NaN never compares
+    vals = np.full((6, 5, 4), 0.5, np.float32)
+    vals[1, 2, 3] = vals[4, 0, 0] = -2.0
+    vals[2, 1, 1] = vals[0, 4, 3] = 7.0
+    vals[3, 3, 3] = np.nan
+    codes = vals.view(np.uint32)
+    got = gpu_aggregates(codes, 7, 0.0, 1.0, (0, 0, 0), (4, 5, 6))
+    ref = ob.aggregates_range(ob.Volume(codes, 7), (0, 0, 0), (4, 5, 6))
+    assert (got.min, tuple(got.argmin), got.max, tuple(got.argmax)) == (-2.0, (3, 2, 1), 7.0, (3, 4, 0))
+    assert (ref.min, tuple(ref.argmin), ref.max, tuple(ref.argmax)) == (-2.0, (3, 2, 1), 7.0, (3, 4, 0))
+    assert np.isnan(got.sum) and np.isnan(ref.sum)
+    vals2 = np.array([np.inf, -np.inf, np.nan, 1.0], np.float32).reshape(1, 1, 4)
+    got = gpu_aggregates(vals2.view(np.uint32), 7, 0.0, 1.0, (0, 0, 0), (4, 1, 1))
+    ref = ob.aggregates_range(ob.Volume(vals2.view(np.uint32), 7), (0, 0, 0), (4, 1, 1))
+    assert (got.min, tuple(got.argmin), got.max, tuple(got.argmax)) == (ref.min, tuple(ref.argmin), ref.max,
+                                                                        tuple(ref.argmax)) == (-np.inf, (1, 0, 0), np.inf, (0, 0, 0))
+    # all NaN: min stays FLT_MAX, argmin {0,0,0}
+    nan = np.full((1, 2, 3), np.nan, np.float32).view(np.uint32)
+    got = gpu_aggregates(nan, 7, 0.0, 1.0, (0, 0, 0), (3, 2, 1))
+    assert got.min == np.finfo(np.float32).max and tuple(got.argmin) == (0, 0, 0)
+    assert got.max == -np.finfo(np.float32).max and tuple(got.argmax) == (0, 0, 0)
+    # sub-range: mean divides by the WHOLE volume's voxel count (Aggregates_serial.hpp:61-63)
+    codes = np.full((10, 10, 10), 128, np.uint8)
+    got = gpu_aggregates(codes, 4, 0.0, 1.0, (0, 0, 0), (10, 10, 1))
+    ref = ob.aggregates_range(ob.Volume(codes, 4), (0, 0, 0), (10, 10, 1))
+    assert got.mean == np.float32(np.float64(np.float32(got.sum)) / 1000)
+    assert abs(got.mean - ref.mean) <= 100 * EPS * abs(ref.mean)      # serial float sum of 100 terms
+
+
+@pytest.mark.gpu
+def test_aggregate_slab_partials_combine_to_the_whole():
+    """Z-slab partials (multi-GPU building block): two slabs with their global z offset,
+    combined, mean of the whole, pass 2, finish == single-volume result."""
+    rng = np.random.default_rng(3)
+    codes = rng.integers(0, 65536, (20, 17, 33), dtype=np.uint16)
+    whole = gpu_aggregates(codes, 5, -1.0, 3.0, (0, 0, 0), (33, 17, 20))
+    P = _lib.HipAggregatePartial_t
+    slabs = [(0, 7), (7, 20)]
+    vols = [gpu_volume(np.ascontiguousarray(codes[z0:z1]), 5, -1.0, 3.0) for z0, z1 in slabs]
+    set_device(vkt.ExecutionPolicy.Device_GPU)
+    try:
+        acc1 = P()
+        lib.vktHipAggregatePartialInit(C.byref(acc1))
+        for (z0, z1), v in zip(slabs, vols):
+            p = P()
+            assert lib.vktHipAggregatesPass(v.hip_view(), _lib.Vec3i_t(0, 0, 0), _lib.Vec3i_t(33, 17, z1 - z0), z0, 1,
+                                            0.0, C.byref(p)) == 0
+            lib.vktHipAggregatePartialCombine(C.byref(acc1), C.byref(p))
+        mean = lib.vktHipAggregatesMean(C.byref(acc1), codes.size)
+        acc2 = P()
+        lib.vktHipAggregatePartialInit(C.byref(acc2))
+        for (z0, z1), v in zip(slabs, vols):
+            p = P()
+            assert lib.vktHipAggregatesPass(v.hip_view(), _lib.Vec3i_t(0, 0, 0), _lib.Vec3i_t(33, 17, z1 - z0), z0, 2,
+                                            mean, C.byref(p)) == 0
+            lib.vktHipAggregatePartialCombine(C.byref(acc2), C.byref(p))
+    finally:
+        set_device(vkt.ExecutionPolicy.Device_CPU)
+    out = _lib.Aggregates_t()
+    lib.vktHipAggregatesFinish(C.byref(acc1), C.byref(acc2), codes.size, 33, 17, C.byref(out))
+    assert (out.min, out.max) == (whole.min, whole.max)
+    assert (out.argmin.x, out.argmin.y, out.argmin.z) == tuple(whole.argmin)
+    assert (out.argmax.x, out.argmax.y, out.argmax.z) == tuple(whole.argmax)
+    assert out.mean == whole.mean and abs(out.var - whole.var) <= float(np.spacing(np.float32(whole.var)))

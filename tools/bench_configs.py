@@ -126,6 +126,25 @@ def main():
             del arr, V
         ep.device = vkt.ExecutionPolicy.Device_CPU
         vkt.SetThreadExecutionPolicy(ep)
+    if want("reduce"):
+        # ComputeHistogram / ComputeAggregates on a device-resident 1024^3 UInt16
+        n = 1024
+        V = alloc((n,) * 3, 5, seed=11)
+        last = Vec3i_t(n, n, n)
+        bins = C.c_void_p()
+        lib.vktHipAllocate(C.byref(bins), 65536 * 8)
+        for nb in (256, 4096, 65536):
+            ms = timed(lambda: lib.vktHipHistogramRange(V, o, last, bins, nb, 0), R)
+            report(f"reduce Histogram 1024^3 UInt16 {nb} bins", ms, 2 * n ** 3, n ** 3)
+        Vc = alloc((n,) * 3, 5)
+        lib.vktHipFillRange(Vc, o, last, C.c_float(0.5))
+        ms = timed(lambda: lib.vktHipHistogramRange(Vc, o, last, bins, 256, 0), R)
+        report("reduce Histogram 1024^3 UInt16 256 bins, constant volume", ms, 2 * n ** 3, n ** 3)
+        agg = _lib.Aggregates_t()
+        ms = timed(lambda: lib.vktHipAggregatesRange(V, o, last, C.byref(agg)), R)
+        report("reduce Aggregates 1024^3 UInt16 (2 passes, incl. D2H of the result)", ms, 2 * 2 * n ** 3, n ** 3)
+        free(V, Vc)
+        lib.vktHipFree(bins)
     if not want("metric"):
         return
 

@@ -68,6 +68,17 @@ class HipBrickRange_t(C.Structure):
 
 
 c_arr = C.c_void_p            # vktArray3D_vktStructuredVolume (opaque handle)
+c_hist = C.c_void_p           # vktHistogram (opaque handle)
+
+
+class Aggregates_t(C.Structure):
+    _fields_ = [("min", f32), ("max", f32), ("mean", f32), ("stddev", f32), ("var", f32), ("sum", f32),
+                ("prod", f32), ("argmin", Vec3i_t), ("argmax", Vec3i_t)]
+
+
+class HipAggregatePartial_t(C.Structure):
+    _fields_ = [("sum", C.c_double), ("prod", C.c_double), ("sumSq", C.c_double), ("minValue", f32),
+                ("maxValue", f32), ("minIndex", u64), ("maxIndex", u64), ("count", u64)]
 
 UnaryOp = C.CFUNCTYPE(None, i32, i32, i32, VoxelView_t)
 BinaryOp = C.CFUNCTYPE(None, i32, i32, i32, VoxelView_t, VoxelView_t)
@@ -182,6 +193,23 @@ SIGNATURES = {
     "vktArray3D_vktStructuredVolume_Dims": (Vec3i_t, [c_arr]),
     "vktArray3D_vktStructuredVolume_NumElements": (C.c_size_t, [c_arr]),
     "vktBrickDecomposeSV": (c_err, [c_arr, c_vol] + _R9),
+    # Aggregates.h / Histogram (C entry points added by this library)
+    "vktComputeAggregatesSV": (c_err, [c_vol, P(Aggregates_t)]),
+    "vktComputeAggregatesRangeSV": (c_err, [c_vol, P(Aggregates_t), i32, i32, i32, i32, i32, i32]),
+    "vktHistogramCreate": (None, [P(c_hist), C.c_size_t]),
+    "vktHistogramDestroy": (None, [c_hist]),
+    "vktHistogramGetNumBins": (C.c_size_t, [c_hist]),
+    "vktHistogramGetBinCounts": (C.c_void_p, [c_hist]),
+    "vktComputeHistogramSV": (c_err, [c_vol, c_hist]),
+    "vktComputeHistogramRangeSV": (c_err, [c_vol, c_hist, i32, i32, i32, i32, i32, i32]),
+    "vktHipAggregatesRange": (c_err, [HipVolumeView_t, Vec3i_t, Vec3i_t, P(Aggregates_t)]),
+    "vktHipAggregatePartialInit": (c_err, [P(HipAggregatePartial_t)]),
+    "vktHipAggregatePartialCombine": (c_err, [P(HipAggregatePartial_t), P(HipAggregatePartial_t)]),
+    "vktHipAggregatesMean": (f32, [P(HipAggregatePartial_t), u64]),
+    "vktHipAggregatesPass": (c_err, [HipVolumeView_t, Vec3i_t, Vec3i_t, i32, i32, f32, P(HipAggregatePartial_t)]),
+    "vktHipAggregatesFinish": (c_err, [P(HipAggregatePartial_t), P(HipAggregatePartial_t), u64, i32, i32,
+                                       P(Aggregates_t)]),
+    "vktHipHistogramRange": (c_err, [HipVolumeView_t, Vec3i_t, Vec3i_t, C.c_void_p, u64, i32]),
     "vktBrickDecomposeResizeSV": (c_err, [c_arr, c_vol] + _R9),
 }
 for _op in ARITH_OPS:

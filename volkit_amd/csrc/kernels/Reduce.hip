@@ -1,0 +1,565 @@
+// Reduce.hip -- ComputeAggregates / ComputeHistogram on gfx950.
+//
+// Reference semantics (the serial path; the CUDA Aggregates is a missing stub and the CUDA
+// Histogram ignores `first`, src/vkt/Histogram_cuda.cu:27-40):
+//  * ComputeAggregatesRange_serial (src/vkt/Aggregates_serial.hpp:20-83): min/max updated on
+//    a strict `<` / `>` in z->y->x order starting from +FLT_MAX / -FLT_MAX (so NaN and values
+//    at or beyond +-FLT_MAX never become min/max; argmin/argmax = first occurrence, {0,0,0}
+//    if none); mean and sum = float accumulation of the values; prod = float product;
+//    mean /= N and var = sum((v - mean)^2) / N where N is the voxel count of the WHOLE volume
+//    (not the range; :61-63, :80); stddev = sqrtf(var).
+//  * ComputeHistogramRange_serial (src/vkt/Histogram_serial.hpp:20-50): bins zeroed, then
+//    bins[(size_t)((v - lo) * (numBins / (hi - lo)))]++ with float arithmetic.
+//
+// Exactness: min/max/argmin/argmax and every histogram count are bit-exact.  The float sums
+// of the reference are order-dependent; here sum, prod and sum((v-mean)^2) accumulate the same
+// per-voxel float terms in double precision with a deterministic tree (run-to-run identical)
+// and round once -- equal to the serial result within the serial path's own rounding error
+// (tests state the bound).  Histogram indices outside [0, numBins) and NaN, which the
+// reference writes out of bounds (UB), are not counted.
+//
+// MI355X design: one wave per range row (x across lanes, coalesced), grid-stride over rows
+// with ~8 workgroups per CU; per-wave shuffle reductions, LDS across waves, one partial per
+// workgroup, a single-workgroup tree for the final result (no float atomics: deterministic).
+// Histogram: per-workgroup LDS bins (u32) when they fit, flushed with 64-bit global atomics;
+// a wave whose 64 voxels fall into one bin adds them with one atomic.
+
+#include "KernelCommon.hpp"
+#include "../runtime/Runtime.hpp"
+#include "volkit_hip.h"
+
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+
+namespace vkt
+{
+namespace hipk
+{
+    bool validView(vktHipVolumeView_t const& v);
+
+    struct BoxArgs
+    {
+        uint8_t const* data;
+        int32_t dimX, dimY;         // volume pitch
+        int32_t fx, fy, fz;         // range origin (voxel coordinates of the local buffer)
+        int32_t nx;
+        uint32_t rows;              // ny * nz
+        FastDiv fdNy;
+        int32_t fmt;
+        float lo, hi;
+        int64_t zGlobal;            // added to z for global linear indices (Z-slab offset)
+    };
+
+    __device__ __forceinline__ float valueAt(BoxArgs const& a, uint64_t voxel, uint32_t bpv)
+    {
+        return codec::decode(loadCodeDyn(a.data, voxel, bpv), a.fmt, a.lo, a.hi);
+    }
+
+    // ---- Aggregates ---------------------------------------------------------------------
+    constexpr uint64_t kNoIndex = ~0ull;
+
+    __device__ __forceinline__ void minCombine(float& v, uint64_t& i, float v2, uint64_t i2)
+    {
+        if (v2 < v || (v2 == v && i2 < i))
+        {
+            v = v2;
+            i = i2;
+        }
+    }
+
+    __device__ __forceinline__ void maxCombine(float& v, uint64_t& i, float v2, uint64_t i2)
+    {
+        if (v2 > v || (v2 == v && i2 < i))
+        {
+            v = v2;
+            i = i2;
+        }
+    }
+
+    __device__ __forceinline__ double shflXorD(double v, int m)
+    {
+        return __shfl_xor(v, m);
+    }
+
+    __device__ __forceinline__ uint64_t shflXorU(uint64_t v, int m)
+    {
+        uint32_t lo = __shfl_xor(static_cast<uint32_t>(v), m);
+        uint32_t hi = __shfl_xor(static_cast<uint32_t>(v >> 32), m);
+        return (static_cast<uint64_t>(hi) << 32) | lo;
+    }
+
+    // Whole-wave / workgroup reduction of a partial (lane 0 of the block ends with it).
+    __device__ void blockReduce(vktHipAggregatePartial_t& p)
+    {
+        for (int m = 32; m >= 1; m >>= 1)
+        {
+            float mv = __shfl_xor(p.minValue, m), xv = __shfl_xor(p.maxValue, m);
+            uint64_t mi = shflXorU(p.minIndex, m), xi = shflXorU(p.maxIndex, m);
+            double s = shflXorD(p.sum, m), q = shflXorD(p.prod, m), s2 = shflXorD(p.sumSq, m);
+            uint64_t c = shflXorU(p.count, m);
+            minCombine(p.minValue, p.minIndex, mv, mi);
+            maxCombine(p.maxValue, p.maxIndex, xv, xi);
+            p.sum += s;
+            p.prod *= q;
+            p.sumSq += s2;
+            p.count += c;
+        }
+        __shared__ vktHipAggregatePartial_t lds[kBlock / 64];
+        int const wave = threadIdx.x >> 6;
+        if ((threadIdx.x & 63) == 0)
+            lds[wave] = p;
+        __syncthreads();
+        if (threadIdx.x == 0)
+        {
+            for (int w = 1; w < static_cast<int>(blockDim.x >> 6); ++w)
+            {
+                vktHipAggregatePartial_t const& o = lds[w];
+                minCombine(p.minValue, p.minIndex, o.minValue, o.minIndex);
+                maxCombine(p.maxValue, p.maxIndex, o.maxValue, o.maxIndex);
+                p.sum += o.sum;
+                p.prod *= o.prod;
+                p.sumSq += o.sumSq;
+                p.count += o.count;
+            }
+        }
+    }
+
+    __device__ __forceinline__ vktHipAggregatePartial_t emptyPartial()
+    {
+        vktHipAggregatePartial_t p;
+        p.sum = 0.0;
+        p.prod = 1.0;
+        p.sumSq = 0.0;
+        p.minValue = FLT_MAX;
+        p.maxValue = -FLT_MAX;
+        p.minIndex = kNoIndex;
+        p.maxIndex = kNoIndex;
+        p.count = 0;
+        return p;
+    }
+
+    // PASS 1: min/argmin/max/argmax/sum/prod/count.  PASS 2: sumSq of (v - mean)^2 with the
+    // float difference and square of the reference, mean read from `meanPtr` (device) when
+    // non-null, else `meanValue`.
+    template <int PASS>
+    __global__ __launch_bounds__(kBlock) void aggregatesKernel(BoxArgs a, float const* meanPtr, float meanValue,
+                                                              vktHipAggregatePartial_t* partials)
+    {
+        uint32_t const bpv = codec::bytesPerVoxel(a.fmt);
+        int const lane = threadIdx.x & 63;
+        uint32_t const wavesPerBlock = blockDim.x >> 6;
+        uint32_t const totalWaves = gridDim.x * wavesPerBlock;
+        float const mean = PASS == 2 ? (meanPtr ? *meanPtr : meanValue) : 0.f;
+        vktHipAggregatePartial_t p = emptyPartial();
+        for (uint32_t r = blockIdx.x * wavesPerBlock + (threadIdx.x >> 6); r < a.rows; r += totalWaves)
+        {
+            uint32_t const zr = fdiv(r, a.fdNy);
+            uint32_t const yr = r - zr * a.fdNy.d;
+            int64_t const z = a.fz + static_cast<int64_t>(zr), y = a.fy + static_cast<int64_t>(yr);
+            uint64_t const rowBase = (static_cast<uint64_t>(z) * static_cast<uint64_t>(a.dimY) + static_cast<uint64_t>(y)) *
+                                     static_cast<uint64_t>(a.dimX);
+            uint64_t const globalRowBase =
+                (static_cast<uint64_t>(z + a.zGlobal) * static_cast<uint64_t>(a.dimY) + static_cast<uint64_t>(y)) *
+                static_cast<uint64_t>(a.dimX);
+            for (int32_t x = lane; x < a.nx; x += 64)
+            {
+                uint64_t const xx = static_cast<uint64_t>(a.fx + x);
+                float const v = valueAt(a, rowBase + xx, bpv);
+                if constexpr (PASS == 1)
+                {
+                    uint64_t const gi = globalRowBase + xx;
+                    if (v < FLT_MAX)
+                        minCombine(p.minValue, p.minIndex, v, gi);
+                    if (v > -FLT_MAX)
+                        maxCombine(p.maxValue, p.maxIndex, v, gi);
+                    p.sum += static_cast<double>(v);
+                    p.prod *= static_cast<double>(v);
+                    p.count += 1;
+                }
+                else
+                {
+                    float const d = v - mean;
+                    float const d2 = d * d;
+                    p.sumSq += static_cast<double>(d2);
+                }
+            }
+        }
+        blockReduce(p);
+        if (threadIdx.x == 0)
+            partials[blockIdx.x] = p;
+    }
+
+    // One workgroup reduces n partials into out[0]; optionally derives the reference's float
+    // mean for pass 2: mean = (float)((double)(float)sum / numElems).
+    __global__ __launch_bounds__(kBlock) void aggregatesFinalKernel(vktHipAggregatePartial_t const* partials,
+                                                                   uint32_t n, vktHipAggregatePartial_t* out,
+                                                                   float* meanOut, double numElems)
+    {
+        vktHipAggregatePartial_t p = emptyPartial();
+        for (uint32_t i = threadIdx.x; i < n; i += blockDim.x)
+        {
+            vktHipAggregatePartial_t const& o = partials[i];
+            minCombine(p.minValue, p.minIndex, o.minValue, o.minIndex);
+            maxCombine(p.maxValue, p.maxIndex, o.maxValue, o.maxIndex);
+            p.sum += o.sum;
+            p.prod *= o.prod;
+            p.sumSq += o.sumSq;
+            p.count += o.count;
+        }
+        blockReduce(p);
+        if (threadIdx.x == 0)
+        {
+            *out = p;
+            if (meanOut)
+                *meanOut = static_cast<float>(static_cast<double>(static_cast<float>(p.sum)) / numElems);
+        }
+    }
+
+    // ---- Histogram ----------------------------------------------------------------------
+    struct HistArgs
+    {
+        unsigned long long* bins;
+        uint64_t numBins;
+        float scale;                // (float)numBins / (hi - lo), as the reference computes it
+        int32_t useLds;
+    };
+
+    // bin of one value, or ~0 when the reference would index out of bounds / NaN
+    __device__ __forceinline__ uint64_t binOf(float v, float lo, float scale, uint64_t numBins)
+    {
+        float const f = (v - lo) * scale;
+        // (size_t)f on x86-64: truncation toward zero; (-1, 0) -> 0; NaN / negative -> OOB
+        if (!(f > -1.0f) || !(f < 9.2233720e18f))
+            return ~0ull;
+        uint64_t const b = static_cast<uint64_t>(static_cast<int64_t>(f));
+        return b < numBins ? b : ~0ull;
+    }
+
+    constexpr uint32_t kMaxLdsBins = 16384;   // 64 KiB of u32 counters per workgroup
+
+    __global__ __launch_bounds__(kBlock) void histogramKernel(BoxArgs a, HistArgs h)
+    {
+        extern __shared__ uint32_t ldsBins[];
+        uint32_t const bpv = codec::bytesPerVoxel(a.fmt);
+        int const lane = threadIdx.x & 63;
+        uint32_t const nb = static_cast<uint32_t>(h.numBins);
+        if (h.useLds)
+        {
+            for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x)
+                ldsBins[i] = 0;
+            __syncthreads();
+        }
+        uint32_t const wavesPerBlock = blockDim.x >> 6;
+        uint32_t const totalWaves = gridDim.x * wavesPerBlock;
+        for (uint32_t r = blockIdx.x * wavesPerBlock + (threadIdx.x >> 6); r < a.rows; r += totalWaves)
+        {
+            uint32_t const zr = fdiv(r, a.fdNy);
+            uint32_t const yr = r - zr * a.fdNy.d;
+            uint64_t const rowBase = (static_cast<uint64_t>(a.fz + static_cast<int64_t>(zr)) * static_cast<uint64_t>(a.dimY) +
+                                      static_cast<uint64_t>(a.fy + static_cast<int64_t>(yr))) *
+                                         static_cast<uint64_t>(a.dimX) +
+                                     static_cast<uint64_t>(a.fx);
+            for (int32_t x0 = 0; x0 < a.nx; x0 += 64)
+            {
+                int32_t const x = x0 + lane;
+                uint64_t b = ~0ull;
+                if (x < a.nx)
+                    b = binOf(valueAt(a, rowBase + static_cast<uint64_t>(x), bpv), a.lo, h.scale, h.numBins);
+                // one bin for the whole wave (constant regions): a single atomic
+                uint64_t const b0 = (static_cast<uint64_t>(__shfl(static_cast<uint32_t>(b >> 32), 0)) << 32) |
+                                    __shfl(static_cast<uint32_t>(b), 0);
+                uint64_t const same = __ballot(b == b0);
+                uint64_t const live = __ballot(x < a.nx);
+                if (same == ~0ull || (same & live) == live)
+                {
+                    if (lane == 0 && b0 != ~0ull)
+                    {
+                        uint32_t const n = static_cast<uint32_t>(__popcll(live));
+                        if (h.useLds)
+                            atomicAdd(&ldsBins[static_cast<uint32_t>(b0)], n);
+                        else
+                            atomicAdd(&h.bins[b0], static_cast<unsigned long long>(n));
+                    }
+                    continue;
+                }
+                if (b != ~0ull)
+                {
+                    if (h.useLds)
+                        atomicAdd(&ldsBins[static_cast<uint32_t>(b)], 1u);
+                    else
+                        atomicAdd(&h.bins[b], 1ull);
+                }
+            }
+        }
+        if (h.useLds)
+        {
+            __syncthreads();
+            for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x)
+            {
+                uint32_t const c = ldsBins[i];
+                if (c)
+                    atomicAdd(&h.bins[i], static_cast<unsigned long long>(c));
+            }
+        }
+    }
+
+    __global__ void zeroU64Kernel(unsigned long long* p, uint64_t n)
+    {
+        uint64_t const i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+        if (i < n)
+            p[i] = 0ull;
+    }
+
+    // ---- host helpers -------------------------------------------------------------------
+    bool makeBox(vktHipVolumeView_t const& v, vktVec3i_t first, vktVec3i_t last, int64_t zGlobal, BoxArgs& a,
+                 char const* what, vktError& err)
+    {
+        err = vktNoError;
+        if (!validView(v))
+        {
+            err = rt::fail(what);
+            return false;
+        }
+        int64_t nx = int64_t(last.x) - first.x, ny = int64_t(last.y) - first.y, nz = int64_t(last.z) - first.z;
+        if (nx <= 0 || ny <= 0 || nz <= 0)
+            return false;   // empty range: nothing to read
+        if (first.x < 0 || first.y < 0 || first.z < 0 || last.x > v.dimX || last.y > v.dimY || last.z > v.dimZ)
+        {
+            err = rt::fail("range outside the volume (the reference reads out of bounds)");
+            return false;
+        }
+        if (ny * nz >= (1ll << 32))
+        {
+            err = rt::fail("range has too many rows");
+            return false;
+        }
+        a.data = v.data;
+        a.dimX = v.dimX;
+        a.dimY = v.dimY;
+        a.fx = first.x;
+        a.fy = first.y;
+        a.fz = first.z;
+        a.nx = static_cast<int32_t>(nx);
+        a.rows = static_cast<uint32_t>(ny * nz);
+        a.fdNy = makeFastDiv(static_cast<uint32_t>(ny));
+        a.fmt = v.dataFormat;
+        a.lo = v.mappingLo;
+        a.hi = v.mappingHi;
+        a.zGlobal = zGlobal;
+        return true;
+    }
+
+    unsigned rowGrid(uint32_t rows) { return streamingGrid(rows, kBlock / 64, 8); }
+
+    struct AggScratch
+    {
+        rt::StreamScratch dev;
+        vktHipAggregatePartial_t* host = nullptr;   // pinned: [0] pass 1, [1] pass 2
+    };
+
+    AggScratch& aggScratch()
+    {
+        static AggScratch s;
+        return s;
+    }
+
+} // hipk
+} // vkt
+
+using namespace vkt;
+using namespace vkt::hipk;
+
+extern "C" {
+
+vktError vktHipAggregatePartialInit(vktHipAggregatePartial_t* p)
+{
+    if (!p)
+        return rt::fail("vktHipAggregatePartialInit: null pointer");
+    std::memset(p, 0, sizeof(*p));
+    p->prod = 1.0;
+    p->minValue = FLT_MAX;
+    p->maxValue = -FLT_MAX;
+    p->minIndex = kNoIndex;
+    p->maxIndex = kNoIndex;
+    return vktNoError;
+}
+
+vktError vktHipAggregatePartialCombine(vktHipAggregatePartial_t* acc, vktHipAggregatePartial_t const* other)
+{
+    if (!acc || !other)
+        return rt::fail("vktHipAggregatePartialCombine: null pointer");
+    vktHipAggregatePartial_t const& o = *other;
+    if (o.minValue < acc->minValue || (o.minValue == acc->minValue && o.minIndex < acc->minIndex))
+    {
+        acc->minValue = o.minValue;
+        acc->minIndex = o.minIndex;
+    }
+    if (o.maxValue > acc->maxValue || (o.maxValue == acc->maxValue && o.maxIndex < acc->maxIndex))
+    {
+        acc->maxValue = o.maxValue;
+        acc->maxIndex = o.maxIndex;
+    }
+    acc->sum += o.sum;
+    acc->prod *= o.prod;
+    acc->sumSq += o.sumSq;
+    acc->count += o.count;
+    return vktNoError;
+}
+
+float vktHipAggregatesMean(vktHipAggregatePartial_t const* pass1, uint64_t numElems)
+{
+    return static_cast<float>(static_cast<double>(static_cast<float>(pass1->sum)) / static_cast<double>(numElems));
+}
+
+vktError vktHipAggregatesPass(vktHipVolumeView_t volume, vktVec3i_t first, vktVec3i_t last, int32_t zGlobalOffset,
+                              int32_t pass, float mean, vktHipAggregatePartial_t* out)
+{
+    if (!out || (pass != 1 && pass != 2))
+        return rt::fail("vktHipAggregatesPass: bad arguments");
+    vktHipAggregatePartialInit(out);
+    BoxArgs a{};
+    vktError e;
+    if (!makeBox(volume, first, last, zGlobalOffset, a, "vktHipAggregatesPass: invalid volume view", e))
+        return e;
+    hipStream_t s = rt::computeStream();
+    unsigned const g = rowGrid(a.rows);
+    AggScratch& sc = aggScratch();
+    size_t const bytes = (static_cast<size_t>(g) + 1) * sizeof(vktHipAggregatePartial_t);
+    auto* partials = static_cast<vktHipAggregatePartial_t*>(sc.dev.acquire(bytes, s));
+    if (!partials)
+        return vktInvalidValue;
+    if (!sc.host && rt::check(hipHostMalloc(reinterpret_cast<void**>(&sc.host), 2 * sizeof(vktHipAggregatePartial_t)),
+                              "hipHostMalloc") != vktNoError)
+    {
+        sc.dev.release(s);
+        return vktInvalidValue;
+    }
+    if (pass == 1)
+        hipLaunchKernelGGL(aggregatesKernel<1>, dim3(g), dim3(kBlock), 0, s, a, nullptr, 0.f, partials);
+    else
+        hipLaunchKernelGGL(aggregatesKernel<2>, dim3(g), dim3(kBlock), 0, s, a, nullptr, mean, partials);
+    hipLaunchKernelGGL(aggregatesFinalKernel, dim3(1), dim3(kBlock), 0, s, partials, g, partials + g,
+                       static_cast<float*>(nullptr), 1.0);
+    e = rt::check(hipMemcpyAsync(sc.host, partials + g, sizeof(vktHipAggregatePartial_t), hipMemcpyDeviceToHost, s),
+                  "hipMemcpyAsync(aggregates)");
+    sc.dev.release(s);
+    if (e != vktNoError)
+        return e;
+    VKT_HIP_TRY(hipStreamSynchronize(s));
+    *out = sc.host[0];
+    return rt::finishLaunch("AggregatesPass_hip");
+}
+
+vktError vktHipAggregatesFinish(vktHipAggregatePartial_t const* pass1, vktHipAggregatePartial_t const* pass2,
+                                uint64_t numElems, int32_t dimX, int32_t dimY, vktAggregates_t* out)
+{
+    if (!pass1 || !pass2 || !out)
+        return rt::fail("vktHipAggregatesFinish: null pointer");
+    std::memset(out, 0, sizeof(*out));   // Aggregates_serial.hpp:27
+    auto coords = [&](uint64_t i) {
+        uint64_t const px = static_cast<uint64_t>(dimX), py = static_cast<uint64_t>(dimY);
+        return vktVec3i_t{static_cast<int>(i % px), static_cast<int>((i / px) % py), static_cast<int>(i / (px * py))};
+    };
+    out->min = pass1->minIndex == kNoIndex ? FLT_MAX : pass1->minValue;
+    out->max = pass1->maxIndex == kNoIndex ? -FLT_MAX : pass1->maxValue;
+    if (pass1->minIndex != kNoIndex)
+        out->argmin = coords(pass1->minIndex);
+    if (pass1->maxIndex != kNoIndex)
+        out->argmax = coords(pass1->maxIndex);
+    out->sum = static_cast<float>(pass1->sum);
+    out->prod = pass1->count ? static_cast<float>(pass1->prod) : 1.f;
+    double const n = static_cast<double>(numElems);
+    out->mean = static_cast<float>(static_cast<double>(out->sum) / n);     // mean /= (double)numElems
+    float const varAcc = static_cast<float>(pass2->sumSq);
+    out->var = static_cast<float>(static_cast<double>(varAcc) / n);
+    out->stddev = sqrtf(out->var);
+    return vktNoError;
+}
+
+vktError vktHipAggregatesRange(vktHipVolumeView_t volume, vktVec3i_t first, vktVec3i_t last, vktAggregates_t* out)
+{
+    if (!out)
+        return rt::fail("vktHipAggregatesRange: null pointer");
+    vktHipAggregatePartial_t p1, p2;
+    vktHipAggregatePartialInit(&p1);
+    vktHipAggregatePartialInit(&p2);
+    uint64_t const numElems = static_cast<uint64_t>(volume.dimX > 0 ? volume.dimX : 0) *
+                              static_cast<uint64_t>(volume.dimY > 0 ? volume.dimY : 0) *
+                              static_cast<uint64_t>(volume.dimZ > 0 ? volume.dimZ : 0);
+    BoxArgs a{};
+    vktError e;
+    if (makeBox(volume, first, last, 0, a, "vktHipAggregatesRange: invalid volume view", e))
+    {
+        // both passes and the mean stay on the device: one host round trip at the end
+        hipStream_t s = rt::computeStream();
+        unsigned const g = rowGrid(a.rows);
+        AggScratch& sc = aggScratch();
+        size_t const bytes = (2 * static_cast<size_t>(g) + 2) * sizeof(vktHipAggregatePartial_t) + 16;
+        auto* partials = static_cast<vktHipAggregatePartial_t*>(sc.dev.acquire(bytes, s));
+        if (!partials)
+            return vktInvalidValue;
+        if (!sc.host && rt::check(hipHostMalloc(reinterpret_cast<void**>(&sc.host),
+                                                2 * sizeof(vktHipAggregatePartial_t)),
+                                  "hipHostMalloc") != vktNoError)
+        {
+            sc.dev.release(s);
+            return vktInvalidValue;
+        }
+        vktHipAggregatePartial_t* res = partials + 2 * g;   // [0] pass 1, [1] pass 2
+        float* meanDev = reinterpret_cast<float*>(res + 2);
+        hipLaunchKernelGGL(aggregatesKernel<1>, dim3(g), dim3(kBlock), 0, s, a, nullptr, 0.f, partials);
+        hipLaunchKernelGGL(aggregatesFinalKernel, dim3(1), dim3(kBlock), 0, s, partials, g, res, meanDev,
+                           static_cast<double>(numElems));
+        hipLaunchKernelGGL(aggregatesKernel<2>, dim3(g), dim3(kBlock), 0, s, a, meanDev, 0.f, partials + g);
+        hipLaunchKernelGGL(aggregatesFinalKernel, dim3(1), dim3(kBlock), 0, s, partials + g, g, res + 1,
+                           static_cast<float*>(nullptr), 1.0);
+        e = rt::check(hipMemcpyAsync(sc.host, res, 2 * sizeof(vktHipAggregatePartial_t), hipMemcpyDeviceToHost, s),
+                      "hipMemcpyAsync(aggregates)");
+        sc.dev.release(s);
+        if (e != vktNoError)
+            return e;
+        VKT_HIP_TRY(hipStreamSynchronize(s));
+        p1 = sc.host[0];
+        p2 = sc.host[1];
+        e = rt::finishLaunch("AggregatesRange_hip");
+        if (e != vktNoError)
+            return e;
+    }
+    else if (e != vktNoError)
+        return e;
+    return vktHipAggregatesFinish(&p1, &p2, numElems, volume.dimX, volume.dimY, out);
+}
+
+vktError vktHipHistogramRange(vktHipVolumeView_t volume, vktVec3i_t first, vktVec3i_t last, uint64_t* bins,
+                              uint64_t numBins, int32_t accumulate)
+{
+    if (numBins > 0 && bins == nullptr)
+        return rt::fail("vktHipHistogramRange: null bins");
+    hipStream_t s = rt::computeStream();
+    if (!accumulate && numBins > 0)
+    {
+        unsigned const g = static_cast<unsigned>((numBins + kBlock - 1) / kBlock);
+        hipLaunchKernelGGL(zeroU64Kernel, dim3(g), dim3(kBlock), 0, s, reinterpret_cast<unsigned long long*>(bins),
+                           numBins);
+    }
+    BoxArgs a{};
+    vktError e;
+    if (numBins > 0 && makeBox(volume, first, last, 0, a, "vktHipHistogramRange: invalid volume view", e))
+    {
+        HistArgs h;
+        h.bins = reinterpret_cast<unsigned long long*>(bins);
+        h.numBins = numBins;
+        volatile float range = volume.mappingHi - volume.mappingLo;
+        volatile float nbf = static_cast<float>(numBins);          // size_t -> float
+        h.scale = nbf / range;                                     // numBins / (hi - lo)
+        h.useLds = numBins <= kMaxLdsBins;
+        size_t const lds = h.useLds ? numBins * sizeof(uint32_t) : 0;
+        hipLaunchKernelGGL(histogramKernel, dim3(rowGrid(a.rows)), dim3(kBlock), lds, s, a, h);
+    }
+    else if (numBins > 0 && e != vktNoError)
+        return e;
+    return rt::finishLaunch("HistogramRange_hip");
+}
+
+} // extern "C"

@@ -447,6 +447,85 @@ def BrickDecomposeResize(decomp: Array3D_StructuredVolume, volume: StructuredVol
                                          *_decompose_args("BrickDecomposeResize", args))
 
 
+# ---- Aggregates.hpp / Histogram.hpp ---------------------------------------------------------
+class Aggregates:
+    """SWIG's ``vkt.Aggregates()`` (reference include/cpp/vkt/Aggregates.hpp:14-25)."""
+
+    __slots__ = ("min", "max", "mean", "stddev", "var", "sum", "prod", "argmin", "argmax")
+
+    def __init__(self):
+        self.min = self.max = self.mean = self.stddev = self.var = self.sum = self.prod = 0.0
+        self.argmin, self.argmax = Vec3i(), Vec3i()
+
+    def _set(self, c: "_lib.Aggregates_t"):
+        self.min, self.max, self.mean, self.stddev = c.min, c.max, c.mean, c.stddev
+        self.var, self.sum, self.prod = c.var, c.sum, c.prod
+        self.argmin = Vec3i(c.argmin.x, c.argmin.y, c.argmin.z)
+        self.argmax = Vec3i(c.argmax.x, c.argmax.y, c.argmax.z)
+
+
+def ComputeAggregates(volume: StructuredVolume, aggregates: Aggregates) -> int:
+    c = _lib.Aggregates_t()
+    err = lib.vktComputeAggregatesSV(volume.handle, C.byref(c))
+    if err == NoError:
+        aggregates._set(c)
+    return err
+
+
+def ComputeAggregatesRange(volume: StructuredVolume, aggregates: Aggregates, *coords) -> int:
+    f = _ints(coords, 6)
+    c = _lib.Aggregates_t()
+    err = lib.vktComputeAggregatesRangeSV(volume.handle, C.byref(c), *f)
+    if err == NoError:
+        aggregates._set(c)
+    return err
+
+
+class Histogram:
+    """vkt::Histogram (reference include/cpp/vkt/Histogram.hpp:14-25): numBins size_t counters
+    in a ManagedBuffer (migrated with the thread policy)."""
+
+    def __init__(self, numBins: int):
+        h = C.c_void_p()
+        lib.vktHistogramCreate(C.byref(h), int(numBins))
+        self._h = h
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            lib.vktHistogramDestroy(h)
+            self._h = None
+
+    @property
+    def handle(self):
+        return self._h
+
+    def getNumBins(self) -> int:
+        return lib.vktHistogramGetNumBins(self._h)
+
+    def getBinCounts(self) -> np.ndarray:
+        """Copy of the bin counts (uint64), read from wherever the policy puts them."""
+        n = self.getNumBins()
+        out = np.zeros(n, dtype=np.uint64)
+        if n == 0:
+            return out
+        ptr = lib.vktHistogramGetBinCounts(self._h)
+        if on_gpu():
+            if lib.vktHipMemcpy(out.ctypes.data, ptr, out.nbytes, CopyKind_DeviceToHost) != NoError:
+                raise RuntimeError(_lib.last_error())
+        else:
+            C.memmove(out.ctypes.data, ptr, out.nbytes)
+        return out
+
+
+def ComputeHistogram(volume: StructuredVolume, histogram: Histogram) -> int:
+    return lib.vktComputeHistogramSV(volume.handle, histogram.handle)
+
+
+def ComputeHistogramRange(volume: StructuredVolume, histogram: Histogram, *coords) -> int:
+    return lib.vktComputeHistogramRangeSV(volume.handle, histogram.handle, *_ints(coords, 6))
+
+
 # ---- backend utilities (include/volkit_hip.h) ----------------------------------------------
 def Synthesize(volume: StructuredVolume, seed: int) -> int:
     """Fill a GPU-resident volume with the counter-based synthetic codes (see volkit_hip.h)."""
