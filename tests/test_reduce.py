@@ -165,7 +165,7 @@ CASES = [
 @pytest.mark.gpu
 @pytest.mark.parametrize("fmt", [4, 5, 2, 6, 7])
 @pytest.mark.parametrize("mapping", [(0.0, 1.0), (-1.0, 3.0)])
-@pytest.mark.parametrize("nbins", [1, 7, 256, 1000, 20000])
+@pytest.mark.parametrize("nbins", [1, 7, 256, 1000, 20000, 65536, 100000, 400000])
 def test_histogram_parity(fmt, mapping, nbins):
     rng = np.random.default_rng(fmt * 7 + nbins)
     for dims, first, last in CASES:

@@ -30,6 +30,7 @@
 
 #include <cfloat>
 #include <cmath>
+#include <algorithm>
 #include <cstring>
 
 namespace vkt
@@ -51,9 +52,51 @@ namespace hipk
         int64_t zGlobal;            // added to z for global linear indices (Z-slab offset)
     };
 
-    __device__ __forceinline__ float valueAt(BoxArgs const& a, uint64_t voxel, uint32_t bpv)
+    // Visits every voxel of the range: one wave per row, grid-stride over rows.  VEC (rows
+    // start on an 8-voxel boundary, row length a multiple of 8, 16-B aligned base): lane l
+    // loads voxels [8l + 512k, +8) with one 8/16/32-byte load, two chunks in flight per lane.
+    // visit(value, x-offset in the row, row base index of the local buffer, z, y).
+    template <int BPV, bool VEC, class Visit>
+    __device__ __forceinline__ void forEachVoxel(BoxArgs const& a, Visit&& visit)
     {
-        return codec::decode(loadCodeDyn(a.data, voxel, bpv), a.fmt, a.lo, a.hi);
+        int const lane = threadIdx.x & 63;
+        uint32_t const wavesPerBlock = blockDim.x >> 6;
+        uint32_t const totalWaves = gridDim.x * wavesPerBlock;
+        for (uint32_t r = blockIdx.x * wavesPerBlock + (threadIdx.x >> 6); r < a.rows; r += totalWaves)
+        {
+            uint32_t const zr = fdiv(r, a.fdNy);
+            uint32_t const yr = r - zr * a.fdNy.d;
+            int64_t const z = a.fz + static_cast<int64_t>(zr), y = a.fy + static_cast<int64_t>(yr);
+            uint64_t const rowBase = (static_cast<uint64_t>(z) * static_cast<uint64_t>(a.dimY) + static_cast<uint64_t>(y)) *
+                                         static_cast<uint64_t>(a.dimX) +
+                                     static_cast<uint64_t>(a.fx);
+            if constexpr (VEC)
+            {
+                for (int32_t x0 = 8 * lane; x0 < a.nx; x0 += 2 * 512)
+                {
+                    uint32_t c0[8], c1[8];
+                    int32_t const x1 = x0 + 512;
+                    bool const has1 = x1 < a.nx;
+                    load8<BPV>(a.data, rowBase + static_cast<uint64_t>(x0), c0);
+                    load8<BPV>(a.data, rowBase + static_cast<uint64_t>(has1 ? x1 : x0), c1);
+#pragma unroll
+                    for (int i = 0; i < 8; ++i)
+                        visit(codec::decode(c0[i], a.fmt, a.lo, a.hi), x0 + i, z, y);
+                    if (has1)
+                    {
+#pragma unroll
+                        for (int i = 0; i < 8; ++i)
+                            visit(codec::decode(c1[i], a.fmt, a.lo, a.hi), x1 + i, z, y);
+                    }
+                }
+            }
+            else
+            {
+                for (int32_t x = lane; x < a.nx; x += 64)
+                    visit(codec::decode(loadCode<BPV>(a.data, rowBase + static_cast<uint64_t>(x)), a.fmt, a.lo, a.hi), x,
+                          z, y);
+            }
+        }
     }
 
     // ---- Aggregates ---------------------------------------------------------------------
@@ -142,49 +185,42 @@ namespace hipk
     // PASS 1: min/argmin/max/argmax/sum/prod/count.  PASS 2: sumSq of (v - mean)^2 with the
     // float difference and square of the reference, mean read from `meanPtr` (device) when
     // non-null, else `meanValue`.
-    template <int PASS>
+    template <int PASS, int BPV, bool VEC>
     __global__ __launch_bounds__(kBlock) void aggregatesKernel(BoxArgs a, float const* meanPtr, float meanValue,
                                                               vktHipAggregatePartial_t* partials)
     {
-        uint32_t const bpv = codec::bytesPerVoxel(a.fmt);
-        int const lane = threadIdx.x & 63;
-        uint32_t const wavesPerBlock = blockDim.x >> 6;
-        uint32_t const totalWaves = gridDim.x * wavesPerBlock;
         float const mean = PASS == 2 ? (meanPtr ? *meanPtr : meanValue) : 0.f;
         vktHipAggregatePartial_t p = emptyPartial();
-        for (uint32_t r = blockIdx.x * wavesPerBlock + (threadIdx.x >> 6); r < a.rows; r += totalWaves)
-        {
-            uint32_t const zr = fdiv(r, a.fdNy);
-            uint32_t const yr = r - zr * a.fdNy.d;
-            int64_t const z = a.fz + static_cast<int64_t>(zr), y = a.fy + static_cast<int64_t>(yr);
-            uint64_t const rowBase = (static_cast<uint64_t>(z) * static_cast<uint64_t>(a.dimY) + static_cast<uint64_t>(y)) *
-                                     static_cast<uint64_t>(a.dimX);
-            uint64_t const globalRowBase =
-                (static_cast<uint64_t>(z + a.zGlobal) * static_cast<uint64_t>(a.dimY) + static_cast<uint64_t>(y)) *
-                static_cast<uint64_t>(a.dimX);
-            for (int32_t x = lane; x < a.nx; x += 64)
+        uint64_t const px = static_cast<uint64_t>(a.dimX), py = static_cast<uint64_t>(a.dimY);
+        forEachVoxel<BPV, VEC>(a, [&](float v, int32_t x, int64_t z, int64_t y) {
+            if constexpr (PASS == 1)
             {
-                uint64_t const xx = static_cast<uint64_t>(a.fx + x);
-                float const v = valueAt(a, rowBase + xx, bpv);
-                if constexpr (PASS == 1)
+                if (v < p.minValue || v > p.maxValue)   // rare after the first voxels: index math only then
                 {
-                    uint64_t const gi = globalRowBase + xx;
-                    if (v < FLT_MAX)
-                        minCombine(p.minValue, p.minIndex, v, gi);
-                    if (v > -FLT_MAX)
-                        maxCombine(p.maxValue, p.maxIndex, v, gi);
-                    p.sum += static_cast<double>(v);
-                    p.prod *= static_cast<double>(v);
-                    p.count += 1;
+                    uint64_t const gi = (static_cast<uint64_t>(z + a.zGlobal) * py + static_cast<uint64_t>(y)) * px +
+                                        static_cast<uint64_t>(a.fx + x);
+                    if (v < p.minValue)   // v < FLT_MAX implied by the FLT_MAX start
+                    {
+                        p.minValue = v;
+                        p.minIndex = gi;
+                    }
+                    if (v > p.maxValue)
+                    {
+                        p.maxValue = v;
+                        p.maxIndex = gi;
+                    }
                 }
-                else
-                {
-                    float const d = v - mean;
-                    float const d2 = d * d;
-                    p.sumSq += static_cast<double>(d2);
-                }
+                p.sum += static_cast<double>(v);
+                p.prod *= static_cast<double>(v);
+                p.count += 1;
             }
-        }
+            else
+            {
+                float const d = v - mean;
+                float const d2 = d * d;
+                p.sumSq += static_cast<double>(d2);
+            }
+        });
         blockReduce(p);
         if (threadIdx.x == 0)
             partials[blockIdx.x] = p;
@@ -223,6 +259,8 @@ namespace hipk
         uint64_t numBins;
         float scale;                // (float)numBins / (hi - lo), as the reference computes it
         int32_t useLds;
+        uint64_t tileBase;          // LDS path: this launch counts bins [tileBase, tileBase + tileBins)
+        uint32_t tileBins;
     };
 
     // bin of one value, or ~0 when the reference would index out of bounds / NaN
@@ -236,62 +274,59 @@ namespace hipk
         return b < numBins ? b : ~0ull;
     }
 
-    constexpr uint32_t kMaxLdsBins = 16384;   // 64 KiB of u32 counters per workgroup
+    // u32 counters a workgroup may hold in LDS (device limit per workgroup, 64 KiB at least)
+    uint32_t ldsBinCapacity()
+    {
+        static uint32_t const cap = [] {
+            int bytes = 0;
+            if (hipDeviceGetAttribute(&bytes, hipDeviceAttributeMaxSharedMemoryPerBlock, rt::device()) != hipSuccess ||
+                bytes < 65536)
+                bytes = 65536;
+            return static_cast<uint32_t>(bytes / sizeof(uint32_t));
+        }();
+        return cap;
+    }
 
+    // Each lane run-length-combines consecutive voxels of the same bin before it touches the
+    // counters (constant or smooth regions: one atomic per run instead of per voxel).
+    template <int BPV, bool VEC>
     __global__ __launch_bounds__(kBlock) void histogramKernel(BoxArgs a, HistArgs h)
     {
         extern __shared__ uint32_t ldsBins[];
-        uint32_t const bpv = codec::bytesPerVoxel(a.fmt);
-        int const lane = threadIdx.x & 63;
-        uint32_t const nb = static_cast<uint32_t>(h.numBins);
+        uint32_t const nb = h.tileBins;
         if (h.useLds)
         {
             for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x)
                 ldsBins[i] = 0;
             __syncthreads();
         }
-        uint32_t const wavesPerBlock = blockDim.x >> 6;
-        uint32_t const totalWaves = gridDim.x * wavesPerBlock;
-        for (uint32_t r = blockIdx.x * wavesPerBlock + (threadIdx.x >> 6); r < a.rows; r += totalWaves)
-        {
-            uint32_t const zr = fdiv(r, a.fdNy);
-            uint32_t const yr = r - zr * a.fdNy.d;
-            uint64_t const rowBase = (static_cast<uint64_t>(a.fz + static_cast<int64_t>(zr)) * static_cast<uint64_t>(a.dimY) +
-                                      static_cast<uint64_t>(a.fy + static_cast<int64_t>(yr))) *
-                                         static_cast<uint64_t>(a.dimX) +
-                                     static_cast<uint64_t>(a.fx);
-            for (int32_t x0 = 0; x0 < a.nx; x0 += 64)
+        uint64_t runBin = ~0ull;
+        uint32_t runCount = 0;
+        auto flush = [&]() {
+            if (runCount)
             {
-                int32_t const x = x0 + lane;
-                uint64_t b = ~0ull;
-                if (x < a.nx)
-                    b = binOf(valueAt(a, rowBase + static_cast<uint64_t>(x), bpv), a.lo, h.scale, h.numBins);
-                // one bin for the whole wave (constant regions): a single atomic
-                uint64_t const b0 = (static_cast<uint64_t>(__shfl(static_cast<uint32_t>(b >> 32), 0)) << 32) |
-                                    __shfl(static_cast<uint32_t>(b), 0);
-                uint64_t const same = __ballot(b == b0);
-                uint64_t const live = __ballot(x < a.nx);
-                if (same == ~0ull || (same & live) == live)
+                if (h.useLds)
                 {
-                    if (lane == 0 && b0 != ~0ull)
-                    {
-                        uint32_t const n = static_cast<uint32_t>(__popcll(live));
-                        if (h.useLds)
-                            atomicAdd(&ldsBins[static_cast<uint32_t>(b0)], n);
-                        else
-                            atomicAdd(&h.bins[b0], static_cast<unsigned long long>(n));
-                    }
-                    continue;
+                    uint64_t const t = runBin - h.tileBase;   // wraps high for bins below the tile
+                    if (t < nb)
+                        atomicAdd(&ldsBins[static_cast<uint32_t>(t)], runCount);
                 }
-                if (b != ~0ull)
-                {
-                    if (h.useLds)
-                        atomicAdd(&ldsBins[static_cast<uint32_t>(b)], 1u);
-                    else
-                        atomicAdd(&h.bins[b], 1ull);
-                }
+                else
+                    atomicAdd(&h.bins[runBin], static_cast<unsigned long long>(runCount));
             }
-        }
+        };
+        forEachVoxel<BPV, VEC>(a, [&](float v, int32_t, int64_t, int64_t) {
+            uint64_t const b = binOf(v, a.lo, h.scale, h.numBins);
+            if (b == runBin)
+            {
+                runCount += b != ~0ull ? 1u : 0u;   // uncounted voxels never accumulate
+                return;
+            }
+            flush();
+            runBin = b;
+            runCount = b != ~0ull ? 1u : 0u;
+        });
+        flush();
         if (h.useLds)
         {
             __syncthreads();
@@ -299,7 +334,7 @@ namespace hipk
             {
                 uint32_t const c = ldsBins[i];
                 if (c)
-                    atomicAdd(&h.bins[i], static_cast<unsigned long long>(c));
+                    atomicAdd(&h.bins[h.tileBase + i], static_cast<unsigned long long>(c));
             }
         }
     }
@@ -351,6 +386,28 @@ namespace hipk
     }
 
     unsigned rowGrid(uint32_t rows) { return streamingGrid(rows, kBlock / 64, 8); }
+
+    bool vecRows(BoxArgs const& a)
+    {
+        uint32_t const bpv = codec::bytesPerVoxel(a.fmt);
+        return (bpv == 1 || bpv == 2 || bpv == 4) && a.fx % 8 == 0 && a.nx % 8 == 0 && a.dimX % 8 == 0 &&
+               reinterpret_cast<uintptr_t>(a.data) % 16 == 0;
+    }
+
+    // dispatch on bytes per voxel and the vector-row condition
+#define VKT_REDUCE_DISPATCH(KERNEL, ...)                                                                      \
+    do {                                                                                                      \
+        uint32_t const bpv_ = codec::bytesPerVoxel(a.fmt);                                                    \
+        bool const vec_ = vecRows(a);                                                                         \
+        if (bpv_ == 1) { if (vec_) KERNEL(1, true, __VA_ARGS__); else KERNEL(1, false, __VA_ARGS__); }        \
+        else if (bpv_ == 2) { if (vec_) KERNEL(2, true, __VA_ARGS__); else KERNEL(2, false, __VA_ARGS__); }   \
+        else { if (vec_) KERNEL(4, true, __VA_ARGS__); else KERNEL(4, false, __VA_ARGS__); }                  \
+    } while (0)
+
+#define VKT_AGG_LAUNCH(B, V, PASS, G, S, MEANPTR, MEANV, OUT) \
+    hipLaunchKernelGGL((aggregatesKernel<PASS, B, V>), dim3(G), dim3(kBlock), 0, S, a, MEANPTR, MEANV, OUT)
+#define VKT_HIST_LAUNCH(B, V, G, LDS, S) \
+    hipLaunchKernelGGL((histogramKernel<B, V>), dim3(G), dim3(kBlock), LDS, S, a, h)
 
     struct AggScratch
     {
@@ -436,9 +493,9 @@ vktError vktHipAggregatesPass(vktHipVolumeView_t volume, vktVec3i_t first, vktVe
         return vktInvalidValue;
     }
     if (pass == 1)
-        hipLaunchKernelGGL(aggregatesKernel<1>, dim3(g), dim3(kBlock), 0, s, a, nullptr, 0.f, partials);
+        VKT_REDUCE_DISPATCH(VKT_AGG_LAUNCH, 1, g, s, nullptr, 0.f, partials);
     else
-        hipLaunchKernelGGL(aggregatesKernel<2>, dim3(g), dim3(kBlock), 0, s, a, nullptr, mean, partials);
+        VKT_REDUCE_DISPATCH(VKT_AGG_LAUNCH, 2, g, s, nullptr, mean, partials);
     hipLaunchKernelGGL(aggregatesFinalKernel, dim3(1), dim3(kBlock), 0, s, partials, g, partials + g,
                        static_cast<float*>(nullptr), 1.0);
     e = rt::check(hipMemcpyAsync(sc.host, partials + g, sizeof(vktHipAggregatePartial_t), hipMemcpyDeviceToHost, s),
@@ -508,10 +565,10 @@ vktError vktHipAggregatesRange(vktHipVolumeView_t volume, vktVec3i_t first, vktV
         }
         vktHipAggregatePartial_t* res = partials + 2 * g;   // [0] pass 1, [1] pass 2
         float* meanDev = reinterpret_cast<float*>(res + 2);
-        hipLaunchKernelGGL(aggregatesKernel<1>, dim3(g), dim3(kBlock), 0, s, a, nullptr, 0.f, partials);
+        VKT_REDUCE_DISPATCH(VKT_AGG_LAUNCH, 1, g, s, nullptr, 0.f, partials);
         hipLaunchKernelGGL(aggregatesFinalKernel, dim3(1), dim3(kBlock), 0, s, partials, g, res, meanDev,
                            static_cast<double>(numElems));
-        hipLaunchKernelGGL(aggregatesKernel<2>, dim3(g), dim3(kBlock), 0, s, a, meanDev, 0.f, partials + g);
+        VKT_REDUCE_DISPATCH(VKT_AGG_LAUNCH, 2, g, s, meanDev, 0.f, partials + g);
         hipLaunchKernelGGL(aggregatesFinalKernel, dim3(1), dim3(kBlock), 0, s, partials + g, g, res + 1,
                            static_cast<float*>(nullptr), 1.0);
         e = rt::check(hipMemcpyAsync(sc.host, res, 2 * sizeof(vktHipAggregatePartial_t), hipMemcpyDeviceToHost, s),
@@ -553,9 +610,33 @@ vktError vktHipHistogramRange(vktHipVolumeView_t volume, vktVec3i_t first, vktVe
         volatile float range = volume.mappingHi - volume.mappingLo;
         volatile float nbf = static_cast<float>(numBins);          // size_t -> float
         h.scale = nbf / range;                                     // numBins / (hi - lo)
-        h.useLds = numBins <= kMaxLdsBins;
-        size_t const lds = h.useLds ? numBins * sizeof(uint32_t) : 0;
-        hipLaunchKernelGGL(histogramKernel, dim3(rowGrid(a.rows)), dim3(kBlock), lds, s, a, h);
+        // LDS counters in tiles of up to ldsBins bins, one pass over the range per tile (u32
+        // per workgroup cannot overflow: a workgroup visits < 2^32 voxels); beyond 8 tiles the
+        // counters go straight to global 64-bit atomics.
+        uint32_t const ldsBins = ldsBinCapacity();
+        uint64_t const tiles = (numBins + ldsBins - 1) / ldsBins;
+        h.useLds = tiles <= 8;
+        if (h.useLds)
+        {
+            uint32_t const tileBins = static_cast<uint32_t>(numBins < ldsBins ? numBins : ldsBins);
+            size_t const lds = static_cast<size_t>(tileBins) * sizeof(uint32_t);
+            // occupancy-limited by LDS: enough workgroups for every CU, no more
+            unsigned const perCU = static_cast<unsigned>(std::max<size_t>(1, (160u * 1024u) / std::max<size_t>(lds, 1)));
+            unsigned const g = streamingGrid(a.rows, kBlock / 64, std::min(8u, perCU));
+            for (uint64_t t = 0; t < tiles; ++t)
+            {
+                h.tileBase = t * tileBins;
+                h.tileBins = static_cast<uint32_t>(std::min<uint64_t>(tileBins, numBins - h.tileBase));
+                VKT_REDUCE_DISPATCH(VKT_HIST_LAUNCH, g, lds, s);
+            }
+        }
+        else
+        {
+            h.tileBase = 0;
+            h.tileBins = 0;
+            unsigned const g = rowGrid(a.rows);
+            VKT_REDUCE_DISPATCH(VKT_HIST_LAUNCH, g, 0, s);
+        }
     }
     else if (numBins > 0 && e != vktNoError)
         return e;
