@@ -122,3 +122,97 @@ def resample_slab(dst_view, src_view, filter_mode: int, plan: ResamplePlan) -> i
     """Run the HIP slab resample for this rank (views from StructuredVolume.hip_view())."""
     return lib.vktHipResampleSlab(dst_view, src_view, filter_mode, plan.dst_gdz, plan.dst[0], plan.src_gdz,
                                   plan.local_src[0])
+
+
+# ---- reductions over Z-slabs (SURVEY.md §8(f) F2: the first all-reduce users) -------------------
+PARTIAL_BYTES = C.sizeof(_lib.HipAggregatePartial_t)
+
+
+def slab_range(first, last, z0: int, z1: int):
+    """Intersect the global range [first, last) with the owned planes [z0, z1): local
+    (first, last) of this slab's buffer, or None when the slab holds none of it."""
+    lo, hi = max(first[2], z0), min(last[2], z1)
+    if hi <= lo or last[0] <= first[0] or last[1] <= first[1]:
+        return None
+    return (first[0], first[1], lo - z0), (last[0], last[1], hi - z0)
+
+
+def _gpu_pass(view, first, last, z0, pass_no, mean):
+    p = _lib.HipAggregatePartial_t()
+    err = lib.vktHipAggregatesPass(view, _lib.Vec3i_t(*first), _lib.Vec3i_t(*last), z0, pass_no, C.c_float(mean),
+                                   C.byref(p))
+    if err != 0:
+        raise RuntimeError(_lib.last_error())
+    return p
+
+
+def _allgather_partials(p, group=None, device=None):
+    """Every rank's partial, in rank order (one all_gather of PARTIAL_BYTES per rank; on a
+    device tensor for nccl, a host tensor for gloo)."""
+    import torch
+    import torch.distributed as dist
+
+    mine = torch.frombuffer(bytearray(bytes(p)), dtype=torch.uint8)
+    if device is not None and dist.get_backend(group) != "gloo":
+        mine = mine.to(device)
+    world = dist.get_world_size(group)
+    out = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(out, mine, group=group)
+    return [_lib.HipAggregatePartial_t.from_buffer_copy(bytes(t.cpu().numpy())) for t in out]
+
+
+def combine_partials(parts):
+    acc = _lib.HipAggregatePartial_t()
+    lib.vktHipAggregatePartialInit(C.byref(acc))
+    for p in parts:
+        lib.vktHipAggregatePartialCombine(C.byref(acc), C.byref(p))
+    return acc
+
+
+def aggregates(view, global_dims, z0: int, first, last, group=None, device=None, pass_fn=None):
+    """ComputeAggregatesRange over a Z-slab partitioned volume: each rank reduces its planes
+    (pass 1), partials are all-gathered and combined in rank order (deterministic), the
+    reference's float mean of the WHOLE volume follows, then pass 2 and a second exchange.
+    `view` is this rank's slab (global planes [z0, z0 + view.dimZ)); returns Aggregates_t."""
+    pass_fn = pass_fn or _gpu_pass
+    gx, gy, gz = global_dims
+    rng = slab_range(first, last, z0, z0 + view.dimZ)
+    empty = _lib.HipAggregatePartial_t()
+    lib.vktHipAggregatePartialInit(C.byref(empty))
+    p1 = pass_fn(view, *rng, z0, 1, 0.0) if rng else empty
+    acc1 = combine_partials(_allgather_partials(p1, group, device))
+    n = gx * gy * gz
+    mean = lib.vktHipAggregatesMean(C.byref(acc1), n)
+    p2 = pass_fn(view, *rng, z0, 2, mean) if rng else empty
+    acc2 = combine_partials(_allgather_partials(p2, group, device))
+    out = _lib.Aggregates_t()
+    lib.vktHipAggregatesFinish(C.byref(acc1), C.byref(acc2), n, gx, gy, C.byref(out))
+    return out
+
+
+def _gpu_count(view, first, last, bins, num_bins):
+    err = lib.vktHipHistogramRange(view, _lib.Vec3i_t(*first), _lib.Vec3i_t(*last), C.c_void_p(bins.data_ptr()),
+                                   num_bins, 0)
+    if err != 0:
+        raise RuntimeError(_lib.last_error())
+
+
+def histogram(view, z0: int, first, last, bins, num_bins: int, group=None, count_fn=None):
+    """ComputeHistogramRange over a Z-slab partitioned volume: each rank counts its planes
+    into `bins` (an int64 tensor of num_bins counters; a device tensor for the GPU backend),
+    then one all_reduce(SUM) -- RCCL over xGMI with the nccl backend (gloo reduces a host
+    copy).  Counts are integers: the result is exact."""
+    import torch.distributed as dist
+
+    rng = slab_range(first, last, z0, z0 + view.dimZ)
+    if rng:
+        (count_fn or _gpu_count)(view, rng[0], rng[1], bins, num_bins)
+    else:
+        bins.zero_()
+    if bins.is_cuda and dist.get_backend(group) == "gloo":
+        host = bins.cpu()
+        dist.all_reduce(host, op=dist.ReduceOp.SUM, group=group)
+        bins.copy_(host)
+    else:
+        dist.all_reduce(bins, op=dist.ReduceOp.SUM, group=group)
+    return bins
