@@ -17,6 +17,7 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <cstdio>
 #include <memory>
 
 #ifndef VKTAPI
@@ -51,6 +52,18 @@ namespace vkt
     };
 
     enum class OpenMode { Read, Write, ReadWrite };
+
+    //--- DataSource (reference include/cpp/vkt/common.hpp:81-91) ---------------------------
+    class DataSource
+    {
+    public:
+        virtual ~DataSource() {}
+        virtual std::size_t read(char* buf, std::size_t len) = 0;
+        virtual std::size_t write(char const* buf, std::size_t len) = 0;
+        virtual bool seek(std::size_t pos) = 0;
+        virtual bool flush() = 0;
+        virtual bool good() const = 0;
+    };
 
     //--- linalg.hpp (reference include/cpp/vkt/linalg.hpp) -------------------------------
     struct Vec2f { float x, y; };
@@ -528,5 +541,80 @@ namespace vkt
     VKTAPI Error ComputeHistogramRange(StructuredVolume& volume, Histogram& histogram, int32_t firstX, int32_t firstY,
                                        int32_t firstZ, int32_t lastX, int32_t lastY, int32_t lastZ);
     VKTAPI Error ComputeHistogramRange(StructuredVolume& volume, Histogram& histogram, Vec3i first, Vec3i last);
+
+    //--- RawFile.hpp (reference include/cpp/vkt/RawFile.hpp:15-60) --------------------------
+    // Dims and format are parsed from the file name ("<X>x<Y>x<Z>" and "[u]int<bits>" tokens
+    // separated by '_', src/vkt/RawFile.cpp:36-106).  Deviations (documented fixes):
+    // read()/write() return BYTES (the reference returns fread's item count, so every
+    // InputStream::read reported ReadError on success); RawFile(FILE*) uses the given stream
+    // and does not close it (the reference fopen()s a null name).
+    class VKTAPI RawFile : public DataSource
+    {
+    public:
+        RawFile(char const* fileName, char const* mode);
+        RawFile(FILE* file);
+        ~RawFile();
+
+        virtual std::size_t read(char* buf, std::size_t len);
+        virtual std::size_t write(char const* buf, std::size_t len);
+        virtual bool seek(std::size_t pos);
+        virtual bool flush();
+        virtual bool good() const;
+
+        void setDims(Vec3i dims);
+        Vec3i getDims() const;
+        void setDataFormat(DataFormat dataFormat);
+        DataFormat getDataFormat() const;
+
+    private:
+        char const* fileName_ = 0;
+        char const* mode_ = 0;
+        FILE* file_ = 0;
+        bool owned_ = false;
+        Vec3i dims_ = {0, 0, 0};
+        DataFormat dataFormat_ = DataFormat::UInt8;
+    };
+
+    //--- InputStream.hpp / OutputStream.hpp (reference include/cpp/vkt/InputStream.hpp:14-40,
+    //    OutputStream.hpp:14-42).  A volume resident in HBM (GPU policy) streams through
+    //    pinned double buffers on the side copy stream -- the file read of chunk i+1 overlaps
+    //    the DMA of chunk i; the reference would fread() into a device pointer.
+    class VKTAPI InputStream
+    {
+    public:
+        InputStream(DataSource& source);
+
+        Error read(StructuredVolume& volume);
+        Error readRange(StructuredVolume& dst, int32_t firstX, int32_t firstY, int32_t firstZ, int32_t lastX,
+                        int32_t lastY, int32_t lastZ);
+        Error readRange(StructuredVolume& dst, Vec3i first, Vec3i last);
+        Error seek(std::size_t pos);
+
+    private:
+        DataSource& dataSource_;
+    };
+
+    class VKTAPI OutputStream
+    {
+    public:
+        OutputStream(DataSource& source);
+
+        Error write(StructuredVolume& volume);
+        Error writeRange(StructuredVolume& dst, int32_t firstX, int32_t firstY, int32_t firstZ, int32_t lastX,
+                         int32_t lastY, int32_t lastZ);
+        Error writeRange(StructuredVolume& dst, Vec3i first, Vec3i last);
+        Error seek(std::size_t pos);
+        Error flush();
+
+    private:
+        DataSource& dataSource_;
+    };
+
+    //--- StructuredVolume stream format of the reference CLI (src/cli/main.cpp:32-88):
+    // u32 magic 0x1, u32 asset type 0x0 (SV), Vec3i dims, u32 format, Vec3f dist, Vec2f mapping,
+    // then the voxel bytes.  ReadSVStream builds the volume with dims.z (the CLI passes dims.x
+    // for z, main.cpp:65).
+    VKTAPI Error ReadSVStream(DataSource& source, StructuredVolume& volume);
+    VKTAPI Error WriteSVStream(DataSource& source, StructuredVolume& volume);
 
 } // vkt

@@ -20,6 +20,7 @@
 
 #include <stddef.h>
 #include <stdint.h>
+#include <stdio.h>
 
 #ifndef VKTAPI
 #define VKTAPI __attribute__((visibility("default")))
@@ -256,6 +257,46 @@ VKTAPI vktError vktBrickDecomposeResizeSV(vktArray3D_vktStructuredVolume decomp,
                                           int32_t brickSizeX, int32_t brickSizeY, int32_t brickSizeZ,
                                           int32_t haloSizeNegX, int32_t haloSizeNegY, int32_t haloSizeNegZ,
                                           int32_t haloSizePosX, int32_t haloSizePosY, int32_t haloSizePosZ);
+
+/* ---- RawFile.h / InputStream.h (reference include/c/vkt/RawFile.h:16-40,
+ *      include/c/vkt/InputStream.h:14-34; handles of forward.h) ------------------------
+ * vktRawFileRead returns bytes (the reference returns fread's item count).  OutputStream
+ * and the SV stream format have no C API in the reference; added here. */
+struct vktDataSource_impl;
+typedef struct vktDataSource_impl* vktDataSource;
+struct vktRawFile_impl;
+typedef struct vktRawFile_impl* vktRawFile;
+struct vktInputStream_impl;
+typedef struct vktInputStream_impl* vktInputStream;
+struct vktOutputStream_impl;
+typedef struct vktOutputStream_impl* vktOutputStream;
+VKTAPI void vktRawFileCreateS(vktRawFile* file, char const* fileName, char const* mode);
+VKTAPI void vktRawFileCreateFD(vktRawFile* file, FILE* fd);
+VKTAPI vktDataSource vktRawFileGetBase(vktRawFile file);
+VKTAPI void vktRawFileDestroy(vktRawFile file);
+VKTAPI size_t vktRawFileRead(vktRawFile file, char* buf, size_t len);
+VKTAPI vktBool_t vktRawFileGood(vktRawFile file);
+VKTAPI vktVec3i_t vktRawFileGetDims3iv(vktRawFile file);
+VKTAPI vktDataFormat vktRawFileGetDataFormat(vktRawFile file);
+VKTAPI void vktInputStreamCreate(vktInputStream* stream, vktDataSource source);
+VKTAPI void vktInputStreamDestroy(vktInputStream stream);
+VKTAPI vktError vktInputStreamReadSV(vktInputStream stream, vktStructuredVolume volume);
+VKTAPI vktError vktInputStreamReadRangeSV(vktInputStream stream, vktStructuredVolume volume,
+                                          int32_t firstX, int32_t firstY, int32_t firstZ,
+                                          int32_t lastX, int32_t lastY, int32_t lastZ);
+VKTAPI vktError vktInputStreamSeek(vktInputStream stream, size_t pos);
+VKTAPI void vktOutputStreamCreate(vktOutputStream* stream, vktDataSource source);
+VKTAPI void vktOutputStreamDestroy(vktOutputStream stream);
+VKTAPI vktError vktOutputStreamWriteSV(vktOutputStream stream, vktStructuredVolume volume);
+VKTAPI vktError vktOutputStreamWriteRangeSV(vktOutputStream stream, vktStructuredVolume volume,
+                                            int32_t firstX, int32_t firstY, int32_t firstZ,
+                                            int32_t lastX, int32_t lastY, int32_t lastZ);
+VKTAPI vktError vktOutputStreamSeek(vktOutputStream stream, size_t pos);
+VKTAPI vktError vktOutputStreamFlush(vktOutputStream stream);
+/* the reference CLI's StructuredVolume stream (src/cli/main.cpp:32-88); ReadSVStream
+ * re-creates *volume (a handle created before, e.g. with vktStructuredVolumeCreate). */
+VKTAPI vktError vktReadSVStream(vktDataSource source, vktStructuredVolume volume);
+VKTAPI vktError vktWriteSVStream(vktDataSource source, vktStructuredVolume volume);
 
 /* ---- Aggregates.h (reference include/c/vkt/Aggregates.h:17-44) ---------- */
 typedef struct {

@@ -145,6 +145,59 @@ def main():
         report("reduce Aggregates 1024^3 UInt16 (2 passes, incl. D2H of the result)", ms, 2 * 2 * n ** 3, n ** 3)
         free(V, Vc)
         lib.vktHipFree(bins)
+    if want("io"):
+        # InputStream / OutputStream into / out of HBM: 1 GiB UInt16 file in
+        # the page cache; staged double-buffered path vs host read + migrate()
+        import time
+        import numpy as np
+        import volkit_amd.volkit as vkt
+        path = "/tmp/vkt_io_1024x1024x512_uint16.raw"
+        nbytes = 1024 * 1024 * 512 * 2
+        np.random.default_rng(0).integers(0, 65535, nbytes // 2, dtype=np.uint16).tofile(path)
+        ep = vkt.GetThreadExecutionPolicy()
+
+        def dev(d):
+            ep.device = d
+            vkt.SetThreadExecutionPolicy(ep)
+
+        def wall(fn, reps=3):
+            ts = []
+            for _ in range(reps):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                fn()
+                torch.cuda.synchronize()
+                ts.append(time.perf_counter() - t0)
+            return sorted(ts)[len(ts) // 2] * 1e3
+
+        dev(vkt.ExecutionPolicy.Device_GPU)
+        V = vkt.StructuredVolume(1024, 1024, 512, vkt.DataFormat_UInt16)
+
+        def staged():
+            f = vkt.RawFile(path, "rb")
+            assert vkt.InputStream(f).read(V) == 0
+            f.close()
+        report("io InputStream.read 1 GiB -> HBM (pinned double buffers, copy stream)", wall(staged), nbytes, nbytes // 2)
+
+        def naive():
+            dev(vkt.ExecutionPolicy.Device_CPU)
+            H = vkt.StructuredVolume(1024, 1024, 512, vkt.DataFormat_UInt16)
+            f = vkt.RawFile(path, "rb")
+            assert vkt.InputStream(f).read(H) == 0
+            f.close()
+            dev(vkt.ExecutionPolicy.Device_GPU)
+            H.migrate()
+        report("io host read + migrate() 1 GiB (reference flow)", wall(naive), nbytes, nbytes // 2)
+
+        def out():
+            f = vkt.RawFile("/tmp/vkt_io_out.raw", "wb")
+            assert vkt.OutputStream(f).write(V) == 0
+            f.close()
+        report("io OutputStream.write HBM -> 1 GiB file", wall(out), nbytes, nbytes // 2)
+        dev(vkt.ExecutionPolicy.Device_CPU)
+        del V
+        os.remove(path)
+        os.remove("/tmp/vkt_io_out.raw")
     if not want("metric"):
         return
 

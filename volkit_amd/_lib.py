@@ -210,6 +210,28 @@ SIGNATURES = {
     "vktHipAggregatesFinish": (c_err, [P(HipAggregatePartial_t), P(HipAggregatePartial_t), u64, i32, i32,
                                        P(Aggregates_t)]),
     "vktHipHistogramRange": (c_err, [HipVolumeView_t, Vec3i_t, Vec3i_t, C.c_void_p, u64, i32]),
+    # RawFile.h / InputStream.h (+ OutputStream / SV stream C entry points added here)
+    "vktRawFileCreateS": (None, [P(C.c_void_p), C.c_char_p, C.c_char_p]),
+    "vktRawFileCreateFD": (None, [P(C.c_void_p), C.c_void_p]),
+    "vktRawFileGetBase": (C.c_void_p, [C.c_void_p]),
+    "vktRawFileDestroy": (None, [C.c_void_p]),
+    "vktRawFileRead": (C.c_size_t, [C.c_void_p, C.c_void_p, C.c_size_t]),
+    "vktRawFileGood": (C.c_uint8, [C.c_void_p]),
+    "vktRawFileGetDims3iv": (Vec3i_t, [C.c_void_p]),
+    "vktRawFileGetDataFormat": (C.c_int, [C.c_void_p]),
+    "vktInputStreamCreate": (None, [P(C.c_void_p), C.c_void_p]),
+    "vktInputStreamDestroy": (None, [C.c_void_p]),
+    "vktInputStreamReadSV": (c_err, [C.c_void_p, c_vol]),
+    "vktInputStreamReadRangeSV": (c_err, [C.c_void_p, c_vol, i32, i32, i32, i32, i32, i32]),
+    "vktInputStreamSeek": (c_err, [C.c_void_p, C.c_size_t]),
+    "vktOutputStreamCreate": (None, [P(C.c_void_p), C.c_void_p]),
+    "vktOutputStreamDestroy": (None, [C.c_void_p]),
+    "vktOutputStreamWriteSV": (c_err, [C.c_void_p, c_vol]),
+    "vktOutputStreamWriteRangeSV": (c_err, [C.c_void_p, c_vol, i32, i32, i32, i32, i32, i32]),
+    "vktOutputStreamSeek": (c_err, [C.c_void_p, C.c_size_t]),
+    "vktOutputStreamFlush": (c_err, [C.c_void_p]),
+    "vktReadSVStream": (c_err, [C.c_void_p, c_vol]),
+    "vktWriteSVStream": (c_err, [C.c_void_p, c_vol]),
     "vktBrickDecomposeResizeSV": (c_err, [c_arr, c_vol] + _R9),
 }
 for _op in ARITH_OPS:

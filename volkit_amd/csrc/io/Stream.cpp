@@ -1,0 +1,633 @@
+// Stream.cpp -- RawFile, InputStream / OutputStream and the CLI's StructuredVolume stream
+// format: the host <-> HBM staging path that feeds migrate().
+//
+// Reference: src/vkt/RawFile.cpp:36-230, src/vkt/InputStream.cpp:22-190,
+// src/vkt/OutputStream.cpp:20-90, src/cli/main.cpp:32-88 (SV serialisation).
+//
+// Semantics kept: InputStream::read reads getSizeInBytes() bytes into the volume;
+// readRange reads (lastX-firstX)*bpv bytes per row (z, y) in z->y order and stores each line
+// at x = 0 of its row -- the reference's offset omits firstX (InputStream.cpp:62), and so does
+// OutputStream::writeRange (OutputStream.cpp:52); errors: InvalidDataSource when the source is
+// not good, ReadError / WriteError on short transfers.
+// Fixed (documented): RawFile::read/write return bytes, not fread's item count (which made
+// every reference InputStream::read report ReadError); RawFile(FILE*) uses the stream it is
+// given; the SV stream reader uses dims.z (main.cpp:65 passes dims.x).
+//
+// MI355X design: a volume that lives in HBM (thread policy GPU) is streamed through two
+// pinned 64 MiB staging buffers on the side copy stream.  While chunk i is in flight
+// (hipMemcpyAsync / hipMemcpy2DAsync for row ranges), the file read or write of chunk i+1
+// proceeds on the host; each buffer is reused only after its event completed.  The copy
+// stream first waits for the compute stream (earlier kernels on the volume finish first) and
+// the compute stream waits for the copies (later kernels see the data).  Under the CPU policy
+// the bytes go straight to / from host memory, as in the reference.
+
+#include "../runtime/Runtime.hpp"
+#include "../StructuredVolume_impl.hpp"
+#include "../common/Codec.hpp"
+#include "volkit_hip.h"
+
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <sstream>
+#include <string>
+#include <vector>
+
+namespace vkt
+{
+namespace
+{
+    std::vector<std::string> splitString(std::string const& s, char delim)
+    {
+        std::vector<std::string> out;
+        std::istringstream in(s);
+        for (std::string tok; std::getline(in, tok, delim);)
+            out.push_back(tok);
+        return out;
+    }
+
+    bool policyIsGpu() { return GetThreadExecutionPolicy().device == ExecutionPolicy::Device::GPU; }
+
+    // Two pinned staging buffers + events, shared by all streams of the process.
+    struct Staging
+    {
+        static constexpr std::size_t kChunk = 64u << 20;
+        std::mutex m;
+        uint8_t* buf[2] = {nullptr, nullptr};
+        hipEvent_t ev[2] = {nullptr, nullptr};
+        bool pending[2] = {false, false};
+
+        vktError init()
+        {
+            for (int i = 0; i < 2; ++i)
+            {
+                if (!buf[i])
+                    VKT_HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&buf[i]), kChunk, hipHostMallocDefault));
+                if (!ev[i])
+                    VKT_HIP_TRY(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
+            }
+            return vktNoError;
+        }
+
+        vktError wait(int i)
+        {
+            if (pending[i])
+            {
+                pending[i] = false;
+                VKT_HIP_TRY(hipEventSynchronize(ev[i]));
+            }
+            return vktNoError;
+        }
+
+        vktError record(int i)
+        {
+            VKT_HIP_TRY(hipEventRecord(ev[i], rt::copyStream()));
+            pending[i] = true;
+            return vktNoError;
+        }
+    };
+
+    Staging& staging()
+    {
+        static Staging* s = new Staging;   // leaked on purpose: no teardown-order issues
+        return *s;
+    }
+
+    // One row segment of a range transfer: `rows` consecutive rows of plane z starting at y.
+    struct Rows
+    {
+        std::size_t devOffset;   // byte offset of the first line in the volume
+        std::size_t rows;
+    };
+
+    // Plan the lines of readRange/writeRange (z -> y order) as per-plane runs.
+    std::vector<Rows> rangeRuns(Vec3i dims, uint32_t bpv, Vec3i first, Vec3i last)
+    {
+        std::vector<Rows> runs;
+        for (int32_t z = first.z; z != last.z; ++z)
+        {
+            std::size_t off = (static_cast<std::size_t>(z) * static_cast<std::size_t>(dims.x) *
+                                   static_cast<std::size_t>(dims.y) +
+                               static_cast<std::size_t>(first.y) * static_cast<std::size_t>(dims.x)) *
+                              bpv;
+            runs.push_back(Rows{off, static_cast<std::size_t>(last.y - first.y)});
+        }
+        return runs;
+    }
+
+    bool rangeValid(StructuredVolume& v, Vec3i first, Vec3i last)
+    {
+        Vec3i d = v.getDims();
+        return first.x >= 0 && first.y >= 0 && first.z >= 0 && last.x <= d.x && last.y <= d.y && last.z <= d.z &&
+               last.x >= first.x && last.y >= first.y && last.z >= first.z;
+    }
+
+    // ---- file -> HBM ----------------------------------------------------------------------
+    // Reads `lineBytes`-byte lines (lines of one run are `pitch` bytes apart in the volume)
+    // into the device volume; returns the bytes read.
+    std::size_t readToDevice(DataSource& src, uint8_t* dev, std::vector<Rows> const& runs, std::size_t lineBytes,
+                             std::size_t pitch, vktError& err)
+    {
+        Staging& st = staging();
+        std::lock_guard<std::mutex> lock(st.m);
+        err = st.init();
+        if (err == vktNoError)
+            err = rt::copyStreamAfterCompute();
+        if (err != vktNoError)
+            return 0;
+        hipStream_t cs = rt::copyStream();
+        bool const contiguous = lineBytes == pitch;
+        std::size_t const linesPerChunk = std::max<std::size_t>(1, Staging::kChunk / std::max<std::size_t>(lineBytes, 1));
+        std::size_t total = 0;
+        int b = 0;
+        bool shortRead = false;
+        for (Rows const& run : runs)
+        {
+            std::size_t done = 0;   // lines of this run
+            while (done < run.rows && !shortRead)
+            {
+                std::size_t lines = std::min(linesPerChunk, run.rows - done);
+                std::size_t bytes = lines * lineBytes;
+                if (lineBytes > Staging::kChunk)   // giant rows: byte chunks of one line
+                {
+                    lines = 1;
+                    bytes = lineBytes;
+                }
+                if ((err = st.wait(b)) != vktNoError)
+                    return total;
+                std::size_t got = 0;
+                if (bytes <= Staging::kChunk)
+                {
+                    // one file read for all lines of the chunk (they are consecutive in the file)
+                    got = src.read(reinterpret_cast<char*>(st.buf[b]), bytes);
+                    std::size_t const fullLines = got / std::max<std::size_t>(lineBytes, 1);
+                    uint8_t* d = dev + run.devOffset + done * pitch;
+                    hipError_t he;
+                    if (contiguous)
+                        he = hipMemcpyAsync(d, st.buf[b], got, hipMemcpyHostToDevice, cs);
+                    else
+                        he = hipMemcpy2DAsync(d, pitch, st.buf[b], lineBytes, lineBytes, fullLines,
+                                              hipMemcpyHostToDevice, cs);
+                    if ((err = rt::check(he, "InputStream: H2D staging copy")) != vktNoError)
+                        return total;
+                }
+                else
+                {
+                    // a line longer than the staging buffer: stream it in byte chunks
+                    std::size_t off = 0;
+                    while (off < bytes)
+                    {
+                        std::size_t n = std::min(Staging::kChunk, bytes - off);
+                        if ((err = st.wait(b)) != vktNoError)
+                            return total;
+                        std::size_t g = src.read(reinterpret_cast<char*>(st.buf[b]), n);
+                        if ((err = rt::check(hipMemcpyAsync(dev + run.devOffset + done * pitch + off, st.buf[b], g,
+                                                            hipMemcpyHostToDevice, cs),
+                                             "InputStream: H2D staging copy")) != vktNoError)
+                            return total;
+                        if ((err = st.record(b)) != vktNoError)
+                            return total;
+                        b ^= 1;
+                        got += g;
+                        off += g;
+                        if (g < n)
+                            break;
+                    }
+                    total += got;
+                    done += 1;
+                    if (got < bytes)
+                        shortRead = true;
+                    continue;
+                }
+                if ((err = st.record(b)) != vktNoError)
+                    return total;
+                b ^= 1;
+                total += got;
+                done += lines;
+                if (got < bytes)
+                    shortRead = true;
+            }
+        }
+        if (err == vktNoError)
+            err = rt::computeStreamAfterCopy();
+        if (err == vktNoError)
+            err = rt::check(hipStreamSynchronize(cs), "InputStream: copy stream");
+        st.pending[0] = st.pending[1] = false;
+        return total;
+    }
+
+    // ---- HBM -> file ----------------------------------------------------------------------
+    std::size_t writeFromDevice(DataSource& dst, uint8_t const* dev, std::vector<Rows> const& runs,
+                                std::size_t lineBytes, std::size_t pitch, vktError& err)
+    {
+        Staging& st = staging();
+        std::lock_guard<std::mutex> lock(st.m);
+        err = st.init();
+        if (err == vktNoError)
+            err = rt::copyStreamAfterCompute();
+        if (err != vktNoError)
+            return 0;
+        hipStream_t cs = rt::copyStream();
+        bool const contiguous = lineBytes == pitch;
+        std::size_t const maxBytes = std::max<std::size_t>(lineBytes, 1);
+        std::size_t const linesPerChunk = std::max<std::size_t>(1, Staging::kChunk / maxBytes);
+        // chunk list: (device address, lines) -- issue D2H of chunk i+1 before writing chunk i
+        struct Chunk
+        {
+            uint8_t const* src;
+            std::size_t lines, bytes;
+        };
+        std::vector<Chunk> chunks;
+        for (Rows const& run : runs)
+            for (std::size_t done = 0; done < run.rows;)
+            {
+                if (lineBytes > Staging::kChunk)
+                {
+                    for (std::size_t off = 0; off < lineBytes; off += Staging::kChunk)
+                        chunks.push_back(Chunk{dev + run.devOffset + done * pitch + off, 0,
+                                               std::min(Staging::kChunk, lineBytes - off)});
+                    done += 1;
+                    continue;
+                }
+                std::size_t lines = std::min(linesPerChunk, run.rows - done);
+                chunks.push_back(Chunk{dev + run.devOffset + done * pitch, lines, lines * lineBytes});
+                done += lines;
+            }
+        auto issue = [&](std::size_t i, int b) -> vktError {
+            Chunk const& c = chunks[i];
+            hipError_t he;
+            if (contiguous || c.lines == 0)
+                he = hipMemcpyAsync(st.buf[b], c.src, c.bytes, hipMemcpyDeviceToHost, cs);
+            else
+                he = hipMemcpy2DAsync(st.buf[b], lineBytes, c.src, pitch, lineBytes, c.lines, hipMemcpyDeviceToHost,
+                                      cs);
+            VKT_HIP_TRY(he);
+            return st.record(b);
+        };
+        std::size_t total = 0;
+        if (!chunks.empty() && (err = issue(0, 0)) != vktNoError)
+            return 0;
+        for (std::size_t i = 0; i < chunks.size(); ++i)
+        {
+            int const b = static_cast<int>(i & 1);
+            if (i + 1 < chunks.size() && (err = issue(i + 1, b ^ 1)) != vktNoError)
+                return total;
+            if ((err = st.wait(b)) != vktNoError)
+                return total;
+            std::size_t put = dst.write(reinterpret_cast<char const*>(st.buf[b]), chunks[i].bytes);
+            total += put;
+            if (put < chunks[i].bytes)
+            {
+                (void)hipStreamSynchronize(cs);
+                st.pending[0] = st.pending[1] = false;
+                return total;
+            }
+        }
+        return total;
+    }
+} // namespace
+
+//--- RawFile ---------------------------------------------------------------------------------
+RawFile::RawFile(char const* fileName, char const* mode) : fileName_(fileName), mode_(mode)
+{
+    file_ = std::fopen(fileName_, mode_);
+    owned_ = true;
+    // dims / data format from the file name (reference RawFile.cpp:43-106)
+    for (std::string const& str : splitString(fileName_ ? fileName_ : "", '_'))
+    {
+        int32_t dx = 0, dy = 0, dz = 0;
+        unsigned short bits = 0;
+        if (std::sscanf(str.c_str(), "%dx%dx%d", &dx, &dy, &dz) == 3)
+            dims_ = {dx, dy, dz};
+        if (std::sscanf(str.c_str(), "int%hu", &bits) == 1)
+            dataFormat_ = bits == 8 ? DataFormat::Int8 : bits == 16 ? DataFormat::Int16
+                        : bits == 32 ? DataFormat::Int32 : DataFormat::Unspecified;
+        if (std::sscanf(str.c_str(), "uint%hu", &bits) == 1)
+            dataFormat_ = bits == 8 ? DataFormat::UInt8 : bits == 16 ? DataFormat::UInt16
+                        : bits == 32 ? DataFormat::UInt32 : DataFormat::Unspecified;
+    }
+}
+
+RawFile::RawFile(FILE* file) : file_(file), owned_(false) {}
+
+RawFile::~RawFile()
+{
+    if (file_ && owned_)
+        std::fclose(file_);
+}
+
+std::size_t RawFile::read(char* buf, std::size_t len) { return good() ? std::fread(buf, 1, len, file_) : 0; }
+
+std::size_t RawFile::write(char const* buf, std::size_t len) { return good() ? std::fwrite(buf, 1, len, file_) : 0; }
+
+bool RawFile::seek(std::size_t pos) { return good() && std::fseek(file_, static_cast<long>(pos), SEEK_SET) == 0; }
+
+bool RawFile::flush() { return good() && std::fflush(file_) == 0; }
+
+bool RawFile::good() const { return file_ != nullptr; }
+
+void RawFile::setDims(Vec3i dims) { dims_ = dims; }
+
+Vec3i RawFile::getDims() const { return dims_; }
+
+void RawFile::setDataFormat(DataFormat dataFormat) { dataFormat_ = dataFormat; }
+
+DataFormat RawFile::getDataFormat() const { return dataFormat_; }
+
+//--- InputStream -----------------------------------------------------------------------------
+InputStream::InputStream(DataSource& source) : dataSource_(source) {}
+
+Error InputStream::read(StructuredVolume& volume)
+{
+    if (!dataSource_.good())
+        return InvalidDataSource;
+    std::size_t const n = volume.getSizeInBytes();
+    std::size_t len;
+    if (policyIsGpu())
+    {
+        vktError e;
+        len = readToDevice(dataSource_, volume.getData(), {Rows{0, 1}}, n, n, e);
+        if (e != vktNoError)
+            return InvalidValue;
+    }
+    else
+        len = dataSource_.read(reinterpret_cast<char*>(volume.getData()), n);
+    return len == n ? NoError : ReadError;
+}
+
+Error InputStream::readRange(StructuredVolume& dst, int32_t fx, int32_t fy, int32_t fz, int32_t lx, int32_t ly,
+                             int32_t lz)
+{
+    return readRange(dst, Vec3i{fx, fy, fz}, Vec3i{lx, ly, lz});
+}
+
+Error InputStream::readRange(StructuredVolume& dst, Vec3i first, Vec3i last)
+{
+    if (!dataSource_.good())
+        return InvalidDataSource;
+    if (!rangeValid(dst, first, last))
+    {
+        rt::fail("InputStream::readRange: range outside the volume");
+        return InvalidValue;
+    }
+    uint32_t const bpv = codec::bytesPerVoxel(static_cast<int32_t>(dst.getDataFormat()));
+    Vec3i const dims = dst.getDims();
+    std::size_t const lineBytes = static_cast<std::size_t>(last.x - first.x) * bpv;
+    std::size_t const pitch = static_cast<std::size_t>(dims.x) * bpv;
+    std::size_t const expect = static_cast<std::size_t>(last.z - first.z) * (last.y - first.y) * lineBytes;
+    std::vector<Rows> runs = rangeRuns(dims, bpv, first, last);
+    std::size_t len = 0;
+    if (policyIsGpu())
+    {
+        vktError e;
+        len = readToDevice(dataSource_, dst.getData(), runs, lineBytes, pitch, e);
+        if (e != vktNoError)
+            return InvalidValue;
+    }
+    else
+    {
+        uint8_t* base = dst.getData();
+        for (Rows const& r : runs)
+            for (std::size_t i = 0; i < r.rows; ++i)
+                len += dataSource_.read(reinterpret_cast<char*>(base + r.devOffset + i * pitch), lineBytes);
+    }
+    return len == expect ? NoError : ReadError;
+}
+
+Error InputStream::seek(std::size_t pos) { return dataSource_.seek(pos) ? NoError : InvalidValue; }
+
+//--- OutputStream ----------------------------------------------------------------------------
+OutputStream::OutputStream(DataSource& source) : dataSource_(source) {}
+
+Error OutputStream::write(StructuredVolume& volume)
+{
+    if (!dataSource_.good())
+        return InvalidDataSource;
+    std::size_t const n = volume.getSizeInBytes();
+    std::size_t len;
+    if (policyIsGpu())
+    {
+        vktError e;
+        len = writeFromDevice(dataSource_, volume.getData(), {Rows{0, 1}}, n, n, e);
+        if (e != vktNoError)
+            return InvalidValue;
+    }
+    else
+        len = dataSource_.write(reinterpret_cast<char const*>(volume.getData()), n);
+    return len == n ? NoError : WriteError;
+}
+
+Error OutputStream::writeRange(StructuredVolume& dst, int32_t fx, int32_t fy, int32_t fz, int32_t lx, int32_t ly,
+                               int32_t lz)
+{
+    return writeRange(dst, Vec3i{fx, fy, fz}, Vec3i{lx, ly, lz});
+}
+
+Error OutputStream::writeRange(StructuredVolume& dst, Vec3i first, Vec3i last)
+{
+    if (!dataSource_.good())
+        return InvalidDataSource;
+    if (!rangeValid(dst, first, last))
+    {
+        rt::fail("OutputStream::writeRange: range outside the volume");
+        return InvalidValue;
+    }
+    uint32_t const bpv = codec::bytesPerVoxel(static_cast<int32_t>(dst.getDataFormat()));
+    Vec3i const dims = dst.getDims();
+    std::size_t const lineBytes = static_cast<std::size_t>(last.x - first.x) * bpv;
+    std::size_t const pitch = static_cast<std::size_t>(dims.x) * bpv;
+    std::size_t const expect = static_cast<std::size_t>(last.z - first.z) * (last.y - first.y) * lineBytes;
+    std::vector<Rows> runs = rangeRuns(dims, bpv, first, last);
+    std::size_t len = 0;
+    if (policyIsGpu())
+    {
+        vktError e;
+        len = writeFromDevice(dataSource_, dst.getData(), runs, lineBytes, pitch, e);
+        if (e != vktNoError)
+            return InvalidValue;
+    }
+    else
+    {
+        uint8_t const* base = dst.getData();
+        for (Rows const& r : runs)
+            for (std::size_t i = 0; i < r.rows; ++i)
+                len += dataSource_.write(reinterpret_cast<char const*>(base + r.devOffset + i * pitch), lineBytes);
+    }
+    return len == expect ? NoError : WriteError;
+}
+
+Error OutputStream::seek(std::size_t pos) { return dataSource_.seek(pos) ? NoError : InvalidValue; }
+
+Error OutputStream::flush() { return dataSource_.flush() ? NoError : InvalidValue; }
+
+//--- SV stream (reference CLI, src/cli/main.cpp:32-88) ----------------------------------------
+namespace
+{
+    constexpr uint32_t kMagic = 0x1, kAssetSV = 0x0;
+
+    template <class T>
+    bool readPod(DataSource& s, T& v)
+    {
+        return s.read(reinterpret_cast<char*>(&v), sizeof(T)) == sizeof(T);
+    }
+
+    template <class T>
+    bool writePod(DataSource& s, T const& v)
+    {
+        return s.write(reinterpret_cast<char const*>(&v), sizeof(T)) == sizeof(T);
+    }
+} // namespace
+
+Error ReadSVStream(DataSource& source, StructuredVolume& volume)
+{
+    if (!source.good())
+        return InvalidDataSource;
+    uint32_t magic = 0, asset = 0, fmt = 0;
+    Vec3i dims{0, 0, 0};
+    Vec3f dist{1.f, 1.f, 1.f};
+    Vec2f mapping{0.f, 1.f};
+    if (!readPod(source, magic) || !readPod(source, asset))
+        return ReadError;
+    if (magic != kMagic || asset != kAssetSV)
+    {
+        rt::fail("ReadSVStream: not a StructuredVolume stream (magic / asset type)");
+        return ReadError;
+    }
+    if (!readPod(source, dims) || !readPod(source, fmt) || !readPod(source, dist) || !readPod(source, mapping))
+        return ReadError;
+    if (dims.x < 0 || dims.y < 0 || dims.z < 0 || codec::bytesPerVoxel(static_cast<int32_t>(fmt)) == 255u)
+    {
+        rt::fail("ReadSVStream: bad header");
+        return ReadError;
+    }
+    volume = StructuredVolume(dims.x, dims.y, dims.z, static_cast<DataFormat>(fmt), dist.x, dist.y, dist.z, mapping.x,
+                              mapping.y);
+    InputStream in(source);
+    return in.read(volume);
+}
+
+Error WriteSVStream(DataSource& source, StructuredVolume& volume)
+{
+    if (!source.good())
+        return InvalidDataSource;
+    Vec3i dims = volume.getDims();
+    uint32_t fmt = static_cast<uint32_t>(volume.getDataFormat());
+    Vec3f dist = volume.getDist();
+    Vec2f mapping = volume.getVoxelMapping();
+    if (!writePod(source, kMagic) || !writePod(source, kAssetSV) || !writePod(source, dims) ||
+        !writePod(source, fmt) || !writePod(source, dist) || !writePod(source, mapping))
+        return WriteError;
+    OutputStream out(source);
+    return out.write(volume);
+}
+
+} // vkt
+
+//--- C API -----------------------------------------------------------------------------------
+struct vktDataSource_impl
+{
+    vkt::DataSource* source = nullptr;
+};
+
+struct vktRawFile_impl
+{
+    vktRawFile_impl(char const* name, char const* mode) : file(name, mode) { base.source = &file; }
+    explicit vktRawFile_impl(FILE* fd) : file(fd) { base.source = &file; }
+    vkt::RawFile file;
+    vktDataSource_impl base;
+};
+
+struct vktInputStream_impl
+{
+    explicit vktInputStream_impl(vktDataSource s) : stream(*s->source) {}
+    vkt::InputStream stream;
+};
+
+struct vktOutputStream_impl
+{
+    explicit vktOutputStream_impl(vktDataSource s) : stream(*s->source) {}
+    vkt::OutputStream stream;
+};
+
+extern "C" {
+
+void vktRawFileCreateS(vktRawFile* file, char const* fileName, char const* mode)
+{
+    *file = new vktRawFile_impl(fileName, mode);
+}
+
+void vktRawFileCreateFD(vktRawFile* file, FILE* fd) { *file = new vktRawFile_impl(fd); }
+
+vktDataSource vktRawFileGetBase(vktRawFile file) { return &file->base; }
+
+void vktRawFileDestroy(vktRawFile file) { delete file; }
+
+size_t vktRawFileRead(vktRawFile file, char* buf, size_t len) { return file->file.read(buf, len); }
+
+vktBool_t vktRawFileGood(vktRawFile file) { return file->file.good() ? VKT_TRUE : VKT_FALSE; }
+
+vktVec3i_t vktRawFileGetDims3iv(vktRawFile file)
+{
+    vkt::Vec3i d = file->file.getDims();
+    return vktVec3i_t{d.x, d.y, d.z};
+}
+
+vktDataFormat vktRawFileGetDataFormat(vktRawFile file) { return static_cast<vktDataFormat>(file->file.getDataFormat()); }
+
+void vktInputStreamCreate(vktInputStream* stream, vktDataSource source) { *stream = new vktInputStream_impl(source); }
+
+void vktInputStreamDestroy(vktInputStream stream) { delete stream; }
+
+vktError vktInputStreamReadSV(vktInputStream stream, vktStructuredVolume volume)
+{
+    return static_cast<vktError>(stream->stream.read(volume->volume));
+}
+
+vktError vktInputStreamReadRangeSV(vktInputStream stream, vktStructuredVolume volume, int32_t fx, int32_t fy,
+                                   int32_t fz, int32_t lx, int32_t ly, int32_t lz)
+{
+    return static_cast<vktError>(stream->stream.readRange(volume->volume, fx, fy, fz, lx, ly, lz));
+}
+
+vktError vktInputStreamSeek(vktInputStream stream, size_t pos) { return static_cast<vktError>(stream->stream.seek(pos)); }
+
+void vktOutputStreamCreate(vktOutputStream* stream, vktDataSource source)
+{
+    *stream = new vktOutputStream_impl(source);
+}
+
+void vktOutputStreamDestroy(vktOutputStream stream) { delete stream; }
+
+vktError vktOutputStreamWriteSV(vktOutputStream stream, vktStructuredVolume volume)
+{
+    return static_cast<vktError>(stream->stream.write(volume->volume));
+}
+
+vktError vktOutputStreamWriteRangeSV(vktOutputStream stream, vktStructuredVolume volume, int32_t fx, int32_t fy,
+                                     int32_t fz, int32_t lx, int32_t ly, int32_t lz)
+{
+    return static_cast<vktError>(stream->stream.writeRange(volume->volume, fx, fy, fz, lx, ly, lz));
+}
+
+vktError vktOutputStreamSeek(vktOutputStream stream, size_t pos)
+{
+    return static_cast<vktError>(stream->stream.seek(pos));
+}
+
+vktError vktOutputStreamFlush(vktOutputStream stream) { return static_cast<vktError>(stream->stream.flush()); }
+
+vktError vktReadSVStream(vktDataSource source, vktStructuredVolume volume)
+{
+    if (!source || !volume)
+        return vktInvalidValue;
+    return static_cast<vktError>(vkt::ReadSVStream(*source->source, volume->volume));
+}
+
+vktError vktWriteSVStream(vktDataSource source, vktStructuredVolume volume)
+{
+    if (!source || !volume)
+        return vktInvalidValue;
+    return static_cast<vktError>(vkt::WriteSVStream(*source->source, volume->volume));
+}
+
+} // extern "C"

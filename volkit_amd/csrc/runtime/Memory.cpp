@@ -44,29 +44,6 @@ namespace
         return *s;
     }
 
-    // Copy stream waits for the compute stream's current tail.
-    vktError copyStreamAfterCompute()
-    {
-        hipEvent_t ev;
-        VKT_HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        vktError e = rt::check(hipEventRecord(ev, rt::computeStream()), "hipEventRecord(compute)");
-        if (e == vktNoError)
-            e = rt::check(hipStreamWaitEvent(rt::copyStream(), ev, 0), "hipStreamWaitEvent(copy)");
-        (void)hipEventDestroy(ev);
-        return e;
-    }
-
-    // Compute stream waits for the copy stream's current tail.
-    vktError computeStreamAfterCopy()
-    {
-        hipEvent_t ev;
-        VKT_HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        vktError e = rt::check(hipEventRecord(ev, rt::copyStream()), "hipEventRecord(copy)");
-        if (e == vktNoError)
-            e = rt::check(hipStreamWaitEvent(rt::computeStream(), ev, 0), "hipStreamWaitEvent(compute)");
-        (void)hipEventDestroy(ev);
-        return e;
-    }
 } // namespace
 
 namespace detail
@@ -87,13 +64,13 @@ namespace detail
         case CopyKind::DeviceToHost:
         {
             hipMemcpyKind kind = ck == CopyKind::HostToDevice ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost;
-            vktError e = copyStreamAfterCompute();
+            vktError e = rt::copyStreamAfterCompute();
             if (e != vktNoError)
                 return e;
             VKT_HIP_TRY(hipMemcpyAsync(dst, src, size, kind, rt::copyStream()));
             if (ck == CopyKind::HostToDevice)
             {
-                e = computeStreamAfterCopy();
+                e = rt::computeStreamAfterCopy();
                 if (e != vktNoError)
                     return e;
             }
@@ -201,6 +178,36 @@ void MemsetRange(void* dst, void const* src, std::size_t dstSize, std::size_t sr
         std::memcpy(static_cast<char*>(dst) + i * srcSize, src, srcSize);
 }
 
+} // vkt
+
+namespace vkt
+{
+namespace rt
+{
+    // Copy stream waits for the compute stream's current tail.
+    vktError copyStreamAfterCompute()
+    {
+        hipEvent_t ev;
+        VKT_HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        vktError e = check(hipEventRecord(ev, computeStream()), "hipEventRecord(compute)");
+        if (e == vktNoError)
+            e = check(hipStreamWaitEvent(copyStream(), ev, 0), "hipStreamWaitEvent(copy)");
+        (void)hipEventDestroy(ev);
+        return e;
+    }
+
+    // Compute stream waits for the copy stream's current tail.
+    vktError computeStreamAfterCopy()
+    {
+        hipEvent_t ev;
+        VKT_HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        vktError e = check(hipEventRecord(ev, copyStream()), "hipEventRecord(copy)");
+        if (e == vktNoError)
+            e = check(hipStreamWaitEvent(computeStream(), ev, 0), "hipStreamWaitEvent(compute)");
+        (void)hipEventDestroy(ev);
+        return e;
+    }
+} // rt
 } // vkt
 
 extern "C" {

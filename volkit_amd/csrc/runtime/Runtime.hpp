@@ -69,6 +69,12 @@ namespace rt
 
     bool kernelTimingEnabled();
 
+    // Stream ordering between the compute stream and the side copy stream (event based):
+    // the copy stream waits for everything queued on the compute stream so far / the compute
+    // stream waits for everything queued on the copy stream so far.
+    vktError copyStreamAfterCompute();
+    vktError computeStreamAfterCopy();
+
     // Device scratch for one backend call site, reused across calls (no per-call hipMalloc,
     // and no stream-ordered pool: hipMallocAsync blocks filled by an H2D copy were
     // intermittently seen stale by the next kernel on gfx950/ROCm 7.2 -- DESIGN.md §4.6).

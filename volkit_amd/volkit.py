@@ -526,6 +526,104 @@ def ComputeHistogramRange(volume: StructuredVolume, histogram: Histogram, *coord
     return lib.vktComputeHistogramRangeSV(volume.handle, histogram.handle, *_ints(coords, 6))
 
 
+# ---- RawFile.hpp / InputStream.hpp / OutputStream.hpp ------------------------------------------
+class RawFile:
+    """SWIG's ``vkt.RawFile(fileName, mode)`` (reference include/cpp/vkt/RawFile.hpp:15-60):
+    dims and format parsed from names like ``foo_256x256x128_uint16.raw``."""
+
+    def __init__(self, fileName: str, mode: str):
+        h = C.c_void_p()
+        self._name = fileName.encode()   # the C++ object keeps the pointer
+        lib.vktRawFileCreateS(C.byref(h), self._name, mode.encode())
+        self._h = h
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            lib.vktRawFileDestroy(h)
+            self._h = None
+
+    def close(self):
+        self.__del__()
+
+    def base(self):
+        return lib.vktRawFileGetBase(self._h)
+
+    def good(self) -> bool:
+        return bool(lib.vktRawFileGood(self._h))
+
+    def getDims(self) -> Vec3i:
+        d = lib.vktRawFileGetDims3iv(self._h)
+        return Vec3i(d.x, d.y, d.z)
+
+    def getDataFormat(self) -> int:
+        return lib.vktRawFileGetDataFormat(self._h)
+
+    def read(self, n: int) -> bytes:
+        buf = (C.c_char * n)()
+        got = lib.vktRawFileRead(self._h, buf, n)
+        return bytes(buf[:got])
+
+
+class InputStream:
+    """``vkt.InputStream(file)``; ``read(volume)`` streams straight into HBM under the GPU
+    policy (pinned double buffers on the copy stream)."""
+
+    def __init__(self, source: RawFile):
+        h = C.c_void_p()
+        lib.vktInputStreamCreate(C.byref(h), source.base())
+        self._h, self._source = h, source
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            lib.vktInputStreamDestroy(h)
+            self._h = None
+
+    def read(self, volume: StructuredVolume) -> int:
+        return lib.vktInputStreamReadSV(self._h, volume.handle)
+
+    def readRange(self, volume: StructuredVolume, *coords) -> int:
+        return lib.vktInputStreamReadRangeSV(self._h, volume.handle, *_ints(coords, 6))
+
+    def seek(self, pos: int) -> int:
+        return lib.vktInputStreamSeek(self._h, int(pos))
+
+
+class OutputStream:
+    def __init__(self, source: RawFile):
+        h = C.c_void_p()
+        lib.vktOutputStreamCreate(C.byref(h), source.base())
+        self._h, self._source = h, source
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            lib.vktOutputStreamDestroy(h)
+            self._h = None
+
+    def write(self, volume: StructuredVolume) -> int:
+        return lib.vktOutputStreamWriteSV(self._h, volume.handle)
+
+    def writeRange(self, volume: StructuredVolume, *coords) -> int:
+        return lib.vktOutputStreamWriteRangeSV(self._h, volume.handle, *_ints(coords, 6))
+
+    def seek(self, pos: int) -> int:
+        return lib.vktOutputStreamSeek(self._h, int(pos))
+
+    def flush(self) -> int:
+        return lib.vktOutputStreamFlush(self._h)
+
+
+def ReadSVStream(source: RawFile, volume: StructuredVolume) -> int:
+    """The reference CLI's StructuredVolume stream (src/cli/main.cpp:32-69)."""
+    return lib.vktReadSVStream(source.base(), volume.handle)
+
+
+def WriteSVStream(source: RawFile, volume: StructuredVolume) -> int:
+    return lib.vktWriteSVStream(source.base(), volume.handle)
+
+
 # ---- backend utilities (include/volkit_hip.h) ----------------------------------------------
 def Synthesize(volume: StructuredVolume, seed: int) -> int:
     """Fill a GPU-resident volume with the counter-based synthetic codes (see volkit_hip.h)."""
