@@ -617,4 +617,87 @@ namespace vkt
     VKTAPI Error ReadSVStream(DataSource& source, StructuredVolume& volume);
     VKTAPI Error WriteSVStream(DataSource& source, StructuredVolume& volume);
 
+    //--- LookupTable.hpp (reference include/cpp/vkt/LookupTable.hpp:14-70) ------------------
+    // RGBA32F transfer function for the renderers (a managed buffer like the volumes).
+    class VKTAPI LookupTable : public ManagedBuffer<uint8_t>
+    {
+    public:
+        LookupTable();
+        LookupTable(int32_t dimX, int32_t dimY, int32_t dimZ, ColorFormat format);
+
+        void setDims(int32_t dimX, int32_t dimY, int32_t dimZ);
+        void getDims(int32_t& dimX, int32_t& dimY, int32_t& dimZ);
+        void setDims(Vec3i dims);
+        Vec3i getDims() const;
+
+        void setColorFormat(ColorFormat cf);
+        ColorFormat getColorFormat() const;
+
+        //! Copy getSizeInBytes() bytes from host memory into the table
+        void setData(uint8_t* data);
+        uint8_t* getData();
+        std::size_t getSizeInBytes() const;
+
+    private:
+        Vec3i dims_ = {0, 0, 0};
+        ColorFormat format_ = ColorFormat::Unspecified;
+    };
+
+    //--- Render.hpp (reference include/cpp/vkt/Render.hpp:16-179, structured volumes) ------
+    enum class RenderAlgo
+    {
+        RayMarching,
+        ImplicitIso,
+        MultiScattering,
+    };
+
+    struct RenderState
+    {
+        RenderAlgo renderAlgo = RenderAlgo::RayMarching;
+        float dtRayMarching = 1.f;
+        uint16_t numIsoSurfaces = 1;
+        enum { MaxIsoSurfaces = 10 };
+        float isoSurfaces[MaxIsoSurfaces] = {.5f};
+        float dtImplicitIso = 1.f;
+        float majorant = 1.f;
+        unsigned animationFrame = 0;
+        ResourceHandle rgbaLookupTable = ResourceHandle(-1);
+        ResourceHandle histogram = ResourceHandle(-1);
+        int viewportWidth = 512;
+        int viewportHeight = 512;
+        Bool sRGB = 1;
+        struct
+        {
+            Bool isSet = 0;
+            Vec3f eye = {0.f, 0.f, 0.f};
+            Vec3f center = {0.f, 0.f, -1.f};
+            Vec3f up = {0.f, 1.f, 0.f};
+            float fovy = 45.f;
+            float lensRadius = .001f;
+            float focalDistance = 10.f;
+        } initialCamera;
+        struct
+        {
+            Bool enabled = 0;
+            char const* fileName = "";
+            Bool takeOnClose = 0;
+            char key = 'p';
+            char const* message = "";
+        } snapshotTool;
+    };
+
+    // The reference opens an interactive viewer.  This build renders headless: Render
+    // accumulates VKT_RENDER_FRAMES frames (default 64) of renderState.animationFrame's
+    // volume on the GPU, writes a PPM snapshot when snapshotTool.enabled, and returns the
+    // camera it used in newRenderState->initialCamera.
+    VKTAPI Error Render(StructuredVolume& volume, RenderState const& renderState = {},
+                        RenderState* newRenderState = 0);
+    VKTAPI Error RenderFrames(StructuredVolume* volumes, std::size_t numAnimationFrames,
+                              RenderState const& renderState = {}, RenderState* newRenderState = 0);
+
+    //! Headless extension: accumulate numFrames frames into `rgba` (host, width*height RGBA
+    //! floats, row 0 = bottom, sRGB applied when renderState.sRGB).
+    VKTAPI Error RenderToImage(StructuredVolume& volume, RenderState const& renderState, unsigned numFrames,
+                               float* rgba);
+
 } // vkt

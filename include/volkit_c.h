@@ -331,6 +331,71 @@ VKTAPI vktError vktComputeHistogramRangeSV(vktStructuredVolume volume, vktHistog
                                            int32_t firstX, int32_t firstY, int32_t firstZ,
                                            int32_t lastX, int32_t lastY, int32_t lastZ);
 
+/* ---- LookupTable.h (reference include/c/vkt/LookupTable.h:18-58) --------- */
+struct vktLookupTable_impl;
+typedef struct vktLookupTable_impl* vktLookupTable;
+VKTAPI void vktLookupTableCreate(vktLookupTable* lut, int32_t dimX, int32_t dimY, int32_t dimZ,
+                                 vktColorFormat format);
+VKTAPI void vktLookupTableDestroy(vktLookupTable lut);
+VKTAPI void vktLookupTableSetDims3i(vktLookupTable lut, int32_t dimX, int32_t dimY, int32_t dimZ);
+VKTAPI void vktLookupTableGetDims3i(vktLookupTable lut, int32_t* dimX, int32_t* dimY, int32_t* dimZ);
+VKTAPI void vktLookupTableSetDims3iv(vktLookupTable lut, vktVec3i_t dims);
+VKTAPI vktVec3i_t vktLookupTableGetDims3iv(vktLookupTable lut);
+VKTAPI void vktLookupTableSetColorFormat(vktLookupTable lut, vktColorFormat format);
+VKTAPI vktColorFormat vktLookupTableGetColorFormat(vktLookupTable lut);
+VKTAPI void vktLookupTableSetData(vktLookupTable lut, uint8_t* data);
+VKTAPI uint8_t* vktLookupTableGetData(vktLookupTable lut);
+VKTAPI size_t vktLookupTableGetSizeInBytes(vktLookupTable lut);
+VKTAPI vktResourceHandle vktLookupTableGetResourceHandle(vktLookupTable lut);
+VKTAPI void vktLookupTableMigrate(vktLookupTable lut);
+
+/* ---- Render.h (reference include/c/vkt/Render.h:15-150, structured volumes) ---- */
+typedef enum {
+    vktRenderAlgoRayMarching,
+    vktRenderAlgoImplicitIso,
+    vktRenderAlgoMultiScattering,
+} vktRenderAlgo;
+
+typedef struct {
+    vktRenderAlgo renderAlgo;
+    float dtRayMarching;
+    uint16_t numIsoSurfaces;
+    float isoSurfaces[10];
+    float dtImplicitIso;
+    float majorant;
+    unsigned animationFrame;
+    vktResourceHandle rgbaLookupTable;
+    vktResourceHandle histogram;
+    int viewportWidth;
+    int viewportHeight;
+    vktBool_t sRGB;
+    struct {
+        vktBool_t isSet;
+        vktVec3f_t eye;
+        vktVec3f_t center;
+        vktVec3f_t up;
+        float fovy;
+        float lensRadius;
+        float focalDistance;
+    } initialCamera;
+    struct {
+        vktBool_t enabled;
+        char const* fileName;
+        vktBool_t takeOnClose;
+        char key;
+        char const* message;
+    } snapshotTool;
+} vktRenderState_t;
+
+/* header-inline in the reference; exported here */
+VKTAPI void vktRenderStateDefaultInit(vktRenderState_t* renderState);
+/* headless (see vkt::Render in volkit.hpp) */
+VKTAPI vktError vktRenderSV(vktStructuredVolume volume, vktRenderState_t renderState,
+                            vktRenderState_t* newRenderState);
+/* extension: accumulate numFrames frames into host RGBA floats (width*height*4, row 0 = bottom) */
+VKTAPI vktError vktRenderSVToImage(vktStructuredVolume volume, vktRenderState_t renderState,
+                                   uint32_t numFrames, float* rgba);
+
 #ifdef __cplusplus
 }
 #endif

@@ -176,6 +176,38 @@ VKTAPI vktError vktHipAggregatesFinish(vktHipAggregatePartial_t const* pass1, vk
 VKTAPI vktError vktHipHistogramRange(vktHipVolumeView_t volume, vktVec3i_t first, vktVec3i_t last, uint64_t* bins,
                                      uint64_t numBins, int32_t accumulate);
 
+/* ---- rendering (reference src/vkt/Render_kernel.hpp) -----------------
+ * One frame = one sample per pixel of the reference's RayMarching / ImplicitIso /
+ * MultiScattering kernels, accumulated as accum = (1 - 1/f)*accum + (1/f)*sample
+ * (AccumulationKernel::accum).  Camera basis precomputed on the host: the primary ray of
+ * pixel (x, y) (y = 0 is the bottom row) with jitter (jx, jy) has direction
+ * normalize(W + sx*U + sy*V), sx = 2(x+jx)/width - 1, sy = 2(y+jy)/height - 1; a thin lens of
+ * radius lensRadius refocuses it at focalDistance along W.  Volume texture: nearest, clamp
+ * (Render.cpp:446-447), unorm values (code / 255 or / 65535; Float32 normalised by its
+ * mapping); transfer function: RGBA32F nearest / clamp, or none. */
+typedef struct {
+    int32_t algo;                 /* vktRenderAlgo: 0 RayMarching, 1 ImplicitIso, 2 MultiScattering */
+    int32_t width, height;
+    uint32_t frameBegin;          /* frames frameBegin+1 .. frameBegin+numFrames; 0 = clear */
+    float eye[3], U[3], V[3], W[3], right[3], up[3];
+    float lensRadius, focalDistance;
+    float bbox[3];                /* object box [0, bbox] = dims * dist */
+    float dtRayMarching, dtImplicitIso, majorant;
+    int32_t numIsoSurfaces;
+    float isoSurfaces[10];
+    int32_t sRGB;
+    float const* lut;             /* device RGBA32F table, or NULL */
+    int32_t lutSize;
+} vktHipRenderParams_t;
+/* accum / color: device arrays of width*height RGBA floats (row-major, row 0 = bottom);
+ * color = sRGB(accum) when params->sRGB. */
+VKTAPI vktError vktHipRender(vktHipVolumeView_t volume, vktHipRenderParams_t const* params, float* accum,
+                             float* color, int32_t numFrames);
+/* The parameter block vkt::Render / vktRenderSV build from a render state (camera from
+ * initialCamera or view_all of the box; lut left NULL). */
+VKTAPI vktError vktHipRenderParamsFromState(vktRenderState_t const* renderState, vktVec3f_t bbox,
+                                            vktHipRenderParams_t* params);
+
 /* Synthetic benchmark/test input: byte i of the volume = byte (i % 8) of
  * splitmix64(seed + (i / 8)) -- counter-based, so the oracle reproduces it exactly
  * (oracle/vkt_oracle.c: vkt_oracle_synth). */

@@ -213,3 +213,26 @@ def histogram_range(v: Volume, first, last, num_bins: int):
     skipped = _lib.vko_histogram_range(v.ref, _i3(*first), _i3(*last),
                                        bins.ctypes.data_as(C.POINTER(C.c_uint64)), num_bins)
     return bins[:num_bins], int(skipped)
+
+
+# ---- renderers (reference src/vkt/Render_kernel.hpp:80-418) ----------------------------------
+class RenderParams(C.Structure):
+    """Same layout as vktHipRenderParams_t / vko_render_params."""
+    _fields_ = [("algo", C.c_int32), ("width", C.c_int32), ("height", C.c_int32), ("frameBegin", C.c_uint32),
+                ("eye", C.c_float * 3), ("U", C.c_float * 3), ("V", C.c_float * 3), ("W", C.c_float * 3),
+                ("right", C.c_float * 3), ("up", C.c_float * 3), ("lensRadius", C.c_float),
+                ("focalDistance", C.c_float), ("bbox", C.c_float * 3), ("dtRayMarching", C.c_float),
+                ("dtImplicitIso", C.c_float), ("majorant", C.c_float), ("numIsoSurfaces", C.c_int32),
+                ("isoSurfaces", C.c_float * 10), ("sRGB", C.c_int32), ("lut", C.c_void_p), ("lutSize", C.c_int32)]
+
+
+_lib.vko_render.argtypes = [C.POINTER(_Vol), C.POINTER(RenderParams), C.c_void_p, C.c_void_p, C.c_int32]
+
+
+def render(v: Volume, params: RenderParams, frames: int, accum=None):
+    """-> (accum, color) float32 arrays of shape (height, width, 4)."""
+    h, w = params.height, params.width
+    acc = np.zeros((h, w, 4), np.float32) if accum is None else np.ascontiguousarray(accum, np.float32).copy()
+    col = np.zeros((h, w, 4), np.float32)
+    _lib.vko_render(v.ref, C.byref(params), acc.ctypes.data, col.ctypes.data, frames)
+    return acc, col

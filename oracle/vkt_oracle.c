@@ -408,6 +408,294 @@ uint64_t vko_histogram_range(const vko_volume* v, const int32_t first[3], const 
     return skipped;
 }
 
+/* ---- renderers, reference src/vkt/Render_kernel.hpp:80-418 -------------------------- */
+/* deterministic math restated from common/RenderMath.hpp (same float operation sequences) */
+static uint32_t r_f2u(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
+static float r_u2f(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
+
+static float r_ln(float x)
+{
+    if (!(x > 0.f))
+        return x == 0.f ? -r_u2f(0x7F800000u) : r_u2f(0x7FC00000u);
+    if (x == r_u2f(0x7F800000u))
+        return x;
+    int32_t e = 0;
+    if (x < 1.17549435e-38f) { x = x * 16777216.f; e = -24; }
+    uint32_t b = r_f2u(x);
+    e += (int32_t)((b >> 23) & 0xFFu) - 127;
+    float m = r_u2f((b & 0x007FFFFFu) | 0x3F800000u);
+    if (m > 1.41421356f) { m = m * 0.5f; e += 1; }
+    float f = m - 1.f, s = f / (2.f + f), z = s * s;
+    float q = 0.111111111f;
+    q = q * z + 0.142857143f;
+    q = q * z + 0.2f;
+    q = q * z + 0.333333333f;
+    q = q * z + 1.f;
+    float lnm = 2.f * s * q, ef = (float)e;
+    return ef * 0.693145752f + (lnm + ef * 1.42860677e-06f);
+}
+
+static float r_exp(float x)
+{
+    if (x != x) return x;
+    if (x > 88.7228394f) return r_u2f(0x7F800000u);
+    if (x < -87.3365479f) return 0.f;
+    float kf = floorf(x * 1.44269504f + 0.5f);
+    float r = (x - kf * 0.693145752f) - kf * 1.42860677e-06f;
+    float q = 1.98412698e-04f;
+    q = q * r + 1.38888889e-03f;
+    q = q * r + 8.33333333e-03f;
+    q = q * r + 4.16666667e-02f;
+    q = q * r + 1.66666667e-01f;
+    q = q * r + 0.5f;
+    q = q * r + 1.f;
+    q = q * r + 1.f;
+    int32_t k = (int32_t)kf;
+    if (k < -126) { q = q * r_u2f((uint32_t)(k + 126 + 127) << 23); return q * 1.17549435e-38f; }
+    if (k > 127) return r_u2f(0x7F800000u);
+    return q * r_u2f((uint32_t)(k + 127) << 23);
+}
+
+static float r_pow(float x, float y)
+{
+    if (x == 0.f) return y > 0.f ? 0.f : (y == 0.f ? 1.f : r_u2f(0x7F800000u));
+    if (x == 1.f || y == 0.f) return 1.f;
+    return r_exp(y * r_ln(x));
+}
+
+static void r_sincos(float a, float* s, float* c)
+{
+    float kf = floorf(a * 0.636619772f + 0.5f);
+    float r = (a - kf * 1.57079601f) - kf * 3.13916473e-07f;
+    float z = r * r;
+    float ps = -1.98412698e-04f;
+    ps = ps * z + 8.33333333e-03f;
+    ps = ps * z - 1.66666667e-01f;
+    float sr = r + r * z * ps;
+    float pc = 2.48015873e-05f;
+    pc = pc * z - 1.38888889e-03f;
+    pc = pc * z + 4.16666667e-02f;
+    float cr = (1.f - 0.5f * z) + z * z * pc;
+    int32_t q = (int32_t)kf & 3;
+    if (q == 0) { *s = sr; *c = cr; }
+    else if (q == 1) { *s = cr; *c = -sr; }
+    else if (q == 2) { *s = -sr; *c = -cr; }
+    else { *s = -cr; *c = sr; }
+}
+
+typedef struct { uint64_t state, inc; } r_rng;
+static r_rng r_rng_make(uint32_t pixel, uint32_t frame)
+{
+    r_rng g;
+    g.inc = (vko_splitmix64((uint64_t)pixel ^ 0xD1B54A32D192ED03ull) << 1) | 1ull;
+    g.state = vko_splitmix64(((uint64_t)frame << 32) ^ pixel);
+    return g;
+}
+static uint32_t r_rng_u32(r_rng* g)
+{
+    uint64_t old = g->state;
+    g->state = old * 6364136223846793005ull + g->inc;
+    uint32_t x = (uint32_t)(((old >> 18) ^ old) >> 27);
+    uint32_t rot = (uint32_t)(old >> 59);
+    return (x >> rot) | (x << ((32u - rot) & 31u));
+}
+static float r_rng_next(r_rng* g) { return (float)(r_rng_u32(g) >> 8) * 5.96046448e-08f; }
+
+typedef struct { float x, y, z; } r_v3;
+static r_v3 rv(float x, float y, float z) { r_v3 r = {x, y, z}; return r; }
+static r_v3 rv_add(r_v3 a, r_v3 b) { return rv(a.x + b.x, a.y + b.y, a.z + b.z); }
+static r_v3 rv_sub(r_v3 a, r_v3 b) { return rv(a.x - b.x, a.y - b.y, a.z - b.z); }
+static r_v3 rv_scale(r_v3 a, float s) { return rv(a.x * s, a.y * s, a.z * s); }
+static r_v3 rv_mul(r_v3 a, r_v3 b) { return rv(a.x * b.x, a.y * b.y, a.z * b.z); }
+static r_v3 rv_div(r_v3 a, r_v3 b) { return rv(a.x / b.x, a.y / b.y, a.z / b.z); }
+static float rv_dot(r_v3 a, r_v3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+static r_v3 rv_norm(r_v3 a) { return rv_scale(a, 1.f / sqrtf(rv_dot(a, a))); }
+static r_v3 rv_arr(const float* a) { return rv(a[0], a[1], a[2]); }
+
+typedef struct { float tnear, tfar; int hit; } r_hit;
+static r_hit r_intersect(r_v3 ori, r_v3 dir, r_v3 box)
+{
+    r_v3 inv = rv(1.f / dir.x, 1.f / dir.y, 1.f / dir.z);
+    r_v3 t1 = rv_mul(rv(0.f - ori.x, 0.f - ori.y, 0.f - ori.z), inv);
+    r_v3 t2 = rv_mul(rv_sub(box, ori), inv);
+    r_hit h;
+    h.tnear = fmaxf(fmaxf(fminf(t1.x, t2.x), fminf(t1.y, t2.y)), fminf(t1.z, t2.z));
+    h.tfar = fminf(fminf(fmaxf(t1.x, t2.x), fmaxf(t1.y, t2.y)), fmaxf(t1.z, t2.z));
+    h.hit = h.tnear <= h.tfar;
+    return h;
+}
+
+/* texture_ref filter Nearest, address Clamp (Render.cpp:446-447) */
+static int32_t r_tex_index(float c, int32_t n)
+{
+    float f = c * (float)n;
+    if (!(f >= 0.f)) f = 0.f;
+    float hi = (float)(n - 1);
+    if (f > hi) f = hi;
+    return (int32_t)floorf(f);
+}
+
+static float r_texel(const vko_volume* v, r_v3 c)
+{
+    size_t i = ((size_t)r_tex_index(c.z, v->dims[2]) * (size_t)v->dims[1] + (size_t)r_tex_index(c.y, v->dims[1])) *
+                   (size_t)v->dims[0] + (size_t)r_tex_index(c.x, v->dims[0]);
+    if (v->fmt == 4) return (float)v->data[i] / 255.f;   /* unorm<8> */
+    if (v->fmt == 5) { uint16_t u; memcpy(&u, v->data + 2 * i, 2); return (float)u / 65535.f; }
+    float f; memcpy(&f, v->data + 4 * i, 4);
+    return (f - v->lo) / (v->hi - v->lo);
+}
+
+static void r_lut(const vko_render_params* p, float val, float out[4])
+{
+    int32_t i = r_tex_index(val, p->lut_size);
+    for (int k = 0; k < 4; ++k) out[k] = p->lut[4 * i + k];
+}
+
+static float r_srgb(float x) { return x <= 0.0031308f ? 12.92f * x : 1.055f * r_pow(x, 1.f / 2.4f) - 0.055f; }
+
+static void r_sample(const vko_volume* v, const vko_render_params* p, int32_t x, int32_t y, uint32_t frame, float out[4])
+{
+    r_rng gen = r_rng_make((uint32_t)y * (uint32_t)p->width + (uint32_t)x, frame);
+    float jx = r_rng_next(&gen), jy = r_rng_next(&gen);
+    float sx = 2.f * ((float)x + jx) / (float)p->width - 1.f;
+    float sy = 2.f * ((float)y + jy) / (float)p->height - 1.f;
+    r_v3 W = rv_arr(p->W);
+    r_v3 dir = rv_norm(rv_add(rv_add(W, rv_scale(rv_arr(p->U), sx)), rv_scale(rv_arr(p->V), sy)));
+    r_v3 ori = rv_arr(p->eye);
+    float lu = r_rng_next(&gen), lv = r_rng_next(&gen);
+    if (p->lens_radius > 0.f) {
+        r_v3 focus = rv_add(ori, rv_scale(dir, p->focal_distance / rv_dot(dir, W)));
+        float r = p->lens_radius * sqrtf(lu), s, c;
+        r_sincos(6.28318531f * lv, &s, &c);
+        ori = rv_add(rv_add(ori, rv_scale(rv_arr(p->right), r * c)), rv_scale(rv_arr(p->up), r * s));
+        dir = rv_norm(rv_sub(focus, ori));
+    }
+    r_v3 box = rv_arr(p->bbox);
+    r_hit h = r_intersect(ori, dir, box);
+    out[0] = out[1] = out[2] = out[3] = 0.f;
+    if (p->algo == 0) { /* RayMarchingKernel, :80-158 */
+        float t = h.tnear;
+        r_v3 tc = rv_div(rv_add(ori, rv_scale(dir, t)), box);
+        r_v3 inc = rv_div(rv_scale(dir, p->dt_ray_marching), box);
+        float dst[4] = {0.f, 0.f, 0.f, 0.f};
+        while (t < h.tfar) {
+            float voxel = r_texel(v, tc), col[4];
+            if (p->lut) r_lut(p, voxel, col); else col[0] = col[1] = col[2] = col[3] = voxel;
+            col[3] = 1.f - r_pow(1.f - col[3], p->dt_ray_marching);
+            col[0] *= col[3]; col[1] *= col[3]; col[2] *= col[3];
+            float rem = 1.f - dst[3];
+            for (int k = 0; k < 4; ++k) dst[k] += col[k] * rem;
+            if (dst[3] == 1.f) break;
+            tc = rv_add(tc, inc);
+            t += p->dt_ray_marching;
+        }
+        for (int k = 0; k < 4; ++k) out[k] = dst[k];
+        return;
+    }
+    if (p->algo == 1) { /* ImplicitIsoKernel, :164-268 */
+        float t = h.tnear, last = -1e20f, isoT = -1e20f;
+        r_v3 tc = rv_div(rv_add(ori, rv_scale(dir, t)), box);
+        r_v3 inc = rv_div(rv_scale(dir, p->dt_implicit_iso), box);
+        float dst[4] = {0.f, 0.f, 0.f, 0.f};
+        while (t < h.tfar) {
+            float voxel = r_texel(v, tc);
+            if (last >= -1e10f) {
+                for (int32_t i = 0; i < p->num_iso; ++i) {
+                    float iso = p->iso[i];
+                    if ((last <= iso && voxel >= iso) || (last >= iso && voxel <= iso)) {
+                        float col[4], d = 0.01f;
+                        if (p->lut) r_lut(p, voxel, col); else col[0] = col[1] = col[2] = col[3] = voxel;
+                        isoT = t;
+                        r_v3 s1 = rv(r_texel(v, rv_add(tc, rv(d, 0.f, 0.f))), r_texel(v, rv_add(tc, rv(0.f, d, 0.f))),
+                                     r_texel(v, rv_add(tc, rv(0.f, 0.f, d))));
+                        r_v3 s2 = rv(r_texel(v, rv_sub(tc, rv(d, 0.f, 0.f))), r_texel(v, rv_sub(tc, rv(0.f, d, 0.f))),
+                                     r_texel(v, rv_sub(tc, rv(0.f, 0.f, d))));
+                        r_v3 N = rv_norm(rv_sub(s2, s1));
+                        float kd = fmaxf(0.f, rv_dot(N, rv(-dir.x, -dir.y, -dir.z))) * voxel;
+                        dst[0] = 0.2f + col[0] * kd;
+                        dst[1] = 0.2f + col[1] * kd;
+                        dst[2] = 0.2f + col[2] * kd;
+                        dst[3] = 1.f;
+                    }
+                }
+            }
+            if (isoT >= -1e10f) break;
+            tc = rv_add(tc, inc);
+            t += p->dt_implicit_iso;
+            last = voxel;
+        }
+        for (int k = 0; k < 4; ++k) out[k] = dst[k];
+        return;
+    }
+    /* MultiScatteringKernel, :276-418 */
+    r_v3 thr = rv(1.f, 1.f, 1.f);
+    float mu_ = p->majorant;
+    if (h.hit) {
+        ori = rv_add(ori, rv_scale(dir, h.tnear));
+        h.tfar -= h.tnear;
+        uint32_t bounce = 0;
+        for (;;) {
+            float t = 0.f;
+            r_v3 pos;
+            int interact;
+            for (;;) { /* sample_interaction, :320-341 */
+                t -= r_ln(1.f - r_rng_next(&gen)) / mu_;
+                pos = rv_add(ori, rv_scale(dir, t));
+                if (t >= h.tfar) { interact = 0; break; }
+                float voxel = r_texel(v, rv_div(pos, box)), mu;
+                if (p->lut) { float col[4]; r_lut(p, voxel, col); mu = col[3]; } else mu = voxel;
+                if (!(mu < r_rng_next(&gen) * mu_)) { interact = 1; break; }
+            }
+            if (!interact) break;
+            ori = pos;
+            if (bounce++ >= 1024) { thr = rv(0.f, 0.f, 0.f); break; }
+            float voxel = r_texel(v, rv_div(ori, box));
+            r_v3 alb;
+            if (p->lut) { float col[4]; r_lut(p, voxel, col); alb = rv(col[0], col[1], col[2]); }
+            else alb = rv(voxel, voxel, voxel);
+            thr = rv_mul(thr, alb);
+            float prob = fmaxf(fmaxf(thr.x, thr.y), thr.z);
+            if (prob < 0.2f) {
+                if (r_rng_next(&gen) > prob) { thr = rv(0.f, 0.f, 0.f); break; }
+                thr = rv(thr.x / prob, thr.y / prob, thr.z / prob);
+            }
+            float cz = 1.f - 2.f * r_rng_next(&gen);
+            float sr = sqrtf(fmaxf(0.f, 1.f - cz * cz)), s, c;
+            r_sincos(6.28318531f * r_rng_next(&gen), &s, &c);
+            dir = rv(sr * c, sr * s, cz);
+            h = r_intersect(ori, dir, box);
+        }
+    }
+    float ty = (float)y / (float)p->height;
+    out[0] = ((1.f - ty) * 1.f + ty * 0.5f) * thr.x;
+    out[1] = ((1.f - ty) * 1.f + ty * 0.7f) * thr.y;
+    out[2] = ((1.f - ty) * 1.f + ty * 1.0f) * thr.z;
+    out[3] = 1.f;
+}
+
+void vko_render(const vko_volume* v, const vko_render_params* p, float* accum, float* color, int32_t num_frames)
+{
+    for (int32_t y = 0; y < p->height; ++y)
+        for (int32_t x = 0; x < p->width; ++x) {
+            size_t pix = (size_t)y * (size_t)p->width + (size_t)x;
+            float acc[4] = {0.f, 0.f, 0.f, 0.f};
+            if (p->frame_begin > 0)
+                for (int k = 0; k < 4; ++k) acc[k] = accum[4 * pix + k];
+            for (int32_t f = 1; f <= num_frames; ++f) {
+                uint32_t frame = p->frame_begin + (uint32_t)f;
+                float s[4];
+                r_sample(v, p, x, y, frame, s);
+                float alpha = 1.f / (float)frame; /* AccumulationKernel::accum */
+                for (int k = 0; k < 4; ++k) acc[k] = (1.f - alpha) * acc[k] + alpha * s[k];
+            }
+            for (int k = 0; k < 4; ++k) accum[4 * pix + k] = acc[k];
+            if (color) {
+                for (int k = 0; k < 3; ++k) color[4 * pix + k] = p->srgb ? r_srgb(acc[k]) : acc[k];
+                color[4 * pix + 3] = acc[3];
+            }
+        }
+}
+
 /* ---- synthetic input -------------------------------------------------------------- */
 uint64_t vko_splitmix64(uint64_t x)
 {

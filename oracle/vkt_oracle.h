@@ -69,6 +69,27 @@ void vko_aggregates_range(const vko_volume* v, const int32_t first[3], const int
 uint64_t vko_histogram_range(const vko_volume* v, const int32_t first[3], const int32_t last[3], uint64_t* bins,
                              uint64_t num_bins);
 
+/* Renderers of reference src/vkt/Render_kernel.hpp:80-418 (RayMarching, ImplicitIso,
+ * MultiScattering), one sample per pixel and frame, accumulated like AccumulationKernel::accum.
+ * Layout of the parameter block = vktHipRenderParams_t (include/volkit_hip.h).  Camera rays,
+ * RNG (PCG32 per pixel and frame) and ln/exp/pow/sincos are restated from this project's
+ * common/RenderMath.hpp: the visionaray sequences of the reference are unpinned. */
+typedef struct {
+    int32_t algo, width, height;
+    uint32_t frame_begin;
+    float eye[3], U[3], V[3], W[3], right[3], up[3];
+    float lens_radius, focal_distance;
+    float bbox[3];
+    float dt_ray_marching, dt_implicit_iso, majorant;
+    int32_t num_iso;
+    float iso[10];
+    int32_t srgb;
+    const float* lut;
+    int32_t lut_size;
+} vko_render_params;
+/* accum / color: width*height*4 floats (row 0 = bottom); accum read when frame_begin > 0 */
+void vko_render(const vko_volume* v, const vko_render_params* p, float* accum, float* color, int32_t num_frames);
+
 /* Synthetic input shared with the GPU generator (include/volkit_hip.h vktHipSynthesize). */
 uint64_t vko_splitmix64(uint64_t x);
 void vko_synth(uint8_t* data, size_t nbytes, uint64_t seed);

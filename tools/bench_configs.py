@@ -145,6 +145,23 @@ def main():
         report("reduce Aggregates 1024^3 UInt16 (2 passes, incl. D2H of the result)", ms, 2 * 2 * n ** 3, n ** 3)
         free(V, Vc)
         lib.vktHipFree(bins)
+    if want("config5"):
+        # BASELINE config 5: 1024^3 UInt8 multi-scattering, 1024^2 viewport (headless frames)
+        import volkit_amd.volkit as vkt
+        n = 1024
+        V = alloc((n,) * 3, 4, seed=21)
+        for algo, lab, frames in ((2, "MultiScattering", 8), (0, "RayMarching", 4), (1, "ImplicitIso", 4)):
+            rs = vkt.RenderState()
+            rs.viewportWidth = rs.viewportHeight = 1024
+            rs.renderAlgo = algo
+            p = _lib.HipRenderParams_t()
+            lib.vktHipRenderParamsFromState(C.byref(rs._c), _lib.Vec3fC_t(n, n, n), C.byref(p))
+            acc = torch.empty(1024 * 1024 * 4, dtype=torch.float32, device="cuda")
+            col = torch.empty_like(acc)
+            ms = timed(lambda: lib.vktHipRender(V, C.byref(p), acc.data_ptr(), col.data_ptr(), frames), 3) / frames
+            print(json.dumps({"case": f"config5 Render {lab} 1024^3 UInt8, 1024^2 viewport", "ms_per_frame": round(ms, 3),
+                              "Mpaths/s": round(1024 * 1024 / ms / 1e3, 1)}), flush=True)
+        free(V)
     if want("io"):
         # InputStream / OutputStream into / out of HBM: 1 GiB UInt16 file in
         # the page cache; staged double-buffered path vs host read + migrate()

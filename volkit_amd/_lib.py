@@ -80,6 +80,37 @@ class HipAggregatePartial_t(C.Structure):
     _fields_ = [("sum", C.c_double), ("prod", C.c_double), ("sumSq", C.c_double), ("minValue", f32),
                 ("maxValue", f32), ("minIndex", u64), ("maxIndex", u64), ("count", u64)]
 
+class Vec3fC_t(C.Structure):
+    _fields_ = [("x", C.c_float), ("y", C.c_float), ("z", C.c_float)]
+
+
+class _InitialCamera(C.Structure):
+    _fields_ = [("isSet", C.c_uint8), ("eye", Vec3fC_t), ("center", Vec3fC_t), ("up", Vec3fC_t),
+                ("fovy", C.c_float), ("lensRadius", C.c_float), ("focalDistance", C.c_float)]
+
+
+class _SnapshotTool(C.Structure):
+    _fields_ = [("enabled", C.c_uint8), ("fileName", C.c_char_p), ("takeOnClose", C.c_uint8),
+                ("key", C.c_char), ("message", C.c_char_p)]
+
+
+class RenderState_t(C.Structure):
+    _fields_ = [("renderAlgo", C.c_int), ("dtRayMarching", C.c_float), ("numIsoSurfaces", C.c_uint16),
+                ("isoSurfaces", C.c_float * 10), ("dtImplicitIso", C.c_float), ("majorant", C.c_float),
+                ("animationFrame", C.c_uint), ("rgbaLookupTable", C.c_uint32), ("histogram", C.c_uint32),
+                ("viewportWidth", C.c_int), ("viewportHeight", C.c_int), ("sRGB", C.c_uint8),
+                ("initialCamera", _InitialCamera), ("snapshotTool", _SnapshotTool)]
+
+
+class HipRenderParams_t(C.Structure):
+    _fields_ = [("algo", i32), ("width", i32), ("height", i32), ("frameBegin", u32),
+                ("eye", f32 * 3), ("U", f32 * 3), ("V", f32 * 3), ("W", f32 * 3), ("right", f32 * 3), ("up", f32 * 3),
+                ("lensRadius", f32), ("focalDistance", f32), ("bbox", f32 * 3),
+                ("dtRayMarching", f32), ("dtImplicitIso", f32), ("majorant", f32),
+                ("numIsoSurfaces", i32), ("isoSurfaces", f32 * 10), ("sRGB", i32),
+                ("lut", C.c_void_p), ("lutSize", i32)]
+
+
 UnaryOp = C.CFUNCTYPE(None, i32, i32, i32, VoxelView_t)
 BinaryOp = C.CFUNCTYPE(None, i32, i32, i32, VoxelView_t, VoxelView_t)
 
@@ -231,6 +262,25 @@ SIGNATURES = {
     "vktOutputStreamSeek": (c_err, [C.c_void_p, C.c_size_t]),
     "vktOutputStreamFlush": (c_err, [C.c_void_p]),
     "vktReadSVStream": (c_err, [C.c_void_p, c_vol]),
+    # LookupTable.h / Render.h (+ headless extensions)
+    "vktLookupTableCreate": (None, [P(C.c_void_p), i32, i32, i32, C.c_int]),
+    "vktLookupTableDestroy": (None, [C.c_void_p]),
+    "vktLookupTableSetDims3i": (None, [C.c_void_p, i32, i32, i32]),
+    "vktLookupTableGetDims3i": (None, [C.c_void_p, P(i32), P(i32), P(i32)]),
+    "vktLookupTableSetDims3iv": (None, [C.c_void_p, Vec3i_t]),
+    "vktLookupTableGetDims3iv": (Vec3i_t, [C.c_void_p]),
+    "vktLookupTableSetColorFormat": (None, [C.c_void_p, C.c_int]),
+    "vktLookupTableGetColorFormat": (C.c_int, [C.c_void_p]),
+    "vktLookupTableSetData": (None, [C.c_void_p, C.c_void_p]),
+    "vktLookupTableGetData": (C.c_void_p, [C.c_void_p]),
+    "vktLookupTableGetSizeInBytes": (C.c_size_t, [C.c_void_p]),
+    "vktLookupTableGetResourceHandle": (u32, [C.c_void_p]),
+    "vktLookupTableMigrate": (None, [C.c_void_p]),
+    "vktRenderStateDefaultInit": (None, [P(RenderState_t)]),
+    "vktRenderSV": (c_err, [c_vol, RenderState_t, P(RenderState_t)]),
+    "vktRenderSVToImage": (c_err, [c_vol, RenderState_t, u32, C.c_void_p]),
+    "vktHipRender": (c_err, [HipVolumeView_t, P(HipRenderParams_t), C.c_void_p, C.c_void_p, i32]),
+    "vktHipRenderParamsFromState": (c_err, [P(RenderState_t), Vec3fC_t, P(HipRenderParams_t)]),
     "vktWriteSVStream": (c_err, [C.c_void_p, c_vol]),
     "vktBrickDecomposeResizeSV": (c_err, [c_arr, c_vol] + _R9),
 }

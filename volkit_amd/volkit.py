@@ -624,6 +624,92 @@ def WriteSVStream(source: RawFile, volume: StructuredVolume) -> int:
     return lib.vktWriteSVStream(source.base(), volume.handle)
 
 
+# ---- LookupTable.hpp / Render.hpp ----------------------------------------------------------------
+(ColorFormat_Unspecified, ColorFormat_R8, ColorFormat_RG8, ColorFormat_RGB8, ColorFormat_RGBA8, ColorFormat_R16UI,
+ ColorFormat_RG16UI, ColorFormat_RGB16UI, ColorFormat_RGBA16UI, ColorFormat_R32UI, ColorFormat_RG32UI,
+ ColorFormat_RGB32UI, ColorFormat_RGBA32UI, ColorFormat_R32F, ColorFormat_RG32F, ColorFormat_RGB32F,
+ ColorFormat_RGBA32F) = range(17)
+RenderAlgo_RayMarching, RenderAlgo_ImplicitIso, RenderAlgo_MultiScattering = 0, 1, 2
+
+
+class LookupTable:
+    """``vkt.LookupTable(5, 1, 1, vkt.ColorFormat_RGBA32F)`` with ``setData`` (reference
+    include/cpp/vkt/LookupTable.hpp; src/examples/Histogram.cpp:48-56)."""
+
+    def __init__(self, dimX: int, dimY: int, dimZ: int, colorFormat: int):
+        h = C.c_void_p()
+        lib.vktLookupTableCreate(C.byref(h), int(dimX), int(dimY), int(dimZ), int(colorFormat))
+        self._h = h
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            lib.vktLookupTableDestroy(h)
+            self._h = None
+
+    def setData(self, data) -> None:
+        arr = np.ascontiguousarray(np.asarray(data, dtype=np.float32))
+        if arr.nbytes != self.getSizeInBytes():
+            raise ValueError(f"expected {self.getSizeInBytes()} bytes, got {arr.nbytes}")
+        lib.vktLookupTableSetData(self._h, arr.ctypes.data)
+
+    def getDims(self) -> Vec3i:
+        d = lib.vktLookupTableGetDims3iv(self._h)
+        return Vec3i(d.x, d.y, d.z)
+
+    def getSizeInBytes(self) -> int:
+        return lib.vktLookupTableGetSizeInBytes(self._h)
+
+    def getResourceHandle(self) -> int:
+        return lib.vktLookupTableGetResourceHandle(self._h)
+
+
+class RenderState:
+    """``vkt.RenderState()`` with the reference's fields and defaults (Render.hpp:23-130)."""
+
+    def __init__(self):
+        self._c = _lib.RenderState_t()
+        lib.vktRenderStateDefaultInit(C.byref(self._c))
+        self._keep = []
+
+    def __getattr__(self, name):
+        c = self.__dict__.get("_c")
+        if c is not None and name in dict(c._fields_):
+            return getattr(c, name)
+        raise AttributeError(name)
+
+    def __setattr__(self, name, value):
+        if name.startswith("_"):
+            object.__setattr__(self, name, value)
+        elif name in dict(_lib.RenderState_t._fields_):
+            setattr(self._c, name, value)
+        else:
+            raise AttributeError(name)
+
+    def setSnapshot(self, fileName: str, message: str = "") -> None:
+        b, m = fileName.encode(), message.encode()
+        self._keep = [b, m]
+        self._c.snapshotTool.enabled = 1
+        self._c.snapshotTool.fileName = b
+        self._c.snapshotTool.message = m
+
+
+def Render(volume: StructuredVolume, renderState: RenderState = None, newRenderState: RenderState = None) -> int:
+    """Headless render (VKT_RENDER_FRAMES frames), snapshot written if requested."""
+    rs = renderState or RenderState()
+    out = newRenderState._c if newRenderState is not None else None
+    return lib.vktRenderSV(volume.handle, rs._c, C.byref(out) if out is not None else None)
+
+
+def RenderToImage(volume: StructuredVolume, renderState: RenderState, numFrames: int) -> np.ndarray:
+    """Extension: (height, width, 4) float32 image, row 0 = bottom, after numFrames frames."""
+    img = np.zeros((renderState.viewportHeight, renderState.viewportWidth, 4), dtype=np.float32)
+    err = lib.vktRenderSVToImage(volume.handle, renderState._c, int(numFrames), img.ctypes.data)
+    if err != NoError:
+        raise RuntimeError(_lib.last_error())
+    return img
+
+
 # ---- backend utilities (include/volkit_hip.h) ----------------------------------------------
 def Synthesize(volume: StructuredVolume, seed: int) -> int:
     """Fill a GPU-resident volume with the counter-based synthetic codes (see volkit_hip.h)."""
