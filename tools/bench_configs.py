@@ -149,11 +149,25 @@ def main():
         # BASELINE config 5: 1024^3 UInt8 multi-scattering, 1024^2 viewport (headless frames)
         import volkit_amd.volkit as vkt
         n = 1024
-        V = alloc((n,) * 3, 4, seed=21)
+        V = alloc((n,) * 3, 4)
+        # smooth procedural density (a soft ball with a low-density halo and ripples), built
+        # plane by plane on the device: long Woodcock paths, unlike white noise
+        zz = torch.arange(n, device="cuda", dtype=torch.float32)
+        yy, xx = torch.meshgrid(zz, zz, indexing="ij")
+        vol = torch.empty((n, n, n), dtype=torch.uint8, device="cuda")
+        for z in range(n):
+            r = torch.sqrt((xx - n / 2) ** 2 + (yy - n / 2) ** 2 + (z - n / 2) ** 2) / (0.45 * n)
+            d = torch.clamp(1.0 - r, 0, 1) * (0.15 + 0.1 * torch.sin(xx * 0.05) * torch.cos(yy * 0.03))
+            vol[z] = torch.clamp(d * 255, 0, 255).to(torch.uint8)
+        lib.vktHipMemcpy(C.c_void_p(V.data), C.c_void_p(vol.data_ptr()), n ** 3, 3)
+        torch.cuda.synchronize()
+        del vol
         for algo, lab, frames in ((2, "MultiScattering", 8), (0, "RayMarching", 4), (1, "ImplicitIso", 4)):
             rs = vkt.RenderState()
             rs.viewportWidth = rs.viewportHeight = 1024
             rs.renderAlgo = algo
+            rs.dtRayMarching = rs.dtImplicitIso = 1.0
+            rs.isoSurfaces[0] = 0.1
             p = _lib.HipRenderParams_t()
             lib.vktHipRenderParamsFromState(C.byref(rs._c), _lib.Vec3fC_t(n, n, n), C.byref(p))
             acc = torch.empty(1024 * 1024 * 4, dtype=torch.float32, device="cuda")
