@@ -187,3 +187,36 @@ def test_zslab_resample_matches_whole_volume(hip, world, fmt, fm, sdims, ddims):
             np.testing.assert_array_equal(got, exp)
         Sl.free()
         Dl.free()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_zslab_linear_specials_in_halo_planes(hip, world):
+    """Float32 Linear (optimistic convert + fix-up path): non-finite values and -0 only in the
+    planes just above each slab boundary (the z+1 halo a slab reads but does not own) and in
+    the first row after a plane end (hi.x of the previous plane's last voxel)."""
+    from volkit_amd import slab
+    sx, sy, sz = 32, 16, 12
+    dx, dy, dz = 64, 32, 24
+    g = np.random.default_rng(world).uniform(0, 1, (sz, sy, sx)).astype(np.float32)
+    for rank in range(1, world):
+        z0, _ = slab.slab_bounds(sz, world, rank)
+        g[z0, 3, 5] = np.inf
+        g[z0, 0, 0] = np.nan
+        g[z0 - 1, sy - 1, sx - 1] = -0.0
+    glob = g.view(np.uint32)
+    ref = ob.Volume.zeros((dx, dy, dz), 7)
+    ob.resample(ref, ob.Volume(glob, 7), 1)
+    for rank in range(world):
+        plan = slab.plan_resample(dz, sz, world, rank, 1, True)
+        d0, d1 = plan.dst
+        l0, l1 = plan.local_src
+        Sl = DevVol(hip, (sx, sy, l1 - l0), 7)
+        Sl.upload(glob[l0:l1])
+        Dl = DevVol(hip, (dx, dy, d1 - d0), 7)
+        assert slab.resample_slab(Dl.view, Sl.view, 1, plan) == 0, hip.last_error()
+        got, exp = Dl.download(), ref.codes[d0:d1]
+        fg, fe = got.view(np.float32), exp.view(np.float32)
+        np.testing.assert_array_equal(np.isnan(fg), np.isnan(fe))
+        np.testing.assert_array_equal(got[~np.isnan(fe)], exp[~np.isnan(fe)])
+        Sl.free()
+        Dl.free()

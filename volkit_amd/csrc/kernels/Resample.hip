@@ -267,6 +267,8 @@ namespace hipk
         Run const* runsZ = nullptr;
         int32_t const* xtab = nullptr;
         int32_t const* zsrc = nullptr;   // source plane of every local dst plane
+        bool yAllRows = false;           // the y runs read every source row 0..sdy-1, in order
+        bool zContiguous = false;        // the z runs read consecutive source planes
         int32_t aff[2][6] = {{0, 0, 0, 0, 0, 0}, {0, 0, 0, 0, 0, 0}};   // {aff, sa, da, dl, s0, d0}
     };
 
@@ -333,6 +335,12 @@ namespace hipk
         t.k = rep ? k : 0;
         affineOf(ry, t.aff[0]);
         affineOf(rz, t.aff[1]);
+        t.yAllRows = static_cast<int32_t>(ry.size()) == sdy;
+        for (size_t i = 0; t.yAllRows && i < ry.size(); ++i)
+            t.yAllRows = ry[i].s == static_cast<int32_t>(i);
+        t.zContiguous = true;
+        for (size_t i = 1; i < rz.size(); ++i)
+            t.zContiguous = t.zContiguous && rz[i].s == rz[i - 1].s + 1;
         t.minSz = rz.empty() ? 0 : rz.front().s;
         t.maxSz = rz.empty() ? -1 : rz.back().s;
         // layout: x table first (16-byte aligned for vector reads, padded to 4 entries), runs after
@@ -419,7 +427,8 @@ namespace hipk
     }
 
     bool launchRowKernel(ResampleArgs const& a, int32_t k, uint64_t tasks, uint32_t bs, uint32_t bd, bool identity,
-                         bool chain, vktHipVolumeView_t const& src, vktHipVolumeView_t const& dst, hipStream_t s)
+                         bool chain, vktHipVolumeView_t const& src, vktHipVolumeView_t const& dst, hipStream_t s,
+                         Tables const& tb)
     {
         if (!(k == 1 || k == 2 || k == 4))
             return false;
@@ -440,6 +449,47 @@ namespace hipk
                 return false;   // per-dst-voxel chain kernel handles these
             ResampleArgs b = a;
             b.srcRows = static_cast<uint64_t>(src.dimY) * static_cast<uint64_t>(src.dimZ);
+            if (b.planeLayout && tb.yAllRows && tb.zContiguous)
+            {
+                // Optimistic path: the detect pass loads every source row of planes
+                // [minSz, maxSz] anyway; only the local planes above maxSz (z+1 halo) are
+                // scanned separately.  Then one fix-up pass over the few flagged tasks.
+                static rt::StreamScratch flags;
+                uint64_t const nTasks = static_cast<uint64_t>(a.nRunsY) * static_cast<uint64_t>(a.nRunsZ);
+                uint64_t const flagBytes = (b.srcRows + 15) / 16 * 16;
+                uint8_t* dirty = nTasks < (1ull << 31)
+                                     ? static_cast<uint8_t*>(flags.acquire(flagBytes + 4 * (nTasks + 1), s))
+                                     : nullptr;
+                if (dirty)
+                {
+                    uint32_t* list = reinterpret_cast<uint32_t*>(dirty + flagBytes);
+                    bool ok = hipMemsetAsync(dirty, 0, flagBytes + 4, s) == hipSuccess;   // flags + list count
+                    int32_t const above = tb.maxSz + 1 - a.srcZ0;   // first local plane above the task planes
+                    if (ok && above < src.dimZ)
+                    {
+                        uint64_t const row0 = static_cast<uint64_t>(above) * static_cast<uint64_t>(src.dimY);
+                        uint64_t const nrows = b.srcRows - row0;
+                        unsigned const g = static_cast<unsigned>((nrows + kBlock / 64 - 1) / (kBlock / 64));
+                        uint8_t const* base = src.data + row0 * static_cast<uint64_t>(src.dimX) * 4u;
+                        if (src.dimX % 4 == 0)
+                            hipLaunchKernelGGL(rowDirtyKernel<true>, dim3(g), dim3(kBlock), 0, s, base, src.dimX, nrows,
+                                               dirty + row0);
+                        else
+                            hipLaunchKernelGGL(rowDirtyKernel<false>, dim3(g), dim3(kBlock), 0, s, base, src.dimX,
+                                               nrows, dirty + row0);
+                    }
+                    if (ok)
+                    {
+                        b.rowDirty = dirty;
+                        b.rowDirtyOut = dirty;
+                        launchLinearOptimistic(b, k, bd, instrPerRow, list, s);
+                        flags.release(s);
+                        return true;
+                    }
+                    (void)hipGetLastError();
+                    flags.release(s);
+                }
+            }
             // rowDirty, then rowChain for the plane layout; without scratch every task takes
             // the chain (still exact)
             static rt::StreamScratch scratch;
@@ -588,7 +638,7 @@ namespace hipk
         unsigned grid = streamingGrid(tasks, kBlock / 64);
 
         uint32_t const bs = codec::bytesPerVoxel(src.dataFormat), bd = codec::bytesPerVoxel(dst.dataFormat);
-        if (launchRowKernel(a, t.k, tasks, bs, bd, identity, chain, src, dst, s))
+        if (launchRowKernel(a, t.k, tasks, bs, bd, identity, chain, src, dst, s, t))
             return rt::finishLaunch(chain ? "Resample_hip(row, linear chain)" : "Resample_hip(row)");
         if (chain)
         {

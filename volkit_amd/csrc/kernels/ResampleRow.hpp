@@ -62,6 +62,7 @@ namespace hipk
         int32_t dnz;
         int32_t planeLayout;       // 1: resamplePlaneKernel, 0: resampleRowKernel
         FastDiv fdInstr, fdRunsY, fdDaZ;   // task decomposition without integer division
+        uint8_t* rowDirtyOut;      // MODE 3: flags written by the detect pass (zeroed before)
         // MODE 2, plane layout: one byte per local source row r, nonzero if the chain of a
         // voxel in row r can differ from v000 (OR of rowDirty over the rows its chain reads);
         // built from rowDirty by rowChainKernel.  nullptr = chain everywhere.
@@ -282,6 +283,50 @@ namespace hipk
     }
 
 
+    // The reference's sampleLinear chain for the N source voxels [sx, sx + N) of row r00
+    // (codes in sc), with neighbour rows r10 (y+1), r01 (z+1), r11 and hi.x = the next voxel in
+    // memory (from the next lane, or loaded directly at the lane / row end; past the buffer end
+    // clamped to the last voxel).  Overwrites sc with the destination codes.
+    template <int BPVS, int N, int FS, int FD>
+    __device__ __forceinline__ void chainEval(ResampleArgs const& a, uint64_t r00, uint64_t r10, uint64_t r01,
+                                              uint64_t r11, uint64_t sx, bool rowEnd, int lane, uint32_t (&sc)[N])
+    {
+        uint32_t c10[N], c01[N], c11[N];
+        loadN<BPVS, N, true>(a.src, r10 + sx, c10);
+        loadN<BPVS, N, true>(a.src, r01 + sx, c01);
+        loadN<BPVS, N, true>(a.src, r11 + sx, c11);
+        uint32_t e00 = __shfl_down(sc[0], 1), e10 = __shfl_down(c10[0], 1);
+        uint32_t e01 = __shfl_down(c01[0], 1), e11 = __shfl_down(c11[0], 1);
+        if (lane == 63 || rowEnd)
+        {
+            uint64_t const last = a.srcVoxels - 1;   // reference reads past the end: clamp
+            auto flat = [&](uint64_t i) { return loadCode<BPVS>(a.src, i < last ? i : last); };
+            e00 = flat(r00 + sx + N);
+            e10 = flat(r10 + sx + N);
+            e01 = flat(r01 + sx + N);
+            e11 = flat(r11 + sx + N);
+        }
+        int32_t const fs = FS == -1 ? a.fs : FS;
+        auto dec = [&](uint32_t c) { return codec::decode(c, fs, a.slo, a.shi); };
+        float const f = 0.f;   // every fraction of sampleLinear(int,int,int) is 0
+        uint32_t out[N];
+#pragma unroll
+        for (int i = 0; i < N; ++i)
+        {
+            float v0 = dec(sc[i]), v1 = dec(i + 1 < N ? sc[i + 1] : e00);
+            float v2 = dec(c10[i]), v3 = dec(i + 1 < N ? c10[i + 1] : e10);
+            float v4 = dec(c01[i]), v5 = dec(i + 1 < N ? c01[i + 1] : e01);
+            float v6 = dec(c11[i]), v7 = dec(i + 1 < N ? c11[i + 1] : e11);
+            float value = codec::lerp(codec::lerp(codec::lerp(v0, v1, f), codec::lerp(v2, v3, f), f),
+                                      codec::lerp(codec::lerp(v4, v5, f), codec::lerp(v6, v7, f), f), f);
+            bool w;
+            out[i] = codec::encode(value, FD == -1 ? a.fd : FD, a.dm, w);
+        }
+#pragma unroll
+        for (int i = 0; i < N; ++i)
+            sc[i] = out[i];
+    }
+
     // ---- plane-linear variant: the write stream sweeps the destination in memory order ----
     // One wave (and one 64-thread workgroup) per task = (dst plane, source-row run in y, one
     // 64-lane store instruction of x): it loads the N = V/K source voxels per lane that feed
@@ -352,42 +397,23 @@ namespace hipk
                         sc[i] = convertCode<FS, FD>(sc[i], a);
                 }
                 else
-                {
-                    uint32_t c10[N], c01[N], c11[N];
-                    loadN<BPVS, N, true>(a.src, r10 + sx, c10);
-                    loadN<BPVS, N, true>(a.src, r01 + sx, c01);
-                    loadN<BPVS, N, true>(a.src, r11 + sx, c11);
-                    uint32_t e00 = __shfl_down(sc[0], 1), e10 = __shfl_down(c10[0], 1);
-                    uint32_t e01 = __shfl_down(c01[0], 1), e11 = __shfl_down(c11[0], 1);
-                    if (lane == 63 || dx + V >= a.ddx)
-                    {
-                        uint64_t const last = a.srcVoxels - 1;   // reference reads past the end: clamp
-                        auto flat = [&](uint64_t i) { return loadCode<BPVS>(a.src, i < last ? i : last); };
-                        e00 = flat(r00 + sx + N);
-                        e10 = flat(r10 + sx + N);
-                        e01 = flat(r01 + sx + N);
-                        e11 = flat(r11 + sx + N);
-                    }
-                    int32_t const fs = FS == -1 ? a.fs : FS;
-                    auto dec = [&](uint32_t c) { return codec::decode(c, fs, a.slo, a.shi); };
-                    float const f = 0.f;   // every fraction of sampleLinear(int,int,int) is 0
-                    uint32_t out[N];
+                    chainEval<BPVS, N, FS, FD>(a, r00, r10, r01, r11, sx, dx + V >= a.ddx, lane, sc);
+            }
+            else if constexpr (MODE == 3)
+            {
+                // optimistic Float32 "Linear": write the conversion of v000 and flag the source
+                // row if it holds a value that can make the chain differ (resampleFixupKernel
+                // then rewrites the tasks next to flagged rows)
+                bool sens = false;
 #pragma unroll
-                    for (int i = 0; i < N; ++i)
-                    {
-                        float v0 = dec(sc[i]), v1 = dec(i + 1 < N ? sc[i + 1] : e00);
-                        float v2 = dec(c10[i]), v3 = dec(i + 1 < N ? c10[i + 1] : e10);
-                        float v4 = dec(c01[i]), v5 = dec(i + 1 < N ? c01[i + 1] : e01);
-                        float v6 = dec(c11[i]), v7 = dec(i + 1 < N ? c11[i + 1] : e11);
-                        float value = codec::lerp(codec::lerp(codec::lerp(v0, v1, f), codec::lerp(v2, v3, f), f),
-                                                  codec::lerp(codec::lerp(v4, v5, f), codec::lerp(v6, v7, f), f), f);
-                        bool w;
-                        out[i] = codec::encode(value, FD == -1 ? a.fd : FD, a.dm, w);
-                    }
+                for (int i = 0; i < N; ++i)
+                    sens = sens || chainSensitive(sc[i]);
+                if (sens)   // rare; any lane may set the row's flag
+                    a.rowDirtyOut[static_cast<uint64_t>(sz - a.srcZ0) * static_cast<uint64_t>(a.sdy) +
+                                  static_cast<uint64_t>(ry.s)] = 1;
 #pragma unroll
-                    for (int i = 0; i < N; ++i)
-                        sc[i] = out[i];
-                }
+                for (int i = 0; i < N; ++i)
+                    sc[i] = convertCode<FS, FD>(sc[i], a);
             }
             uint32_t code[V];
 #pragma unroll
@@ -401,6 +427,71 @@ namespace hipk
             }
         }
     }
+
+    // After a MODE 3 pass.  Scan: one THREAD per task (y run, z run) ORs the flags of the rows
+    // its chain reads (r00, r10, r01, r11 and the row after each in memory) and appends the
+    // flagged tasks to a work list.  Fix-up: a fixed grid of waves drains the list, re-evaluating
+    // the chain for each listed task and overwriting what MODE 3 wrote there.
+    __device__ __forceinline__ bool taskFlagged(ResampleArgs const& a, Run const& ry, Run const& rz)
+    {
+        int32_t const hy = ry.s + 1 < a.sdy ? ry.s + 1 : a.sdy - 1;
+        int32_t const hz = rz.s + 1 < a.srcGlobalDz ? rz.s + 1 : a.srcGlobalDz - 1;
+        uint64_t const sdy = static_cast<uint64_t>(a.sdy);
+        uint64_t const z0 = static_cast<uint64_t>(rz.s - a.srcZ0) * sdy, z1 = static_cast<uint64_t>(hz - a.srcZ0) * sdy;
+        uint64_t const lastRow = a.srcRows - 1;
+        uint32_t dirty = 0;
+        for (uint64_t r : {z0 + ry.s, z0 + hy, z1 + ry.s, z1 + hy})
+            dirty |= a.rowDirty[r] | a.rowDirty[r < lastRow ? r + 1 : lastRow];
+        return dirty != 0;
+    }
+
+    template <int BPVD, int K>
+    __global__ __launch_bounds__(64) void resampleFixupKernel(ResampleArgs a, uint32_t const* list)
+    {
+        constexpr int BPVS = 4;
+        constexpr int V = 16 / BPVD;
+        constexpr int N = V / K;
+        constexpr int kInstr = 64 * V;
+        int const lane = threadIdx.x & 63;
+        uint32_t const nY = static_cast<uint32_t>(a.nRunsY);
+        uint32_t const instrPerRow = a.fdInstr.d;
+        uint32_t const count = __builtin_amdgcn_readfirstlane(list[0]);
+        for (uint32_t w = blockIdx.x; w < count; w += gridDim.x)
+        {
+            uint32_t const t = __builtin_amdgcn_readfirstlane(list[1 + w]);
+            uint32_t const iz = t / nY, iy = t - iz * nY;
+            Run const ry = runY(a, iy);
+            Run const rz = runZ(a, iz);
+            int32_t const hy = ry.s + 1 < a.sdy ? ry.s + 1 : a.sdy - 1;
+            int32_t const hz = rz.s + 1 < a.srcGlobalDz ? rz.s + 1 : a.srcGlobalDz - 1;
+            uint64_t const r00 = srcRowIndex(a, ry.s, rz.s), r10 = srcRowIndex(a, hy, rz.s);
+            uint64_t const r01 = srcRowIndex(a, ry.s, hz), r11 = srcRowIndex(a, hy, hz);
+            for (uint32_t g = 0; g < instrPerRow; ++g)
+            {
+                int32_t dx = kInstr * static_cast<int32_t>(g) + V * lane;
+                bool const active = dx < a.ddx;
+                dx = active ? dx : a.ddx - V;
+                uint64_t const sx = static_cast<uint64_t>(dx / K);
+                uint32_t sc[N];
+                loadN<BPVS, N, true>(a.src, r00 + sx, sc);
+                chainEval<BPVS, N, codec::FmtFloat32, -1>(a, r00, r10, r01, r11, sx, dx + V >= a.ddx, lane, sc);
+                uint32_t code[V];
+#pragma unroll
+                for (int i = 0; i < V; ++i)
+                    code[i] = sc[i / K];
+                if (active)
+                    for (int32_t zd = rz.d0; zd < rz.d1; ++zd)
+                        for (int32_t yd = ry.d0; yd < ry.d1; ++yd)
+                            store16<BPVD>(a.dst, dstRowIndex(a, yd, zd) + static_cast<uint64_t>(dx), code);
+            }
+        }
+    }
+
+    // Float32 "Linear", optimistic: MODE 3 plane pass (convert + flag) then the fix-up
+    // (ResampleRow2.hip).  grid of the fix-up: one wave per (y run, z run), capped.
+    // `list`: device work list of 1 + nRunsY*nRunsZ uint32 (count first, zeroed by the caller).
+    void launchLinearOptimistic(ResampleArgs const& a, int32_t k, uint32_t bpvd, int32_t instrPerRow, uint32_t* list,
+                                hipStream_t s);
 
     // Row-kernel launchers, one translation unit per MODE (0 identity, 1 convert, 2 chain).
     // k: integer x ratio; instrPerRow: 64-lane 16-byte store instructions per dst row.

@@ -10,6 +10,8 @@ namespace hipk
     {
         if (fs == codec::FmtUInt16 && fd == codec::FmtUInt16)
             launchRowK<2, 2, 1, codec::FmtUInt16, codec::FmtUInt16>(a, k, grid, instrPerRow, s);
+        else if (fs == codec::FmtFloat32 && fd == codec::FmtFloat32)   // config 3 Nearest
+            launchRowK<4, 4, 1, codec::FmtFloat32, codec::FmtFloat32>(a, k, grid, instrPerRow, s);
         else if (fs == codec::FmtUInt8 && fd == codec::FmtUInt8)
             launchRowK<1, 1, 1, codec::FmtUInt8, codec::FmtUInt8>(a, k, grid, instrPerRow, s);
         else if (bpv == 1) launchRowK<1, 1, 1, -1, -1>(a, k, grid, instrPerRow, s);
