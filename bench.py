@@ -29,8 +29,11 @@ HBM_PEAK_GBS = 8000.0   # MI355X spec (MI355X_MICROARCH.md: HBM3E 8.0 TB/s)
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--steps", type=int, default=50)
+    # the first ~10-20 ms of sustained streaming run below the steady HBM rate (measured with
+    # tools/libbench.cpp: 1.09 ms per SumRange in the first 10 launches, 1.01 ms after), so the
+    # default warm-up covers ~35 ms; an explicit --warmup is honoured as given
+    p.add_argument("--warmup", type=int, default=25)
     p.add_argument("--dst", type=int, default=1024, help="per-GPU dst cube edge (source = dst/2)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-dst", type=int, default=768, help="dst edge of the CPU-baseline sample")

@@ -42,8 +42,9 @@ namespace codec
 
     VKT_HD int32_t cvtt_i32(float f)
     {
-        // x86 cvttss2si: truncate; NaN or |f| >= 2^31 -> 0x80000000.
-        return (f >= -2147483648.0f && f < 2147483648.0f) ? static_cast<int32_t>(f) : INT32_MIN;
+        // x86 cvttss2si: truncate; NaN or |f| >= 2^31 -> 0x80000000.  (-2^31 itself takes the
+        // fallback, which is its own conversion: one compare with an |.| source modifier.)
+        return fabsf(f) < 2147483648.0f ? static_cast<int32_t>(f) : INT32_MIN;
     }
 
     VKT_HD int64_t cvtt_i64(float f)
@@ -91,18 +92,28 @@ namespace codec
         int32_t rangeIsPow2;
     };
 
+    // DIV selects the division at compile time where the caller has dispatched on
+    // m.rangeIsPow2 (1: multiply by the exact reciprocal, 2: IEEE divide; 0: test at run
+    // time -- a uniform branch per voxel that keeps hipcc from interleaving voxels).
+    template <int DIV = 0>
     VKT_HD float normalise(float value, MapParams const& m)
     {
         float v = value - m.lo;
-        return m.rangeIsPow2 ? v * m.invRange : v / m.range;
+        if constexpr (DIV == 1)
+            return v * m.invRange;
+        else if constexpr (DIV == 2)
+            return v / m.range;
+        else
+            return m.rangeIsPow2 ? v * m.invRange : v / m.range;
     }
 
     // ---- encode (MapVoxelImpl) -------------------------------------------------------
     // Returns the stored code in the low bytesPerVoxel(fmt) bytes; `write` is false for
     // the formats the reference's switch skips (Int8, Int32, Unspecified).
+    template <int DIV = 0>
     VKT_HD uint32_t encode(float value, int32_t fmt, MapParams const& m, bool& write)
     {
-        float v = normalise(value, m);
+        float v = normalise<DIV>(value, m);
         write = true;
         switch (fmt)
         {

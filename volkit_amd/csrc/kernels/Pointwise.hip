@@ -178,11 +178,14 @@ namespace hipk
         if (p.vec && fs == fd)
         {
             if (fs == codec::FmtUInt8)
-                return launchPointwise<1, 1>(p, ConvertF<codec::FmtUInt8, codec::FmtUInt8>{fs, fd, src.mappingLo, src.mappingHi, dm}, s);
+                return dm.rangeIsPow2 ? launchPointwise<1, 1>(p, ConvertF<codec::FmtUInt8, codec::FmtUInt8, 1>{fs, fd, src.mappingLo, src.mappingHi, dm}, s)
+                                      : launchPointwise<1, 1>(p, ConvertF<codec::FmtUInt8, codec::FmtUInt8, 2>{fs, fd, src.mappingLo, src.mappingHi, dm}, s);
             if (fs == codec::FmtUInt16)
-                return launchPointwise<1, 2>(p, ConvertF<codec::FmtUInt16, codec::FmtUInt16>{fs, fd, src.mappingLo, src.mappingHi, dm}, s);
+                return dm.rangeIsPow2 ? launchPointwise<1, 2>(p, ConvertF<codec::FmtUInt16, codec::FmtUInt16, 1>{fs, fd, src.mappingLo, src.mappingHi, dm}, s)
+                                      : launchPointwise<1, 2>(p, ConvertF<codec::FmtUInt16, codec::FmtUInt16, 2>{fs, fd, src.mappingLo, src.mappingHi, dm}, s);
             if (fs == codec::FmtFloat32)
-                return launchPointwise<1, 4>(p, ConvertF<codec::FmtFloat32, codec::FmtFloat32>{fs, fd, src.mappingLo, src.mappingHi, dm}, s);
+                return dm.rangeIsPow2 ? launchPointwise<1, 4>(p, ConvertF<codec::FmtFloat32, codec::FmtFloat32, 1>{fs, fd, src.mappingLo, src.mappingHi, dm}, s)
+                                      : launchPointwise<1, 4>(p, ConvertF<codec::FmtFloat32, codec::FmtFloat32, 2>{fs, fd, src.mappingLo, src.mappingHi, dm}, s);
         }
         return launchByBpv<1>(p, ConvertF<kDyn, kDyn>{fs, fd, src.mappingLo, src.mappingHi, dm}, s);
     }

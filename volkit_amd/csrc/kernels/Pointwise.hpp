@@ -80,7 +80,19 @@ namespace hipk
     // op against 4.5-4.7 TB/s for a grid-stride sweep), keeps kUnroll items per lane in
     // flight (all loads issued before the first store), and uses nontemporal loads and
     // stores: every byte is touched once.
-    constexpr int kUnroll = 4;
+    //
+    // Quantum per workgroup: ONE wave, 32 B of every operand per lane (two 16-B items for
+    // UInt16, four 8-B items for UInt8, one 32-B item for Float32) = 2 KiB per operand.
+    // Measured on MI355X for the 3-stream UInt16 Sum at 1024^3 (tools/kbench7.hip,
+    // kbench9.hip, after clocks settle): 0.98-0.99 ms (6.5 TB/s) against 1.01-1.08 ms for
+    // the former 4 waves x 4 items (16 KiB per operand): small one-shot workgroups keep more
+    // distinct DRAM pages in flight per CU while the moving window stays compact.
+    constexpr int kVecBlock = 64;
+    template <int BPV>
+    constexpr int vecUnroll()
+    {
+        return BPV == 1 ? 4 : BPV == 2 ? 2 : 1;
+    }
 
     // MODE 0: one collapsed row; 1: rows, 32-bit magic division; 2: rows, 64-bit division.
     template <int NS, int BPV, int MODE, class F>
@@ -128,9 +140,10 @@ namespace hipk
     __device__ __forceinline__ void pointwiseVecSpan(Operand const& d, Operand const& s1, Operand const& s2,
                                                      Geom const& g, uint64_t beg, uint64_t end, F const& f)
     {
-        constexpr uint64_t kQ = static_cast<uint64_t>(kBlock) * kUnroll;
+        constexpr int kUnroll = vecUnroll<BPV>();
+        constexpr uint64_t kQ = static_cast<uint64_t>(kVecBlock) * kUnroll;
         uint64_t it = beg + threadIdx.x;
-        for (; it + (kUnroll - 1) * static_cast<uint64_t>(kBlock) < end; it += kQ)
+        for (; it + (kUnroll - 1) * static_cast<uint64_t>(kVecBlock) < end; it += kQ)
         {
             uint32_t a[kUnroll][8], b[kUnroll][8];
             uint64_t od[kUnroll];
@@ -138,7 +151,7 @@ namespace hipk
             for (int u = 0; u < kUnroll; ++u)
             {
                 uint64_t o1, o2;
-                pointwiseVecItem<NS, BPV, MODE, F>(d, s1, s2, g, it + static_cast<uint64_t>(u) * kBlock, o1, o2,
+                pointwiseVecItem<NS, BPV, MODE, F>(d, s1, s2, g, it + static_cast<uint64_t>(u) * kVecBlock, o1, o2,
                                                    od[u]);
                 if constexpr (NS >= 1)
                     load8<BPV, true>(s1.data, o1, a[u]);
@@ -155,7 +168,7 @@ namespace hipk
                 store8<BPV, true>(d.data, od[u], o);
             }
         }
-        for (; it < end; it += kBlock)
+        for (; it < end; it += kVecBlock)
         {
             uint32_t a[8], b[8], o[8];
             uint64_t o1, o2, od;
@@ -171,19 +184,20 @@ namespace hipk
         }
     }
 
-    // Work distribution: workgroup q handles the q-th quantum of kBlock*kUnroll items and
+    // Work distribution: workgroup q handles the q-th quantum of kVecBlock*kUnroll items and
     // the grid holds one workgroup per quantum (grid-stride only beyond 2^30 quanta).  Short
     // one-shot workgroups dispatched in order make the whole chip sweep memory as one
     // compact moving window: measured 1.05 ms (6.1 TB/s) for UInt16 Sum at 1024^3 against
-    // 1.20 ms for 4096 persistent workgroups that each stream their own span.
+    // 1.20 ms for 4096 persistent workgroups that each stream their own span (16-KiB quanta;
+    // the 2-KiB quanta above gain another ~5%).
     template <int NS, int BPV, class F>
-    __global__ __launch_bounds__(kBlock) void pointwiseVecKernel(Operand d, Operand s1, Operand s2, Geom g, F f)
+    __global__ __launch_bounds__(kVecBlock) void pointwiseVecKernel(Operand d, Operand s1, Operand s2, Geom g, F f)
     {
         uint64_t const cpr = static_cast<uint64_t>(g.vnx8 - g.vhead) >> 3;   // chunks per row
         uint64_t const rows = static_cast<uint64_t>(g.vny) * static_cast<uint64_t>(g.vnz);
         uint64_t const items = cpr * rows;
         uint64_t const ny = static_cast<uint64_t>(g.vny);
-        constexpr uint64_t kQ = static_cast<uint64_t>(kBlock) * kUnroll;
+        constexpr uint64_t kQ = static_cast<uint64_t>(kVecBlock) * vecUnroll<BPV>();
         for (uint64_t q = blockIdx.x; q * kQ < items; q += gridDim.x)
         {
             uint64_t const beg = q * kQ;
@@ -275,16 +289,17 @@ namespace hipk
             {
                 uint64_t items = static_cast<uint64_t>(p.g.vny) * static_cast<uint64_t>(p.g.vnz) *
                                  static_cast<uint64_t>((p.g.vnx8 - p.g.vhead) / 8);
-                uint64_t quanta = (items + kBlock * kUnroll - 1) / (kBlock * kUnroll);
+                constexpr uint64_t kQ = static_cast<uint64_t>(kVecBlock) * vecUnroll<BPV>();
+                uint64_t quanta = (items + kQ - 1) / kQ;
                 // enough threads for the scalar row edges too (narrow boxes are all edge)
                 uint64_t edgeItems = static_cast<uint64_t>(p.g.vny) * static_cast<uint64_t>(p.g.vnz) *
                                      static_cast<uint64_t>(p.g.vhead + (p.g.vnx - p.g.vnx8));
-                uint64_t edgeBlocks = (edgeItems + kBlock - 1) / kBlock;
-                edgeBlocks = edgeBlocks < 2048 ? edgeBlocks : 2048;
+                uint64_t edgeBlocks = (edgeItems + kVecBlock - 1) / kVecBlock;
+                edgeBlocks = edgeBlocks < 4096 ? edgeBlocks : 4096;
                 if (quanta < edgeBlocks)
                     quanta = edgeBlocks;
                 unsigned grid = static_cast<unsigned>(quanta < (1u << 30) ? (quanta > 0 ? quanta : 1) : (1u << 30));
-                hipLaunchKernelGGL((pointwiseVecKernel<NS, BPV, F>), dim3(grid), dim3(kBlock), 0, stream,
+                hipLaunchKernelGGL((pointwiseVecKernel<NS, BPV, F>), dim3(grid), dim3(kVecBlock), 0, stream,
                                    p.d, p.s1, p.s2, p.g, f);
                 return vktNoError;
             }

@@ -27,7 +27,7 @@ namespace hipk
 
     // dst = map_dst(unmap_src(code))  (CopyRange by value, Copy_serial.hpp:69-70;
     // Resample same-dims branch, Resample_serial.hpp:32-48)
-    template <int FS, int FD>
+    template <int FS, int FD, int DIV = 0>
     struct ConvertF
     {
         int32_t fs, fd;
@@ -37,7 +37,7 @@ namespace hipk
         {
             float v = codec::decode(a, FS == kDyn ? fs : FS, slo, shi);
             bool w;
-            return codec::encode(v, FD == kDyn ? fd : FD, dm, w);
+            return codec::encode<DIV>(v, FD == kDyn ? fd : FD, dm, w);
         }
     };
 
@@ -57,7 +57,7 @@ namespace hipk
         else return codec::clampRef(fabsf(a - b), lo, hi);
     }
 
-    template <int OP, int FS1, int FS2, int FD>
+    template <int OP, int FS1, int FS2, int FD, int DIV = 0>
     struct ArithF
     {
         int32_t fs1, fs2, fd;
@@ -69,7 +69,7 @@ namespace hipk
             float v2 = codec::decode(b, FS2 == kDyn ? fs2 : FS2, lo2, hi2);
             float r = applyOp<OP>(v1, v2, dm.lo, dm.hi);
             bool w;
-            return codec::encode(r, FD == kDyn ? fd : FD, dm, w);
+            return codec::encode<DIV>(r, FD == kDyn ? fd : FD, dm, w);
         }
     };
 
@@ -94,18 +94,19 @@ namespace hipk
         int32_t f1 = a.dataFormat, f2 = b.dataFormat, fd = d.dataFormat;
         if (p.vec && f1 == f2 && f1 == fd)
         {
+#define VKT_ARITH_FIXED(FMT, BPV)                                                                              \
+    return dm.rangeIsPow2                                                                                      \
+               ? launchPointwise<2, BPV>(p, ArithF<OP, FMT, FMT, FMT, 1>{f1, f2, fd, a.mappingLo, a.mappingHi,  \
+                                                                         b.mappingLo, b.mappingHi, dm}, s)      \
+               : launchPointwise<2, BPV>(p, ArithF<OP, FMT, FMT, FMT, 2>{f1, f2, fd, a.mappingLo, a.mappingHi,  \
+                                                                         b.mappingLo, b.mappingHi, dm}, s)
             if (fd == codec::FmtUInt16)
-                return launchPointwise<2, 2>(
-                    p, ArithF<OP, codec::FmtUInt16, codec::FmtUInt16, codec::FmtUInt16>{
-                           f1, f2, fd, a.mappingLo, a.mappingHi, b.mappingLo, b.mappingHi, dm}, s);
+                VKT_ARITH_FIXED(codec::FmtUInt16, 2);
             if (fd == codec::FmtUInt8)
-                return launchPointwise<2, 1>(
-                    p, ArithF<OP, codec::FmtUInt8, codec::FmtUInt8, codec::FmtUInt8>{
-                           f1, f2, fd, a.mappingLo, a.mappingHi, b.mappingLo, b.mappingHi, dm}, s);
+                VKT_ARITH_FIXED(codec::FmtUInt8, 1);
             if (fd == codec::FmtFloat32)
-                return launchPointwise<2, 4>(
-                    p, ArithF<OP, codec::FmtFloat32, codec::FmtFloat32, codec::FmtFloat32>{
-                           f1, f2, fd, a.mappingLo, a.mappingHi, b.mappingLo, b.mappingHi, dm}, s);
+                VKT_ARITH_FIXED(codec::FmtFloat32, 4);
+#undef VKT_ARITH_FIXED
         }
         return launchByBpv<2>(p, ArithF<OP, kDyn, kDyn, kDyn>{f1, f2, fd, a.mappingLo, a.mappingHi, b.mappingLo,
                                                                b.mappingHi, dm}, s);
