@@ -4,11 +4,13 @@ One step = the metric pipeline on device-resident synthetic data:
     Resample(R, S, Linear)      S = 512^3 UInt16  ->  R = 1024^3 UInt16
     SumRange(D, R, B, 0, dims)  B, D = 1024^3 UInt16
 per GPU.  With N GPUs (torchrun, one process per GPU, RCCL) the volumes are Z-slab
-partitioned: global dst = 1024 x 1024 x (1024*N), source 512 x 512 x (512*N); every rank
-owns one 1024^3 dst slab and its 512^3 source slab (weak scaling; at N=8 the global dst has
-the voxel count of the 2048^3 config).  The exact z index table keeps every rank's reads in
-its own source slab for this ratio and format, so no plane crosses ranks (the exchange plan
-is still computed and executed -- it is empty).
+partitioned and the global grid doubles one axis per doubling of N (x, then y, then z):
+N=1 1024^3, N=2 2048x1024x1024, N=4 2048x2048x1024, N=8 2048^3 (BASELINE config 4:
+1024^3 -> 2048^3 + SumRange 2048^3), the source being half of it per axis.  Every rank owns
+1024^3 dst voxels (weak scaling).  The exact z index table keeps every rank's reads in its
+own source slab for this ratio and format, so no plane crosses ranks (the exchange plan is
+still computed and executed -- it is empty).  --layout-gpus M runs rank 0's
+slab of the M-GPU layout on one GPU (per-rank rehearsal of the multi-GPU shapes).
 
 value = dst voxels of all ranks / wall time per step (Gvoxels/s).  roofline: the dominant
 kernel (SumRange: 6 B/voxel algorithmic) timed with HIP events on the compute stream.
@@ -37,11 +39,27 @@ def parse():
     p.add_argument("--dst", type=int, default=1024, help="per-GPU dst cube edge (source = dst/2)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-dst", type=int, default=768, help="dst edge of the CPU-baseline sample")
+    p.add_argument("--layout-gpus", type=int, default=0,
+                   help="single process: run rank 0's slab of the M-GPU global layout")
     p.add_argument("--dist-backend", default="nccl",
                    help="torch.distributed backend for N>1 (nccl = RCCL over xGMI; gloo only for rehearsal)")
     p.add_argument("--rehearse-one-device", action="store_true",
                    help="put every rank on device 0 (multi-rank rehearsal on a 1-GPU box, with --dist-backend gloo)")
     return p.parse_args()
+
+
+def global_dims(edge, n):
+    """Global dst dims for n GPUs: edge^3, doubling x, y, z in turn for each doubling of n
+    (n=8 -> (2*edge)^3, BASELINE config 4).  Non-powers of two stack slabs in z."""
+    dims = [edge, edge, edge]
+    if n & (n - 1) == 0:
+        k = 0
+        while (1 << k) < n:
+            dims[k % 3] *= 2
+            k += 1
+    else:
+        dims[2] *= n
+    return dims
 
 
 def cpu_baseline(dst_edge):
@@ -98,25 +116,29 @@ def main():
     ep.device = vkt.ExecutionPolicy.Device_GPU
     vkt.SetThreadExecutionPolicy(ep)
 
-    E = args.dst
-    S = E // 2
     UINT16, LINEAR = vkt.DataFormat_UInt16, vkt.FilterMode_Linear
-    dst_gdz, src_gdz = E * world, S * world
-    plan = slab.plan_resample(dst_gdz, src_gdz, world, rank, LINEAR, chain=False)
+    layout_n = world
+    if args.layout_gpus:
+        if world != 1:
+            raise SystemExit("--layout-gpus is a single-process option")
+        layout_n = args.layout_gpus
+    DX, DY, dst_gdz = global_dims(args.dst, layout_n)
+    SX, SY, src_gdz = DX // 2, DY // 2, dst_gdz // 2
+    plan = slab.plan_resample(dst_gdz, src_gdz, layout_n, rank, LINEAR, chain=False)
     ls0, ls1 = plan.local_src
     dz0, dz1 = plan.dst
 
     # device-resident volumes (allocated on HBM directly: GPU policy at construction)
-    Sv = vkt.StructuredVolume(S, S, ls1 - ls0, UINT16)
-    Rv = vkt.StructuredVolume(E, E, dz1 - dz0, UINT16)
-    Bv = vkt.StructuredVolume(E, E, dz1 - dz0, UINT16)
-    Dv = vkt.StructuredVolume(E, E, dz1 - dz0, UINT16)
+    Sv = vkt.StructuredVolume(SX, SY, ls1 - ls0, UINT16)
+    Rv = vkt.StructuredVolume(DX, DY, dz1 - dz0, UINT16)
+    Bv = vkt.StructuredVolume(DX, DY, dz1 - dz0, UINT16)
+    Dv = vkt.StructuredVolume(DX, DY, dz1 - dz0, UINT16)
     for k, v in enumerate((Sv, Bv)):
         assert vkt.Synthesize(v, 0x5EED + k + 1000 * rank) == 0, vkt.last_error()
     sview, rview, bview, dview = Sv.hip_view(), Rv.hip_view(), Bv.hip_view(), Dv.hip_view()
     first = _lib_vec(0, 0, 0)
-    last = _lib_vec(E, E, dz1 - dz0)
-    plane_bytes = S * S * 2
+    last = _lib_vec(DX, DY, dz1 - dz0)
+    plane_bytes = SX * SY * 2
 
     def planes(g0, g1):
         return slab.device_tensor(sview.data + (g0 - ls0) * plane_bytes, (g1 - g0) * plane_bytes)
@@ -165,21 +187,21 @@ def main():
     res_ms = sum(a.elapsed_time(b) for a, b in t_res) / len(t_res)
     sum_ms = sum(a.elapsed_time(b) for a, b in t_sum) / len(t_sum)
     ms_per_step = elapsed * 1e3 / args.steps
-    vox_rank = E * E * (dz1 - dz0)
-    total_vox = E * E * dst_gdz
+    vox_rank = DX * DY * (dz1 - dz0)
+    total_vox = vox_rank * world
     value = total_vox / (ms_per_step / 1e3) / 1e9
 
     # algorithmic bytes per launch: SumRange 6 B/voxel; Resample
     # N_src*2 + N_dst*2
     sum_bytes = 6 * vox_rank
-    res_bytes = 2 * S * S * (ls1 - ls0) + 2 * vox_rank
+    res_bytes = 2 * SX * SY * (ls1 - ls0) + 2 * vox_rank
     pipe_bytes = sum_bytes + res_bytes
     traffic = None
     tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(tf):
         try:
             pm = json.load(open(tf))
-            if pm.get("bench_dst_edge") == E:   # only for the workload the counters were taken on
+            if pm.get("bench_dst_edge") == args.dst and layout_n == 1:   # only for the workload the counters were taken on
                 traffic = pm.get("SumRange_bytes_per_launch")
         except Exception:
             traffic = None
@@ -198,9 +220,12 @@ def main():
         "dtype": "u16",
         "data": "synthetic (splitmix64 codes, device-resident)",
         "config": {
-            "workload": f"Resample {S}^3->{E}^3 UInt16 Linear + SumRange {E}^3 UInt16 per GPU",
-            "global_dst": [E, E, dst_gdz], "global_src": [S, S, src_gdz],
-            "parallelism": f"zslab{world}", "halo_planes_per_rank": plan.halo_planes,
+            "workload": f"Resample {SX}x{SY}x{src_gdz}->{DX}x{DY}x{dst_gdz} UInt16 Linear + SumRange "
+                        f"{DX}x{DY}x{dst_gdz} UInt16, Z-slab over {layout_n} GPU(s)"
+                        + (f" (rank 0's slab only, on 1 GPU)" if layout_n != world else ""),
+            "global_dst": [DX, DY, dst_gdz], "global_src": [SX, SY, src_gdz],
+            "slab_dst_per_rank": [DX, DY, dz1 - dz0],
+            "parallelism": f"zslab{layout_n}", "halo_planes_per_rank": plan.halo_planes,
         },
         "pipeline_hbm_gbs": round(pipe_bytes * world / (ms_per_step / 1e3) / 1e9, 1),
         "kernels_ms": {"Resample": round(res_ms, 4), "SumRange": round(sum_ms, 4)},

@@ -120,11 +120,20 @@ def test_plan_partition_covers_volume():
 
 
 def test_metric_config_needs_no_halo():
-    """Weak-scaling bench layout: dst 1024*N planes from src 512*N, UInt16 -> no exchange."""
+    """bench.py's weak-scaling layout (N=8: 1024^3 -> 2048^3, BASELINE config 4), UInt16 ->
+    no exchange; every rank owns the same number of dst voxels."""
+    import bench
     from volkit_amd import slab
+    assert bench.global_dims(1024, 1) == [1024, 1024, 1024]
+    assert bench.global_dims(1024, 2) == [2048, 1024, 1024]
+    assert bench.global_dims(1024, 4) == [2048, 2048, 1024]
+    assert bench.global_dims(1024, 8) == [2048, 2048, 2048]
     for world in (2, 4, 8):
+        dx, dy, dz = bench.global_dims(1024, world)
         for rank in range(world):
-            p = slab.plan_resample(1024 * world, 512 * world, world, rank, 1, chain=False)
+            p = slab.plan_resample(dz, dz // 2, world, rank, 1, chain=False)
             assert p.recvs == [] and p.sends == []
-            pf = slab.plan_resample(1024 * world, 512 * world, world, rank, 1, chain=True)
+            z0, z1 = p.dst
+            assert dx * dy * (z1 - z0) == 1024 ** 3
+            pf = slab.plan_resample(dz, dz // 2, world, rank, 1, chain=True)
             assert pf.halo_planes == (0 if rank == world - 1 else 2)
