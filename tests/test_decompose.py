@@ -24,6 +24,12 @@ LAYOUTS = [
     ((33, 17, 5), (8, 32, 2), (2, 0, 1), (0, 3, 0)),
     ((64, 64, 64), (64, 64, 64), (0, 0, 0), (0, 0, 0)),
     ((7, 5, 3), (1, 2, 3), (0, 1, 0), (1, 0, 2)),
+    # 16-byte items spanning two brick rows (linear mode), clamped halos on every face
+    ((70, 40, 33), (20, 20, 20), (1, 2, 1), (3, 1, 2)),
+    ((100, 37, 19), (37, 13, 7), (2, 2, 2), (2, 2, 2)),
+    ((131, 9, 4), (64, 4, 4), (5, 0, 0), (7, 0, 0)),
+    # bricks of many 16-KiB workgroup chunks, chunk boundaries inside rows
+    ((150, 97, 61), (64, 48, 40), (1, 1, 1), (2, 1, 3)),
 ]
 
 
@@ -160,6 +166,36 @@ def test_brick_with_other_mapping_converts():
         ref = ob.Volume.zeros(bdims, 5, lo, hi)
         ob.copy_range(ref, src, *ranges[idx])
         np.testing.assert_array_equal(got[idx], ref.codes, err_msg=f"brick {idx}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fmt", [4, 5, 7])
+def test_brick_larger_than_its_range(fmt):
+    """A brick allocated larger than its copy box keeps its own row/plane pitch (row mode of
+    the batched kernel): voxels outside the box are left untouched."""
+    rng = np.random.default_rng(fmt)
+    codes = rand_codes(rng, fmt, (11, 13, 41))
+
+    def tweak(arr):
+        arr[(0, 1, 1)].setDims(40, 9, 8)
+        arr[(1, 0, 0)].setDims(23, 9, 6)
+
+    err, got = gpu_decompose(codes, fmt, (0.0, 1.0), (20, 6, 5), (1, 1, 0), (2, 0, 1), tweak)
+    assert err == vkt.NoError, vkt.last_error()
+    src = ob.Volume(codes, fmt)
+    nb, layout = ob.brick_layout(src.dims, (20, 6, 5), (1, 1, 0), (2, 0, 1))
+    ranges = ob.brick_ranges(src.dims, nb, (20, 6, 5), (1, 1, 0), (2, 0, 1))
+    for idx, bdims in layout.items():
+        bdims = {(0, 1, 1): (40, 9, 8), (1, 0, 0): (23, 9, 6)}.get(idx, bdims)
+        ref = ob.Volume.zeros(bdims, fmt)
+        ob.copy_range(ref, src, *ranges[idx])
+        g = got[idx]
+        if idx in ((0, 1, 1), (1, 0, 0)):
+            # the resized brick's bytes outside the box were never written: compare the box
+            fz, fy, fx = [r1 - r0 for r0, r1 in zip(ranges[idx][0][::-1], ranges[idx][1][::-1])]
+            np.testing.assert_array_equal(g[:fz, :fy, :fx], ref.codes[:fz, :fy, :fx], err_msg=f"brick {idx}")
+        else:
+            np.testing.assert_array_equal(g, ref.codes, err_msg=f"brick {idx}")
 
 
 @pytest.mark.gpu

@@ -112,11 +112,15 @@ def main():
         ep.device = vkt.ExecutionPolicy.Device_GPU
         vkt.SetThreadExecutionPolicy(ep)
         n = 1024
-        for bs, halo in ((64, 1), (128, 0), (32, 1)):
+        cases = [(64, (1, 1, 1)), (128, (0, 0, 0)), (32, (1, 1, 1))]
+        if os.environ.get("VKT_DECOMP_CASES"):   # "bs:hx,hy,hz;..."
+            cases = [(int(c.split(":")[0]), tuple(int(h) for h in c.split(":")[1].split(",")))
+                     for c in os.environ["VKT_DECOMP_CASES"].split(";")]
+        for bs, halo in cases:
             V = vkt.StructuredVolume(n, n, n, vkt.DataFormat_UInt16)
             vkt.Synthesize(V, 77)
             arr = vkt.Array3D_StructuredVolume()
-            b3, h3 = vkt.Vec3i(bs, bs, bs), vkt.Vec3i(halo, halo, halo)
+            b3, h3 = vkt.Vec3i(bs, bs, bs), vkt.Vec3i(*halo)
             vkt.BrickDecomposeResize(arr, V, b3, h3, h3)
             vox = sum(arr[(i, j, k)].getSizeInBytes() // 2 for k in range(arr.dims().z)
                       for j in range(arr.dims().y) for i in range(arr.dims().x))
