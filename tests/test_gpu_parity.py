@@ -282,17 +282,35 @@ def test_arithmetic_subbox_phases(g, o, fmt):
             assert_codes_equal(out, ref, fmt, f"{op} fmt={fmt} {first}->{last}+{off}")
 
 
-@pytest.mark.parametrize("sfmt,dfmt", [(5, 5), (4, 4), (7, 7), (7, 5), (5, 7)])
+@pytest.mark.parametrize("sfmt,dfmt", [(5, 5), (4, 4), (7, 7), (7, 5), (5, 7), (4, 7), (7, 4)])
 def test_resample_vector_gather_and_row_chain(g, o, sfmt, dfmt):
     rng = np.random.default_rng(sfmt * 10 + dfmt)
     for sd, dd in (((96, 20, 12), (64, 24, 16)), ((40, 24, 10), (128, 16, 20)), ((64, 32, 8), (256, 64, 16)),
-                   ((256, 8, 4), (512, 16, 8)), ((100, 10, 5), (400, 20, 10))):
+                   ((256, 8, 4), (512, 16, 8)), ((100, 10, 5), (400, 20, 10)),
+                   # LDS-staged gather: 16-byte-multiple source rows, non-integer ratios
+                   ((48, 20, 12), (80, 24, 16)), ((256, 12, 6), (144, 20, 9)), ((64, 9, 7), (208, 13, 11))):
         src = rand_codes(rng, sfmt, sd[::-1])
         for smap, dmap in (((0.0, 1.0), (0.0, 1.0)), ((0.0, 1.0), (-1.0, 3.0))):
             for fm in (0, 1):
                 out = g.resample(dfmt, dmap, dd, sfmt, smap, src, fm)
                 ref = o.resample(dfmt, dmap, dd, sfmt, smap, src, fm)
                 assert_codes_equal(out, ref, dfmt, f"resample {sd}->{dd} {sfmt}->{dfmt} fm={fm} {smap}->{dmap}")
+
+
+@pytest.mark.parametrize("sfmt", [4, 5, 2])
+def test_resample_integer_source_to_float_linear(g, o, sfmt):
+    """Integer codes -> Float32 "Linear": the chain equals v000 unless the source mapping can
+    unmap to -0 (lo = hi = -0 side), which a Float32 destination would store as +0 after the
+    chain.  Mappings that can / cannot produce -0, integer and non-integer ratios."""
+    rng = np.random.default_rng(sfmt + 7)
+    for sd, dd in (((32, 16, 8), (64, 32, 16)), ((30, 17, 9), (64, 40, 16)), ((64, 16, 8), (40, 10, 5))):
+        src = rand_codes(rng, sfmt, sd[::-1])
+        src.reshape(-1)[:7] = 0   # code 0 -> lo (-0 for lo = -0)
+        for smap in ((0.0, 1.0), (-0.0, 1.0), (-0.0, -1.0), (-0.0, -0.0), (-1.0, -0.0), (2.0, -3.0)):
+            for dmap in ((0.0, 1.0), (-1.0, 3.0)):
+                out = g.resample(7, dmap, dd, sfmt, smap, src, 1)
+                ref = o.resample(7, dmap, dd, sfmt, smap, src, 1)
+                assert_codes_equal(out, ref, 7, f"resample {sd}->{dd} {sfmt}->7 Linear {smap}->{dmap}")
 
 
 @pytest.mark.parametrize("dfmt", [7, 5])
@@ -302,7 +320,9 @@ def test_resample_chain_sparse_specials(g, o, dfmt):
     sit where the chain's neighbourhood crosses rows: a row's first voxel (hi.x of the row
     before), the y+1 / z+1 neighbour rows, the last voxel of the buffer (clamped hi.x)."""
     rng = np.random.default_rng(99 + dfmt)
-    for sd, dd in (((64, 32, 8), (128, 64, 16)), ((64, 16, 6), (64, 32, 12)), ((32, 8, 4), (128, 32, 16))):
+    for sd, dd in (((64, 32, 8), (128, 64, 16)), ((64, 16, 6), (64, 32, 12)), ((32, 8, 4), (128, 32, 16)),
+                   # non-integer ratios: flagged gather (rowDirty + rowChain pre-pass)
+                   ((60, 30, 9), (128, 64, 16)), ((64, 16, 6), (48, 20, 5)), ((33, 8, 4), (100, 30, 9))):
         sx, sy, sz = sd
         vals = rng.uniform(0.0, 1.0, size=(sz, sy, sx)).astype(np.float32)
         cases = [

@@ -105,6 +105,20 @@ def main():
             ms = timed(lambda: lib.vktHipResample(Rv, S, fm), max(3, R // 3))
             report(f"config3 Resample 1024^3->2048^3 Float32 {lab}", ms, 4 * s ** 3 + 4 * e ** 3, e ** 3)
         free(S, Rv)
+    if want("gather"):
+        # non-integer ratios (gather path): up/down-sampling 768^3 <-> 1024^3, all dst formats
+        cases = [(768, 1024, 5, 1), (1024, 768, 5, 1), (768, 1024, 4, 1), (768, 1024, 7, 0), (768, 1024, 7, 1),
+                 (1024, 768, 7, 1), (1000, 1024, 5, 1)]
+        for se, de, fmt, fm in cases:
+            b = {4: 1, 5: 2, 7: 4}[fmt]
+            S = alloc((se,) * 3, fmt, seed=21)
+            if fmt == 7:
+                rng_fill(S, se ** 3)
+            Rv = alloc((de,) * 3, fmt)
+            ms = timed(lambda: lib.vktHipResample(Rv, S, fm), max(3, R // 2))
+            report(f"gather Resample {se}^3->{de}^3 fmt{fmt} {'Linear' if fm else 'Nearest'}", ms,
+                   b * se ** 3 + b * de ** 3, de ** 3)
+            free(S, Rv)
     if want("decompose"):
         # BrickDecompose: 1024^3 UInt16 into 64^3 bricks with a 1-voxel halo
         import volkit_amd.volkit as vkt

@@ -72,10 +72,63 @@ namespace hipk
         }
     }
 
+    // ---- "Linear" with float semantics: the exact sampleLinear lerp chain -------------
+    // Value depends only on the source position, so it is evaluated per destination voxel
+    // from the 8 neighbours (StructuredVolumeView.hpp:80-119): lo = (sx,sy,sz); hi.x reads
+    // the next voxel in memory (unclamped in the reference); hi.y, hi.z are clamped.
+    __device__ __forceinline__ float flatValue(ResampleArgs const& a, uint64_t voxel, uint32_t bs)
+    {
+        if (voxel >= a.srcVoxels)
+            voxel = a.srcVoxels - 1;   // reference reads past the buffer end (UB); clamp
+        return codec::decode(loadCodeDyn(a.src, voxel, bs), a.fs, a.slo, a.shi);
+    }
+
+    // One task (source row (ry.s, rz.s) -> its dst rectangle) of the chain, lane-strided.
+    __device__ __forceinline__ void chainTask(ResampleArgs const& a, Run const& ry, Run const& rz, int lane)
+    {
+        uint32_t const bs = codec::bytesPerVoxel(a.fs), bd = codec::bytesPerVoxel(a.fd);
+        int32_t const hy = ry.s + 1 < a.sdy ? ry.s + 1 : a.sdy - 1;
+        int32_t const hz = rz.s + 1 < a.srcGlobalDz ? rz.s + 1 : a.srcGlobalDz - 1;
+        uint64_t const r00 = srcRowIndex(a, ry.s, rz.s), r10 = srcRowIndex(a, hy, rz.s);
+        uint64_t const r01 = srcRowIndex(a, ry.s, hz), r11 = srcRowIndex(a, hy, hz);
+        for (int32_t x = lane; x < a.ddx; x += 64)
+        {
+            uint64_t const sx = static_cast<uint64_t>(a.xtab[x]);
+            float v0 = flatValue(a, r00 + sx, bs), v1 = flatValue(a, r00 + sx + 1, bs);
+            float v2 = flatValue(a, r10 + sx, bs), v3 = flatValue(a, r10 + sx + 1, bs);
+            float v4 = flatValue(a, r01 + sx, bs), v5 = flatValue(a, r01 + sx + 1, bs);
+            float v6 = flatValue(a, r11 + sx, bs), v7 = flatValue(a, r11 + sx + 1, bs);
+            float const f = 0.f;   // xf1 - lo.x etc.: lo is never clamped, so every fraction is 0
+            float value = codec::lerp(codec::lerp(codec::lerp(v0, v1, f), codec::lerp(v2, v3, f), f),
+                                      codec::lerp(codec::lerp(v4, v5, f), codec::lerp(v6, v7, f), f), f);
+            bool w;
+            uint32_t c = codec::encode(value, a.fd, a.dm, w);
+            for (int32_t zd = rz.d0; zd < rz.d1; ++zd)
+                for (int32_t yd = ry.d0; yd < ry.d1; ++yd)
+                    storeCodeDyn(a.dst, dstRowIndex(a, yd, zd) + static_cast<uint64_t>(x), bd, c);
+        }
+    }
+
+    __global__ __launch_bounds__(kBlock) void resampleChainKernel(ResampleArgs a)
+    {
+        int const lane = threadIdx.x & 63;
+        uint32_t const wavesPerBlock = blockDim.x >> 6;
+        uint32_t const wave = xcdSwizzle(blockIdx.x, gridDim.x) * wavesPerBlock + (threadIdx.x >> 6);
+        uint32_t const totalWaves = gridDim.x * wavesPerBlock;
+        uint32_t const tasks = static_cast<uint32_t>(a.nRunsY) * static_cast<uint32_t>(a.nRunsZ);
+        for (uint32_t t = wave; t < tasks; t += totalWaves)
+            chainTask(a, runY(a, t % static_cast<uint32_t>(a.nRunsY)), runZ(a, t / static_cast<uint32_t>(a.nRunsY)),
+                      lane);
+    }
+
     // Vectorised gather: lane l handles V = 16 / BPVD consecutive destination voxels, reads
     // their V exact x-table entries and V source codes (the row is L1/L2-resident while the
     // wave sweeps it) and writes one 16-byte nontemporal store per destination row.
-    template <int BPVD, bool CONV>
+    // CHAIN (Float32 "Linear", any ratio): a task whose source rows' chain neighbourhood holds
+    // a non-finite value or a -0 (a.rowChain, from rowDirtyKernel + rowChainKernel) evaluates
+    // the full lerp chain (chainTask); every other task's chain equals v000 exactly, so it is
+    // a plain gather -- the 8 neighbour reads per voxel are skipped.
+    template <int BPVD, bool CONV, bool CHAIN = false>
     __global__ __launch_bounds__(kBlock) void resampleGatherVecKernel(ResampleArgs a)
     {
         constexpr int V = 16 / BPVD;
@@ -92,6 +145,14 @@ namespace hipk
             Run const ry = runY(a, t % static_cast<uint32_t>(a.nRunsY));
             Run const rz = runZ(a, t / static_cast<uint32_t>(a.nRunsY));
             uint64_t const srow = srcRowIndex(a, ry.s, rz.s);
+            if constexpr (CHAIN)
+            {
+                if (a.rowChain[srow / static_cast<uint64_t>(a.sdx)])   // wave-uniform
+                {
+                    chainTask(a, ry, rz, lane);
+                    continue;
+                }
+            }
             for (int32_t dx = V * lane; dx < a.ddx; dx += 64 * V)
             {
                 int32_t xs[V];
@@ -123,50 +184,87 @@ namespace hipk
         }
     }
 
-    // ---- "Linear" with float semantics: the exact sampleLinear lerp chain -------------
-    // Value depends only on the source position, so it is evaluated per destination voxel
-    // from the 8 neighbours (StructuredVolumeView.hpp:80-119): lo = (sx,sy,sz); hi.x reads
-    // the next voxel in memory (unclamped in the reference); hi.y, hi.z are clamped.
-    __device__ __forceinline__ float flatValue(ResampleArgs const& a, uint64_t voxel, uint32_t bs)
+    // LDS-staged gather (any ratio): each wave copies its task's source row into its own LDS
+    // slot with coalesced 16-byte loads (every source byte read from L2/HBM once, instead of
+    // one 1-4-byte gather instruction per destination voxel), the workgroup keeps the exact x
+    // table in LDS, and lane l assembles V = 16 / BPVD destination voxels from LDS reads and
+    // writes one 16-byte nontemporal store per destination row of the task's rectangle.
+    // Preconditions (host): rows are 16-byte multiples, 16-byte aligned buffers, 4 slots fit.
+    template <int BPVS, int BPVD, bool CONV, bool CHAIN>
+    __global__ __launch_bounds__(kBlock) void resampleGatherLdsKernel(ResampleArgs a, uint32_t slotBytes)
     {
-        if (voxel >= a.srcVoxels)
-            voxel = a.srcVoxels - 1;   // reference reads past the buffer end (UB); clamp
-        return codec::decode(loadCodeDyn(a.src, voxel, bs), a.fs, a.slo, a.shi);
-    }
-
-    __global__ __launch_bounds__(kBlock) void resampleChainKernel(ResampleArgs a)
-    {
+        constexpr int V = 16 / BPVD;
+        extern __shared__ u32x4 ldsRaw[];
+        uint8_t* const lds = reinterpret_cast<uint8_t*>(ldsRaw);
+        int32_t* const xt = reinterpret_cast<int32_t*>(lds);                  // ddx entries (padded)
+        uint32_t const xtBytes = (static_cast<uint32_t>(a.ddx) * 4u + 15u) & ~15u;
         int const lane = threadIdx.x & 63;
+        uint32_t const wib = threadIdx.x >> 6;
+        uint8_t* const slot = lds + xtBytes + wib * slotBytes;
+        for (uint32_t i = threadIdx.x * 4; i < static_cast<uint32_t>(a.ddx); i += kBlock * 4)
+            *reinterpret_cast<u32x4*>(xt + i) = *reinterpret_cast<u32x4 const*>(a.xtab + i);
+        __syncthreads();
+
         uint32_t const wavesPerBlock = blockDim.x >> 6;
-        uint32_t const wave = xcdSwizzle(blockIdx.x, gridDim.x) * wavesPerBlock + (threadIdx.x >> 6);
+        uint32_t const wave = __builtin_amdgcn_readfirstlane(xcdSwizzle(blockIdx.x, gridDim.x) * wavesPerBlock + wib);
         uint32_t const totalWaves = gridDim.x * wavesPerBlock;
         uint32_t const tasks = static_cast<uint32_t>(a.nRunsY) * static_cast<uint32_t>(a.nRunsZ);
-        uint32_t const bs = codec::bytesPerVoxel(a.fs), bd = codec::bytesPerVoxel(a.fd);
-
+        uint32_t const rowBytes = static_cast<uint32_t>(a.sdx) * BPVS;
         for (uint32_t t = wave; t < tasks; t += totalWaves)
         {
             Run const ry = runY(a, t % static_cast<uint32_t>(a.nRunsY));
             Run const rz = runZ(a, t / static_cast<uint32_t>(a.nRunsY));
-            int32_t const hy = ry.s + 1 < a.sdy ? ry.s + 1 : a.sdy - 1;
-            int32_t const hz = rz.s + 1 < a.srcGlobalDz ? rz.s + 1 : a.srcGlobalDz - 1;
-            uint64_t const r00 = srcRowIndex(a, ry.s, rz.s), r10 = srcRowIndex(a, hy, rz.s);
-            uint64_t const r01 = srcRowIndex(a, ry.s, hz), r11 = srcRowIndex(a, hy, hz);
-            for (int32_t x = lane; x < a.ddx; x += 64)
+            uint64_t const srow = srcRowIndex(a, ry.s, rz.s);
+            if constexpr (CHAIN)
             {
-                uint64_t const sx = static_cast<uint64_t>(a.xtab[x]);
-                float v0 = flatValue(a, r00 + sx, bs), v1 = flatValue(a, r00 + sx + 1, bs);
-                float v2 = flatValue(a, r10 + sx, bs), v3 = flatValue(a, r10 + sx + 1, bs);
-                float v4 = flatValue(a, r01 + sx, bs), v5 = flatValue(a, r01 + sx + 1, bs);
-                float v6 = flatValue(a, r11 + sx, bs), v7 = flatValue(a, r11 + sx + 1, bs);
-                float const f = 0.f;   // xf1 - lo.x etc.: lo is never clamped, so every fraction is 0
-                float value = codec::lerp(codec::lerp(codec::lerp(v0, v1, f), codec::lerp(v2, v3, f), f),
-                                          codec::lerp(codec::lerp(v4, v5, f), codec::lerp(v6, v7, f), f), f);
-                bool w;
-                uint32_t c = codec::encode(value, a.fd, a.dm, w);
+                if (a.rowChain[srow / static_cast<uint64_t>(a.sdx)])   // wave-uniform
+                {
+                    chainTask(a, ry, rz, lane);
+                    continue;
+                }
+            }
+            uint8_t const* sp = a.src + srow * BPVS;
+            // stage: all of a lane's loads in flight before the first LDS write
+            constexpr int kStage = 4;
+            for (uint32_t o0 = 16u * lane; o0 < rowBytes; o0 += 1024u * kStage)
+            {
+                u32x4 w[kStage];
+#pragma unroll
+                for (int j = 0; j < kStage; ++j)
+                    if (o0 + 1024u * j < rowBytes)
+                        w[j] = __builtin_nontemporal_load(reinterpret_cast<u32x4 const*>(sp + o0 + 1024u * j));
+#pragma unroll
+                for (int j = 0; j < kStage; ++j)
+                    if (o0 + 1024u * j < rowBytes)
+                        *reinterpret_cast<u32x4*>(slot + o0 + 1024u * j) = w[j];
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            for (int32_t dx = V * lane; dx < a.ddx; dx += 64 * V)
+            {
+                uint32_t code[V];
+#pragma unroll
+                for (int i = 0; i < V; i += 4)
+                {
+                    u32x4 const q = *reinterpret_cast<u32x4 const*>(xt + dx + i);
+                    int32_t const xs[4] = {static_cast<int32_t>(q.x), static_cast<int32_t>(q.y),
+                                           static_cast<int32_t>(q.z), static_cast<int32_t>(q.w)};
+#pragma unroll
+                    for (int j = 0; j < 4 && i + j < V; ++j)
+                    {
+                        uint32_t const c = loadCode<BPVS>(slot, static_cast<uint64_t>(xs[j]));
+                        code[i + j] = CONV ? convertCode<-1, -1>(c, a) : c;
+                    }
+                }
                 for (int32_t zd = rz.d0; zd < rz.d1; ++zd)
                     for (int32_t yd = ry.d0; yd < ry.d1; ++yd)
-                        storeCodeDyn(a.dst, dstRowIndex(a, yd, zd) + static_cast<uint64_t>(x), bd, c);
+                        store16<BPVD>(a.dst, dstRowIndex(a, yd, zd) + static_cast<uint64_t>(dx), code);
             }
+            // the slot is rewritten by the next task: every lane's reads first
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
     }
 
@@ -404,11 +502,35 @@ namespace hipk
         return false;      // Float32: raw bits, anything goes
     }
 
-    // Both properties are enumerations over up to 65536 codes (~ms); cache them per mapping.
+    // Can an unmapped source value be -0?  (lerp(a, b, 0) = a + 0*b turns a = -0 into +0 for
+    // b >= +0, which a Float32 destination stores differently.)  (1-t)*lo + t*hi is -0 only
+    // when both products are -0, impossible if lo > 0 or hi > 0.
+    bool negativeZeroPossibleUncached(int32_t fs, float lo, float hi)
+    {
+        if (fs == codec::FmtUInt8 || fs == codec::FmtUInt16 || fs == codec::FmtInt16)
+        {
+            uint32_t n = fs == codec::FmtUInt8 ? 256u : 65536u;
+            for (uint32_t c = 0; c < n; ++c)
+            {
+                float const v = codec::decode(c, fs, lo, hi);
+                if (v == 0.f && std::signbit(v))
+                    return true;
+            }
+            return false;
+        }
+        if (fs == codec::FmtUInt32)
+            return !(lo > 0.f || hi > 0.f);
+        if (fs == codec::FmtInt8 || fs == codec::FmtInt32)
+            return false;   // unmap leaves +0.f
+        return true;        // Float32: raw bits
+    }
+
+    // All properties are enumerations over up to 65536 codes (~ms); cache them per mapping.
     struct ConvProps
     {
         bool identity;
         bool finite;
+        bool negZero;
     };
 
     ConvProps conversionProperties(int32_t fs, float slo, float shi, int32_t fd, float dlo, float dhi)
@@ -421,7 +543,8 @@ namespace hipk
         auto it = cache.find(key);
         if (it != cache.end())
             return it->second;
-        ConvProps p{identityConversionUncached(fs, slo, shi, fd, dlo, dhi), allSourceValuesFiniteUncached(fs, slo, shi)};
+        ConvProps p{identityConversionUncached(fs, slo, shi, fd, dlo, dhi), allSourceValuesFiniteUncached(fs, slo, shi),
+                    negativeZeroPossibleUncached(fs, slo, shi)};
         cache[key] = p;
         return p;
     }
@@ -527,6 +650,49 @@ namespace hipk
         return true;
     }
 
+    bool gatherLdsEnabled()   // A/B tuning knob: VKT_GATHER=vec keeps the per-voxel gather
+    {
+        static bool const on = !(std::getenv("VKT_GATHER") && std::string(std::getenv("VKT_GATHER")) == "vec");
+        return on;
+    }
+
+    // LDS-staged gather when the rows and tables fit (see resampleGatherLdsKernel).
+    bool launchGatherLds(ResampleArgs const& b, uint32_t bs, uint32_t bd, bool identity, bool chain, uint64_t tasks,
+                         hipStream_t s)
+    {
+        if ((bs != 1 && bs != 2 && bs != 4) || (bd != 1 && bd != 2 && bd != 4) || (chain && bs != 4))
+            return false;
+        uint64_t const rowBytes = static_cast<uint64_t>(b.sdx) * bs;
+        uint64_t const xtBytes = (static_cast<uint64_t>(b.ddx) * 4 + 15) & ~uint64_t(15);
+        uint64_t const lds = xtBytes + (kBlock / 64) * rowBytes;
+        if (rowBytes % 16 != 0 || reinterpret_cast<uintptr_t>(b.src) % 16 != 0 || lds > 65536)
+            return false;
+        uint64_t blocks = (tasks + 3) / 4;   // one task per wave
+        unsigned const g = static_cast<unsigned>(blocks < (1u << 30) ? blocks : (1u << 30));
+        uint32_t const slot = static_cast<uint32_t>(rowBytes);
+#define VKT_GL(S, D, C, H) hipLaunchKernelGGL((resampleGatherLdsKernel<S, D, C, H>), dim3(g), dim3(kBlock), lds, s, b, slot)
+#define VKT_GL_D(S, C, H) do { if (bd == 1) VKT_GL(S, 1, C, H); else if (bd == 2) VKT_GL(S, 2, C, H); else VKT_GL(S, 4, C, H); } while (0)
+        if (chain)
+        {
+            if (identity) VKT_GL_D(4, false, true); else VKT_GL_D(4, true, true);
+        }
+        else if (bs == 1)
+        {
+            if (identity) VKT_GL_D(1, false, false); else VKT_GL_D(1, true, false);
+        }
+        else if (bs == 2)
+        {
+            if (identity) VKT_GL_D(2, false, false); else VKT_GL_D(2, true, false);
+        }
+        else
+        {
+            if (identity) VKT_GL_D(4, false, false); else VKT_GL_D(4, true, false);
+        }
+#undef VKT_GL_D
+#undef VKT_GL
+        return true;
+    }
+
     vktError resampleSlab(vktHipVolumeView_t dst, vktHipVolumeView_t src, vktFilterMode fm, int32_t dgz, int32_t dz0,
                           int32_t sgz, int32_t sz0)
     {
@@ -568,7 +734,11 @@ namespace hipk
         ConvProps const props = conversionProperties(src.dataFormat, src.mappingLo, src.mappingHi, dst.dataFormat,
                                                      dst.mappingLo, dst.mappingHi);
         bool const identity = props.identity;
-        bool const chain = fm == vktFilterModeLinear && (dst.dataFormat == codec::FmtFloat32 || !props.finite);
+        // "Linear" = the 8-neighbour lerp chain with every fraction 0; it differs
+        // from v000 only through a non-finite neighbour, or a -0 v000 stored by a Float32
+        // destination.  When the source mapping can produce neither, Linear IS Nearest.
+        bool const chain = fm == vktFilterModeLinear &&
+                           (!props.finite || (dst.dataFormat == codec::FmtFloat32 && props.negZero));
         // planes this dst slab reads: for the chain also the clamped z+1 neighbour plane and
         // the first voxel of the plane after it (hi.x of that plane's last voxel)
         int32_t needLo = t.minSz, needHi = t.maxSz;
@@ -640,13 +810,53 @@ namespace hipk
         uint32_t const bs = codec::bytesPerVoxel(src.dataFormat), bd = codec::bytesPerVoxel(dst.dataFormat);
         if (launchRowKernel(a, t.k, tasks, bs, bd, identity, chain, src, dst, s, t))
             return rt::finishLaunch(chain ? "Resample_hip(row, linear chain)" : "Resample_hip(row)");
+        uint32_t const v = bd <= 4 ? 16 / bd : 0;
+        bool const vecDst = v != 0 && dst.dimX % v == 0 && reinterpret_cast<uintptr_t>(dst.data) % 16 == 0;
+        if (chain && vecDst && src.dataFormat == codec::FmtFloat32 && reinterpret_cast<uintptr_t>(src.data) % 16 == 0)
+        {
+            // any ratio, Float32 source: flag the source rows holding a non-finite value or a
+            // -0 (one streaming read of the source), OR the flags over each row's chain
+            // neighbourhood, then gather -- only flagged tasks evaluate the chain
+            static rt::StreamScratch scratch;
+            uint64_t const srcRows = static_cast<uint64_t>(src.dimY) * static_cast<uint64_t>(src.dimZ);
+            uint8_t* dirty = static_cast<uint8_t*>(scratch.acquire(2 * srcRows, s));
+            if (dirty)
+            {
+                unsigned const gd = static_cast<unsigned>((srcRows + kBlock / 64 - 1) / (kBlock / 64));
+                if (src.dimX % 4 == 0)
+                    hipLaunchKernelGGL(rowDirtyKernel<true>, dim3(gd), dim3(kBlock), 0, s, src.data, src.dimX, srcRows,
+                                       dirty);
+                else
+                    hipLaunchKernelGGL(rowDirtyKernel<false>, dim3(gd), dim3(kBlock), 0, s, src.data, src.dimX, srcRows,
+                                       dirty);
+                unsigned const gc = static_cast<unsigned>((srcRows + kBlock - 1) / kBlock);
+                hipLaunchKernelGGL(rowChainKernel, dim3(gc), dim3(kBlock), 0, s, dirty, src.dimY, src.dimZ, a.srcZ0,
+                                   a.srcGlobalDz, dirty + srcRows);
+                ResampleArgs b = a;
+                b.rowChain = dirty + srcRows;
+                if (!gatherLdsEnabled() || !launchGatherLds(b, bs, bd, identity, true, tasks, s))
+                {
+                    uint64_t blocks = (tasks + 3) / 4;   // one task per wave
+                    unsigned g = static_cast<unsigned>(blocks < (1u << 30) ? blocks : (1u << 30));
+#define VKT_GVC(B, C) hipLaunchKernelGGL((resampleGatherVecKernel<B, C, true>), dim3(g), dim3(kBlock), 0, s, b)
+                    if (bd == 1) { if (identity) VKT_GVC(1, false); else VKT_GVC(1, true); }
+                    else if (bd == 2) { if (identity) VKT_GVC(2, false); else VKT_GVC(2, true); }
+                    else { if (identity) VKT_GVC(4, false); else VKT_GVC(4, true); }
+#undef VKT_GVC
+                }
+                scratch.release(s);
+                return rt::finishLaunch("Resample_hip(linear chain, flagged gather)");
+            }
+            (void)hipGetLastError();
+        }
         if (chain)
         {
             hipLaunchKernelGGL(resampleChainKernel, dim3(grid), dim3(kBlock), 0, s, a);
             return rt::finishLaunch("Resample_hip(linear chain, gather)");
         }
-        uint32_t const v = bd <= 4 ? 16 / bd : 0;
-        if (v != 0 && dst.dimX % v == 0 && reinterpret_cast<uintptr_t>(dst.data) % 16 == 0)
+        if (vecDst && gatherLdsEnabled() && launchGatherLds(a, bs, bd, identity, false, tasks, s))
+            return rt::finishLaunch("Resample_hip(gather, LDS)");
+        if (vecDst)
         {
             uint64_t blocks = (tasks + 3) / 4;   // one task per wave
             unsigned g = static_cast<unsigned>(blocks < (1u << 30) ? blocks : (1u << 30));
