@@ -38,6 +38,7 @@ def parse():
     p.add_argument("--warmup", type=int, default=25)
     p.add_argument("--dst", type=int, default=1024, help="per-GPU dst cube edge (source = dst/2)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-copy-peak", action="store_true", help="skip the measured D2D-copy peak")
     p.add_argument("--cpu-dst", type=int, default=768, help="dst edge of the CPU-baseline sample")
     p.add_argument("--layout-gpus", type=int, default=0,
                    help="single process: run rank 0's slab of the M-GPU global layout")
@@ -186,6 +187,8 @@ def main():
 
     res_ms = sum(a.elapsed_time(b) for a, b in t_res) / len(t_res)
     sum_ms = sum(a.elapsed_time(b) for a, b in t_sum) / len(t_sum)
+    copy_gbs = achievable_copy_gbs(torch, Rv.hip_view(), Dv.hip_view(), 2 * DX * DY * (dz1 - dz0)) \
+        if not args.no_copy_peak else None
     ms_per_step = elapsed * 1e3 / args.steps
     vox_rank = DX * DY * (dz1 - dz0)
     total_vox = vox_rank * world
@@ -239,6 +242,9 @@ def main():
             "traffic": traffic,
             "resample_achieved": round(res_bytes / (res_ms / 1e3) / 1e9, 1),
             "pipeline_frac": round(pipe_bytes / ((res_ms + sum_ms) / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+            # the fraction against a measured D2D copy as well as the spec peak
+            "d2d_copy_gbs": copy_gbs,
+            "frac_vs_d2d_copy": round(sum_bytes / (sum_ms / 1e3) / 1e9 / copy_gbs, 4) if copy_gbs else None,
         },
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -253,6 +259,31 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def achievable_copy_gbs(torch, src_view, dst_view, nbytes, reps=10):
+    """Achievable HBM rate on this box: a plain device-to-device hipMemcpyAsync (the runtime's
+    own blit kernel) of one whole volume, read + write bytes / HIP-event time, after the timed
+    region (it never overlaps the measured steps)."""
+    import ctypes as C
+    stream = torch.cuda.current_stream()
+    hip = C.CDLL("libamdhip64.so")
+    hip.hipMemcpyAsync.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p]
+
+    def copy():
+        if hip.hipMemcpyAsync(C.c_void_p(dst_view.data), C.c_void_p(src_view.data), C.c_size_t(nbytes), 3,
+                              C.c_void_p(stream.cuda_stream)) != 0:
+            raise RuntimeError("hipMemcpyAsync D2D failed")
+
+    for _ in range(3):
+        copy()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        copy()
+    e1.record()
+    torch.cuda.synchronize()
+    return round(2 * nbytes * reps / (e0.elapsed_time(e1) / 1e3) / 1e9, 1)
 
 
 def _lib_vec(x, y, z):

@@ -161,14 +161,23 @@ CASES = [
     ((1, 1, 1), (0, 0, 0), (1, 1, 1)),
 ]
 
+# ranges of the streaming histogram kernel (8-voxel-aligned rows): one contiguous span (whole
+# volume with a partial last step, whole planes, part of one plane) and a strided box
+FAST_CASES = [
+    ((256, 33, 17), (0, 0, 0), (256, 33, 17)),
+    ((64, 24, 10), (0, 0, 2), (64, 24, 9)),
+    ((64, 24, 10), (0, 5, 4), (64, 17, 5)),
+    ((64, 24, 10), (8, 3, 2), (56, 20, 9)),
+]
+
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("fmt", [4, 5, 2, 6, 7])
 @pytest.mark.parametrize("mapping", [(0.0, 1.0), (-1.0, 3.0)])
-@pytest.mark.parametrize("nbins", [1, 7, 256, 1000, 20000, 65536, 100000, 400000])
+@pytest.mark.parametrize("nbins", [1, 7, 256, 1000, 10240, 10241, 20000, 65536, 100000, 400000])
 def test_histogram_parity(fmt, mapping, nbins):
     rng = np.random.default_rng(fmt * 7 + nbins)
-    for dims, first, last in CASES:
+    for dims, first, last in CASES + FAST_CASES:
         codes = rand_codes(rng, fmt, dims[::-1], specials=True)
         got = gpu_histogram(codes, fmt, *mapping, first, last, nbins)
         ref, _ = ob.histogram_range(ob.Volume(codes, fmt, *mapping), first, last, nbins)
@@ -183,6 +192,13 @@ def test_histogram_constant_volume_and_reference_example():
     ref, _ = ob.histogram_range(ob.Volume(codes, 4), (0, 0, 0), (130, 65, 33), 256)
     np.testing.assert_array_equal(got, ref)
     assert got.sum() == codes.size
+    # the streaming kernel: every lane of every wave on the same bin (replicated counters)
+    for fmt, code in ((4, 200), (5, 40000), (7, 0x3F000000)):
+        codes = np.full((9, 40, 512), code, ob.CODE_DTYPE[fmt])
+        got = gpu_histogram(codes, fmt, 0.0, 1.0, (0, 0, 0), (512, 40, 9), 256)
+        ref, _ = ob.histogram_range(ob.Volume(codes, fmt), (0, 0, 0), (512, 40, 9), 256)
+        np.testing.assert_array_equal(got, ref)
+        assert got.sum() == codes.size
 
 
 def check_float(name, gpu, oracle, exact, terms_abs_sum, n):

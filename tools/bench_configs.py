@@ -151,9 +151,19 @@ def main():
         last = Vec3i_t(n, n, n)
         bins = C.c_void_p()
         lib.vktHipAllocate(C.byref(bins), 65536 * 8)
-        for nb in (256, 4096, 65536):
+        for nb in (256, 1024, 4096, 10240, 65536):
             ms = timed(lambda: lib.vktHipHistogramRange(V, o, last, bins, nb, 0), R)
             report(f"reduce Histogram 1024^3 UInt16 {nb} bins", ms, 2 * n ** 3, n ** 3)
+        sub0, sub1 = Vec3i_t(64, 64, 64), Vec3i_t(960, 960, 960)
+        ms = timed(lambda: lib.vktHipHistogramRange(V, sub0, sub1, bins, 256, 0), R)
+        report("reduce Histogram UInt16 896^3 sub-box of 1024^3, 256 bins", ms, 2 * 896 ** 3, 896 ** 3)
+        for fmt, bpv, name in ((4, 1, "UInt8"), (7, 4, "Float32")):
+            W = alloc((n,) * 3, fmt, seed=12 if fmt != 7 else None)
+            if fmt == 7:
+                rng_fill(W, n ** 3)   # uniform [0, 1): every voxel lands in a bin
+            ms = timed(lambda: lib.vktHipHistogramRange(W, o, last, bins, 256, 0), R)
+            report(f"reduce Histogram 1024^3 {name} 256 bins", ms, bpv * n ** 3, n ** 3)
+            free(W)
         Vc = alloc((n,) * 3, 5)
         lib.vktHipFillRange(Vc, o, last, C.c_float(0.5))
         ms = timed(lambda: lib.vktHipHistogramRange(Vc, o, last, bins, 256, 0), R)

@@ -339,6 +339,181 @@ namespace hipk
         }
     }
 
+    // ---- Histogram, streaming path (UInt8 / UInt16 / Float32, <= kFastMaxBins bins) --------
+    // The per-voxel work of histogramKernel (runtime-format decode, 64-bit bin math, run
+    // tracking) made it VALU-bound at ~2 TB/s; here the format is a template parameter, the bin
+    // index is 32-bit and the counters live in LDS:
+    //  * up to kReplicatedMaxBins bins (!TILED, 256-thread workgroups, 4 per CU): R = 2^rShift
+    //    copies of each counter, interleaved so lane l adds to copy l mod R: with R = 32 the 32
+    //    lanes of each LDS lane group hit 32 different banks (MI355X_MICROARCH.md §LDS:
+    //    ds_write_b32/ds_add_u32 bank = (addr/4) mod 32).  Out-of-range / NaN voxels add to a
+    //    trash row (bin nb) instead of branching.
+    //  * more bins (TILED, one 1024-thread workgroup per CU holding up to ~40 K counters): one
+    //    pass over the range per tile of bins, adds outside the tile masked off.
+    // UInt8 looks the counter offset up in a 256-entry LDS table (its decode has a true IEEE
+    // division); UInt16 / Float32 evaluate decode and the bin in packed f32 pairs
+    // (v_pk_mul/add_f32, the same roundings as the scalar form: no contraction).
+    // Items: 8 consecutive voxels of one range row; a wave takes 4 x 64 items per step (all
+    // loads in flight before the first atomic), grid-stride; CONTIG ranges are one span.
+    constexpr uint32_t kReplicatedMaxBins = 10240;
+    constexpr uint32_t kFastMaxTiles = 8;
+    constexpr int kTileBlock = 1024;
+
+    struct FastHistArgs
+    {
+        uint8_t const* data;        // CONTIG: first voxel of the span; else the volume base
+        uint64_t items;             // 8-voxel items in the range
+        FastDiv fdIpr, fdNy;        // non-CONTIG: items per row, rows per plane of the range
+        int32_t dimX, dimY, fx, fy, fz;
+        float lo, hi, scale, nbf;
+        uint32_t nb, rShift;
+        uint32_t tileBase, tileBins;   // TILED: this launch counts bins [tileBase, +tileBins)
+        unsigned long long* bins;
+    };
+
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+    __device__ __forceinline__ uint32_t fastBin(float f, float nbf, uint32_t nb)
+    {
+        // == binOf for numBins <= 2^24: -1 < f < numBins <=> 0 <= (size_t)f < numBins
+        return (f > -1.0f && f < nbf) ? static_cast<uint32_t>(static_cast<int32_t>(f)) : nb;
+    }
+
+    template <int FMT, bool CONTIG, bool TILED, int BLOCK>
+    __global__ __launch_bounds__(BLOCK) void histogramFastKernel(FastHistArgs h)
+    {
+        constexpr int BPV = FMT == codec::FmtUInt8 ? 1 : FMT == codec::FmtUInt16 ? 2 : 4;
+        constexpr int U = 4;
+        constexpr uint32_t kOff = ~0u;   // UInt8 table: code outside the tile
+        extern __shared__ uint32_t cnt[];
+        __shared__ uint32_t lut[FMT == codec::FmtUInt8 ? 256 : 1];
+        uint32_t const rowShift = h.rShift + 2;   // byte offset of a counter row
+        uint32_t const total = TILED ? h.tileBins : (h.nb + 1) << h.rShift;
+        for (uint32_t i = threadIdx.x; i < total; i += BLOCK)
+            cnt[i] = 0;
+        if constexpr (FMT == codec::FmtUInt8)
+        {
+            for (uint32_t c = threadIdx.x; c < 256; c += BLOCK)
+            {
+                float const v = codec::decode(c, codec::FmtUInt8, h.lo, h.hi);
+                uint32_t const b = fastBin((v - h.lo) * h.scale, h.nbf, h.nb);
+                if constexpr (TILED)
+                    lut[c] = b - h.tileBase < h.tileBins ? (b - h.tileBase) << 2 : kOff;
+                else
+                    lut[c] = b << rowShift;
+            }
+        }
+        __syncthreads();
+        uint32_t const lane = threadIdx.x & 63;
+        // this lane's copy of counter row 0; row b is at + (b << rowShift) (one v_lshl_add)
+        char* const cLane = reinterpret_cast<char*>(cnt) + (TILED ? 0u : (lane & ((1u << h.rShift) - 1u)) << 2);
+
+        auto voxelOf = [&](uint64_t item) -> uint64_t {
+            if constexpr (CONTIG)
+                return item * 8;
+            else
+            {
+                uint32_t const i = static_cast<uint32_t>(item);
+                uint32_t const r = fdiv(i, h.fdIpr);
+                uint32_t const xi = i - r * h.fdIpr.d;
+                uint32_t const zr = fdiv(r, h.fdNy);
+                uint32_t const yr = r - zr * h.fdNy.d;
+                return ((static_cast<uint64_t>(h.fz + zr) * static_cast<uint64_t>(h.dimY) + (h.fy + yr)) *
+                            static_cast<uint64_t>(h.dimX) +
+                        static_cast<uint64_t>(h.fx)) +
+                       8ull * xi;
+            }
+        };
+        auto add = [&](uint32_t b) {
+            if constexpr (TILED)
+            {
+                uint32_t const t = b - h.tileBase;
+                if (t < h.tileBins)
+                    atomicAdd(&cnt[t], 1u);
+            }
+            else
+                atomicAdd(reinterpret_cast<uint32_t*>(cLane + (b << rowShift)), 1u);
+        };
+        auto count8 = [&](uint32_t const (&c)[8]) {
+            if constexpr (FMT == codec::FmtUInt8)
+            {
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                {
+                    uint32_t const o = lut[c[j]];
+                    if (!TILED || o != kOff)
+                        atomicAdd(reinterpret_cast<uint32_t*>(cLane + o), 1u);
+                }
+            }
+            else
+            {
+#pragma unroll
+                for (int j = 0; j < 8; j += 2)
+                {
+                    f32x2 v;
+                    if constexpr (FMT == codec::FmtUInt16)
+                    {
+                        // decode: lerp(lo, hi, code / 65535.999f), 65535.999f == 2^16 (exact)
+                        f32x2 const t = f32x2{static_cast<float>(c[j]), static_cast<float>(c[j + 1])} *
+                                        (1.0f / 65536.0f);
+                        f32x2 const s = 1.0f - t;
+                        f32x2 const p = s * h.lo;
+                        f32x2 const q = t * h.hi;
+                        v = p + q;
+                    }
+                    else
+                        v = f32x2{codec::bitsToFloat(c[j]), codec::bitsToFloat(c[j + 1])};
+                    f32x2 const f = (v - h.lo) * h.scale;
+                    add(fastBin(f.x, h.nbf, h.nb));
+                    add(fastBin(f.y, h.nbf, h.nb));
+                }
+            }
+        };
+
+        uint64_t const wave = static_cast<uint64_t>(blockIdx.x) * (BLOCK / 64) + (threadIdx.x >> 6);
+        uint64_t const waves = static_cast<uint64_t>(gridDim.x) * (BLOCK / 64);
+        uint64_t const steps = h.items / (64 * U);
+        for (uint64_t st = wave; st < steps; st += waves)
+        {
+            uint32_t c[U][8];
+#pragma unroll
+            for (int k = 0; k < U; ++k)
+                load8<BPV, true>(h.data, voxelOf(st * (64 * U) + k * 64 + lane), c[k]);
+#pragma unroll
+            for (int k = 0; k < U; ++k)
+                count8(c[k]);
+        }
+        for (uint64_t it = steps * (64 * U) + wave * 64 + lane; it < h.items; it += waves * 64)
+        {
+            uint32_t c[8];
+            load8<BPV, true>(h.data, voxelOf(it), c);
+            count8(c);
+        }
+        __syncthreads();
+        if constexpr (TILED)
+        {
+            for (uint32_t t = threadIdx.x; t < h.tileBins; t += BLOCK)
+            {
+                uint32_t const c = cnt[t];
+                if (c)
+                    atomicAdd(&h.bins[h.tileBase + t], static_cast<unsigned long long>(c));
+            }
+        }
+        else
+        {
+            // sum the R copies of each bin (rotated start: the lanes of a group read different banks)
+            uint32_t const R = 1u << h.rShift;
+            for (uint32_t b = threadIdx.x; b < h.nb; b += BLOCK)
+            {
+                uint32_t sum = 0;
+                for (uint32_t r = 0; r < R; ++r)
+                    sum += cnt[(b << h.rShift) + ((r + b) & (R - 1))];
+                if (sum)
+                    atomicAdd(&h.bins[b], static_cast<unsigned long long>(sum));
+            }
+        }
+    }
+
     __global__ void zeroU64Kernel(unsigned long long* p, uint64_t n)
     {
         uint64_t const i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -408,6 +583,83 @@ namespace hipk
     hipLaunchKernelGGL((aggregatesKernel<PASS, B, V>), dim3(G), dim3(kBlock), 0, S, a, MEANPTR, MEANV, OUT)
 #define VKT_HIST_LAUNCH(B, V, G, LDS, S) \
     hipLaunchKernelGGL((histogramKernel<B, V>), dim3(G), dim3(kBlock), LDS, S, a, h)
+
+    // Launches histogramFastKernel when the range qualifies (see its comment); false otherwise.
+    bool launchFastHistogram(BoxArgs const& a, HistArgs const& hh, hipStream_t s)
+    {
+        int32_t const fmt = a.fmt;
+        if ((fmt != codec::FmtUInt8 && fmt != codec::FmtUInt16 && fmt != codec::FmtFloat32) || !vecRows(a))
+            return false;
+        // LDS counters of one 1024-thread workgroup (the device limit minus the static table)
+        uint32_t const tileCap = (ldsBinCapacity() * 4u - 1024u) / 4u;
+        uint64_t const tiles = (hh.numBins + tileCap - 1) / tileCap;
+        if (tiles > kFastMaxTiles)
+            return false;
+        uint32_t const bpv = codec::bytesPerVoxel(fmt);
+        uint64_t const ny = a.fdNy.d;   // range rows = ny * nz
+        uint64_t const nz = a.rows / ny;
+        bool const contig = a.nx == a.dimX && (ny == static_cast<uint64_t>(a.dimY) || nz == 1);
+        uint64_t const items = static_cast<uint64_t>(a.nx / 8) * a.rows;
+        if (!contig && items >= (1ull << 32))
+            return false;
+        FastHistArgs h{};
+        h.items = items;
+        h.dimX = a.dimX;
+        h.dimY = a.dimY;
+        h.fx = a.fx;
+        h.fy = a.fy;
+        h.fz = a.fz;
+        h.fdIpr = makeFastDiv(static_cast<uint32_t>(a.nx / 8));
+        h.fdNy = a.fdNy;
+        h.data = contig ? a.data + ((static_cast<uint64_t>(a.fz) * a.dimY + a.fy) * a.dimX) * bpv : a.data;
+        h.lo = a.lo;
+        h.hi = a.hi;
+        h.scale = hh.scale;
+        h.nb = static_cast<uint32_t>(hh.numBins);
+        h.nbf = static_cast<float>(hh.numBins);
+        h.bins = hh.bins;
+#define VKT_FAST_HIST(FMT, TILED, BLOCK, G, LDS)                                                                   \
+    do {                                                                                                           \
+        if (contig)                                                                                                \
+            hipLaunchKernelGGL((histogramFastKernel<FMT, true, TILED, BLOCK>), dim3(G), dim3(BLOCK), LDS, s, h);    \
+        else                                                                                                       \
+            hipLaunchKernelGGL((histogramFastKernel<FMT, false, TILED, BLOCK>), dim3(G), dim3(BLOCK), LDS, s, h);   \
+    } while (0)
+#define VKT_FAST_HIST_FMT(TILED, BLOCK, G, LDS)                                                                    \
+    do {                                                                                                           \
+        if (fmt == codec::FmtUInt8) VKT_FAST_HIST(codec::FmtUInt8, TILED, BLOCK, G, LDS);                          \
+        else if (fmt == codec::FmtUInt16) VKT_FAST_HIST(codec::FmtUInt16, TILED, BLOCK, G, LDS);                   \
+        else VKT_FAST_HIST(codec::FmtFloat32, TILED, BLOCK, G, LDS);                                               \
+    } while (0)
+        if (h.nb <= kReplicatedMaxBins)
+        {
+            // replicas: as many as fit in 40 KiB (4 workgroups per CU), at most one per bank (32)
+            uint32_t rs = 5;
+            while (rs > 0 && (static_cast<uint64_t>(h.nb) + 1) * (4ull << rs) > 40u * 1024u)
+                --rs;
+            h.rShift = rs;
+            h.tileBase = 0;
+            h.tileBins = h.nb;
+            size_t const lds = (static_cast<size_t>(h.nb) + 1) * (4u << rs);
+            unsigned const perCU = static_cast<unsigned>(std::min<size_t>(8, (160u * 1024u) / (lds + 1024u)));
+            unsigned const g = streamingGrid(items, 64u * 4u * (kBlock / 64), std::max(1u, perCU));
+            VKT_FAST_HIST_FMT(false, kBlock, g, lds);
+        }
+        else
+        {
+            h.rShift = 0;
+            unsigned const g = streamingGrid(items, 64u * 4u * (kTileBlock / 64), 1);
+            for (uint64_t t = 0; t < tiles; ++t)
+            {
+                h.tileBase = static_cast<uint32_t>(t * tileCap);
+                h.tileBins = static_cast<uint32_t>(std::min<uint64_t>(tileCap, hh.numBins - h.tileBase));
+                VKT_FAST_HIST_FMT(true, kTileBlock, g, static_cast<size_t>(h.tileBins) * 4u);
+            }
+        }
+#undef VKT_FAST_HIST_FMT
+#undef VKT_FAST_HIST
+        return true;
+    }
 
     struct AggScratch
     {
@@ -610,6 +862,8 @@ vktError vktHipHistogramRange(vktHipVolumeView_t volume, vktVec3i_t first, vktVe
         volatile float range = volume.mappingHi - volume.mappingLo;
         volatile float nbf = static_cast<float>(numBins);          // size_t -> float
         h.scale = nbf / range;                                     // numBins / (hi - lo)
+        if (launchFastHistogram(a, h, s))
+            return rt::finishLaunch("HistogramRange_hip");
         // LDS counters in tiles of up to ldsBins bins, one pass over the range per tile (u32
         // per workgroup cannot overflow: a workgroup visits < 2^32 voxels); beyond 8 tiles the
         // counters go straight to global 64-bit atomics.
