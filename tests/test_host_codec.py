@@ -80,3 +80,12 @@ def test_float32_unmap_is_raw_bits(vkt):
         b = bits.to_bytes(4, "little")
         got = vkt.UnmapVoxel(b, 7, -1.0, 3.0)
         assert struct.pack("<f", got) == b or np.isnan(got)
+
+
+def test_uint8_unmap_division_equals_reciprocal_product():
+    """Codec.hpp decodes UInt8 with code * 0x3B800021 instead of the reference's IEEE division
+    code / 255.999f (VoxelMapping.hpp:122-127): equal for every one of the 256 codes."""
+    codes = np.arange(256, dtype=np.float32)
+    inv = np.float32(1.0) / np.float32(255.999)
+    assert struct.unpack("<I", struct.pack("<f", inv))[0] == 0x3B800021
+    np.testing.assert_array_equal((codes / np.float32(255.999)).view(np.uint32), (codes * inv).view(np.uint32))

@@ -95,6 +95,14 @@ def main():
             ms = timed(lambda: lib.vktHipArithmeticRange(op, D, A, B, o, last, o), R)
             report(f"config2 {name} 512^3 UInt16", ms, 6 * n ** 3, n ** 3)
         free(A, B, D)
+        # the same ops on UInt8 volumes (decode = lerp of code / 255.999f), 1024^3
+        m = 1024
+        A, B, D = alloc((m,) * 3, 4, seed=1), alloc((m,) * 3, 4, seed=2), alloc((m,) * 3, 4)
+        last = Vec3i_t(m, m, m)
+        for name, op in (("SafeSum", 5), ("SumRange", 0)):
+            ms = timed(lambda: lib.vktHipArithmeticRange(op, D, A, B, o, last, o), R)
+            report(f"config2-u8 {name} 1024^3 UInt8", ms, 3 * m ** 3, m ** 3)
+        free(A, B, D)
     # config 3: 1024^3 Float32 -> 2048^3 Linear (lerp-chain kernel) and Nearest (replication)
     s, e = 1024, 2048
     if want("config3"):

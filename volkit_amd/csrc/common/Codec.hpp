@@ -134,6 +134,9 @@ namespace codec
     }
 
     // ---- decode (UnmapVoxelImpl) -----------------------------------------------------
+    // float(1 / 255.999f) = 0x3B800021; c / 255.999f == c * kInv255999 for c = 0..255
+    constexpr float kInv255999 = 0x1.000042p-8f;
+
     // `prior` is the value the reference leaves untouched for Int8/Int32/Unspecified
     // (getValue initialises it to 0.f, src/vkt/StructuredVolume.cpp:196).
     VKT_HD float decode(uint32_t code, int32_t fmt, float lo, float hi, float prior = 0.f)
@@ -145,8 +148,11 @@ namespace codec
             float f = static_cast<float>(static_cast<int16_t>(static_cast<uint16_t>(code)));
             return lerp(lo, hi, (f + 32767.f) / 65535.999f);
         }
-        case FmtUInt8:   // VoxelMapping.hpp:122-127 (a true IEEE division by 255.999f)
-            return lerp(lo, hi, static_cast<float>(code & 0xFFu) / 255.999f);
+        case FmtUInt8:   // VoxelMapping.hpp:122-127: an IEEE division by 255.999f, which for
+                         // each of the 256 codes rounds to the same float as the product with
+                         // kInv255999 (checked exhaustively: tests/test_host_codec.py), so the
+                         // ~10-instruction gfx950 division sequence is not needed
+            return lerp(lo, hi, static_cast<float>(code & 0xFFu) * kInv255999);
         case FmtUInt16:  // VoxelMapping.hpp:130-142 (divisor rounds to 2^16: exact)
             return lerp(lo, hi, static_cast<float>(code & 0xFFFFu) / 65535.999f);
         case FmtUInt32:  // VoxelMapping.hpp:145-160

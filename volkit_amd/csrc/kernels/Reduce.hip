@@ -634,6 +634,8 @@ namespace hipk
         if (h.nb <= kReplicatedMaxBins)
         {
             // replicas: as many as fit in 40 KiB (4 workgroups per CU), at most one per bank (32)
+            // (R = 32 keeps a constant or skewed volume -- empty space -- at the streaming rate:
+            // 0.36 ms at 1024^3 UInt16 vs 0.89 ms with R = 4; uniform random data is ~flat in R)
             uint32_t rs = 5;
             while (rs > 0 && (static_cast<uint64_t>(h.nb) + 1) * (4ull << rs) > 40u * 1024u)
                 --rs;
