@@ -70,6 +70,41 @@ def test_oracle_background_and_accumulation():
     assert (col == 0).all()
 
 
+def _round_f32(x):
+    """Exact round-to-nearest-even of a Fraction to float32 (normal range)."""
+    from fractions import Fraction
+    import math
+    if x == 0:
+        return Fraction(0)
+    sign, x = (1, x) if x > 0 else (-1, -x)
+    e = x.numerator.bit_length() - x.denominator.bit_length()
+    while Fraction(2) ** e > x:
+        e -= 1
+    while Fraction(2) ** (e + 1) <= x:
+        e += 1
+    scale = Fraction(2) ** (e - 23)
+    m = x / scale
+    fl = math.floor(m)
+    rem = m - fl
+    if rem > Fraction(1, 2) or (rem == Fraction(1, 2) and fl % 2 == 1):
+        fl += 1
+    return sign * fl * scale
+
+
+@pytest.mark.parametrize("d,n", [(255, 256), (65535, 65536)])
+def test_texel_unorm_division_emulation_is_exact(d, n):
+    """Render.hip unormDiv<D>: q0 = c*RN(1/D); e = fma(-q0, D, c); q = fma(e, RN(1/D), q0)
+    equals the reference texture's float(c) / D for every code (exact rational arithmetic)."""
+    from fractions import Fraction
+    D = Fraction(d)
+    r = _round_f32(1 / D)
+    assert float(r) == float(np.float32(1) / np.float32(d))
+    for c in range(n):
+        q0 = _round_f32(c * r)
+        e = _round_f32(Fraction(c) - q0 * D)
+        assert _round_f32(e * r + q0) == _round_f32(Fraction(c) / D), c
+
+
 def test_cpu_policy_is_refused():
     v = vkt.StructuredVolume(4, 4, 4, vkt.DataFormat_UInt8)
     rs = vkt.RenderState()

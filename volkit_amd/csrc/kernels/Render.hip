@@ -83,20 +83,75 @@ namespace hipk
         int32_t nx, ny, nz;
         int32_t fmt;
         float lo, hi;
+        int32_t nbx, nby;   // bricked copy: bricks per row / per column (8^3 voxels each)
     };
 
+    // texel offset of voxel (x, y, z): dense x-fastest, or the 8^3-brick copy
+    template <bool BRICK>
+    __device__ __forceinline__ uint64_t texOffset(Tex const& t, uint32_t x, uint32_t y, uint32_t z)
+    {
+        if constexpr (BRICK)
+            return ((static_cast<uint64_t>(z >> 3) * static_cast<uint32_t>(t.nby) + (y >> 3)) *
+                        static_cast<uint64_t>(static_cast<uint32_t>(t.nbx)) +
+                    (x >> 3)) * 512u +
+                   (((z & 7u) << 6) | ((y & 7u) << 3) | (x & 7u));
+        else
+            return (static_cast<uint64_t>(z) * static_cast<uint64_t>(t.ny) + y) * static_cast<uint64_t>(t.nx) + x;
+    }
+
+    constexpr uint64_t kMaxBrickBytes = 8ull << 30;
+
+    // dense -> 8^3 bricks (one thread per 8-voxel brick row; edge bricks clamp-replicate)
+    template <int BPV>
+    __global__ void brickKernel(uint8_t const* src, uint8_t* dst, int32_t nx, int32_t ny, int32_t nz, int32_t nbx,
+                                int32_t nby, uint64_t rows)
+    {
+        uint64_t const r = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+        if (r >= rows)
+            return;
+        uint32_t const ly = r & 7u, lz = (r >> 3) & 7u;
+        uint64_t const b = r >> 6;
+        uint32_t const bx = static_cast<uint32_t>(b % static_cast<uint32_t>(nbx));
+        uint64_t const byz = b / static_cast<uint32_t>(nbx);
+        uint32_t const by = static_cast<uint32_t>(byz % static_cast<uint32_t>(nby));
+        uint32_t const bz = static_cast<uint32_t>(byz / static_cast<uint32_t>(nby));
+        uint32_t const y = min(by * 8u + ly, static_cast<uint32_t>(ny - 1));
+        uint32_t const z = min(bz * 8u + lz, static_cast<uint32_t>(nz - 1));
+        uint64_t const row = (static_cast<uint64_t>(z) * static_cast<uint32_t>(ny) + y) * static_cast<uint32_t>(nx);
+        for (uint32_t lx = 0; lx < 8; ++lx)
+        {
+            uint32_t const x = min(bx * 8u + lx, static_cast<uint32_t>(nx - 1));
+            for (int k = 0; k < BPV; ++k)
+                dst[(r * 8 + lx) * BPV + k] = src[(row + x) * BPV + k];
+        }
+    }
+
+    // code / D for an integer code, correctly rounded, in three instructions instead of the
+    // IEEE division sequence: q0 = code * RN(1/D), one fma residual, one fma correction.
+    // Checked with exact rational arithmetic for every code of both texel formats (D = 255:
+    // 256 codes, D = 65535: 65 536 codes; tests/test_render.py) -- the plain product alone is
+    // off by one ulp for 126 and 512 of them.
+    template <int D>
+    __device__ __forceinline__ float unormDiv(uint32_t code)
+    {
+        constexpr float kD = static_cast<float>(D);
+        constexpr float kR = D == 255 ? 0x1.010102p-8f : 0x1.000100p-16f;   // RN(1 / D)
+        float const c = static_cast<float>(code);
+        float const q0 = c * kR;
+        float const e = __builtin_fmaf(-q0, kD, c);
+        return __builtin_fmaf(e, kR, q0);
+    }
+
     // raw texel value as the reference's texture returns it: unorm for integer formats
-    template <int FMT>
+    template <int FMT, bool BRICK>
     __device__ __forceinline__ float texel(Tex const& t, V3 c)
     {
-        uint64_t const i = (static_cast<uint64_t>(texIndex(c.z, t.nz)) * static_cast<uint64_t>(t.ny) +
-                            static_cast<uint64_t>(texIndex(c.y, t.ny))) *
-                               static_cast<uint64_t>(t.nx) +
-                           static_cast<uint64_t>(texIndex(c.x, t.nx));
+        uint64_t const i = texOffset<BRICK>(t, static_cast<uint32_t>(texIndex(c.x, t.nx)),
+                                     static_cast<uint32_t>(texIndex(c.y, t.ny)), static_cast<uint32_t>(texIndex(c.z, t.nz)));
         if constexpr (FMT == codec::FmtUInt8)
-            return static_cast<float>(t.data[i]) / 255.f;
+            return unormDiv<255>(t.data[i]);   // == float(code) / 255.f
         else if constexpr (FMT == codec::FmtUInt16)
-            return static_cast<float>(reinterpret_cast<uint16_t const*>(t.data)[i]) / 65535.f;
+            return unormDiv<65535>(reinterpret_cast<uint16_t const*>(t.data)[i]);   // == float(code) / 65535.f
         else
             return (reinterpret_cast<float const*>(t.data)[i] - t.lo) / (t.hi - t.lo);
     }
@@ -119,18 +174,16 @@ namespace hipk
         return x <= 0.0031308f ? 12.92f * x : 1.055f * rmath::pow(x, 1.f / 2.4f) - 0.055f;
     }
 
-    template <int FMT>
-    __device__ void samplePixel(vktHipRenderParams_t const& p, Tex const& tex, Lut const& lut, int32_t x, int32_t y,
-                                uint32_t frame, float (&out)[4])
+    // primary ray of pixel (x, y): jittered pixel position, thin lens (4 draws, always)
+    __device__ __forceinline__ void primaryRay(vktHipRenderParams_t const& p, rmath::Rng& gen, int32_t x, int32_t y,
+                                               V3& ori, V3& dir)
     {
-        rmath::Rng gen(static_cast<uint32_t>(y) * static_cast<uint32_t>(p.width) + static_cast<uint32_t>(x), frame);
-        // primary ray: jittered pixel position, thin lens
         float const jx = gen.next(), jy = gen.next();
         float const sx = 2.f * (static_cast<float>(x) + jx) / static_cast<float>(p.width) - 1.f;
         float const sy = 2.f * (static_cast<float>(y) + jy) / static_cast<float>(p.height) - 1.f;
         V3 const W = v3(p.W);
-        V3 dir = normalize(W + v3(p.U) * sx + v3(p.V) * sy);
-        V3 ori = v3(p.eye);
+        dir = normalize(W + v3(p.U) * sx + v3(p.V) * sy);
+        ori = v3(p.eye);
         float const lu = gen.next(), lv = gen.next();
         if (p.lensRadius > 0.f)
         {
@@ -141,12 +194,31 @@ namespace hipk
             ori = ori + v3(p.right) * (r * c) + v3(p.up) * (r * s);
             dir = normalize(focus - ori);
         }
+    }
+
+    // sky gradient of the reference (1 - t) * (1,1,1) + t * (.5,.7,1), t = y / height
+    __device__ __forceinline__ void skyTimes(vktHipRenderParams_t const& p, int32_t y, V3 thr, float (&out)[4])
+    {
+        float const ty = static_cast<float>(y) / static_cast<float>(p.height);
+        out[0] = ((1.f - ty) * 1.f + ty * 0.5f) * thr.x;
+        out[1] = ((1.f - ty) * 1.f + ty * 0.7f) * thr.y;
+        out[2] = ((1.f - ty) * 1.f + ty * 1.0f) * thr.z;
+        out[3] = 1.f;
+    }
+
+    template <int FMT, int ALGO, bool BRICK>
+    __device__ void samplePixel(vktHipRenderParams_t const& p, Tex const& tex, Lut const& lut, int32_t x, int32_t y,
+                                uint32_t frame, float (&out)[4])
+    {
+        rmath::Rng gen(static_cast<uint32_t>(y) * static_cast<uint32_t>(p.width) + static_cast<uint32_t>(x), frame);
+        V3 ori, dir;
+        primaryRay(p, gen, x, y, ori, dir);
         V3 const box = v3(p.bbox);
         Hit h = intersectBox(ori, dir, box);
         float const v0 = 0.f;
         out[0] = out[1] = out[2] = out[3] = v0;
 
-        if (p.algo == 0)   // ray marching
+        if constexpr (ALGO == 0)   // ray marching
         {
             float t = h.tnear;
             V3 tc = div(ori + dir * t, box);
@@ -154,7 +226,7 @@ namespace hipk
             float dst[4] = {0.f, 0.f, 0.f, 0.f};
             while (t < h.tfar)
             {
-                float const voxel = texel<FMT>(tex, tc);
+                float const voxel = texel<FMT, BRICK>(tex, tc);
                 float col[4];
                 if (lut.rgba)
                     lutLookup(lut, voxel, col);
@@ -176,7 +248,7 @@ namespace hipk
                 out[k] = dst[k];
             return;
         }
-        if (p.algo == 1)   // implicit iso
+        if constexpr (ALGO == 1)   // implicit iso
         {
             float t = h.tnear;
             V3 tc = div(ori + dir * t, box);
@@ -185,7 +257,7 @@ namespace hipk
             float dst[4] = {0.f, 0.f, 0.f, 0.f};
             while (t < h.tfar)
             {
-                float const voxel = texel<FMT>(tex, tc);
+                float const voxel = texel<FMT, BRICK>(tex, tc);
                 if (last >= -1e10f)
                 {
                     for (int32_t i = 0; i < p.numIsoSurfaces; ++i)
@@ -200,10 +272,10 @@ namespace hipk
                                 col[0] = col[1] = col[2] = col[3] = voxel;
                             isoT = t;
                             float const d = 0.01f;
-                            V3 s1{texel<FMT>(tex, tc + V3{d, 0.f, 0.f}), texel<FMT>(tex, tc + V3{0.f, d, 0.f}),
-                                  texel<FMT>(tex, tc + V3{0.f, 0.f, d})};
-                            V3 s2{texel<FMT>(tex, tc - V3{d, 0.f, 0.f}), texel<FMT>(tex, tc - V3{0.f, d, 0.f}),
-                                  texel<FMT>(tex, tc - V3{0.f, 0.f, d})};
+                            V3 s1{texel<FMT, BRICK>(tex, tc + V3{d, 0.f, 0.f}), texel<FMT, BRICK>(tex, tc + V3{0.f, d, 0.f}),
+                                  texel<FMT, BRICK>(tex, tc + V3{0.f, 0.f, d})};
+                            V3 s2{texel<FMT, BRICK>(tex, tc - V3{d, 0.f, 0.f}), texel<FMT, BRICK>(tex, tc - V3{0.f, d, 0.f}),
+                                  texel<FMT, BRICK>(tex, tc - V3{0.f, 0.f, d})};
                             V3 const N = normalize(s2 - s1);
                             float const kd = fmaxf(0.f, dot(N, V3{-dir.x, -dir.y, -dir.z})) * voxel;
                             dst[0] = 0.2f + col[0] * kd;
@@ -246,7 +318,7 @@ namespace hipk
                         interact = false;
                         break;
                     }
-                    float const voxel = texel<FMT>(tex, div(pos, box));
+                    float const voxel = texel<FMT, BRICK>(tex, div(pos, box));
                     float mu;
                     if (lut.rgba)
                     {
@@ -270,7 +342,7 @@ namespace hipk
                     thr = V3{0.f, 0.f, 0.f};
                     break;
                 }
-                float const voxel = texel<FMT>(tex, div(ori, box));
+                float const voxel = texel<FMT, BRICK>(tex, div(ori, box));
                 V3 alb;
                 if (lut.rgba)
                 {
@@ -300,17 +372,13 @@ namespace hipk
                 h = intersectBox(ori, dir, box);
             }
         }
-        float const ty = static_cast<float>(y) / static_cast<float>(p.height);
-        out[0] = ((1.f - ty) * 1.f + ty * 0.5f) * thr.x;
-        out[1] = ((1.f - ty) * 1.f + ty * 0.7f) * thr.y;
-        out[2] = ((1.f - ty) * 1.f + ty * 1.0f) * thr.z;
-        out[3] = 1.f;
+        skyTimes(p, y, thr, out);
     }
 
     // 8x8-pixel tile per wave; a 256-thread workgroup covers 16x16 pixels
-    template <int FMT>
-    __global__ __launch_bounds__(kBlock) void renderKernel(vktHipRenderParams_t p, Tex tex, Lut lut, float* accum,
-                                                          float* color, int32_t numFrames)
+    template <int FMT, int ALGO, bool BRICK>
+    __device__ __forceinline__ void renderPixel(vktHipRenderParams_t const& p, Tex const& tex, Lut const& lut,
+                                                float* accum, float* color, int32_t numFrames)
     {
         int const t = threadIdx.x;
         int const wave = t >> 6, lane = t & 63;
@@ -327,7 +395,7 @@ namespace hipk
         {
             uint32_t const frame = p.frameBegin + static_cast<uint32_t>(f);
             float s[4];
-            samplePixel<FMT>(p, tex, lut, x, y, frame, s);
+            samplePixel<FMT, ALGO, BRICK>(p, tex, lut, x, y, frame, s);
             float const alpha = 1.f / static_cast<float>(frame);
             for (int k = 0; k < 4; ++k)
                 acc[k] = (1.f - alpha) * acc[k] + alpha * s[k];
@@ -340,6 +408,32 @@ namespace hipk
                 color[4 * pix + k] = p.sRGB ? linearToSrgb(acc[k]) : acc[k];
             color[4 * pix + 3] = acc[3];
         }
+    }
+
+    // One kernel per algorithm, so each gets its own register allocation and occupancy.
+    // Capping ray marching and multi-scattering at 4 waves per SIMD (amdgpu_waves_per_eu) keeps
+    // the texel working set of the resident waves in the caches (config 5, 1024^3 UInt8:
+    // RayMarching 2.50 -> 2.23 ms, MultiScattering 3.47 -> 3.29 ms per frame); ImplicitIso
+    // runs best uncapped.
+    template <int FMT>
+    __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 4))) void renderRayMarchingKernel(
+        vktHipRenderParams_t p, Tex tex, Lut lut, float* accum, float* color, int32_t numFrames)
+    {
+        renderPixel<FMT, 0, false>(p, tex, lut, accum, color, numFrames);
+    }
+
+    template <int FMT>
+    __global__ __launch_bounds__(kBlock) void renderImplicitIsoKernel(vktHipRenderParams_t p, Tex tex, Lut lut,
+                                                                     float* accum, float* color, int32_t numFrames)
+    {
+        renderPixel<FMT, 1, false>(p, tex, lut, accum, color, numFrames);
+    }
+
+    template <int FMT, bool BRICK>
+    __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 4))) void renderMultiScatteringKernel(
+        vktHipRenderParams_t p, Tex tex, Lut lut, float* accum, float* color, int32_t numFrames)
+    {
+        renderPixel<FMT, 2, BRICK>(p, tex, lut, accum, color, numFrames);
     }
 
 } // hipk
@@ -369,19 +463,73 @@ vktError vktHipRender(vktHipVolumeView_t volume, vktHipRenderParams_t const* par
         return rt::fail("vktHipRender: volume format must be UInt8, UInt16 or Float32 (reference texel types)");
     if (numFrames == 0)
         return vktNoError;
-    Tex tex{volume.data, volume.dimX, volume.dimY, volume.dimZ, fmt, volume.mappingLo, volume.mappingHi};
+    Tex tex{volume.data, volume.dimX, volume.dimY, volume.dimZ, fmt, volume.mappingLo, volume.mappingHi, 0, 0};
+    hipStream_t s = rt::computeStream();
     Lut lut{p.lut, p.lutSize};
     dim3 grid(static_cast<unsigned>((p.width + 15) / 16), static_cast<unsigned>((p.height + 15) / 16));
-    hipStream_t s = rt::computeStream();
-    if (fmt == codec::FmtUInt8)
-        hipLaunchKernelGGL(renderKernel<codec::FmtUInt8>, grid, dim3(kBlock), 0, s, p, tex, lut, accum, color,
-                           numFrames);
-    else if (fmt == codec::FmtUInt16)
-        hipLaunchKernelGGL(renderKernel<codec::FmtUInt16>, grid, dim3(kBlock), 0, s, p, tex, lut, accum, color,
-                           numFrames);
+    if (p.algo == 0 || p.algo == 1)
+    {
+#define VKT_RENDER(KERNEL)                                                                                          \
+    do {                                                                                                            \
+        if (fmt == codec::FmtUInt8)                                                                                 \
+            hipLaunchKernelGGL(KERNEL<codec::FmtUInt8>, grid, dim3(kBlock), 0, s, p, tex, lut, accum, color, numFrames);   \
+        else if (fmt == codec::FmtUInt16)                                                                           \
+            hipLaunchKernelGGL(KERNEL<codec::FmtUInt16>, grid, dim3(kBlock), 0, s, p, tex, lut, accum, color, numFrames);  \
+        else                                                                                                        \
+            hipLaunchKernelGGL(KERNEL<codec::FmtFloat32>, grid, dim3(kBlock), 0, s, p, tex, lut, accum, color, numFrames); \
+    } while (0)
+        if (p.algo == 0)
+            VKT_RENDER(renderRayMarchingKernel);
+        else
+            VKT_RENDER(renderImplicitIsoKernel);
+#undef VKT_RENDER
+        return rt::finishLaunch("Render_hip");
+    }
+    // Multi-scattering samples the volume at scattered, isotropic positions: it reads an 8^3-
+    // brick copy made for the call (one streaming pass; config 5: 3.29 -> 2.92 ms per frame
+    // over 8 frames), when the copy fits kMaxBrickBytes; else the dense volume.
+    static rt::StreamScratch bricks;
+    int32_t const nbx = (volume.dimX + 7) / 8, nby = (volume.dimY + 7) / 8, nbz = (volume.dimZ + 7) / 8;
+    uint32_t const bpv = codec::bytesPerVoxel(fmt);
+    uint64_t const brickRows = static_cast<uint64_t>(nbx) * static_cast<uint64_t>(nby) * static_cast<uint64_t>(nbz) * 64;
+    uint8_t* b = brickRows * 8 * bpv <= kMaxBrickBytes ? static_cast<uint8_t*>(bricks.acquire(brickRows * 8 * bpv, s))
+                                                       : nullptr;
+    if (!b)
+        (void)hipGetLastError();   // a failed scratch allocation only means: render the dense volume
+    if (b)
+    {
+        unsigned const g = static_cast<unsigned>((brickRows + 255) / 256);
+#define VKT_BRICK(BPV)                                                                                           \
+    hipLaunchKernelGGL(brickKernel<BPV>, dim3(g), dim3(256), 0, s, volume.data, b, volume.dimX, volume.dimY,     \
+                       volume.dimZ, nbx, nby, brickRows)
+        if (bpv == 1)
+            VKT_BRICK(1);
+        else if (bpv == 2)
+            VKT_BRICK(2);
+        else
+            VKT_BRICK(4);
+#undef VKT_BRICK
+        tex.data = b;
+        tex.nbx = nbx;
+        tex.nby = nby;
+    }
+#define VKT_RENDER_MS(BRICK)                                                                                      \
+    do {                                                                                                          \
+        if (fmt == codec::FmtUInt8)                                                                               \
+            hipLaunchKernelGGL((renderMultiScatteringKernel<codec::FmtUInt8, BRICK>), grid, dim3(kBlock), 0, s, p, tex, lut, accum, color, numFrames); \
+        else if (fmt == codec::FmtUInt16)                                                                         \
+            hipLaunchKernelGGL((renderMultiScatteringKernel<codec::FmtUInt16, BRICK>), grid, dim3(kBlock), 0, s, p, tex, lut, accum, color, numFrames); \
+        else                                                                                                      \
+            hipLaunchKernelGGL((renderMultiScatteringKernel<codec::FmtFloat32, BRICK>), grid, dim3(kBlock), 0, s, p, tex, lut, accum, color, numFrames); \
+    } while (0)
+    if (b)
+    {
+        VKT_RENDER_MS(true);
+        bricks.release(s);
+    }
     else
-        hipLaunchKernelGGL(renderKernel<codec::FmtFloat32>, grid, dim3(kBlock), 0, s, p, tex, lut, accum, color,
-                           numFrames);
+        VKT_RENDER_MS(false);
+#undef VKT_RENDER_MS
     return rt::finishLaunch("Render_hip");
 }
 
