@@ -33,13 +33,14 @@ namespace hipk
                                 hipStream_t s)
     {
         uint64_t const tasks = static_cast<uint64_t>(a.dnz) * a.nRunsY * static_cast<uint64_t>(instrPerRow);
-        unsigned const g = static_cast<unsigned>(tasks < (1u << 30) ? tasks : (1u << 30));
         uint64_t const fixTasks = static_cast<uint64_t>(a.nRunsY) * a.nRunsZ;
         unsigned const gs = static_cast<unsigned>((fixTasks + 255) / 256);
         unsigned const gf = 2048;   // drains the work list (exits at once when it is empty)
 #define VKT_OPT(B, K)                                                                                           \
     do {                                                                                                        \
-        hipLaunchKernelGGL((resamplePlaneKernel<4, B, K, 3, codec::FmtFloat32, -1>), dim3(g), dim3(64), 0, s, a); \
+        planeChunks(a, tasks, [&](ResampleArgs const& c, unsigned g) {                                         \
+            hipLaunchKernelGGL((resamplePlaneKernel<4, B, K, 3, codec::FmtFloat32, -1>), dim3(g), dim3(64), 0, s, c); \
+        });                                                                                                     \
         hipLaunchKernelGGL(resampleFixupScanKernel, dim3(gs), dim3(256), 0, s, a, list);                     \
         hipLaunchKernelGGL((resampleFixupKernel<B, K>), dim3(gf), dim3(64), 0, s, a, list);                   \
     } while (0)
