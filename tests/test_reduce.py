@@ -212,7 +212,7 @@ def check_float(name, gpu, oracle, exact, terms_abs_sum, n):
                                          (6, (0.25, 7.5))])
 def test_aggregates_parity(fmt, mapping):
     rng = np.random.default_rng(fmt)
-    for dims, first, last in CASES:
+    for dims, first, last in CASES + FAST_CASES:
         codes = rand_codes(rng, fmt, dims[::-1])
         got = gpu_aggregates(codes, fmt, *mapping, first, last)
         ref = ob.aggregates_range(ob.Volume(codes, fmt, *mapping), first, last)
@@ -267,12 +267,18 @@ def test_aggregates_ties_specials_and_whole_volume_mean():
 
 
 @pytest.mark.gpu
-def test_aggregate_slab_partials_combine_to_the_whole():
+@pytest.mark.parametrize("nx", [33, 64])   # row kernel / streaming kernel
+def test_aggregate_slab_partials_combine_to_the_whole(nx):
     """Z-slab partials (multi-GPU building block): two slabs with their global z offset,
     combined, mean of the whole, pass 2, finish == single-volume result."""
     rng = np.random.default_rng(3)
-    codes = rng.integers(0, 65536, (20, 17, 33), dtype=np.uint16)
-    whole = gpu_aggregates(codes, 5, -1.0, 3.0, (0, 0, 0), (33, 17, 20))
+    codes = rng.integers(0, 65536, (20, 17, nx), dtype=np.uint16)
+    codes[3, 5, 7] = codes[15, 2, 1] = 0          # tied minima in different slabs
+    codes[12, 9, 2] = codes[16, 0, 0] = 65535     # tied maxima in the second slab
+    whole = gpu_aggregates(codes, 5, -1.0, 3.0, (0, 0, 0), (nx, 17, 20))
+    ref = ob.aggregates_range(ob.Volume(codes, 5, -1.0, 3.0), (0, 0, 0), (nx, 17, 20))
+    assert tuple(whole.argmin) == tuple(ref.argmin) == (7, 5, 3)
+    assert tuple(whole.argmax) == tuple(ref.argmax) == (2, 9, 12)
     P = _lib.HipAggregatePartial_t
     slabs = [(0, 7), (7, 20)]
     vols = [gpu_volume(np.ascontiguousarray(codes[z0:z1]), 5, -1.0, 3.0) for z0, z1 in slabs]
@@ -282,7 +288,7 @@ def test_aggregate_slab_partials_combine_to_the_whole():
         lib.vktHipAggregatePartialInit(C.byref(acc1))
         for (z0, z1), v in zip(slabs, vols):
             p = P()
-            assert lib.vktHipAggregatesPass(v.hip_view(), _lib.Vec3i_t(0, 0, 0), _lib.Vec3i_t(33, 17, z1 - z0), z0, 1,
+            assert lib.vktHipAggregatesPass(v.hip_view(), _lib.Vec3i_t(0, 0, 0), _lib.Vec3i_t(nx, 17, z1 - z0), z0, 1,
                                             0.0, C.byref(p)) == 0
             lib.vktHipAggregatePartialCombine(C.byref(acc1), C.byref(p))
         mean = lib.vktHipAggregatesMean(C.byref(acc1), codes.size)
@@ -290,13 +296,13 @@ def test_aggregate_slab_partials_combine_to_the_whole():
         lib.vktHipAggregatePartialInit(C.byref(acc2))
         for (z0, z1), v in zip(slabs, vols):
             p = P()
-            assert lib.vktHipAggregatesPass(v.hip_view(), _lib.Vec3i_t(0, 0, 0), _lib.Vec3i_t(33, 17, z1 - z0), z0, 2,
+            assert lib.vktHipAggregatesPass(v.hip_view(), _lib.Vec3i_t(0, 0, 0), _lib.Vec3i_t(nx, 17, z1 - z0), z0, 2,
                                             mean, C.byref(p)) == 0
             lib.vktHipAggregatePartialCombine(C.byref(acc2), C.byref(p))
     finally:
         set_device(vkt.ExecutionPolicy.Device_CPU)
     out = _lib.Aggregates_t()
-    lib.vktHipAggregatesFinish(C.byref(acc1), C.byref(acc2), codes.size, 33, 17, C.byref(out))
+    lib.vktHipAggregatesFinish(C.byref(acc1), C.byref(acc2), codes.size, nx, 17, C.byref(out))
     assert (out.min, out.max) == (whole.min, whole.max)
     assert (out.argmin.x, out.argmin.y, out.argmin.z) == tuple(whole.argmin)
     assert (out.argmax.x, out.argmax.y, out.argmax.z) == tuple(whole.argmax)

@@ -369,6 +369,8 @@ namespace hipk
         uint32_t nb, rShift;
         uint32_t tileBase, tileBins;   // TILED: this launch counts bins [tileBase, +tileBins)
         unsigned long long* bins;
+        uint64_t giBase;            // aggregates, CONTIG: global linear index of the span start
+        int64_t zGlobal;            // aggregates: Z-slab offset added to z for global indices
     };
 
     typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -377,6 +379,26 @@ namespace hipk
     {
         // == binOf for numBins <= 2^24: -1 < f < numBins <=> 0 <= (size_t)f < numBins
         return (f > -1.0f && f < nbf) ? static_cast<uint32_t>(static_cast<int32_t>(f)) : nb;
+    }
+
+    // first voxel of 8-voxel item `item` (offset into h.data); non-CONTIG items < 2^32
+    template <bool CONTIG>
+    __device__ __forceinline__ uint64_t spanVoxel(FastHistArgs const& h, uint64_t item)
+    {
+        if constexpr (CONTIG)
+            return item * 8;
+        else
+        {
+            uint32_t const i = static_cast<uint32_t>(item);
+            uint32_t const r = fdiv(i, h.fdIpr);
+            uint32_t const xi = i - r * h.fdIpr.d;
+            uint32_t const zr = fdiv(r, h.fdNy);
+            uint32_t const yr = r - zr * h.fdNy.d;
+            return ((static_cast<uint64_t>(h.fz + zr) * static_cast<uint64_t>(h.dimY) + (h.fy + yr)) *
+                        static_cast<uint64_t>(h.dimX) +
+                    static_cast<uint64_t>(h.fx)) +
+                   8ull * xi;
+        }
     }
 
     template <int FMT, bool CONTIG, bool TILED, int BLOCK>
@@ -408,22 +430,7 @@ namespace hipk
         // this lane's copy of counter row 0; row b is at + (b << rowShift) (one v_lshl_add)
         char* const cLane = reinterpret_cast<char*>(cnt) + (TILED ? 0u : (lane & ((1u << h.rShift) - 1u)) << 2);
 
-        auto voxelOf = [&](uint64_t item) -> uint64_t {
-            if constexpr (CONTIG)
-                return item * 8;
-            else
-            {
-                uint32_t const i = static_cast<uint32_t>(item);
-                uint32_t const r = fdiv(i, h.fdIpr);
-                uint32_t const xi = i - r * h.fdIpr.d;
-                uint32_t const zr = fdiv(r, h.fdNy);
-                uint32_t const yr = r - zr * h.fdNy.d;
-                return ((static_cast<uint64_t>(h.fz + zr) * static_cast<uint64_t>(h.dimY) + (h.fy + yr)) *
-                            static_cast<uint64_t>(h.dimX) +
-                        static_cast<uint64_t>(h.fx)) +
-                       8ull * xi;
-            }
-        };
+        auto voxelOf = [&](uint64_t item) { return spanVoxel<CONTIG>(h, item); };
         auto add = [&](uint32_t b) {
             if constexpr (TILED)
             {
@@ -514,6 +521,96 @@ namespace hipk
         }
     }
 
+    // ---- Aggregates, streaming path (UInt8 / UInt16 / Float32, 8-voxel-aligned rows) -----
+    // Same item walk as histogramFastKernel (4 x 64 items per wave-step, all loads in flight
+    // first; CONTIG ranges one span) with a compile-time decode.  A lane visits its voxels in
+    // increasing index order, so the strict </> updates keep the first occurrence within the
+    // lane and minCombine/maxCombine (index tie-break) keep it across lanes: arg indices are
+    // exact whatever the schedule.  Sums accumulate per lane in double, then the fixed
+    // shuffle / LDS / partials tree (deterministic for a given grid).
+    template <int PASS, int FMT, bool CONTIG>
+    __global__ __launch_bounds__(kBlock) void aggregatesFastKernel(FastHistArgs h, float const* meanPtr,
+                                                                  float meanValue, vktHipAggregatePartial_t* partials)
+    {
+        constexpr int BPV = FMT == codec::FmtUInt8 ? 1 : FMT == codec::FmtUInt16 ? 2 : 4;
+        constexpr int U = 4;
+        float const mean = PASS == 2 ? (meanPtr ? *meanPtr : meanValue) : 0.f;
+        vktHipAggregatePartial_t p = emptyPartial();
+        uint32_t const lane = threadIdx.x & 63;
+        uint64_t const px = static_cast<uint64_t>(h.dimX), py = static_cast<uint64_t>(h.dimY);
+        // global linear index of voxel j of item `item`
+        auto globalIndex = [&](uint64_t item, int j) -> uint64_t {
+            if constexpr (CONTIG)
+                return h.giBase + item * 8 + static_cast<uint64_t>(j);
+            else
+            {
+                uint32_t const i = static_cast<uint32_t>(item);
+                uint32_t const r = fdiv(i, h.fdIpr);
+                uint32_t const xi = i - r * h.fdIpr.d;
+                uint32_t const zr = fdiv(r, h.fdNy);
+                uint32_t const yr = r - zr * h.fdNy.d;
+                return (static_cast<uint64_t>(h.fz + zr + h.zGlobal) * py + static_cast<uint64_t>(h.fy + yr)) * px +
+                       static_cast<uint64_t>(h.fx) + 8ull * xi + static_cast<uint64_t>(j);
+            }
+        };
+        auto visit8 = [&](uint32_t const (&c)[8], uint64_t item) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+            {
+                float const v = codec::decode(c[j], FMT, h.lo, h.hi);
+                if constexpr (PASS == 1)
+                {
+                    if (v < p.minValue || v > p.maxValue)   // rare after the first voxels
+                    {
+                        uint64_t const gi = globalIndex(item, j);
+                        if (v < p.minValue)
+                        {
+                            p.minValue = v;
+                            p.minIndex = gi;
+                        }
+                        if (v > p.maxValue)
+                        {
+                            p.maxValue = v;
+                            p.maxIndex = gi;
+                        }
+                    }
+                    p.sum += static_cast<double>(v);
+                    p.prod *= static_cast<double>(v);
+                }
+                else
+                {
+                    float const d = v - mean;
+                    float const d2 = d * d;
+                    p.sumSq += static_cast<double>(d2);
+                }
+            }
+            if constexpr (PASS == 1)
+                p.count += 8;
+        };
+        uint64_t const wave = static_cast<uint64_t>(blockIdx.x) * (kBlock / 64) + (threadIdx.x >> 6);
+        uint64_t const waves = static_cast<uint64_t>(gridDim.x) * (kBlock / 64);
+        uint64_t const steps = h.items / (64 * U);
+        for (uint64_t st = wave; st < steps; st += waves)
+        {
+            uint32_t c[U][8];
+#pragma unroll
+            for (int k = 0; k < U; ++k)
+                load8<BPV, true>(h.data, spanVoxel<CONTIG>(h, st * (64 * U) + k * 64 + lane), c[k]);
+#pragma unroll
+            for (int k = 0; k < U; ++k)
+                visit8(c[k], st * (64 * U) + k * 64 + lane);
+        }
+        for (uint64_t it = steps * (64 * U) + wave * 64 + lane; it < h.items; it += waves * 64)
+        {
+            uint32_t c[8];
+            load8<BPV, true>(h.data, spanVoxel<CONTIG>(h, it), c);
+            visit8(c, it);
+        }
+        blockReduce(p);
+        if (threadIdx.x == 0)
+            partials[blockIdx.x] = p;
+    }
+
     __global__ void zeroU64Kernel(unsigned long long* p, uint64_t n)
     {
         uint64_t const i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -584,25 +681,21 @@ namespace hipk
 #define VKT_HIST_LAUNCH(B, V, G, LDS, S) \
     hipLaunchKernelGGL((histogramKernel<B, V>), dim3(G), dim3(kBlock), LDS, S, a, h)
 
-    // Launches histogramFastKernel when the range qualifies (see its comment); false otherwise.
-    bool launchFastHistogram(BoxArgs const& a, HistArgs const& hh, hipStream_t s)
+    // Item walk of the streaming kernels (histogramFastKernel, aggregatesFastKernel) over a
+    // range: UInt8/UInt16/Float32 with 8-voxel-aligned rows; false if the range does not qualify.
+    bool makeSpanArgs(BoxArgs const& a, FastHistArgs& h, bool& contig)
     {
         int32_t const fmt = a.fmt;
         if ((fmt != codec::FmtUInt8 && fmt != codec::FmtUInt16 && fmt != codec::FmtFloat32) || !vecRows(a))
             return false;
-        // LDS counters of one 1024-thread workgroup (the device limit minus the static table)
-        uint32_t const tileCap = (ldsBinCapacity() * 4u - 1024u) / 4u;
-        uint64_t const tiles = (hh.numBins + tileCap - 1) / tileCap;
-        if (tiles > kFastMaxTiles)
-            return false;
         uint32_t const bpv = codec::bytesPerVoxel(fmt);
         uint64_t const ny = a.fdNy.d;   // range rows = ny * nz
         uint64_t const nz = a.rows / ny;
-        bool const contig = a.nx == a.dimX && (ny == static_cast<uint64_t>(a.dimY) || nz == 1);
+        contig = a.nx == a.dimX && (ny == static_cast<uint64_t>(a.dimY) || nz == 1);
         uint64_t const items = static_cast<uint64_t>(a.nx / 8) * a.rows;
         if (!contig && items >= (1ull << 32))
             return false;
-        FastHistArgs h{};
+        h = FastHistArgs{};
         h.items = items;
         h.dimX = a.dimX;
         h.dimY = a.dimY;
@@ -611,9 +704,29 @@ namespace hipk
         h.fz = a.fz;
         h.fdIpr = makeFastDiv(static_cast<uint32_t>(a.nx / 8));
         h.fdNy = a.fdNy;
-        h.data = contig ? a.data + ((static_cast<uint64_t>(a.fz) * a.dimY + a.fy) * a.dimX) * bpv : a.data;
+        uint64_t const start = (static_cast<uint64_t>(a.fz) * a.dimY + a.fy) * a.dimX;   // CONTIG: fx == 0
+        h.data = contig ? a.data + start * bpv : a.data;
         h.lo = a.lo;
         h.hi = a.hi;
+        h.zGlobal = a.zGlobal;
+        h.giBase = start + static_cast<uint64_t>(a.zGlobal) * a.dimY * a.dimX;
+        return true;
+    }
+
+    // Launches histogramFastKernel when the range qualifies (see its comment); false otherwise.
+    bool launchFastHistogram(BoxArgs const& a, HistArgs const& hh, hipStream_t s)
+    {
+        int32_t const fmt = a.fmt;
+        // LDS counters of one 1024-thread workgroup (the device limit minus the static table)
+        uint32_t const tileCap = (ldsBinCapacity() * 4u - 1024u) / 4u;
+        uint64_t const tiles = (hh.numBins + tileCap - 1) / tileCap;
+        if (tiles > kFastMaxTiles)
+            return false;
+        FastHistArgs h;
+        bool contig;
+        if (!makeSpanArgs(a, h, contig))
+            return false;
+        uint64_t const items = h.items;
         h.scale = hh.scale;
         h.nb = static_cast<uint32_t>(hh.numBins);
         h.nbf = static_cast<float>(hh.numBins);
@@ -661,6 +774,51 @@ namespace hipk
 #undef VKT_FAST_HIST_FMT
 #undef VKT_FAST_HIST
         return true;
+    }
+
+    // Grid of one aggregates pass (= number of partials it writes) and its launch: the
+    // streaming kernel when the range qualifies, else the row kernel.
+    unsigned aggGrid(BoxArgs const& a)
+    {
+        FastHistArgs h;
+        bool contig;
+        if (makeSpanArgs(a, h, contig))
+            return streamingGrid(h.items, 64u * 4u * (kBlock / 64), 8);
+        return rowGrid(a.rows);
+    }
+
+    void launchAggregates(BoxArgs const& a, int pass, unsigned g, hipStream_t s, float const* meanPtr, float meanV,
+                          vktHipAggregatePartial_t* out)
+    {
+        FastHistArgs h;
+        bool contig;
+        if (makeSpanArgs(a, h, contig))
+        {
+#define VKT_AGG_FAST(PASS, FMT)                                                                                  \
+    do {                                                                                                         \
+        if (contig)                                                                                              \
+            hipLaunchKernelGGL((aggregatesFastKernel<PASS, FMT, true>), dim3(g), dim3(kBlock), 0, s, h, meanPtr, meanV, out); \
+        else                                                                                                     \
+            hipLaunchKernelGGL((aggregatesFastKernel<PASS, FMT, false>), dim3(g), dim3(kBlock), 0, s, h, meanPtr, meanV, out); \
+    } while (0)
+#define VKT_AGG_FAST_FMT(PASS)                                                                                   \
+    do {                                                                                                         \
+        if (a.fmt == codec::FmtUInt8) VKT_AGG_FAST(PASS, codec::FmtUInt8);                                       \
+        else if (a.fmt == codec::FmtUInt16) VKT_AGG_FAST(PASS, codec::FmtUInt16);                                \
+        else VKT_AGG_FAST(PASS, codec::FmtFloat32);                                                              \
+    } while (0)
+            if (pass == 1)
+                VKT_AGG_FAST_FMT(1);
+            else
+                VKT_AGG_FAST_FMT(2);
+#undef VKT_AGG_FAST_FMT
+#undef VKT_AGG_FAST
+            return;
+        }
+        if (pass == 1)
+            VKT_REDUCE_DISPATCH(VKT_AGG_LAUNCH, 1, g, s, meanPtr, meanV, out);
+        else
+            VKT_REDUCE_DISPATCH(VKT_AGG_LAUNCH, 2, g, s, meanPtr, meanV, out);
     }
 
     struct AggScratch
@@ -734,7 +892,7 @@ vktError vktHipAggregatesPass(vktHipVolumeView_t volume, vktVec3i_t first, vktVe
     if (!makeBox(volume, first, last, zGlobalOffset, a, "vktHipAggregatesPass: invalid volume view", e))
         return e;
     hipStream_t s = rt::computeStream();
-    unsigned const g = rowGrid(a.rows);
+    unsigned const g = aggGrid(a);
     AggScratch& sc = aggScratch();
     size_t const bytes = (static_cast<size_t>(g) + 1) * sizeof(vktHipAggregatePartial_t);
     auto* partials = static_cast<vktHipAggregatePartial_t*>(sc.dev.acquire(bytes, s));
@@ -746,10 +904,7 @@ vktError vktHipAggregatesPass(vktHipVolumeView_t volume, vktVec3i_t first, vktVe
         sc.dev.release(s);
         return vktInvalidValue;
     }
-    if (pass == 1)
-        VKT_REDUCE_DISPATCH(VKT_AGG_LAUNCH, 1, g, s, nullptr, 0.f, partials);
-    else
-        VKT_REDUCE_DISPATCH(VKT_AGG_LAUNCH, 2, g, s, nullptr, mean, partials);
+    launchAggregates(a, pass, g, s, nullptr, pass == 1 ? 0.f : mean, partials);
     hipLaunchKernelGGL(aggregatesFinalKernel, dim3(1), dim3(kBlock), 0, s, partials, g, partials + g,
                        static_cast<float*>(nullptr), 1.0);
     e = rt::check(hipMemcpyAsync(sc.host, partials + g, sizeof(vktHipAggregatePartial_t), hipMemcpyDeviceToHost, s),
@@ -804,7 +959,7 @@ vktError vktHipAggregatesRange(vktHipVolumeView_t volume, vktVec3i_t first, vktV
     {
         // both passes and the mean stay on the device: one host round trip at the end
         hipStream_t s = rt::computeStream();
-        unsigned const g = rowGrid(a.rows);
+        unsigned const g = aggGrid(a);
         AggScratch& sc = aggScratch();
         size_t const bytes = (2 * static_cast<size_t>(g) + 2) * sizeof(vktHipAggregatePartial_t) + 16;
         auto* partials = static_cast<vktHipAggregatePartial_t*>(sc.dev.acquire(bytes, s));
@@ -819,10 +974,10 @@ vktError vktHipAggregatesRange(vktHipVolumeView_t volume, vktVec3i_t first, vktV
         }
         vktHipAggregatePartial_t* res = partials + 2 * g;   // [0] pass 1, [1] pass 2
         float* meanDev = reinterpret_cast<float*>(res + 2);
-        VKT_REDUCE_DISPATCH(VKT_AGG_LAUNCH, 1, g, s, nullptr, 0.f, partials);
+        launchAggregates(a, 1, g, s, nullptr, 0.f, partials);
         hipLaunchKernelGGL(aggregatesFinalKernel, dim3(1), dim3(kBlock), 0, s, partials, g, res, meanDev,
                            static_cast<double>(numElems));
-        VKT_REDUCE_DISPATCH(VKT_AGG_LAUNCH, 2, g, s, meanDev, 0.f, partials + g);
+        launchAggregates(a, 2, g, s, meanDev, 0.f, partials + g);
         hipLaunchKernelGGL(aggregatesFinalKernel, dim3(1), dim3(kBlock), 0, s, partials + g, g, res + 1,
                            static_cast<float*>(nullptr), 1.0);
         e = rt::check(hipMemcpyAsync(sc.host, res, 2 * sizeof(vktHipAggregatePartial_t), hipMemcpyDeviceToHost, s),
