@@ -1,0 +1,30 @@
+#!/bin/bash
+# Round evidence on the GPU box, every step under its own time limit, stopping at the first
+# failure: smoke -> full GPU tests -> default bench -> rocprofv3 kernel stats of the bench ->
+# FETCH_SIZE / WRITE_SIZE PMC passes (separate runs) -> kernel stats of every
+# tools/bench_configs.py group and the grid-size sweep.  Output: gpurun_out/final/.
+set -u
+cd "$(dirname "$0")/.."
+export TMPDIR=/tmp
+O=gpurun_out/final
+mkdir -p $O
+step() {  # name, limit, command...
+    local name=$1 limit=$2; shift 2
+    echo "== $name $(date +%T)"
+    timeout -k 10 "$limit" "$@" > "$O/$name.log" 2>&1
+    local rc=$?
+    echo "== $name rc=$rc"
+    tail -n 3 "$O/$name.log"
+    return $rc
+}
+B="python3 bench.py --no-cpu-baseline --no-copy-peak"   # the default steps / warm-up of the bench line
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1
+step pytest_gpu 900 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread || exit 1
+step bench 300 python bench.py || exit 1
+step prof_trace 300 rocprofv3 --kernel-trace --stats -d $O/prof/trace -o run --output-format csv -- $B || exit 1
+step prof_fetch 300 rocprofv3 --pmc FETCH_SIZE -d $O/prof/fetch -o run --output-format csv -- $B || exit 1
+step prof_write 300 rocprofv3 --pmc WRITE_SIZE -d $O/prof/write -o run --output-format csv -- $B || exit 1
+python3 scripts/parse_pmc.py $O/prof 1024 > $O/pmc_summary.json || exit 1
+step configs 600 rocprofv3 --kernel-trace --stats -d $O/configs -o run --output-format csv -- python3 tools/bench_configs.py --reps 5 || exit 1
+step sizes 300 python3 tools/bench_sizes.py || exit 1
+echo done
