@@ -190,7 +190,10 @@ namespace hipk
     // table in LDS, and lane l assembles V = 16 / BPVD destination voxels from LDS reads and
     // writes one 16-byte nontemporal store per destination row of the task's rectangle.
     // Preconditions (host): rows are 16-byte multiples, 16-byte aligned buffers, 4 slots fit.
-    template <int BPVS, int BPVD, bool CONV, bool CHAIN>
+    // DETECT (Float32 "Linear", optimistic): every staged source row is also checked for values
+    // that can make the lerp chain differ from v000 (chainSensitive); such a row's flag is set
+    // in a.rowDirtyOut and resampleGatherFixupKernel later re-evaluates the affected tasks.
+    template <int BPVS, int BPVD, bool CONV, bool CHAIN, bool DETECT = false>
     __global__ __launch_bounds__(kBlock) void resampleGatherLdsKernel(ResampleArgs a, uint32_t slotBytes)
     {
         constexpr int V = 16 / BPVD;
@@ -237,6 +240,17 @@ namespace hipk
                 for (int j = 0; j < kStage; ++j)
                     if (o0 + 1024u * j < rowBytes)
                         *reinterpret_cast<u32x4*>(slot + o0 + 1024u * j) = w[j];
+                if constexpr (DETECT)
+                {
+                    bool sens = false;
+#pragma unroll
+                    for (int j = 0; j < kStage; ++j)
+                        if (o0 + 1024u * j < rowBytes)
+                            sens = sens || chainSensitive(w[j].x) || chainSensitive(w[j].y) ||
+                                   chainSensitive(w[j].z) || chainSensitive(w[j].w);
+                    if (sens)   // rare; any lane may set the row's flag
+                        a.rowDirtyOut[srow / static_cast<uint64_t>(a.sdx)] = 1;
+                }
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -265,6 +279,25 @@ namespace hipk
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+    }
+
+    // Fix-up of the optimistic Float32 "Linear" gather: one wave per task; tasks whose source
+    // row's chain neighbourhood holds a flagged row (a.rowChain, from rowChainKernel) rewrite
+    // their destination rectangle with the full sampleLinear chain.
+    __global__ __launch_bounds__(kBlock) void resampleGatherFixupKernel(ResampleArgs a)
+    {
+        int const lane = threadIdx.x & 63;
+        uint32_t const wave = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+        uint32_t const totalWaves = gridDim.x * (kBlock / 64);
+        uint32_t const tasks = static_cast<uint32_t>(a.nRunsY) * static_cast<uint32_t>(a.nRunsZ);
+        for (uint32_t t = wave; t < tasks; t += totalWaves)
+        {
+            Run const ry = runY(a, t % static_cast<uint32_t>(a.nRunsY));
+            Run const rz = runZ(a, t / static_cast<uint32_t>(a.nRunsY));
+            uint64_t const srow = srcRowIndex(a, ry.s, rz.s);
+            if (a.rowChain[srow / static_cast<uint64_t>(a.sdx)])   // wave-uniform, rare
+                chainTask(a, ry, rz, lane);
         }
     }
 
@@ -658,9 +691,9 @@ namespace hipk
 
     // LDS-staged gather when the rows and tables fit (see resampleGatherLdsKernel).
     bool launchGatherLds(ResampleArgs const& b, uint32_t bs, uint32_t bd, bool identity, bool chain, uint64_t tasks,
-                         hipStream_t s)
+                         hipStream_t s, bool detect = false)
     {
-        if ((bs != 1 && bs != 2 && bs != 4) || (bd != 1 && bd != 2 && bd != 4) || (chain && bs != 4))
+        if ((bs != 1 && bs != 2 && bs != 4) || (bd != 1 && bd != 2 && bd != 4) || ((chain || detect) && bs != 4))
             return false;
         uint64_t const rowBytes = static_cast<uint64_t>(b.sdx) * bs;
         uint64_t const xtBytes = (static_cast<uint64_t>(b.ddx) * 4 + 15) & ~uint64_t(15);
@@ -678,7 +711,14 @@ namespace hipk
         uint32_t const slot = static_cast<uint32_t>(rowBytes);
 #define VKT_GL(S, D, C, H) hipLaunchKernelGGL((resampleGatherLdsKernel<S, D, C, H>), dim3(g), dim3(kBlock), lds, s, b, slot)
 #define VKT_GL_D(S, C, H) do { if (bd == 1) VKT_GL(S, 1, C, H); else if (bd == 2) VKT_GL(S, 2, C, H); else VKT_GL(S, 4, C, H); } while (0)
-        if (chain)
+#define VKT_GLX(D, C) hipLaunchKernelGGL((resampleGatherLdsKernel<4, D, C, false, true>), dim3(g), dim3(kBlock), lds, s, b, slot)
+        if (detect)
+        {
+            if (bd == 1) { if (identity) VKT_GLX(1, false); else VKT_GLX(1, true); }
+            else if (bd == 2) { if (identity) VKT_GLX(2, false); else VKT_GLX(2, true); }
+            else { if (identity) VKT_GLX(4, false); else VKT_GLX(4, true); }
+        }
+        else if (chain)
         {
             if (identity) VKT_GL_D(4, false, true); else VKT_GL_D(4, true, true);
         }
@@ -694,6 +734,7 @@ namespace hipk
         {
             if (identity) VKT_GL_D(4, false, false); else VKT_GL_D(4, true, false);
         }
+#undef VKT_GLX
 #undef VKT_GL_D
 #undef VKT_GL
         return true;
@@ -826,6 +867,42 @@ namespace hipk
             static rt::StreamScratch scratch;
             uint64_t const srcRows = static_cast<uint64_t>(src.dimY) * static_cast<uint64_t>(src.dimZ);
             uint8_t* dirty = static_cast<uint8_t*>(scratch.acquire(2 * srcRows, s));
+            // Optimistic variant when the tasks stage every source row of planes [minSz,
+            // maxSz] (y runs read every row, z runs consecutive planes): the gather itself flags
+            // the rows it stages, the local planes above maxSz (z+1 halo) are scanned, then
+            // rowChainKernel and a fix-up pass over the flagged tasks -- no pre-pass read of
+            // the source (768^3 -> 1024^3 Float32 Linear: see DESIGN.md §4.2b)
+            if (dirty && t.yAllRows && t.zContiguous && gatherLdsEnabled())
+            {
+                ResampleArgs b = a;
+                b.rowDirtyOut = dirty;
+                b.rowChain = dirty + srcRows;
+                bool ok = hipMemsetAsync(dirty, 0, srcRows, s) == hipSuccess;
+                int32_t const above = t.maxSz + 1 - a.srcZ0;   // first local plane above the task planes
+                if (ok && above < src.dimZ)
+                {
+                    uint64_t const row0 = static_cast<uint64_t>(above > 0 ? above : 0) * static_cast<uint64_t>(src.dimY);
+                    uint64_t const nrows = srcRows - row0;
+                    unsigned const gd = static_cast<unsigned>((nrows + kBlock / 64 - 1) / (kBlock / 64));
+                    uint8_t const* base = src.data + row0 * static_cast<uint64_t>(src.dimX) * 4u;
+                    if (src.dimX % 4 == 0)
+                        hipLaunchKernelGGL(rowDirtyKernel<true>, dim3(gd), dim3(kBlock), 0, s, base, src.dimX, nrows,
+                                           dirty + row0);
+                    else
+                        hipLaunchKernelGGL(rowDirtyKernel<false>, dim3(gd), dim3(kBlock), 0, s, base, src.dimX, nrows,
+                                           dirty + row0);
+                }
+                if (ok && launchGatherLds(b, bs, bd, identity, false, tasks, s, true))
+                {
+                    unsigned const gc = static_cast<unsigned>((srcRows + kBlock - 1) / kBlock);
+                    hipLaunchKernelGGL(rowChainKernel, dim3(gc), dim3(kBlock), 0, s, dirty, src.dimY, src.dimZ, a.srcZ0,
+                                       a.srcGlobalDz, dirty + srcRows);
+                    unsigned const gf = streamingGrid(tasks, kBlock / 64, 8);
+                    hipLaunchKernelGGL(resampleGatherFixupKernel, dim3(gf), dim3(kBlock), 0, s, b);
+                    scratch.release(s);
+                    return rt::finishLaunch("Resample_hip(linear chain, optimistic gather)");
+                }
+            }
             if (dirty)
             {
                 unsigned const gd = static_cast<unsigned>((srcRows + kBlock / 64 - 1) / (kBlock / 64));
