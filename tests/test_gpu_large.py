@@ -3,7 +3,8 @@
 
 * full-size parity where the oracle finishes in seconds (512^3 UInt16 arithmetic, config 2);
 * size-independent properties at the metric sizes: 2x Resample of integer (and finite,
-  non-negative float) data is exact replication; Sum with a zero volume is the identity for
+  non-negative float) data is exact replication; config 3 at full size (1024^3 -> 2048^3
+  Float32 Linear, 32 GiB) with a non-finite source voxel, checked plane by plane on the device; Sum with a zero volume is the identity for
   every UInt16 code; Fill writes one code everywhere; Copy reproduces its source;
 * Z-slab resample: P slabs of a global volume, each resampled from its local planes (owned +
   exchanged halo, per volkit_amd.slab's plan), equal the whole-volume oracle resample.
@@ -131,6 +132,45 @@ def test_float_resample_replication_512_to_1024(hip):
         for dy in (0, 1):
             for dx in (0, 1):
                 np.testing.assert_array_equal(r[dz::2, dy::2, dx::2], src.view(np.uint32))
+    S.free()
+    R.free()
+
+
+def test_config3_full_size_linear_with_specials(hip):
+    """BASELINE config 3 at full size: Resample 1024^3 -> 2048^3 Float32 Linear (32 GiB dst),
+    source uniform in [0, 1) plus +inf at one interior voxel p, checked on the device plane by
+    plane.  With fractions 0 the sampleLinear chain of source voxel s is v(s) + 0 * (its 7
+    neighbours, hi.x = next voxel in memory): inf where s == p (inf + 0 * finite), NaN where p is
+    one of s's 7 neighbours (0 * inf), else v(s) -- and dst(d) = chain(d // 2)."""
+    import torch
+    s, e = 1024, 2048
+    p = (517, 301, 700)   # (x, y, z), interior
+    S = DevVol(hip, (s, s, s), 7)
+    R = DevVol(hip, (e, e, e), 7)
+    gen = torch.Generator(device="cuda").manual_seed(3)
+    src = torch.rand((s, s, s), device="cuda", dtype=torch.float32, generator=gen)
+    src[p[2], p[1], p[0]] = float("inf")
+    assert hip.lib.vktHipMemcpy(S.ptr, src.data_ptr(), S.nbytes, 3) == 0
+    assert hip.lib.vktHipResample(R.view, S.view, 1) == 0
+    assert hip.lib.vktHipSynchronize() == 0
+    expect = src.clone()
+    for dz in (0, 1):
+        for dy in (0, 1):
+            for dx in (0, 1):
+                if dx or dy or dz:
+                    expect[p[2] - dz, p[1] - dy, p[0] - dx] = float("nan")
+    # copy the dst out plane pair by plane pair (device to device) and compare on the device
+    plane = e * e
+    for z in range(s):
+        t = torch.empty((2, e, e), device="cuda", dtype=torch.float32)
+        assert hip.lib.vktHipMemcpy(t.data_ptr(), R.ptr + 2 * z * plane * 4, 2 * plane * 4, 3) == 0
+        ref = expect[z].repeat_interleave(2, 0).repeat_interleave(2, 1)
+        for k in (0, 1):
+            got = t[k]
+            nan_g, nan_r = torch.isnan(got), torch.isnan(ref)
+            assert torch.equal(nan_g, nan_r), f"NaN mask differs in dst plane {2 * z + k}"
+            assert torch.equal(got[~nan_g], ref[~nan_r]), f"dst plane {2 * z + k}"
+    assert int(torch.isnan(expect).sum()) == 7
     S.free()
     R.free()
 
