@@ -134,6 +134,27 @@ def test_arithmetic_ragged_whole_volume(g, o):
         assert_codes_equal(out, ref, fmt, f"ragged fmt={fmt}")
 
 
+@pytest.mark.parametrize("op", OPS)
+def test_arithmetic_unit_mapping_all_code_pairs(g, o, op):
+    """The unit mapping (+0, 1) takes a compile-time path without the codec's lerp and
+    normalisation (codec::decodeUnit / normalise<3>): every UInt8 code pair, a UInt16 sweep
+    that covers every code as either operand, and the look-alike mappings -0 / 1.0 - ulp that
+    must NOT take it."""
+    a8 = np.repeat(np.arange(256, dtype=np.uint8), 256).reshape(16, 16, 256)
+    b8 = np.tile(np.arange(256, dtype=np.uint8), 256).reshape(16, 16, 256)
+    c16 = np.arange(65536, dtype=np.uint16)
+    a16 = np.concatenate([c16, np.random.default_rng(3).permutation(c16)]).reshape(8, 64, 256)
+    b16 = np.concatenate([np.random.default_rng(4).permutation(c16), c16]).reshape(8, 64, 256)
+    near1 = float(np.nextafter(np.float32(1.0), np.float32(0.0)))
+    for mapping in ((0.0, 1.0), (-0.0, 1.0), (0.0, near1)):
+        for fmt, a, b in ((4, a8, b8), (5, a16, b16)):
+            d = np.zeros_like(a)
+            last = (a.shape[2], a.shape[1], a.shape[0])
+            out = g.arith(op, [fmt] * 3, [mapping] * 3, a, b, d.copy(), (0, 0, 0), last, (0, 0, 0))
+            ref = o.arith(op, [fmt] * 3, [mapping] * 3, a, b, d.copy(), (0, 0, 0), last, (0, 0, 0))
+            assert_codes_equal(out, ref, fmt, f"{op} fmt={fmt} map={mapping} all code pairs")
+
+
 def test_arithmetic_float_bit_patterns(g, o):
     # every float bit pattern class, including NaN payloads, denormals and infinities
     rng = np.random.default_rng(17)

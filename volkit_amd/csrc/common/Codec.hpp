@@ -94,10 +94,14 @@ namespace codec
 
     // DIV selects the division at compile time where the caller has dispatched on
     // m.rangeIsPow2 (1: multiply by the exact reciprocal, 2: IEEE divide; 0: test at run
-    // time -- a uniform branch per voxel that keeps hipcc from interleaving voxels).
+    // time -- a uniform branch per voxel that keeps hipcc from interleaving voxels;
+    // 3: the unit mapping lo = +0, hi = 1 (isUnitMapping), where (value - 0) / 1 == value for
+    // every float including -0, +-inf and NaN, so normalising is the identity).
     template <int DIV = 0>
     VKT_HD float normalise(float value, MapParams const& m)
     {
+        if constexpr (DIV == 3)
+            return value;
         float v = value - m.lo;
         if constexpr (DIV == 1)
             return v * m.invRange;
@@ -162,6 +166,36 @@ namespace codec
         default:
             return prior;
         }
+    }
+
+    // decode() for a volume whose mapping is the unit mapping (isUnitMapping): lerp(+0, 1, t)
+    // = (1 - t) * +0 + t * 1 = +0 + t = t exactly for every t the integer formats produce
+    // (finite, t > -1, 1 - t > 0 so the first product is +0; t = +0 gives +0 + +0 = +0), so
+    // the four lerp operations drop out.
+    VKT_HD float decodeUnit(uint32_t code, int32_t fmt, float prior = 0.f)
+    {
+        switch (fmt)
+        {
+        case FmtInt16:
+            return (static_cast<float>(static_cast<int16_t>(static_cast<uint16_t>(code))) + 32767.f) / 65535.999f;
+        case FmtUInt8:
+            return static_cast<float>(code & 0xFFu) * kInv255999;
+        case FmtUInt16:
+            return static_cast<float>(code & 0xFFFFu) / 65535.999f;
+        case FmtUInt32:
+            return static_cast<float>(code) / 4294967295.999f;
+        case FmtFloat32:
+            return bitsToFloat(code);
+        default:
+            return prior;
+        }
+    }
+
+    // Mapping (lo, hi) is exactly (+0, 1): bit compare, since lo = -0 makes
+    // normalise(-0) = -0 - -0 = +0 (not the identity).
+    VKT_HD bool isUnitMapping(float lo, float hi)
+    {
+        return floatToBits(lo) == 0u && floatToBits(hi) == 0x3F800000u;
     }
 
     // Host helper: build MapParams for a volume's mapping.

@@ -136,6 +136,12 @@ namespace hipk
     // One workgroup's span [beg, end) of 8-voxel items.  The main loop is branch-free so that
     // the compiler keeps all kUnroll x NS loads in flight (a guard per item made hipcc wait
     // vmcnt(0) after every item); the remainder loop handles the last partial quantum.
+    // Functors with kPacked16 work on raw dwords of two UInt16 codes (F::pk).
+    template <class F, class = void>
+    struct IsPacked16 { static constexpr bool value = false; };
+    template <class F>
+    struct IsPacked16<F, decltype(void(F::kPacked16))> { static constexpr bool value = F::kPacked16; };
+
     template <int NS, int BPV, int MODE, class F>
     __device__ __forceinline__ void pointwiseVecSpan(Operand const& d, Operand const& s1, Operand const& s2,
                                                      Geom const& g, uint64_t beg, uint64_t end, F const& f)
@@ -143,6 +149,43 @@ namespace hipk
         constexpr int kUnroll = vecUnroll<BPV>();
         constexpr uint64_t kQ = static_cast<uint64_t>(kVecBlock) * kUnroll;
         uint64_t it = beg + threadIdx.x;
+        if constexpr (BPV == 2 && NS == 2 && IsPacked16<F>::value)
+        {
+            // same schedule as below (all loads of a quantum before its stores), no unpacking:
+            // 16 B of each source -> 16 B of dst
+            auto apply = [&](u32x4 const& a, u32x4 const& b, uint64_t od) {
+                u32x4 r;
+                r.x = f.pk(a.x, b.x);
+                r.y = f.pk(a.y, b.y);
+                r.z = f.pk(a.z, b.z);
+                r.w = f.pk(a.w, b.w);
+                __builtin_nontemporal_store(r, reinterpret_cast<u32x4*>(d.data + 2 * od));
+            };
+            for (; it + (kUnroll - 1) * static_cast<uint64_t>(kVecBlock) < end; it += kQ)
+            {
+                u32x4 a[kUnroll], b[kUnroll];
+                uint64_t od[kUnroll];
+#pragma unroll
+                for (int u = 0; u < kUnroll; ++u)
+                {
+                    uint64_t o1, o2;
+                    pointwiseVecItem<NS, BPV, MODE, F>(d, s1, s2, g, it + static_cast<uint64_t>(u) * kVecBlock, o1, o2,
+                                                       od[u]);
+                    a[u] = loadVec<u32x4, true>(s1.data + 2 * o1);
+                    b[u] = loadVec<u32x4, true>(s2.data + 2 * o2);
+                }
+#pragma unroll
+                for (int u = 0; u < kUnroll; ++u)
+                    apply(a[u], b[u], od[u]);
+            }
+            for (; it < end; it += kVecBlock)
+            {
+                uint64_t o1, o2, od;
+                pointwiseVecItem<NS, BPV, MODE, F>(d, s1, s2, g, it, o1, o2, od);
+                apply(loadVec<u32x4, true>(s1.data + 2 * o1), loadVec<u32x4, true>(s2.data + 2 * o2), od);
+            }
+            return;
+        }
         for (; it + (kUnroll - 1) * static_cast<uint64_t>(kVecBlock) < end; it += kQ)
         {
             uint32_t a[kUnroll][8], b[kUnroll][8];

@@ -35,7 +35,8 @@ namespace hipk
         MapParams dm;
         __device__ __forceinline__ uint32_t operator()(uint32_t a, uint32_t) const
         {
-            float v = codec::decode(a, FS == kDyn ? fs : FS, slo, shi);
+            // DIV 3: source and destination mappings are both the unit mapping
+            float v = DIV == 3 ? codec::decodeUnit(a, FS == kDyn ? fs : FS) : codec::decode(a, FS == kDyn ? fs : FS, slo, shi);
             bool w;
             return codec::encode<DIV>(v, FD == kDyn ? fd : FD, dm, w);
         }
@@ -65,13 +66,63 @@ namespace hipk
         MapParams dm;
         __device__ __forceinline__ uint32_t operator()(uint32_t a, uint32_t b) const
         {
-            float v1 = codec::decode(a, FS1 == kDyn ? fs1 : FS1, lo1, hi1);
-            float v2 = codec::decode(b, FS2 == kDyn ? fs2 : FS2, lo2, hi2);
+            // DIV 3: all three mappings are the unit mapping (codec::isUnitMapping)
+            float v1 = DIV == 3 ? codec::decodeUnit(a, FS1 == kDyn ? fs1 : FS1) : codec::decode(a, FS1 == kDyn ? fs1 : FS1, lo1, hi1);
+            float v2 = DIV == 3 ? codec::decodeUnit(b, FS2 == kDyn ? fs2 : FS2) : codec::decode(b, FS2 == kDyn ? fs2 : FS2, lo2, hi2);
             float r = applyOp<OP>(v1, v2, dm.lo, dm.hi);
             bool w;
             return codec::encode<DIV>(r, FD == kDyn ? fd : FD, dm, w);
         }
     };
+
+    // UInt16 codes with the unit mapping on all three volumes: decodeUnit(c) = c * 2^-16
+    // exactly, so a + b, a - b and |a - b| are exact in f32 (at most 17 significant bits),
+    // normalise<3> is the identity, and * 65535.999f (== 65536.0f), cvtt, & 0xFFFF give back
+    // the integer result modulo 2^16.  Hence, bit for bit:
+    //   Sum (a + b) mod 2^16, Diff (a - b) mod 2^16, AbsDiff and SafeAbsDiff |a - b| (< 1,
+    //   never clamped), SafeDiff max(a - b, 0), SafeSum a + b < 2^16 ? a + b : 0 (the clamp to
+    //   1.0 encodes to 65536 & 0xFFFF = 0).
+    // Prod/Quot round in f32 and keep the float path.  Checked against the oracle for every
+    // code as either operand (tests/test_gpu_parity.py::test_arithmetic_unit_mapping_*).
+    // kPacked16: pointwiseVecSpan applies pk() to whole dwords (two voxels; v_pk_*_u16).
+    template <int OP>
+    struct IntArithU16F
+    {
+        static constexpr bool kPacked16 = true;
+        typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
+
+        __device__ __forceinline__ uint32_t operator()(uint32_t a, uint32_t b) const
+        {
+            if constexpr (OP == vktHipOpSum) return (a + b) & 0xFFFFu;
+            else if constexpr (OP == vktHipOpDiff) return (a - b) & 0xFFFFu;
+            else if constexpr (OP == vktHipOpSafeSum) return a + b < 0x10000u ? a + b : 0u;
+            else if constexpr (OP == vktHipOpSafeDiff) return a > b ? a - b : 0u;
+            else return a > b ? a - b : b - a;   // AbsDiff, SafeAbsDiff
+        }
+
+        __device__ __forceinline__ uint32_t pk(uint32_t a, uint32_t b) const
+        {
+            u16x2 const x = __builtin_bit_cast(u16x2, a), y = __builtin_bit_cast(u16x2, b);
+            u16x2 r;
+            if constexpr (OP == vktHipOpSum) r = x + y;
+            else if constexpr (OP == vktHipOpDiff) r = x - y;
+            else if constexpr (OP == vktHipOpSafeSum)
+            {
+                u16x2 const s = x + y;   // wrapped; it overflowed iff s < x
+                r = s & ~__builtin_bit_cast(u16x2, s < x);
+            }
+            else if constexpr (OP == vktHipOpSafeDiff) r = __builtin_elementwise_sub_sat(x, y);
+            else r = __builtin_elementwise_sub_sat(x, y) | __builtin_elementwise_sub_sat(y, x);
+            return __builtin_bit_cast(uint32_t, r);
+        }
+    };
+
+    template <int OP>
+    constexpr bool hasIntArithU16()
+    {
+        return OP == vktHipOpSum || OP == vktHipOpDiff || OP == vktHipOpAbsDiff || OP == vktHipOpSafeSum ||
+               OP == vktHipOpSafeDiff || OP == vktHipOpSafeAbsDiff;
+    }
 
     template <int NS, class F>
     vktError launchByBpv(PwPlan const& p, F const& f, hipStream_t s)
@@ -94,12 +145,20 @@ namespace hipk
         int32_t f1 = a.dataFormat, f2 = b.dataFormat, fd = d.dataFormat;
         if (p.vec && f1 == f2 && f1 == fd)
         {
+        // unit mappings everywhere (the canonical [0, 1] inputs): the codec's lerp and
+        // normalisation are identities (codec::decodeUnit / normalise<3>)
+        bool const unit = codec::isUnitMapping(a.mappingLo, a.mappingHi) &&
+                          codec::isUnitMapping(b.mappingLo, b.mappingHi) &&
+                          codec::isUnitMapping(d.mappingLo, d.mappingHi);
+#define VKT_ARITH_LAUNCH(FMT, BPV, DIV)                                                                        \
+    launchPointwise<2, BPV>(p, ArithF<OP, FMT, FMT, FMT, DIV>{f1, f2, fd, a.mappingLo, a.mappingHi, b.mappingLo, \
+                                                              b.mappingHi, dm}, s)
 #define VKT_ARITH_FIXED(FMT, BPV)                                                                              \
-    return dm.rangeIsPow2                                                                                      \
-               ? launchPointwise<2, BPV>(p, ArithF<OP, FMT, FMT, FMT, 1>{f1, f2, fd, a.mappingLo, a.mappingHi,  \
-                                                                         b.mappingLo, b.mappingHi, dm}, s)      \
-               : launchPointwise<2, BPV>(p, ArithF<OP, FMT, FMT, FMT, 2>{f1, f2, fd, a.mappingLo, a.mappingHi,  \
-                                                                         b.mappingLo, b.mappingHi, dm}, s)
+    return unit ? VKT_ARITH_LAUNCH(FMT, BPV, 3)                                                                \
+                : dm.rangeIsPow2 ? VKT_ARITH_LAUNCH(FMT, BPV, 1) : VKT_ARITH_LAUNCH(FMT, BPV, 2)
+            if constexpr (hasIntArithU16<OP>())
+                if (fd == codec::FmtUInt16 && unit)
+                    return launchPointwise<2, 2>(p, IntArithU16F<OP>{}, s);
             if (fd == codec::FmtUInt16)
                 VKT_ARITH_FIXED(codec::FmtUInt16, 2);
             if (fd == codec::FmtUInt8)
@@ -107,6 +166,7 @@ namespace hipk
             if (fd == codec::FmtFloat32)
                 VKT_ARITH_FIXED(codec::FmtFloat32, 4);
 #undef VKT_ARITH_FIXED
+#undef VKT_ARITH_LAUNCH
         }
         return launchByBpv<2>(p, ArithF<OP, kDyn, kDyn, kDyn>{f1, f2, fd, a.mappingLo, a.mappingHi, b.mappingLo,
                                                                b.mappingHi, dm}, s);
