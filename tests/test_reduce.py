@@ -185,6 +185,26 @@ def test_histogram_parity(fmt, mapping, nbins):
 
 
 @pytest.mark.gpu
+def test_histogram_uint16_unit_mapping_every_code():
+    """UInt16 + unit mapping + 2^k bins takes the integer path (bin = code >> (16 - k)): every
+    code, each power of two up to 2^17, and the look-alike mappings that must not take it."""
+    codes = np.arange(65536, dtype=np.uint16).reshape(16, 16, 256)
+    near1 = float(np.nextafter(np.float32(1.0), np.float32(2.0)))
+    for mapping in ((0.0, 1.0), (-0.0, 1.0), (0.0, near1)):
+        for nbins in (1, 2, 16, 256, 1024, 4096, 65536, 131072, 3, 65535):
+            got = gpu_histogram(codes, 5, *mapping, (0, 0, 0), (256, 16, 16), nbins)
+            ref, _ = ob.histogram_range(ob.Volume(codes, 5, *mapping), (0, 0, 0), (256, 16, 16), nbins)
+            np.testing.assert_array_equal(got, ref, err_msg=f"map={mapping} nbins={nbins}")
+    # UInt8: the shift path is taken when the host evaluation of all 256 bins is c >> s
+    codes = np.tile(np.arange(256, dtype=np.uint8), 64).reshape(8, 8, 256)
+    for mapping in ((0.0, 1.0), (-0.0, 1.0), (-1.0, 3.0), (0.0, 0.5), (0.0, 2.0)):
+        for nbins in (1, 2, 64, 128, 256, 512, 255, 1000):
+            got = gpu_histogram(codes, 4, *mapping, (0, 0, 0), (256, 8, 8), nbins)
+            ref, _ = ob.histogram_range(ob.Volume(codes, 4, *mapping), (0, 0, 0), (256, 8, 8), nbins)
+            np.testing.assert_array_equal(got, ref, err_msg=f"u8 map={mapping} nbins={nbins}")
+
+
+@pytest.mark.gpu
 def test_histogram_constant_volume_and_reference_example():
     """Wave-uniform bins (one atomic per wave) and src/examples/Histogram.cpp's 256 bins."""
     codes = np.full((33, 65, 130), 200, np.uint8)
@@ -208,7 +228,7 @@ def check_float(name, gpu, oracle, exact, terms_abs_sum, n):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("fmt,mapping", [(4, (0.0, 1.0)), (5, (-1.0, 3.0)), (2, (0.0, 1.0)), (7, (0.0, 1.0)),
+@pytest.mark.parametrize("fmt,mapping", [(4, (0.0, 1.0)), (5, (-1.0, 3.0)), (5, (0.0, 1.0)), (4, (-0.0, 1.0)), (2, (0.0, 1.0)), (7, (0.0, 1.0)),
                                          (6, (0.25, 7.5))])
 def test_aggregates_parity(fmt, mapping):
     rng = np.random.default_rng(fmt)

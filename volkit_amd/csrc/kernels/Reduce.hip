@@ -367,6 +367,7 @@ namespace hipk
         int32_t dimX, dimY, fx, fy, fz;
         float lo, hi, scale, nbf;
         uint32_t nb, rShift;
+        uint32_t binShift;          // SHIFT (UInt16, unit mapping, nb = 2^k <= 2^16): bin = code >> binShift
         uint32_t tileBase, tileBins;   // TILED: this launch counts bins [tileBase, +tileBins)
         unsigned long long* bins;
         uint64_t giBase;            // aggregates, CONTIG: global linear index of the span start
@@ -401,7 +402,13 @@ namespace hipk
         }
     }
 
-    template <int FMT, bool CONTIG, bool TILED, int BLOCK>
+    // SHIFT: the bin of every code is code >> binShift, so one shift replaces the decode, the
+    // range test and the conversion (UInt16) or the LDS table read (UInt8).  UInt16: taken
+    // for the unit mapping (+0, 1) and numBins = 2^k, k <= 16, where decode(c) = c * 2^-16
+    // exactly (codec::decodeUnit), scale = numBins / 1 = 2^k, and f = c * 2^(k-16) is exact and
+    // in [0, numBins), so the reference's (size_t)((v - lo) * scale) is c >> (16 - k).
+    // UInt8: taken when the host evaluation of all 256 bins (hostBinU8) is such a shift.
+    template <int FMT, bool CONTIG, bool TILED, int BLOCK, bool SHIFT = false>
     __global__ __launch_bounds__(BLOCK) void histogramFastKernel(FastHistArgs h)
     {
         constexpr int BPV = FMT == codec::FmtUInt8 ? 1 : FMT == codec::FmtUInt16 ? 2 : 4;
@@ -413,7 +420,7 @@ namespace hipk
         uint32_t const total = TILED ? h.tileBins : (h.nb + 1) << h.rShift;
         for (uint32_t i = threadIdx.x; i < total; i += BLOCK)
             cnt[i] = 0;
-        if constexpr (FMT == codec::FmtUInt8)
+        if constexpr (FMT == codec::FmtUInt8 && !SHIFT)
         {
             for (uint32_t c = threadIdx.x; c < 256; c += BLOCK)
             {
@@ -442,7 +449,13 @@ namespace hipk
                 atomicAdd(reinterpret_cast<uint32_t*>(cLane + (b << rowShift)), 1u);
         };
         auto count8 = [&](uint32_t const (&c)[8]) {
-            if constexpr (FMT == codec::FmtUInt8)
+            if constexpr (SHIFT)
+            {
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    add(c[j] >> h.binShift);
+            }
+            else if constexpr (FMT == codec::FmtUInt8)
             {
 #pragma unroll
                 for (int j = 0; j < 8; ++j)
@@ -528,7 +541,8 @@ namespace hipk
     // lane and minCombine/maxCombine (index tie-break) keep it across lanes: arg indices are
     // exact whatever the schedule.  Sums accumulate per lane in double, then the fixed
     // shuffle / LDS / partials tree (deterministic for a given grid).
-    template <int PASS, int FMT, bool CONTIG>
+    // UNIT: the mapping is the unit mapping (+0, 1), decode without the lerp (codec::decodeUnit).
+    template <int PASS, int FMT, bool CONTIG, bool UNIT = false>
     __global__ __launch_bounds__(kBlock) void aggregatesFastKernel(FastHistArgs h, float const* meanPtr,
                                                                   float meanValue, vktHipAggregatePartial_t* partials)
     {
@@ -557,7 +571,7 @@ namespace hipk
 #pragma unroll
             for (int j = 0; j < 8; ++j)
             {
-                float const v = codec::decode(c[j], FMT, h.lo, h.hi);
+                float const v = UNIT ? codec::decodeUnit(c[j], FMT) : codec::decode(c[j], FMT, h.lo, h.hi);
                 if constexpr (PASS == 1)
                 {
                     if (v < p.minValue || v > p.maxValue)   // rare after the first voxels
@@ -713,6 +727,15 @@ namespace hipk
         return true;
     }
 
+    // fastBin of a UInt8 code, evaluated on the host with the kernel's float operations
+    uint64_t hostBinU8(uint32_t c, float lo, float hi, float scale, float nbf, uint64_t nb)
+    {
+        volatile float v = codec::decode(c, codec::FmtUInt8, lo, hi);
+        volatile float d = v - lo;
+        volatile float f = d * scale;
+        return (f > -1.0f && f < nbf) ? static_cast<uint64_t>(static_cast<int32_t>(f)) : nb;
+    }
+
     // Launches histogramFastKernel when the range qualifies (see its comment); false otherwise.
     bool launchFastHistogram(BoxArgs const& a, HistArgs const& hh, hipStream_t s)
     {
@@ -731,6 +754,24 @@ namespace hipk
         h.nb = static_cast<uint32_t>(hh.numBins);
         h.nbf = static_cast<float>(hh.numBins);
         h.bins = hh.bins;
+        // integer bins (SHIFT, see histogramFastKernel): unit mapping, numBins = 2^k, k <= 16
+        uint32_t k = 0;
+        while (k < 16 && (1ull << k) < hh.numBins)
+            ++k;
+        bool shift = fmt == codec::FmtUInt16 && codec::isUnitMapping(a.lo, a.hi) && (1ull << k) == hh.numBins &&
+                     hh.scale == static_cast<float>(hh.numBins);
+        h.binShift = 16u - k;
+        if (fmt == codec::FmtUInt8)
+        {
+            // the kernel's own bin formula for all 256 codes, on the host (Codec.hpp is shared)
+            for (uint32_t sh = 0; sh < 8 && !shift; ++sh)
+            {
+                shift = true;
+                for (uint32_t c = 0; c < 256 && shift; ++c)
+                    shift = hostBinU8(c, a.lo, a.hi, hh.scale, static_cast<float>(hh.numBins), hh.numBins) == (c >> sh);
+                h.binShift = sh;
+            }
+        }
 #define VKT_FAST_HIST(FMT, TILED, BLOCK, G, LDS)                                                                   \
     do {                                                                                                           \
         if (contig)                                                                                                \
@@ -740,7 +781,23 @@ namespace hipk
     } while (0)
 #define VKT_FAST_HIST_FMT(TILED, BLOCK, G, LDS)                                                                    \
     do {                                                                                                           \
-        if (fmt == codec::FmtUInt8) VKT_FAST_HIST(codec::FmtUInt8, TILED, BLOCK, G, LDS);                          \
+        if (fmt == codec::FmtUInt8 && shift) {                                                                     \
+            if (contig)                                                                                            \
+                hipLaunchKernelGGL((histogramFastKernel<codec::FmtUInt8, true, TILED, BLOCK, true>), dim3(G),      \
+                                   dim3(BLOCK), LDS, s, h);                                                        \
+            else                                                                                                   \
+                hipLaunchKernelGGL((histogramFastKernel<codec::FmtUInt8, false, TILED, BLOCK, true>), dim3(G),     \
+                                   dim3(BLOCK), LDS, s, h);                                                        \
+        }                                                                                                          \
+        else if (fmt == codec::FmtUInt8) VKT_FAST_HIST(codec::FmtUInt8, TILED, BLOCK, G, LDS);                     \
+        else if (shift) {                                                                                          \
+            if (contig)                                                                                            \
+                hipLaunchKernelGGL((histogramFastKernel<codec::FmtUInt16, true, TILED, BLOCK, true>), dim3(G),     \
+                                   dim3(BLOCK), LDS, s, h);                                                        \
+            else                                                                                                   \
+                hipLaunchKernelGGL((histogramFastKernel<codec::FmtUInt16, false, TILED, BLOCK, true>), dim3(G),    \
+                                   dim3(BLOCK), LDS, s, h);                                                        \
+        }                                                                                                          \
         else if (fmt == codec::FmtUInt16) VKT_FAST_HIST(codec::FmtUInt16, TILED, BLOCK, G, LDS);                   \
         else VKT_FAST_HIST(codec::FmtFloat32, TILED, BLOCK, G, LDS);                                               \
     } while (0)
@@ -794,18 +851,23 @@ namespace hipk
         bool contig;
         if (makeSpanArgs(a, h, contig))
         {
-#define VKT_AGG_FAST(PASS, FMT)                                                                                  \
+            bool const unit = codec::isUnitMapping(a.lo, a.hi);
+#define VKT_AGG_FAST_U(PASS, FMT, U)                                                                             \
     do {                                                                                                         \
         if (contig)                                                                                              \
-            hipLaunchKernelGGL((aggregatesFastKernel<PASS, FMT, true>), dim3(g), dim3(kBlock), 0, s, h, meanPtr, meanV, out); \
+            hipLaunchKernelGGL((aggregatesFastKernel<PASS, FMT, true, U>), dim3(g), dim3(kBlock), 0, s, h, meanPtr, meanV, out); \
         else                                                                                                     \
-            hipLaunchKernelGGL((aggregatesFastKernel<PASS, FMT, false>), dim3(g), dim3(kBlock), 0, s, h, meanPtr, meanV, out); \
+            hipLaunchKernelGGL((aggregatesFastKernel<PASS, FMT, false, U>), dim3(g), dim3(kBlock), 0, s, h, meanPtr, meanV, out); \
+    } while (0)
+#define VKT_AGG_FAST(PASS, FMT)                                                                                  \
+    do {                                                                                                         \
+        if (unit) VKT_AGG_FAST_U(PASS, FMT, true); else VKT_AGG_FAST_U(PASS, FMT, false);                        \
     } while (0)
 #define VKT_AGG_FAST_FMT(PASS)                                                                                   \
     do {                                                                                                         \
         if (a.fmt == codec::FmtUInt8) VKT_AGG_FAST(PASS, codec::FmtUInt8);                                       \
         else if (a.fmt == codec::FmtUInt16) VKT_AGG_FAST(PASS, codec::FmtUInt16);                                \
-        else VKT_AGG_FAST(PASS, codec::FmtFloat32);                                                              \
+        else VKT_AGG_FAST_U(PASS, codec::FmtFloat32, false);                                                     \
     } while (0)
             if (pass == 1)
                 VKT_AGG_FAST_FMT(1);
@@ -813,6 +875,7 @@ namespace hipk
                 VKT_AGG_FAST_FMT(2);
 #undef VKT_AGG_FAST_FMT
 #undef VKT_AGG_FAST
+#undef VKT_AGG_FAST_U
             return;
         }
         if (pass == 1)
