@@ -289,20 +289,30 @@ namespace hipk
     // stream-ordered H2D copy on the compute stream.  Both are reused only after the previous
     // decomposition's kernel finished (event recorded behind it), so a caller that switches
     // the compute stream between calls cannot race the table.
+    // A ring of kDescSlots tables: call n waits only for call n - kDescSlots, so the host
+    // planning of the next decomposition (tens of thousands of descriptors for 32^3 bricks of
+    // a 1024^3 volume) overlaps the kernel of the previous one instead of idling the GPU.
     struct DescTable
     {
-        std::mutex m;
         BrickDesc* host = nullptr;
         BrickDesc* dev = nullptr;
         size_t cap = 0;
         hipEvent_t done = nullptr;
         bool pending = false;
     };
+    constexpr int kDescSlots = 3;
 
-    DescTable& descTable()
+    struct DescRing
     {
-        static DescTable t;
-        return t;
+        std::mutex m;
+        DescTable slot[kDescSlots];
+        int next = 0;
+    };
+
+    DescRing& descRing()
+    {
+        static DescRing r;
+        return r;
     }
 
 } // hipk
@@ -324,14 +334,59 @@ vktError vktHipBrickDecompose(vktHipVolumeView_t source, vktHipBrickRange_t cons
     if (source.dimX <= 0 || source.dimY <= 0 || source.dimZ <= 0)
         return rt::fail("vktHipBrickDecompose: empty source volume");
 
-    // validate everything before the first launch (reference: out-of-range writes are UB)
-    std::vector<BrickDesc> fast;
-    std::vector<int32_t> slow;
-    fast.reserve(static_cast<size_t>(numBricks));
-    uint32_t maxItems = 0;
     uint32_t const bpv = codec::bytesPerVoxel(source.dataFormat);
     if (bpv != 1 && bpv != 2 && bpv != 4)
         return rt::fail("vktHipBrickDecompose: unsupported data format");
+    // The descriptors are written straight into the pinned staging table of the next ring
+    // slot (held under the ring lock until the launch), validating everything before the first
+    // launch (reference: out-of-range writes are UB).
+    DescRing& ring = descRing();
+    std::unique_lock<std::mutex> lock(ring.m);
+    DescTable& st = ring.slot[ring.next];
+    if (st.pending)
+    {
+        VKT_HIP_TRY(hipEventSynchronize(st.done));
+        st.pending = false;
+    }
+    size_t const need = static_cast<size_t>(numBricks);
+    if (st.cap < need)
+    {
+        if (st.host)
+            VKT_HIP_TRY(hipHostFree(st.host));
+        if (st.dev)
+            VKT_HIP_TRY(hipFree(st.dev));
+        st.host = nullptr;
+        st.dev = nullptr;
+        st.cap = 0;
+        VKT_HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&st.host), need * sizeof(BrickDesc)));
+        VKT_HIP_TRY(hipMalloc(reinterpret_cast<void**>(&st.dev), need * sizeof(BrickDesc)));
+        st.cap = need;
+    }
+    if (!st.done)
+        VKT_HIP_TRY(hipEventCreateWithFlags(&st.done, hipEventDisableTiming));
+    BrickDesc* const fast = st.host;
+    size_t nFast = 0;
+    std::vector<int32_t> slow;
+    uint32_t maxItems = 0;
+    // bricks of a decomposition share a few sizes: reuse the last divisor of each kind (each
+    // makeFastDiv costs a 64-bit division; 32^3 bricks of 1024^3 are 32 768 descriptors)
+    struct LastDiv
+    {
+        FastDiv f{0u, 0u, 0u};
+        bool valid = false;
+        FastDiv operator()(uint32_t d)
+        {
+            if (!valid || f.d != d)
+            {
+                f = makeFastDiv(d);
+                valid = true;
+            }
+            return f;
+        }
+    } divSeg, divX, divWpr, divY;
+    int64_t const V = 16 / bpv;                            // voxels per 16-B segment
+    uint32_t const vShift = bpv == 1 ? 4u : bpv == 2 ? 3u : 2u;
+    bool const srcAligned = source.dimX >= V && reinterpret_cast<uintptr_t>(source.data) % 16 == 0;
     for (int32_t i = 0; i < numBricks; ++i)
     {
         vktHipBrickRange_t const& br = bricks[i];
@@ -353,72 +408,48 @@ vktError vktHipBrickDecompose(vktHipVolumeView_t source, vktHipBrickRange_t cons
             slow.push_back(i);
             continue;
         }
-        BrickDesc d{};
+        BrickDesc& d = fast[nFast++];
+        d = BrickDesc{};
         d.dst = br.brick.data;
         d.dimX = br.brick.dimX;
         d.dimY = br.brick.dimY;
         d.fx = br.first.x;
         d.fy = br.first.y;
         d.fz = br.first.z;
-        int64_t const V = 16 / bpv;
-        uint32_t const seg = static_cast<uint32_t>((nx + V - 1) / V);   // 16-B segments per row
+        uint32_t const seg = static_cast<uint32_t>((nx + V - 1) >> vShift);   // 16-B segments per row
         d.nx = static_cast<int32_t>(nx);
         d.nvox = static_cast<uint32_t>(nv);
-        d.linear = nx == br.brick.dimX && ny == br.brick.dimY && nx >= V &&
-                   source.dimX >= V && reinterpret_cast<uintptr_t>(source.data) % 16 == 0 &&
+        d.linear = nx == br.brick.dimX && ny == br.brick.dimY && nx >= V && srcAligned &&
                    reinterpret_cast<uintptr_t>(br.brick.data) % 16 == 0;
-        d.nitems = d.linear ? static_cast<uint32_t>((nv + V - 1) / V) : static_cast<uint32_t>(ny * nz) * seg;
-        d.fseg = makeFastDiv(seg);
-        d.fdx = makeFastDiv(static_cast<uint32_t>(nx));
+        d.nitems = d.linear ? static_cast<uint32_t>((nv + V - 1) >> vShift) : static_cast<uint32_t>(ny * nz) * seg;
+        d.fseg = divSeg(seg);
+        d.fdx = divX(static_cast<uint32_t>(nx));
         {
             int64_t const span = std::min<int64_t>(br.first.x + nx, source.dimX) - std::max<int32_t>(br.first.x, 0);
-            d.fwpr = makeFastDiv(span > 0 ? static_cast<uint32_t>((span * bpv + 15) / 16 + 1) : 0u);
+            d.fwpr = divWpr(span > 0 ? static_cast<uint32_t>((span * bpv + 15) / 16 + 1) : 0u);
         }
-        d.fdy = makeFastDiv(static_cast<uint32_t>(ny));
+        d.fdy = divY(static_cast<uint32_t>(ny));
         maxItems = d.nitems > maxItems ? d.nitems : maxItems;
-        fast.push_back(d);
     }
 
     hipStream_t s = rt::computeStream();
-    if (!fast.empty())
+    if (nFast > 0)
     {
         uint64_t const chunks = (maxItems + kBrickChunk - 1) / kBrickChunk;
-        uint64_t const blocks = chunks * fast.size();
+        uint64_t const blocks = chunks * nFast;
         if (blocks >= (1ull << 32))
             return rt::fail("vktHipBrickDecompose: too many bricks for one launch");
-        DescTable& st = descTable();
-        std::lock_guard<std::mutex> lock(st.m);
-        if (st.pending)
-        {
-            VKT_HIP_TRY(hipEventSynchronize(st.done));
-            st.pending = false;
-        }
-        if (st.cap < fast.size())
-        {
-            if (st.host)
-                VKT_HIP_TRY(hipHostFree(st.host));
-            if (st.dev)
-                VKT_HIP_TRY(hipFree(st.dev));
-            st.host = nullptr;
-            st.dev = nullptr;
-            st.cap = 0;
-            VKT_HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&st.host), fast.size() * sizeof(BrickDesc)));
-            VKT_HIP_TRY(hipMalloc(reinterpret_cast<void**>(&st.dev), fast.size() * sizeof(BrickDesc)));
-            st.cap = fast.size();
-        }
-        if (!st.done)
-            VKT_HIP_TRY(hipEventCreateWithFlags(&st.done, hipEventDisableTiming));
-        std::copy(fast.begin(), fast.end(), st.host);
+        ring.next = (ring.next + 1) % kDescSlots;
         BrickDesc* dev = st.dev;
-        VKT_HIP_TRY(hipMemcpyAsync(dev, st.host, fast.size() * sizeof(BrickDesc), hipMemcpyHostToDevice, s));
+        VKT_HIP_TRY(hipMemcpyAsync(dev, st.host, nFast * sizeof(BrickDesc), hipMemcpyHostToDevice, s));
         FastDiv const fdc = makeFastDiv(static_cast<uint32_t>(chunks));
         // group = the run of leading bricks with the same y/z box (one brick row of an
         // Array3D).  Any group size dividing the brick count maps blocks 1:1 onto (brick,
         // chunk); it only changes the order in which bricks are visited.
         size_t run = 1;
-        while (run < fast.size() && fast[run].fy == fast[0].fy && fast[run].fz == fast[0].fz)
+        while (run < nFast && fast[run].fy == fast[0].fy && fast[run].fz == fast[0].fz)
             ++run;
-        FastDiv const fdg = makeFastDiv(static_cast<uint32_t>(fast.size() % run == 0 ? run : 1));
+        FastDiv const fdg = makeFastDiv(static_cast<uint32_t>(nFast % run == 0 ? run : 1));
         unsigned const g = static_cast<unsigned>(blocks);
         if (bpv == 1)
             hipLaunchKernelGGL(brickCopyKernel<1>, dim3(g), dim3(kBlock), 0, s, dev, fdc, fdg, source.data, source.dimX,
@@ -433,6 +464,7 @@ vktError vktHipBrickDecompose(vktHipVolumeView_t source, vktHipBrickRange_t cons
         VKT_HIP_TRY(hipEventRecord(st.done, s));
         st.pending = true;
     }
+    lock.unlock();
     // bricks that need the unmap -> map conversion: one CopyRange each
     for (int32_t i : slow)
     {

@@ -44,9 +44,7 @@ namespace hipk
         FastDiv f{d, 0u, 0u};
         if (d == 0)
             return f;
-        uint32_t l = 0;
-        while ((1ull << l) < d)
-            ++l;
+        uint32_t const l = d <= 1 ? 0u : 32u - static_cast<uint32_t>(__builtin_clz(d - 1));   // ceil(log2 d)
         f.l = l;
         f.m = static_cast<uint32_t>(((1ull << 32) * ((1ull << l) - d)) / d + 1);
         return f;
