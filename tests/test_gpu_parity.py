@@ -362,3 +362,31 @@ def test_resample_chain_sparse_specials(g, o, dfmt):
                 out = g.resample(dfmt, dmap, dd, 7, (0.0, 1.0), src, 1)
                 ref = o.resample(dfmt, dmap, dd, 7, (0.0, 1.0), src, 1)
                 assert_codes_equal(out, ref, dfmt, f"chain {sd}->{dd} specials={specials} dmap={dmap}")
+
+
+@pytest.mark.parametrize("dfmt", [7, 5])
+def test_resample_chain_downsampling_unstaged_rows(g, o, dfmt):
+    """Float32 "Linear" when downsampling: the optimistic LDS gather flags only the source rows
+    it stages, and rowDirtyUnstagedKernel classifies the rows no task stages.  16 -> 12 per axis
+    stages y, z in {0,1,2,4,5,6,8,9,10,12,13,14}: specials in the skipped rows 3, 7, 11, 15 are
+    only reachable through the y+1 / z+1 neighbours of a staged row."""
+    rng = np.random.default_rng(7 + dfmt)
+    for sd, dd in (((16, 16, 16), (12, 12, 12)), ((64, 24, 20), (48, 18, 15)), ((32, 16, 16), (16, 12, 12))):
+        sx, sy, sz = sd
+        vals = rng.uniform(0.0, 1.0, size=(sz, sy, sx)).astype(np.float32)
+        cases = [
+            [((1, 3, 5), np.nan)],                          # skipped y row of a staged plane
+            [((7, 5, 0), np.inf)],                          # skipped plane, first voxel of a row
+            [((3, 3, sx - 1), -np.inf)],                    # skipped row and plane, row end
+            [((sz - 1, sy - 1, sx - 1), -0.0)],             # last voxel (clamped neighbours)
+            [((2, 2, 3), np.nan), ((11, 7, 1), -0.0)],      # staged row + skipped row
+        ]
+        for specials in cases:
+            v = vals.copy()
+            for (z, y, x), val in specials:
+                v[z, y, x] = val
+            src = v.view(np.uint32)
+            for dmap in ((0.0, 1.0), (-1.0, 3.0)):
+                out = g.resample(dfmt, dmap, dd, 7, (0.0, 1.0), src, 1)
+                ref = o.resample(dfmt, dmap, dd, 7, (0.0, 1.0), src, 1)
+                assert_codes_equal(out, ref, dfmt, f"down {sd}->{dd} specials={specials} dmap={dmap}")

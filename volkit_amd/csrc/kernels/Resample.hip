@@ -333,6 +333,33 @@ namespace hipk
             dirty[row] = any != 0;
     }
 
+    // rowDirtyKernel over the local rows NO task stages (staged[y] && staged[sdy + global z]
+    // skipped): the optimistic LDS gather flags the rows it stages itself, so together every
+    // row a chain can read is classified with one read of each source row.
+    __global__ __launch_bounds__(kBlock) void rowDirtyUnstagedKernel(uint8_t const* src, int32_t sdx, int32_t sdy,
+                                                                     uint64_t rows, int32_t srcZ0, uint8_t const* staged,
+                                                                     uint8_t* dirty)
+    {
+        int const lane = threadIdx.x & 63;
+        uint64_t const row = static_cast<uint64_t>(blockIdx.x) * (kBlock / 64) + (threadIdx.x >> 6);
+        if (row >= rows)
+            return;
+        uint32_t const z = static_cast<uint32_t>(row / static_cast<uint64_t>(sdy));
+        uint32_t const y = static_cast<uint32_t>(row - static_cast<uint64_t>(z) * static_cast<uint64_t>(sdy));
+        if (staged[y] && staged[static_cast<uint32_t>(sdy) + static_cast<uint32_t>(srcZ0) + z])
+            return;
+        uint32_t const* p = reinterpret_cast<uint32_t const*>(src) + row * static_cast<uint64_t>(sdx);
+        bool d = false;
+        for (int32_t x = 4 * lane; x < sdx; x += 256)
+        {
+            u32x4 v = __builtin_nontemporal_load(reinterpret_cast<u32x4 const*>(p + x));
+            d = d || chainSensitive(v.x) || chainSensitive(v.y) || chainSensitive(v.z) || chainSensitive(v.w);
+        }
+        uint64_t const any = __ballot(d);
+        if (lane == 0)
+            dirty[row] = any != 0;
+    }
+
     // rowChain[r] = OR of rowDirty over the rows the chain of row r's voxels reads:
     // (y,z), (y+1,z), (y,z+1), (y+1,z+1) -- y+1 / z+1 clamped like sampleLinear -- and the
     // row after each in memory (hi.x of the last voxel).  Indices are clamped into the local
@@ -398,6 +425,7 @@ namespace hipk
         Run const* runsZ = nullptr;
         int32_t const* xtab = nullptr;
         int32_t const* zsrc = nullptr;   // source plane of every local dst plane
+        uint8_t const* staged = nullptr; // sdy bytes (y) then sgz bytes (global z): 1 = a task reads it
         bool yAllRows = false;           // the y runs read every source row 0..sdy-1, in order
         bool zContiguous = false;        // the z runs read consecutive source planes
         int32_t aff[2][6] = {{0, 0, 0, 0, 0, 0}, {0, 0, 0, 0, 0, 0}};   // {aff, sa, da, dl, s0, d0}
@@ -490,6 +518,18 @@ namespace hipk
         t.runsY = reinterpret_cast<Run const*>(t.dev + xwords);
         t.runsZ = reinterpret_cast<Run const*>(t.dev + xwords + 3 * ry.size());
         t.zsrc = t.dev + xwords + 3 * ry.size() + 3 * rz.size();
+        {
+            // rows the tasks stage (the optimistic Float32 Linear gather flags those itself)
+            std::vector<uint8_t> st(static_cast<size_t>(sdy) + static_cast<size_t>(sgz), 0);
+            for (Run const& r : ry)
+                st[static_cast<size_t>(r.s)] = 1;
+            for (Run const& r : rz)
+                st[static_cast<size_t>(sdy) + static_cast<size_t>(r.s)] = 1;
+            uint8_t* d = nullptr;
+            VKT_HIP_TRY(hipMalloc(&d, st.size()));
+            VKT_HIP_TRY(hipMemcpy(d, st.data(), st.size(), hipMemcpyHostToDevice));
+            t.staged = d;
+        }
         cache[{dev, key}] = t;
         out = t;
         return vktNoError;
@@ -867,30 +907,22 @@ namespace hipk
             static rt::StreamScratch scratch;
             uint64_t const srcRows = static_cast<uint64_t>(src.dimY) * static_cast<uint64_t>(src.dimZ);
             uint8_t* dirty = static_cast<uint8_t*>(scratch.acquire(2 * srcRows, s));
-            // Optimistic variant when the tasks stage every source row of planes [minSz,
-            // maxSz] (y runs read every row, z runs consecutive planes): the gather itself flags
-            // the rows it stages, the local planes above maxSz (z+1 halo) are scanned, then
-            // rowChainKernel and a fix-up pass over the flagged tasks -- no pre-pass read of
-            // the source (768^3 -> 1024^3 Float32 Linear: see DESIGN.md §4.2b)
-            if (dirty && t.yAllRows && t.zContiguous && gatherLdsEnabled())
+            // Optimistic variant: the LDS gather flags the rows it stages itself, the local rows
+            // no task stages (skipped rows when downsampling, the z+1 halo planes) are scanned
+            // (rowDirtyUnstagedKernel), then rowChainKernel and a fix-up pass over the flagged
+            // tasks -- every source row is read once (768^3 -> 1024^3 and 1024^3 -> 768^3
+            // Float32 Linear: see DESIGN.md §4.2b)
+            if (dirty && t.staged && src.dimX % 4 == 0 && gatherLdsEnabled())
             {
                 ResampleArgs b = a;
                 b.rowDirtyOut = dirty;
                 b.rowChain = dirty + srcRows;
                 bool ok = hipMemsetAsync(dirty, 0, srcRows, s) == hipSuccess;
-                int32_t const above = t.maxSz + 1 - a.srcZ0;   // first local plane above the task planes
-                if (ok && above < src.dimZ)
+                if (ok)
                 {
-                    uint64_t const row0 = static_cast<uint64_t>(above > 0 ? above : 0) * static_cast<uint64_t>(src.dimY);
-                    uint64_t const nrows = srcRows - row0;
-                    unsigned const gd = static_cast<unsigned>((nrows + kBlock / 64 - 1) / (kBlock / 64));
-                    uint8_t const* base = src.data + row0 * static_cast<uint64_t>(src.dimX) * 4u;
-                    if (src.dimX % 4 == 0)
-                        hipLaunchKernelGGL(rowDirtyKernel<true>, dim3(gd), dim3(kBlock), 0, s, base, src.dimX, nrows,
-                                           dirty + row0);
-                    else
-                        hipLaunchKernelGGL(rowDirtyKernel<false>, dim3(gd), dim3(kBlock), 0, s, base, src.dimX, nrows,
-                                           dirty + row0);
+                    unsigned const gd = static_cast<unsigned>((srcRows + kBlock / 64 - 1) / (kBlock / 64));
+                    hipLaunchKernelGGL(rowDirtyUnstagedKernel, dim3(gd), dim3(kBlock), 0, s, src.data, src.dimX,
+                                       src.dimY, srcRows, a.srcZ0, t.staged, dirty);
                 }
                 if (ok && launchGatherLds(b, bs, bd, identity, false, tasks, s, true))
                 {
