@@ -117,6 +117,38 @@ namespace hipk
         }
     };
 
+    // UInt8 codes with the unit mapping on all three volumes: the same IEEE operations as
+    // ArithF<OP, UInt8, UInt8, UInt8, 3> (t = c * kInv255999, the op, * 255.999f, truncate), with
+    // what the value ranges make redundant dropped: t in [0, 1), so Sum / Prod / SafeSum /
+    // SafeProd results are >= +0 and Diff-type results are in (-1, 1) and never -0 (x - x = +0);
+    // hence the reference clamp max(0, min(x, 1)) is min(x, 1) for SafeSum, max(x, 0) for
+    // SafeDiff and the identity for SafeAbsDiff / SafeProd, and |x * 255.999f| < 512 makes the
+    // x86 cvttss2si range check dead (plain v_cvt_i32_f32).  Quot / SafeQuot (inf, NaN) keep
+    // ArithF.  Checked against the oracle on every code pair.
+    template <int OP>
+    struct UnitArithU8F
+    {
+        __device__ __forceinline__ uint32_t operator()(uint32_t a, uint32_t b) const
+        {
+            float const x = static_cast<float>(a & 0xFFu) * codec::kInv255999;
+            float const y = static_cast<float>(b & 0xFFu) * codec::kInv255999;
+            float r;
+            if constexpr (OP == vktHipOpSum) r = x + y;
+            else if constexpr (OP == vktHipOpDiff) r = x - y;
+            else if constexpr (OP == vktHipOpProd || OP == vktHipOpSafeProd) r = x * y;
+            else if constexpr (OP == vktHipOpAbsDiff || OP == vktHipOpSafeAbsDiff) r = fabsf(x - y);
+            else if constexpr (OP == vktHipOpSafeSum) r = fminf(x + y, 1.0f);
+            else r = fmaxf(x - y, 0.0f);   // SafeDiff
+            return static_cast<uint32_t>(static_cast<int32_t>(r * 255.999f)) & 0xFFu;
+        }
+    };
+
+    template <int OP>
+    constexpr bool hasUnitArithU8()
+    {
+        return OP != vktHipOpQuot && OP != vktHipOpSafeQuot;
+    }
+
     template <int OP>
     constexpr bool hasIntArithU16()
     {
@@ -159,6 +191,9 @@ namespace hipk
             if constexpr (hasIntArithU16<OP>())
                 if (fd == codec::FmtUInt16 && unit)
                     return launchPointwise<2, 2>(p, IntArithU16F<OP>{}, s);
+            if constexpr (hasUnitArithU8<OP>())
+                if (fd == codec::FmtUInt8 && unit)
+                    return launchPointwise<2, 1>(p, UnitArithU8F<OP>{}, s);
             if (fd == codec::FmtUInt16)
                 VKT_ARITH_FIXED(codec::FmtUInt16, 2);
             if (fd == codec::FmtUInt8)
