@@ -254,6 +254,12 @@ def main():
             "sample": f"oracle restatement of the reference serial path, Resample {args.cpu_dst // 2}^3->"
                       f"{args.cpu_dst}^3 UInt16 Linear + SumRange {args.cpu_dst}^3, {dt:.1f} s, 1 thread of "
                       f"{os.cpu_count()} host CPUs",
+            # the compiled reference serial path, measured in the survey container
+            # (1 thread, g++ -O2): SumRange UInt16 33.8-37.9 ns/voxel + Resample UInt16 Linear 41.5
+            # ns/dst voxel -> ~75-79 ns per pipeline voxel.  Not re-measured here (the reference
+            # does not travel to the GPU box); the port above skips its per-voxel migrate().
+            "reference_equivalent": {"value": round(1.0 / ((33.8e-9 + 37.9e-9) / 2 + 41.5e-9) / 1e9, 5), "unit": "Gvoxels/s",
+                                     "basis": "BASELINE.md §2 survey probe, 1 core, not re-measured"},
         }
     if rank == 0:
         print(json.dumps(out), flush=True)
