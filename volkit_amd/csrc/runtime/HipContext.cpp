@@ -5,6 +5,8 @@
 // stream ids) as the vktHip* runtime functions of include/volkit_hip.h.
 
 #include "Runtime.hpp"
+
+#include <rocprofiler-sdk-roctx/roctx.h>
 #include "volkit_hip.h"
 
 #include <atomic>
@@ -175,9 +177,12 @@ namespace rt
 
     bool kernelTimingEnabled() { return ctx().timing.load() != 0; }
 
+    // Every backend call is also a roctx range named after the reference's backend function
+    // (e.g. "SumRange_hip"), so `rocprofv3 --marker-trace` attributes kernels to API calls.
     ScopedKernelTimer::ScopedKernelTimer(char const* name, bool log)
         : name_(name), active_(log || kernelTimingEnabled()), log_(log)
     {
+        roctxRangePushA(name);
         if (!active_)
             return;
         hipStream_t s = computeStream();
@@ -191,6 +196,10 @@ namespace rt
 
     ScopedKernelTimer::~ScopedKernelTimer()
     {
+        struct Pop
+        {
+            ~Pop() { roctxRangePop(); }
+        } pop;
         if (!active_)
             return;
         (void)hipEventRecord(stop_, computeStream());
