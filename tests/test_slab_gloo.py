@@ -25,6 +25,8 @@ CASES = [
     (3, (10, 9, 37), (7, 6, 64), 4, 0, False),     # non-integer z ratio, uneven slabs
     (3, (10, 9, 37), (7, 6, 64), 7, 1, True),
     (2, (8, 8, 40), (8, 8, 13), 7, 1, True),       # downsampling
+    (4, (12, 10, 21), (12, 10, 50), 7, 1, True),   # 4 ranks, uneven slabs, Float32 chain halos
+    (8, (8, 6, 16), (16, 12, 32), 7, 1, True),     # 8 ranks (the node's GPU count), 2x
 ]
 
 
