@@ -36,13 +36,19 @@ namespace hipk
         uint64_t const fixTasks = static_cast<uint64_t>(a.nRunsY) * a.nRunsZ;
         unsigned const gs = static_cast<unsigned>((fixTasks + 255) / 256);
         unsigned const gf = 2048;   // drains the work list (exits at once when it is empty)
-#define VKT_OPT(B, K)                                                                                           \
+#define VKT_OPT_F(B, K, FD)                                                                                     \
     do {                                                                                                        \
         planeChunks(a, tasks, [&](ResampleArgs const& c, unsigned g) {                                         \
-            hipLaunchKernelGGL((resamplePlaneKernel<4, B, K, 3, codec::FmtFloat32, -1>), dim3(g), dim3(64), 0, s, c); \
+            hipLaunchKernelGGL((resamplePlaneKernel<4, B, K, 3, codec::FmtFloat32, FD>), dim3(g), dim3(64), 0, s, c); \
         });                                                                                                     \
         hipLaunchKernelGGL(resampleFixupScanKernel, dim3(gs), dim3(256), 0, s, a, list);                     \
         hipLaunchKernelGGL((resampleFixupKernel<B, K>), dim3(gf), dim3(64), 0, s, a, list);                   \
+    } while (0)
+    // Float32 destinations (config 3) get the encode with the format fixed at compile time
+#define VKT_OPT(B, K)                                                                                           \
+    do {                                                                                                        \
+        if (B == 4 && a.fd == codec::FmtFloat32) VKT_OPT_F(B, K, codec::FmtFloat32);                            \
+        else VKT_OPT_F(B, K, -1);                                                                               \
     } while (0)
 #define VKT_OPT_K(B)                            \
     do {                                        \
@@ -58,6 +64,7 @@ namespace hipk
             VKT_OPT_K(1);
 #undef VKT_OPT_K
 #undef VKT_OPT
+#undef VKT_OPT_F
     }
 } // hipk
 } // vkt
