@@ -25,7 +25,7 @@ def load(pattern, counter):
 
 
 def short(name):
-    for key, label in (("ArithF<0, 5, 5, 5", "SumRange(UInt16)"), ("resamplePlaneKernel", "Resample(replicate)"), ("resampleRowKernel", "Resample(replicate)"), ("resampleRepKernel", "Resample(replicate)"),
+    for key, label in (("ArithF<0, 5, 5, 5", "SumRange(UInt16)"), ("IntArithU16F<0>", "SumRange(UInt16)"), ("resamplePlaneKernel", "Resample(replicate)"), ("resampleRowKernel", "Resample(replicate)"), ("resampleRepKernel", "Resample(replicate)"),
                        ("synthKernel", "Synthesize")):
         if key in name:
             return label

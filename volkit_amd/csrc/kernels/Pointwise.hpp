@@ -15,6 +15,8 @@
 #pragma once
 
 #include "KernelCommon.hpp"
+
+#include <type_traits>
 #include "volkit_c.h"
 
 namespace vkt
@@ -81,17 +83,34 @@ namespace hipk
     // flight (all loads issued before the first store), and uses nontemporal loads and
     // stores: every byte is touched once.
     //
-    // Quantum per workgroup: ONE wave, 32 B of every operand per lane (two 16-B items for
-    // UInt16, four 8-B items for UInt8, one 32-B item for Float32) = 2 KiB per operand.
-    // Measured on MI355X for the 3-stream UInt16 Sum at 1024^3 (tools/kbench7.hip,
-    // kbench9.hip, after clocks settle): 0.98-0.99 ms (6.5 TB/s) against 1.01-1.08 ms for
-    // the former 4 waves x 4 items (16 KiB per operand): small one-shot workgroups keep more
-    // distinct DRAM pages in flight per CU while the moving window stays compact.
+    // Quantum per workgroup: ONE wave.  First measured for the 3-stream UInt16 Sum at 1024^3
+    // (tools/kbench7.hip, kbench9.hip): 2 KiB per operand ran 0.98-0.99 ms (6.5 TB/s) against
+    // 1.01-1.08 ms for 4 waves x 4 items (16 KiB per operand): small one-shot workgroups keep
+    // more distinct DRAM pages in flight per CU while the moving window stays compact.
+    //
+    // Quantum size per stream count, measured with tools/kbench_fill.hip on 2 GiB buffers
+    // (MI355X, one-wave workgroups, 16-B nontemporal accesses): pure stores run best at 4 KiB
+    // per workgroup (6.4-6.5 TB/s vs 5.1-5.3 at 2 KiB and 5.7-5.9 at 8 KiB); copies and the
+    // 3-stream sum at 1 KiB of each stream (copy 6.82 vs 6.55 TB/s at 2 KiB, sum 6.34 vs 6.14).
+    // Items are 8 voxels, so Float32 (32-B items) cannot go below 2 KiB per stream.
     constexpr int kVecBlock = 64;
-    template <int BPV>
+    template <int NS, int BPV>
     constexpr int vecUnroll()
     {
-        return BPV == 1 ? 4 : BPV == 2 ? 2 : 1;
+        if constexpr (NS == 0)
+            return BPV == 1 ? 8 : BPV == 2 ? 4 : 2;   // 4 KiB of stores
+        else
+            return BPV == 1 ? 4 : BPV == 2 ? 2 : 1;  // 2 KiB per stream
+    }
+
+    // Unroll of a launch: the 3-stream UInt16 ops over ONE collapsed row (whole volumes, the
+    // metric's SumRange) take 1 KiB per stream -- alternating-process A/B on MI355X: 1024^3
+    // SumRange 0.950-0.954 ms vs 0.968-0.984 ms at 2 KiB; strided sub-boxes ran 3-4 % slower
+    // with 1 KiB, copies (NS = 1) saw no difference, so everything else keeps vecUnroll.
+    template <int NS, int BPV>
+    constexpr int vecUnrollOneRow()
+    {
+        return NS == 2 && BPV == 2 ? 1 : vecUnroll<NS, BPV>();
     }
 
     // MODE 0: one collapsed row; 1: rows, 32-bit magic division; 2: rows, 64-bit division.
@@ -142,11 +161,11 @@ namespace hipk
     template <class F>
     struct IsPacked16<F, decltype(void(F::kPacked16))> { static constexpr bool value = F::kPacked16; };
 
-    template <int NS, int BPV, int MODE, class F>
+    template <int NS, int BPV, int MODE, int U, class F>
     __device__ __forceinline__ void pointwiseVecSpan(Operand const& d, Operand const& s1, Operand const& s2,
                                                      Geom const& g, uint64_t beg, uint64_t end, F const& f)
     {
-        constexpr int kUnroll = vecUnroll<BPV>();
+        constexpr int kUnroll = U;
         constexpr uint64_t kQ = static_cast<uint64_t>(kVecBlock) * kUnroll;
         uint64_t it = beg + threadIdx.x;
         if constexpr (BPV == 2 && NS == 2 && IsPacked16<F>::value)
@@ -241,7 +260,7 @@ namespace hipk
     // handled by the first launch only.
     constexpr uint64_t kMaxQuantaPerLaunch = 1ull << 20;
 
-    template <int NS, int BPV, class F>
+    template <int NS, int BPV, int U, class F>
     __global__ __launch_bounds__(kVecBlock) void pointwiseVecKernel(Operand d, Operand s1, Operand s2, Geom g, F f,
                                                                    uint64_t qBase, uint64_t qEnd, int32_t edges)
     {
@@ -249,17 +268,17 @@ namespace hipk
         uint64_t const rows = static_cast<uint64_t>(g.vny) * static_cast<uint64_t>(g.vnz);
         uint64_t const items = cpr * rows;
         uint64_t const ny = static_cast<uint64_t>(g.vny);
-        constexpr uint64_t kQ = static_cast<uint64_t>(kVecBlock) * vecUnroll<BPV>();
+        constexpr uint64_t kQ = static_cast<uint64_t>(kVecBlock) * U;
         for (uint64_t q = qBase + blockIdx.x; q < qEnd && q * kQ < items; q += gridDim.x)
         {
             uint64_t const beg = q * kQ;
             uint64_t const end = beg + kQ < items ? beg + kQ : items;
             if (rows == 1)
-                pointwiseVecSpan<NS, BPV, 0>(d, s1, s2, g, beg, end, f);
+                pointwiseVecSpan<NS, BPV, 0, U>(d, s1, s2, g, beg, end, f);
             else if (g.fast32)
-                pointwiseVecSpan<NS, BPV, 1>(d, s1, s2, g, beg, end, f);
+                pointwiseVecSpan<NS, BPV, 1, U>(d, s1, s2, g, beg, end, f);
             else
-                pointwiseVecSpan<NS, BPV, 2>(d, s1, s2, g, beg, end, f);
+                pointwiseVecSpan<NS, BPV, 2, U>(d, s1, s2, g, beg, end, f);
         }
 
         // scalar edges of every row: head [0, vhead) and tail [vnx8, vnx)
@@ -339,25 +358,32 @@ namespace hipk
         {
             if (p.vec && p.bpv == BPV)
             {
-                uint64_t items = static_cast<uint64_t>(p.g.vny) * static_cast<uint64_t>(p.g.vnz) *
-                                 static_cast<uint64_t>((p.g.vnx8 - p.g.vhead) / 8);
-                constexpr uint64_t kQ = static_cast<uint64_t>(kVecBlock) * vecUnroll<BPV>();
-                uint64_t const quanta = (items + kQ - 1) / kQ;
+                uint64_t const rows = static_cast<uint64_t>(p.g.vny) * static_cast<uint64_t>(p.g.vnz);
+                uint64_t items = rows * static_cast<uint64_t>((p.g.vnx8 - p.g.vhead) / 8);
                 // enough threads for the scalar row edges too (narrow boxes are all edge)
-                uint64_t edgeItems = static_cast<uint64_t>(p.g.vny) * static_cast<uint64_t>(p.g.vnz) *
-                                     static_cast<uint64_t>(p.g.vhead + (p.g.vnx - p.g.vnx8));
+                uint64_t edgeItems = rows * static_cast<uint64_t>(p.g.vhead + (p.g.vnx - p.g.vnx8));
                 uint64_t edgeBlocks = (edgeItems + kVecBlock - 1) / kVecBlock;
                 edgeBlocks = edgeBlocks < 4096 ? edgeBlocks : 4096;
-                uint64_t q0 = 0;
-                do
-                {
-                    uint64_t const n = quanta - q0 < kMaxQuantaPerLaunch ? quanta - q0 : kMaxQuantaPerLaunch;
-                    uint64_t const g = q0 == 0 && n < edgeBlocks ? edgeBlocks : n;
-                    hipLaunchKernelGGL((pointwiseVecKernel<NS, BPV, F>), dim3(static_cast<unsigned>(g > 0 ? g : 1)),
-                                       dim3(kVecBlock), 0, stream, p.d, p.s1, p.s2, p.g, f, q0, q0 + n,
-                                       static_cast<int32_t>(q0 == 0));
-                    q0 += n;
-                } while (q0 < quanta);
+                auto launch = [&](auto unroll) {
+                    constexpr int U = decltype(unroll)::value;
+                    constexpr uint64_t kQ = static_cast<uint64_t>(kVecBlock) * U;
+                    uint64_t const quanta = (items + kQ - 1) / kQ;
+                    uint64_t q0 = 0;
+                    do
+                    {
+                        uint64_t const n = quanta - q0 < kMaxQuantaPerLaunch ? quanta - q0 : kMaxQuantaPerLaunch;
+                        uint64_t const g = q0 == 0 && n < edgeBlocks ? edgeBlocks : n;
+                        hipLaunchKernelGGL((pointwiseVecKernel<NS, BPV, U, F>), dim3(static_cast<unsigned>(g > 0 ? g : 1)),
+                                           dim3(kVecBlock), 0, stream, p.d, p.s1, p.s2, p.g, f, q0, q0 + n,
+                                           static_cast<int32_t>(q0 == 0));
+                        q0 += n;
+                    } while (q0 < quanta);
+                };
+                constexpr int kU = vecUnroll<NS, BPV>(), kU1 = vecUnrollOneRow<NS, BPV>();
+                if (kU1 != kU && rows == 1)
+                    launch(std::integral_constant<int, kU1>{});
+                else
+                    launch(std::integral_constant<int, kU>{});
                 return vktNoError;
             }
         }
