@@ -368,10 +368,14 @@ namespace hipk
                     constexpr int U = decltype(unroll)::value;
                     constexpr uint64_t kQ = static_cast<uint64_t>(kVecBlock) * U;
                     uint64_t const quanta = (items + kQ - 1) / kQ;
+                    // the launch split counts items (kMaxQuantaPerLaunch quanta of the default
+                    // unroll): a 1024^3 SumRange stays one launch with 1-KiB quanta (A/B: one or
+                    // two launches per call ran equally fast at 1024^3 and 2048^3)
+                    constexpr uint64_t maxQ = kMaxQuantaPerLaunch * vecUnroll<NS, BPV>() / U;
                     uint64_t q0 = 0;
                     do
                     {
-                        uint64_t const n = quanta - q0 < kMaxQuantaPerLaunch ? quanta - q0 : kMaxQuantaPerLaunch;
+                        uint64_t const n = quanta - q0 < maxQ ? quanta - q0 : maxQ;
                         uint64_t const g = q0 == 0 && n < edgeBlocks ? edgeBlocks : n;
                         hipLaunchKernelGGL((pointwiseVecKernel<NS, BPV, U, F>), dim3(static_cast<unsigned>(g > 0 ? g : 1)),
                                            dim3(kVecBlock), 0, stream, p.d, p.s1, p.s2, p.g, f, q0, q0 + n,
