@@ -1,4 +1,4 @@
-// Codec.hpp -- float <-> stored-code mapping, bit-exact with the reference serial path.
+// volkit_codec.hpp -- float <-> stored-code mapping, bit-exact with the reference serial path.
 //
 // Restates MapVoxelImpl / UnmapVoxelImpl (reference src/vkt/VoxelMapping.hpp:15-95, 98-177)
 // with every implementation-defined step made explicit, so host code (gcc/clang x86-64)
@@ -19,6 +19,11 @@
 #include <hip/hip_runtime.h>
 
 #define VKT_HD __host__ __device__ __forceinline__
+// The reference rounds every f32 operation separately (x86 SSE, no FMA).  The library is
+// built with -ffp-contract=off; this header is also included by user translation units
+// (volkit_transform.hpp), where hipcc contracts a*b+c into FMAs by default, so every
+// function with a multiply feeding an add turns contraction off for its own body.
+#define VKT_NO_CONTRACT _Pragma("clang fp contract(off)")
 
 namespace vkt
 {
@@ -55,6 +60,7 @@ namespace codec
 
     VKT_HD float lerp(float a, float b, float t)
     {
+        VKT_NO_CONTRACT
         float s = 1.0f - t;
         float p = s * a;
         float q = t * b;
@@ -100,6 +106,7 @@ namespace codec
     template <int DIV = 0>
     VKT_HD float normalise(float value, MapParams const& m)
     {
+        VKT_NO_CONTRACT
         if constexpr (DIV == 3)
             return value;
         float v = value - m.lo;
@@ -117,6 +124,7 @@ namespace codec
     template <int DIV = 0>
     VKT_HD uint32_t encode(float value, int32_t fmt, MapParams const& m, bool& write)
     {
+        VKT_NO_CONTRACT
         float v = normalise<DIV>(value, m);
         write = true;
         switch (fmt)
@@ -145,6 +153,7 @@ namespace codec
     // (getValue initialises it to 0.f, src/vkt/StructuredVolume.cpp:196).
     VKT_HD float decode(uint32_t code, int32_t fmt, float lo, float hi, float prior = 0.f)
     {
+        VKT_NO_CONTRACT
         switch (fmt)
         {
         case FmtInt16:   // VoxelMapping.hpp:107-119
@@ -174,6 +183,7 @@ namespace codec
     // the four lerp operations drop out.
     VKT_HD float decodeUnit(uint32_t code, int32_t fmt, float prior = 0.f)
     {
+        VKT_NO_CONTRACT
         switch (fmt)
         {
         case FmtInt16:

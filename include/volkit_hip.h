@@ -60,6 +60,17 @@ VKTAPI const char* vktHipGetLastErrorString(void);
 VKTAPI vktError vktHipSetKernelTiming(int32_t enable);
 VKTAPI vktError vktHipGetLastKernelMs(float* ms);
 
+/* Scope for a kernel launched by the CALLER on the compute stream (used by the
+ * device-functor Transform templates of volkit_transform.hpp): Begin checks the thread
+ * policy (GPU, else vktInvalidValue), opens the roctx range and the printPerformance timer
+ * and returns the compute stream; End picks up launch errors, waits when async execution
+ * is off, and closes the scope. */
+typedef struct vktHipKernelScope_impl* vktHipKernelScope;
+VKTAPI vktError vktHipKernelScopeBegin(const char* name, vktHipKernelScope* scope, void** hipStream);
+VKTAPI vktError vktHipKernelScopeEnd(vktHipKernelScope scope);
+/* Record `message` as the calling thread's last error, log it; returns vktInvalidValue. */
+VKTAPI vktError vktHipReportError(const char* message);
+
 /* ---- memory: replaces Allocate_cuda/Free_cuda/MemsetRange_cuda
  *      (reference src/vkt/Memory_cuda.hpp:16-31) and the cudaMemcpy of src/vkt/Memory.cpp:40-75 */
 VKTAPI vktError vktHipAllocate(void** ptr, size_t size);

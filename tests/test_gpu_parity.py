@@ -198,9 +198,31 @@ def test_resample_float_bit_patterns(g, o):
 
 
 # ---- Transform -------------------------------------------------------------------------
+class _View:
+    def __init__(self, b):
+        self.bytes = b
+
+
+def _oracle_transform1(codes, fmt, first, last, op):
+    from oracle import binding as ob
+    v = ob.Volume(codes.copy(), fmt)
+    ob.transform_range1(v, first, last, lambda x, y, z, b, f, lo, hi: op(x, y, z, _View(b)))
+    return v.codes
+
+
+def _oracle_transform2(c1, c2, fmt, first, last, op):
+    from oracle import binding as ob
+    v1, v2 = ob.Volume(c1.copy(), fmt), ob.Volume(c2.copy(), fmt)
+    ob.transform_range2(v1, v2, first, last, (0, 0, 0), lambda x, y, z, b1, b2: op(x, y, z, _View(b1), _View(b2)))
+    return v1.codes, v2.codes
+
+
 def test_transform_examples(g):
-    """Unary checkerboard of reference src/examples/Arithmetic.cpp:8-21 and binary OR of
-    src/examples/CoreAlgorithms.c:20-24, through the C ABI with the GPU policy."""
+    """Host-callback Transform (the reference's function-pointer API, staged through host
+    memory under the GPU policy) vs the oracle's TransformRange_serial restatement: unary
+    checkerboard of reference src/examples/Arithmetic.cpp:8-21, binary OR of
+    src/examples/CoreAlgorithms.c:20-24, and the range form's diagonal marker
+    (CoreAlgorithms.c:14-18)."""
     vkt = g.vkt
     n = 32
 
@@ -211,28 +233,26 @@ def test_transform_examples(g):
             v.bytes[0] = 128 if ((y % 2 == z % 2 and li % 2 == 0) or (y % 2 != z % 2 and li % 2 == 1)) else 0
         return op
 
-    v1 = g.volume(np.zeros((n, n, n), np.uint8), 4, (0.0, 1.0))
-    g._run(lambda: vkt.Transform(v1, checker(3)))
-    got = v1.to_numpy()
-    z, y, x = np.meshgrid(np.arange(n), np.arange(n), np.arange(n), indexing="ij")
-    xs, ys, zs = x >> 3, y >> 3, z >> 3
-    li = zs * 1024 + ys * 32 + xs
-    exp = np.where(((ys % 2 == zs % 2) & (li % 2 == 0)) | ((ys % 2 != zs % 2) & (li % 2 == 1)), 128, 0)
-    np.testing.assert_array_equal(got, exp.astype(np.uint8))
+    for level in (3, 2):
+        v1 = g.volume(np.zeros((n, n, n), np.uint8), 4, (0.0, 1.0))
+        g._run(lambda: vkt.Transform(v1, checker(level)))
+        ref = _oracle_transform1(np.zeros((n, n, n), np.uint8), 4, (0, 0, 0), (n, n, n), checker(level))
+        np.testing.assert_array_equal(v1.to_numpy(), ref)
 
-    a = g.volume(np.random.default_rng(1).integers(0, 256, (8, 8, 8), dtype=np.uint8), 4, (0.0, 1.0))
-    b = g.volume(np.random.default_rng(2).integers(0, 256, (8, 8, 8), dtype=np.uint8), 4, (0.0, 1.0))
-    ea = a.to_numpy() | b.to_numpy()
+    ca = np.random.default_rng(1).integers(0, 256, (8, 8, 8), dtype=np.uint8)
+    cb = np.random.default_rng(2).integers(0, 256, (8, 8, 8), dtype=np.uint8)
+    a = g.volume(ca, 4, (0.0, 1.0))
+    b = g.volume(cb, 4, (0.0, 1.0))
 
     def orop(x, y, z, v1, v2):
         v1.bytes[0] |= v2.bytes[0]
         v2.bytes[0] = v1.bytes[0]
 
     g._run(lambda: vkt.Transform(a, b, orop))
-    np.testing.assert_array_equal(a.to_numpy(), ea)
-    np.testing.assert_array_equal(b.to_numpy(), ea)
+    ra, rb = _oracle_transform2(ca, cb, 4, (0, 0, 0), (8, 8, 8), orop)
+    np.testing.assert_array_equal(a.to_numpy(), ra)
+    np.testing.assert_array_equal(b.to_numpy(), rb)
 
-    # range form: diagonal marker of CoreAlgorithms.c:14-18
     c = g.volume(np.zeros((24, 24, 24), np.uint8), 4, (0.0, 1.0))
 
     def diag(x, y, z, v):
@@ -240,11 +260,8 @@ def test_transform_examples(g):
             v.bytes[0] = 0xFF
 
     g._run(lambda: vkt.TransformRange(c, 2, 2, 2, 22, 22, 22, diag))
-    got = c.to_numpy()
-    exp = np.zeros((24, 24, 24), np.uint8)
-    for i in range(2, 22):
-        exp[i, i, i] = 0xFF
-    np.testing.assert_array_equal(got, exp)
+    ref = _oracle_transform1(np.zeros((24, 24, 24), np.uint8), 4, (2, 2, 2), (22, 22, 22), diag)
+    np.testing.assert_array_equal(c.to_numpy(), ref)
 
 
 # ---- runtime semantics -------------------------------------------------------------------

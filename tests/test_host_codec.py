@@ -1,4 +1,4 @@
-"""The codec header the kernels use (volkit_amd/csrc/common/Codec.hpp), compiled for the host
+"""The codec header the kernels use (include/volkit_codec.hpp), compiled for the host
 inside libvolkit (vktMapVoxel / vktUnmapVoxel), against the oracle's restatement of
 reference src/vkt/VoxelMapping.hpp -- every code of the 8/16-bit formats and a spread of
 float inputs including the reference's traps.  CPU only."""

@@ -128,6 +128,18 @@ def main():
             ms = timed(lambda: lib.vktHipResample(Rv, S, fm), max(3, R // 3))
             report(f"config3 Resample 1024^3->2048^3 Float32 {lab}", ms, 4 * s ** 3 + 4 * e ** 3, e ** 3)
         free(S, Rv)
+    if want("transform"):
+        # device-functor Transform (include/volkit_transform.hpp) through the test fixture
+        # tests/native/libtransform_ops.so; unary algorithmic bytes 2b per voxel
+        t = C.CDLL(os.path.join(ROOT, "tests", "native", "libtransform_ops.so"))
+        t.vktt_bench_unary.argtypes = [C.c_int] * 6 + [C.POINTER(C.c_float)]
+        ms = C.c_float(0.0)
+        m = 1024
+        for op, lab, fmt, b, rw in ((2, "Diagonal", 4, 1, 2), (2, "Diagonal", 5, 2, 2), (2, "Diagonal", 7, 4, 2),
+                                    (0, "Checkered<3> (write-only: loads are dead)", 4, 1, 1)):
+            if t.vktt_bench_unary(op, m, m, m, fmt, R, C.byref(ms)) != 0:
+                raise RuntimeError(_lib.last_error())
+            report(f"Transform {lab} 1024^3 fmt={fmt}", ms.value, rw * b * m ** 3, m ** 3)
     if want("gather"):
         # non-integer ratios (gather path): up/down-sampling 768^3 <-> 1024^3, all dst formats
         cases = [(768, 1024, 5, 1), (1024, 768, 5, 1), (768, 1024, 4, 1), (768, 1024, 7, 0), (768, 1024, 7, 1),

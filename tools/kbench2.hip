@@ -8,7 +8,7 @@
 #include <vector>
 
 #include "kernels/KernelCommon.hpp"
-#include "common/Codec.hpp"
+#include "volkit_codec.hpp"
 
 using namespace vkt::hipk;
 using vkt::codec::MapParams;

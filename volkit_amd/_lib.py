@@ -188,6 +188,9 @@ SIGNATURES = {
     "vktHipGetLastErrorString": (C.c_char_p, []),
     "vktHipSetKernelTiming": (c_err, [i32]),
     "vktHipGetLastKernelMs": (c_err, [P(f32)]),
+    "vktHipKernelScopeBegin": (c_err, [C.c_char_p, P(C.c_void_p), P(C.c_void_p)]),
+    "vktHipKernelScopeEnd": (c_err, [C.c_void_p]),
+    "vktHipReportError": (c_err, [C.c_char_p]),
     "vktHipAllocate": (c_err, [P(C.c_void_p), C.c_size_t]),
     "vktHipFree": (c_err, [C.c_void_p]),
     "vktHipMemcpy": (c_err, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]),

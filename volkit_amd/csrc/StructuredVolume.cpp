@@ -10,7 +10,7 @@
 // dereferencing a device pointer on the host as the reference would.
 
 #include "runtime/Runtime.hpp"
-#include "common/Codec.hpp"
+#include "volkit_codec.hpp"
 #include "StructuredVolume_impl.hpp"
 
 namespace vkt

@@ -23,7 +23,7 @@
 
 #include "../runtime/Runtime.hpp"
 #include "../StructuredVolume_impl.hpp"
-#include "../common/Codec.hpp"
+#include "volkit_codec.hpp"
 #include "volkit_hip.h"
 
 #include <algorithm>

@@ -8,7 +8,7 @@
 #include <cstdint>
 #include <hip/hip_runtime.h>
 
-#include "../common/Codec.hpp"
+#include "volkit_codec.hpp"
 
 namespace vkt
 {

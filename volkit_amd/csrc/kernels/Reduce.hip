@@ -763,7 +763,7 @@ namespace hipk
         h.binShift = 16u - k;
         if (fmt == codec::FmtUInt8)
         {
-            // the kernel's own bin formula for all 256 codes, on the host (Codec.hpp is shared)
+            // the kernel's own bin formula for all 256 codes, on the host (volkit_codec.hpp is shared)
             for (uint32_t sh = 0; sh < 8 && !shift; ++sh)
             {
                 shift = true;

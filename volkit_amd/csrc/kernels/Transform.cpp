@@ -10,7 +10,7 @@
 // copy, so aliasing behaves exactly as in the serial loop.
 
 #include "../runtime/Runtime.hpp"
-#include "../common/Codec.hpp"
+#include "volkit_codec.hpp"
 #include "volkit_hip.h"
 
 #include <algorithm>

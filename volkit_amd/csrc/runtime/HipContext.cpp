@@ -302,4 +302,42 @@ vktError vktHipGetLastKernelMs(float* ms)
     return vktNoError;
 }
 
+// Scope for a kernel the caller launches itself on the compute stream (the device-functor
+// Transform templates of include/volkit_transform.hpp): the same policy check, roctx range,
+// printPerformance timer and launch/async handling as the library's own entry points.
+struct vktHipKernelScope_impl
+{
+    explicit vktHipKernelScope_impl(char const* n, bool log) : name(n), timer(n, log) {}
+    char const* name;
+    vkt::rt::ScopedKernelTimer timer;
+};
+
+vktError vktHipKernelScopeBegin(char const* name, vktHipKernelScope* scope, void** stream)
+{
+    if (name == nullptr || scope == nullptr || stream == nullptr)
+        return rt::fail("vktHipKernelScopeBegin: null pointer");
+    *scope = nullptr;
+    vkt::ExecutionPolicy ep = vkt::GetThreadExecutionPolicy();
+    if (ep.device != vkt::ExecutionPolicy::Device::GPU)
+        return rt::fail((std::string(name) + ": CPU execution policy (volkit-amd implements the GPU backend only; "
+                                              "set ExecutionPolicy::Device::GPU)").c_str());
+    *stream = rt::computeStream();
+    *scope = new vktHipKernelScope_impl(name, ep.printPerformance != vkt::False);
+    return vktNoError;
+}
+
+vktError vktHipKernelScopeEnd(vktHipKernelScope scope)
+{
+    if (scope == nullptr)
+        return rt::fail("vktHipKernelScopeEnd: null scope");
+    vktError e = rt::finishLaunch(scope->name);
+    delete scope;   // stops the timer, pops the roctx range
+    return e;
+}
+
+vktError vktHipReportError(char const* message)
+{
+    return rt::fail(message != nullptr ? message : "vktHipReportError");
+}
+
 } // extern "C"
