@@ -1,0 +1,116 @@
+"""MemsetRange on the GPU (replaces MemsetRange_cuda, reference src/vkt/Memory_cuda.cu:15-49;
+serial semantics src/vkt/Memory_serial.hpp:24-37): dstSize / patternSize whole copies of the
+host pattern, byte for byte, and nothing past them.  Checked against numpy's np.resize of the
+pattern (the semantics are byte-level and exact), for pattern sizes 1..300 B, destination sizes
+that are not multiples of the pattern, and unaligned destinations; plus ManagedBuffer<T>::fill
+(reference include/cpp/vkt/ManagedBuffer.hpp:257), which calls it under the GPU policy."""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PATTERN_SIZES = [1, 2, 3, 4, 8, 16, 17, 256, 300]
+
+
+@pytest.fixture(scope="module")
+def L():
+    import torch
+    assert torch.cuda.is_available()
+    from volkit_amd import _lib
+    return _lib
+
+
+def expected(before, pattern, dst_size):
+    out = before.copy()
+    n = (dst_size // len(pattern)) * len(pattern)
+    out[:n] = np.resize(pattern, n)
+    return out
+
+
+def run_memset(L, dev, before, offset, pattern, dst_size):
+    lib = L.lib
+    assert lib.vktHipMemcpy(C.c_void_p(dev), before.ctypes.data_as(C.c_void_p), before.nbytes, 1) == 0
+    pat = np.ascontiguousarray(pattern, dtype=np.uint8)
+    rc = lib.vktHipMemsetRange(C.c_void_p(dev + offset), pat.ctypes.data_as(C.c_void_p), dst_size, pat.size)
+    assert rc == 0, L.last_error()
+    after = np.empty_like(before)
+    assert lib.vktHipMemcpy(after.ctypes.data_as(C.c_void_p), C.c_void_p(dev), before.nbytes, 2) == 0
+    return after
+
+
+@pytest.mark.parametrize("psize", PATTERN_SIZES)
+def test_memset_range_patterns(L, psize):
+    rng = np.random.default_rng(psize)
+    total = 70_000
+    p = C.c_void_p()
+    assert L.lib.vktHipAllocate(C.byref(p), total) == 0
+    try:
+        for offset in (0, 1, 3, 16, 17):
+            for dst_size in (psize * 1000, psize * 1000 + psize - 1, psize * 7 + 1, psize, psize - 1, 0,
+                             total - offset - 5):
+                if dst_size < 0 or dst_size > total - offset:   # stay inside the allocation
+                    continue
+                before = rng.integers(0, 256, total, dtype=np.uint8)
+                pattern = rng.integers(0, 256, psize, dtype=np.uint8)
+                after = run_memset(L, p.value, before, offset, pattern, dst_size)
+                ref = before.copy()
+                ref[offset:offset + dst_size] = expected(before[offset:offset + dst_size], pattern, dst_size)
+                bad = np.flatnonzero(after != ref)
+                assert bad.size == 0, (psize, offset, dst_size, bad[:5])
+    finally:
+        L.lib.vktHipFree(p)
+
+
+def test_memset_range_large_vector_path(L):
+    """256 MiB + 5 bytes with a 4-byte pattern: the 16-byte vector kernel plus the byte tail."""
+    n = (256 << 20) + 5
+    p = C.c_void_p()
+    assert L.lib.vktHipAllocate(C.byref(p), n) == 0
+    try:
+        pattern = np.array([0x12, 0x34, 0x56, 0x78], np.uint8)
+        before = np.full(n, 0xEE, np.uint8)
+        after = run_memset(L, p.value, before, 0, pattern, n)
+        k = (n // 4) * 4
+        assert np.array_equal(after[:k].view(np.uint32)[: k // 4 - 1], np.full(k // 4 - 1, 0x78563412, np.uint32))
+        assert np.array_equal(after[k:], before[k:])
+    finally:
+        L.lib.vktHipFree(p)
+
+
+def test_memset_repeated_big_patterns_stay_exact(L):
+    """Patterns over 256 B go through a device copy of the pattern in the call site's scratch;
+    consecutive calls with different patterns must each see their own bytes."""
+    rng = np.random.default_rng(9)
+    total = 300 * 64
+    p = C.c_void_p()
+    assert L.lib.vktHipAllocate(C.byref(p), total) == 0
+    try:
+        for i in range(20):
+            pattern = rng.integers(0, 256, 300, dtype=np.uint8)
+            before = np.zeros(total, np.uint8)
+            after = run_memset(L, p.value, before, 0, pattern, total)
+            assert np.array_equal(after, np.resize(pattern, total)), i
+    finally:
+        L.lib.vktHipFree(p)
+
+
+@pytest.fixture(scope="module")
+def fx():
+    import volkit_amd  # noqa: F401
+    lib = C.CDLL(os.path.join(HERE, "native", "libfixtures.so"))
+    lib.vktt_managed_fill.argtypes = [C.c_int, C.c_size_t, C.c_void_p, C.c_void_p]
+    return lib
+
+
+@pytest.mark.parametrize("psize", PATTERN_SIZES)
+def test_managed_buffer_fill(fx, psize):
+    rng = np.random.default_rng(1000 + psize)
+    for count in (1, 7, 1000, 4097):
+        pattern = rng.integers(0, 256, psize, dtype=np.uint8)
+        out = np.zeros(count * psize, np.uint8)
+        assert fx.vktt_managed_fill(psize, count, pattern.ctypes.data, out.ctypes.data) == 0
+        assert np.array_equal(out, np.resize(pattern, count * psize)), (psize, count)

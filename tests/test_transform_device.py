@@ -18,7 +18,7 @@ from test_gpu_parity import assert_codes_equal, rand_codes
 pytestmark = pytest.mark.gpu
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(HERE, "native", "libtransform_ops.so")
+LIB = os.path.join(HERE, "native", "libfixtures.so")
 
 UNARY_OPS = {0: "Checkered<3>", 1: "Checkered<2>", 2: "Diagonal", 3: "Rescale", 4: "ScratchProbe"}
 BINARY_OPS = {0: "Or", 1: "MixFormats"}

@@ -242,19 +242,32 @@ namespace hipk
         {
             Pattern256 pat{};
             uint8_t* big = nullptr;
+            // patterns over 256 B: the grow-only scratch of this call site (not a stream-ordered
+            // pool block -- DESIGN.md §4.6), filled by a synchronous H2D copy on the compute
+            // stream (the pageable source must be consumed before returning)
+            static rt::StreamScratch bigScratch;
             if (patternSize <= sizeof(pat.bytes))
                 std::memcpy(pat.bytes, pb, patternSize);
             else
             {
-                VKT_HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&big), patternSize, s));
-                VKT_HIP_TRY(hipMemcpyAsync(big, pb, patternSize, hipMemcpyHostToDevice, s));
-                VKT_HIP_TRY(hipStreamSynchronize(s));   // pageable source must be consumed
+                big = static_cast<uint8_t*>(bigScratch.acquire(patternSize, s));
+                if (big == nullptr)
+                    return vktInvalidValue;
+                vktError e = rt::check(hipMemcpyAsync(big, pb, patternSize, hipMemcpyHostToDevice, s),
+                                       "MemsetRange: pattern upload");
+                if (e == vktNoError)
+                    e = rt::check(hipStreamSynchronize(s), "MemsetRange: pattern upload");
+                if (e != vktNoError)
+                {
+                    bigScratch.release(s);
+                    return e;
+                }
             }
             hipLaunchKernelGGL(memsetBytesKernel, dim3(streamingGrid(nbytes - head, kBlock)), dim3(kBlock), 0, s,
                                static_cast<uint8_t*>(dst), head, nbytes, static_cast<uint32_t>(patternSize), pat,
                                big);
             if (big != nullptr)
-                VKT_HIP_TRY(hipFreeAsync(big, s));
+                bigScratch.release(s);
         }
         return rt::finishLaunch("MemsetRange");
     }
