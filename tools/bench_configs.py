@@ -130,8 +130,8 @@ def main():
         free(S, Rv)
     if want("transform"):
         # device-functor Transform (include/volkit_transform.hpp) through the test fixture
-        # tests/native/libtransform_ops.so; unary algorithmic bytes 2b per voxel
-        t = C.CDLL(os.path.join(ROOT, "tests", "native", "libtransform_ops.so"))
+        # tests/native/libfixtures.so; unary algorithmic bytes 2b per voxel
+        t = C.CDLL(os.path.join(ROOT, "tests", "native", "libfixtures.so"))
         t.vktt_bench_unary.argtypes = [C.c_int] * 6 + [C.POINTER(C.c_float)]
         ms = C.c_float(0.0)
         m = 1024
@@ -140,6 +140,20 @@ def main():
             if t.vktt_bench_unary(op, m, m, m, fmt, R, C.byref(ms)) != 0:
                 raise RuntimeError(_lib.last_error())
             report(f"Transform {lab} 1024^3 fmt={fmt}", ms.value, rw * b * m ** 3, m ** 3)
+    if want("memset"):
+        # MemsetRange / ManagedBuffer::fill at 1024^3-UInt16 scale (2 GiB), write-only bytes
+        nb = 2 << 30
+        p = C.c_void_p()
+        if lib.vktHipAllocate(C.byref(p), nb + 64) != 0:
+            raise RuntimeError(_lib.last_error())
+        import numpy as np
+        for psize, off in ((2, 0), (4, 1), (2, 16), (3, 0), (12, 0), (17, 0), (300, 0)):
+            pat = np.arange(1, psize + 1, dtype=np.uint8)
+            n = nb - off
+            ms = timed(lambda: lib.vktHipMemsetRange(C.c_void_p(p.value + off), pat.ctypes.data_as(C.c_void_p), n,
+                                                     psize), R)
+            report(f"MemsetRange 2 GiB pattern {psize} B dst+{off}", ms, (n // psize) * psize, n // 2)
+        lib.vktHipFree(p)
     if want("gather"):
         # non-integer ratios (gather path): up/down-sampling 768^3 <-> 1024^3, all dst formats
         cases = [(768, 1024, 5, 1), (1024, 768, 5, 1), (768, 1024, 4, 1), (768, 1024, 7, 0), (768, 1024, 7, 1),
