@@ -13,10 +13,19 @@ still computed and executed -- it is empty).  --layout-gpus M
 slab of the M-GPU layout on one GPU (per-rank rehearsal of the multi-GPU shapes).
 
 value = dst voxels of all ranks / wall time per step (Gvoxels/s).  roofline: the dominant
-kernel (SumRange: 6 B/voxel algorithmic) timed with HIP events on the compute stream.
-cpu_baseline: the oracle restatement (port, 1 thread) on a bounded sample of the same pipeline.
+kernel (SumRange: 6 B/voxel algorithmic) timed with HIP events on the library's compute
+stream.  After the timed region, secondary measurements go into the same JSON line (none of
+them is `value`):
+  * mapping_m1_3   -- the same pipeline with mapping [-1, 3] on every volume (the float-codec
+                      kernels; SURVEY §8(d) "a second run uses mapping [-1,3]");
+  * f32_linear     -- Float32 "Linear" Resample with the z+1 halo plane exchanged between
+                      neighbour ranks over torch.distributed on device tensors (RCCL over
+                      xGMI at N>1): per rank 512^3 -> 1024^3 of the same global layout;
+  * copy_peak      -- the library's own Copy 1024^3 UInt16, the achievable streaming rate;
+  * cpu_baseline   -- the oracle port (1 thread) on the full 1024^3 pipeline and on 512^3.
 """
 import argparse
+import ctypes as C
 import json
 import os
 import sys
@@ -38,8 +47,10 @@ def parse():
     p.add_argument("--warmup", type=int, default=25)
     p.add_argument("--dst", type=int, default=1024, help="per-GPU dst cube edge (source = dst/2)")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--no-copy-peak", action="store_true", help="skip the measured D2D-copy peak")
-    p.add_argument("--cpu-dst", type=int, default=768, help="dst edge of the CPU-baseline sample")
+    p.add_argument("--no-copy-peak", action="store_true", help="skip the library-Copy achievable peak")
+    p.add_argument("--no-secondary", action="store_true",
+                   help="skip the mapping [-1,3] and Float32-Linear secondary measurements")
+    p.add_argument("--cpu-dst", type=int, default=1024, help="dst edge of the CPU-baseline run")
     p.add_argument("--layout-gpus", type=int, default=0,
                    help="single process: run rank 0's slab of the M-GPU global layout")
     p.add_argument("--dist-backend", default="nccl",
@@ -65,8 +76,7 @@ def global_dims(edge, n):
 
 def cpu_baseline(dst_edge):
     """Oracle (C restatement of the reference serial path, 1 thread) on the same pipeline at
-    dst_edge^3; returns Gvoxels/s of dst voxels."""
-    import numpy as np
+    dst_edge^3; returns (Gvoxels/s of dst voxels, seconds)."""
     from oracle import binding as ob
 
     s = dst_edge // 2
@@ -78,8 +88,47 @@ def cpu_baseline(dst_edge):
     ob.resample(r, src, 1)
     ob.arith_range("Sum", d, r, b, (0, 0, 0), (dst_edge,) * 3)
     dt = time.perf_counter() - t0
-    del np
     return dst_edge ** 3 / dt / 1e9, dt
+
+
+class Ctx:
+    """Process-group / stream context shared by the measurements."""
+
+    def __init__(self, torch, dist, world, rank, backend):
+        self.torch, self.dist, self.world, self.rank, self.backend = torch, dist, world, rank, backend
+
+    def barrier_sync(self):
+        self.torch.cuda.synchronize()
+        if self.world > 1:
+            self.dist.barrier()
+        self.torch.cuda.synchronize()
+
+    def max_over_ranks(self, x):
+        if self.world == 1:
+            return x
+        dev = "cuda" if self.backend == "nccl" else "cpu"
+        t = self.torch.tensor([x], device=dev, dtype=self.torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def timed(self, step, steps, warmup, nev):
+        """warmup untimed steps, then `steps` timed steps between barrier + synchronize on both
+        sides; step(ev) records nev+1 events.  Returns (max-over-ranks seconds, per-interval
+        mean kernel ms)."""
+        torch = self.torch
+        for _ in range(warmup):
+            step(None)
+        self.barrier_sync()
+        evs = []
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(nev + 1)]
+            step(ev)
+            evs.append(ev)
+        self.barrier_sync()
+        elapsed = self.max_over_ranks(time.perf_counter() - t0)
+        ms = [sum(e[i].elapsed_time(e[i + 1]) for e in evs) / len(evs) for i in range(nev)]
+        return elapsed, ms
 
 
 def main():
@@ -102,22 +151,26 @@ def main():
     import volkit_amd.volkit as vkt
     from volkit_amd import slab
     from volkit_amd._lib import lib, HipVolumeView_t
-    import ctypes as C
 
     if lib.vktHipSetDevice(local) != 0:
         raise RuntimeError(vkt.last_error())
     # One dedicated (non-NULL) stream for our kernels and for torch's events / RCCL calls:
     # torch's default stream is the legacy NULL stream, which would serialise against the
-    # backend's blocking stream at every event record.
-    stream = torch.cuda.Stream()
-    lib.vktHipSetComputeStream(C.c_void_p(stream.cuda_stream))
+    # backend's blocking stream at every event record.  Events are recorded on the stream the
+    # library reports as its compute stream (the same one), so they bracket its kernels.
+    own = torch.cuda.Stream()
+    lib.vktHipSetComputeStream(C.c_void_p(own.cuda_stream))
+    sp = C.c_void_p()
+    lib.vktHipGetComputeStream(C.byref(sp))
+    stream = torch.cuda.ExternalStream(sp.value)
     torch.cuda.set_stream(stream)
+    ctx = Ctx(torch, dist, world, rank, args.dist_backend)
 
     ep = vkt.GetThreadExecutionPolicy()
     ep.device = vkt.ExecutionPolicy.Device_GPU
     vkt.SetThreadExecutionPolicy(ep)
 
-    UINT16, LINEAR = vkt.DataFormat_UInt16, vkt.FilterMode_Linear
+    UINT16, FLOAT32, LINEAR = vkt.DataFormat_UInt16, vkt.DataFormat_Float32, vkt.FilterMode_Linear
     layout_n = world
     if args.layout_gpus:
         if world != 1:
@@ -144,51 +197,25 @@ def main():
     def planes(g0, g1):
         return slab.device_tensor(sview.data + (g0 - ls0) * plane_bytes, (g1 - g0) * plane_bytes)
 
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-    t_res, t_sum = [], []
+    def pipeline(views):
+        s_, r_, b_, d_ = views
 
-    def step(timed):
-        if plan.recvs or plan.sends:
-            slab.exchange_planes(plan, planes)
-        if timed:
-            ev[0].record()
-        e1 = lib.vktHipResampleSlab(rview, sview, LINEAR, dst_gdz, dz0, src_gdz, ls0)
-        if timed:
-            ev[1].record()
-        e2 = lib.vktHipArithmeticRange(0, dview, rview, bview, first, last, _lib_vec(0, 0, 0))
-        if timed:
-            ev[2].record()
-        if e1 or e2:
-            raise RuntimeError(vkt.last_error())
+        def step(ev):
+            if plan.recvs or plan.sends:
+                slab.exchange_planes(plan, planes)
+            if ev:
+                ev[0].record(stream)
+            e1 = lib.vktHipResampleSlab(r_, s_, LINEAR, dst_gdz, dz0, src_gdz, ls0)
+            if ev:
+                ev[1].record(stream)
+            e2 = lib.vktHipArithmeticRange(0, d_, r_, b_, first, last, _lib_vec(0, 0, 0))
+            if ev:
+                ev[2].record(stream)
+            if e1 or e2:
+                raise RuntimeError(vkt.last_error())
+        return step
 
-    for _ in range(args.warmup):
-        step(False)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(True)
-        # per-step kernel times are read after the loop (events stay valid)
-        t_res.append((ev[0], ev[1]))
-        t_sum.append((ev[1], ev[2]))
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        dev = "cuda" if args.dist_backend == "nccl" else "cpu"
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
-    res_ms = sum(a.elapsed_time(b) for a, b in t_res) / len(t_res)
-    sum_ms = sum(a.elapsed_time(b) for a, b in t_sum) / len(t_sum)
-    copy_gbs = achievable_copy_gbs(torch, Rv.hip_view(), Dv.hip_view(), 2 * DX * DY * (dz1 - dz0)) \
-        if not args.no_copy_peak else None
+    elapsed, (res_ms, sum_ms) = ctx.timed(pipeline((sview, rview, bview, dview)), args.steps, args.warmup, 2)
     ms_per_step = elapsed * 1e3 / args.steps
     vox_rank = DX * DY * (dz1 - dz0)
     total_vox = vox_rank * world
@@ -209,6 +236,9 @@ def main():
         except Exception:
             traffic = None
 
+    def gbs(nbytes, ms):
+        return round(nbytes / (ms / 1e3) / 1e9, 1)
+
     out = {
         "metric": "Gvoxels/s + achieved HBM GB/s, Resample+SumRange 1024^3 UInt16",
         "value": round(value, 3),
@@ -225,7 +255,7 @@ def main():
         "config": {
             "workload": f"Resample {SX}x{SY}x{src_gdz}->{DX}x{DY}x{dst_gdz} UInt16 Linear + SumRange "
                         f"{DX}x{DY}x{dst_gdz} UInt16, Z-slab over {layout_n} GPU(s)"
-                        + (f" (rank 0's slab only, on 1 GPU)" if layout_n != world else ""),
+                        + (" (rank 0's slab only, on 1 GPU)" if layout_n != world else ""),
             "global_dst": [DX, DY, dst_gdz], "global_src": [SX, SY, src_gdz],
             "slab_dst_per_rank": [DX, DY, dz1 - dz0],
             "parallelism": f"zslab{layout_n}", "halo_planes_per_rank": plan.halo_planes,
@@ -235,31 +265,73 @@ def main():
         "roofline": {
             "kernel": "SumRange (arithmetic pointwise, UInt16)",
             "bound": "hbm",
-            "achieved": round(sum_bytes / (sum_ms / 1e3) / 1e9, 1),
+            "achieved": gbs(sum_bytes, sum_ms),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(sum_bytes / (sum_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
             "traffic": traffic,
-            "resample_achieved": round(res_bytes / (res_ms / 1e3) / 1e9, 1),
+            "resample_achieved": gbs(res_bytes, res_ms),
             "pipeline_frac": round(pipe_bytes / ((res_ms + sum_ms) / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
-            # the fraction against a measured D2D copy as well as the spec peak
-            "d2d_copy_gbs": copy_gbs,
-            "frac_vs_d2d_copy": round(sum_bytes / (sum_ms / 1e3) / 1e9 / copy_gbs, 4) if copy_gbs else None,
         },
     }
+
+    if not args.no_secondary:
+        # same pipeline, same buffers, mapping [-1, 3] on every volume: the float codec runs
+        # (the unit-mapping integer specialisations of DESIGN §4.1 do not apply)
+        fp = [HipVolumeView_t(v.data, v.dimX, v.dimY, v.dimZ, v.dataFormat, -1.0, 3.0)
+              for v in (sview, rview, bview, dview)]
+        el_fp, (res_fp, sum_fp) = ctx.timed(pipeline(fp), args.steps, max(5, args.warmup // 2), 2)
+        msfp = el_fp * 1e3 / args.steps
+        out["mapping_m1_3"] = {
+            "value": round(total_vox / (msfp / 1e3) / 1e9, 3), "unit": "Gvoxels/s", "ms_per_step": round(msfp, 4),
+            "kernels_ms": {"Resample": round(res_fp, 4), "SumRange": round(sum_fp, 4)},
+            "SumRange_achieved": gbs(sum_bytes, sum_fp),
+            "SumRange_frac": round(sum_bytes / (sum_fp / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+            "resample_achieved": gbs(res_bytes, res_fp),
+            "note": "same workload and buffers, mapping [-1,3] on all volumes (float-codec kernels)",
+        }
+        out["f32_linear"] = f32_linear(ctx, vkt, slab, lib, args, layout_n, stream)
+
+    if not args.no_copy_peak:
+        # achievable streaming rate on this box: the library's own CopyRange of one volume
+        # (vector pointwise kernel, read + write bytes), after the timed regions
+        def copy_step(ev):
+            if ev:
+                ev[0].record(stream)
+            if lib.vktHipCopyRange(dview, bview, first, last, _lib_vec(0, 0, 0)):
+                raise RuntimeError(vkt.last_error())
+            if ev:
+                ev[1].record(stream)
+        _, (copy_ms,) = ctx.timed(copy_step, 10, 3, 1)
+        copy_gbs = gbs(4 * vox_rank, copy_ms)
+        out["copy_peak"] = {"kernel": f"CopyRange {DX}x{DY}x{dz1 - dz0} UInt16 (library)", "ms": round(copy_ms, 4),
+                            "achieved": copy_gbs, "unit": "GB/s"}
+        out["roofline"]["frac_vs_copy_peak"] = round(out["roofline"]["achieved"] / copy_gbs, 4)
+
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         gv, dt = cpu_baseline(args.cpu_dst)
+        at512 = None
+        if args.cpu_dst > 512:
+            gv512, dt512 = cpu_baseline(512)
+            at512 = {"value": round(gv512, 5), "seconds": round(dt512, 2)}
+        # the compiled reference serial path, measured in the survey container
+        # (1 thread, g++ -O2): SumRange UInt16 33.8-37.9 ns/voxel + Resample UInt16 Linear 41.5
+        # ns/dst voxel -> ~77.4 ns per pipeline voxel.  The port skips the reference's per-voxel
+        # migrate() + policy lookup; the calibration factor is reference ns / port ns, with the
+        # port's ns measured here (the reference does not travel to the GPU box).
+        ref_ns = (33.8 + 37.9) / 2 + 41.5
+        port_ns = dt * 1e9 / args.cpu_dst ** 3
         out["cpu_baseline"] = {
             "value": round(gv, 5), "unit": "Gvoxels/s", "cores": 1, "kind": "port",
-            "sample": f"oracle restatement of the reference serial path, Resample {args.cpu_dst // 2}^3->"
-                      f"{args.cpu_dst}^3 UInt16 Linear + SumRange {args.cpu_dst}^3, {dt:.1f} s, 1 thread of "
-                      f"{os.cpu_count()} host CPUs",
-            # the compiled reference serial path, measured in the survey container
-            # (1 thread, g++ -O2): SumRange UInt16 33.8-37.9 ns/voxel + Resample UInt16 Linear 41.5
-            # ns/dst voxel -> ~75-79 ns per pipeline voxel.  Not re-measured here (the reference
-            # does not travel to the GPU box); the port above skips its per-voxel migrate().
-            "reference_equivalent": {"value": round(1.0 / ((33.8e-9 + 37.9e-9) / 2 + 41.5e-9) / 1e9, 5), "unit": "Gvoxels/s",
-                                     "basis": "BASELINE.md §2 survey probe, 1 core, not re-measured"},
+            "sample": f"oracle restatement of the reference serial path on the full headline workload: "
+                      f"Resample {args.cpu_dst // 2}^3->{args.cpu_dst}^3 UInt16 Linear + SumRange "
+                      f"{args.cpu_dst}^3, {dt:.1f} s, 1 thread of {os.cpu_count()} host CPUs",
+            "at_512": at512,
+            "reference_equivalent": {
+                "value": round(1.0 / (ref_ns * 1e-9) / 1e9, 5), "unit": "Gvoxels/s",
+                "calibration_factor": round(ref_ns / port_ns, 3),
+                "basis": "BASELINE.md §2 survey probe of the compiled reference (1 core), "
+                         "reference ns/voxel / port ns/voxel measured here"},
         }
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -267,29 +339,61 @@ def main():
         dist.destroy_process_group()
 
 
-def achievable_copy_gbs(torch, src_view, dst_view, nbytes, reps=10):
-    """Achievable HBM rate on this box: a plain device-to-device hipMemcpyAsync (the runtime's
-    own blit kernel) of one whole volume, read + write bytes / HIP-event time, after the timed
-    region (it never overlaps the measured steps)."""
-    import ctypes as C
-    stream = torch.cuda.current_stream()
-    hip = C.CDLL("libamdhip64.so")
-    hip.hipMemcpyAsync.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p]
-
-    def copy():
-        if hip.hipMemcpyAsync(C.c_void_p(dst_view.data), C.c_void_p(src_view.data), C.c_size_t(nbytes), 3,
-                              C.c_void_p(stream.cuda_stream)) != 0:
-            raise RuntimeError("hipMemcpyAsync D2D failed")
-
-    for _ in range(3):
-        copy()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        copy()
-    e1.record()
+def f32_linear(ctx, vkt, slab, lib, args, layout_n, stream):
+    """Float32 Linear Resample, per rank (dst/2)^3 -> dst^3 of the global layout, source
+    uniform in [0, 1) (BASELINE config 3's input), with the chain's z+1 halo planes exchanged
+    between neighbour ranks on device tensors (torch.distributed: RCCL over xGMI at N>1)."""
+    torch = ctx.torch
+    rank, world = ctx.rank, ctx.world
+    LINEAR, FLOAT32 = vkt.FilterMode_Linear, vkt.DataFormat_Float32
+    DX, DY, dgz = global_dims(args.dst, layout_n)
+    SX, SY, sgz = DX // 2, DY // 2, dgz // 2
+    plan = slab.plan_resample(dgz, sgz, layout_n, rank, LINEAR, chain=True)
+    ls0, ls1 = plan.local_src
+    o0, o1 = plan.owned_src
+    dz0, dz1 = plan.dst
+    S = vkt.StructuredVolume(SX, SY, ls1 - ls0, FLOAT32)
+    R = vkt.StructuredVolume(DX, DY, dz1 - dz0, FLOAT32)
+    sv, rv = S.hip_view(), R.hip_view()
+    plane = SX * SY * 4
+    src_t = slab.device_tensor(sv.data, (ls1 - ls0) * plane).view(torch.float32)
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(0x5EED + rank)
+    src_t.uniform_(0.0, 1.0, generator=gen)   # halo planes are overwritten by the exchange
     torch.cuda.synchronize()
-    return round(2 * nbytes * reps / (e0.elapsed_time(e1) / 1e3) / 1e9, 1)
+
+    def planes(g0, g1):
+        return slab.device_tensor(sv.data + (g0 - ls0) * plane, (g1 - g0) * plane)
+
+    def step(ev):
+        if ev:
+            ev[0].record(stream)
+        if world > 1 and (plan.recvs or plan.sends):   # (--layout-gpus: rank 0's slab alone)
+            slab.exchange_planes(plan, planes)
+        if ev:
+            ev[1].record(stream)
+        if lib.vktHipResampleSlab(rv, sv, LINEAR, dgz, dz0, sgz, ls0):
+            raise RuntimeError(vkt.last_error())
+        if ev:
+            ev[2].record(stream)
+
+    steps = max(5, args.steps // 2)
+    elapsed, (ex_ms, res_ms) = ctx.timed(step, steps, 3, 2)
+    ms = elapsed * 1e3 / steps
+    vox = DX * DY * (dz1 - dz0)
+    nbytes = 4 * SX * SY * (o1 - o0) + 4 * vox
+    out = {
+        "workload": f"Resample {SX}x{SY}x{sgz}->{DX}x{DY}x{dgz} Float32 Linear (source uniform [0,1)), "
+                    f"Z-slab over {layout_n} GPU(s), z+1 halo exchanged on device tensors "
+                    f"({'RCCL' if ctx.backend == 'nccl' and world > 1 else ctx.backend if world > 1 else 'none'})",
+        "value": round(vox * world / (ms / 1e3) / 1e9, 3), "unit": "Gvoxels/s", "ms_per_step": round(ms, 4),
+        "resample_ms": round(res_ms, 4), "exchange_ms": round(ex_ms, 4),
+        "halo_planes_per_rank": plan.halo_planes, "halo_bytes_per_rank": plan.halo_planes * plane,
+        "resample_achieved": round(nbytes / (res_ms / 1e3) / 1e9, 1),
+        "resample_frac": round(nbytes / (res_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+    }
+    del S, R
+    return out
 
 
 def _lib_vec(x, y, z):

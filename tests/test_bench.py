@@ -39,6 +39,10 @@ def test_bench_small_run_prints_one_contract_line():
     assert roof["bound"] == "hbm" and roof["unit"] == "GB/s" and roof["peak"] == 8000.0
     assert 0 < roof["frac"] == pytest.approx(roof["achieved"] / roof["peak"], abs=1e-3)
     assert roof["traffic"] is None            # PMC traffic is keyed to the 1024^3 workload only
-    assert roof["d2d_copy_gbs"] > 0
+    assert out["copy_peak"]["achieved"] > 0 and roof["frac_vs_copy_peak"] > 0
+    fp = out["mapping_m1_3"]
+    assert fp["value"] > 0 and 0 < fp["SumRange_frac"] < 1.2
+    f32 = out["f32_linear"]
+    assert f32["value"] > 0 and f32["halo_planes_per_rank"] == 0 and "Float32 Linear" in f32["workload"]
     cpu = out["cpu_baseline"]
     assert cpu["kind"] == "port" and cpu["cores"] == 1 and cpu["value"] > 0

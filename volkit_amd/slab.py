@@ -92,17 +92,31 @@ def plan_resample(dst_gdz: int, src_gdz: int, world: int, rank: int, filter_mode
 
 def exchange_planes(plan: ResamplePlan, planes: Callable[[int, int], "torch.Tensor"], group=None) -> None:
     """Point-to-point halo exchange: `planes(g0, g1)` returns a writable uint8 tensor view of
-    global source planes [g0, g1) in the local buffer.  One batched isend/irecv round."""
+    global source planes [g0, g1) in the local buffer.  One batched isend/irecv round.
+
+    With the nccl backend (RCCL over xGMI) device planes move device to device: RCCL runs on
+    its own stream after the current stream's work, and the current stream waits for the
+    receives, so a kernel enqueued next reads the halo.  gloo moves host tensors only, so device
+    planes are staged through host copies there (CPU tests, 1-GPU rehearsals)."""
     import torch.distributed as dist
 
-    ops = []
+    staged = dist.get_backend(group) == "gloo"
+    ops, landing = [], []
     for peer, g0, g1 in plan.sends:
-        ops.append(dist.P2POp(dist.isend, planes(g0, g1).contiguous(), peer, group))
+        t = planes(g0, g1).contiguous()
+        ops.append(dist.P2POp(dist.isend, t.cpu() if staged and t.is_cuda else t, peer, group))
     for peer, g0, g1 in plan.recvs:
-        ops.append(dist.P2POp(dist.irecv, planes(g0, g1), peer, group))
+        t = planes(g0, g1)
+        if staged and t.is_cuda:
+            host = t.new_empty(t.shape, device="cpu")
+            landing.append((t, host))
+            t = host
+        ops.append(dist.P2POp(dist.irecv, t, peer, group))
     if ops:
         for req in dist.batch_isend_irecv(ops):
             req.wait()
+    for dev, host in landing:
+        dev.copy_(host)
 
 
 class DeviceBytes:
