@@ -218,6 +218,24 @@ int vktt_run_binary(int op, int alias, void* data1, int dx1, int dy1, int dz1, i
     return rc;
 }
 
+// Binary Transform with a __device__ lambda (the form INTEGRATION.md §2 shows): OR of two
+// UInt8 volumes of the same dims, both updated.
+int vktt_lambda_or(void* data1, void* data2, int dx, int dy, int dz)
+{
+    GpuPolicy gpu;
+    vkt::StructuredVolume v1(dx, dy, dz, vkt::DataFormat::UInt8), v2(dx, dy, dz, vkt::DataFormat::UInt8);
+    upload(v1, data1);
+    upload(v2, data2);
+    int rc = static_cast<int>(vkt::Transform(v1, v2, [] __device__(int32_t, int32_t, int32_t, vkt::VoxelView a,
+                                                                  vkt::VoxelView b) {
+        a.bytes[0] |= b.bytes[0];
+        b.bytes[0] = a.bytes[0];
+    }));
+    download(data1, v1);
+    download(data2, v2);
+    return rc;
+}
+
 // The same op as a host callback for the oracle.
 void* vktt_host_unary(int op)
 {

@@ -40,6 +40,7 @@ def t():
     lib.vktt_host_binary.restype = p
     lib.vktt_host_binary.argtypes = [i]
     lib.vktt_bench_unary.argtypes = [i, i, i, i, i, i, C.POINTER(f)]
+    lib.vktt_lambda_or.argtypes = [p, p, i, i, i]
     return lib
 
 
@@ -190,3 +191,15 @@ def test_bench_entry_runs(t):
     ms = C.c_float(0.0)
     assert t.vktt_bench_unary(2, 256, 256, 256, 4, 3, C.byref(ms)) == 0
     assert ms.value > 0.0
+
+
+def test_device_lambda(t):
+    """vkt::Transform(v1, v2, [] __device__ (...) {...}) -- a device lambda as the binary op."""
+    rng = np.random.default_rng(4)
+    a = rng.integers(0, 256, (9, 17, 48), dtype=np.uint8)
+    b = rng.integers(0, 256, (9, 17, 48), dtype=np.uint8)
+    ga, gb = a.copy(), b.copy()
+    assert t.vktt_lambda_or(ga.ctypes.data, gb.ctypes.data, 48, 17, 9) == 0
+    r1, r2 = oracle_binary(t, 0, a, 4, (0.0, 1.0), b, 4, (0.0, 1.0), (0, 0, 0), (48, 17, 9))
+    np.testing.assert_array_equal(ga, r1)
+    np.testing.assert_array_equal(gb, r2)

@@ -4,12 +4,15 @@
 // unordered_map<thread::id, policy> (a data race under concurrent Set/Get).
 // A thread_local gives the same observable semantics -- per calling thread, default
 // {CPU, Serial, CUDA(=GPU backend), false}, not inherited by child threads -- without the race.
+// Extension: VKT_DEFAULT_DEVICE=GPU makes Device::GPU the initial device of every thread.
 //
 // Resource registry: reference src/vkt/ManagedResource.cpp:16-40 (monotonic uint32 handles
 // over an unlocked map); here guarded by a mutex.
 
 #include "Runtime.hpp"
 
+#include <cstdlib>
+#include <cstring>
 #include <mutex>
 #include <unordered_map>
 
@@ -17,7 +20,22 @@ namespace vkt
 {
     namespace
     {
-        thread_local ExecutionPolicy tlsPolicy;
+        // Initial policy of every thread: the reference's default {CPU, Serial, CUDA, false},
+        // unless VKT_DEFAULT_DEVICE=GPU asks for the GPU device -- then unmodified reference
+        // programs, which never set a policy, run their algorithms on this GPU backend.
+        ExecutionPolicy initialPolicy()
+        {
+            static ExecutionPolicy const p = [] {
+                ExecutionPolicy e;
+                char const* d = std::getenv("VKT_DEFAULT_DEVICE");
+                if (d != nullptr && (std::strcmp(d, "GPU") == 0 || std::strcmp(d, "gpu") == 0))
+                    e.device = ExecutionPolicy::Device::GPU;
+                return e;
+            }();
+            return p;
+        }
+
+        thread_local ExecutionPolicy tlsPolicy = initialPolicy();
 
         std::mutex& registryMutex()
         {
