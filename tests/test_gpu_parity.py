@@ -155,6 +155,83 @@ def test_arithmetic_unit_mapping_all_code_pairs(g, o, op):
             assert_codes_equal(out, ref, fmt, f"{op} fmt={fmt} map={mapping} all code pairs")
 
 
+@pytest.mark.parametrize("op", ["Sum", "Diff", "SafeSum", "SafeDiff", "AbsDiff", "SafeAbsDiff"])
+def test_arithmetic_unit_mapping_code_pairs_strided_subbox(g, o, op):
+    """The unit-mapping integer paths (IntArithU16F, UnitArithU8F) on a strided sub-box: odd
+    first.x, an extent that is not a multiple of 8, several rows -- the padded row items that
+    straddle the row ends (masked stores), the multi-row addressing, every UInt8 code pair and
+    every UInt16 code as either operand."""
+    # dims x multiple of 8 (vector path with several rows); box x 3..(3+253), odd start
+    a8 = np.zeros((18, 16, 264), np.uint8)
+    b8 = np.zeros_like(a8)
+    a8[1:17, :, 3:259] = np.repeat(np.arange(256, dtype=np.uint8), 256).reshape(16, 16, 256)
+    b8[1:17, :, 3:259] = np.tile(np.arange(256, dtype=np.uint8), 256).reshape(16, 16, 256)
+    c16 = np.arange(65536, dtype=np.uint16)
+    a16 = np.zeros((10, 64, 264), np.uint16)
+    b16 = np.zeros_like(a16)
+    a16[1:9, :, 3:259] = np.concatenate([c16, np.random.default_rng(5).permutation(c16)]).reshape(8, 64, 256)
+    b16[1:9, :, 3:259] = np.concatenate([np.random.default_rng(6).permutation(c16), c16]).reshape(8, 64, 256)
+    for fmt, a, b in ((4, a8, b8), (5, a16, b16)):
+        nz, ny = a.shape[0], a.shape[1]
+        for first, last in (((3, 0, 1), (259, ny, nz - 1)), ((3, 1, 1), (256, ny - 1, nz - 1)),
+                            ((5, 0, 0), (262, ny, nz))):
+            d = np.full_like(a, 7)
+            out = g.arith(op, [fmt] * 3, [(0.0, 1.0)] * 3, a, b, d.copy(), first, last, (0, 0, 0))
+            ref = o.arith(op, [fmt] * 3, [(0.0, 1.0)] * 3, a, b, d.copy(), first, last, (0, 0, 0))
+            assert_codes_equal(out, ref, fmt, f"{op} fmt={fmt} sub-box {first}->{last}")
+
+
+@pytest.mark.parametrize("max_quanta", [1, 2, 3])
+def test_pointwise_multi_launch_split(g, o, max_quanta):
+    """Lower the launch split (knob pointwise.max_quanta_per_launch) so small ops need several
+    launches: one collapsed row with a scalar head and tail (edges only in the first launch)
+    and padded multi-row boxes, vs the oracle."""
+    from volkit_amd._lib import lib
+    rng = np.random.default_rng(max_quanta)
+    assert lib.vktHipSetTuningKnob(b"pointwise.max_quanta_per_launch", max_quanta) == 0
+    try:
+        for fmt in (5, 4, 7):
+            for dims, first, last in (((37, 23, 11), (0, 0, 1), (37, 23, 11)),    # one row, head 5
+                                      ((40, 23, 11), (3, 2, 1), (37, 21, 10)),    # padded rows
+                                      ((64, 31, 9), (0, 0, 0), (64, 31, 9))):     # whole volume
+                a = rand_codes(rng, fmt, dims[::-1])
+                b = rand_codes(rng, fmt, dims[::-1])
+                d = rand_codes(rng, fmt, dims[::-1])
+                for op in ("Sum", "SafeDiff"):
+                    for mapping in ((0.0, 1.0), (-1.0, 3.0)):
+                        out = g.arith(op, [fmt] * 3, [mapping] * 3, a, b, d.copy(), first, last, (0, 0, 0))
+                        ref = o.arith(op, [fmt] * 3, [mapping] * 3, a, b, d.copy(), first, last, (0, 0, 0))
+                        assert_codes_equal(out, ref, fmt, f"{op} fmt={fmt} {dims} {first}->{last} q={max_quanta}")
+                v = 0.3
+                out = g.fill_range(fmt, (0.0, 1.0), dims, d.copy(), first, last, v)
+                ref = o.fill_range(fmt, (0.0, 1.0), dims, d.copy(), first, last, v)
+                assert_codes_equal(out, ref, fmt, f"fill fmt={fmt} {dims} {first}->{last}")
+    finally:
+        lib.vktHipSetTuningKnob(b"pointwise.max_quanta_per_launch", -1)
+
+
+@pytest.mark.parametrize("padded", [0, 1])
+def test_pointwise_padded_rows_knob(g, o, padded):
+    """Multi-row boxes with and without padded row items (the scalar-edge pass they replace)."""
+    from volkit_amd._lib import lib
+    rng = np.random.default_rng(40 + padded)
+    assert lib.vktHipSetTuningKnob(b"pointwise.padded_rows", padded) == 0
+    try:
+        for fmt in (4, 5, 7):
+            a = rand_codes(rng, fmt, (9, 21, 1200))
+            b = rand_codes(rng, fmt, (9, 21, 1200))
+            d = rand_codes(rng, fmt, (9, 21, 1200))
+            for first, last, off in (((1, 1, 1), (1199, 20, 8), (0, 0, 0)), ((7, 0, 0), (9, 21, 9), (0, 0, 0)),
+                                     ((2, 3, 1), (1030, 15, 7), (8, 2, 1)), ((0, 0, 0), (1200, 21, 9), (0, 0, 0)),
+                                     ((3, 2, 2), (1027, 19, 8), (0, 0, 0))):
+                for op in ("SafeSum", "AbsDiff", "Quot"):
+                    out = g.arith(op, [fmt] * 3, [(0.0, 1.0)] * 3, a, b, d.copy(), first, last, off)
+                    ref = o.arith(op, [fmt] * 3, [(0.0, 1.0)] * 3, a, b, d.copy(), first, last, off)
+                    assert_codes_equal(out, ref, fmt, f"{op} fmt={fmt} {first}->{last} off={off} padded={padded}")
+    finally:
+        lib.vktHipSetTuningKnob(b"pointwise.padded_rows", -1)
+
+
 def test_arithmetic_float_bit_patterns(g, o):
     # every float bit pattern class, including NaN payloads, denormals and infinities
     rng = np.random.default_rng(17)

@@ -191,6 +191,7 @@ SIGNATURES = {
     "vktHipKernelScopeBegin": (c_err, [C.c_char_p, P(C.c_void_p), P(C.c_void_p)]),
     "vktHipKernelScopeEnd": (c_err, [C.c_void_p]),
     "vktHipReportError": (c_err, [C.c_char_p]),
+    "vktHipSetTuningKnob": (c_err, [C.c_char_p, C.c_int64]),
     "vktHipAllocate": (c_err, [P(C.c_void_p), C.c_size_t]),
     "vktHipFree": (c_err, [C.c_void_p]),
     "vktHipMemcpy": (c_err, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]),

@@ -15,6 +15,7 @@
 #pragma once
 
 #include "KernelCommon.hpp"
+#include "../runtime/Runtime.hpp"
 
 #include <type_traits>
 #include "volkit_c.h"
@@ -45,8 +46,12 @@ namespace hipk
         int64_t nx, ny, nz;      // raw extents (scalar path)
         int64_t vnx, vny, vnz;   // collapsed extents (vector path)
         int64_t vnx8;            // end of the 8-aligned middle of each row: vhead + 8 * chunks
-        int64_t vhead;           // scalar head voxels per row (common misalignment phase)
+        int64_t vhead;           // scalar head voxels per row (common misalignment phase);
+                                 // padded rows: -(phase), the row's first item starts before it
         int32_t fast32;          // all index arithmetic fits 32 bits -> magic-number division
+        int32_t padded;          // rows > 1: every row is covered by whole 8-voxel items from the
+                                 // 8-aligned voxel at or below its start; items that straddle the
+                                 // row ends load the whole vector and store only the row's voxels
         FastDiv divCpr, divVny;  // vector path: items -> (row, chunk), row -> (j, k)
         FastDiv divNx, divNy;    // scalar path: voxel -> (i, j, k)
     };
@@ -103,16 +108,6 @@ namespace hipk
             return BPV == 1 ? 4 : BPV == 2 ? 2 : 1;  // 2 KiB per stream
     }
 
-    // Unroll of a launch: the 3-stream UInt16 ops over ONE collapsed row (whole volumes, the
-    // metric's SumRange) take 1 KiB per stream -- alternating-process A/B on MI355X: 1024^3
-    // SumRange 0.950-0.954 ms vs 0.968-0.984 ms at 2 KiB; strided sub-boxes ran 3-4 % slower
-    // with 1 KiB, copies (NS = 1) saw no difference, so everything else keeps vecUnroll.
-    template <int NS, int BPV>
-    constexpr int vecUnrollOneRow()
-    {
-        return NS == 2 && BPV == 2 ? 1 : vecUnroll<NS, BPV>();
-    }
-
     // MODE 0: one collapsed row; 1: rows, 32-bit magic division; 2: rows, 64-bit division.
     template <int NS, int BPV, int MODE, class F>
     __device__ __forceinline__ void pointwiseVecItem(Operand const& d, Operand const& s1, Operand const& s2,
@@ -128,7 +123,8 @@ namespace hipk
         }
         else
         {
-            uint64_t j, k, x;
+            uint64_t j, k, x;   // x wraps below 0 for a padded row's first item: the sums below
+                                // are taken modulo 2^64 and land on the 8-aligned voxel
             if constexpr (MODE == 1)
             {
                 uint32_t r = fdiv(static_cast<uint32_t>(it), g.divCpr);
@@ -161,6 +157,40 @@ namespace hipk
     template <class F>
     struct IsPacked16<F, decltype(void(F::kPacked16))> { static constexpr bool value = F::kPacked16; };
 
+    // Padded rows: the row-relative x of item `it` (for the straddle test of its store); the
+    // same division pointwiseVecItem does for the item's offsets.
+    template <int MODE>
+    __device__ __forceinline__ int64_t paddedRowX(Geom const& g, uint64_t it)
+    {
+        if constexpr (MODE == 1)
+        {
+            uint32_t r = fdiv(static_cast<uint32_t>(it), g.divCpr);
+            return g.vhead + (static_cast<int64_t>(static_cast<uint32_t>(it) - r * g.divCpr.d) << 3);
+        }
+        else
+        {
+            uint64_t const cpr = static_cast<uint64_t>(g.vnx8 - g.vhead) >> 3;
+            return g.vhead + static_cast<int64_t>((it % cpr) << 3);
+        }
+    }
+
+    // Store the 8 codes of an item whose row-relative start is x; only voxels inside [0, vnx)
+    // of the row are written when the item straddles a row end.
+    template <int BPV>
+    __device__ __forceinline__ void storeItemMasked(uint8_t* base, uint64_t od, int64_t x, int64_t vnx,
+                                                    uint32_t const (&c)[8])
+    {
+        if (x >= 0 && x + 8 <= vnx)
+            store8<BPV, true>(base, od, c);
+        else
+        {
+#pragma unroll
+            for (int v = 0; v < 8; ++v)
+                if (x + v >= 0 && x + v < vnx)
+                    storeCode<BPV>(base, od + v, c[v]);
+        }
+    }
+
     template <int NS, int BPV, int MODE, int U, class F>
     __device__ __forceinline__ void pointwiseVecSpan(Operand const& d, Operand const& s1, Operand const& s2,
                                                      Geom const& g, uint64_t beg, uint64_t end, F const& f)
@@ -172,12 +202,26 @@ namespace hipk
         {
             // same schedule as below (all loads of a quantum before its stores), no unpacking:
             // 16 B of each source -> 16 B of dst
-            auto apply = [&](u32x4 const& a, u32x4 const& b, uint64_t od) {
+            auto apply = [&](u32x4 const& a, u32x4 const& b, uint64_t od, uint64_t item) {
                 u32x4 r;
                 r.x = f.pk(a.x, b.x);
                 r.y = f.pk(a.y, b.y);
                 r.z = f.pk(a.z, b.z);
                 r.w = f.pk(a.w, b.w);
+                if constexpr (MODE != 0)
+                {
+                    if (g.padded)
+                    {
+                        int64_t const x = paddedRowX<MODE>(g, item);
+                        if (x < 0 || x + 8 > g.vnx)
+                        {
+                            uint32_t c[8] = {r.x & 0xFFFFu, r.x >> 16, r.y & 0xFFFFu, r.y >> 16,
+                                             r.z & 0xFFFFu, r.z >> 16, r.w & 0xFFFFu, r.w >> 16};
+                            storeItemMasked<2>(d.data, od, x, g.vnx, c);
+                            return;
+                        }
+                    }
+                }
                 __builtin_nontemporal_store(r, reinterpret_cast<u32x4*>(d.data + 2 * od));
             };
             for (; it + (kUnroll - 1) * static_cast<uint64_t>(kVecBlock) < end; it += kQ)
@@ -195,13 +239,13 @@ namespace hipk
                 }
 #pragma unroll
                 for (int u = 0; u < kUnroll; ++u)
-                    apply(a[u], b[u], od[u]);
+                    apply(a[u], b[u], od[u], it + static_cast<uint64_t>(u) * kVecBlock);
             }
             for (; it < end; it += kVecBlock)
             {
                 uint64_t o1, o2, od;
                 pointwiseVecItem<NS, BPV, MODE, F>(d, s1, s2, g, it, o1, o2, od);
-                apply(loadVec<u32x4, true>(s1.data + 2 * o1), loadVec<u32x4, true>(s2.data + 2 * o2), od);
+                apply(loadVec<u32x4, true>(s1.data + 2 * o1), loadVec<u32x4, true>(s2.data + 2 * o2), od, it);
             }
             return;
         }
@@ -227,6 +271,15 @@ namespace hipk
 #pragma unroll
                 for (int v = 0; v < 8; ++v)
                     o[v] = f(NS >= 1 ? a[u][v] : 0u, NS >= 2 ? b[u][v] : 0u);
+                if constexpr (MODE != 0)
+                {
+                    if (g.padded)
+                    {
+                        storeItemMasked<BPV>(d.data, od[u],
+                                             paddedRowX<MODE>(g, it + static_cast<uint64_t>(u) * kVecBlock), g.vnx, o);
+                        continue;
+                    }
+                }
                 store8<BPV, true>(d.data, od[u], o);
             }
         }
@@ -242,6 +295,14 @@ namespace hipk
 #pragma unroll
             for (int v = 0; v < 8; ++v)
                 o[v] = f(NS >= 1 ? a[v] : 0u, NS >= 2 ? b[v] : 0u);
+            if constexpr (MODE != 0)
+            {
+                if (g.padded)
+                {
+                    storeItemMasked<BPV>(d.data, od, paddedRowX<MODE>(g, it), g.vnx, o);
+                    continue;
+                }
+            }
             store8<BPV, true>(d.data, od, o);
         }
     }
@@ -258,7 +319,8 @@ namespace hipk
     // as one launch of 8 M workgroups and 8.3 ms as 1 M-workgroup launches (the per-voxel rate
     // of the 1024^3 case); launches of 4 M workgroups were as slow as one.  Row edges are
     // handled by the first launch only.
-    constexpr uint64_t kMaxQuantaPerLaunch = 1ull << 20;
+    constexpr uint64_t kMaxQuantaPerLaunch = 1ull << 20;   // default of the knob below
+    static_assert(kMaxQuantaPerLaunch > 0, "");
 
     template <int NS, int BPV, int U, class F>
     __global__ __launch_bounds__(kVecBlock) void pointwiseVecKernel(Operand d, Operand s1, Operand s2, Geom g, F f,
@@ -269,9 +331,11 @@ namespace hipk
         uint64_t const items = cpr * rows;
         uint64_t const ny = static_cast<uint64_t>(g.vny);
         constexpr uint64_t kQ = static_cast<uint64_t>(kVecBlock) * U;
-        for (uint64_t q = qBase + blockIdx.x; q < qEnd && q * kQ < items; q += gridDim.x)
+        for (uint64_t q = qBase + blockIdx.x; q < qEnd; q += gridDim.x)
         {
             uint64_t const beg = q * kQ;
+            if (beg >= items)
+                break;
             uint64_t const end = beg + kQ < items ? beg + kQ : items;
             if (rows == 1)
                 pointwiseVecSpan<NS, BPV, 0, U>(d, s1, s2, g, beg, end, f);
@@ -282,9 +346,11 @@ namespace hipk
         }
 
         // scalar edges of every row: head [0, vhead) and tail [vnx8, vnx)
+        if (g.padded || !edges)
+            return;
         uint64_t const head = static_cast<uint64_t>(g.vhead);
         uint64_t const tailLen = head + static_cast<uint64_t>(g.vnx - g.vnx8);
-        if (tailLen == 0 || !edges)
+        if (tailLen == 0)
             return;
         uint64_t const tid = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
         uint64_t const stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
@@ -361,17 +427,20 @@ namespace hipk
                 uint64_t const rows = static_cast<uint64_t>(p.g.vny) * static_cast<uint64_t>(p.g.vnz);
                 uint64_t items = rows * static_cast<uint64_t>((p.g.vnx8 - p.g.vhead) / 8);
                 // enough threads for the scalar row edges too (narrow boxes are all edge)
-                uint64_t edgeItems = rows * static_cast<uint64_t>(p.g.vhead + (p.g.vnx - p.g.vnx8));
+                uint64_t edgeItems = p.g.padded ? 0 : rows * static_cast<uint64_t>(p.g.vhead + (p.g.vnx - p.g.vnx8));
                 uint64_t edgeBlocks = (edgeItems + kVecBlock - 1) / kVecBlock;
                 edgeBlocks = edgeBlocks < 4096 ? edgeBlocks : 4096;
                 auto launch = [&](auto unroll) {
                     constexpr int U = decltype(unroll)::value;
                     constexpr uint64_t kQ = static_cast<uint64_t>(kVecBlock) * U;
+                    // (row-aligned quanta -- no 128-B line of a row shared by two workgroups --
+                    // measured no better in an in-process A/B: 800^3 sub-box of 1024^3 at x0 = 100
+                    // 0.603 vs 0.589 ms flat, at x0 = 96 0.537 vs 0.551 ms)
                     uint64_t const quanta = (items + kQ - 1) / kQ;
-                    // the launch split counts items (kMaxQuantaPerLaunch quanta of the default
-                    // unroll): a 1024^3 SumRange stays one launch with 1-KiB quanta (A/B: one or
-                    // two launches per call ran equally fast at 1024^3 and 2048^3)
-                    constexpr uint64_t maxQ = kMaxQuantaPerLaunch * vecUnroll<NS, BPV>() / U;
+                    // the launch split counts quanta of the default unroll (knob
+                    // pointwise.max_quanta_per_launch, default kMaxQuantaPerLaunch)
+                    uint64_t const maxQ = static_cast<uint64_t>(rt::knob(rt::Knob::PointwiseMaxQuanta)) *
+                                              vecUnroll<NS, BPV>() / U;
                     uint64_t q0 = 0;
                     do
                     {
@@ -383,11 +452,9 @@ namespace hipk
                         q0 += n;
                     } while (q0 < quanta);
                 };
-                constexpr int kU = vecUnroll<NS, BPV>(), kU1 = vecUnrollOneRow<NS, BPV>();
-                if (kU1 != kU && rows == 1)
-                    launch(std::integral_constant<int, kU1>{});
-                else
-                    launch(std::integral_constant<int, kU>{});
+                // (a 1-KiB quantum for the one-row 3-stream UInt16 ops measured the same as 2 KiB
+                // in an in-process A/B, 0.985 vs 0.986 ms for 1024^3 SumRange: one unroll for all)
+                launch(std::integral_constant<int, vecUnroll<NS, BPV>()>{});
                 return vktNoError;
             }
         }

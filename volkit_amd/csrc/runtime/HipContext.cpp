@@ -12,6 +12,7 @@
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <iostream>
 #include <mutex>
 
@@ -177,6 +178,23 @@ namespace rt
 
     bool kernelTimingEnabled() { return ctx().timing.load() != 0; }
 
+    namespace
+    {
+        struct KnobDef
+        {
+            char const* name;
+            int64_t def;
+        };
+        constexpr KnobDef kKnobs[] = {
+            {"pointwise.padded_rows", 1},
+            {"pointwise.max_quanta_per_launch", int64_t(1) << 20},
+        };
+        static_assert(sizeof(kKnobs) / sizeof(kKnobs[0]) == static_cast<size_t>(Knob::Count), "knob table");
+        std::atomic<int64_t> gKnobs[static_cast<int>(Knob::Count)] = {{kKnobs[0].def}, {kKnobs[1].def}};
+    } // namespace
+
+    int64_t knob(Knob k) { return gKnobs[static_cast<int>(k)].load(std::memory_order_relaxed); }
+
     // Every backend call is also a roctx range named after the reference's backend function
     // (e.g. "SumRange_hip"), so `rocprofv3 --marker-trace` attributes kernels to API calls.
     ScopedKernelTimer::ScopedKernelTimer(char const* name, bool log)
@@ -333,6 +351,21 @@ vktError vktHipKernelScopeEnd(vktHipKernelScope scope)
     vktError e = rt::finishLaunch(scope->name);
     delete scope;   // stops the timer, pops the roctx range
     return e;
+}
+
+vktError vktHipSetTuningKnob(char const* name, int64_t value)
+{
+    if (name == nullptr)
+        return rt::fail("vktHipSetTuningKnob: null name");
+    for (size_t i = 0; i < static_cast<size_t>(rt::Knob::Count); ++i)
+        if (std::strcmp(name, rt::kKnobs[i].name) == 0)
+        {
+            if (value <= 0 && i == static_cast<size_t>(rt::Knob::PointwiseMaxQuanta))
+                value = rt::kKnobs[i].def;
+            rt::gKnobs[i].store(value < 0 ? rt::kKnobs[i].def : value);
+            return vktNoError;
+        }
+    return rt::fail((std::string("vktHipSetTuningKnob: unknown knob ") + name).c_str());
 }
 
 vktError vktHipReportError(char const* message)

@@ -69,6 +69,17 @@ namespace rt
 
     bool kernelTimingEnabled();
 
+    // Tuning knobs (vktHipSetTuningKnob): defaults are the measured best settings; tests and
+    // tools/bench_configs.py change them to reach rare code paths (multi-launch splits) and to
+    // A/B a choice inside one process on the same allocations.
+    enum class Knob : int
+    {
+        PointwisePaddedRows = 0,       // 1: multi-row boxes use padded row items (no scalar edges)
+        PointwiseMaxQuanta,            // launch split, in quanta of the default unroll (2^20)
+        Count
+    };
+    int64_t knob(Knob k);
+
     // Stream ordering between the compute stream and the side copy stream (event based):
     // the copy stream waits for everything queued on the compute stream so far / the compute
     // stream waits for everything queued on the copy stream so far.
