@@ -69,6 +69,9 @@ namespace hipk
         uint8_t const* rowChain;
         // resamplePlaneKernel: this launch runs tasks [taskBase, taskEnd) (planeChunks)
         uint32_t taskBase, taskEnd;
+        // optimistic gather: nonzero iff any rowChain byte is set (written by rowChainKernel);
+        // the fix-up pass returns at once when it is 0 (the common case).  nullptr = scan.
+        uint32_t const* anyChain;
     };
 
     // Plane-layout launches are split into at most kMaxPlaneTasksPerLaunch one-wave workgroups
