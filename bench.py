@@ -280,17 +280,23 @@ def main():
         # (the unit-mapping integer specialisations of DESIGN §4.1 do not apply)
         fp = [HipVolumeView_t(v.data, v.dimX, v.dimY, v.dimZ, v.dataFormat, -1.0, 3.0)
               for v in (sview, rview, bview, dview)]
-        el_fp, (res_fp, sum_fp) = ctx.timed(pipeline(fp), args.steps, max(5, args.warmup // 2), 2)
-        msfp = el_fp * 1e3 / args.steps
-        out["mapping_m1_3"] = {
-            "value": round(total_vox / (msfp / 1e3) / 1e9, 3), "unit": "Gvoxels/s", "ms_per_step": round(msfp, 4),
-            "kernels_ms": {"Resample": round(res_fp, 4), "SumRange": round(sum_fp, 4)},
-            "SumRange_achieved": gbs(sum_bytes, sum_fp),
-            "SumRange_frac": round(sum_bytes / (sum_fp / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
-            "resample_achieved": gbs(res_bytes, res_fp),
-            "note": "same workload and buffers, mapping [-1,3] on all volumes (float-codec kernels)",
-        }
-        out["f32_linear"] = f32_linear(ctx, vkt, slab, lib, args, layout_n, stream)
+        def mapping_m1_3():
+            el_fp, (res_fp, sum_fp) = ctx.timed(pipeline(fp), args.steps, max(5, args.warmup // 2), 2)
+            msfp = el_fp * 1e3 / args.steps
+            return {
+                "value": round(total_vox / (msfp / 1e3) / 1e9, 3), "unit": "Gvoxels/s",
+                "ms_per_step": round(msfp, 4),
+                "kernels_ms": {"Resample": round(res_fp, 4), "SumRange": round(sum_fp, 4)},
+                "SumRange_achieved": gbs(sum_bytes, sum_fp),
+                "SumRange_frac": round(sum_bytes / (sum_fp / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                "resample_achieved": gbs(res_bytes, res_fp),
+                "note": "same workload and buffers, mapping [-1,3] on all volumes (float-codec kernels)",
+            }
+        # a failing secondary measurement is recorded in the line instead of losing the headline
+        # (the failures these guard against -- a library error, an allocation -- are the same on
+        # every rank, so no rank is left waiting in a collective)
+        out["mapping_m1_3"] = secondary(mapping_m1_3)
+        out["f32_linear"] = secondary(lambda: f32_linear(ctx, vkt, slab, lib, args, layout_n, stream))
 
     if not args.no_copy_peak:
         # achievable streaming rate on this box: the library's own CopyRange of one volume
@@ -337,6 +343,15 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def secondary(fn):
+    """Run one secondary measurement; an exception becomes {"error": ...} in the JSON line."""
+    try:
+        return fn()
+    except Exception as e:   # noqa: BLE001 -- reported, not swallowed
+        print(f"bench: secondary measurement failed: {e!r}", file=sys.stderr, flush=True)
+        return {"error": repr(e)[:300]}
 
 
 def f32_linear(ctx, vkt, slab, lib, args, layout_n, stream):

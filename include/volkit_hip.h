@@ -69,7 +69,8 @@ typedef struct vktHipKernelScope_impl* vktHipKernelScope;
 VKTAPI vktError vktHipKernelScopeBegin(const char* name, vktHipKernelScope* scope, void** hipStream);
 VKTAPI vktError vktHipKernelScopeEnd(vktHipKernelScope scope);
 /* Tuning knobs (process-wide; a negative value restores the default): "pointwise.padded_rows"
- * (1), "pointwise.max_quanta_per_launch" (2^20).  For tests and
+ * (1), "pointwise.max_quanta_per_launch" (2^20), "pointwise.general" (1; 0 sends boxes the
+ * aligned vector path cannot take to the per-voxel kernel).  For tests and
  * in-process A/B measurements; unknown names return vktInvalidValue. */
 VKTAPI vktError vktHipSetTuningKnob(const char* name, int64_t value);
 /* Record `message` as the calling thread's last error, log it; returns vktInvalidValue. */

@@ -1,0 +1,198 @@
+"""The general vector path of the pointwise engine (kernels/Pointwise.hpp, pointwiseGenKernel)
+vs the oracle: boxes the aligned path cannot take -- operands at different 8-voxel phases
+(CopyRange x0 = 3 -> 0, arithmetic dstOffset), row pitches that are not multiples of 8,
+clamped CopyRange sources (halo copies past every border, reference Copy_serial.hpp:38-40),
+format conversion between voxel sizes, view pointers that are not 16-B aligned.  Volumes live
+in plain device buffers and the backend is called through the C ABI (include/volkit_hip.h),
+so one case costs a kernel launch, not a volume migration.  Bit-exact (NaN matches NaN)."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from backends import CODE_DTYPE, OracleBackend
+from test_gpu_parity import assert_codes_equal, rand_codes
+
+pytestmark = pytest.mark.gpu
+
+BPV = {1: 1, 2: 2, 3: 4, 4: 1, 5: 2, 6: 4, 7: 4}
+OPS = ["Sum", "Diff", "Prod", "Quot", "AbsDiff", "SafeSum", "SafeDiff", "SafeProd", "SafeQuot", "SafeAbsDiff"]
+
+
+@pytest.fixture(scope="module")
+def o():
+    return OracleBackend()
+
+
+@pytest.fixture(scope="module")
+def lib():
+    import torch
+    from volkit_amd._lib import lib as L
+    torch.cuda.set_device(0)
+    return L
+
+
+class Dev:
+    """A volume's codes in a device buffer at byte offset `pad` (view pointer pad bytes past a
+    256-B aligned allocation)."""
+
+    def __init__(self, codes, fmt, mapping=(0.0, 1.0), pad=0):
+        import torch
+        from volkit_amd._lib import HipVolumeView_t
+        self.codes = np.ascontiguousarray(codes)
+        self.fmt, self.pad = fmt, pad
+        z, y, x = codes.shape
+        raw = self.codes.view(np.uint8).reshape(-1)
+        self.buf = torch.zeros(raw.size + pad + 64, dtype=torch.uint8, device="cuda")
+        self.buf[pad:pad + raw.size].copy_(torch.from_numpy(raw.copy()))
+        self.view = HipVolumeView_t(self.buf.data_ptr() + pad, x, y, z, fmt, float(mapping[0]), float(mapping[1]))
+
+    def read(self):
+        import torch
+        torch.cuda.synchronize()
+        raw = self.buf[self.pad:self.pad + self.codes.nbytes].cpu().numpy()
+        return raw.view(CODE_DTYPE[self.fmt]).reshape(self.codes.shape)
+
+
+def vec(x):
+    from volkit_amd._lib import Vec3i_t
+    return Vec3i_t(*x)
+
+
+def last_error():
+    from volkit_amd import _lib
+    return _lib.last_error()
+
+
+def knob(lib, on):
+    assert lib.vktHipSetTuningKnob(b"pointwise.general", 1 if on else 0) == 0
+
+
+def copy_case(lib, o, sfmt, dfmt, smap, dmap, src, dst_init, first, last, off, spad=0, dpad=0, what=""):
+    s = Dev(src, sfmt, smap, spad)
+    d = Dev(dst_init, dfmt, dmap, dpad)
+    err = lib.vktHipCopyRange(d.view, s.view, vec(first), vec(last), vec(off))
+    assert err == 0, f"{what}: {last_error()}"
+    ref = o.copy_range(dfmt, dmap, None, dst_init.copy(), sfmt, smap, src, first, last, off)
+    assert_codes_equal(d.read(), ref, dfmt, what)
+
+
+@pytest.mark.parametrize("sfmt,dfmt", [(4, 4), (5, 5), (7, 7), (2, 2), (6, 6)])
+def test_copy_phase_sweep_bytewise(lib, o, sfmt, dfmt):
+    """Every source x phase against several destination phases, rows not multiples of 8,
+    ranges clamped on every side."""
+    rng = np.random.default_rng(7 * sfmt + dfmt)
+    src = rand_codes(rng, sfmt, (5, 7, 29))          # dims (29, 7, 5)
+    dinit = rand_codes(rng, dfmt, (6, 6, 43))        # dims (43, 6, 6)
+    for sx in range(9):
+        for dx in (0, 1, 3, 5, 7, 8):
+            # interior box, then a box clamped at x/y/z on both sides
+            for first, last in (((sx, 1, 1), (sx + 19, 6, 4)), ((sx - 5, -2, -1), (sx + 30, 4, 5))):
+                n = [l - f for f, l in zip(first, last)]
+                off = (dx, 0, 0) if n[0] + dx <= 43 else (43 - n[0], 0, 0)
+                copy_case(lib, o, sfmt, dfmt, (0.0, 1.0), (0.0, 1.0), src, dinit, first, last, off,
+                          what=f"copy {sfmt} sx={sx} dx={dx} {first}->{last}+{off}")
+
+
+@pytest.mark.parametrize("sfmt,dfmt", [(5, 4), (4, 5), (4, 7), (7, 4), (5, 7), (7, 5), (2, 6), (6, 2), (1, 5), (5, 3)])
+@pytest.mark.parametrize("maps", [((0.0, 1.0), (0.0, 1.0)), ((0.0, 1.0), (-1.0, 3.0)), ((0.25, 7.5), (0.0, 1.0))])
+def test_copy_convert_phases(lib, o, sfmt, dfmt, maps):
+    """CopyRange with unmap -> map between voxel sizes (general path with mixed sizes)."""
+    rng = np.random.default_rng(13 * sfmt + dfmt)
+    src = rand_codes(rng, sfmt, (4, 9, 37))
+    dinit = rand_codes(rng, dfmt, (7, 12, 43))
+    for first, last, off in (((0, 0, 0), (37, 9, 4), (0, 0, 0)), ((3, 1, 0), (30, 8, 4), (1, 0, 1)),
+                             ((-2, -1, -1), (39, 10, 5), (0, 0, 0)), ((5, 2, 1), (12, 3, 2), (7, 5, 3))):
+        copy_case(lib, o, sfmt, dfmt, maps[0], maps[1], src, dinit, first, last, off,
+                  what=f"convert {sfmt}->{dfmt} {maps} {first}->{last}+{off}")
+
+
+@pytest.mark.parametrize("fmt", [4, 5, 7])
+def test_copy_unaligned_view_pointers(lib, o, fmt):
+    """View pointers one voxel (not 16 B) past an aligned address, source and destination."""
+    b = BPV[fmt]
+    rng = np.random.default_rng(fmt)
+    src = rand_codes(rng, fmt, (3, 5, 64))
+    dinit = rand_codes(rng, fmt, (3, 5, 64))
+    for spad, dpad in ((b, 0), (0, b), (3 * b, 5 * b), (8 * b, 8 * b)):
+        for first, last, off in (((0, 0, 0), (64, 5, 3), (0, 0, 0)), ((1, 0, 0), (60, 5, 3), (2, 0, 0)),
+                                 ((-1, 0, 0), (63, 5, 3), (0, 0, 0))):
+            copy_case(lib, o, fmt, fmt, (0.0, 1.0), (0.0, 1.0), src, dinit, first, last, off, spad, dpad,
+                      what=f"copy pads {spad},{dpad} {first}->{last}+{off}")
+
+
+def test_copy_narrow_rows(lib, o):
+    """Boxes 1..9 voxels wide: every item straddles a row end or a clamped border."""
+    rng = np.random.default_rng(3)
+    for fmt in (4, 5, 7):
+        src = rand_codes(rng, fmt, (4, 5, 11))
+        dinit = rand_codes(rng, fmt, (4, 6, 13))
+        for w in range(1, 10):
+            for fx in (-3, 0, 1, 6):
+                copy_case(lib, o, fmt, fmt, (0.0, 1.0), (0.0, 1.0), src, dinit, (fx, -1, 0), (fx + w, 5, 4), (2, 0, 0),
+                          what=f"narrow fmt={fmt} w={w} fx={fx}")
+
+
+@pytest.mark.parametrize("fmt", [4, 5, 7])
+@pytest.mark.parametrize("mapping", [(0.0, 1.0), (-1.0, 3.0)])
+def test_arith_dst_offset_phases(lib, o, fmt, mapping):
+    """Arithmetic with an x dstOffset of every phase: destination and sources at different
+    phases (the packed UInt16 / UInt8 unit-mapping functors and the float codec)."""
+    rng = np.random.default_rng(fmt)
+    a = rand_codes(rng, fmt, (4, 6, 45))
+    b = rand_codes(rng, fmt, (4, 6, 45))
+    dinit = rand_codes(rng, fmt, (5, 7, 53))
+    from volkit_amd._lib import lib as L
+    for op in OPS:
+        idx = OPS.index(op)
+        for dx in range(8):
+            for first, last in (((0, 0, 0), (45, 6, 4)), ((3, 1, 1), (40, 5, 3))):
+                da, db, dd = Dev(a, fmt, mapping), Dev(b, fmt, mapping, 2 * BPV[fmt]), Dev(dinit, fmt, mapping)
+                assert L.vktHipArithmeticRange(idx, dd.view, da.view, db.view, vec(first), vec(last),
+                                               vec((dx, 1, 1))) == 0
+                ref = o.arith(op, [fmt] * 3, [mapping] * 3, a, b, dinit.copy(), first, last, (dx, 1, 1))
+                assert_codes_equal(dd.read(), ref, fmt, f"{op} fmt={fmt} {mapping} dx={dx} {first}->{last}")
+
+
+def test_general_knob_matches_scalar_kernel(lib, o):
+    """The same phase-shifted and clamped cases through the general path and, with the knob
+    off, through the per-voxel kernel: both equal the oracle."""
+    rng = np.random.default_rng(11)
+    src = rand_codes(rng, 5, (6, 10, 70))
+    dinit = rand_codes(rng, 5, (6, 10, 70))
+    try:
+        for on in (True, False):
+            knob(lib, on)
+            for first, last, off in (((3, 0, 0), (70, 10, 6), (0, 0, 0)), ((-4, -3, -2), (66, 12, 7), (0, 0, 0)),
+                                     ((1, 2, 3), (69, 9, 5), (0, 1, 0))):
+                n = [l - f for f, l in zip(first, last)]
+                if n[0] > 70 or n[1] > 10 or n[2] > 6:
+                    continue
+                copy_case(lib, o, 5, 5, (0.0, 1.0), (0.0, 1.0), src, dinit, first, last, off,
+                          what=f"knob={on} {first}->{last}+{off}")
+    finally:
+        knob(lib, True)
+        assert lib.vktHipSetTuningKnob(b"pointwise.general", -1) == 0
+
+
+def test_general_multi_launch(lib, o):
+    """Launch split of the general path (knob pointwise.max_quanta_per_launch = 1)."""
+    rng = np.random.default_rng(12)
+    src = rand_codes(rng, 5, (5, 9, 300))
+    dinit = rand_codes(rng, 5, (6, 11, 301))
+    assert lib.vktHipSetTuningKnob(b"pointwise.max_quanta_per_launch", 1) == 0
+    try:
+        copy_case(lib, o, 5, 5, (0.0, 1.0), (0.0, 1.0), src, dinit, (3, -1, 0), (300, 10, 5), (1, 0, 0),
+                  what="multi-launch")
+    finally:
+        assert lib.vktHipSetTuningKnob(b"pointwise.max_quanta_per_launch", -1) == 0
+
+
+def test_copy_halo_large(lib, o):
+    """A clamped halo copy at a size with many workgroups: 258 x 130 x 9 UInt16 from first =
+    (-1, -1, -1) of a 256 x 128 x 7 volume, oracle on the whole result."""
+    rng = np.random.default_rng(21)
+    src = rand_codes(rng, 5, (7, 128, 256))
+    dinit = np.zeros((9, 130, 258), np.uint16)
+    copy_case(lib, o, 5, 5, (0.0, 1.0), (0.0, 1.0), src, dinit, (-1, -1, -1), (257, 129, 8), (0, 0, 0),
+              what="halo 258x130x9")

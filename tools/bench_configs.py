@@ -201,6 +201,33 @@ def main():
         report("weak Resample 1024^3->768^3 Float32 Linear (gather)", timed(lambda: lib.vktHipResample(Rv, S, 1), R),
                4 * 1024 ** 3 + 4 * 768 ** 3, 768 ** 3)
         free(S, Rv)
+    if want("general"):
+        # boxes the aligned vector path cannot take: operands at different 8-voxel phases,
+        # clamped (halo) CopyRange sources, mixed formats
+        m = 1024
+        A, B, D = alloc((m,) * 3, 5, seed=1), alloc((m,) * 3, 5, seed=2), alloc((m,) * 3, 5)
+        nv = (m - 3) * m * m
+        report("general CopyRange 1021x1024x1024 UInt16 src x0=3 -> dst x0=0 (phase shift)",
+               timed(lambda: lib.vktHipCopyRange(D, A, Vec3i_t(3, 0, 0), Vec3i_t(m, m, m), o), R), 4 * nv, nv)
+        nv = 1000 * 1000 * 1000
+        report("general CopyRange 1000^3 of 1024^3 UInt16 src (5,7,9) -> dst (1,2,3)",
+               timed(lambda: lib.vktHipCopyRange(D, A, Vec3i_t(5, 7, 9), Vec3i_t(1005, 1007, 1009), Vec3i_t(1, 2, 3)),
+                     R), 4 * nv, nv)
+        nv = (m - 3) * m * m
+        report("general SumRange 1021x1024x1024 UInt16 dstOffset x=3 (phase shift)",
+               timed(lambda: lib.vktHipArithmeticRange(0, D, A, B, o, Vec3i_t(m - 3, m, m), Vec3i_t(3, 0, 0)), R),
+               6 * nv, nv)
+        free(D)
+        H = alloc((m - 2,) * 3, 5)   # halo copy: (m-2)^3 dst from first=-1 .. m-1 (clamped border)
+        h = m - 2
+        report(f"general CopyRange clamped halo: {h}^3 from first=(-1,-1,-1) of {h - 2}^3-box UInt16",
+               timed(lambda: lib.vktHipCopyRange(H, A, Vec3i_t(-1, -1, -1), Vec3i_t(h - 1, h - 1, h - 1), o), R),
+               4 * h ** 3, h ** 3)
+        free(H)
+        F = alloc((m,) * 3, 7)
+        report("general CopyRange 1024^3 UInt16 -> Float32 (convert)",
+               timed(lambda: lib.vktHipCopyRange(F, A, o, Vec3i_t(m, m, m), o), R), 6 * m ** 3, m ** 3)
+        free(A, B, F)
     if want("gather"):
         # non-integer ratios (gather path): up/down-sampling 768^3 <-> 1024^3, all dst formats
         cases = [(768, 1024, 5, 1), (1024, 768, 5, 1), (768, 1024, 4, 1), (768, 1024, 7, 0), (768, 1024, 7, 1),

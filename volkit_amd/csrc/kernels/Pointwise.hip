@@ -34,7 +34,7 @@ namespace hipk
         Operand* ops[3] = {&p.d, &p.s1, &p.s2};
         int nops = ns + 1;
 
-        bool vec = true;
+        bool vec = true, uniform = true, anyClamp = false, gen = true;
         uint32_t bpv = p.d.bpv;
         for (int i = 0; i < nops; ++i)
         {
@@ -45,11 +45,17 @@ namespace hipk
             o.sz = dx * dy;
             if (o.clamp || o.bpv != bpv)
                 vec = false;
+            uniform = uniform && o.bpv == bpv;
+            anyClamp = anyClamp || o.clamp;
+            // general path: 1/2/4-byte voxels at voxel-aligned addresses
+            gen = gen && (o.bpv == 1 || o.bpv == 2 || o.bpv == 4) &&
+                  reinterpret_cast<uintptr_t>(o.data) % o.bpv == 0;
         }
 
-        // collapse rows that are contiguous in every operand
+        // collapse rows that are contiguous in every operand (not when a source clamps: its
+        // rows repeat at the border)
         int64_t vnx = nx, vny = ny, vnz = nz;
-        bool mergeY = vny > 1;
+        bool mergeY = vny > 1 && !anyClamp;
         for (int i = 0; i < nops && mergeY; ++i)
             mergeY = ops[i]->sy == vnx;
         if (mergeY)
@@ -57,7 +63,7 @@ namespace hipk
             vnx *= vny;
             vny = 1;
         }
-        if (vny == 1 && vnz > 1)
+        if (vny == 1 && vnz > 1 && !anyClamp)
         {
             bool mergeZ = true;
             for (int i = 0; i < nops && mergeZ; ++i)
@@ -120,6 +126,23 @@ namespace hipk
             vec = false;
         p.vec = vec;
         p.bpv = bpv;
+
+        // general vector path (Pointwise.hpp): any phase, pitch or clamp; voxel sizes may differ
+        // (launchPointwise takes it for uniform sizes, convertBox for mixed ones)
+        GenGeom& gg = p.gg;
+        gg.vnx = vnx;
+        gg.vny = vny;
+        gg.vnz = vnz;
+        gg.cpr = static_cast<uint64_t>((vnx + 14) / 8);
+        uint64_t const rows = static_cast<uint64_t>(vny) * static_cast<uint64_t>(vnz);
+        gg.items = rows * gg.cpr;
+        gg.dph = static_cast<int32_t>((reinterpret_cast<uintptr_t>(p.d.data) / p.d.bpv) & 7);
+        gg.fast32 = gg.items < (1ull << 32) ? 1 : 0;
+        gg.anyClamp = anyClamp ? 1 : 0;
+        gg.divCpr = makeFastDiv(static_cast<uint32_t>(gg.cpr));
+        gg.divVny = makeFastDiv(static_cast<uint32_t>(vny));
+        p.gen = gen && !vec && rt::knob(rt::Knob::PointwiseGeneral) != 0;
+        p.uniform = uniform;
         return p;
     }
 
@@ -180,6 +203,41 @@ namespace hipk
     }
 
     // ---- conversion (shared with Resample's same-dims branch) ---------------------------
+    // Source and destination voxel sizes differ: general vector path, formats fixed at compile
+    // time for the UInt8 / UInt16 / Float32 pairs, run-time formats otherwise.
+    template <int FS, int FD, int BS, int BD>
+    vktError convertFixed(PwPlan const& p, float slo, float shi, MapParams const& dm, hipStream_t s)
+    {
+        return dm.rangeIsPow2 ? launchGen<1, BD, BS, BS>(p, ConvertF<FS, FD, 1>{FS, FD, slo, shi, dm}, s)
+                              : launchGen<1, BD, BS, BS>(p, ConvertF<FS, FD, 2>{FS, FD, slo, shi, dm}, s);
+    }
+
+    template <int BS, int BD>
+    vktError convertDyn(PwPlan const& p, int32_t fs, int32_t fd, float slo, float shi, MapParams const& dm,
+                        hipStream_t s)
+    {
+        return launchGen<1, BD, BS, BS>(p, ConvertF<kDyn, kDyn>{fs, fd, slo, shi, dm}, s);
+    }
+
+    vktError convertMixed(PwPlan const& p, int32_t fs, int32_t fd, float slo, float shi, MapParams const& dm,
+                          hipStream_t s)
+    {
+        constexpr int U8 = codec::FmtUInt8, U16 = codec::FmtUInt16, F32 = codec::FmtFloat32;
+        if (fs == U8 && fd == U16) return convertFixed<U8, U16, 1, 2>(p, slo, shi, dm, s);
+        if (fs == U8 && fd == F32) return convertFixed<U8, F32, 1, 4>(p, slo, shi, dm, s);
+        if (fs == U16 && fd == U8) return convertFixed<U16, U8, 2, 1>(p, slo, shi, dm, s);
+        if (fs == U16 && fd == F32) return convertFixed<U16, F32, 2, 4>(p, slo, shi, dm, s);
+        if (fs == F32 && fd == U8) return convertFixed<F32, U8, 4, 1>(p, slo, shi, dm, s);
+        if (fs == F32 && fd == U16) return convertFixed<F32, U16, 4, 2>(p, slo, shi, dm, s);
+        uint32_t const bs = p.s1.bpv, bd = p.d.bpv;
+        if (bs == 1 && bd == 2) return convertDyn<1, 2>(p, fs, fd, slo, shi, dm, s);
+        if (bs == 1 && bd == 4) return convertDyn<1, 4>(p, fs, fd, slo, shi, dm, s);
+        if (bs == 2 && bd == 1) return convertDyn<2, 1>(p, fs, fd, slo, shi, dm, s);
+        if (bs == 2 && bd == 4) return convertDyn<2, 4>(p, fs, fd, slo, shi, dm, s);
+        if (bs == 4 && bd == 1) return convertDyn<4, 1>(p, fs, fd, slo, shi, dm, s);
+        return convertDyn<4, 2>(p, fs, fd, slo, shi, dm, s);
+    }
+
     vktError convertBox(vktHipVolumeView_t dst, vktHipVolumeView_t src, vktVec3i_t srcOrigin, bool clampSrc,
                         vktVec3i_t dstOrigin, int64_t nx, int64_t ny, int64_t nz)
     {
@@ -189,7 +247,7 @@ namespace hipk
         PwPlan p = planPointwise(1, od, os, os, nx, ny, nz);
         MapParams dm = codec::makeMapParams(dst.mappingLo, dst.mappingHi);
         int32_t fs = src.dataFormat, fd = dst.dataFormat;
-        if (p.vec && fs == fd)
+        if ((p.vec || (p.gen && p.uniform)) && fs == fd)
         {
             if (fs == codec::FmtUInt8)
                 return dm.rangeIsPow2 ? launchPointwise<1, 1>(p, ConvertF<codec::FmtUInt8, codec::FmtUInt8, 1>{fs, fd, src.mappingLo, src.mappingHi, dm}, s)
@@ -201,6 +259,8 @@ namespace hipk
                 return dm.rangeIsPow2 ? launchPointwise<1, 4>(p, ConvertF<codec::FmtFloat32, codec::FmtFloat32, 1>{fs, fd, src.mappingLo, src.mappingHi, dm}, s)
                                       : launchPointwise<1, 4>(p, ConvertF<codec::FmtFloat32, codec::FmtFloat32, 2>{fs, fd, src.mappingLo, src.mappingHi, dm}, s);
         }
+        if (p.gen && !p.uniform)
+            return convertMixed(p, fs, fd, src.mappingLo, src.mappingHi, dm, s);
         return launchByBpv<1>(p, ConvertF<kDyn, kDyn>{fs, fd, src.mappingLo, src.mappingHi, dm}, s);
     }
 

@@ -18,6 +18,7 @@
 #include "../runtime/Runtime.hpp"
 
 #include <type_traits>
+#include <utility>
 #include "volkit_c.h"
 
 namespace vkt
@@ -55,6 +56,8 @@ namespace hipk
         FastDiv divCpr, divVny;  // vector path: items -> (row, chunk), row -> (j, k)
         FastDiv divNx, divNy;    // scalar path: voxel -> (i, j, k)
     };
+
+    struct PassF;   // PointwiseOps.hpp: dst = source code (bytewise CopyRange)
 
     // Sentinel for "format known only at run time".
     constexpr int kDyn = -1;
@@ -370,6 +373,350 @@ namespace hipk
         }
     }
 
+    // ---- general vector path ---------------------------------------------------------
+    // For boxes the aligned path above cannot take: operands at different 8-voxel phases (a
+    // CopyRange from x0 = 3 to x0 = 0, an arithmetic dstOffset), row pitches that are not
+    // multiples of 8, clamped CopyRange sources (halo copies past the border), and sources of a
+    // different voxel size than the destination (CopyRange with format conversion).
+    //
+    // Items are 8 destination voxels aligned to the destination's memory: row (j, k) of the
+    // box is covered by cpr = ceil((vnx + 7) / 8) chunks starting at x = -(phase of the row
+    // start), so every item stores 8*BD aligned bytes (one 16-B vector for UInt16) and items
+    // that straddle a row end store only the row's voxels.  A source's 8 voxels start at any
+    // byte offset s: the lane loads the aligned 16-B words covering them (2 words, 3 for
+    // 4-byte voxels; a neighbour lane's words are the same lines, served by L1) and shifts
+    // them in registers -- a per-lane barrel shifter: select by 8 bytes, by 4 bytes, then
+    // v_alignbyte_b32 by s & 3 (~15 VALU ops per 16 B).  Items whose source voxels leave the
+    // source row (clamped x at the volume border) or the box row (straddling items) go voxel
+    // by voxel with the reference clamp (Copy_serial.hpp:38-40); y and z clamp per row.
+    // Traffic = the algorithmic bytes: each source line is fetched from HBM once (the words
+    // a lane shares with its neighbour hit L1 / L2).
+    struct GenGeom
+    {
+        int64_t vnx, vny, vnz;   // box (collapsed when no operand clamps)
+        uint64_t cpr;            // chunks per row: ceil((vnx + 7) / 8)
+        uint64_t items;          // rows * cpr
+        int32_t dph;             // (d.data / BD) & 7: phase of destination voxel 0
+        int32_t fast32;          // items and rows fit 32 bits
+        int32_t anyClamp;        // some source clamps (then rows are not collapsed)
+        FastDiv divCpr, divVny;
+    };
+
+    // 8 consecutive codes starting at voxel `voxel` of a B-byte-per-voxel volume at any byte
+    // offset: out = 2*B dwords of the little-endian byte stream.  Only words holding needed bytes
+    // are loaded (an unneeded trailing word is replaced by the last needed one), so no load
+    // leaves the 16-B blocks of the valid voxels.  The shifter's selects use constant indices
+    // only (index_sequence folds): a select between two elements of a loop-indexed array is
+    // folded into a dynamically indexed load before unrolling, which sends the array to scratch.
+    template <std::size_t... T>
+    __device__ __forceinline__ void shiftSel(uint32_t const* in, uint32_t* out, bool c, int by,
+                                             std::index_sequence<T...>)
+    {
+        ((out[T] = c ? in[T + by] : in[T]), ...);
+    }
+
+    template <std::size_t... T>
+    __device__ __forceinline__ void shiftAlign(uint32_t const* in, uint32_t* out, uint32_t r,
+                                               std::index_sequence<T...>)
+    {
+        ((out[T] = __builtin_amdgcn_alignbyte(in[T + 1], in[T], r)), ...);
+    }
+
+    // The window is split in two halves so that a lane issues the loads of all its items
+    // before it shifts the first one (the shift waits for its words).
+    template <int B>
+    struct Window
+    {
+        static constexpr int NW = B == 4 ? 3 : 2;   // 16-B words covering 8*B bytes at any offset
+        uint32_t w[4 * NW];
+        uint32_t s;                                 // byte offset of the first voxel in word 0
+    };
+
+    // Voxels [lo, hi) of the 8 (0 <= lo < hi <= 8) are the valid ones (an item straddling a row
+    // end): words are clamped to the ones holding valid voxels, the other codes are garbage.
+    template <int B>
+    __device__ __forceinline__ void loadWindow(uint8_t const* data, int64_t voxel, int32_t lo, int32_t hi,
+                                               Window<B>& win)
+    {
+        uint8_t const* const p = data + voxel * B;   // may lie before the row (x < 0): address only
+        uint32_t const s = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(p) & 15u);
+        uint8_t const* const p0 = p - s;
+        uint8_t const* const vf = p + lo * B;
+        uint8_t const* const vl = p + hi * B - 1;
+        uint8_t const* const pf = vf - (reinterpret_cast<uintptr_t>(vf) & 15u);
+        uint8_t const* const pl = vl - (reinterpret_cast<uintptr_t>(vl) & 15u);
+        auto word = [&](int i) {
+            uint8_t const* a = p0 + 16 * i;
+            a = a < pf ? pf : a;
+            return *reinterpret_cast<u32x4 const*>(a < pl ? a : pl);
+        };
+        win.s = s;
+        u32x4 const v0 = word(0);
+        u32x4 const v1 = word(1);
+        win.w[0] = v0.x; win.w[1] = v0.y; win.w[2] = v0.z; win.w[3] = v0.w;
+        win.w[4] = v1.x; win.w[5] = v1.y; win.w[6] = v1.z; win.w[7] = v1.w;
+        if constexpr (Window<B>::NW == 3)
+        {
+            u32x4 const v2 = word(2);
+            win.w[8] = v2.x; win.w[9] = v2.y; win.w[10] = v2.z; win.w[11] = v2.w;
+        }
+    }
+
+    template <int B>
+    __device__ __forceinline__ void shiftWindow(Window<B> const& win, uint32_t (&out)[2 * B])
+    {
+        constexpr int NO = 2 * B;   // output dwords
+        uint32_t a[NO + 2], b[NO + 1];
+        shiftSel(win.w, a, (win.s & 8u) != 0, 2, std::make_index_sequence<NO + 2>{});
+        shiftSel(a, b, (win.s & 4u) != 0, 1, std::make_index_sequence<NO + 1>{});
+        shiftAlign(b, out, win.s & 3u, std::make_index_sequence<NO>{});
+    }
+
+    template <int B>
+    __device__ __forceinline__ void unpack8(uint32_t const (&w)[2 * B], uint32_t (&c)[8])
+    {
+#pragma unroll
+        for (int v = 0; v < 8; ++v)
+        {
+            if constexpr (B == 1)
+                c[v] = (w[v / 4] >> (8 * (v % 4))) & 0xFFu;
+            else if constexpr (B == 2)
+                c[v] = (w[v / 2] >> (16 * (v % 2))) & 0xFFFFu;
+            else
+                c[v] = w[v];
+        }
+    }
+
+    // Voxel index of box x = 0 in row (j, k) of operand o, and of x = 0 of the volume row it
+    // reads (clamped rows: the reference clamps y and z, x per voxel).
+    __device__ __forceinline__ int64_t genRowStart(Operand const& o, uint64_t j, uint64_t k, int64_t& row0)
+    {
+        if (!o.clamp)
+        {
+            int64_t const r = o.base + static_cast<int64_t>(k) * o.sz + static_cast<int64_t>(j) * o.sy;
+            row0 = r - o.origin[0];
+            return r;
+        }
+        int32_t const y = clampRefI(o.origin[1] + static_cast<int32_t>(j), 0, o.dims[1] - 1);
+        int32_t const z = clampRefI(o.origin[2] + static_cast<int32_t>(k), 0, o.dims[2] - 1);
+        row0 = (static_cast<int64_t>(z) * o.dims[1] + y) * static_cast<int64_t>(o.dims[0]);
+        return row0 + o.origin[0];
+    }
+
+    template <int BS>
+    __device__ __forceinline__ uint32_t genLoadOne(Operand const& o, int64_t rowStart, int64_t row0, int64_t x)
+    {
+        if (!o.clamp)
+            return loadCode<BS>(o.data, static_cast<uint64_t>(rowStart + x));
+        int32_t const sx = clampRefI(o.origin[0] + static_cast<int32_t>(x), 0, o.dims[0] - 1);
+        return loadCode<BS>(o.data, static_cast<uint64_t>(row0 + sx));
+    }
+
+    __device__ __forceinline__ bool genInterior(Operand const& o, int64_t x)
+    {
+        return !o.clamp || (o.origin[0] + x >= 0 && o.origin[0] + x + 8 <= o.dims[0]);
+    }
+
+    // 8 codes -> 2*B dwords of packed codes
+    template <int B, std::size_t... V>
+    __device__ __forceinline__ void packCodes(uint32_t const (&c)[8], Window<B>& win, std::index_sequence<V...>)
+    {
+        ((win.w[V] = B == 1 ? c[4 * V] | c[4 * V + 1] << 8 | c[4 * V + 2] << 16 | c[4 * V + 3] << 24
+                   : B == 2 ? c[2 * V] | c[2 * V + 1] << 16 : c[V]), ...);
+    }
+
+    // Clamped x-border item (a clamped source reads voxels left of x = 0 or right of dimX - 1):
+    // voxel by voxel with the reference clamp, in a pass after the streamed items (its loads
+    // would otherwise be merged with the window registers and make the wave wait early).
+    template <int B>
+    __device__ __forceinline__ void loadBorder(Operand const& o, int64_t rowStart, int64_t row0, int64_t x,
+                                               uint32_t (&c)[8])
+    {
+#pragma unroll
+        for (int v = 0; v < 8; ++v)
+            c[v] = genLoadOne<B>(o, rowStart, row0, x + v);
+    }
+
+    // MODE 1/2: items [beg, end) packed across rows (32-bit / 64-bit division).
+    template <int NS, int BD, int B1, int B2, int MODE, int U, class F>
+    __device__ __forceinline__ void pointwiseGenSpan(Operand const& d, Operand const& s1, Operand const& s2,
+                                                     GenGeom const& g, uint64_t beg, uint64_t end, F const& f)
+    {
+        constexpr bool kPack = BD == 2 && B1 == 2 && B2 == 2 && NS == 2 && IsPacked16<F>::value;
+        constexpr bool kPass = NS == 1 && BD == B1 && std::is_same<F, PassF>::value;
+        Window<B1> wa[U];
+        Window<NS >= 2 ? B2 : 1> wb[U];
+        int64_t xs[U], od[U], r1[U], r10[U], r2[U], r20[U];
+        bool win[U], border[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+        {
+            uint64_t j, k, c;
+            uint64_t const it = beg + threadIdx.x + static_cast<uint64_t>(u) * kVecBlock;
+            bool live = it < end;
+            uint64_t const ii = live ? it : beg;
+            if constexpr (MODE == 1)
+            {
+                uint32_t const rr = fdiv(static_cast<uint32_t>(ii), g.divCpr);
+                c = static_cast<uint32_t>(ii) - rr * g.divCpr.d;
+                uint32_t const kk = fdiv(rr, g.divVny);
+                k = kk;
+                j = rr - kk * g.divVny.d;
+            }
+            else
+            {
+                uint64_t const r = ii / g.cpr;
+                c = ii - r * g.cpr;
+                j = r % static_cast<uint64_t>(g.vny);
+                k = r / static_cast<uint64_t>(g.vny);
+            }
+            int64_t const dr = d.base + static_cast<int64_t>(k) * d.sz + static_cast<int64_t>(j) * d.sy;
+            int64_t const x = 8 * static_cast<int64_t>(c) - ((g.dph + dr) & 7);
+            xs[u] = x;
+            od[u] = dr + x;
+            live = live && x < g.vnx;
+            r1[u] = r10[u] = r2[u] = r20[u] = 0;
+            if constexpr (NS >= 1)
+                r1[u] = genRowStart(s1, j, k, r10[u]);
+            if constexpr (NS >= 2)
+                r2[u] = genRowStart(s2, j, k, r20[u]);
+            bool const clampX = NS >= 1 && g.anyClamp && !(genInterior(s1, x) && (NS < 2 || genInterior(s2, x)));
+            border[u] = live && clampX;
+            win[u] = live && !clampX;
+            // voxels of the item inside the box row
+            int32_t const lo = x < 0 ? static_cast<int32_t>(-x) : 0;
+            int32_t const hi = x + 8 > g.vnx ? static_cast<int32_t>(g.vnx - x) : 8;
+            if (win[u])
+            {
+                if constexpr (NS >= 1)
+                    loadWindow<B1>(s1.data, r1[u] + x, lo, hi, wa[u]);
+                if constexpr (NS >= 2)
+                    loadWindow<B2>(s2.data, r2[u] + x, lo, hi, wb[u]);
+            }
+        }
+        auto result = [&](uint32_t const* a, uint32_t const* b, uint32_t (&rd)[2 * BD]) {
+            if constexpr (kPass)
+            {
+#pragma unroll
+                for (int m = 0; m < 2 * BD; ++m)
+                    rd[m] = a[m];
+            }
+            else if constexpr (kPack)
+            {
+#pragma unroll
+                for (int m = 0; m < 4; ++m)
+                    rd[m] = f.pk(a[m], b[m]);
+            }
+            else
+            {
+                uint32_t aa[2 * B1], bb[2 * (NS >= 2 ? B2 : 1)];
+#pragma unroll
+                for (int m = 0; m < 2 * B1; ++m)
+                    aa[m] = NS >= 1 ? a[m] : 0u;
+#pragma unroll
+                for (int m = 0; m < 2 * (NS >= 2 ? B2 : 1); ++m)
+                    bb[m] = NS >= 2 ? b[m] : 0u;
+                uint32_t ca[8], cb[8] = {0, 0, 0, 0, 0, 0, 0, 0}, oc[8];
+                unpack8<B1>(aa, ca);
+                if constexpr (NS >= 2)
+                    unpack8<B2>(bb, cb);
+#pragma unroll
+                for (int v = 0; v < 8; ++v)
+                    oc[v] = f(NS >= 1 ? ca[v] : 0u, cb[v]);
+                Window<BD> t;
+                packCodes<BD>(oc, t, std::make_index_sequence<2 * BD>{});
+#pragma unroll
+                for (int m = 0; m < 2 * BD; ++m)
+                    rd[m] = t.w[m];
+            }
+        };
+        auto store = [&](int u, uint32_t const (&rd)[2 * BD]) {
+            uint64_t const o = static_cast<uint64_t>(od[u]);
+            if (xs[u] >= 0 && xs[u] + 8 <= g.vnx)
+            {
+                if constexpr (BD == 1)
+                    *reinterpret_cast<u32x2*>(d.data + o) = u32x2{rd[0], rd[1]};
+                else if constexpr (BD == 2)
+                    __builtin_nontemporal_store(u32x4{rd[0], rd[1], rd[2], rd[3]},
+                                                reinterpret_cast<u32x4*>(d.data + 2 * o));
+                else
+                {
+                    __builtin_nontemporal_store(u32x4{rd[0], rd[1], rd[2], rd[3]}, reinterpret_cast<u32x4*>(d.data + 4 * o));
+                    __builtin_nontemporal_store(u32x4{rd[4], rd[5], rd[6], rd[7]},
+                                                reinterpret_cast<u32x4*>(d.data + 4 * o + 16));
+                }
+            }
+            else
+            {
+                // an item straddling a row end: only the row's voxels
+                uint32_t oc[8];
+                unpack8<BD>(rd, oc);
+#pragma unroll
+                for (int v = 0; v < 8; ++v)
+                    if (xs[u] + v >= 0 && xs[u] + v < g.vnx)
+                        storeCode<BD>(d.data, o + v, oc[v]);
+            }
+        };
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+        {
+            if (!win[u])
+                continue;
+            uint32_t a[2 * B1], b[2 * (NS >= 2 ? B2 : 1)], rd[2 * BD];
+            if constexpr (NS >= 1)
+                shiftWindow<B1>(wa[u], a);
+            if constexpr (NS >= 2)
+                shiftWindow<B2>(wb[u], b);
+            result(a, b, rd);
+            store(u, rd);
+        }
+        if (!g.anyClamp)
+            return;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+        {
+            if (!border[u])
+                continue;
+            uint32_t ca[8], cb[8], a[2 * B1], b[2 * (NS >= 2 ? B2 : 1)], rd[2 * BD];
+            loadBorder<B1>(s1, r1[u], r10[u], xs[u], ca);
+            if constexpr (NS >= 2)
+                loadBorder<B2>(s2, r2[u], r20[u], xs[u], cb);
+            Window<B1> ta;
+            packCodes<B1>(ca, ta, std::make_index_sequence<2 * B1>{});
+#pragma unroll
+            for (int m = 0; m < 2 * B1; ++m)
+                a[m] = ta.w[m];
+            if constexpr (NS >= 2)
+            {
+                Window<B2> tb;
+                packCodes<B2>(cb, tb, std::make_index_sequence<2 * B2>{});
+#pragma unroll
+                for (int m = 0; m < 2 * B2; ++m)
+                    b[m] = tb.w[m];
+            }
+            result(a, b, rd);
+            store(u, rd);
+        }
+    }
+
+    template <int NS, int BD, int B1, int B2, int U, class F>
+    __global__ __launch_bounds__(kVecBlock) void pointwiseGenKernel(Operand d, Operand s1, Operand s2, GenGeom g, F f,
+                                                                   uint64_t qBase, uint64_t qEnd)
+    {
+        constexpr uint64_t kQ = static_cast<uint64_t>(kVecBlock) * U;
+        for (uint64_t q = qBase + blockIdx.x; q < qEnd; q += gridDim.x)
+        {
+            uint64_t const beg = q * kQ;
+            if (beg >= g.items)
+                break;
+            uint64_t const end = beg + kQ < g.items ? beg + kQ : g.items;
+            if (g.fast32)
+                pointwiseGenSpan<NS, BD, B1, B2, 1, U>(d, s1, s2, g, beg, end, f);
+            else
+                pointwiseGenSpan<NS, BD, B1, B2, 2, U>(d, s1, s2, g, beg, end, f);
+        }
+    }
+
     template <int NS, class F>
     __global__ __launch_bounds__(kBlock) void pointwiseScalarKernel(Operand d, Operand s1, Operand s2, Geom g, F f)
     {
@@ -409,9 +756,35 @@ namespace hipk
     {
         Operand d, s1, s2;
         Geom g;
+        GenGeom gg;
         bool vec;        // vector path eligible (aligned, unclamped, uniform voxel size)
-        uint32_t bpv;    // common bytes per voxel when vec
+        bool gen;        // general vector path eligible (any phase / pitch / clamp)
+        bool uniform;    // every operand has the destination's voxel size
+        uint32_t bpv;    // destination bytes per voxel
     };
+
+    // General vector path launch (operand voxel sizes BD, B1, B2 fixed at compile time).
+    template <int NS, int BD, int B1, int B2, class F>
+    vktError launchGen(PwPlan const& p, F const& f, hipStream_t stream)
+    {
+        constexpr int U = NS == 0 ? 2 : vecUnroll<NS, BD>();
+        constexpr uint64_t kQ = static_cast<uint64_t>(kVecBlock) * U;
+        // (measured and rejected: one row segment per workgroup, row coordinates on the scalar
+        // unit -- 1021-voxel rows split into two 65-chunk segments, SumRange with dstOffset x = 3
+        // at 1021 x 1024^2: 1.15 -> 1.62 ms; half-size quanta cost more than the index math saved)
+        GenGeom const& gg = p.gg;
+        uint64_t const quanta = (gg.items + kQ - 1) / kQ;
+        uint64_t const maxQ = static_cast<uint64_t>(rt::knob(rt::Knob::PointwiseMaxQuanta));
+        uint64_t q0 = 0;
+        do
+        {
+            uint64_t const n = quanta - q0 < maxQ ? quanta - q0 : maxQ;
+            hipLaunchKernelGGL((pointwiseGenKernel<NS, BD, B1, B2, U, F>), dim3(static_cast<unsigned>(n > 0 ? n : 1)),
+                               dim3(kVecBlock), 0, stream, p.d, p.s1, p.s2, gg, f, q0, q0 + n);
+            q0 += n;
+        } while (q0 < quanta);
+        return vktNoError;
+    }
 
     // Builds the plan for `ns` sources over a box of extent n (all > 0).
     PwPlan planPointwise(int ns, Operand d, Operand s1, Operand s2, int64_t nx, int64_t ny, int64_t nz);
@@ -457,6 +830,8 @@ namespace hipk
                 launch(std::integral_constant<int, vecUnroll<NS, BPV>()>{});
                 return vktNoError;
             }
+            if (p.gen && p.uniform && p.bpv == BPV)
+                return launchGen<NS, BPV, BPV, BPV>(p, f, stream);
         }
         uint64_t total = static_cast<uint64_t>(p.g.nx) * static_cast<uint64_t>(p.g.ny) * static_cast<uint64_t>(p.g.nz);
         unsigned grid = streamingGrid(total, kBlock);

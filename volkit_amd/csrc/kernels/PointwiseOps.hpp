@@ -175,7 +175,7 @@ namespace hipk
     {
         MapParams dm = codec::makeMapParams(d.mappingLo, d.mappingHi);
         int32_t f1 = a.dataFormat, f2 = b.dataFormat, fd = d.dataFormat;
-        if (p.vec && f1 == f2 && f1 == fd)
+        if ((p.vec || (p.gen && p.uniform)) && f1 == f2 && f1 == fd)
         {
         // unit mappings everywhere (the canonical [0, 1] inputs): the codec's lerp and
         // normalisation are identities (codec::decodeUnit / normalise<3>)
