@@ -70,7 +70,9 @@ VKTAPI vktError vktHipKernelScopeBegin(const char* name, vktHipKernelScope* scop
 VKTAPI vktError vktHipKernelScopeEnd(vktHipKernelScope scope);
 /* Tuning knobs (process-wide; a negative value restores the default): "pointwise.padded_rows"
  * (1), "pointwise.max_quanta_per_launch" (2^20), "pointwise.general" (1; 0 sends boxes the
- * aligned vector path cannot take to the per-voxel kernel).  For tests and
+ * aligned vector path cannot take to the per-voxel kernel), "pointwise.merge_sectors" (1; 0 stops
+ * the general path from completing the 64-B sectors at the row ends of a box by rewriting the
+ * destination's own bytes around it).  For tests and
  * in-process A/B measurements; unknown names return vktInvalidValue. */
 VKTAPI vktError vktHipSetTuningKnob(const char* name, int64_t value);
 /* Record `message` as the calling thread's last error, log it; returns vktInvalidValue. */

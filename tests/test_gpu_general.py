@@ -196,3 +196,62 @@ def test_copy_halo_large(lib, o):
     dinit = np.zeros((9, 130, 258), np.uint16)
     copy_case(lib, o, 5, 5, (0.0, 1.0), (0.0, 1.0), src, dinit, (-1, -1, -1), (257, 129, 8), (0, 0, 0),
               what="halo 258x130x9")
+
+
+@pytest.mark.parametrize("fmt", [4, 5, 7])
+def test_sector_completion(lib, o, fmt):
+    """64-B sector completion at the row ends (pointwise.merge_sectors): destinations whose size
+    and start are 64-B aligned, box rows with >= 64-B gaps -- the bytes around each box row in
+    its end sectors are rewritten with their own values; everything outside the box must stay
+    as it was.  Copies (same and shifted phases, clamped), arithmetic, fill; knob on and off."""
+    b = BPV[fmt]
+    sv = 64 // b                      # voxels per sector
+    X = 3 * sv                        # row = 3 sectors
+    rng = np.random.default_rng(50 + fmt)
+    src = rand_codes(rng, fmt, (5, 7, X))
+    src2 = rand_codes(rng, fmt, (5, 7, X))
+    dinit = rand_codes(rng, fmt, (6, 8, X))
+    boxes = [((1, 0, 0), (1 + sv, 7, 5), (0, 0, 0)),            # one sector wide, starts mid-sector
+             ((sv - 1, 1, 1), (2 * sv, 6, 4), (3, 1, 1)),       # shifted destination
+             ((0, 0, 0), (2 * sv, 7, 5), (sv // 2, 1, 1)),      # gap of exactly one sector
+             ((-2, -1, 0), (sv + 3, 6, 5), (5, 0, 1)),          # clamped source
+             ((7, 2, 2), (9, 3, 3), (sv - 1, 4, 4))]            # tiny box straddling a sector end
+    try:
+        for on in (True, False):
+            assert lib.vktHipSetTuningKnob(b"pointwise.merge_sectors", 1 if on else 0) == 0
+            for first, last, off in boxes:
+                copy_case(lib, o, fmt, fmt, (0.0, 1.0), (0.0, 1.0), src, dinit, first, last, off,
+                          what=f"merge={on} copy {first}->{last}+{off}")
+                inside = min(first) >= 0 and last[0] <= X and last[1] <= 7 and last[2] <= 5
+                inside = inside and last[0] + off[0] <= X and last[1] + off[1] <= 8 and last[2] + off[2] <= 6
+                if inside:   # arithmetic writes dst[first + off .. last + off)
+                    for op in ("Sum", "SafeDiff", "Quot"):
+                        da, db, dd = Dev(src, fmt), Dev(src2, fmt), Dev(dinit, fmt)
+                        from volkit_amd._lib import lib as L
+                        assert L.vktHipArithmeticRange(OPS.index(op), dd.view, da.view, db.view, vec(first),
+                                                       vec(last), vec(off)) == 0
+                        ref = o.arith(op, [fmt] * 3, [(0.0, 1.0)] * 3, src, src2, dinit.copy(), first, last, off)
+                        assert_codes_equal(dd.read(), ref, fmt, f"merge={on} {op} {first}->{last}+{off}")
+    finally:
+        assert lib.vktHipSetTuningKnob(b"pointwise.merge_sectors", -1) == 0
+
+
+def test_sector_completion_fill_and_subbox(lib, o):
+    """FillRange and the aligned-phase sub-box (routed to the general path when its rows end
+    inside a sector) on a 64-B aligned destination."""
+    from volkit_amd._lib import lib as L
+    rng = np.random.default_rng(77)
+    for fmt in (4, 5, 7):
+        X = 192 // BPV[fmt] * 2
+        a = rand_codes(rng, fmt, (6, 9, X))
+        bb = rand_codes(rng, fmt, (6, 9, X))
+        dinit = rand_codes(rng, fmt, (6, 9, X))
+        for first, last in (((8, 1, 1), (X - 40, 8, 5)), ((3, 0, 0), (X // 2 + 1, 9, 6)), ((0, 2, 1), (X - 33, 3, 2))):
+            dd = Dev(dinit, fmt)
+            assert L.vktHipFillRange(dd.view, vec(first), vec(last), C.c_float(0.3)) == 0
+            ref = o.fill_range(fmt, (0.0, 1.0), (X, 9, 6), dinit.copy(), first, last, 0.3)
+            assert_codes_equal(dd.read(), ref, fmt, f"fill fmt={fmt} {first}->{last}")
+            da, db, dd = Dev(a, fmt), Dev(bb, fmt), Dev(dinit, fmt)
+            assert L.vktHipArithmeticRange(5, dd.view, da.view, db.view, vec(first), vec(last), vec((0, 0, 0))) == 0
+            ref = o.arith("SafeSum", [fmt] * 3, [(0.0, 1.0)] * 3, a, bb, dinit.copy(), first, last, (0, 0, 0))
+            assert_codes_equal(dd.read(), ref, fmt, f"SafeSum fmt={fmt} {first}->{last}")

@@ -217,6 +217,31 @@ def main():
         report("general SumRange 1021x1024x1024 UInt16 dstOffset x=3 (phase shift)",
                timed(lambda: lib.vktHipArithmeticRange(0, D, A, B, o, Vec3i_t(m - 3, m, m), Vec3i_t(3, 0, 0)), R),
                6 * nv, nv)
+        # references: the aligned path on a multi-row box of the same shape (x0 = 8 -> 0), and the
+        # general path on one collapsed row (whole volume, source view one voxel off)
+        nv = (m - 8) * m * m
+        report("general-ref CopyRange 1016x1024x1024 UInt16 src x0=8 -> dst x0=0 (aligned path, rows)",
+               timed(lambda: lib.vktHipCopyRange(D, A, Vec3i_t(8, 0, 0), Vec3i_t(m, m, m), o), R), 4 * nv, nv)
+        # partial 128-B lines at the row ends: x 64..960 covers whole lines, 64..959 / 63..959 not
+        # in-process A/B of the 64-B sector completion (knob pointwise.merge_sectors), alternating
+        cases = ((64, 960), (64, 959), (63, 959), (64, 952), (64, 944), (64, 928), (100, 900))
+        ab = {}
+        for rnd in range(3):
+            for mg in (1, 0):
+                lib.vktHipSetTuningKnob(b"pointwise.merge_sectors", mg)
+                for x0, x1 in cases:
+                    ab.setdefault((x0, x1, mg), []).append(timed(
+                        lambda: lib.vktHipCopyRange(D, A, Vec3i_t(x0, 0, 0), Vec3i_t(x1, m, m), Vec3i_t(x0, 0, 0)), R))
+        lib.vktHipSetTuningKnob(b"pointwise.merge_sectors", -1)
+        for (x0, x1, mg), ts in sorted(ab.items()):
+            ts.sort()
+            nv = (x1 - x0) * m * m
+            report(f"general-ref CopyRange rows x {x0}..{x1} of 1024^3 UInt16 (same x in src and dst) merge={mg} "
+                   f"(median of 3 rounds, spread {ts[0]:.4f}-{ts[-1]:.4f})", ts[1], 4 * nv, nv)
+        A1 = HipVolumeView_t(A.data + 2, m, m, m - 1, 5, 0.0, 1.0)
+        nv = m * m * (m - 1)
+        report("general-ref CopyRange 1024x1024x1023 UInt16, source view +1 voxel (one collapsed row, shifted)",
+               timed(lambda: lib.vktHipCopyRange(D, A1, o, Vec3i_t(m, m, m - 1), o), R), 4 * nv, nv)
         free(D)
         H = alloc((m - 2,) * 3, 5)   # halo copy: (m-2)^3 dst from first=-1 .. m-1 (clamped border)
         h = m - 2

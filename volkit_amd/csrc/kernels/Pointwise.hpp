@@ -399,6 +399,11 @@ namespace hipk
         int32_t dph;             // (d.data / BD) & 7: phase of destination voxel 0
         int32_t fast32;          // items and rows fit 32 bits
         int32_t anyClamp;        // some source clamps (then rows are not collapsed)
+        int32_t fast;            // 32-bit addressing (pointwiseGenSpanFast): every operand < 4 GiB,
+                                 // row / plane pitches and box rows / planes < 2^24 (24-bit muls)
+        int32_t merge;           // complete the 64-B sectors at the row ends (fast path only)
+        int32_t sv;              // voxels per 64-B sector (64 / BD)
+        int32_t dph64;           // (d.data / BD) mod sv
         FastDiv divCpr, divVny;
     };
 
@@ -699,6 +704,289 @@ namespace hipk
         }
     }
 
+    // ---- the same with 32-bit addressing (GenGeom::fast) ----------------------------------
+    // Measured: the 64-bit version issues ~136 VALU per item (64-bit multiplies, 64-bit pointer
+    // compares for the word clamps) and is VALU-bound (SQ_ACTIVE_INST_VALU x 4 cycles ~ 97 % of
+    // the SIMD cycles for a phase-shifted copy).  Here row offsets are 24-bit multiply-adds,
+    // window words are 32-bit byte offsets from the operand's 16-B aligned base clamped with one
+    // v_med3_i32, and loads / stores address base (scalar) + 32-bit offset.
+    struct FastOp
+    {
+        uint8_t const* abase;   // data & ~15
+        int32_t mis;            // data & 15
+        uint32_t base, sy, sz;  // voxel index of box (0,0,0), row and plane pitch
+    };
+
+    __device__ __forceinline__ FastOp fastOp(Operand const& o)
+    {
+        FastOp r;
+        uintptr_t const a = reinterpret_cast<uintptr_t>(o.data);
+        r.abase = o.data - (a & 15u);
+        r.mis = static_cast<int32_t>(a & 15u);
+        r.base = static_cast<uint32_t>(o.base);
+        r.sy = static_cast<uint32_t>(o.sy);
+        r.sz = static_cast<uint32_t>(o.sz);
+        return r;
+    }
+
+    // voxel index of box x = 0 in row (j, k); clamped rows as genRowStart
+    __device__ __forceinline__ int32_t fastRowStart(Operand const& o, FastOp const& f, uint32_t j, uint32_t k)
+    {
+        if (!o.clamp)
+            return static_cast<int32_t>(f.base + __umul24(k, f.sz) + __umul24(j, f.sy));
+        uint32_t const y = static_cast<uint32_t>(clampRefI(o.origin[1] + static_cast<int32_t>(j), 0, o.dims[1] - 1));
+        uint32_t const z = static_cast<uint32_t>(clampRefI(o.origin[2] + static_cast<int32_t>(k), 0, o.dims[2] - 1));
+        return static_cast<int32_t>(__umul24(z, f.sz) + __umul24(y, f.sy)) + o.origin[0];
+    }
+
+    // voxel: index of the item's first voxel, modulo 2^32 (it lies before voxel 0 for an item
+    // that starts left of the row at the very start of the volume); the words actually loaded
+    // hold valid voxels [lo, hi) only, so their offsets are true non-negative offsets < 2^32.
+    template <int B>
+    __device__ __forceinline__ void loadWindowFast(FastOp const& f, uint32_t voxel, int32_t lo, int32_t hi,
+                                                   Window<B>& win)
+    {
+        uint32_t const bo = voxel * B + static_cast<uint32_t>(f.mis);    // byte offset from abase
+        uint32_t const fo = (bo + static_cast<uint32_t>(lo * B)) & ~15u;   // first / last word holding
+        uint32_t const lw = (bo + static_cast<uint32_t>(hi * B - 1)) & ~15u;   // a valid voxel
+        int32_t const dw = static_cast<int32_t>((bo & ~15u) - fo);         // word 0 relative to fo: -16 or 0
+        int32_t const span = static_cast<int32_t>(lw - fo);
+        win.s = bo & 15u;
+        auto word = [&](int i) {
+            int32_t const o = min(max(dw + 16 * i, 0), span);
+            return *reinterpret_cast<u32x4 const*>(f.abase + (fo + static_cast<uint32_t>(o)));
+        };
+        u32x4 const v0 = word(0);
+        u32x4 const v1 = word(1);
+        win.w[0] = v0.x; win.w[1] = v0.y; win.w[2] = v0.z; win.w[3] = v0.w;
+        win.w[4] = v1.x; win.w[5] = v1.y; win.w[6] = v1.z; win.w[7] = v1.w;
+        if constexpr (Window<B>::NW == 3)
+        {
+            u32x4 const v2 = word(2);
+            win.w[8] = v2.x; win.w[9] = v2.y; win.w[10] = v2.z; win.w[11] = v2.w;
+        }
+    }
+
+    template <int NS, int BD, int B1, int B2, int U, class F>
+    __device__ __forceinline__ void pointwiseGenSpanFast(Operand const& d, Operand const& s1, Operand const& s2,
+                                                         GenGeom const& g, uint32_t beg, uint32_t end, F const& f)
+    {
+        constexpr bool kPack = BD == 2 && B1 == 2 && B2 == 2 && NS == 2 && IsPacked16<F>::value;
+        constexpr bool kPass = NS == 1 && BD == B1 && std::is_same<F, PassF>::value;
+        FastOp const fd = fastOp(d), f1 = fastOp(s1), f2 = fastOp(s2);
+        int32_t const vnx = static_cast<int32_t>(g.vnx);
+        Window<B1> wa[U];
+        Window<NS >= 2 ? B2 : 1> wb[U];
+        uint32_t dd[U][2 * BD];   // merge: the destination's own codes of an edge item
+        int32_t xs[U];
+        uint32_t od[U], r1[U], r2[U], js[U], ks[U];
+        bool win[U], border[U], pad[U];
+        // items start on 8-voxel (merge: 64-B sector) boundaries of the destination
+        uint32_t const unitMask = g.merge ? static_cast<uint32_t>(g.sv - 1) : 7u;
+        uint32_t const dphU = g.merge ? static_cast<uint32_t>(g.dph64) : static_cast<uint32_t>(g.dph);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+        {
+            uint32_t const it = beg + threadIdx.x + static_cast<uint32_t>(u) * kVecBlock;
+            bool live = it < end;
+            uint32_t const ii = live ? it : beg;
+            uint32_t const rr = fdiv(ii, g.divCpr);
+            uint32_t const c = ii - rr * g.divCpr.d;
+            uint32_t const k = fdiv(rr, g.divVny);
+            uint32_t const j = rr - k * g.divVny.d;
+            js[u] = j;
+            ks[u] = k;
+            uint32_t const dr = fd.base + __umul24(k, fd.sz) + __umul24(j, fd.sy);
+            int32_t const ps = static_cast<int32_t>((dphU + dr) & unitMask);
+            int32_t const x = static_cast<int32_t>(8 * c) - ps;
+            xs[u] = x;
+            od[u] = dr + static_cast<uint32_t>(x);   // modulo 2^32, like the window voxels
+            // row's item range: [-ps, vnx) rounded up to the unit (a whole 64-B sector when merging)
+            int32_t const rowEnd = static_cast<int32_t>((static_cast<uint32_t>(ps + vnx) + unitMask) & ~unitMask) - ps;
+            live = live && x < (g.merge ? rowEnd : vnx);
+            bool const boxPart = x + 8 > 0 && x < vnx;   // the item holds voxels of the box row
+            pad[u] = live && !boxPart;                   // merge only: sector completion, no box voxel
+            r1[u] = r2[u] = 0;
+            if constexpr (NS >= 1)
+                r1[u] = static_cast<uint32_t>(fastRowStart(s1, f1, j, k));
+            if constexpr (NS >= 2)
+                r2[u] = static_cast<uint32_t>(fastRowStart(s2, f2, j, k));
+            bool const clampX = NS >= 1 && g.anyClamp && !(genInterior(s1, x) && (NS < 2 || genInterior(s2, x)));
+            border[u] = live && boxPart && clampX;
+            win[u] = live && boxPart && !clampX;
+            int32_t const lo = x < 0 ? -x : 0;
+            int32_t const hi = x + 8 > vnx ? vnx - x : 8;
+            if (win[u])
+            {
+                if constexpr (NS >= 1)
+                    loadWindowFast<B1>(f1, r1[u] + static_cast<uint32_t>(x), lo, hi, wa[u]);
+                if constexpr (NS >= 2)
+                    loadWindowFast<B2>(f2, r2[u] + static_cast<uint32_t>(x), lo, hi, wb[u]);
+            }
+            if (g.merge && live && !(x >= 0 && x + 8 <= vnx))
+            {
+                // edge or pad item: the destination chunk itself (8*BD aligned bytes)
+                uint8_t const* const q = d.data + od[u] * BD;
+                if constexpr (BD == 1)
+                {
+                    u32x2 const v = *reinterpret_cast<u32x2 const*>(q);
+                    dd[u][0] = v.x; dd[u][1] = v.y;
+                }
+                else
+                {
+#pragma unroll
+                    for (int h = 0; h < BD / 2; ++h)
+                    {
+                        u32x4 const v = *reinterpret_cast<u32x4 const*>(q + 16 * h);
+                        dd[u][4 * h] = v.x; dd[u][4 * h + 1] = v.y; dd[u][4 * h + 2] = v.z; dd[u][4 * h + 3] = v.w;
+                    }
+                }
+            }
+        }
+        auto result = [&](uint32_t const* a, uint32_t const* b, uint32_t (&rd)[2 * BD]) {
+            if constexpr (kPass)
+            {
+#pragma unroll
+                for (int m = 0; m < 2 * BD; ++m)
+                    rd[m] = a[m];
+            }
+            else if constexpr (kPack)
+            {
+#pragma unroll
+                for (int m = 0; m < 4; ++m)
+                    rd[m] = f.pk(a[m], b[m]);
+            }
+            else
+            {
+                uint32_t aa[2 * B1], bb[2 * (NS >= 2 ? B2 : 1)];
+#pragma unroll
+                for (int m = 0; m < 2 * B1; ++m)
+                    aa[m] = NS >= 1 ? a[m] : 0u;
+#pragma unroll
+                for (int m = 0; m < 2 * (NS >= 2 ? B2 : 1); ++m)
+                    bb[m] = NS >= 2 ? b[m] : 0u;
+                uint32_t ca[8], cb[8] = {0, 0, 0, 0, 0, 0, 0, 0}, oc[8];
+                unpack8<B1>(aa, ca);
+                if constexpr (NS >= 2)
+                    unpack8<B2>(bb, cb);
+#pragma unroll
+                for (int v = 0; v < 8; ++v)
+                    oc[v] = f(NS >= 1 ? ca[v] : 0u, cb[v]);
+                Window<BD> t;
+                packCodes<BD>(oc, t, std::make_index_sequence<2 * BD>{});
+#pragma unroll
+                for (int m = 0; m < 2 * BD; ++m)
+                    rd[m] = t.w[m];
+            }
+        };
+        auto storeFull = [&](int u, uint32_t const (&rd)[2 * BD]) {
+            uint8_t* const p = d.data + od[u] * BD;
+            if constexpr (BD == 1)
+                *reinterpret_cast<u32x2*>(p) = u32x2{rd[0], rd[1]};
+            else if constexpr (BD == 2)
+                __builtin_nontemporal_store(u32x4{rd[0], rd[1], rd[2], rd[3]}, reinterpret_cast<u32x4*>(p));
+            else
+            {
+                __builtin_nontemporal_store(u32x4{rd[0], rd[1], rd[2], rd[3]}, reinterpret_cast<u32x4*>(p));
+                __builtin_nontemporal_store(u32x4{rd[4], rd[5], rd[6], rd[7]}, reinterpret_cast<u32x4*>(p + 16));
+            }
+        };
+        auto store = [&](int u, uint32_t const (&rd)[2 * BD]) {
+            if (g.merge && !(xs[u] >= 0 && xs[u] + 8 <= vnx))
+            {
+                // the row's voxels from rd, the rest of the chunk from the destination itself: one
+                // whole-chunk store, so every 64-B sector of the row ends is written completely
+                uint32_t oc[8], dc[8];
+                unpack8<BD>(rd, oc);
+                unpack8<BD>(dd[u], dc);
+#pragma unroll
+                for (int v = 0; v < 8; ++v)
+                    oc[v] = xs[u] + v >= 0 && xs[u] + v < vnx ? oc[v] : dc[v];
+                Window<BD> t;
+                packCodes<BD>(oc, t, std::make_index_sequence<2 * BD>{});
+                uint32_t m[2 * BD];
+#pragma unroll
+                for (int i = 0; i < 2 * BD; ++i)
+                    m[i] = t.w[i];
+                storeFull(u, m);
+                return;
+            }
+            if (xs[u] >= 0 && xs[u] + 8 <= vnx)
+            {
+                uint8_t* const p = d.data + od[u] * BD;
+                if constexpr (BD == 1)
+                    *reinterpret_cast<u32x2*>(p) = u32x2{rd[0], rd[1]};
+                else if constexpr (BD == 2)
+                    __builtin_nontemporal_store(u32x4{rd[0], rd[1], rd[2], rd[3]}, reinterpret_cast<u32x4*>(p));
+                else
+                {
+                    __builtin_nontemporal_store(u32x4{rd[0], rd[1], rd[2], rd[3]}, reinterpret_cast<u32x4*>(p));
+                    __builtin_nontemporal_store(u32x4{rd[4], rd[5], rd[6], rd[7]}, reinterpret_cast<u32x4*>(p + 16));
+                }
+            }
+            else
+            {
+                uint32_t oc[8];
+                unpack8<BD>(rd, oc);
+#pragma unroll
+                for (int v = 0; v < 8; ++v)
+                    if (xs[u] + v >= 0 && xs[u] + v < vnx)
+                        storeCode<BD>(d.data + (od[u] + v) * BD, 0, oc[v]);
+            }
+        };
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+        {
+            if (pad[u])
+            {
+                storeFull(u, dd[u]);   // sector completion: the destination's own bytes
+                continue;
+            }
+            if (!win[u])
+                continue;
+            uint32_t a[2 * B1], b[2 * (NS >= 2 ? B2 : 1)], rd[2 * BD];
+            if constexpr (NS >= 1)
+                shiftWindow<B1>(wa[u], a);
+            if constexpr (NS >= 2)
+                shiftWindow<B2>(wb[u], b);
+            result(a, b, rd);
+            store(u, rd);
+        }
+        if (!g.anyClamp)
+            return;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+        {
+            if (!border[u])
+                continue;
+            // clamped x border: voxel by voxel (rows as genRowStart: x = 0 of the volume row)
+            int64_t r10 = 0, r20 = 0;
+            int64_t const q1 = genRowStart(s1, js[u], ks[u], r10);
+            int64_t q2 = 0;
+            if constexpr (NS >= 2)
+                q2 = genRowStart(s2, js[u], ks[u], r20);
+            uint32_t ca[8], cb[8], a[2 * B1], b[2 * (NS >= 2 ? B2 : 1)], rd[2 * BD];
+            loadBorder<B1>(s1, q1, r10, xs[u], ca);
+            if constexpr (NS >= 2)
+                loadBorder<B2>(s2, q2, r20, xs[u], cb);
+            Window<B1> ta;
+            packCodes<B1>(ca, ta, std::make_index_sequence<2 * B1>{});
+#pragma unroll
+            for (int m = 0; m < 2 * B1; ++m)
+                a[m] = ta.w[m];
+            if constexpr (NS >= 2)
+            {
+                Window<B2> tb;
+                packCodes<B2>(cb, tb, std::make_index_sequence<2 * B2>{});
+#pragma unroll
+                for (int m = 0; m < 2 * B2; ++m)
+                    b[m] = tb.w[m];
+            }
+            result(a, b, rd);
+            store(u, rd);
+        }
+    }
+
     template <int NS, int BD, int B1, int B2, int U, class F>
     __global__ __launch_bounds__(kVecBlock) void pointwiseGenKernel(Operand d, Operand s1, Operand s2, GenGeom g, F f,
                                                                    uint64_t qBase, uint64_t qEnd)
@@ -710,7 +998,10 @@ namespace hipk
             if (beg >= g.items)
                 break;
             uint64_t const end = beg + kQ < g.items ? beg + kQ : g.items;
-            if (g.fast32)
+            if (g.fast)
+                pointwiseGenSpanFast<NS, BD, B1, B2, U>(d, s1, s2, g, static_cast<uint32_t>(beg),
+                                                        static_cast<uint32_t>(end), f);
+            else if (g.fast32)
                 pointwiseGenSpan<NS, BD, B1, B2, 1, U>(d, s1, s2, g, beg, end, f);
             else
                 pointwiseGenSpan<NS, BD, B1, B2, 2, U>(d, s1, s2, g, beg, end, f);

@@ -77,6 +77,7 @@ namespace rt
         PointwisePaddedRows = 0,       // 1: multi-row boxes use padded row items (no scalar edges)
         PointwiseMaxQuanta,            // launch split, in quanta of the default unroll (2^20)
         PointwiseGeneral,              // 0: boxes the aligned path cannot take use the scalar kernel
+        PointwiseMergeSectors,         // 0: no 64-B sector completion at row ends (general path)
         Count
     };
     int64_t knob(Knob k);
