@@ -304,3 +304,29 @@ def test_close_rows_large(lib, o):
     hsrc = rand_codes(rng, 5, (6, 30, 1020))
     copy_case(lib, o, 5, 5, (0.0, 1.0), (0.0, 1.0), hsrc, h, (-1, -1, -1), (1021, 31, 7), (0, 0, 0),
               what="span halo 1022x32x8")
+
+
+@pytest.mark.parametrize("fmt", [4, 5, 7])
+def test_sector_completion_aligned_path(lib, o, fmt):
+    """The aligned vector path's sector completion (padded rows, same phase in source and
+    destination, rows ending inside 64-B sectors): CopyRange and FillRange, knob on and off."""
+    from volkit_amd._lib import lib as L
+    b = BPV[fmt]
+    X = 256 // b                                   # 256-B rows: 64-B multiples, room for gaps
+    rng = np.random.default_rng(60 + fmt)
+    src = rand_codes(rng, fmt, (6, 9, X))
+    dinit = rand_codes(rng, fmt, (6, 9, X))
+    cases = [((8, 1, 1), (X - 40, 8, 5)), ((24, 0, 0), (X // 2 + 8, 9, 6)), ((0, 2, 1), (X - 40, 3, 2)),
+             ((40, 1, 0), (48, 8, 6))]
+    try:
+        for on in (True, False):
+            assert lib.vktHipSetTuningKnob(b"pointwise.merge_sectors", 1 if on else 0) == 0
+            for first, last in cases:
+                copy_case(lib, o, fmt, fmt, (0.0, 1.0), (0.0, 1.0), src, dinit, first, last, first,
+                          what=f"aligned merge={on} copy {first}->{last}")
+                dd = Dev(dinit, fmt)
+                assert L.vktHipFillRange(dd.view, vec(first), vec(last), C.c_float(0.7)) == 0
+                ref = o.fill_range(fmt, (0.0, 1.0), (X, 9, 6), dinit.copy(), first, last, 0.7)
+                assert_codes_equal(dd.read(), ref, fmt, f"aligned merge={on} fill {first}->{last}")
+    finally:
+        assert lib.vktHipSetTuningKnob(b"pointwise.merge_sectors", -1) == 0

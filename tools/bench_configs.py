@@ -168,19 +168,23 @@ def main():
         A, B, D = alloc((m,) * 3, 5, seed=1), alloc((m,) * 3, 5, seed=2), alloc((m,) * 3, 5)
         sub0, sub1 = Vec3i_t(100, 100, 100), Vec3i_t(900, 900, 900)
         a0, a1 = Vec3i_t(96, 100, 100), Vec3i_t(896, 900, 900)
-        # in-process A/B of the padded-row items (knob) on the same allocations, alternating
+        # in-process A/B of the 64-B sector completion (knob pointwise.merge_sectors) on the same
+        # allocations, alternating: SafeSumRange and CopyRange over the sub-boxes
         ab = {}
         for rnd in range(4):
-            for pad in (1, 0):
-                lib.vktHipSetTuningKnob(b"pointwise.padded_rows", pad)
+            for mg in (1, 0):
+                lib.vktHipSetTuningKnob(b"pointwise.merge_sectors", mg)
                 for lab, f0, f1 in (("x0=100", sub0, sub1), ("x0=96", a0, a1)):
-                    ab.setdefault((lab, pad), []).append(
+                    ab.setdefault(("SafeSumRange", lab, mg), []).append(
                         timed(lambda: lib.vktHipArithmeticRange(5, D, A, B, f0, f1, o), R))
-        lib.vktHipSetTuningKnob(b"pointwise.padded_rows", -1)
-        for (lab, pad), ts in sorted(ab.items()):
+                    ab.setdefault(("CopyRange", lab, mg), []).append(
+                        timed(lambda: lib.vktHipCopyRange(D, A, f0, f1, f0), R))
+        lib.vktHipSetTuningKnob(b"pointwise.merge_sectors", -1)
+        for (op, lab, mg), ts in sorted(ab.items()):
             ts.sort()
-            report(f"weak SafeSumRange 800^3 sub-box of 1024^3 UInt16 {lab} padded={pad} "
-                   f"(median of 4 rounds, spread {ts[0]:.4f}-{ts[-1]:.4f})", ts[len(ts) // 2], 6 * 800 ** 3, 800 ** 3)
+            nb = (6 if op == "SafeSumRange" else 4) * 800 ** 3
+            report(f"weak {op} 800^3 sub-box of 1024^3 UInt16 {lab} merge={mg} "
+                   f"(median of 4 rounds, spread {ts[0]:.4f}-{ts[-1]:.4f})", ts[len(ts) // 2], nb, 800 ** 3)
         # what the multi-row boxes lose: line-aligned row starts, long rows (whole x lines)
         for lab, f0, f1 in (("x 64..864 (rows start on a 128-B line)", Vec3i_t(64, 100, 100), Vec3i_t(864, 900, 900)),
                             ("x 0..800", Vec3i_t(0, 100, 100), Vec3i_t(800, 900, 900)),

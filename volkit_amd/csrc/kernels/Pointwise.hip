@@ -96,6 +96,8 @@ namespace hipk
         // scalar edge pass over every row cost ~20 % (800^3 sub-box of 1024^3 at x0 = 100:
         // 0.666 ms vs 0.533 ms at x0 = 96, where rows have no edges).
         p.g.padded = 0;
+        p.g.merge = 0;
+        p.g.vhead0 = p.g.vend0 = 0;
         if (vny * vnz > 1 && rt::knob(rt::Knob::PointwisePaddedRows) != 0)
         {
             p.g.padded = 1;
@@ -126,6 +128,38 @@ namespace hipk
             vec = false;
         p.vec = vec;
         p.bpv = bpv;
+
+        // Padded rows with 64-B sector completion (a partly written sector costs HBM a
+        // read-modify-write): the items extend to the destination's sector
+        // boundaries; chunks outside the box are its own bytes, loaded and stored back whole;
+        // sources are read only inside the original 8-aligned row items.  Needs one sector phase
+        // for every row, >= 64-B gaps between box rows and planes (no sector holds two rows'
+        // voxels) and a 64-B aligned destination (every sector inside it).  Copies, conversions
+        // and fills only: in-process A/B on an 800^3 sub-box of 1024^3 at x0 = 100, CopyRange
+        // 0.480 -> 0.422 ms, SafeSumRange 0.627 -> 0.649 ms (its partly read source sectors stay).
+        if (vec && p.g.padded && ns <= 1)
+        {
+            int64_t const bd = bpv;
+            int64_t const sv = 64 / bd;
+            uint64_t const dBytes = static_cast<uint64_t>(p.d.dims[0]) * static_cast<uint64_t>(p.d.dims[1]) *
+                                    static_cast<uint64_t>(p.d.dims[2]) * bpv;
+            bool const ok = rt::knob(rt::Knob::PointwiseMergeSectors) != 0 &&
+                            reinterpret_cast<uintptr_t>(p.d.data) % 64 == 0 && dBytes % 64 == 0 &&
+                            (vny <= 1 || ((p.d.sy * bd) % 64 == 0 && (p.d.sy - vnx) * bd >= 64)) &&
+                            (vnz <= 1 || ((p.d.sz * bd) % 64 == 0 && (p.d.sz - (vny - 1) * p.d.sy - vnx) * bd >= 64));
+            int64_t const ph = static_cast<int64_t>(static_cast<uint64_t>(p.d.base) % static_cast<uint64_t>(sv));
+            if (ok && (ph != 0 || (ph + vnx) % sv != 0))
+            {
+                p.g.merge = 1;
+                p.g.vhead0 = p.g.vhead;
+                p.g.vend0 = p.g.vnx8;
+                p.g.vhead = -ph;
+                p.g.vnx8 = -ph + (ph + vnx + sv - 1) / sv * sv;
+                uint64_t const items = static_cast<uint64_t>((p.g.vnx8 - p.g.vhead) / 8) * static_cast<uint64_t>(vny) * vnz;
+                p.g.fast32 = items < (1ull << 32) && total < (1ull << 32) ? 1 : 0;
+                p.g.divCpr = makeFastDiv(static_cast<uint32_t>((p.g.vnx8 - p.g.vhead) / 8));
+            }
+        }
 
         // general vector path (Pointwise.hpp): any phase, pitch or clamp; voxel sizes may differ
         // (launchPointwise takes it for uniform sizes, convertBox for mixed ones)
@@ -166,8 +200,9 @@ namespace hipk
             int64_t const sv = 64 / bd;
             uint64_t const dBytes = static_cast<uint64_t>(p.d.dims[0]) * static_cast<uint64_t>(p.d.dims[1]) *
                                     static_cast<uint64_t>(p.d.dims[2]) * bd;
-            // (copies, conversions and fills only: a 3-stream op measured slower this way, an
-            // 800^3 SafeSumRange sub-box of 1024^3 at x0 = 100: 0.589 -> 0.634 ms)
+            // (copies, conversions and fills only: a 3-stream op measured slower on this path, an
+            // 800^3 SafeSumRange sub-box of 1024^3 at x0 = 100: 0.589 -> 0.634 ms; the aligned
+            // path completes sectors on its own, above)
             bool merge = ns <= 1 && gg.fast && rt::knob(rt::Knob::PointwiseMergeSectors) != 0 &&
                          reinterpret_cast<uintptr_t>(p.d.data) % 64 == 0 && dBytes % 64 == 0;
             if (merge && vny > 1)
@@ -185,11 +220,6 @@ namespace hipk
                 gg.fast = gg.fast && gg.fast32;
                 gg.merge = gg.fast;
                 gg.divCpr = makeFastDiv(static_cast<uint32_t>(gg.cpr));
-                // aligned multi-row boxes whose rows end inside a sector take the general path too
-                bool const uniformPhase = (vny <= 1 || (p.d.sy * bd) % 64 == 0) && (vnz <= 1 || (p.d.sz * bd) % 64 == 0);
-                bool const partial = !uniformPhase || (gg.dph64 + p.d.base) % sv != 0 || (vnx * bd) % 64 != 0;
-                if (vec && rows > 1 && partial && gg.merge)
-                    vec = false;
             }
         }
         gg.divCpr = makeFastDiv(static_cast<uint32_t>(gg.cpr));

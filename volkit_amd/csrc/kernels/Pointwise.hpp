@@ -55,6 +55,12 @@ namespace hipk
                                  // row ends load the whole vector and store only the row's voxels
         FastDiv divCpr, divVny;  // vector path: items -> (row, chunk), row -> (j, k)
         FastDiv divNx, divNy;    // scalar path: voxel -> (i, j, k)
+        // padded rows with 64-B sector completion (Pointwise.hip planPointwise): items cover the
+        // destination's whole end sectors [vhead, vnx8); sources are read only inside the rows'
+        // 8-aligned items [vhead0, vend0) (item x clamped there), the chunks outside the box are
+        // the destination's own bytes loaded and stored back whole
+        int32_t merge;
+        int64_t vhead0, vend0;
     };
 
     struct PassF;   // PointwiseOps.hpp: dst = source code (bytewise CopyRange)
@@ -115,7 +121,7 @@ namespace hipk
     template <int NS, int BPV, int MODE, class F>
     __device__ __forceinline__ void pointwiseVecItem(Operand const& d, Operand const& s1, Operand const& s2,
                                                      Geom const& g, uint64_t it, uint64_t& o1, uint64_t& o2,
-                                                     uint64_t& od)
+                                                     uint64_t& od, int64_t* rowX = nullptr)
     {
         if constexpr (MODE == 0)
         {
@@ -145,10 +151,27 @@ namespace hipk
                 j = r % ny;
                 k = r / ny;
             }
+            od = d.base + k * d.sz + j * d.sy + x;
+            if (rowX)
+                *rowX = static_cast<int64_t>(x);
+            if (g.merge)
+            {
+                // sector completion: sources only inside the rows' own 8-aligned items
+                int64_t xl = static_cast<int64_t>(x);
+                xl = xl < g.vhead0 ? g.vhead0 : (xl > g.vend0 - 8 ? g.vend0 - 8 : xl);
+                x = static_cast<uint64_t>(xl);
+            }
             o1 = s1.base + k * s1.sz + j * s1.sy + x;
             o2 = s2.base + k * s2.sz + j * s2.sy + x;
-            od = d.base + k * d.sz + j * d.sy + x;
         }
+    }
+
+    // Sector completion: an edge item (straddling a row end, or wholly outside the box inside
+    // an end sector) is stored whole, its voxels outside [0, vnx) being the destination's own.
+    template <int BPV>
+    __device__ __forceinline__ void loadDstChunk(uint8_t const* base, uint64_t od, uint32_t (&c)[8])
+    {
+        load8<BPV, false>(base, od, c);
     }
 
     // One workgroup's span [beg, end) of 8-voxel items.  The main loop is branch-free so that
@@ -160,31 +183,23 @@ namespace hipk
     template <class F>
     struct IsPacked16<F, decltype(void(F::kPacked16))> { static constexpr bool value = F::kPacked16; };
 
-    // Padded rows: the row-relative x of item `it` (for the straddle test of its store); the
-    // same division pointwiseVecItem does for the item's offsets.
-    template <int MODE>
-    __device__ __forceinline__ int64_t paddedRowX(Geom const& g, uint64_t it)
-    {
-        if constexpr (MODE == 1)
-        {
-            uint32_t r = fdiv(static_cast<uint32_t>(it), g.divCpr);
-            return g.vhead + (static_cast<int64_t>(static_cast<uint32_t>(it) - r * g.divCpr.d) << 3);
-        }
-        else
-        {
-            uint64_t const cpr = static_cast<uint64_t>(g.vnx8 - g.vhead) >> 3;
-            return g.vhead + static_cast<int64_t>((it % cpr) << 3);
-        }
-    }
-
     // Store the 8 codes of an item whose row-relative start is x; only voxels inside [0, vnx)
     // of the row are written when the item straddles a row end.
     template <int BPV>
     __device__ __forceinline__ void storeItemMasked(uint8_t* base, uint64_t od, int64_t x, int64_t vnx,
-                                                    uint32_t const (&c)[8])
+                                                    uint32_t const (&c)[8], bool merge = false,
+                                                    uint32_t const* own = nullptr)
     {
         if (x >= 0 && x + 8 <= vnx)
             store8<BPV, true>(base, od, c);
+        else if (merge)
+        {
+            uint32_t m[8];
+#pragma unroll
+            for (int v = 0; v < 8; ++v)
+                m[v] = x + v >= 0 && x + v < vnx ? c[v] : own[v];
+            store8<BPV, true>(base, od, m);
+        }
         else
         {
 #pragma unroll
@@ -205,7 +220,7 @@ namespace hipk
         {
             // same schedule as below (all loads of a quantum before its stores), no unpacking:
             // 16 B of each source -> 16 B of dst
-            auto apply = [&](u32x4 const& a, u32x4 const& b, uint64_t od, uint64_t item) {
+            auto apply = [&](u32x4 const& a, u32x4 const& b, uint64_t od, int64_t x, uint32_t const* own) {
                 u32x4 r;
                 r.x = f.pk(a.x, b.x);
                 r.y = f.pk(a.y, b.y);
@@ -215,12 +230,11 @@ namespace hipk
                 {
                     if (g.padded)
                     {
-                        int64_t const x = paddedRowX<MODE>(g, item);
                         if (x < 0 || x + 8 > g.vnx)
                         {
                             uint32_t c[8] = {r.x & 0xFFFFu, r.x >> 16, r.y & 0xFFFFu, r.y >> 16,
                                              r.z & 0xFFFFu, r.z >> 16, r.w & 0xFFFFu, r.w >> 16};
-                            storeItemMasked<2>(d.data, od, x, g.vnx, c);
+                            storeItemMasked<2>(d.data, od, x, g.vnx, c, g.merge != 0, own);
                             return;
                         }
                     }
@@ -231,41 +245,57 @@ namespace hipk
             {
                 u32x4 a[kUnroll], b[kUnroll];
                 uint64_t od[kUnroll];
+                int64_t xr[kUnroll];
+                uint32_t own[kUnroll][8];
 #pragma unroll
                 for (int u = 0; u < kUnroll; ++u)
                 {
                     uint64_t o1, o2;
+                    xr[u] = 0;
                     pointwiseVecItem<NS, BPV, MODE, F>(d, s1, s2, g, it + static_cast<uint64_t>(u) * kVecBlock, o1, o2,
-                                                       od[u]);
+                                                       od[u], &xr[u]);
                     a[u] = loadVec<u32x4, true>(s1.data + 2 * o1);
                     b[u] = loadVec<u32x4, true>(s2.data + 2 * o2);
+                    if constexpr (MODE != 0)
+                        if (g.merge && (xr[u] < 0 || xr[u] + 8 > g.vnx))
+                            loadDstChunk<2>(d.data, od[u], own[u]);
                 }
 #pragma unroll
                 for (int u = 0; u < kUnroll; ++u)
-                    apply(a[u], b[u], od[u], it + static_cast<uint64_t>(u) * kVecBlock);
+                    apply(a[u], b[u], od[u], xr[u], own[u]);
             }
             for (; it < end; it += kVecBlock)
             {
                 uint64_t o1, o2, od;
-                pointwiseVecItem<NS, BPV, MODE, F>(d, s1, s2, g, it, o1, o2, od);
-                apply(loadVec<u32x4, true>(s1.data + 2 * o1), loadVec<u32x4, true>(s2.data + 2 * o2), od, it);
+                int64_t xr = 0;
+                uint32_t own[8];
+                pointwiseVecItem<NS, BPV, MODE, F>(d, s1, s2, g, it, o1, o2, od, &xr);
+                if constexpr (MODE != 0)
+                    if (g.merge && (xr < 0 || xr + 8 > g.vnx))
+                        loadDstChunk<2>(d.data, od, own);
+                apply(loadVec<u32x4, true>(s1.data + 2 * o1), loadVec<u32x4, true>(s2.data + 2 * o2), od, xr, own);
             }
             return;
         }
         for (; it + (kUnroll - 1) * static_cast<uint64_t>(kVecBlock) < end; it += kQ)
         {
-            uint32_t a[kUnroll][8], b[kUnroll][8];
+            uint32_t a[kUnroll][8], b[kUnroll][8], own[kUnroll][8];
             uint64_t od[kUnroll];
+            int64_t xr[kUnroll];
 #pragma unroll
             for (int u = 0; u < kUnroll; ++u)
             {
                 uint64_t o1, o2;
+                xr[u] = 0;
                 pointwiseVecItem<NS, BPV, MODE, F>(d, s1, s2, g, it + static_cast<uint64_t>(u) * kVecBlock, o1, o2,
-                                                   od[u]);
+                                                   od[u], &xr[u]);
                 if constexpr (NS >= 1)
                     load8<BPV, true>(s1.data, o1, a[u]);
                 if constexpr (NS >= 2)
                     load8<BPV, true>(s2.data, o2, b[u]);
+                if constexpr (MODE != 0)
+                    if (g.merge && (xr[u] < 0 || xr[u] + 8 > g.vnx))
+                        loadDstChunk<BPV>(d.data, od[u], own[u]);
             }
 #pragma unroll
             for (int u = 0; u < kUnroll; ++u)
@@ -278,8 +308,7 @@ namespace hipk
                 {
                     if (g.padded)
                     {
-                        storeItemMasked<BPV>(d.data, od[u],
-                                             paddedRowX<MODE>(g, it + static_cast<uint64_t>(u) * kVecBlock), g.vnx, o);
+                        storeItemMasked<BPV>(d.data, od[u], xr[u], g.vnx, o, g.merge != 0, own[u]);
                         continue;
                     }
                 }
@@ -288,13 +317,17 @@ namespace hipk
         }
         for (; it < end; it += kVecBlock)
         {
-            uint32_t a[8], b[8], o[8];
+            uint32_t a[8], b[8], o[8], own[8];
             uint64_t o1, o2, od;
-            pointwiseVecItem<NS, BPV, MODE, F>(d, s1, s2, g, it, o1, o2, od);
+            int64_t xr = 0;
+            pointwiseVecItem<NS, BPV, MODE, F>(d, s1, s2, g, it, o1, o2, od, &xr);
             if constexpr (NS >= 1)
                 load8<BPV, true>(s1.data, o1, a);
             if constexpr (NS >= 2)
                 load8<BPV, true>(s2.data, o2, b);
+            if constexpr (MODE != 0)
+                if (g.merge && (xr < 0 || xr + 8 > g.vnx))
+                    loadDstChunk<BPV>(d.data, od, own);
 #pragma unroll
             for (int v = 0; v < 8; ++v)
                 o[v] = f(NS >= 1 ? a[v] : 0u, NS >= 2 ? b[v] : 0u);
@@ -302,7 +335,7 @@ namespace hipk
             {
                 if (g.padded)
                 {
-                    storeItemMasked<BPV>(d.data, od, paddedRowX<MODE>(g, it), g.vnx, o);
+                    storeItemMasked<BPV>(d.data, od, xr, g.vnx, o, g.merge != 0, own);
                     continue;
                 }
             }
