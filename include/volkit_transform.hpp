@@ -123,6 +123,7 @@ namespace transform_detail
     {
         int32_t x0, y0, z0;
         uint32_t nx;
+        int32_t rx0, rx1;   // padded launches: the range's own x [rx0, rx1) inside [x0, x0 + nx)
         uint32_t row0;
         uint64_t items;
         FastDiv perRow;   // items per row
@@ -209,7 +210,11 @@ namespace transform_detail
     // ---- unary, 16-byte vectors: item = one 16-byte vector of one row -------------------
     // GUARD = false: the launch holds whole workgroups of valid items only (no per-item
     // branch between the loads; with one, hipcc waits for each load before the next).
-    template <int BPV, bool GUARD, class Op>
+    // PAD: the launch covers each row from the aligned chunk at or below the range start to
+    // the one at or above its end (16-B, or 64-B sectors where the rows allow: a partly written
+    // 64-B sector costs HBM a read-modify-write); voxels outside [rx0, rx1) are stored back as
+    // they were loaded, without calling the functor.
+    template <int BPV, bool GUARD, bool PAD, class Op>
     __global__ void __launch_bounds__(kBlock) unaryVecKernel(Vol v, Rows g, uint32_t itemBase, Op op)
     {
         constexpr int V = 16 / BPV;
@@ -240,8 +245,11 @@ namespace transform_detail
             {
                 uint8_t bytes[8];
                 unpack<BPV>(w[u], k, bytes);
-                VoxelView voxel{bytes, v.format, v.lo, v.hi};
-                op(xs[u] + k, ys[u], zs[u], voxel);
+                if (!PAD || (xs[u] + k >= g.rx0 && xs[u] + k < g.rx1))
+                {
+                    VoxelView voxel{bytes, v.format, v.lo, v.hi};
+                    op(xs[u] + k, ys[u], zs[u], voxel);
+                }
                 pack<BPV>(out, k, bytes);
             }
             if (!GUARD || ok[u])
@@ -272,7 +280,7 @@ namespace transform_detail
     // ALIAS: both handles name one buffer with one layout: the voxel is loaded once, both
     // scratches start from it, and volume2's bytes are stored (the serial loop stores
     // volume1's, then volume2's, to the same address).
-    template <int BPV, bool GUARD, bool ALIAS, class Op>
+    template <int BPV, bool GUARD, bool ALIAS, bool PAD, class Op>
     __global__ void __launch_bounds__(kBlock) binaryVecKernel(Vol v1, Vol v2, Rows g, uint32_t itemBase, Op op)
     {
         constexpr int V = 16 / BPV;
@@ -309,9 +317,12 @@ namespace transform_detail
                 uint8_t b1[8], b2[8];
                 unpack<BPV>(w1[u], k, b1);
                 unpack<BPV>(ALIAS ? w1[u] : w2[u], k, b2);
-                VoxelView voxel1{b1, v1.format, v1.lo, v1.hi};
-                VoxelView voxel2{b2, v2.format, v2.lo, v2.hi};
-                op(xs[u] + k, ys[u], zs[u], voxel1, voxel2);
+                if (!PAD || (xs[u] + k >= g.rx0 && xs[u] + k < g.rx1))
+                {
+                    VoxelView voxel1{b1, v1.format, v1.lo, v1.hi};
+                    VoxelView voxel2{b2, v2.format, v2.lo, v2.hi};
+                    op(xs[u] + k, ys[u], zs[u], voxel1, voxel2);
+                }
                 if constexpr (!ALIAS)
                     pack<BPV>(o1, k, b1);
                 pack<BPV>(o2, k, b2);
@@ -389,6 +400,26 @@ namespace transform_detail
                (static_cast<uint64_t>(nx) * bpv) % 16 == 0 && (v.dimX * bpv) % 16 == 0;
     }
 
+    // Padding unit for a range that vec16 refuses: rows start on 16-B (64-B) boundaries, so a
+    // row's chunks belong to that row alone; 0 = no padded launch.
+    inline int padUnit(Vol const& v, int bpv)
+    {
+        uintptr_t const a = reinterpret_cast<uintptr_t>(v.data);
+        if (a % 64 == 0 && (v.dimX * bpv) % 64 == 0)
+            return 64;
+        if (a % 16 == 0 && (v.dimX * bpv) % 16 == 0)
+            return 16;
+        return 0;
+    }
+
+    // first/last widened to whole units of the row (x in voxels)
+    inline void padRange(Vec3i& first, Vec3i& last, int unit, int bpv)
+    {
+        int const vu = unit / bpv;
+        first.x = first.x / vu * vu;
+        last.x = (last.x + vu - 1) / vu * vu;
+    }
+
     // Calls launch(Rows, grid) for row ranges of at most kMaxItemsPerLaunch items.
     template <class Launch>
     hipError_t forRows(Vec3i first, Vec3i last, uint32_t perRow, Launch&& launch)
@@ -407,6 +438,8 @@ namespace transform_detail
             g.y0 = first.y;
             g.z0 = first.z;
             g.nx = nx;
+            g.rx0 = first.x;
+            g.rx1 = last.x;
             g.row0 = static_cast<uint32_t>(r0);
             g.items = nr * perRow;
             g.perRow = makeFastDiv(perRow);
@@ -481,21 +514,32 @@ namespace transform_detail
         uint32_t nx = static_cast<uint32_t>(last.x - first.x);
         hipStream_t s = scope.stream;
         hipError_t err = hipSuccess;
-        if (vec16(v, first.x, nx, bpv))
+        bool const aligned = vec16(v, first.x, nx, bpv);
+        int const unit = aligned ? 0 : padUnit(v, bpv);
+        if (aligned || unit != 0)
         {
-            uint32_t perRow = nx * bpv / 16;
-            err = forRows(first, last, perRow, [&](Rows const& g) {
+            Vec3i pf = first, pl = last;
+            if (!aligned)
+                padRange(pf, pl, unit, bpv);
+            uint32_t perRow = static_cast<uint32_t>(pl.x - pf.x) * bpv / 16;
+            err = forRows(pf, pl, perRow, [&](Rows const& gp) {
+                Rows g = gp;
+                g.rx0 = first.x;
+                g.rx1 = last.x;
                 launchVec(g, [&](bool guard, uint32_t base, uint32_t blocks) {
                     dim3 grid(blocks), block(kBlock);
+#define VKT_UN_VEC_(B, G, P) unaryVecKernel<B, G, P><<<grid, block, 0, s>>>(v, g, base, op)
+#define VKT_UN_VEC_B_(B)                                                               \
+    (aligned ? (guard ? VKT_UN_VEC_(B, true, false) : VKT_UN_VEC_(B, false, false))    \
+             : (guard ? VKT_UN_VEC_(B, true, true) : VKT_UN_VEC_(B, false, true)))
                     if (bpv == 1)
-                        guard ? unaryVecKernel<1, true><<<grid, block, 0, s>>>(v, g, base, op)
-                              : unaryVecKernel<1, false><<<grid, block, 0, s>>>(v, g, base, op);
+                        VKT_UN_VEC_B_(1);
                     else if (bpv == 2)
-                        guard ? unaryVecKernel<2, true><<<grid, block, 0, s>>>(v, g, base, op)
-                              : unaryVecKernel<2, false><<<grid, block, 0, s>>>(v, g, base, op);
+                        VKT_UN_VEC_B_(2);
                     else
-                        guard ? unaryVecKernel<4, true><<<grid, block, 0, s>>>(v, g, base, op)
-                              : unaryVecKernel<4, false><<<grid, block, 0, s>>>(v, g, base, op);
+                        VKT_UN_VEC_B_(4);
+#undef VKT_UN_VEC_B_
+#undef VKT_UN_VEC_
                 });
                 return hipPeekAtLastError();
             });
@@ -564,16 +608,26 @@ namespace transform_detail
         }
         uint32_t nx = static_cast<uint32_t>(last.x - first.x);
         hipStream_t s = scope.stream;
-        if (b1 == b2 && vec16(a, first.x, nx, b1) && vec16(b, first.x, nx, b2))
+        bool const aligned = b1 == b2 && vec16(a, first.x, nx, b1) && vec16(b, first.x, nx, b2);
+        int const ua = b1 == b2 && !aligned ? padUnit(a, b1) : 0, ub = b1 == b2 && !aligned ? padUnit(b, b2) : 0;
+        int const unit = ua < ub ? ua : ub;
+        if (aligned || unit != 0)
         {
-            uint32_t perRow = nx * b1 / 16;
-            (void)forRows(first, last, perRow, [&](Rows const& g) {
+            Vec3i pf = first, pl = last;
+            if (!aligned)
+                padRange(pf, pl, unit, b1);
+            uint32_t perRow = static_cast<uint32_t>(pl.x - pf.x) * b1 / 16;
+            (void)forRows(pf, pl, perRow, [&](Rows const& gp) {
+                Rows g = gp;
+                g.rx0 = first.x;
+                g.rx1 = last.x;
                 launchVec(g, [&](bool guard, uint32_t base, uint32_t blocks) {
                     dim3 grid(blocks), block(kBlock);
-#define VKT_BIN_VEC_(B, G, A) binaryVecKernel<B, G, A><<<grid, block, 0, s>>>(a, b, g, base, op)
-#define VKT_BIN_VEC_B_(B)                                                                 \
-    (alias ? (guard ? VKT_BIN_VEC_(B, true, true) : VKT_BIN_VEC_(B, false, true))         \
-           : (guard ? VKT_BIN_VEC_(B, true, false) : VKT_BIN_VEC_(B, false, false)))
+#define VKT_BIN_VEC_(B, G, A, P) binaryVecKernel<B, G, A, P><<<grid, block, 0, s>>>(a, b, g, base, op)
+#define VKT_BIN_VEC_P_(B, P)                                                                    \
+    (alias ? (guard ? VKT_BIN_VEC_(B, true, true, P) : VKT_BIN_VEC_(B, false, true, P))         \
+           : (guard ? VKT_BIN_VEC_(B, true, false, P) : VKT_BIN_VEC_(B, false, false, P)))
+#define VKT_BIN_VEC_B_(B) (aligned ? VKT_BIN_VEC_P_(B, false) : VKT_BIN_VEC_P_(B, true))
                     if (b1 == 1)
                         VKT_BIN_VEC_B_(1);
                     else if (b1 == 2)
@@ -581,6 +635,7 @@ namespace transform_detail
                     else
                         VKT_BIN_VEC_B_(4);
 #undef VKT_BIN_VEC_B_
+#undef VKT_BIN_VEC_P_
 #undef VKT_BIN_VEC_
                 });
                 return hipPeekAtLastError();

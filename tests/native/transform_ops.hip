@@ -257,9 +257,11 @@ void* vktt_host_binary(int op)
     return out;
 }
 
-// Device-resident timing: `reps` unary TransformRange calls over the whole volume, after
-// 3 warm-up calls; *ms = average per call (HIP events on volkit's compute stream).
-int vktt_bench_unary(int op, int dx, int dy, int dz, int fmt, int reps, float* ms)
+// Device-resident timing: `reps` unary TransformRange calls over [first, last) (the whole
+// volume when last.x <= 0), after 3 warm-up calls; *ms = average per call (HIP events on
+// volkit's compute stream).
+int vktt_bench_unary_range(int op, int dx, int dy, int dz, int fmt, int fx, int fy, int fz, int lx, int ly, int lz,
+                           int reps, float* ms)
 {
     GpuPolicy gpu;
     vkt::StructuredVolume v(dx, dy, dz, static_cast<vkt::DataFormat>(fmt));
@@ -271,7 +273,10 @@ int vktt_bench_unary(int op, int dx, int dy, int dz, int fmt, int reps, float* m
     hipStream_t stream = static_cast<hipStream_t>(s);
     int rc = 0;
     auto call = [&] {
-        int e = withUnary(op, [&](auto f) { return static_cast<int>(vkt::Transform(v, f)); });
+        int e = withUnary(op, [&](auto f) {
+            return lx <= 0 ? static_cast<int>(vkt::Transform(v, f))
+                           : static_cast<int>(vkt::TransformRange(v, vkt::Vec3i{fx, fy, fz}, vkt::Vec3i{lx, ly, lz}, f));
+        });
         if (e != 0)
             rc = e;
     };
@@ -291,6 +296,11 @@ int vktt_bench_unary(int op, int dx, int dy, int dz, int fmt, int reps, float* m
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     return rc;
+}
+
+int vktt_bench_unary(int op, int dx, int dy, int dz, int fmt, int reps, float* ms)
+{
+    return vktt_bench_unary_range(op, dx, dy, dz, fmt, 0, 0, 0, 0, 0, 0, reps, ms);
 }
 
 } // extern "C"

@@ -91,6 +91,8 @@ RANGES = [
     ((24, 24, 24), (2, 2, 2), (22, 22, 22)),
     ((16, 16, 16), (5, 5, 5), (6, 6, 6)),
     ((16, 16, 16), (4, 4, 4), (4, 9, 9)),
+    ((64, 16, 8), (3, 1, 1), (61, 15, 7)),      # rows on 64-B boundaries: padded to sectors
+    ((128, 4, 3), (17, 0, 0), (100, 4, 3)),
 ]
 
 

@@ -140,6 +140,14 @@ def main():
             if t.vktt_bench_unary(op, m, m, m, fmt, R, C.byref(ms)) != 0:
                 raise RuntimeError(_lib.last_error())
             report(f"Transform {lab} 1024^3 fmt={fmt}", ms.value, rw * b * m ** 3, m ** 3)
+        # TransformRange over a sub-box whose rows start and end inside 16-B chunks (the shape of
+        # CoreAlgorithms.c's TransformRange 2..22, scaled): padded vector path
+        t.vktt_bench_unary_range.argtypes = [C.c_int] * 12 + [C.POINTER(C.c_float)]
+        for fmt, b in ((4, 1), (5, 2), (7, 4)):
+            if t.vktt_bench_unary_range(2, m, m, m, fmt, 2, 2, 2, m - 2, m - 2, m - 2, R, C.byref(ms)) != 0:
+                raise RuntimeError(_lib.last_error())
+            nv = (m - 4) ** 3
+            report(f"TransformRange Diagonal 2..{m - 2} of 1024^3 fmt={fmt}", ms.value, 2 * b * nv, nv)
     if want("memset"):
         # MemsetRange / ManagedBuffer::fill at 1024^3-UInt16 scale (2 GiB), write-only bytes
         nb = 2 << 30
