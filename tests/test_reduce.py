@@ -168,6 +168,11 @@ FAST_CASES = [
     ((64, 24, 10), (0, 0, 2), (64, 24, 9)),
     ((64, 24, 10), (0, 5, 4), (64, 17, 5)),
     ((64, 24, 10), (8, 3, 2), (56, 20, 9)),
+    # padded rows (range rows starting / ending off the 8-voxel grid): masked end items
+    ((64, 24, 10), (3, 3, 2), (61, 20, 9)),
+    ((64, 24, 10), (5, 0, 0), (6, 24, 10)),
+    ((64, 24, 10), (9, 1, 1), (15, 2, 2)),
+    ((128, 8, 4), (1, 0, 0), (128, 8, 4)),
 ]
 
 

@@ -320,6 +320,13 @@ def main():
         sub0, sub1 = Vec3i_t(64, 64, 64), Vec3i_t(960, 960, 960)
         ms = timed(lambda: lib.vktHipHistogramRange(V, sub0, sub1, bins, 256, 0), R)
         report("reduce Histogram UInt16 896^3 sub-box of 1024^3, 256 bins", ms, 2 * 896 ** 3, 896 ** 3)
+        # rows that start and end off the 8-voxel grid (x 100..900)
+        u0, u1 = Vec3i_t(100, 100, 100), Vec3i_t(900, 900, 900)
+        ms = timed(lambda: lib.vktHipHistogramRange(V, u0, u1, bins, 256, 0), R)
+        report("reduce Histogram UInt16 800^3 sub-box of 1024^3 at x0=100, 256 bins", ms, 2 * 800 ** 3, 800 ** 3)
+        agg0 = _lib.Aggregates_t()
+        ms = timed(lambda: lib.vktHipAggregatesRange(V, u0, u1, C.byref(agg0)), R)
+        report("reduce Aggregates UInt16 800^3 sub-box of 1024^3 at x0=100 (2 passes)", ms, 2 * 2 * 800 ** 3, 800 ** 3)
         for fmt, bpv, name in ((4, 1, "UInt8"), (7, 4, "Float32")):
             W = alloc((n,) * 3, fmt, seed=12 if fmt != 7 else None)
             if fmt == 7:

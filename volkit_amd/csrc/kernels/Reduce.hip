@@ -372,6 +372,10 @@ namespace hipk
         unsigned long long* bins;
         uint64_t giBase;            // aggregates, CONTIG: global linear index of the span start
         int64_t zGlobal;            // aggregates: Z-slab offset added to z for global indices
+        // padded rows (range rows starting or ending off the 8-voxel grid): items cover each row
+        // from px0 = fx & ~7 to the 8-aligned end; voxels outside [rx0, rx1) are not visited
+        int32_t px0, rx0, rx1;
+        uint32_t padded;
     };
 
     typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -397,9 +401,27 @@ namespace hipk
             uint32_t const yr = r - zr * h.fdNy.d;
             return ((static_cast<uint64_t>(h.fz + zr) * static_cast<uint64_t>(h.dimY) + (h.fy + yr)) *
                         static_cast<uint64_t>(h.dimX) +
-                    static_cast<uint64_t>(h.fx)) +
+                    static_cast<uint64_t>(h.px0)) +
                    8ull * xi;
         }
+    }
+
+    // Valid voxels of item `item` (bit j = voxel j): all of them except in padded rows' end items.
+    template <bool CONTIG>
+    __device__ __forceinline__ uint32_t itemMask(FastHistArgs const& h, uint64_t item)
+    {
+        if (CONTIG || !h.padded)
+            return 0xFFu;
+        uint32_t const i = static_cast<uint32_t>(item);
+        uint32_t const xi = i - fdiv(i, h.fdIpr) * h.fdIpr.d;
+        int32_t const x0 = h.px0 + 8 * static_cast<int32_t>(xi);
+        if (x0 >= h.rx0 && x0 + 8 <= h.rx1)
+            return 0xFFu;
+        uint32_t m = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            m |= (x0 + j >= h.rx0 && x0 + j < h.rx1) ? 1u << j : 0u;
+        return m;
     }
 
     // SHIFT: the bin of every code is code >> binShift, so one shift replaces the decode, the
@@ -448,19 +470,20 @@ namespace hipk
             else
                 atomicAdd(reinterpret_cast<uint32_t*>(cLane + (b << rowShift)), 1u);
         };
-        auto count8 = [&](uint32_t const (&c)[8]) {
+        // m: valid voxels of the item (padded rows); the others go to the trash row / no tile
+        auto count8 = [&](uint32_t const (&c)[8], uint32_t m) {
             if constexpr (SHIFT)
             {
 #pragma unroll
                 for (int j = 0; j < 8; ++j)
-                    add(c[j] >> h.binShift);
+                    add((m >> j) & 1u ? c[j] >> h.binShift : h.nb);
             }
             else if constexpr (FMT == codec::FmtUInt8)
             {
 #pragma unroll
                 for (int j = 0; j < 8; ++j)
                 {
-                    uint32_t const o = lut[c[j]];
+                    uint32_t const o = (m >> j) & 1u ? lut[c[j]] : (TILED ? kOff : h.nb << rowShift);
                     if (!TILED || o != kOff)
                         atomicAdd(reinterpret_cast<uint32_t*>(cLane + o), 1u);
                 }
@@ -484,8 +507,8 @@ namespace hipk
                     else
                         v = f32x2{codec::bitsToFloat(c[j]), codec::bitsToFloat(c[j + 1])};
                     f32x2 const f = (v - h.lo) * h.scale;
-                    add(fastBin(f.x, h.nbf, h.nb));
-                    add(fastBin(f.y, h.nbf, h.nb));
+                    add((m >> j) & 1u ? fastBin(f.x, h.nbf, h.nb) : h.nb);
+                    add((m >> (j + 1)) & 1u ? fastBin(f.y, h.nbf, h.nb) : h.nb);
                 }
             }
         };
@@ -501,13 +524,13 @@ namespace hipk
                 load8<BPV, true>(h.data, voxelOf(st * (64 * U) + k * 64 + lane), c[k]);
 #pragma unroll
             for (int k = 0; k < U; ++k)
-                count8(c[k]);
+                count8(c[k], itemMask<CONTIG>(h, st * (64 * U) + k * 64 + lane));
         }
         for (uint64_t it = steps * (64 * U) + wave * 64 + lane; it < h.items; it += waves * 64)
         {
             uint32_t c[8];
             load8<BPV, true>(h.data, voxelOf(it), c);
-            count8(c);
+            count8(c, itemMask<CONTIG>(h, it));
         }
         __syncthreads();
         if constexpr (TILED)
@@ -564,13 +587,16 @@ namespace hipk
                 uint32_t const zr = fdiv(r, h.fdNy);
                 uint32_t const yr = r - zr * h.fdNy.d;
                 return (static_cast<uint64_t>(h.fz + zr + h.zGlobal) * py + static_cast<uint64_t>(h.fy + yr)) * px +
-                       static_cast<uint64_t>(h.fx) + 8ull * xi + static_cast<uint64_t>(j);
+                       static_cast<uint64_t>(h.px0) + 8ull * xi + static_cast<uint64_t>(j);
             }
         };
         auto visit8 = [&](uint32_t const (&c)[8], uint64_t item) {
+            uint32_t const m = itemMask<CONTIG>(h, item);
 #pragma unroll
             for (int j = 0; j < 8; ++j)
             {
+                if (!((m >> j) & 1u))
+                    continue;   // padded rows: outside the range
                 float const v = UNIT ? codec::decodeUnit(c[j], FMT) : codec::decode(c[j], FMT, h.lo, h.hi);
                 if constexpr (PASS == 1)
                 {
@@ -599,7 +625,7 @@ namespace hipk
                 }
             }
             if constexpr (PASS == 1)
-                p.count += 8;
+                p.count += __builtin_popcount(m);
         };
         uint64_t const wave = static_cast<uint64_t>(blockIdx.x) * (kBlock / 64) + (threadIdx.x >> 6);
         uint64_t const waves = static_cast<uint64_t>(gridDim.x) * (kBlock / 64);
@@ -700,13 +726,21 @@ namespace hipk
     bool makeSpanArgs(BoxArgs const& a, FastHistArgs& h, bool& contig)
     {
         int32_t const fmt = a.fmt;
-        if ((fmt != codec::FmtUInt8 && fmt != codec::FmtUInt16 && fmt != codec::FmtFloat32) || !vecRows(a))
+        if (fmt != codec::FmtUInt8 && fmt != codec::FmtUInt16 && fmt != codec::FmtFloat32)
             return false;
+        // rows on the 8-voxel grid (16-B aligned base, dimX % 8 == 0); a range row that starts or
+        // ends off it is padded to whole items, the extra voxels masked (itemMask)
+        if (a.dimX % 8 != 0 || reinterpret_cast<uintptr_t>(a.data) % 16 != 0)
+            return false;
+        bool const padded = a.fx % 8 != 0 || a.nx % 8 != 0;
+        int32_t const px0 = a.fx & ~7;
+        int32_t const px1 = (a.fx + a.nx + 7) & ~7;
         uint32_t const bpv = codec::bytesPerVoxel(fmt);
         uint64_t const ny = a.fdNy.d;   // range rows = ny * nz
         uint64_t const nz = a.rows / ny;
-        contig = a.nx == a.dimX && (ny == static_cast<uint64_t>(a.dimY) || nz == 1);
-        uint64_t const items = static_cast<uint64_t>(a.nx / 8) * a.rows;
+        contig = !padded && a.nx == a.dimX && (ny == static_cast<uint64_t>(a.dimY) || nz == 1);
+        uint64_t const ipr = static_cast<uint64_t>(px1 - px0) / 8;
+        uint64_t const items = ipr * a.rows;
         if (!contig && items >= (1ull << 32))
             return false;
         h = FastHistArgs{};
@@ -716,7 +750,11 @@ namespace hipk
         h.fx = a.fx;
         h.fy = a.fy;
         h.fz = a.fz;
-        h.fdIpr = makeFastDiv(static_cast<uint32_t>(a.nx / 8));
+        h.px0 = px0;
+        h.rx0 = a.fx;
+        h.rx1 = a.fx + a.nx;
+        h.padded = padded ? 1u : 0u;
+        h.fdIpr = makeFastDiv(static_cast<uint32_t>(ipr));
         h.fdNy = a.fdNy;
         uint64_t const start = (static_cast<uint64_t>(a.fz) * a.dimY + a.fy) * a.dimX;   // CONTIG: fx == 0
         h.data = contig ? a.data + start * bpv : a.data;
