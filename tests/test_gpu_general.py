@@ -330,3 +330,34 @@ def test_sector_completion_aligned_path(lib, o, fmt):
                 assert_codes_equal(dd.read(), ref, fmt, f"aligned merge={on} fill {first}->{last}")
     finally:
         assert lib.vktHipSetTuningKnob(b"pointwise.merge_sectors", -1) == 0
+
+
+def test_general_64bit_addressing(lib, o):
+    """The general path's 64-bit addressing (taken for operands of 4 GiB and more, so never by
+    the small cases above): knob pointwise.general_32bit = 0 forces it on phase shifts, clamped
+    halos, narrow rows, conversions and shifted arithmetic."""
+    from volkit_amd._lib import lib as L
+    rng = np.random.default_rng(123)
+    assert lib.vktHipSetTuningKnob(b"pointwise.general_32bit", 0) == 0
+    try:
+        for fmt in (4, 5, 7):
+            src = rand_codes(rng, fmt, (5, 7, 29))
+            dinit = rand_codes(rng, fmt, (6, 8, 43))
+            for first, last, off in (((3, 1, 1), (22, 6, 4), (0, 0, 0)), ((-5, -2, -1), (24, 6, 5), (7, 0, 0)),
+                                     ((2, 0, 0), (5, 7, 5), (1, 1, 1))):
+                copy_case(lib, o, fmt, fmt, (0.0, 1.0), (0.0, 1.0), src, dinit, first, last, off,
+                          what=f"64-bit copy fmt={fmt} {first}->{last}+{off}")
+                other = {4: 7, 5: 4, 7: 5}[fmt]
+                copy_case(lib, o, other, fmt, (0.0, 1.0), (-1.0, 3.0), rand_codes(rng, other, src.shape), dinit,
+                          first, last, off, what=f"64-bit convert {other}->{fmt} {first}->{last}+{off}")
+            a = rand_codes(rng, fmt, (4, 6, 45))
+            b = rand_codes(rng, fmt, (4, 6, 45))
+            d0 = rand_codes(rng, fmt, (5, 7, 53))
+            for op in ("Sum", "SafeDiff", "Quot"):
+                da, db, dd = Dev(a, fmt), Dev(b, fmt, pad=2 * BPV[fmt]), Dev(d0, fmt)
+                assert L.vktHipArithmeticRange(OPS.index(op), dd.view, da.view, db.view, vec((3, 1, 1)), vec((40, 5, 3)),
+                                               vec((3, 1, 1))) == 0
+                ref = o.arith(op, [fmt] * 3, [(0.0, 1.0)] * 3, a, b, d0.copy(), (3, 1, 1), (40, 5, 3), (3, 1, 1))
+                assert_codes_equal(dd.read(), ref, fmt, f"64-bit {op} fmt={fmt}")
+    finally:
+        assert lib.vktHipSetTuningKnob(b"pointwise.general_32bit", -1) == 0

@@ -186,7 +186,7 @@ namespace hipk
                        (vny <= 1 || (o.sy < (1ll << 24) && o.dims[0] < (1 << 24))) &&
                        (vnz <= 1 || o.sz < (1ll << 24)) && (!o.clamp || static_cast<int64_t>(o.dims[0]) * o.dims[1] < (1ll << 24));
             }
-            gg.fast = fast ? 1 : 0;
+            gg.fast = fast && rt::knob(rt::Knob::PointwiseGeneral32) != 0 ? 1 : 0;
         }
         // 64-B sector completion at the row ends (measured on MI355X: a copy of 1024^2 rows of
         // 896 UInt16 voxels takes 0.61 ms when the rows end on a 64-B boundary and 0.78 ms when

@@ -77,7 +77,8 @@ namespace rt
         PointwisePaddedRows = 0,       // 1: multi-row boxes use padded row items (no scalar edges)
         PointwiseMaxQuanta,            // launch split, in quanta of the default unroll (2^20)
         PointwiseGeneral,              // 0: boxes the aligned path cannot take use the scalar kernel
-        PointwiseMergeSectors,         // 0: no 64-B sector completion at row ends (general path)
+        PointwiseMergeSectors,         // 0: no 64-B sector completion at row ends
+        PointwiseGeneral32,            // 0: the general path uses 64-bit addressing everywhere (tests)
         Count
     };
     int64_t knob(Knob k);
