@@ -361,3 +361,60 @@ def test_general_64bit_addressing(lib, o):
                 assert_codes_equal(dd.read(), ref, fmt, f"64-bit {op} fmt={fmt}")
     finally:
         assert lib.vktHipSetTuningKnob(b"pointwise.general_32bit", -1) == 0
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_random_geometry_fuzz(lib, o, seed):
+    """Random dims, boxes (clamped or not), offsets, view paddings, formats and mappings through
+    CopyRange, FillRange and arithmetic vs the oracle, with the sector completion and the
+    general path's 32-bit addressing on and off: every planning branch of the pointwise engine
+    (aligned rows, padded rows with and without sector completion, general path with and
+    without it, per-voxel kernel for mixed-format arithmetic)."""
+    from volkit_amd._lib import lib as L
+    rng = np.random.default_rng(1000 + seed)
+    fmts = [4, 5, 7, 2, 6]
+    knobs = [(b"pointwise.merge_sectors", 1), (b"pointwise.merge_sectors", 0), (b"pointwise.general_32bit", 0)]
+    try:
+        for case in range(40):
+            kname, kval = knobs[case % len(knobs)]
+            assert lib.vktHipSetTuningKnob(kname, kval) == 0
+            sf = int(rng.choice(fmts))
+            df = sf if rng.random() < 0.7 else int(rng.choice(fmts))
+            b = BPV[df]
+            # destination rows often 64-B multiples (sector completion applies), sometimes not
+            dx = int(rng.choice([64 // b * int(rng.integers(1, 4)), int(rng.integers(5, 90))]))
+            ddims = (dx, int(rng.integers(1, 9)), int(rng.integers(1, 6)))
+            sdims = (int(rng.integers(1, 90)), int(rng.integers(1, 9)), int(rng.integers(1, 6)))
+            src = rand_codes(rng, sf, sdims[::-1])
+            dinit = rand_codes(rng, df, ddims[::-1])
+            n = [int(rng.integers(1, ddims[i] + 1)) for i in range(3)]
+            off = tuple(int(rng.integers(0, ddims[i] - n[i] + 1)) for i in range(3))
+            first = tuple(int(rng.integers(-3, max(-2, sdims[i] - n[i] + 4))) for i in range(3))
+            last = tuple(first[i] + n[i] for i in range(3))
+            smap = [(0.0, 1.0), (-1.0, 3.0)][int(rng.integers(0, 2))]
+            dmap = [(0.0, 1.0), (0.25, 7.5)][int(rng.integers(0, 2))]
+            spad = int(rng.choice([0, 0, BPV[sf], 3 * BPV[sf]]))
+            dpad = int(rng.choice([0, 0, 0, b]))
+            what = f"fuzz{seed}.{case} {kname}={kval} {sf}->{df} s{sdims} d{ddims} {first}->{last}+{off} pads {spad},{dpad}"
+            copy_case(lib, o, sf, df, smap, dmap, src, dinit, first, last, off, spad, dpad, what=what)
+            # fill and arithmetic on boxes inside the destination / sources
+            ff = off
+            fl = tuple(off[i] + n[i] for i in range(3))
+            dd = Dev(dinit, df, dmap, dpad)
+            assert L.vktHipFillRange(dd.view, vec(ff), vec(fl), C.c_float(0.37)) == 0
+            ref = o.fill_range(df, dmap, ddims, dinit.copy(), ff, fl, 0.37)
+            assert_codes_equal(dd.read(), ref, df, "fill " + what)
+            a = rand_codes(rng, df, ddims[::-1])
+            a2 = rand_codes(rng, df, ddims[::-1])
+            op = OPS[int(rng.integers(0, len(OPS)))]
+            box0 = tuple(int(rng.integers(0, ddims[i])) for i in range(3))
+            box1 = tuple(int(rng.integers(box0[i] + 1, ddims[i] + 1)) for i in range(3))
+            da, db, dd = Dev(a, df, dmap, spad * b // BPV[sf]), Dev(a2, df, dmap), Dev(dinit, df, dmap, dpad)
+            assert L.vktHipArithmeticRange(OPS.index(op), dd.view, da.view, db.view, vec(box0), vec(box1),
+                                           vec((0, 0, 0))) == 0
+            ref = o.arith(op, [df] * 3, [dmap] * 3, a, a2, dinit.copy(), box0, box1, (0, 0, 0))
+            assert_codes_equal(dd.read(), ref, df, f"{op} {box0}->{box1} " + what)
+            assert lib.vktHipSetTuningKnob(kname, -1) == 0
+    finally:
+        for kname, _ in knobs:
+            lib.vktHipSetTuningKnob(kname, -1)
