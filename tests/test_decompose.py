@@ -225,3 +225,30 @@ def test_repeated_decompositions_stay_exact():
         ref = ob.brick_decompose(ob.Volume(codes, fmt), brick, (1, 0, 1), (0, 1, 0))
         for idx, v in ref.items():
             np.testing.assert_array_equal(got[idx], v.codes, err_msg=f"iteration {it} brick {idx}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fmt", [4, 5, 7])
+def test_brick_decompose_small_bricks_large_volume(fmt):
+    """32^3 bricks with a 1-voxel halo over a 160x96x64 volume: many bricks per row, items
+    spanning two brick rows in every brick, loads at the first and last source bytes."""
+    rng = np.random.default_rng(fmt + 40)
+    codes = rand_codes(rng, fmt, (64, 96, 160))
+    err, got = gpu_decompose(codes, fmt, (0.0, 1.0), (32, 32, 32), (1, 1, 1), (1, 1, 1))
+    assert err == vkt.NoError, vkt.last_error()
+    ref = ob.brick_decompose(ob.Volume(codes, fmt), (32, 32, 32), (1, 1, 1), (1, 1, 1))
+    for idx, v in ref.items():
+        np.testing.assert_array_equal(got[idx], v.codes, err_msg=f"brick {idx}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fmt", [5, 7])
+def test_brick_decompose_narrow_rows(fmt):
+    """8-voxel brick rows (a 16-KiB chunk spans up to 1025 rows of the staged copy)."""
+    rng = np.random.default_rng(fmt + 50)
+    codes = rand_codes(rng, fmt, (64, 64, 64))
+    err, got = gpu_decompose(codes, fmt, (0.0, 1.0), (8, 64, 64), (0, 0, 0), (0, 0, 0))
+    assert err == vkt.NoError, vkt.last_error()
+    ref = ob.brick_decompose(ob.Volume(codes, fmt), (8, 64, 64), (0, 0, 0), (0, 0, 0))
+    for idx, v in ref.items():
+        np.testing.assert_array_equal(got[idx], v.codes, err_msg=f"brick {idx}")
