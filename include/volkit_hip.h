@@ -73,7 +73,9 @@ VKTAPI vktError vktHipKernelScopeEnd(vktHipKernelScope scope);
  * aligned vector path cannot take to the per-voxel kernel), "pointwise.merge_sectors" (1; 0 stops
  * the general path from completing the 64-B sectors at the row ends of a box by rewriting the
  * destination's own bytes around it), "pointwise.general_32bit" (1; 0 makes the general path use
- * its 64-bit addressing, otherwise taken only for operands of 4 GiB and more).  For tests and
+ * its 64-bit addressing, otherwise taken only for operands of 4 GiB and more), "histogram.packed16"
+ * (1; 0 makes histograms with more bins than one LDS tile of 32-bit counters take one pass per
+ * tile instead of one pass over packed 16-bit counters).  For tests and
  * in-process A/B measurements; unknown names return vktInvalidValue. */
 VKTAPI vktError vktHipSetTuningKnob(const char* name, int64_t value);
 /* Record `message` as the calling thread's last error, log it; returns vktInvalidValue. */

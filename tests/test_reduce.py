@@ -218,12 +218,62 @@ def test_histogram_constant_volume_and_reference_example():
     np.testing.assert_array_equal(got, ref)
     assert got.sum() == codes.size
     # the streaming kernel: every lane of every wave on the same bin (replicated counters)
+    # (20000 / 65536 bins: the tiled and packed-16 paths, one add of the lane count per
+    # wave-uniform bin; the box leaves a partial last step -- waves with inactive lanes)
     for fmt, code in ((4, 200), (5, 40000), (7, 0x3F000000)):
         codes = np.full((9, 40, 512), code, ob.CODE_DTYPE[fmt])
-        got = gpu_histogram(codes, fmt, 0.0, 1.0, (0, 0, 0), (512, 40, 9), 256)
-        ref, _ = ob.histogram_range(ob.Volume(codes, fmt), (0, 0, 0), (512, 40, 9), 256)
-        np.testing.assert_array_equal(got, ref)
-        assert got.sum() == codes.size
+        codes[4, 7:9, 100:300] = code // 2   # one run of another bin, partly wave-uniform
+        for nb in (256, 20000, 65536):
+            for box in (((0, 0, 0), (512, 40, 9)), ((0, 0, 0), (512, 40, 8)), ((8, 1, 0), (504, 39, 9))):
+                got = gpu_histogram(codes, fmt, 0.0, 1.0, *box, nb)
+                ref, _ = ob.histogram_range(ob.Volume(codes, fmt), *box, nb)
+                np.testing.assert_array_equal(got, ref, err_msg=f"fmt={fmt} nb={nb} box={box}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fmt,mapping,nbins,fill", [
+    (5, (0.0, 1.0), 65536, (40000, 40001)),    # integer bins, a low and a high 16-bit half
+    (5, (0.0, 1.0), 65536, (40001,)),
+    (5, (-1.0, 3.0), 50000, (123, 124)),       # float bins
+    (7, (0.0, 1.0), 60000, (0x3F000000, 0x3F000001)),
+])
+def test_histogram_packed16_counter_wraps(fmt, mapping, nbins, fill):
+    """More bins than one LDS tile of 32-bit counters: one pass over packed 16-bit counters.
+    64 Mi voxels on at most two bins: alternating bins (no wave-uniform voxel) cross the 2^14
+    flush threshold of both halves of one counter word many times per workgroup; a single bin
+    is counted in the waves' run registers; a sprinkle of random codes lands everywhere else."""
+    rng = np.random.default_rng(nbins)
+    codes = np.resize(np.array(fill, ob.CODE_DTYPE[fmt]), 1024 * 1024 * 64).reshape(64, 1024, 1024)
+    flat = codes.reshape(-1)
+    idx = rng.choice(flat.size, 100000, replace=False)
+    flat[idx] = rand_codes(rng, fmt, (100000,))
+    full = ((0, 0, 0), (1024, 1024, 64))
+    got = gpu_histogram(codes, fmt, *mapping, *full, nbins)
+    ref, _ = ob.histogram_range(ob.Volume(codes, fmt, *mapping), *full, nbins)
+    np.testing.assert_array_equal(got, ref)
+    # a padded sub-box (masked end items) through the same path
+    box = ((3, 1, 2), (1021, 1000, 60))
+    got = gpu_histogram(codes, fmt, *mapping, *box, nbins)
+    ref, _ = ob.histogram_range(ob.Volume(codes, fmt, *mapping), *box, nbins)
+    np.testing.assert_array_equal(got, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fmt", [5, 7])
+def test_histogram_packed16_matches_tiled_passes(fmt):
+    """Knob histogram.packed16 = 0: one pass per LDS tile of 32-bit counters, same counts."""
+    rng = np.random.default_rng(fmt)
+    codes = rand_codes(rng, fmt, (40, 100, 256), specials=True)
+    runs = []
+    for k in (1, 0):
+        lib.vktHipSetTuningKnob(b"histogram.packed16", k)
+        try:
+            runs.append(gpu_histogram(codes, fmt, 0.0, 1.0, (0, 0, 0), (256, 100, 40), 65536))
+        finally:
+            lib.vktHipSetTuningKnob(b"histogram.packed16", -1)
+    np.testing.assert_array_equal(runs[0], runs[1])
+    ref, _ = ob.histogram_range(ob.Volume(codes, fmt), (0, 0, 0), (256, 100, 40), 65536)
+    np.testing.assert_array_equal(runs[0], ref)
 
 
 def check_float(name, gpu, oracle, exact, terms_abs_sum, n):

@@ -317,6 +317,12 @@ def main():
         for nb in (256, 1024, 4096, 10240, 65536):
             ms = timed(lambda: lib.vktHipHistogramRange(V, o, last, bins, nb, 0), R)
             report(f"reduce Histogram 1024^3 UInt16 {nb} bins", ms, 2 * n ** 3, n ** 3)
+        # one pass over packed 16-bit counters vs one pass per LDS tile (knob histogram.packed16),
+        # integer bins (unit mapping) and float bins (mapping [-1, 3] on the same codes: 50 000 bins)
+        lib.vktHipSetTuningKnob(b"histogram.packed16", 0)
+        ms = timed(lambda: lib.vktHipHistogramRange(V, o, last, bins, 65536, 0), R)
+        report("reduce Histogram 1024^3 UInt16 65536 bins [one pass per tile]", ms, 2 * n ** 3, n ** 3)
+        lib.vktHipSetTuningKnob(b"histogram.packed16", -1)
         sub0, sub1 = Vec3i_t(64, 64, 64), Vec3i_t(960, 960, 960)
         ms = timed(lambda: lib.vktHipHistogramRange(V, sub0, sub1, bins, 256, 0), R)
         report("reduce Histogram UInt16 896^3 sub-box of 1024^3, 256 bins", ms, 2 * 896 ** 3, 896 ** 3)
@@ -338,6 +344,9 @@ def main():
         lib.vktHipFillRange(Vc, o, last, C.c_float(0.5))
         ms = timed(lambda: lib.vktHipHistogramRange(Vc, o, last, bins, 256, 0), R)
         report("reduce Histogram 1024^3 UInt16 256 bins, constant volume", ms, 2 * n ** 3, n ** 3)
+        for nb in (20000, 65536):   # the tiled / packed-16 paths (no counter replicas)
+            ms = timed(lambda: lib.vktHipHistogramRange(Vc, o, last, bins, nb, 0), R)
+            report(f"reduce Histogram 1024^3 UInt16 {nb} bins, constant volume", ms, 2 * n ** 3, n ** 3)
         agg = _lib.Aggregates_t()
         ms = timed(lambda: lib.vktHipAggregatesRange(V, o, last, C.byref(agg)), R)
         report("reduce Aggregates 1024^3 UInt16 (2 passes, incl. D2H of the result)", ms, 2 * 2 * n ** 3, n ** 3)

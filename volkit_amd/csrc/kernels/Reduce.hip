@@ -356,6 +356,7 @@ namespace hipk
     // Items: 8 consecutive voxels of one range row; a wave takes 4 x 64 items per step (all
     // loads in flight before the first atomic), grid-stride; CONTIG ranges are one span.
     constexpr uint32_t kReplicatedMaxBins = 10240;
+    constexpr uint32_t kP16Flush = 0x4000u;   // packed 16-bit counters: moved to HBM at 2^14
     constexpr uint32_t kFastMaxTiles = 8;
     constexpr int kTileBlock = 1024;
 
@@ -430,7 +431,23 @@ namespace hipk
     // exactly (codec::decodeUnit), scale = numBins / 1 = 2^k, and f = c * 2^(k-16) is exact and
     // in [0, numBins), so the reference's (size_t)((v - lo) * scale) is c >> (16 - k).
     // UInt8: taken when the host evaluation of all 256 bins (hostBinU8) is such a shift.
-    template <int FMT, bool CONTIG, bool TILED, int BLOCK, bool SHIFT = false>
+    //
+    // P16 (TILED, UInt16 / Float32, more bins than one tile of 32-bit counters -- a UInt16
+    // histogram with one bin per code): two 16-bit counters per LDS word, so up to ~80 K bins
+    // take ONE pass instead of one pass per tile.  A half must never reach 2^16 (its carry
+    // would corrupt the neighbour, and a wrap could not be told from the neighbour's carry):
+    // a lane whose add returned a half >= kP16Flush moves kP16Flush from that half to the bin
+    // in HBM with a compare-and-swap that succeeds only while the half still holds that much.
+    // Every move is exact whatever the order of the racing adds and movers (and whatever an
+    // LDS atomic returns to same-address lanes of one instruction), a half never goes below
+    // 0, and it stays < 2^16 unless 49 152 adds to that one counter land while every lane
+    // that saw it above the threshold is still on its way to the CAS.  Adds here are 1 per
+    // lane (wave-uniform items go to the run registers below), and same-address lanes of an
+    // LDS atomic serialise (measured: ~2 cycles per lane), so that needs the movers stalled
+    // for ~100 000 cycles while the other waves of the workgroup keep issuing; a context save
+    // stops the whole workgroup.  (A first version flushed on exactly kP16Flush - 1 returned:
+    // 60 moves went missing on 64 Mi voxels alternating between the two halves of one word.)
+    template <int FMT, bool CONTIG, bool TILED, int BLOCK, bool SHIFT = false, bool P16 = false>
     __global__ __launch_bounds__(BLOCK) void histogramFastKernel(FastHistArgs h)
     {
         constexpr int BPV = FMT == codec::FmtUInt8 ? 1 : FMT == codec::FmtUInt16 ? 2 : 4;
@@ -439,7 +456,8 @@ namespace hipk
         extern __shared__ uint32_t cnt[];
         __shared__ uint32_t lut[FMT == codec::FmtUInt8 ? 256 : 1];
         uint32_t const rowShift = h.rShift + 2;   // byte offset of a counter row
-        uint32_t const total = TILED ? h.tileBins : (h.nb + 1) << h.rShift;
+        static_assert(!P16 || (TILED && FMT != codec::FmtUInt8), "P16: tiled UInt16 / Float32");
+        uint32_t const total = TILED ? (P16 ? (h.tileBins + 1) / 2 : h.tileBins) : (h.nb + 1) << h.rShift;
         for (uint32_t i = threadIdx.x; i < total; i += BLOCK)
             cnt[i] = 0;
         if constexpr (FMT == codec::FmtUInt8 && !SHIFT)
@@ -460,6 +478,7 @@ namespace hipk
         char* const cLane = reinterpret_cast<char*>(cnt) + (TILED ? 0u : (lane & ((1u << h.rShift) - 1u)) << 2);
 
         auto voxelOf = [&](uint64_t item) { return spanVoxel<CONTIG>(h, item); };
+        uint32_t runBin = ~0u, runCount = 0u;   // TILED: the wave's run of uniform voxels
         auto add = [&](uint32_t b) {
             if constexpr (TILED)
             {
@@ -470,13 +489,92 @@ namespace hipk
             else
                 atomicAdd(reinterpret_cast<uint32_t*>(cLane + (b << rowShift)), 1u);
         };
+        // The 8 bins of an item.  TILED (no counter replicas): an item whose 8 voxels are on one
+        // bin in every active lane of the wave (constant regions -- empty space) never touches
+        // LDS: the wave counts it in a run register (runBin, runCount; identical in every lane, lane 0
+        // always active) that goes to HBM with one 64-bit atomic when the wave's uniform bin
+        // changes and at the end.  64 lanes adding to one LDS word serialise: a constant 1024^3
+        // volume took 3.5 ms against 0.33 ms streaming.  Other items add 1 per voxel.
+        // P16: all 8 returning adds are issued before the threshold checks.
+        auto flushRun = [&] {
+            if (runCount != 0u && lane == 0u)
+                atomicAdd(&h.bins[h.tileBase + runBin], static_cast<unsigned long long>(runCount));
+        };
+        auto add8 = [&](uint32_t const (&b)[8]) {
+            if constexpr (TILED)
+            {
+                // one check per item: all 8 voxels of every active lane on one bin
+                bool same = true;
+#pragma unroll
+                for (int j = 1; j < 8; ++j)
+                    same = same && b[j] == b[0];
+                uint32_t const t0 = __builtin_amdgcn_readfirstlane(b[0] - h.tileBase);
+                if (__all(same && b[0] - h.tileBase == t0))
+                {
+                    if (t0 < h.tileBins)
+                    {
+                        if (t0 != runBin)
+                        {
+                            flushRun();
+                            runBin = t0;
+                            runCount = 0u;
+                        }
+                        runCount += 8u * static_cast<uint32_t>(__popcll(__activemask()));
+                    }
+                    return;
+                }
+                uint32_t old[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                {
+                    uint32_t const t = b[j] - h.tileBase;
+                    if constexpr (P16)
+                        old[j] = t < h.tileBins ? atomicAdd(&cnt[t >> 1], 1u << ((t & 1u) << 4)) : 0u;
+                    else if (t < h.tileBins)
+                        atomicAdd(&cnt[t], 1u);
+                }
+                if constexpr (P16)
+                {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j)
+                    {
+                        uint32_t const t = b[j] - h.tileBase;
+                        uint32_t const sh = (t & 1u) << 4;
+                        if (t < h.tileBins && ((old[j] >> sh) & 0xFFFFu) >= kP16Flush)
+                        {
+                            // move kP16Flush to HBM if the half still holds that much: a CAS, so
+                            // racing movers never take more than is there
+                            uint32_t cur = atomicAdd(&cnt[t >> 1], 0u);
+                            while (((cur >> sh) & 0xFFFFu) >= kP16Flush)
+                            {
+                                uint32_t const prev = atomicCAS(&cnt[t >> 1], cur, cur - (kP16Flush << sh));
+                                if (prev == cur)
+                                {
+                                    atomicAdd(&h.bins[h.tileBase + t], static_cast<unsigned long long>(kP16Flush));
+                                    break;
+                                }
+                                cur = prev;
+                            }
+                        }
+                    }
+                }
+            }
+            else
+            {
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    add(b[j]);
+            }
+        };
         // m: valid voxels of the item (padded rows); the others go to the trash row / no tile
         auto count8 = [&](uint32_t const (&c)[8], uint32_t m) {
             if constexpr (SHIFT)
             {
+                uint32_t b[8];
 #pragma unroll
                 for (int j = 0; j < 8; ++j)
-                    add((m >> j) & 1u ? c[j] >> h.binShift : h.nb);
+                    b[j] = (m >> j) & 1u ? c[j] >> h.binShift : h.nb;
+                add8(b);
             }
             else if constexpr (FMT == codec::FmtUInt8)
             {
@@ -490,6 +588,7 @@ namespace hipk
             }
             else
             {
+                uint32_t b[8];
 #pragma unroll
                 for (int j = 0; j < 8; j += 2)
                 {
@@ -507,9 +606,10 @@ namespace hipk
                     else
                         v = f32x2{codec::bitsToFloat(c[j]), codec::bitsToFloat(c[j + 1])};
                     f32x2 const f = (v - h.lo) * h.scale;
-                    add((m >> j) & 1u ? fastBin(f.x, h.nbf, h.nb) : h.nb);
-                    add((m >> (j + 1)) & 1u ? fastBin(f.y, h.nbf, h.nb) : h.nb);
+                    b[j] = (m >> j) & 1u ? fastBin(f.x, h.nbf, h.nb) : h.nb;
+                    b[j + 1] = (m >> (j + 1)) & 1u ? fastBin(f.y, h.nbf, h.nb) : h.nb;
                 }
+                add8(b);
             }
         };
 
@@ -532,12 +632,14 @@ namespace hipk
             load8<BPV, true>(h.data, voxelOf(it), c);
             count8(c, itemMask<CONTIG>(h, it));
         }
+        if constexpr (TILED)
+            flushRun();   // (every lane reconverged; lane 0 holds the run)
         __syncthreads();
         if constexpr (TILED)
         {
             for (uint32_t t = threadIdx.x; t < h.tileBins; t += BLOCK)
             {
-                uint32_t const c = cnt[t];
+                uint32_t const c = P16 ? (cnt[t >> 1] >> ((t & 1u) << 4)) & 0xFFFFu : cnt[t];
                 if (c)
                     atomicAdd(&h.bins[h.tileBase + t], static_cast<unsigned long long>(c));
             }
@@ -854,6 +956,32 @@ namespace hipk
             unsigned const perCU = static_cast<unsigned>(std::min<size_t>(8, (160u * 1024u) / (lds + 1024u)));
             unsigned const g = streamingGrid(items, 64u * 4u * (kBlock / 64), std::max(1u, perCU));
             VKT_FAST_HIST_FMT(false, kBlock, g, lds);
+        }
+        else if (tiles > 1 && fmt != codec::FmtUInt8 && (hh.numBins + 1) / 2 <= tileCap &&
+                 rt::knob(rt::Knob::HistogramPacked16) != 0)
+        {
+            // P16: every bin in one pass, two 16-bit counters per LDS word
+            h.rShift = 0;
+            h.tileBase = 0;
+            h.tileBins = h.nb;
+            unsigned const g = streamingGrid(items, 64u * 4u * (kTileBlock / 64), 1);
+            size_t const lds = static_cast<size_t>((h.nb + 1) / 2) * 4u;
+#define VKT_P16(FMT, SH)                                                                                           \
+    do {                                                                                                           \
+        if (contig)                                                                                                \
+            hipLaunchKernelGGL((histogramFastKernel<FMT, true, true, kTileBlock, SH, true>), dim3(g),              \
+                               dim3(kTileBlock), lds, s, h);                                                       \
+        else                                                                                                       \
+            hipLaunchKernelGGL((histogramFastKernel<FMT, false, true, kTileBlock, SH, true>), dim3(g),             \
+                               dim3(kTileBlock), lds, s, h);                                                       \
+    } while (0)
+            if (shift)
+                VKT_P16(codec::FmtUInt16, true);
+            else if (fmt == codec::FmtUInt16)
+                VKT_P16(codec::FmtUInt16, false);
+            else
+                VKT_P16(codec::FmtFloat32, false);
+#undef VKT_P16
         }
         else
         {

@@ -79,6 +79,7 @@ namespace rt
         PointwiseGeneral,              // 0: boxes the aligned path cannot take use the scalar kernel
         PointwiseMergeSectors,         // 0: no 64-B sector completion at row ends
         PointwiseGeneral32,            // 0: the general path uses 64-bit addressing everywhere (tests)
+        HistogramPacked16,             // 0: histograms beyond one LDS tile take one pass per tile
         Count
     };
     int64_t knob(Knob k);
