@@ -35,7 +35,25 @@ namespace vkt
             return p;
         }
 
-        thread_local ExecutionPolicy tlsPolicy = initialPolicy();
+        // Constant-initialised (no per-access TLS init guard) with a lazy first-use flag:
+        // GetThreadExecutionPolicy runs on every getData()/migrate() of every volume.
+        struct TlsPolicy
+        {
+            ExecutionPolicy policy;
+            bool init;
+        };
+        thread_local TlsPolicy tlsPolicy{ExecutionPolicy{}, false};
+
+        ExecutionPolicy& threadPolicy()
+        {
+            TlsPolicy& t = tlsPolicy;
+            if (!t.init)
+            {
+                t.policy = initialPolicy();
+                t.init = true;
+            }
+            return t.policy;
+        }
 
         std::mutex& registryMutex()
         {
@@ -52,9 +70,9 @@ namespace vkt
         ResourceHandle nextHandle = 0;
     } // namespace
 
-    void SetThreadExecutionPolicy(ExecutionPolicy policy) { tlsPolicy = policy; }
+    void SetThreadExecutionPolicy(ExecutionPolicy policy) { threadPolicy() = policy; }
 
-    ExecutionPolicy GetThreadExecutionPolicy() { return tlsPolicy; }
+    ExecutionPolicy GetThreadExecutionPolicy() { return threadPolicy(); }
 
     ResourceHandle RegisterManagedResource(ManagedResource resource)
     {
