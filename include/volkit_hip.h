@@ -133,6 +133,41 @@ VKTAPI vktError vktHipResampleSlabSourceRange(int32_t dstGlobalDimZ, int32_t dst
                                               int32_t needsNeighbours,
                                               int32_t* srcZBegin, int32_t* srcZEnd);
 
+/* Z-slab plan for Resample over `nranks` ranks (no reference counterpart): the
+ * global source planes [*localZ0, *localZ1) rank `rank` holds (its ceil-partition slab plus
+ * the halo its dst slab reads) and the plane ranges it sends to / receives from each peer.
+ * *count receives the number of transfers; `transfers` (may be NULL to query the count) must
+ * hold `capacity` >= *count entries.  Same plan as volkit_amd/slab.py:plan_resample. */
+typedef struct vktHipSlabTransfer
+{
+    int32_t peer;
+    int32_t z0, z1;   /* global source planes [z0, z1) */
+    int32_t send;     /* 1: this rank sends them to peer, 0: receives them from peer */
+} vktHipSlabTransfer_t;
+VKTAPI vktError vktHipSlabResamplePlan(int32_t dstGlobalDimZ, int32_t srcGlobalDimZ, int32_t nranks, int32_t rank,
+                                       vktFilterMode fm, int32_t needsNeighbours, int32_t* localZ0,
+                                       int32_t* localZ1, vktHipSlabTransfer_t* transfers, int32_t capacity,
+                                       int32_t* count);
+
+/* In-library halo exchange over RCCL (xGMI): one communicator per process / GPU.  Rank 0
+ * creates the id, the caller distributes it (MPI, a file, torch.distributed ...), every rank
+ * calls vktHipCommInitRank with it on the device the library uses (vktHipSetDevice). */
+typedef struct
+{
+    char internal[128];   /* ncclUniqueId */
+} vktHipCommId_t;
+typedef struct vktHipComm_impl* vktHipComm_t;
+VKTAPI vktError vktHipCommGetUniqueId(vktHipCommId_t* id);
+VKTAPI vktError vktHipCommInitRank(vktHipComm_t* comm, int32_t nranks, vktHipCommId_t id, int32_t rank);
+VKTAPI vktError vktHipCommDestroy(vktHipComm_t comm);
+/* `localSrc` holds global source planes [localZ0, localZ0 + localSrc.dimZ) (X/Y dims global).
+ * Sends the owned planes the peers' dst slabs read and receives this rank's halo planes into
+ * the buffer: one ncclGroupStart .. ncclGroupEnd round of ncclSend / ncclRecv on the compute
+ * stream, so a vktHipResampleSlab enqueued next reads the halo.  Returns once enqueued. */
+VKTAPI vktError vktHipSlabExchangeHalo(vktHipComm_t comm, vktHipVolumeView_t localSrc, int32_t localZ0,
+                                       int32_t dstGlobalDimZ, int32_t srcGlobalDimZ, vktFilterMode fm,
+                                       int32_t needsNeighbours);
+
 /* replaces TransformRange_cuda (reference src/vkt/Transform_cuda.hpp:12-30, an empty
  * stub there): host callbacks cannot run on the GPU, so the range is staged to host,
  * transformed in the serial order, and written back. */

@@ -1,0 +1,140 @@
+"""Native Z-slab plan and RCCL halo exchange (include/volkit_hip.h: vktHipSlabResamplePlan,
+vktHipComm*, vktHipSlabExchangeHalo; volkit_amd/csrc/runtime/Comm.cpp).
+
+CPU: the C plan equals volkit_amd/slab.py:plan_resample (which the gloo tests exercise) for
+every rank of many layouts, transfers pair up across ranks, and argument errors are
+returned.  GPU: a one-rank communicator (create, exchange -- nothing to move -- destroy).
+The multi-rank exchange needs one GPU per rank (RCCL refuses two ranks on one device):
+`test_two_rank_exchange` runs only where two GPUs are visible, i.e. not on the 1-GPU pool
+this round's GPU tests ran on.
+"""
+import ctypes as C
+import os
+
+import pytest
+
+from volkit_amd import _lib, slab
+from volkit_amd._lib import HipCommId_t, HipSlabTransfer_t, HipVolumeView_t, lib
+
+NEAREST, LINEAR = 0, 1
+
+
+def c_plan(dst_gdz, src_gdz, world, rank, fm, chain):
+    z0, z1, n = C.c_int32(), C.c_int32(), C.c_int32()
+    assert lib.vktHipSlabResamplePlan(dst_gdz, src_gdz, world, rank, fm, int(chain), C.byref(z0), C.byref(z1),
+                                      None, 0, C.byref(n)) == 0, _lib.last_error()
+    xs = (HipSlabTransfer_t * max(1, n.value))()
+    assert lib.vktHipSlabResamplePlan(dst_gdz, src_gdz, world, rank, fm, int(chain), C.byref(z0), C.byref(z1),
+                                      xs, n.value, C.byref(n)) == 0, _lib.last_error()
+    recvs = [(x.peer, x.z0, x.z1) for x in xs[:n.value] if not x.send]
+    sends = [(x.peer, x.z0, x.z1) for x in xs[:n.value] if x.send]
+    return (z0.value, z1.value), sorted(recvs), sorted(sends)
+
+
+LAYOUTS = [(2048, 1024), (1024, 512), (1024, 1024), (1000, 768), (768, 1000), (64, 7), (7, 64), (3, 17), (17, 3),
+           (256, 128), (129, 64)]
+
+
+@pytest.mark.parametrize("dst_gdz,src_gdz", LAYOUTS)
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
+@pytest.mark.parametrize("fm,chain", [(NEAREST, False), (LINEAR, False), (LINEAR, True)])
+def test_native_plan_matches_slab_py(dst_gdz, src_gdz, world, fm, chain):
+    for rank in range(world):
+        py = slab.plan_resample(dst_gdz, src_gdz, world, rank, fm, chain)
+        local, recvs, sends = c_plan(dst_gdz, src_gdz, world, rank, fm, chain)
+        assert local == tuple(py.local_src), (rank, local, py.local_src)
+        assert recvs == sorted(py.recvs), rank
+        assert sends == sorted(py.sends), rank
+
+
+def test_every_plane_received_is_sent_once():
+    """Across all ranks the transfers pair up: each (receiver, sender, planes) appears as a send."""
+    for dst_gdz, src_gdz in LAYOUTS:
+        for world in (2, 3, 8):
+            recvs, sends = set(), set()
+            for rank in range(world):
+                _, r, s = c_plan(dst_gdz, src_gdz, world, rank, LINEAR, True)
+                recvs |= {(rank, p, a, b) for p, a, b in r}
+                sends |= {(p, rank, a, b) for p, a, b in s}
+            assert recvs == sends
+
+
+def test_plan_errors_are_returned():
+    z0, z1, n = C.c_int32(), C.c_int32(), C.c_int32()
+    assert lib.vktHipSlabResamplePlan(64, 32, 4, 4, LINEAR, 1, C.byref(z0), C.byref(z1), None, 0, C.byref(n)) != 0
+    assert "invalid rank" in _lib.last_error()
+    assert lib.vktHipSlabResamplePlan(64, 32, 4, 1, LINEAR, 1, None, C.byref(z1), None, 0, C.byref(n)) != 0
+    # too small a transfer array
+    assert lib.vktHipSlabResamplePlan(64, 32, 4, 1, LINEAR, 1, C.byref(z0), C.byref(z1), None, 0, C.byref(n)) == 0
+    assert n.value > 0
+    xs = (HipSlabTransfer_t * 1)()
+    assert lib.vktHipSlabResamplePlan(64, 32, 4, 1, LINEAR, 1, C.byref(z0), C.byref(z1), xs, n.value - 1,
+                                      C.byref(n)) != 0
+    assert "too small" in _lib.last_error()
+    assert lib.vktHipSlabExchangeHalo(None, HipVolumeView_t(), 0, 64, 32, LINEAR, 1) != 0
+    assert "null communicator" in _lib.last_error()
+
+
+@pytest.mark.gpu
+def test_one_rank_communicator():
+    import torch
+    torch.cuda.init()
+    uid = HipCommId_t()
+    assert lib.vktHipCommGetUniqueId(C.byref(uid)) == 0, _lib.last_error()
+    comm = C.c_void_p()
+    assert lib.vktHipCommInitRank(C.byref(comm), 1, uid, 0) == 0, _lib.last_error()
+    try:
+        buf = torch.zeros(16 * 16 * 8 * 2, dtype=torch.uint8, device="cuda")
+        view = HipVolumeView_t(buf.data_ptr(), 16, 16, 8, 5, 0.0, 1.0)
+        # one rank owns every plane: nothing to move
+        assert lib.vktHipSlabExchangeHalo(comm, view, 0, 16, 8, LINEAR, 1) == 0, _lib.last_error()
+        torch.cuda.synchronize()
+    finally:
+        assert lib.vktHipCommDestroy(comm) == 0, _lib.last_error()
+
+
+def _two_rank_worker(rank, uid_bytes, result_q):
+    import torch
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    torch.cuda.set_device(rank)
+    assert lib.vktHipSetDevice(rank) == 0
+    uid = HipCommId_t()
+    C.memmove(C.addressof(uid), uid_bytes, 128)
+    comm = C.c_void_p()
+    assert lib.vktHipCommInitRank(C.byref(comm), 2, uid, rank) == 0, _lib.last_error()
+    dst_gdz, src_gdz, dx, dy = 64, 32, 32, 8
+    (lo, hi), recvs, sends = c_plan(dst_gdz, src_gdz, 2, rank, LINEAR, True)
+    own = slab.slab_bounds(src_gdz, 2, rank)
+    plane = dx * dy * 4
+    buf = torch.zeros((hi - lo) * plane, dtype=torch.uint8, device="cuda")
+    # every owned plane z holds the byte pattern z + 1; halo planes start at 0
+    for z in range(*own):
+        buf[(z - lo) * plane:(z - lo + 1) * plane] = z + 1
+    view = HipVolumeView_t(buf.data_ptr(), dx, dy, hi - lo, 7, 0.0, 1.0)
+    err = lib.vktHipSlabExchangeHalo(comm, view, lo, dst_gdz, src_gdz, LINEAR, 1)
+    torch.cuda.synchronize()
+    got = buf.view(hi - lo, plane)[:, 0].cpu().numpy().tolist()
+    lib.vktHipCommDestroy(comm)
+    result_q.put((rank, err, lo, got))
+
+
+@pytest.mark.gpu
+def test_two_rank_exchange():
+    """Two processes, one GPU each: every halo plane arrives with its owner's pattern."""
+    import torch
+    import torch.multiprocessing as mp
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two GPUs (RCCL refuses two ranks on one device)")
+    uid = HipCommId_t()
+    assert lib.vktHipCommGetUniqueId(C.byref(uid)) == 0
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_two_rank_worker, args=(r, C.string_at(C.addressof(uid), 128), q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, err, lo, got in res:
+        assert err == 0
+        assert got == [lo + i + 1 for i in range(len(got))], (rank, got)

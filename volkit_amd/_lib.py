@@ -67,6 +67,15 @@ class HipBrickRange_t(C.Structure):
     _fields_ = [("brick", HipVolumeView_t), ("first", Vec3i_t), ("last", Vec3i_t)]
 
 
+class HipSlabTransfer_t(C.Structure):
+    _fields_ = [("peer", i32), ("z0", i32), ("z1", i32), ("send", i32)]
+
+
+class HipCommId_t(C.Structure):
+    _fields_ = [("internal", C.c_char * 128)]
+
+
+c_comm = C.c_void_p           # vktHipComm_t (opaque handle)
 c_arr = C.c_void_p            # vktArray3D_vktStructuredVolume (opaque handle)
 c_hist = C.c_void_p           # vktHistogram (opaque handle)
 
@@ -205,6 +214,12 @@ SIGNATURES = {
     "vktHipResample": (c_err, [HipVolumeView_t, HipVolumeView_t, C.c_int]),
     "vktHipResampleSlab": (c_err, [HipVolumeView_t, HipVolumeView_t, C.c_int, i32, i32, i32, i32]),
     "vktHipResampleSlabSourceRange": (c_err, [i32, i32, i32, i32, C.c_int, i32, P(i32), P(i32)]),
+    "vktHipSlabResamplePlan": (c_err, [i32, i32, i32, i32, C.c_int, i32, P(i32), P(i32), P(HipSlabTransfer_t),
+                                       i32, P(i32)]),
+    "vktHipCommGetUniqueId": (c_err, [P(HipCommId_t)]),
+    "vktHipCommInitRank": (c_err, [P(c_comm), i32, HipCommId_t, i32]),
+    "vktHipCommDestroy": (c_err, [c_comm]),
+    "vktHipSlabExchangeHalo": (c_err, [c_comm, HipVolumeView_t, i32, i32, i32, C.c_int, i32]),
     "vktHipTransformRange1": (c_err, [HipVolumeView_t, Vec3i_t, Vec3i_t, UnaryOp]),
     "vktHipTransformRange2": (c_err, [HipVolumeView_t, HipVolumeView_t, Vec3i_t, Vec3i_t, Vec3i_t, BinaryOp]),
     "vktHipSynthesize": (c_err, [HipVolumeView_t, u64]),

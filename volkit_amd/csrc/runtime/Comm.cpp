@@ -1,0 +1,269 @@
+// Comm.cpp -- in-library Z-slab halo exchange over RCCL (xGMI) for C and C++ callers.
+//
+// The reference is single-device and has no communication layer (its CudaContext is
+// declaration-only: include/c/vkt/CudaContext.h:17-65).  SURVEY.md §8(e) asks for Z-slab
+// partitions with the Resample halo moved by ncclSend / ncclRecv inside one group; the
+// Python layer does the same through torch.distributed (volkit_amd/slab.py).  This file is
+// the native path: the plan (which global source planes every rank owns, holds and moves --
+// the same ceil partition and exact z index table as slab.py, checked against it by
+// tests/test_comm.py) and one grouped RCCL send/receive round on the library's compute
+// stream, so a Resample enqueued next on that stream reads the halo.
+
+#include "Runtime.hpp"
+#include "volkit_codec.hpp"
+#include "volkit_hip.h"
+
+#include <rccl/rccl.h>
+
+#include <dlfcn.h>
+
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <type_traits>
+#include <vector>
+
+struct vktHipComm_impl
+{
+    ncclComm_t comm = nullptr;
+    int32_t rank = 0, nranks = 0;
+};
+
+namespace vkt
+{
+namespace
+{
+    static_assert(sizeof(vktHipCommId_t) == sizeof(ncclUniqueId), "vktHipCommId_t mirrors ncclUniqueId");
+
+    // RCCL is bound at first use, not linked: a process that already holds an RCCL (PyTorch
+    // ships its own librccl.so.1) keeps that one -- linking /opt/rocm's made the loader pick
+    // whichever came first for both users, and two ROCm builds' RCCL/HIP in one process
+    // aborted at exit (free(): invalid pointer).
+    struct Rccl
+    {
+        decltype(&::ncclGetUniqueId) getUniqueId = nullptr;
+        decltype(&::ncclCommInitRank) commInitRank = nullptr;
+        decltype(&::ncclCommDestroy) commDestroy = nullptr;
+        decltype(&::ncclGroupStart) groupStart = nullptr;
+        decltype(&::ncclGroupEnd) groupEnd = nullptr;
+        decltype(&::ncclSend) send = nullptr;
+        decltype(&::ncclRecv) recv = nullptr;
+        decltype(&::ncclGetErrorString) errorString = nullptr;
+        bool ok = false;
+    };
+
+    Rccl const& rccl()
+    {
+        static Rccl r;
+        static std::once_flag once;
+        std::call_once(once, [] {
+            void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+            if (h == nullptr)
+                h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+            if (h == nullptr)
+                h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+            if (h == nullptr)
+                return;
+            auto sym = [&](auto& f, char const* name) {
+                f = reinterpret_cast<std::remove_reference_t<decltype(f)>>(dlsym(h, name));
+                return f != nullptr;
+            };
+            r.ok = sym(r.getUniqueId, "ncclGetUniqueId") && sym(r.commInitRank, "ncclCommInitRank") &&
+                   sym(r.commDestroy, "ncclCommDestroy") && sym(r.groupStart, "ncclGroupStart") &&
+                   sym(r.groupEnd, "ncclGroupEnd") && sym(r.send, "ncclSend") && sym(r.recv, "ncclRecv") &&
+                   sym(r.errorString, "ncclGetErrorString");
+        });
+        return r;
+    }
+
+    vktError ncclFail(char const* what, ncclResult_t r)
+    {
+        return rt::fail((std::string(what) + ": " + rccl().errorString(r)).c_str());
+    }
+
+    vktError noRccl(char const* what)
+    {
+        return rt::fail((std::string(what) + ": librccl.so.1 not found").c_str());
+    }
+
+    // planes [z0, z1) of a ceil partition of n planes over `world` ranks (slab.py:slab_bounds)
+    void slabBounds(int32_t n, int32_t world, int32_t rank, int32_t& z0, int32_t& z1)
+    {
+        int64_t const size = (static_cast<int64_t>(n) + world - 1) / world;
+        z0 = static_cast<int32_t>(std::min<int64_t>(rank * size, n));
+        z1 = static_cast<int32_t>(std::min<int64_t>(z0 + size, n));
+    }
+
+    // global source planes rank r's dst slab reads (empty slab: [0, 0))
+    vktError needOf(int32_t dstG, int32_t srcG, int32_t world, int32_t r, vktFilterMode fm, int32_t chain,
+                    int32_t& s0, int32_t& s1)
+    {
+        int32_t d0, d1;
+        slabBounds(dstG, world, r, d0, d1);
+        s0 = s1 = 0;
+        if (d1 <= d0)
+            return vktNoError;
+        return vktHipResampleSlabSourceRange(dstG, d0, d1, srcG, fm, chain, &s0, &s1);
+    }
+
+    // slab.py:plan_resample -- every rank computes the same global plan; sends are the
+    // peers' needs this rank owns, receives its own needs the peers own
+    vktError plan(int32_t dstG, int32_t srcG, int32_t world, int32_t rank, vktFilterMode fm, int32_t chain,
+                  int32_t& lo, int32_t& hi, std::vector<vktHipSlabTransfer_t>& xs)
+    {
+        if (world <= 0 || rank < 0 || rank >= world || dstG <= 0 || srcG <= 0)
+            return rt::fail("vktHipSlabResamplePlan: invalid rank / world / depths");
+        std::vector<int32_t> n0(world), n1(world);
+        for (int32_t r = 0; r < world; ++r)
+        {
+            vktError const e = needOf(dstG, srcG, world, r, fm, chain, n0[r], n1[r]);
+            if (e != vktNoError)
+                return e;
+        }
+        int32_t o0, o1;
+        slabBounds(srcG, world, rank, o0, o1);
+        bool const needs = n1[rank] > n0[rank];
+        lo = needs ? std::min(o0, n0[rank]) : o0;
+        hi = needs ? std::max(o1, n1[rank]) : o1;
+        xs.clear();
+        for (int32_t peer = 0; peer < world; ++peer)
+        {
+            if (peer == rank)
+                continue;
+            int32_t p0, p1;
+            slabBounds(srcG, world, peer, p0, p1);
+            if (needs)
+            {
+                int32_t const a = std::max(n0[rank], p0), b = std::min(n1[rank], p1);
+                if (b > a)
+                    xs.push_back(vktHipSlabTransfer_t{peer, a, b, 0});
+            }
+            if (n1[peer] > n0[peer])
+            {
+                int32_t const a = std::max(n0[peer], o0), b = std::min(n1[peer], o1);
+                if (b > a)
+                    xs.push_back(vktHipSlabTransfer_t{peer, a, b, 1});
+            }
+        }
+        return vktNoError;
+    }
+} // namespace
+} // namespace vkt
+
+using namespace vkt;
+
+extern "C" {
+
+vktError vktHipSlabResamplePlan(int32_t dstGlobalDimZ, int32_t srcGlobalDimZ, int32_t nranks, int32_t rank,
+                                vktFilterMode fm, int32_t needsNeighbours, int32_t* localZ0, int32_t* localZ1,
+                                vktHipSlabTransfer_t* transfers, int32_t capacity, int32_t* count)
+{
+    if (localZ0 == nullptr || localZ1 == nullptr || count == nullptr)
+        return rt::fail("vktHipSlabResamplePlan: null pointer");
+    std::vector<vktHipSlabTransfer_t> xs;
+    vktError const e = plan(dstGlobalDimZ, srcGlobalDimZ, nranks, rank, fm, needsNeighbours, *localZ0, *localZ1, xs);
+    if (e != vktNoError)
+        return e;
+    *count = static_cast<int32_t>(xs.size());
+    if (transfers != nullptr)
+    {
+        if (capacity < *count)
+            return rt::fail("vktHipSlabResamplePlan: transfer array too small");
+        std::copy(xs.begin(), xs.end(), transfers);
+    }
+    return vktNoError;
+}
+
+vktError vktHipCommGetUniqueId(vktHipCommId_t* id)
+{
+    if (id == nullptr)
+        return rt::fail("vktHipCommGetUniqueId: null pointer");
+    ncclUniqueId u;
+    if (!rccl().ok)
+        return noRccl("vktHipCommGetUniqueId");
+    ncclResult_t const r = rccl().getUniqueId(&u);
+    if (r != ncclSuccess)
+        return ncclFail("vktHipCommGetUniqueId", r);
+    std::memcpy(id->internal, u.internal, sizeof(u.internal));
+    return vktNoError;
+}
+
+vktError vktHipCommInitRank(vktHipComm_t* comm, int32_t nranks, vktHipCommId_t id, int32_t rank)
+{
+    if (comm == nullptr)
+        return rt::fail("vktHipCommInitRank: null pointer");
+    *comm = nullptr;
+    if (nranks <= 0 || rank < 0 || rank >= nranks)
+        return rt::fail("vktHipCommInitRank: invalid rank / nranks");
+    if (!rccl().ok)
+        return noRccl("vktHipCommInitRank");
+    VKT_HIP_TRY(hipSetDevice(rt::device()));   // the communicator lives on the library's device
+    ncclUniqueId u;
+    std::memcpy(u.internal, id.internal, sizeof(u.internal));
+    auto* c = new vktHipComm_impl;
+    ncclResult_t const r = rccl().commInitRank(&c->comm, nranks, u, rank);
+    if (r != ncclSuccess)
+    {
+        delete c;
+        return ncclFail("vktHipCommInitRank", r);
+    }
+    c->rank = rank;
+    c->nranks = nranks;
+    *comm = c;
+    return vktNoError;
+}
+
+vktError vktHipCommDestroy(vktHipComm_t comm)
+{
+    if (comm == nullptr)
+        return vktNoError;
+    ncclResult_t const r = rccl().commDestroy(comm->comm);
+    delete comm;
+    return r == ncclSuccess ? vktNoError : ncclFail("vktHipCommDestroy", r);
+}
+
+vktError vktHipSlabExchangeHalo(vktHipComm_t comm, vktHipVolumeView_t localSrc, int32_t localZ0,
+                                int32_t dstGlobalDimZ, int32_t srcGlobalDimZ, vktFilterMode fm,
+                                int32_t needsNeighbours)
+{
+    if (comm == nullptr)
+        return rt::fail("vktHipSlabExchangeHalo: null communicator");
+    int32_t lo, hi;
+    std::vector<vktHipSlabTransfer_t> xs;
+    vktError const e = plan(dstGlobalDimZ, srcGlobalDimZ, comm->nranks, comm->rank, fm, needsNeighbours, lo, hi, xs);
+    if (e != vktNoError)
+        return e;
+    if (xs.empty())
+        return vktNoError;
+    uint32_t const bpv = codec::bytesPerVoxel(localSrc.dataFormat);
+    if (localSrc.data == nullptr || bpv == 0 || localSrc.dimX <= 0 || localSrc.dimY <= 0 || localSrc.dimZ < 0)
+        return rt::fail("vktHipSlabExchangeHalo: invalid local source view");
+    // every plane moved must lie in the local buffer (global planes [localZ0, localZ0 + dimZ))
+    for (vktHipSlabTransfer_t const& x : xs)
+        if (x.z0 < localZ0 || x.z1 > localZ0 + localSrc.dimZ)
+            return rt::fail("vktHipSlabExchangeHalo: the local source buffer does not hold the planes the plan moves");
+    size_t const plane = static_cast<size_t>(localSrc.dimX) * static_cast<size_t>(localSrc.dimY) * bpv;
+    hipStream_t const s = rt::computeStream();
+    ncclResult_t r = rccl().groupStart();
+    if (r != ncclSuccess)
+        return ncclFail("vktHipSlabExchangeHalo: ncclGroupStart", r);
+    for (vktHipSlabTransfer_t const& x : xs)
+    {
+        uint8_t* const p = localSrc.data + static_cast<size_t>(x.z0 - localZ0) * plane;
+        size_t const bytes = static_cast<size_t>(x.z1 - x.z0) * plane;
+        r = x.send ? rccl().send(p, bytes, ncclUint8, x.peer, comm->comm, s)
+                   : rccl().recv(p, bytes, ncclUint8, x.peer, comm->comm, s);
+        if (r != ncclSuccess)
+        {
+            (void)rccl().groupEnd();
+            return ncclFail("vktHipSlabExchangeHalo: ncclSend/ncclRecv", r);
+        }
+    }
+    r = rccl().groupEnd();
+    if (r != ncclSuccess)
+        return ncclFail("vktHipSlabExchangeHalo: ncclGroupEnd", r);
+    return rt::finishLaunch("SlabExchangeHalo_hip");
+}
+
+} // extern "C"
