@@ -197,7 +197,10 @@ def main():
         for lab, f0, f1 in (("x 64..864 (rows start on a 128-B line)", Vec3i_t(64, 100, 100), Vec3i_t(864, 900, 900)),
                             ("x 0..800", Vec3i_t(0, 100, 100), Vec3i_t(800, 900, 900)),
                             ("x 0..1024 y,z 100..900 (plane-contiguous rows)", Vec3i_t(0, 100, 100),
-                             Vec3i_t(1024, 900, 900))):
+                             Vec3i_t(1024, 900, 900)),
+                            ("x,y 0..1024 z 100..900 (one contiguous run)", Vec3i_t(0, 0, 100),
+                             Vec3i_t(1024, 1024, 900)),
+                            ("whole 1024^3 (one contiguous run)", Vec3i_t(0, 0, 0), Vec3i_t(1024, 1024, 1024))):
             nv = (f1.x - f0.x) * (f1.y - f0.y) * (f1.z - f0.z)
             report(f"weak SafeSumRange sub-box {lab}", timed(lambda: lib.vktHipArithmeticRange(5, D, A, B, f0, f1, o),
                                                            R), 6 * nv, nv)
