@@ -75,19 +75,6 @@ namespace hipk
             return (dw >> (8 * ((k * BPV) % 4))) & ((1u << (8 * BPV)) - 1u);
     }
 
-    // wordCode for a lane-dependent k: a select chain over the four dwords (an indexed
-    // vector access would go through scratch)
-    template <int BPV>
-    __device__ __forceinline__ uint32_t wordCodeDyn(u32x4 w, int32_t k)
-    {
-        uint32_t const q = static_cast<uint32_t>(k * BPV) >> 2;
-        uint32_t const dw = q >= 2u ? (q == 3u ? w.w : w.z) : (q == 1u ? w.y : w.x);
-        if constexpr (BPV == 4)
-            return dw;
-        else
-            return (dw >> (8u * (static_cast<uint32_t>(k * BPV) & 3u))) & ((1u << (8 * BPV)) - 1u);
-    }
-
     template <int BPV>
     __device__ __forceinline__ void ldsStoreCode(uint8_t* lds, int32_t voxel, uint32_t code)
     {
@@ -162,13 +149,11 @@ namespace hipk
                 reinterpret_cast<Unaligned16*>(lds + w.li * BPV)->v = w.v;
             else
             {
-                // only the word's valid voxels [ka, kb) (usually one or two): a wave runs the
-                // longest lane's count, not all V masked iterations
-                int32_t const ka = max(max(lo - w.x0, -w.li), 0);
-                int32_t const kb = min(min(hi - w.x0, chunkVox - w.li), V);
-                for (int32_t k = ka; k < kb; ++k)
-                    ldsStoreCode<BPV>(lds, w.li + k,
-                                      w.whole ? wordCodeDyn<BPV>(w.v, k) : loadCode<BPV>(src, w.rb + w.x0 + k));
+#pragma unroll
+                for (int k = 0; k < V; ++k)
+                    if (w.x0 + k >= lo && w.x0 + k < hi && w.li + k >= 0 && w.li + k < chunkVox)
+                        ldsStoreCode<BPV>(lds, w.li + k,
+                                          w.whole ? wordCode<BPV>(w.v, k) : loadCode<BPV>(src, w.rb + w.x0 + k));
             }
         };
         // all loads of the first kStageWords rounds in flight before the first LDS write (a
