@@ -154,6 +154,34 @@ def test_arith_dst_offset_phases(lib, o, fmt, mapping):
                 assert_codes_equal(dd.read(), ref, fmt, f"{op} fmt={fmt} {mapping} dx={dx} {first}->{last}")
 
 
+@pytest.mark.parametrize("fmt", [4, 7, 3, 6])
+@pytest.mark.parametrize("pad", [0, 16, 8])
+def test_collapsed_row_contiguous_lanes(lib, o, fmt, pad):
+    """Whole-volume (one collapsed row) Fill, Copy and arithmetic on 1- and 4-byte formats:
+    full quanta with 16-B aligned operands take the contiguous-lane loop (UInt8 item pairs in
+    one 16-B access, Float32 items as two 4-voxel halves 1 KiB apart), the partial last
+    quantum and 8-B aligned views (pad 8) the per-item loop.  Every voxel vs the oracle."""
+    rng = np.random.default_rng(fmt * 10 + pad)
+    dims = (3, 7, 613)                       # 12 873 voxels: several full quanta + a partial one
+    a = rand_codes(rng, fmt, dims)
+    b = rand_codes(rng, fmt, dims)
+    dinit = rand_codes(rng, fmt, dims)
+    first, last = (0, 0, 0), (dims[2], dims[1], dims[0])
+    from volkit_amd._lib import lib as L
+    for op in ("Sum", "SafeDiff", "Prod"):
+        da, db, dd = Dev(a, fmt, pad=pad), Dev(b, fmt, pad=pad), Dev(dinit, fmt, pad=pad)
+        assert L.vktHipArithmeticRange(OPS.index(op), dd.view, da.view, db.view, vec(first), vec(last),
+                                       vec((0, 0, 0))) == 0, last_error()
+        ref = o.arith(op, [fmt] * 3, [(0.0, 1.0)] * 3, a, b, dinit.copy(), first, last, (0, 0, 0))
+        assert_codes_equal(dd.read(), ref, fmt, f"{op} fmt={fmt} pad={pad}")
+    copy_case(lib, o, fmt, fmt, (0.0, 1.0), (0.0, 1.0), a, dinit, first, last, (0, 0, 0), pad, pad,
+              f"copy fmt={fmt} pad={pad}")
+    d = Dev(dinit, fmt, pad=pad)
+    assert L.vktHipFillRange(d.view, vec(first), vec(last), C.c_float(0.375)) == 0, last_error()
+    ref = o.fill_range(fmt, (0.0, 1.0), (dims[2], dims[1], dims[0]), dinit.copy(), first, last, 0.375)
+    assert_codes_equal(d.read(), ref, fmt, f"fill fmt={fmt} pad={pad}")
+
+
 def test_general_knob_matches_scalar_kernel(lib, o):
     """The same phase-shifted and clamped cases through the general path and, with the knob
     off, through the per-voxel kernel: both equal the oracle."""

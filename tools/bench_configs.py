@@ -463,6 +463,14 @@ def main():
     report("Resample 1024^3->1000^3 UInt16 Nearest (gather)", timed(lambda: lib.vktHipResample(D1000, Rv, 0), R),
            2 * 1000 ** 3 + 2 * e ** 3, 1000 ** 3)
     free(S, Rv, B, D, D1000)
+    # per-format streaming rates of the pointwise engine (8-voxel items: 8 B / 16 B / 32 B per lane)
+    for fmt, bpv, name in ((4, 1, "UInt8"), (7, 4, "Float32")):
+        A8, B8, D8 = alloc((e,) * 3, fmt, seed=8), alloc((e,) * 3, fmt, seed=9), alloc((e,) * 3, fmt)
+        report(f"Copy 1024^3 {name}", timed(lambda: lib.vktHipCopyRange(D8, A8, o, lastE, o), R),
+               2 * bpv * e ** 3, e ** 3)
+        report(f"SumRange 1024^3 {name}", timed(lambda: lib.vktHipArithmeticRange(0, D8, A8, B8, o, lastE, o), R),
+               3 * bpv * e ** 3, e ** 3)
+        free(A8, B8, D8)
 
     if args.big:
         s, e = 1024, 2048
