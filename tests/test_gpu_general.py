@@ -182,6 +182,31 @@ def test_collapsed_row_contiguous_lanes(lib, o, fmt, pad):
     assert_codes_equal(d.read(), ref, fmt, f"fill fmt={fmt} pad={pad}")
 
 
+@pytest.mark.parametrize("fmt", [4, 7, 6])
+@pytest.mark.parametrize("box", [((0, 1, 1), (256, 30, 6)),      # rows of 32 items (even)
+                                 ((16, 2, 0), (136, 29, 7)),     # 15 items per row
+                                 ((8, 0, 1), (264, 31, 5)),      # 32 items, rows start 8 voxels in
+                                 ((3, 1, 1), (253, 30, 6))])     # padded rows: per-item loop
+def test_multirow_contiguous_lanes(lib, o, fmt, box):
+    """Multi-row boxes through the contiguous-lane loop (4-byte formats; rows without padded
+    edges, 16-B aligned rows in every operand) and the cases that stay on the per-item loop
+    (UInt8, padded rows).  Copy and SafeSum vs the oracle."""
+    rng = np.random.default_rng(fmt + box[0][0])
+    dims = (8, 32, 272)
+    a = rand_codes(rng, fmt, dims)
+    b = rand_codes(rng, fmt, dims)
+    dinit = rand_codes(rng, fmt, dims)
+    first, last = box
+    from volkit_amd._lib import lib as L
+    da, db, dd = Dev(a, fmt), Dev(b, fmt), Dev(dinit, fmt)
+    assert L.vktHipArithmeticRange(OPS.index("SafeSum"), dd.view, da.view, db.view, vec(first), vec(last),
+                                   vec((0, 0, 0))) == 0, last_error()
+    ref = o.arith("SafeSum", [fmt] * 3, [(0.0, 1.0)] * 3, a, b, dinit.copy(), first, last, (0, 0, 0))
+    assert_codes_equal(dd.read(), ref, fmt, f"SafeSum fmt={fmt} box={box}")
+    copy_case(lib, o, fmt, fmt, (0.0, 1.0), (0.0, 1.0), a, dinit, first, last, (0, 0, 0), 0, 0,
+              f"copy fmt={fmt} box={box}")
+
+
 def test_general_knob_matches_scalar_kernel(lib, o):
     """The same phase-shifted and clamped cases through the general path and, with the knob
     off, through the per-voxel kernel: both equal the oracle."""

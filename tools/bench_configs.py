@@ -470,6 +470,13 @@ def main():
                2 * bpv * e ** 3, e ** 3)
         report(f"SumRange 1024^3 {name}", timed(lambda: lib.vktHipArithmeticRange(0, D8, A8, B8, o, lastE, o), R),
                3 * bpv * e ** 3, e ** 3)
+        # multi-row boxes (rows 8-voxel aligned: no padded edges; and x0 = 100)
+        for lab, f0, f1 in (("x 0..800", Vec3i_t(0, 100, 100), Vec3i_t(800, 900, 900)),
+                            ("x0=100", Vec3i_t(100, 100, 100), Vec3i_t(900, 900, 900))):
+            report(f"Copy 800^3 sub-box {lab} of 1024^3 {name}",
+                   timed(lambda: lib.vktHipCopyRange(D8, A8, f0, f1, o), R), 2 * bpv * 800 ** 3, 800 ** 3)
+            report(f"SumRange 800^3 sub-box {lab} of 1024^3 {name}",
+                   timed(lambda: lib.vktHipArithmeticRange(0, D8, A8, B8, f0, f1, o), R), 3 * bpv * 800 ** 3, 800 ** 3)
         free(A8, B8, D8)
 
     if args.big:

@@ -277,45 +277,75 @@ namespace hipk
             }
             return;
         }
-        // One collapsed row, a whole quantum, 16-B aligned operands: every load / store
-        // instruction of a wave covers one contiguous KiB, lane l bytes [16l, 16l + 16).  The
-        // generic loop below moves 8 B per lane for UInt8 (8-B loads run below the 16-B rate)
-        // and, for Float32, two 16-B halves of a 32-B item per lane (each instruction every other
-        // 16 B of 2 KiB): 1024^3 Copy UInt8 0.73 and Float32 0.51 of 8 TB/s against 0.82 for
-        // UInt16.  Here UInt8 item pairs (u, u+1) share one 16-B access, and a Float32 item is
-        // the 4-voxel halves at 4l and 256 + 4l of its 64-item block -- items need not be
-        // contiguous on a collapsed row: every operand uses the same voxels, no row edges.
-        if constexpr (MODE == 0 && (BPV == 4 || (BPV == 1 && kUnroll % 2 == 0)))
+        // Contiguous lanes for UInt8 and Float32 (a whole quantum, rows without padded edges,
+        // 16-B aligned rows in every operand): every load / store instruction of a wave covers
+        // one contiguous KiB, lane l bytes [16l, 16l + 16).  The per-item loop below moves 8 B per
+        // lane for UInt8 (8-B loads run below the 16-B rate) and, for Float32, two 16-B halves of
+        // a 32-B item per lane (each instruction every other 16 B of 2 KiB): 1024^3 Copy UInt8
+        // 0.73 and Float32 0.51 of 8 TB/s against 0.82 for UInt16.  Here UInt8 items 2l, 2l + 1
+        // of a 128-item pair of blocks share one 16-B access (one collapsed row), and Float32
+        // lane l takes half 4(l mod 2) of items l/2 and 32 + l/2 of its 64-item block (a half
+        // never leaves its item, so never its row; every operand uses the same voxels, and
+        // without padded edges no item needs a mask).
+        if constexpr (BPV == 4 || (BPV == 1 && kUnroll % 2 == 0))
         {
             uint64_t const lane = threadIdx.x;
-            uint64_t const first = static_cast<uint64_t>(g.vhead) + (beg << 3);   // quantum's first voxel
             auto aligned = [&](Operand const& op) {
-                return ((reinterpret_cast<uintptr_t>(op.data) + (static_cast<uint64_t>(op.base) + first) * BPV) & 15u) == 0;
+                uint64_t const rowStart = reinterpret_cast<uintptr_t>(op.data) +
+                                          static_cast<uint64_t>(op.base + g.vhead) * BPV;
+                if constexpr (MODE == 0)
+                    return ((rowStart + (beg << 3) * BPV) & 15u) == 0;
+                else
+                    return ((rowStart | static_cast<uint64_t>(op.sy) * BPV | static_cast<uint64_t>(op.sz) * BPV) & 15u) == 0;
             };
-            if (end - beg == kQ && aligned(d) && (NS < 1 || aligned(s1)) && (NS < 2 || aligned(s2)))
+            // multi-row boxes: Float32 only (UInt8 pairs measured 4-5 % slower there than the
+            // per-item loop: x 0..768 / whole-x planes of an 800^3 sub-box of 1024^3)
+            bool const shape = MODE == 0 || (BPV == 4 && !g.padded);
+            if (end - beg == kQ && shape && aligned(d) && (NS < 1 || aligned(s1)) && (NS < 2 || aligned(s2)))
             {
                 uint32_t a[kUnroll][8], b[kUnroll][8];
-                // voxel (quantum-relative) of the lane's first 16 B in block u
-                auto at = [&](int u) -> uint64_t {
+                // voxel offsets (d, s1, s2) of the lane's 16-B access number q of block u
+                auto at = [&](int u, int q, uint64_t& od, uint64_t& o1, uint64_t& o2) {
+                    uint64_t item;
+                    uint64_t sub = 0;
                     if constexpr (BPV == 4)
-                        return static_cast<uint64_t>(u) * 512u + 4u * lane;
+                    {
+                        item = beg + static_cast<uint64_t>(u) * 64u + 32u * static_cast<uint64_t>(q) + lane / 2;
+                        sub = 4u * (lane & 1u);
+                    }
                     else
-                        return static_cast<uint64_t>(u / 2) * 1024u + 16u * lane;
+                        item = beg + static_cast<uint64_t>(u / 2) * 128u + 2u * lane;
+                    pointwiseVecItem<NS, BPV, MODE, F>(d, s1, s2, g, item, o1, o2, od);
+                    od += sub;
+                    o1 += sub;
+                    o2 += sub;
                 };
-                auto load = [&](Operand const& op, uint32_t (&c)[kUnroll][8]) {
+                uint64_t od[kUnroll][2], o1[kUnroll][2], o2[kUnroll][2];
+#pragma unroll
+                for (int u = 0; u < kUnroll; ++u)
+                {
+                    if constexpr (BPV == 4)
+                    {
+                        at(u, 0, od[u][0], o1[u][0], o2[u][0]);
+                        at(u, 1, od[u][1], o1[u][1], o2[u][1]);
+                    }
+                    else if (u % 2 == 0)
+                        at(u, 0, od[u][0], o1[u][0], o2[u][0]);
+                }
+                auto load = [&](Operand const& op, uint64_t const (&off)[kUnroll][2], uint32_t (&c)[kUnroll][8]) {
 #pragma unroll
                     for (int u = 0; u < kUnroll; ++u)
                     {
-                        uint8_t const* p = op.data + (static_cast<uint64_t>(op.base) + first + at(u)) * BPV;
                         if constexpr (BPV == 4)
                         {
-                            u32x4 const x = loadVec<u32x4, true>(p), y = loadVec<u32x4, true>(p + 1024);
+                            u32x4 const x = loadVec<u32x4, true>(op.data + off[u][0] * 4u);
+                            u32x4 const y = loadVec<u32x4, true>(op.data + off[u][1] * 4u);
                             c[u][0] = x.x; c[u][1] = x.y; c[u][2] = x.z; c[u][3] = x.w;
                             c[u][4] = y.x; c[u][5] = y.y; c[u][6] = y.z; c[u][7] = y.w;
                         }
                         else if (u % 2 == 0)
                         {
-                            u32x4 const x = loadVec<u32x4, true>(p);
+                            u32x4 const x = loadVec<u32x4, true>(op.data + off[u][0]);
                             uint32_t const w[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
                             for (int i = 0; i < 8; ++i)
@@ -327,9 +357,9 @@ namespace hipk
                     }
                 };
                 if constexpr (NS >= 1)
-                    load(s1, a);
+                    load(s1, o1, a);
                 if constexpr (NS >= 2)
-                    load(s2, b);
+                    load(s2, o2, b);
                 uint32_t o[kUnroll][8];
 #pragma unroll
                 for (int u = 0; u < kUnroll; ++u)
@@ -339,12 +369,12 @@ namespace hipk
 #pragma unroll
                 for (int u = 0; u < kUnroll; ++u)
                 {
-                    uint8_t* p = d.data + (static_cast<uint64_t>(d.base) + first + at(u)) * BPV;
                     if constexpr (BPV == 4)
                     {
-                        __builtin_nontemporal_store(u32x4{o[u][0], o[u][1], o[u][2], o[u][3]}, reinterpret_cast<u32x4*>(p));
+                        __builtin_nontemporal_store(u32x4{o[u][0], o[u][1], o[u][2], o[u][3]},
+                                                    reinterpret_cast<u32x4*>(d.data + od[u][0] * 4u));
                         __builtin_nontemporal_store(u32x4{o[u][4], o[u][5], o[u][6], o[u][7]},
-                                                    reinterpret_cast<u32x4*>(p + 1024));
+                                                    reinterpret_cast<u32x4*>(d.data + od[u][1] * 4u));
                     }
                     else if (u % 2 == 0)
                     {
@@ -356,7 +386,8 @@ namespace hipk
                             w[2 + i] = o[u + 1][4 * i] | o[u + 1][4 * i + 1] << 8 | o[u + 1][4 * i + 2] << 16 |
                                        o[u + 1][4 * i + 3] << 24;
                         }
-                        __builtin_nontemporal_store(u32x4{w[0], w[1], w[2], w[3]}, reinterpret_cast<u32x4*>(p));
+                        __builtin_nontemporal_store(u32x4{w[0], w[1], w[2], w[3]},
+                                                    reinterpret_cast<u32x4*>(d.data + od[u][0]));
                     }
                 }
                 return;
