@@ -309,6 +309,27 @@ def test_aggregates_parity(fmt, mapping):
 
 
 @pytest.mark.gpu
+def test_aggregates_float32_span_ties():
+    """Float32 spans take contiguous 16-B lanes (a lane's voxels are the halves at 4l and
+    256 + 4l of each 64-item block): ties of the minimum and maximum placed in one lane's two
+    halves, across lanes, blocks and steps must still report the first occurrence."""
+    rng = np.random.default_rng(3)
+    vals = rng.uniform(-1.0, 1.0, (40, 64, 96)).astype(np.float32)
+    flat = vals.reshape(-1)
+    for i in (260 * 8 + 300, 259 * 8 + 3, 5000, 5000 + 256, 70001, 200003):   # minima
+        flat[i] = -5.0
+    for i in (4 * 512 + 256 + 7, 4 * 512 + 11, 99999, 123456):                  # maxima
+        flat[i] = 6.0
+    codes = vals.view(np.uint32)
+    box = ((0, 0, 0), (96, 64, 40))
+    got = gpu_aggregates(codes, 7, 0.0, 1.0, *box)
+    ref = ob.aggregates_range(ob.Volume(codes, 7), *box)
+    assert (got.min, tuple(got.argmin), got.max, tuple(got.argmax)) == (ref.min, tuple(ref.argmin), ref.max,
+                                                                        tuple(ref.argmax))
+    assert ref.min == -5.0 and ref.max == 6.0
+
+
+@pytest.mark.gpu
 def test_aggregates_ties_specials_and_whole_volume_mean():
     # duplicate minima / maxima: first occurrence in z, y, x order; NaN never min / max;
     # +-inf: -inf < FLT_MAX and +inf > -FLT_MAX, so both qualify (the reference starts from

@@ -342,6 +342,9 @@ def main():
                 rng_fill(W, n ** 3)   # uniform [0, 1): every voxel lands in a bin
             ms = timed(lambda: lib.vktHipHistogramRange(W, o, last, bins, 256, 0), R)
             report(f"reduce Histogram 1024^3 {name} 256 bins", ms, bpv * n ** 3, n ** 3)
+            aggW = _lib.Aggregates_t()
+            ms = timed(lambda: lib.vktHipAggregatesRange(W, o, last, C.byref(aggW)), R)
+            report(f"reduce Aggregates 1024^3 {name} (2 passes, incl. D2H of the result)", ms, 2 * bpv * n ** 3, n ** 3)
             free(W)
         Vc = alloc((n,) * 3, 5)
         lib.vktHipFillRange(Vc, o, last, C.c_float(0.5))

@@ -616,12 +616,31 @@ namespace hipk
         uint64_t const wave = static_cast<uint64_t>(blockIdx.x) * (BLOCK / 64) + (threadIdx.x >> 6);
         uint64_t const waves = static_cast<uint64_t>(gridDim.x) * (BLOCK / 64);
         uint64_t const steps = h.items / (64 * U);
+        // Float32 spans: lane l's "item" of a 64-item block is the 4-voxel halves at 4l and
+        // 256 + 4l, so each 16-B load instruction of the wave reads one contiguous KiB (a
+        // histogram does not care which lane counts which voxel; two 16-B halves of a 32-B item
+        // per lane had each instruction touch every other 16 B of 2 KiB)
+        bool const halves = CONTIG && BPV == 4 && (reinterpret_cast<uintptr_t>(h.data) & 15u) == 0;
         for (uint64_t st = wave; st < steps; st += waves)
         {
             uint32_t c[U][8];
+            if (halves)
+            {
 #pragma unroll
-            for (int k = 0; k < U; ++k)
-                load8<BPV, true>(h.data, voxelOf(st * (64 * U) + k * 64 + lane), c[k]);
+                for (int k = 0; k < U; ++k)
+                {
+                    uint8_t const* p = h.data + ((st * (64 * U) + k * 64) * 8 + 4 * lane) * 4;
+                    u32x4 const x = loadVec<u32x4, true>(p), y = loadVec<u32x4, true>(p + 1024);
+                    c[k][0] = x.x; c[k][1] = x.y; c[k][2] = x.z; c[k][3] = x.w;
+                    c[k][4] = y.x; c[k][5] = y.y; c[k][6] = y.z; c[k][7] = y.w;
+                }
+            }
+            else
+            {
+#pragma unroll
+                for (int k = 0; k < U; ++k)
+                    load8<BPV, true>(h.data, voxelOf(st * (64 * U) + k * 64 + lane), c[k]);
+            }
 #pragma unroll
             for (int k = 0; k < U; ++k)
                 count8(c[k], itemMask<CONTIG>(h, st * (64 * U) + k * 64 + lane));
@@ -692,8 +711,16 @@ namespace hipk
                        static_cast<uint64_t>(h.px0) + 8ull * xi + static_cast<uint64_t>(j);
             }
         };
-        auto visit8 = [&](uint32_t const (&c)[8], uint64_t item) {
+        // hb (Float32 spans, `halves`): c holds the halves at 4l and 256 + 4l of the 64-item block
+        // starting at item hb -- still in increasing index order per lane, which the first-
+        // occurrence tie-break of argmin / argmax relies on
+        auto visit8 = [&](uint32_t const (&c)[8], uint64_t item, uint64_t hb = ~0ull) {
             uint32_t const m = itemMask<CONTIG>(h, item);
+            auto gIndex = [&](int j) -> uint64_t {
+                if (CONTIG && hb != ~0ull)
+                    return h.giBase + hb * 8 + 4 * lane + (j < 4 ? static_cast<uint64_t>(j) : 252ull + j);
+                return globalIndex(item, j);
+            };
 #pragma unroll
             for (int j = 0; j < 8; ++j)
             {
@@ -704,7 +731,7 @@ namespace hipk
                 {
                     if (v < p.minValue || v > p.maxValue)   // rare after the first voxels
                     {
-                        uint64_t const gi = globalIndex(item, j);
+                        uint64_t const gi = gIndex(j);
                         if (v < p.minValue)
                         {
                             p.minValue = v;
@@ -732,15 +759,33 @@ namespace hipk
         uint64_t const wave = static_cast<uint64_t>(blockIdx.x) * (kBlock / 64) + (threadIdx.x >> 6);
         uint64_t const waves = static_cast<uint64_t>(gridDim.x) * (kBlock / 64);
         uint64_t const steps = h.items / (64 * U);
+        bool const halves = CONTIG && BPV == 4 && (reinterpret_cast<uintptr_t>(h.data) & 15u) == 0;
         for (uint64_t st = wave; st < steps; st += waves)
         {
             uint32_t c[U][8];
+            if (halves)   // contiguous 16-B lanes, as in histogramFastKernel
+            {
 #pragma unroll
-            for (int k = 0; k < U; ++k)
-                load8<BPV, true>(h.data, spanVoxel<CONTIG>(h, st * (64 * U) + k * 64 + lane), c[k]);
+                for (int k = 0; k < U; ++k)
+                {
+                    uint8_t const* p = h.data + ((st * (64 * U) + k * 64) * 8 + 4 * lane) * 4;
+                    u32x4 const x = loadVec<u32x4, true>(p), y = loadVec<u32x4, true>(p + 1024);
+                    c[k][0] = x.x; c[k][1] = x.y; c[k][2] = x.z; c[k][3] = x.w;
+                    c[k][4] = y.x; c[k][5] = y.y; c[k][6] = y.z; c[k][7] = y.w;
+                }
 #pragma unroll
-            for (int k = 0; k < U; ++k)
-                visit8(c[k], st * (64 * U) + k * 64 + lane);
+                for (int k = 0; k < U; ++k)
+                    visit8(c[k], st * (64 * U) + k * 64 + lane, st * (64 * U) + k * 64);
+            }
+            else
+            {
+#pragma unroll
+                for (int k = 0; k < U; ++k)
+                    load8<BPV, true>(h.data, spanVoxel<CONTIG>(h, st * (64 * U) + k * 64 + lane), c[k]);
+#pragma unroll
+                for (int k = 0; k < U; ++k)
+                    visit8(c[k], st * (64 * U) + k * 64 + lane);
+            }
         }
         for (uint64_t it = steps * (64 * U) + wave * 64 + lane; it < h.items; it += waves * 64)
         {
