@@ -760,10 +760,36 @@ namespace hipk
         uint64_t const waves = static_cast<uint64_t>(gridDim.x) * (kBlock / 64);
         uint64_t const steps = h.items / (64 * U);
         bool const halves = CONTIG && BPV == 4 && (reinterpret_cast<uintptr_t>(h.data) & 15u) == 0;
+        // UInt8 spans: lane l takes items 2l, 2l + 1 of each 128-item pair of blocks with one
+        // 16-B load (8-B loads per lane otherwise); still increasing order per lane
+        bool const pairs = CONTIG && BPV == 1 && U % 2 == 0 && (reinterpret_cast<uintptr_t>(h.data) & 15u) == 0;
         for (uint64_t st = wave; st < steps; st += waves)
         {
             uint32_t c[U][8];
-            if (halves)   // contiguous 16-B lanes, as in histogramFastKernel
+            if (pairs)
+            {
+#pragma unroll
+                for (int k = 0; k < U; k += 2)
+                {
+                    uint64_t const item = st * (64 * U) + static_cast<uint64_t>(k) * 64 + 2 * lane;
+                    u32x4 const x = loadVec<u32x4, true>(h.data + item * 8);
+                    uint32_t const w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+                    for (int i = 0; i < 8; ++i)
+                    {
+                        c[k][i] = (w[i / 4] >> (8 * (i % 4))) & 0xFFu;
+                        c[k + 1][i] = (w[2 + i / 4] >> (8 * (i % 4))) & 0xFFu;
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < U; k += 2)
+                {
+                    uint64_t const item = st * (64 * U) + static_cast<uint64_t>(k) * 64 + 2 * lane;
+                    visit8(c[k], item);
+                    visit8(c[k + 1], item + 1);
+                }
+            }
+            else if (halves)   // contiguous 16-B lanes, as in histogramFastKernel
             {
 #pragma unroll
                 for (int k = 0; k < U; ++k)
