@@ -209,6 +209,45 @@ def test_histogram_uint16_unit_mapping_every_code():
             np.testing.assert_array_equal(got, ref, err_msg=f"u8 map={mapping} nbins={nbins}")
 
 
+# (mapping, numBins) whose oracle bins are (code * numBins) >> 16 for every UInt16 code (the
+# library's mul-shift bins) and ones whose float rounding breaks that (they keep the float formula)
+MULSHIFT_CASES = [((0.0, 1.0), 10240), ((0.0, 1.0), 1000), ((0.0, 1.0), 40960), ((0.0, 1.0), 65535),
+                  ((0.0, 2.0), 1000), ((0.0, 0.5), 768), ((-1.0, 3.0), 10240), ((0.25, 7.5), 3000)]
+FLOATBIN_CASES = [((0.0, 1.0), 20000), ((0.0, 1.0), 3000), ((0.0, 2.0), 12000), ((0.25, 7.5), 30000)]
+
+
+def test_histogram_mulshift_premise_against_oracle():
+    """The premise of the UInt16 mul-shift bins, checked with the oracle's restatement of
+    Histogram_serial.hpp: for the listed cases every code's bin is (c * numBins) >> 16, and for the
+    others it is not (so the host check in the library must reject them)."""
+    codes = np.arange(65536, dtype=np.uint16).reshape(16, 16, 256)
+    c = np.arange(65536, dtype=np.uint64)
+    for cases, expect in ((MULSHIFT_CASES, True), (FLOATBIN_CASES, False)):
+        for mapping, nbins in cases:
+            ref, _ = ob.histogram_range(ob.Volume(codes, 5, *mapping), (0, 0, 0), (256, 16, 16), nbins)
+            ms = np.bincount((c * nbins) >> 16, minlength=nbins).astype(ref.dtype)
+            assert np.array_equal(ref, ms) == expect, f"map={mapping} nbins={nbins}"
+
+
+@pytest.mark.gpu
+def test_histogram_uint16_mulshift_bins():
+    """Mul-shift bins (knob histogram.mulshift) vs the float formula and the oracle: every code,
+    both kinds of case, replicated (<= 10 240 bins) and tiled counters, and a strided padded box."""
+    rng = np.random.default_rng(77)
+    every = np.arange(65536, dtype=np.uint16).reshape(16, 16, 256)
+    rand = rng.integers(0, 65536, (24, 40, 520), dtype=np.uint16)
+    for codes, box in ((every, ((0, 0, 0), (256, 16, 16))), (rand, ((3, 1, 2), (517, 39, 23)))):
+        for mapping, nbins in MULSHIFT_CASES + FLOATBIN_CASES:
+            ref, _ = ob.histogram_range(ob.Volume(codes, 5, *mapping), *box, nbins)
+            for k in (1, 0):
+                lib.vktHipSetTuningKnob(b"histogram.mulshift", k)
+                try:
+                    got = gpu_histogram(codes, 5, *mapping, *box, nbins)
+                finally:
+                    lib.vktHipSetTuningKnob(b"histogram.mulshift", -1)
+                np.testing.assert_array_equal(got, ref, err_msg=f"map={mapping} nbins={nbins} knob={k}")
+
+
 @pytest.mark.gpu
 def test_histogram_constant_volume_and_reference_example():
     """Wave-uniform bins (one atomic per wave) and src/examples/Histogram.cpp's 256 bins."""

@@ -368,7 +368,8 @@ namespace hipk
         int32_t dimX, dimY, fx, fy, fz;
         float lo, hi, scale, nbf;
         uint32_t nb, rShift;
-        uint32_t binShift;          // SHIFT (UInt16, unit mapping, nb = 2^k <= 2^16): bin = code >> binShift
+        uint32_t binShift;          // SHIFT: bin = (code * binMul) >> binShift
+        uint32_t binMul;            // 1 for the power-of-two bins; numBins for UInt16 mul-shift bins
         uint32_t tileBase, tileBins;   // TILED: this launch counts bins [tileBase, +tileBins)
         unsigned long long* bins;
         uint64_t giBase;            // aggregates, CONTIG: global linear index of the span start
@@ -431,6 +432,11 @@ namespace hipk
     // exactly (codec::decodeUnit), scale = numBins / 1 = 2^k, and f = c * 2^(k-16) is exact and
     // in [0, numBins), so the reference's (size_t)((v - lo) * scale) is c >> (16 - k).
     // UInt8: taken when the host evaluation of all 256 bins (hostBinU8) is such a shift.
+    // Mul-shift (UInt16, any other bin count <= 2^16): bin = (code * numBins) >> 16 whenever the
+    // host evaluation of the kernel's float formula over all 65 536 codes (hostBinU16) gives
+    // exactly that -- e.g. the unit mapping with numBins = o * 2^j, o <= 256 (c * numBins * 2^-16
+    // is then exact in f32), or mapping [0, 2] with 1000 bins.  One v_mul_u32_u24 and a shift
+    // instead of the decode, the range test and the conversion (10 240 bins: 0.48 -> see DESIGN).
     //
     // P16 (TILED, UInt16 / Float32, more bins than one tile of 32-bit counters -- a UInt16
     // histogram with one bin per code): two 16-bit counters per LDS word, so up to ~80 K bins
@@ -573,7 +579,8 @@ namespace hipk
                 uint32_t b[8];
 #pragma unroll
                 for (int j = 0; j < 8; ++j)
-                    b[j] = (m >> j) & 1u ? c[j] >> h.binShift : h.nb;
+                    // (HIP's __umul24 returns int: codes >= 2^15 times 65 536 bins are negative)
+                    b[j] = (m >> j) & 1u ? static_cast<uint32_t>(__umul24(c[j], h.binMul)) >> h.binShift : h.nb;
                 add8(b);
             }
             else if constexpr (FMT == codec::FmtUInt8)
@@ -947,6 +954,46 @@ namespace hipk
         return (f > -1.0f && f < nbf) ? static_cast<uint64_t>(static_cast<int32_t>(f)) : nb;
     }
 
+    // fastBin of a UInt16 code, evaluated on the host with the kernel's float operations
+    // (histogramFastKernel's UInt16 decode: t = c * 2^-16, lerp as (1 - t) * lo + t * hi)
+    uint64_t hostBinU16(uint32_t c, float lo, float hi, float scale, float nbf, uint64_t nb)
+    {
+        volatile float t = static_cast<float>(c) * (1.0f / 65536.0f);
+        volatile float sm = 1.0f - t;
+        volatile float p = sm * lo;
+        volatile float q = t * hi;
+        volatile float v = p + q;
+        volatile float d = v - lo;
+        volatile float f = d * scale;
+        return (f > -1.0f && f < nbf) ? static_cast<uint64_t>(static_cast<int32_t>(f)) : nb;
+    }
+
+    // True when every UInt16 code's bin is (code * numBins) >> 16 (mul-shift bins).  The
+    // 65 536-code check costs ~0.2 ms on the host, so the last answer is kept per thread.
+    bool mulShiftBinsU16(float lo, float hi, float scale, uint64_t numBins)
+    {
+        if (numBins == 0 || numBins > 65536u)
+            return false;
+        struct Key
+        {
+            uint32_t lo, hi, scale;
+            uint64_t nb;
+            bool operator==(Key const& o) const { return lo == o.lo && hi == o.hi && scale == o.scale && nb == o.nb; }
+        };
+        Key const key{codec::floatToBits(lo), codec::floatToBits(hi), codec::floatToBits(scale), numBins};
+        thread_local Key lastKey{0, 0, 0, 0};
+        thread_local bool lastResult = false;
+        if (key == lastKey)
+            return lastResult;
+        bool ok = true;
+        float const nbf = static_cast<float>(numBins);
+        for (uint32_t c = 0; c < 65536u && ok; ++c)
+            ok = hostBinU16(c, lo, hi, scale, nbf, numBins) == ((static_cast<uint64_t>(c) * numBins) >> 16);
+        lastKey = key;
+        lastResult = ok;
+        return ok;
+    }
+
     // Launches histogramFastKernel when the range qualifies (see its comment); false otherwise.
     bool launchFastHistogram(BoxArgs const& a, HistArgs const& hh, hipStream_t s)
     {
@@ -972,6 +1019,14 @@ namespace hipk
         bool shift = fmt == codec::FmtUInt16 && codec::isUnitMapping(a.lo, a.hi) && (1ull << k) == hh.numBins &&
                      hh.scale == static_cast<float>(hh.numBins);
         h.binShift = 16u - k;
+        h.binMul = 1u;
+        if (fmt == codec::FmtUInt16 && !shift && rt::knob(rt::Knob::HistogramMulShift) != 0 &&
+            mulShiftBinsU16(a.lo, a.hi, hh.scale, hh.numBins))
+        {
+            shift = true;
+            h.binShift = 16u;
+            h.binMul = static_cast<uint32_t>(hh.numBins);
+        }
         if (fmt == codec::FmtUInt8)
         {
             // the kernel's own bin formula for all 256 codes, on the host (volkit_codec.hpp is shared)

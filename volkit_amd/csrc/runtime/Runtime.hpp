@@ -80,6 +80,7 @@ namespace rt
         PointwiseMergeSectors,         // 0: no 64-B sector completion at row ends
         PointwiseGeneral32,            // 0: the general path uses 64-bit addressing everywhere (tests)
         HistogramPacked16,             // 0: histograms beyond one LDS tile take one pass per tile
+        HistogramMulShift,             // 0: UInt16 bins other than code >> s keep the float formula
         Count
     };
     int64_t knob(Knob k);
