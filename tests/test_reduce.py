@@ -369,6 +369,42 @@ def test_aggregates_float32_span_ties():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("fmt", [4, 5])
+def test_aggregates_integer_pass_unit_mapping(fmt):
+    """UInt8 / UInt16 under the unit mapping (the decodeUnit streaming kernels): tied extremes in
+    different lanes, waves and padded end items, a product that never reaches 0, and sums checked
+    against the exact value (also the guard for the integer pass-1 variants of DESIGN §4.8)."""
+    top = 255 if fmt == 4 else 65535
+    dt = np.uint8 if fmt == 4 else np.uint16
+    rng = np.random.default_rng(41 + fmt)
+    cases = [((24, 40, 1040), (0, 0, 0), (1040, 40, 24)),       # one span
+             ((24, 40, 1040), (3, 1, 2), (1037, 39, 23))]        # padded rows
+    for dims, first, last in cases:
+        codes = rng.integers(1, top, dims, dtype=dt)
+        for z, y, x in ((5, 7, 9), (2, 3, 1000), (20, 30, 40)):   # tied minima, first is the answer
+            codes[z, y, x] = 0
+        for z, y, x in ((6, 1, 511), (6, 1, 513), (22, 38, 8)):   # tied maxima
+            codes[z, y, x] = top
+        for mapping in ((0.0, 1.0), (-0.0, 1.0)):                  # (-0, 1) keeps the float pass
+            got = gpu_aggregates(codes, fmt, *mapping, first, last)
+            ref = ob.aggregates_range(ob.Volume(codes, fmt, *mapping), first, last)
+            what = f"fmt={fmt} box={first}->{last} map={mapping}"
+            assert (got.min, got.max) == (ref.min, ref.max), what
+            assert tuple(got.argmin) == tuple(ref.argmin) and tuple(got.argmax) == tuple(ref.argmax), what
+            vals = values_of(codes, fmt, *mapping)[first[2]:last[2], first[1]:last[1], first[0]:last[0]].reshape(-1)
+            exact = float(np.sum(vals, dtype=np.float64))
+            check_float("sum", got.sum, ref.sum, exact, exact, vals.size)
+    # product: all-top volume, (1 - 2^-16)^n stays far from 0; UInt8 top decodes to < 1 as well
+    codes = np.full((4, 8, 64), top, dt)
+    got = gpu_aggregates(codes, fmt, 0.0, 1.0, (0, 0, 0), (64, 8, 4))
+    ref = ob.aggregates_range(ob.Volume(codes, fmt), (0, 0, 0), (64, 8, 4))
+    v = float(values_of(codes[:1, :1, :1], fmt, 0.0, 1.0).reshape(-1)[0])
+    exact_prod = v ** codes.size
+    assert got.prod != 0.0 and abs(got.prod - exact_prod) <= codes.size * EPS * exact_prod, (got.prod, exact_prod)
+    assert abs(got.prod - ref.prod) <= codes.size * EPS * exact_prod
+
+
+@pytest.mark.gpu
 def test_aggregates_ties_specials_and_whole_volume_mean():
     # duplicate minima / maxima: first occurrence in z, y, x order; NaN never min / max;
     # +-inf: -inf < FLT_MAX and +inf > -FLT_MAX, so both qualify (the reference starts from
