@@ -94,6 +94,24 @@ def _worker(rank, port, q):
         dst = vkt.StructuredVolume(2 * gx, 2 * gy, d1 - d0, vkt.DataFormat_Float32)
         err = slab.resample_slab(dst.hip_view(), sview, vkt.FilterMode_Linear, plan)
         assert err == 0, vkt.last_error()
+        # the overlapped form on device planes: exchange issued, interior dst planes resampled
+        # from the owned source planes, then the boundary planes once the halo has landed
+        own = np.zeros((l1 - l0, gy, gx), np.float32)
+        own[z0 - l0:z1 - l0] = vals[z0:z1]
+        src2 = vkt.StructuredVolume(gx, gy, l1 - l0, vkt.DataFormat_Float32)
+        src2.from_numpy(own.view(np.uint32))
+        sv2 = src2.hip_view()
+        dst2 = vkt.StructuredVolume(2 * gx, 2 * gy, d1 - d0, vkt.DataFormat_Float32)
+
+        def dev_planes(g0, g1):
+            return slab.device_tensor(sv2.data + (g0 - l0) * plane, (g1 - g0) * plane)
+
+        dk = slab.interior_split(plan, vkt.FilterMode_Linear, True)
+        err = slab.resample_slab_overlapped(dst2.hip_view(), sv2, vkt.FilterMode_Linear, plan, True, dev_planes)
+        assert err == 0, vkt.last_error()
+        torch.cuda.synchronize()
+        assert np.array_equal(dst2.to_numpy(), dst.to_numpy()), f"rank {rank}: overlapped != single call (dk={dk})"
+        out["split"] = (d0, dk, d1)
         ep.device = vkt.ExecutionPolicy.Device_CPU
         vkt.SetThreadExecutionPolicy(ep)
         q.put((rank, out, (d0, d1, dst.to_numpy()), plan.halo_planes))
@@ -121,6 +139,10 @@ def test_two_ranks_on_one_gpu():
     vals = _global_volume()
     gz, gy, gx = vals.shape
     whole = ob.Volume(vals.view(np.uint32), 7)
+    for r, out, _, halo in res:
+        assert not isinstance(out, str), out
+        d0, dk, d1 = out.pop("split")
+        assert d0 < dk < d1 or not halo, (r, d0, dk, d1)   # a rank with a halo has an interior
     for key in res[0][1]:
         first, last = key
         ref = ob.aggregates_range(whole, first, last)

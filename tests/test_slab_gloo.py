@@ -139,3 +139,30 @@ def test_metric_config_needs_no_halo():
             assert dx * dy * (z1 - z0) == 1024 ** 3
             pf = slab.plan_resample(dz, dz // 2, world, rank, 1, chain=True)
             assert pf.halo_planes == (0 if rank == world - 1 else 2)
+
+
+@pytest.mark.parametrize("world,src,dst,fmt,fm,chain", CASES + [(8, (16, 16, 256), (32, 32, 512), 7, 1, True),
+                                                            (8, (16, 16, 128), (32, 32, 2048), 7, 1, True)])
+def test_interior_split_reads_only_owned_planes(world, src, dst, fmt, fm, chain):
+    """The overlapped slab resample (slab.resample_slab_overlapped) computes dst planes
+    [dst0, dk) while the halo is in flight: they must read owned source planes only, dk must be
+    the largest such plane, and the boundary [dk, dst1) must read planes of the local buffer."""
+    from volkit_amd import slab
+    for rank in range(world):
+        plan = slab.plan_resample(dst[2], src[2], world, rank, fm, chain)
+        d0, d1 = plan.dst
+        dk = slab.interior_split(plan, fm, chain)
+        assert d0 <= dk <= d1
+        if not plan.recvs:
+            assert dk == d1
+            continue
+        o0, o1 = plan.owned_src
+        l0, l1 = plan.local_src
+        if dk > d0:
+            b, e = slab.source_range(dst[2], d0, dk, src[2], fm, chain)
+            assert o0 <= b and e <= o1, (rank, dk, b, e)
+        if dk < d1:
+            b, e = slab.source_range(dst[2], d0, dk + 1, src[2], fm, chain)
+            assert b < o0 or e > o1, (rank, "dk is not maximal")
+            b, e = slab.source_range(dst[2], dk, d1, src[2], fm, chain)
+            assert l0 <= b and e <= l1

@@ -90,14 +90,16 @@ def plan_resample(dst_gdz: int, src_gdz: int, world: int, rank: int, filter_mode
     return plan
 
 
-def exchange_planes(plan: ResamplePlan, planes: Callable[[int, int], "torch.Tensor"], group=None) -> None:
-    """Point-to-point halo exchange: `planes(g0, g1)` returns a writable uint8 tensor view of
-    global source planes [g0, g1) in the local buffer.  One batched isend/irecv round.
+def start_exchange(plan: ResamplePlan, planes: Callable[[int, int], "torch.Tensor"], group=None):
+    """Issue the halo exchange (one batched isend/irecv round) without waiting for it; returns
+    the pending round for finish_exchange.  `planes(g0, g1)` returns a writable uint8 tensor
+    view of global source planes [g0, g1) in the local buffer.
 
-    With the nccl backend (RCCL over xGMI) device planes move device to device: RCCL runs on
-    its own stream after the current stream's work, and the current stream waits for the
-    receives, so a kernel enqueued next reads the halo.  gloo moves host tensors only, so device
-    planes are staged through host copies there (CPU tests, 1-GPU rehearsals)."""
+    With the nccl backend (RCCL over xGMI) device planes move device to device on RCCL's own
+    stream, which starts after the work already queued on the current stream; kernels enqueued
+    on the current stream before finish_exchange run concurrently with the transfer.  gloo
+    moves host tensors only, so device planes are staged through host copies there (CPU tests,
+    1-GPU rehearsals)."""
     import torch.distributed as dist
 
     staged = dist.get_backend(group) == "gloo"
@@ -112,11 +114,82 @@ def exchange_planes(plan: ResamplePlan, planes: Callable[[int, int], "torch.Tens
             landing.append((t, host))
             t = host
         ops.append(dist.P2POp(dist.irecv, t, peer, group))
-    if ops:
-        for req in dist.batch_isend_irecv(ops):
-            req.wait()
+    return (dist.batch_isend_irecv(ops) if ops else [], landing)
+
+
+def finish_exchange(pending) -> None:
+    """Wait for a round from start_exchange: with RCCL the current stream waits for the
+    receives (the host does not block), so a kernel enqueued next reads the halo."""
+    reqs, landing = pending
+    for req in reqs:
+        req.wait()
     for dev, host in landing:
         dev.copy_(host)
+
+
+def exchange_planes(plan: ResamplePlan, planes: Callable[[int, int], "torch.Tensor"], group=None) -> None:
+    """Point-to-point halo exchange, issued and waited for (start_exchange + finish_exchange)."""
+    finish_exchange(start_exchange(plan, planes, group))
+
+
+def interior_split(plan: ResamplePlan, filter_mode: int, chain: bool) -> int:
+    """dk such that dst planes [dst0, dk) read only source planes this rank owns (the interior:
+    computable while the halo is in flight) and [dk, dst1) read the halo.  dst0 when even the
+    first plane needs a received one; dst1 when nothing is received."""
+    d0, d1 = plan.dst
+    o0, o1 = plan.owned_src
+    if d1 <= d0 or not plan.recvs:
+        return d1
+
+    def owned(dk):
+        b, e = source_range(plan.dst_gdz, d0, dk, plan.src_gdz, filter_mode, chain)
+        return b >= o0 and e <= o1
+
+    lo, hi = d0, d1          # owned(lo) holds trivially for the empty range; find the largest
+    while lo < hi:
+        mid = (lo + hi + 1) // 2
+        if owned(mid):
+            lo = mid
+        else:
+            hi = mid - 1
+    return lo
+
+
+_BYTES_PER_VOXEL = {1: 1, 2: 2, 3: 4, 4: 1, 5: 2, 6: 4, 7: 4}   # DataFormat Int8 .. Float32
+
+
+def sub_view(view, g0: int, g1: int, z0: int):
+    """View of global planes [g0, g1) of a slab view whose first plane is global plane z0."""
+    plane = view.dimX * view.dimY * _BYTES_PER_VOXEL[view.dataFormat]
+    v = _lib.HipVolumeView_t.from_buffer_copy(view)
+    v.data = (view.data or 0) + (g0 - z0) * plane
+    v.dimZ = g1 - g0
+    return v
+
+
+def resample_slab_overlapped(dst_view, src_view, filter_mode: int, plan: ResamplePlan, chain: bool,
+                             planes: Callable[[int, int], "torch.Tensor"], group=None) -> int:
+    """Halo exchange overlapped with the interior: issue the exchange, resample the dst planes
+    that read only owned source planes (source sub-view of exactly those planes, so nothing
+    touches the planes in flight), wait for the receives on the stream, then resample the
+    boundary planes from the source planes they read.  Each call is a slab resample of its own
+    (the same exact index tables), so the result equals resample_slab's."""
+    d0, d1 = plan.dst
+    ls0 = plan.local_src[0]
+    if not plan.recvs and not plan.sends:
+        return resample_slab(dst_view, src_view, filter_mode, plan)
+    pending = start_exchange(plan, planes, group)
+    dk = interior_split(plan, filter_mode, chain)
+    err = 0
+    for a, b, wait in ((d0, dk, False), (dk, d1, True)):
+        if wait:
+            finish_exchange(pending)
+        if b <= a or err:
+            continue
+        s0, s1 = source_range(plan.dst_gdz, a, b, plan.src_gdz, filter_mode, chain)
+        err = lib.vktHipResampleSlab(sub_view(dst_view, a, b, d0), sub_view(src_view, s0, s1, ls0), filter_mode,
+                                     plan.dst_gdz, a, plan.src_gdz, s0)
+    return err
 
 
 class DeviceBytes:
