@@ -509,13 +509,20 @@ namespace hipk
         auto add8 = [&](uint32_t const (&b)[8]) {
             if constexpr (TILED)
             {
-                // one check per item: all 8 voxels of every active lane on one bin
-                bool same = true;
-#pragma unroll
-                for (int j = 1; j < 8; ++j)
-                    same = same && b[j] == b[0];
+                // one check per item: all 8 voxels of every active lane on one bin -- first the
+                // wave-wide test of voxel 0 (fails at once on varied data, one compare + ballot),
+                // the other 7 voxels only when it holds
                 uint32_t const t0 = __builtin_amdgcn_readfirstlane(b[0] - h.tileBase);
-                if (__all(same && b[0] - h.tileBase == t0))
+                bool uniform = __all(b[0] - h.tileBase == t0);
+                if (uniform)
+                {
+                    bool same = true;
+#pragma unroll
+                    for (int j = 1; j < 8; ++j)
+                        same = same && b[j] == b[0];
+                    uniform = __all(same);
+                }
+                if (uniform)
                 {
                     if (t0 < h.tileBins)
                     {
