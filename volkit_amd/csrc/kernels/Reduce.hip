@@ -548,6 +548,15 @@ namespace hipk
                 }
                 if constexpr (P16)
                 {
+                    // no returned word with a half >= kP16Flush (2^14: bit 14 or 15 of a half) --
+                    // nearly always on varied data -- skips the 8 per-voxel threshold tests
+                    uint32_t any = 0;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j)
+                        any |= old[j];
+                    static_assert(kP16Flush == 0x4000u, "threshold bits");
+                    if ((any & 0xC000C000u) == 0u)
+                        return;
 #pragma unroll
                     for (int j = 0; j < 8; ++j)
                     {
