@@ -300,17 +300,19 @@ def test_histogram_packed16_counter_wraps(fmt, mapping, nbins, fill):
 @pytest.mark.gpu
 @pytest.mark.parametrize("fmt", [5, 7])
 def test_histogram_packed16_matches_tiled_passes(fmt):
-    """Knob histogram.packed16 = 0: one pass per LDS tile of 32-bit counters, same counts."""
+    """Knob histogram.packed16 = 0: one pass per LDS tile of 32-bit counters, same counts; knob
+    histogram.p16_step = 0: P16 threshold tests after every item instead of every wave-step."""
     rng = np.random.default_rng(fmt)
     codes = rand_codes(rng, fmt, (40, 100, 256), specials=True)
     runs = []
-    for k in (1, 0):
-        lib.vktHipSetTuningKnob(b"histogram.packed16", k)
+    for knob, k in ((b"histogram.packed16", 1), (b"histogram.packed16", 0), (b"histogram.p16_step", 0)):
+        lib.vktHipSetTuningKnob(knob, k)
         try:
             runs.append(gpu_histogram(codes, fmt, 0.0, 1.0, (0, 0, 0), (256, 100, 40), 65536))
         finally:
-            lib.vktHipSetTuningKnob(b"histogram.packed16", -1)
+            lib.vktHipSetTuningKnob(knob, -1)
     np.testing.assert_array_equal(runs[0], runs[1])
+    np.testing.assert_array_equal(runs[0], runs[2])
     ref, _ = ob.histogram_range(ob.Volume(codes, fmt), (0, 0, 0), (256, 100, 40), 65536)
     np.testing.assert_array_equal(runs[0], ref)
 

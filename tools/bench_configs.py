@@ -333,6 +333,12 @@ def main():
                 ms = timed(lambda: lib.vktHipHistogramRange(V, o, last, bins, nb, 0), R)
                 report(f"reduce Histogram 1024^3 UInt16 {nb} bins [mulshift={k}]", ms, 2 * n ** 3, n ** 3)
             lib.vktHipSetTuningKnob(b"histogram.mulshift", -1)
+        # P16 threshold tests once per wave-step vs after every item
+        for k in (1, 0):
+            lib.vktHipSetTuningKnob(b"histogram.p16_step", k)
+            ms = timed(lambda: lib.vktHipHistogramRange(V, o, last, bins, 65536, 0), R)
+            report(f"reduce Histogram 1024^3 UInt16 65536 bins [p16_step={k}]", ms, 2 * n ** 3, n ** 3)
+        lib.vktHipSetTuningKnob(b"histogram.p16_step", -1)
         sub0, sub1 = Vec3i_t(64, 64, 64), Vec3i_t(960, 960, 960)
         ms = timed(lambda: lib.vktHipHistogramRange(V, sub0, sub1, bins, 256, 0), R)
         report("reduce Histogram UInt16 896^3 sub-box of 1024^3, 256 bins", ms, 2 * 896 ** 3, 896 ** 3)

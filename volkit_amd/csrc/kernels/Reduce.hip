@@ -370,6 +370,7 @@ namespace hipk
         uint32_t nb, rShift;
         uint32_t binShift;          // SHIFT: bin = (code * binMul) >> binShift
         uint32_t binMul;            // 1 for the power-of-two bins; numBins for UInt16 mul-shift bins
+        uint32_t p16Step;           // P16: threshold tests once per wave-step (knob histogram.p16_step)
         uint32_t tileBase, tileBins;   // TILED: this launch counts bins [tileBase, +tileBins)
         unsigned long long* bins;
         uint64_t giBase;            // aggregates, CONTIG: global linear index of the span start
@@ -501,83 +502,97 @@ namespace hipk
         // always active) that goes to HBM with one 64-bit atomic when the wave's uniform bin
         // changes and at the end.  64 lanes adding to one LDS word serialise: a constant 1024^3
         // volume took 3.5 ms against 0.33 ms streaming.  Other items add 1 per voxel.
-        // P16: all 8 returning adds are issued before the threshold checks.
         auto flushRun = [&] {
             if (runCount != 0u && lane == 0u)
                 atomicAdd(&h.bins[h.tileBase + runBin], static_cast<unsigned long long>(runCount));
         };
+        // TILED: an item whose 8 voxels are on one bin in every active lane goes to the run
+        // register; true when it was taken.  One check per item -- first the wave-wide test of
+        // voxel 0 (fails at once on varied data, one compare + ballot), the other 7 voxels only
+        // when it holds.
+        auto takeUniform = [&](uint32_t const (&b)[8]) -> bool {
+            uint32_t const t0 = __builtin_amdgcn_readfirstlane(b[0] - h.tileBase);
+            bool uniform = __all(b[0] - h.tileBase == t0);
+            if (uniform)
+            {
+                bool same = true;
+#pragma unroll
+                for (int j = 1; j < 8; ++j)
+                    same = same && b[j] == b[0];
+                uniform = __all(same);
+            }
+            if (uniform && t0 < h.tileBins)
+            {
+                if (t0 != runBin)
+                {
+                    flushRun();
+                    runBin = t0;
+                    runCount = 0u;
+                }
+                runCount += 8u * static_cast<uint32_t>(__popcll(__activemask()));
+            }
+            return uniform;
+        };
+        // P16: the 8 returning adds of an item; returns the OR of the returned words
+        auto p16Adds = [&](uint32_t const (&b)[8], uint32_t (&old)[8]) -> uint32_t {
+            uint32_t any = 0;
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+            {
+                uint32_t const t = b[j] - h.tileBase;
+                old[j] = t < h.tileBins ? atomicAdd(&cnt[t >> 1], 1u << ((t & 1u) << 4)) : 0u;
+                any |= old[j];
+            }
+            return any;
+        };
+        // P16: a lane whose add returned a half >= kP16Flush moves kP16Flush to HBM.  The tests
+        // run only when the OR of the returned words has bit 14 or 15 of either half set (a
+        // superset of "some half >= 2^14", almost never true on varied data).
+        static_assert(kP16Flush == 0x4000u, "threshold bits");
+        constexpr uint32_t kP16Bits = 0xC000C000u;
+        auto p16Moves = [&](uint32_t const (&b)[8], uint32_t const (&old)[8]) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+            {
+                uint32_t const t = b[j] - h.tileBase;
+                uint32_t const sh = (t & 1u) << 4;
+                if (t < h.tileBins && ((old[j] >> sh) & 0xFFFFu) >= kP16Flush)
+                {
+                    // move kP16Flush to HBM if the half still holds that much: a CAS, so
+                    // racing movers never take more than is there
+                    uint32_t cur = atomicAdd(&cnt[t >> 1], 0u);
+                    while (((cur >> sh) & 0xFFFFu) >= kP16Flush)
+                    {
+                        uint32_t const prev = atomicCAS(&cnt[t >> 1], cur, cur - (kP16Flush << sh));
+                        if (prev == cur)
+                        {
+                            atomicAdd(&h.bins[h.tileBase + t], static_cast<unsigned long long>(kP16Flush));
+                            break;
+                        }
+                        cur = prev;
+                    }
+                }
+            }
+        };
         auto add8 = [&](uint32_t const (&b)[8]) {
             if constexpr (TILED)
             {
-                // one check per item: all 8 voxels of every active lane on one bin -- first the
-                // wave-wide test of voxel 0 (fails at once on varied data, one compare + ballot),
-                // the other 7 voxels only when it holds
-                uint32_t const t0 = __builtin_amdgcn_readfirstlane(b[0] - h.tileBase);
-                bool uniform = __all(b[0] - h.tileBase == t0);
-                if (uniform)
-                {
-                    bool same = true;
-#pragma unroll
-                    for (int j = 1; j < 8; ++j)
-                        same = same && b[j] == b[0];
-                    uniform = __all(same);
-                }
-                if (uniform)
-                {
-                    if (t0 < h.tileBins)
-                    {
-                        if (t0 != runBin)
-                        {
-                            flushRun();
-                            runBin = t0;
-                            runCount = 0u;
-                        }
-                        runCount += 8u * static_cast<uint32_t>(__popcll(__activemask()));
-                    }
+                if (takeUniform(b))
                     return;
-                }
-                uint32_t old[8];
-#pragma unroll
-                for (int j = 0; j < 8; ++j)
-                {
-                    uint32_t const t = b[j] - h.tileBase;
-                    if constexpr (P16)
-                        old[j] = t < h.tileBins ? atomicAdd(&cnt[t >> 1], 1u << ((t & 1u) << 4)) : 0u;
-                    else if (t < h.tileBins)
-                        atomicAdd(&cnt[t], 1u);
-                }
                 if constexpr (P16)
                 {
-                    // no returned word with a half >= kP16Flush (2^14: bit 14 or 15 of a half) --
-                    // nearly always on varied data -- skips the 8 per-voxel threshold tests
-                    uint32_t any = 0;
-#pragma unroll
-                    for (int j = 0; j < 8; ++j)
-                        any |= old[j];
-                    static_assert(kP16Flush == 0x4000u, "threshold bits");
-                    if ((any & 0xC000C000u) == 0u)
-                        return;
+                    uint32_t old[8];
+                    if (p16Adds(b, old) & kP16Bits)
+                        p16Moves(b, old);
+                }
+                else
+                {
 #pragma unroll
                     for (int j = 0; j < 8; ++j)
                     {
                         uint32_t const t = b[j] - h.tileBase;
-                        uint32_t const sh = (t & 1u) << 4;
-                        if (t < h.tileBins && ((old[j] >> sh) & 0xFFFFu) >= kP16Flush)
-                        {
-                            // move kP16Flush to HBM if the half still holds that much: a CAS, so
-                            // racing movers never take more than is there
-                            uint32_t cur = atomicAdd(&cnt[t >> 1], 0u);
-                            while (((cur >> sh) & 0xFFFFu) >= kP16Flush)
-                            {
-                                uint32_t const prev = atomicCAS(&cnt[t >> 1], cur, cur - (kP16Flush << sh));
-                                if (prev == cur)
-                                {
-                                    atomicAdd(&h.bins[h.tileBase + t], static_cast<unsigned long long>(kP16Flush));
-                                    break;
-                                }
-                                cur = prev;
-                            }
-                        }
+                        if (t < h.tileBins)
+                            atomicAdd(&cnt[t], 1u);
                     }
                 }
             }
@@ -588,30 +603,18 @@ namespace hipk
                     add(b[j]);
             }
         };
-        // m: valid voxels of the item (padded rows); the others go to the trash row / no tile
-        auto count8 = [&](uint32_t const (&c)[8], uint32_t m) {
+        // m: valid voxels of the item (padded rows); the others go to the trash row / no tile.
+        // bins8: the 8 bins of an item (UInt16 / Float32; UInt8 counts through its LDS table)
+        auto bins8 = [&](uint32_t const (&c)[8], uint32_t m, uint32_t (&b)[8]) {
             if constexpr (SHIFT)
             {
-                uint32_t b[8];
 #pragma unroll
                 for (int j = 0; j < 8; ++j)
                     // (HIP's __umul24 returns int: codes >= 2^15 times 65 536 bins are negative)
                     b[j] = (m >> j) & 1u ? static_cast<uint32_t>(__umul24(c[j], h.binMul)) >> h.binShift : h.nb;
-                add8(b);
-            }
-            else if constexpr (FMT == codec::FmtUInt8)
-            {
-#pragma unroll
-                for (int j = 0; j < 8; ++j)
-                {
-                    uint32_t const o = (m >> j) & 1u ? lut[c[j]] : (TILED ? kOff : h.nb << rowShift);
-                    if (!TILED || o != kOff)
-                        atomicAdd(reinterpret_cast<uint32_t*>(cLane + o), 1u);
-                }
             }
             else
             {
-                uint32_t b[8];
 #pragma unroll
                 for (int j = 0; j < 8; j += 2)
                 {
@@ -632,7 +635,46 @@ namespace hipk
                     b[j] = (m >> j) & 1u ? fastBin(f.x, h.nbf, h.nb) : h.nb;
                     b[j + 1] = (m >> (j + 1)) & 1u ? fastBin(f.y, h.nbf, h.nb) : h.nb;
                 }
+            }
+        };
+        auto count8 = [&](uint32_t const (&c)[8], uint32_t m) {
+            if constexpr (FMT == codec::FmtUInt8 && !SHIFT)
+            {
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                {
+                    uint32_t const o = (m >> j) & 1u ? lut[c[j]] : (TILED ? kOff : h.nb << rowShift);
+                    if (!TILED || o != kOff)
+                        atomicAdd(reinterpret_cast<uint32_t*>(cLane + o), 1u);
+                }
+            }
+            else
+            {
+                uint32_t b[8];
+                bins8(c, m, b);
                 add8(b);
+            }
+        };
+        // P16, one wave-step of U items: every item's returning adds are in flight before the
+        // (rare) threshold tests, which wait for the returns only once per step
+        auto countStepP16 = [&](uint32_t const (&c)[U][8], uint64_t item0) {
+            uint32_t b[U][8], old[U][8];
+            bool uni[U];
+            uint32_t any = 0;
+#pragma unroll
+            for (int k = 0; k < U; ++k)
+            {
+                bins8(c[k], itemMask<CONTIG>(h, item0 + k * 64), b[k]);
+                uni[k] = takeUniform(b[k]);
+                if (!uni[k])
+                    any |= p16Adds(b[k], old[k]);
+            }
+            if (any & kP16Bits)
+            {
+#pragma unroll
+                for (int k = 0; k < U; ++k)
+                    if (!uni[k])
+                        p16Moves(b[k], old[k]);
             }
         };
 
@@ -664,9 +706,14 @@ namespace hipk
                 for (int k = 0; k < U; ++k)
                     load8<BPV, true>(h.data, voxelOf(st * (64 * U) + k * 64 + lane), c[k]);
             }
+            if (P16 && h.p16Step)
+                countStepP16(c, st * (64 * U) + lane);
+            else
+            {
 #pragma unroll
-            for (int k = 0; k < U; ++k)
-                count8(c[k], itemMask<CONTIG>(h, st * (64 * U) + k * 64 + lane));
+                for (int k = 0; k < U; ++k)
+                    count8(c[k], itemMask<CONTIG>(h, st * (64 * U) + k * 64 + lane));
+            }
         }
         for (uint64_t it = steps * (64 * U) + wave * 64 + lane; it < h.items; it += waves * 64)
         {
@@ -1036,6 +1083,7 @@ namespace hipk
                      hh.scale == static_cast<float>(hh.numBins);
         h.binShift = 16u - k;
         h.binMul = 1u;
+        h.p16Step = rt::knob(rt::Knob::HistogramP16Step) != 0 ? 1u : 0u;
         if (fmt == codec::FmtUInt16 && !shift && rt::knob(rt::Knob::HistogramMulShift) != 0 &&
             mulShiftBinsU16(a.lo, a.hi, hh.scale, hh.numBins))
         {

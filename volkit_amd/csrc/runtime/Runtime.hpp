@@ -81,6 +81,7 @@ namespace rt
         PointwiseGeneral32,            // 0: the general path uses 64-bit addressing everywhere (tests)
         HistogramPacked16,             // 0: histograms beyond one LDS tile take one pass per tile
         HistogramMulShift,             // 0: UInt16 bins other than code >> s keep the float formula
+        HistogramP16Step,              // 0: P16 threshold tests after each item, not each wave-step
         Count
     };
     int64_t knob(Knob k);
