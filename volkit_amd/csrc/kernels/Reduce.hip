@@ -791,6 +791,25 @@ namespace hipk
                     return h.giBase + hb * 8 + 4 * lane + (j < 4 ? static_cast<uint64_t>(j) : 252ull + j);
                 return globalIndex(item, j);
             };
+            // pass 1 over spans: one test per item (its min / max against the lane's) instead of
+            // one branch per voxel; the voxel-by-voxel strict updates run in order only when it
+            // holds.  1024^3 UInt8 pass 1 272 -> 248 us; padded rows (non-CONTIG) lost 300 ->
+            // 350 us with it (UInt16) and keep the per-voxel test.
+            bool update = true;
+            if constexpr (PASS == 1 && CONTIG)
+            {
+                float lo = FLT_MAX, hi = -FLT_MAX;
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                {
+                    float const v = (m >> j) & 1u ? (UNIT ? codec::decodeUnit(c[j], FMT)
+                                                          : codec::decode(c[j], FMT, h.lo, h.hi))
+                                                  : p.minValue;
+                    lo = fminf(lo, v);   // (NaN never qualifies: minNum / maxNum skip it)
+                    hi = fmaxf(hi, v);
+                }
+                update = lo < p.minValue || hi > p.maxValue;
+            }
 #pragma unroll
             for (int j = 0; j < 8; ++j)
             {
@@ -799,7 +818,7 @@ namespace hipk
                 float const v = UNIT ? codec::decodeUnit(c[j], FMT) : codec::decode(c[j], FMT, h.lo, h.hi);
                 if constexpr (PASS == 1)
                 {
-                    if (v < p.minValue || v > p.maxValue)   // rare after the first voxels
+                    if (update && (v < p.minValue || v > p.maxValue))   // rare after the first voxels
                     {
                         uint64_t const gi = gIndex(j);
                         if (v < p.minValue)
