@@ -170,6 +170,24 @@ def main():
                timed(lambda: lib.vktHipArithmeticRange(5, D, A, B, Vec3i_t(100, 100, 100), Vec3i_t(900, 900, 900), o),
                      R), 6 * 800 ** 3, 800 ** 3)
         free(A, B, D)
+    if want("u8sub") or want("f32sub"):
+        # multi-row sub-boxes of 1024^3: one launch per case, for PMC passes
+        m = 1024
+        for fmt, bpv, name, grp in ((4, 1, "UInt8", "u8sub"), (7, 4, "Float32", "f32sub")):
+            if not want(grp):
+                continue
+            A, B, D = alloc((m,) * 3, fmt, seed=1), alloc((m,) * 3, fmt, seed=2), alloc((m,) * 3, fmt)
+            for lab, f0, f1 in (("x0=100", Vec3i_t(100, 100, 100), Vec3i_t(900, 900, 900)),
+                                ("x 0..800", Vec3i_t(0, 100, 100), Vec3i_t(800, 900, 900)),
+                                ("x 0..1024 (planes)", Vec3i_t(0, 100, 100), Vec3i_t(1024, 900, 900))):
+                nv = (f1.x - f0.x) * (f1.y - f0.y) * (f1.z - f0.z)
+                report(f"{grp} CopyRange {lab} same offset {name}",
+                       timed(lambda: lib.vktHipCopyRange(D, A, f0, f1, f0), R), 2 * bpv * nv, nv)
+                report(f"{grp} CopyRange {lab} -> dst 0 {name}",
+                       timed(lambda: lib.vktHipCopyRange(D, A, f0, f1, o), R), 2 * bpv * nv, nv)
+                report(f"{grp} SumRange {lab} {name}",
+                       timed(lambda: lib.vktHipArithmeticRange(0, D, A, B, f0, f1, o), R), 3 * bpv * nv, nv)
+            free(A, B, D)
     if want("weakspots"):
         # the kernels furthest below the roofline in round 1 (VERDICT r1 "What's weak" 5)
         m = 1024
