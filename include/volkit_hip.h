@@ -73,10 +73,21 @@ VKTAPI vktError vktHipKernelScopeEnd(vktHipKernelScope scope);
  * aligned vector path cannot take to the per-voxel kernel), "pointwise.merge_sectors" (1; 0 stops
  * the general path from completing the 64-B sectors at the row ends of a box by rewriting the
  * destination's own bytes around it), "pointwise.general_32bit" (1; 0 makes the general path use
- * its 64-bit addressing, otherwise taken only for operands of 4 GiB and more), "histogram.packed16"
- * (1; 0 makes histograms with more bins than one LDS tile of 32-bit counters take one pass per
- * tile instead of one pass over packed 16-bit counters).  For tests and
- * in-process A/B measurements; unknown names return vktInvalidValue. */
+ * its 64-bit addressing, otherwise taken only for operands of 4 GiB and more), "pointwise.u8_pairs"
+ * (1; 0 keeps UInt8 multi-row boxes on the 8-voxel per-item loop instead of 16-B accesses on a
+ * 16-voxel row grid), "histogram.packed16" (1; 0 makes histograms with more bins than one LDS
+ * tile of 32-bit counters take one pass per tile instead of one pass over packed 16-bit
+ * counters), "histogram.mulshift" (1; 0 makes UInt16 histograms whose bins are (code * numBins)
+ * >> 16 keep the float bin formula), "histogram.p16_step" (1; 0 runs the packed-16 counters'
+ * threshold tests after every item instead of once per wave-step).  For tests and in-process
+ * A/B measurements; unknown names return vktInvalidValue.
+ *
+ * Writes outside a range box: FillRange / CopyRange / convert and device-functor TransformRange
+ * may rewrite, with the destination's own unchanged bytes, up to one 64-B sector around each row
+ * of the box (64-B sector completion; off with "pointwise.merge_sectors" = 0 for
+ * the pointwise ops).  Every call runs on the one compute stream, so the library's own calls
+ * never race; a caller that writes bytes within 64 B of a box row from another stream or the
+ * host while such a call runs must order the two itself. */
 VKTAPI vktError vktHipSetTuningKnob(const char* name, int64_t value);
 /* Record `message` as the calling thread's last error, log it; returns vktInvalidValue. */
 VKTAPI vktError vktHipReportError(const char* message);
@@ -167,6 +178,87 @@ VKTAPI vktError vktHipCommDestroy(vktHipComm_t comm);
 VKTAPI vktError vktHipSlabExchangeHalo(vktHipComm_t comm, vktHipVolumeView_t localSrc, int32_t localZ0,
                                        int32_t dstGlobalDimZ, int32_t srcGlobalDimZ, vktFilterMode fm,
                                        int32_t needsNeighbours);
+/* The same exchange for a partition whose `numSlabs` slabs all live in this process on the
+ * library's device (slab r = rank r of numSlabs; localSrc[r] holds global source planes
+ * [localZ0[r], localZ0[r] + localSrc[r].dimZ)): every receive of the plan is a device-to-device
+ * hipMemcpyAsync from the owning slab's buffer on the compute stream. */
+VKTAPI vktError vktHipSlabExchangeHaloLocal(int32_t numSlabs, vktHipVolumeView_t const* localSrc,
+                                            int32_t const* localZ0, int32_t dstGlobalDimZ, int32_t srcGlobalDimZ,
+                                            vktFilterMode fm, int32_t needsNeighbours);
+
+/* ---- Range calls over Z-slab partitioned volumes (no reference counterpart)
+ * A volume of global depth globalDimZ is split over nranks ranks by the ceil partition: rank r
+ * OWNS global planes [r*ceil(D/n), min((r+1)*ceil(D/n), D)).  A slab is one rank's part: `view`
+ * (X/Y dims global) holds global planes [z0, z0 + view.dimZ), which must include the owned ones
+ * (it may hold halo planes too).  first / last / dstOffset are GLOBAL coordinates with the
+ * reference's semantics (FillRange: dst[x] for x in [first, last); CopyRange:
+ * dst[x - first + dstOffset] = src[clamp(x)], Copy_serial.hpp:38-47; arithmetic:
+ * dst[x + dstOffset] = f(s1[x], s2[x]) at absolute x, Arithmetic_serial.hpp:25-41).  Each rank
+ * writes only the dst planes it owns.  The source planes its dst planes read that other ranks
+ * own -- the planes a dstOffset.z (or a clamped halo) moves across slab boundaries -- are sent
+ * by their owners into a gather buffer; then the rank runs the local op piece by piece.  Global
+ * arguments (ranges, depths) are checked before anything moves, identically on every rank. */
+typedef struct vktHipSlab
+{
+    vktHipVolumeView_t view;
+    int32_t z0;           /* global plane of view plane 0 */
+    int32_t globalDimZ;   /* depth of the whole volume */
+} vktHipSlab_t;
+
+/* One local piece of a rank's part of a Range call: loop planes [zBegin, zEnd) of the
+ * reference's z loop (global), writing global dst planes from dstZ on; per source k, the global
+ * source planes [srcZ[k], srcZ[k] + srcPlanes[k]) it reads (after the CopyRange clamp) and where
+ * from: bufPlane[k] = -1 the own slab, else that plane of the rank's gather buffer for source k. */
+typedef struct vktHipSlabPiece
+{
+    int32_t zBegin, zEnd;
+    int32_t dstZ;
+    int32_t srcZ[2];
+    int32_t srcPlanes[2];
+    int32_t bufPlane[2];
+} vktHipSlabPiece_t;
+/* One move of source planes between two ranks: global planes [z0, z1) of source `source`
+ * (0: src / source1, 1: source2) go from their owner to the receiver's gather buffer at plane
+ * bufPlane.  send = 1: this rank is the owner (peer receives); 0: this rank receives. */
+typedef struct vktHipSlabMove
+{
+    int32_t peer;
+    int32_t send;
+    int32_t source;
+    int32_t z0, z1;
+    int32_t bufPlane;
+} vktHipSlabMove_t;
+typedef enum { vktHipSlabFill = 0, vktHipSlabCopy = 1, vktHipSlabArithmetic = 2 } vktHipSlabOpKind;
+/* The plan of rank `rank` (pieces in z order; moves in the global order every rank issues them,
+ * so two ranks' moves pair up in order); bufPlanes[k] = planes of its gather buffer for source
+ * k.  src2GlobalDimZ is ignored unless kind is vktHipSlabArithmetic; source globals unused for
+ * Fill.  Arrays may be NULL to query the counts; capacities must cover them otherwise. */
+VKTAPI vktError vktHipSlabRangePlan(vktHipSlabOpKind kind, int32_t nranks, int32_t rank, int32_t dstGlobalDimZ,
+                                    int32_t src1GlobalDimZ, int32_t src2GlobalDimZ, vktVec3i_t first,
+                                    vktVec3i_t last, vktVec3i_t dstOffset, vktHipSlabPiece_t* pieces,
+                                    int32_t pieceCapacity, int32_t* numPieces, vktHipSlabMove_t* moves,
+                                    int32_t moveCapacity, int32_t* numMoves, int32_t* bufPlanes);
+/* The Range calls.  comm != NULL: one slab per process (numSlabs = 1, this rank's slab; rank
+ * and world from the communicator), moves over RCCL in one group on the compute stream.
+ * comm == NULL: the process holds every slab on the library's device (numSlabs ranks; slab i
+ * is rank i), moves are device copies on the compute stream.  Returns once enqueued. */
+VKTAPI vktError vktHipSlabFillRange(vktHipComm_t comm, int32_t numSlabs, vktHipSlab_t const* dst,
+                                    vktVec3i_t first, vktVec3i_t last, float value);
+VKTAPI vktError vktHipSlabCopyRange(vktHipComm_t comm, int32_t numSlabs, vktHipSlab_t const* dst,
+                                    vktHipSlab_t const* src, vktVec3i_t first, vktVec3i_t last,
+                                    vktVec3i_t dstOffset);
+VKTAPI vktError vktHipSlabArithmeticRange(vktHipComm_t comm, vktHipArithmeticOp op, int32_t numSlabs,
+                                          vktHipSlab_t const* dest, vktHipSlab_t const* source1,
+                                          vktHipSlab_t const* source2, vktVec3i_t first, vktVec3i_t last,
+                                          vktVec3i_t dstOffset);
+/* The local half of a Range call whose moves the CALLER carried out (volkit_amd/slab.py moves
+ * them over torch.distributed): runs rank `rank`'s pieces, reading remote source planes from
+ * gather1 / gather2 (device buffers holding bufPlanes[0] / bufPlanes[1] planes of source 1 / 2
+ * in plan order; NULL when the plan reads none).  op is ignored unless kind is arithmetic. */
+VKTAPI vktError vktHipSlabRangePieces(vktHipSlabOpKind kind, vktHipArithmeticOp op, int32_t nranks, int32_t rank,
+                                      vktHipSlab_t dst, vktHipSlab_t const* source1, vktHipSlab_t const* source2,
+                                      vktVec3i_t first, vktVec3i_t last, vktVec3i_t dstOffset, float value,
+                                      void* gather1, void* gather2);
 
 /* replaces TransformRange_cuda (reference src/vkt/Transform_cuda.hpp:12-30, an empty
  * stub there): host callbacks cannot run on the GPU, so the range is staged to host,

@@ -188,6 +188,31 @@ def main():
                 report(f"{grp} SumRange {lab} {name}",
                        timed(lambda: lib.vktHipArithmeticRange(0, D, A, B, f0, f1, o), R), 3 * bpv * nv, nv)
             free(A, B, D)
+    if want("u8ab"):
+        # in-process A/B of the UInt8 16-voxel pair grid (knob pointwise.u8_pairs: 0 off, 1
+        # default rule, 2 forced), alternating on the same allocations
+        m = 1024
+        A, B, D = alloc((m,) * 3, 4, seed=1), alloc((m,) * 3, 4, seed=2), alloc((m,) * 3, 4)
+        ab = {}
+        boxes = (("x0=100", Vec3i_t(100, 100, 100), Vec3i_t(900, 900, 900)),
+                 ("x 0..800", Vec3i_t(0, 100, 100), Vec3i_t(800, 900, 900)),
+                 ("x 0..1024 (planes)", Vec3i_t(0, 100, 100), Vec3i_t(1024, 900, 900)))
+        for rnd in range(3):
+            for kv in (0, 1, 2):
+                lib.vktHipSetTuningKnob(b"pointwise.u8_pairs", kv)
+                for lab, f0, f1 in boxes:
+                    ab.setdefault(("CopyRange", lab, kv), []).append(
+                        timed(lambda: lib.vktHipCopyRange(D, A, f0, f1, f0), R))
+                    ab.setdefault(("SumRange", lab, kv), []).append(
+                        timed(lambda: lib.vktHipArithmeticRange(0, D, A, B, f0, f1, o), R))
+        lib.vktHipSetTuningKnob(b"pointwise.u8_pairs", -1)
+        for (op, lab, kv), ts in sorted(ab.items()):
+            ts.sort()
+            f0, f1 = [(b[1], b[2]) for b in boxes if b[0] == lab][0]
+            nv = (f1.x - f0.x) * (f1.y - f0.y) * (f1.z - f0.z)
+            report(f"u8ab {op} {lab} UInt8 u8_pairs={kv} (median of 3 rounds, spread {ts[0]:.4f}-{ts[-1]:.4f})",
+                   ts[1], (2 if op == "CopyRange" else 3) * nv, nv)
+        free(A, B, D)
     if want("weakspots"):
         # the kernels furthest below the roofline in round 1 (VERDICT r1 "What's weak" 5)
         m = 1024

@@ -71,6 +71,19 @@ class HipSlabTransfer_t(C.Structure):
     _fields_ = [("peer", i32), ("z0", i32), ("z1", i32), ("send", i32)]
 
 
+class HipSlab_t(C.Structure):
+    _fields_ = [("view", HipVolumeView_t), ("z0", i32), ("globalDimZ", i32)]
+
+
+class HipSlabPiece_t(C.Structure):
+    _fields_ = [("zBegin", i32), ("zEnd", i32), ("dstZ", i32), ("srcZ", i32 * 2), ("srcPlanes", i32 * 2),
+                ("bufPlane", i32 * 2)]
+
+
+class HipSlabMove_t(C.Structure):
+    _fields_ = [("peer", i32), ("send", i32), ("source", i32), ("z0", i32), ("z1", i32), ("bufPlane", i32)]
+
+
 class HipCommId_t(C.Structure):
     _fields_ = [("internal", C.c_char * 128)]
 
@@ -220,6 +233,15 @@ SIGNATURES = {
     "vktHipCommInitRank": (c_err, [P(c_comm), i32, HipCommId_t, i32]),
     "vktHipCommDestroy": (c_err, [c_comm]),
     "vktHipSlabExchangeHalo": (c_err, [c_comm, HipVolumeView_t, i32, i32, i32, C.c_int, i32]),
+    "vktHipSlabExchangeHaloLocal": (c_err, [i32, P(HipVolumeView_t), P(i32), i32, i32, C.c_int, i32]),
+    "vktHipSlabRangePlan": (c_err, [C.c_int, i32, i32, i32, i32, i32, Vec3i_t, Vec3i_t, Vec3i_t, P(HipSlabPiece_t),
+                                    i32, P(i32), P(HipSlabMove_t), i32, P(i32), P(i32)]),
+    "vktHipSlabFillRange": (c_err, [c_comm, i32, P(HipSlab_t), Vec3i_t, Vec3i_t, f32]),
+    "vktHipSlabCopyRange": (c_err, [c_comm, i32, P(HipSlab_t), P(HipSlab_t), Vec3i_t, Vec3i_t, Vec3i_t]),
+    "vktHipSlabArithmeticRange": (c_err, [c_comm, C.c_int, i32, P(HipSlab_t), P(HipSlab_t), P(HipSlab_t), Vec3i_t,
+                                          Vec3i_t, Vec3i_t]),
+    "vktHipSlabRangePieces": (c_err, [C.c_int, C.c_int, i32, i32, HipSlab_t, P(HipSlab_t), P(HipSlab_t), Vec3i_t,
+                                      Vec3i_t, Vec3i_t, f32, C.c_void_p, C.c_void_p]),
     "vktHipTransformRange1": (c_err, [HipVolumeView_t, Vec3i_t, Vec3i_t, UnaryOp]),
     "vktHipTransformRange2": (c_err, [HipVolumeView_t, HipVolumeView_t, Vec3i_t, Vec3i_t, Vec3i_t, BinaryOp]),
     "vktHipSynthesize": (c_err, [HipVolumeView_t, u64]),

@@ -235,6 +235,60 @@ namespace hipk
         __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(base + voxel * BPV));
     }
 
+    // Bytes [lo, hi) (0 <= lo < hi <= 16) of the 16-B vector v to the 16-B aligned address p,
+    // as naturally aligned 1/2/4/8-B pieces (at most 4 leading pieces that align the start, then
+    // at most 4 trailing ones): no byte outside the range is written.  A row end of a UInt8 box
+    // costs 1-3 stores instead of one byte store per voxel; the byte extraction is shifts of
+    // the two 64-bit halves (no dynamically indexed register array).
+    __device__ __forceinline__ void storeByteRange16(uint8_t* p, u32x4 v, int lo, int hi)
+    {
+        uint64_t const q0 = static_cast<uint64_t>(v.x) | static_cast<uint64_t>(v.y) << 32;
+        uint64_t const q1 = static_cast<uint64_t>(v.z) | static_cast<uint64_t>(v.w) << 32;
+        auto at = [&](int a) -> uint64_t {   // the (up to) 8 bytes starting at byte a
+            uint64_t const l = (a & 8) ? q1 : q0, h = (a & 8) ? 0ull : q1;
+            uint32_t const s = static_cast<uint32_t>(a & 7) * 8u;
+            return s ? (l >> s) | (h << (64u - s)) : l;
+        };
+        int a = lo;
+        if ((a & 1) && a < hi)
+        {
+            __builtin_nontemporal_store(static_cast<uint8_t>(at(a)), p + a);
+            a += 1;
+        }
+        if ((a & 2) && a + 2 <= hi)
+        {
+            __builtin_nontemporal_store(static_cast<uint16_t>(at(a)), reinterpret_cast<uint16_t*>(p + a));
+            a += 2;
+        }
+        if ((a & 4) && a + 4 <= hi)
+        {
+            __builtin_nontemporal_store(static_cast<uint32_t>(at(a)), reinterpret_cast<uint32_t*>(p + a));
+            a += 4;
+        }
+        if ((a & 8) && a + 8 <= hi)
+        {
+            __builtin_nontemporal_store(at(a), reinterpret_cast<uint64_t*>(p + a));
+            a += 8;
+        }
+        if (hi - a >= 8)
+        {
+            __builtin_nontemporal_store(at(a), reinterpret_cast<uint64_t*>(p + a));
+            a += 8;
+        }
+        if (hi - a >= 4)
+        {
+            __builtin_nontemporal_store(static_cast<uint32_t>(at(a)), reinterpret_cast<uint32_t*>(p + a));
+            a += 4;
+        }
+        if (hi - a >= 2)
+        {
+            __builtin_nontemporal_store(static_cast<uint16_t>(at(a)), reinterpret_cast<uint16_t*>(p + a));
+            a += 2;
+        }
+        if (hi - a >= 1)
+            __builtin_nontemporal_store(static_cast<uint8_t>(at(a)), p + a);
+    }
+
     // XCD-aware block order (guide §5.5 T1): hardware deals workgroups round-robin over the
     // 8 XCDs, so block b and b+8 share an L2.  Remap so each XCD walks one contiguous band of
     // logical blocks -- neighbouring rows then hit the same L2.  Speed only, never correctness.

@@ -168,6 +168,39 @@ namespace hipk
         // 1024^3 Float32 Copy x 0..800 0.853 -> 0.753 ms with the flag off (u8_f32 probe, r02).
         if (p.g.padded && !p.g.merge && phase == 0 && vnx % 8 == 0)
             p.g.padded = 0;
+        // UInt8 rows on a 16-voxel grid (pair16, Pointwise.hpp): one 16-B access per lane for
+        // two items instead of one 8-B access per item, byte-range stores at the row ends.
+        // Needs every operand's rows at one phase mod 16 and 16-B aligned row supersets (the
+        // superset stays inside the volume's row: pitches are multiples of 16).
+        p.g.pair16 = 0;
+        if (vec && bpv == 1 && vny * vnz > 1 && rt::knob(rt::Knob::PointwisePaddedRows) != 0 &&
+            rt::knob(rt::Knob::PointwiseU8Pairs) != 0)
+        {
+            int64_t const ph16 = ops[0]->base & 15;
+            bool ok = true;
+            for (int i = 0; i < nops && ok; ++i)
+            {
+                Operand const& o = *ops[i];
+                ok = (o.base & 15) == ph16 && reinterpret_cast<uintptr_t>(o.data) % 16 == 0 &&
+                     (vny <= 1 || (o.sy & 15) == 0) && (vnz <= 1 || (o.sz & 15) == 0);
+            }
+            // Measured (800^3 sub-boxes of 1024^3, profiles/r03/subrows_*): copies gain everywhere
+            // (x0 = 100 0.422 -> 0.295 ms, x 0..800 0.239 -> 0.205 ms); the 3-stream ops gain only
+            // where row ends need masked stores (SumRange x0 = 100 0.425 -> 0.389 ms) and lost on
+            // whole-x planes (0.328 -> 0.375 ms), so edge-free 3-stream boxes keep the per-item
+            // loop (knob value 2 forces pairs for A/B)
+            bool const edges16 = ph16 != 0 || vnx % 16 != 0;
+            if (ok && (ns <= 1 || edges16 || rt::knob(rt::Knob::PointwiseU8Pairs) == 2))
+            {
+                p.g.pair16 = 1;
+                p.g.padded = edges16 ? 1 : 0;
+                p.g.vhead = -ph16;
+                p.g.vnx8 = -ph16 + ((ph16 + vnx + 15) & ~int64_t(15));
+                uint64_t const items = static_cast<uint64_t>((p.g.vnx8 - p.g.vhead) / 8) * static_cast<uint64_t>(vny) * vnz;
+                p.g.fast32 = items < (1ull << 32) && total < (1ull << 32) ? 1 : 0;
+                p.g.divCpr = makeFastDiv(static_cast<uint32_t>((p.g.vnx8 - p.g.vhead) / 8));
+            }
+        }
 
         // general vector path (Pointwise.hpp): any phase, pitch or clamp; voxel sizes may differ
         // (launchPointwise takes it for uniform sizes, convertBox for mixed ones)

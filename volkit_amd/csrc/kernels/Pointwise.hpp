@@ -61,6 +61,10 @@ namespace hipk
         // the destination's own bytes loaded and stored back whole
         int32_t merge;
         int64_t vhead0, vend0;
+        // UInt8 rows (several) on a 16-voxel grid: every row holds an even number of items and
+        // its first item starts 16-B aligned, so items 2l, 2l + 1 form one 16-B access (the
+        // contiguous-lane shape below) with byte-range stores at the row ends
+        int32_t pair16;
     };
 
     struct PassF;   // PointwiseOps.hpp: dst = source code (bytewise CopyRange)
@@ -298,16 +302,20 @@ namespace hipk
                 else
                     return ((rowStart | static_cast<uint64_t>(op.sy) * BPV | static_cast<uint64_t>(op.sz) * BPV) & 15u) == 0;
             };
-            // multi-row boxes: Float32 only (UInt8 pairs measured 4-5 % slower there than the
-            // per-item loop: x 0..768 / whole-x planes of an 800^3 sub-box of 1024^3)
-            bool const shape = MODE == 0 || (BPV == 4 && !g.padded);
+            // multi-row boxes: Float32 without padded rows; UInt8 on the 16-voxel grid (pair16),
+            // byte-range stores at the row ends (the per-item loop stored a straddling item
+            // voxel by voxel: 8 byte stores, 24 store instructions per wave on an 800^3 sub-box
+            // at x0 = 100, 0.30 of 8 TB/s)
+            bool const shape = MODE == 0 || (BPV == 4 && !g.padded) || (BPV == 1 && g.pair16);
             if (end - beg == kQ && shape && aligned(d) && (NS < 1 || aligned(s1)) && (NS < 2 || aligned(s2)))
             {
                 uint32_t a[kUnroll][8], b[kUnroll][8];
+                int64_t xr[kUnroll];
                 // voxel offsets (d, s1, s2) of the lane's 16-B access number q of block u
                 auto at = [&](int u, int q, uint64_t& od, uint64_t& o1, uint64_t& o2) {
                     uint64_t item;
                     uint64_t sub = 0;
+                    xr[u] = 0;
                     if constexpr (BPV == 4)
                     {
                         item = beg + static_cast<uint64_t>(u) * 64u + 32u * static_cast<uint64_t>(q) + lane / 2;
@@ -315,7 +323,7 @@ namespace hipk
                     }
                     else
                         item = beg + static_cast<uint64_t>(u / 2) * 128u + 2u * lane;
-                    pointwiseVecItem<NS, BPV, MODE, F>(d, s1, s2, g, item, o1, o2, od);
+                    pointwiseVecItem<NS, BPV, MODE, F>(d, s1, s2, g, item, o1, o2, od, &xr[u]);
                     od += sub;
                     o1 += sub;
                     o2 += sub;
@@ -385,6 +393,18 @@ namespace hipk
                             w[i] = o[u][4 * i] | o[u][4 * i + 1] << 8 | o[u][4 * i + 2] << 16 | o[u][4 * i + 3] << 24;
                             w[2 + i] = o[u + 1][4 * i] | o[u + 1][4 * i + 1] << 8 | o[u + 1][4 * i + 2] << 16 |
                                        o[u + 1][4 * i + 3] << 24;
+                        }
+                        if constexpr (MODE != 0)
+                        {
+                            int64_t const x = xr[u];
+                            if (g.padded && (x < 0 || x + 16 > g.vnx))
+                            {
+                                // the pair straddles a row end: the row's bytes only
+                                int const lo = x < 0 ? static_cast<int>(-x) : 0;
+                                int const hi = g.vnx - x < 16 ? static_cast<int>(g.vnx - x) : 16;
+                                storeByteRange16(d.data + od[u][0], u32x4{w[0], w[1], w[2], w[3]}, lo, hi);
+                                continue;
+                            }
                         }
                         __builtin_nontemporal_store(u32x4{w[0], w[1], w[2], w[3]},
                                                     reinterpret_cast<u32x4*>(d.data + od[u][0]));

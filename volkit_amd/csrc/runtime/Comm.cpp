@@ -9,11 +9,8 @@
 // tests/test_comm.py) and one grouped RCCL send/receive round on the library's compute
 // stream, so a Resample enqueued next on that stream reads the halo.
 
-#include "Runtime.hpp"
+#include "Comm.hpp"
 #include "volkit_codec.hpp"
-#include "volkit_hip.h"
-
-#include <rccl/rccl.h>
 
 #include <dlfcn.h>
 
@@ -23,12 +20,6 @@
 #include <string>
 #include <type_traits>
 #include <vector>
-
-struct vktHipComm_impl
-{
-    ncclComm_t comm = nullptr;
-    int32_t rank = 0, nranks = 0;
-};
 
 namespace vkt
 {
@@ -87,13 +78,7 @@ namespace
         return rt::fail((std::string(what) + ": librccl.so.1 not found").c_str());
     }
 
-    // planes [z0, z1) of a ceil partition of n planes over `world` ranks (slab.py:slab_bounds)
-    void slabBounds(int32_t n, int32_t world, int32_t rank, int32_t& z0, int32_t& z1)
-    {
-        int64_t const size = (static_cast<int64_t>(n) + world - 1) / world;
-        z0 = static_cast<int32_t>(std::min<int64_t>(rank * size, n));
-        z1 = static_cast<int32_t>(std::min<int64_t>(z0 + size, n));
-    }
+    using comm::slabBounds;
 
     // global source planes rank r's dst slab reads (empty slab: [0, 0))
     vktError needOf(int32_t dstG, int32_t srcG, int32_t world, int32_t r, vktFilterMode fm, int32_t chain,
@@ -149,6 +134,69 @@ namespace
         return vktNoError;
     }
 } // namespace
+
+namespace comm
+{
+    void slabBounds(int32_t n, int32_t world, int32_t rank, int32_t& z0, int32_t& z1)
+    {
+        int64_t const size = (static_cast<int64_t>(n) + world - 1) / world;
+        z0 = static_cast<int32_t>(std::min<int64_t>(static_cast<int64_t>(rank) * size, n));
+        z1 = static_cast<int32_t>(std::min<int64_t>(z0 + size, n));
+    }
+
+    size_t planeBytes(vktHipVolumeView_t const& v)
+    {
+        uint32_t const bpv = codec::bytesPerVoxel(v.dataFormat);
+        if (bpv == 255u || v.dimX < 0 || v.dimY < 0)
+            return 0;
+        return static_cast<size_t>(v.dimX) * static_cast<size_t>(v.dimY) * bpv;
+    }
+
+    vktError planeSpan(vktHipVolumeView_t const& v, int32_t z0, int32_t g0, int32_t g1, char const* what,
+                       uint8_t*& ptr, size_t& bytes)
+    {
+        size_t const plane = planeBytes(v);
+        if (v.data == nullptr || plane == 0 || v.dimZ < 0)
+            return rt::fail((std::string(what) + ": invalid slab view").c_str());
+        if (g0 < z0 || g1 > z0 + v.dimZ || g1 < g0)
+            return rt::fail((std::string(what) + ": the slab buffer does not hold the planes the plan moves").c_str());
+        ptr = v.data + static_cast<size_t>(g0 - z0) * plane;
+        bytes = static_cast<size_t>(g1 - g0) * plane;
+        return vktNoError;
+    }
+
+    vktError rcclRound(vktHipComm_t c, std::vector<Xfer> const& xs, hipStream_t stream, char const* what)
+    {
+        if (xs.empty())
+            return vktNoError;
+        if (!rccl().ok)
+            return noRccl(what);
+        ncclResult_t r = rccl().groupStart();
+        if (r != ncclSuccess)
+            return ncclFail((std::string(what) + ": ncclGroupStart").c_str(), r);
+        for (Xfer const& x : xs)
+        {
+            r = x.send ? rccl().send(x.ptr, x.bytes, ncclUint8, x.peer, c->comm, stream)
+                       : rccl().recv(x.ptr, x.bytes, ncclUint8, x.peer, c->comm, stream);
+            if (r != ncclSuccess)
+            {
+                (void)rccl().groupEnd();
+                return ncclFail((std::string(what) + ": ncclSend/ncclRecv").c_str(), r);
+            }
+        }
+        r = rccl().groupEnd();
+        if (r != ncclSuccess)
+            return ncclFail((std::string(what) + ": ncclGroupEnd").c_str(), r);
+        return vktNoError;
+    }
+
+    vktError localMove(uint8_t* dst, uint8_t const* src, size_t bytes, hipStream_t stream, char const* what)
+    {
+        if (bytes == 0 || dst == src)
+            return vktNoError;
+        return rt::check(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, stream), what);
+    }
+} // namespace comm
 } // namespace vkt
 
 using namespace vkt;
@@ -231,39 +279,58 @@ vktError vktHipSlabExchangeHalo(vktHipComm_t comm, vktHipVolumeView_t localSrc, 
         return rt::fail("vktHipSlabExchangeHalo: null communicator");
     int32_t lo, hi;
     std::vector<vktHipSlabTransfer_t> xs;
-    vktError const e = plan(dstGlobalDimZ, srcGlobalDimZ, comm->nranks, comm->rank, fm, needsNeighbours, lo, hi, xs);
-    if (e != vktNoError)
+    vktError e = plan(dstGlobalDimZ, srcGlobalDimZ, comm->nranks, comm->rank, fm, needsNeighbours, lo, hi, xs);
+    if (e != vktNoError || xs.empty())
         return e;
-    if (xs.empty())
-        return vktNoError;
-    uint32_t const bpv = codec::bytesPerVoxel(localSrc.dataFormat);
-    if (localSrc.data == nullptr || bpv == 0 || localSrc.dimX <= 0 || localSrc.dimY <= 0 || localSrc.dimZ < 0)
-        return rt::fail("vktHipSlabExchangeHalo: invalid local source view");
     // every plane moved must lie in the local buffer (global planes [localZ0, localZ0 + dimZ))
-    for (vktHipSlabTransfer_t const& x : xs)
-        if (x.z0 < localZ0 || x.z1 > localZ0 + localSrc.dimZ)
-            return rt::fail("vktHipSlabExchangeHalo: the local source buffer does not hold the planes the plan moves");
-    size_t const plane = static_cast<size_t>(localSrc.dimX) * static_cast<size_t>(localSrc.dimY) * bpv;
-    hipStream_t const s = rt::computeStream();
-    ncclResult_t r = rccl().groupStart();
-    if (r != ncclSuccess)
-        return ncclFail("vktHipSlabExchangeHalo: ncclGroupStart", r);
+    std::vector<comm::Xfer> moves;
     for (vktHipSlabTransfer_t const& x : xs)
     {
-        uint8_t* const p = localSrc.data + static_cast<size_t>(x.z0 - localZ0) * plane;
-        size_t const bytes = static_cast<size_t>(x.z1 - x.z0) * plane;
-        r = x.send ? rccl().send(p, bytes, ncclUint8, x.peer, comm->comm, s)
-                   : rccl().recv(p, bytes, ncclUint8, x.peer, comm->comm, s);
-        if (r != ncclSuccess)
+        comm::Xfer m{x.peer, x.send, nullptr, 0};
+        e = comm::planeSpan(localSrc, localZ0, x.z0, x.z1, "vktHipSlabExchangeHalo", m.ptr, m.bytes);
+        if (e != vktNoError)
+            return e;
+        moves.push_back(m);
+    }
+    e = comm::rcclRound(comm, moves, rt::computeStream(), "vktHipSlabExchangeHalo");
+    return e != vktNoError ? e : rt::finishLaunch("SlabExchangeHalo_hip");
+}
+
+vktError vktHipSlabExchangeHaloLocal(int32_t numSlabs, vktHipVolumeView_t const* localSrc, int32_t const* localZ0,
+                                     int32_t dstGlobalDimZ, int32_t srcGlobalDimZ, vktFilterMode fm,
+                                     int32_t needsNeighbours)
+{
+    if (numSlabs <= 0 || localSrc == nullptr || localZ0 == nullptr)
+        return rt::fail("vktHipSlabExchangeHaloLocal: invalid slab arrays");
+    // the same plan as the RCCL exchange, every rank's receives executed as device copies from
+    // the owning slab's buffer (the sends are the other side of the same moves)
+    hipStream_t const s = rt::computeStream();
+    for (int32_t r = 0; r < numSlabs; ++r)
+    {
+        int32_t lo, hi;
+        std::vector<vktHipSlabTransfer_t> xs;
+        vktError e = plan(dstGlobalDimZ, srcGlobalDimZ, numSlabs, r, fm, needsNeighbours, lo, hi, xs);
+        if (e != vktNoError)
+            return e;
+        for (vktHipSlabTransfer_t const& x : xs)
         {
-            (void)rccl().groupEnd();
-            return ncclFail("vktHipSlabExchangeHalo: ncclSend/ncclRecv", r);
+            if (x.send)
+                continue;
+            uint8_t *to, *from;
+            size_t n, m;
+            e = comm::planeSpan(localSrc[r], localZ0[r], x.z0, x.z1, "vktHipSlabExchangeHaloLocal", to, n);
+            if (e == vktNoError)
+                e = comm::planeSpan(localSrc[x.peer], localZ0[x.peer], x.z0, x.z1, "vktHipSlabExchangeHaloLocal",
+                                    from, m);
+            if (e == vktNoError && n != m)
+                e = rt::fail("vktHipSlabExchangeHaloLocal: slabs of different plane sizes");
+            if (e == vktNoError)
+                e = comm::localMove(to, from, n, s, "vktHipSlabExchangeHaloLocal: hipMemcpyAsync");
+            if (e != vktNoError)
+                return e;
         }
     }
-    r = rccl().groupEnd();
-    if (r != ncclSuccess)
-        return ncclFail("vktHipSlabExchangeHalo: ncclGroupEnd", r);
-    return rt::finishLaunch("SlabExchangeHalo_hip");
+    return rt::finishLaunch("SlabExchangeHaloLocal_hip");
 }
 
 } // extern "C"

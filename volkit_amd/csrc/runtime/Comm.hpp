@@ -1,0 +1,52 @@
+// Comm.hpp -- internal: the RCCL binding and the plane transport shared by the Z-slab
+// exchange (Comm.cpp) and the Z-slab Range calls (Slab.cpp).
+#pragma once
+
+#include "Runtime.hpp"
+#include "volkit_hip.h"
+
+#include <rccl/rccl.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <vector>
+
+struct vktHipComm_impl
+{
+    ncclComm_t comm = nullptr;
+    int32_t rank = 0, nranks = 0;
+};
+
+namespace vkt
+{
+namespace comm
+{
+    // planes [z0, z1) of a ceil partition of n planes over `world` ranks (slab.py:slab_bounds)
+    void slabBounds(int32_t n, int32_t world, int32_t rank, int32_t& z0, int32_t& z1);
+
+    // Bytes of one plane of a view (dimX * dimY * bpv); 0 for an invalid format.
+    size_t planeBytes(vktHipVolumeView_t const& v);
+
+    // Global planes [g0, g1) of a buffer that holds global planes [z0, z0 + v.dimZ): the device
+    // pointer of plane g0 and the byte count, or an error when the buffer does not hold them.
+    vktError planeSpan(vktHipVolumeView_t const& v, int32_t z0, int32_t g0, int32_t g1, char const* what,
+                       uint8_t*& ptr, size_t& bytes);
+
+    // One point-to-point move of a byte range: `send` to / receive from `peer`.
+    struct Xfer
+    {
+        int32_t peer;
+        int32_t send;
+        uint8_t* ptr;
+        size_t bytes;
+    };
+
+    // The moves as ONE ncclGroupStart .. ncclGroupEnd round of ncclSend / ncclRecv on `stream`
+    // (pairs of ranks match their moves in issue order).
+    vktError rcclRound(vktHipComm_t comm, std::vector<Xfer> const& xs, hipStream_t stream, char const* what);
+
+    // A device-to-device copy on `stream` (the in-process transport: every slab of a
+    // partition held by this process on the library's device).
+    vktError localMove(uint8_t* dst, uint8_t const* src, size_t bytes, hipStream_t stream, char const* what);
+} // namespace comm
+} // namespace vkt

@@ -82,6 +82,7 @@ namespace rt
         HistogramPacked16,             // 0: histograms beyond one LDS tile take one pass per tile
         HistogramMulShift,             // 0: UInt16 bins other than code >> s keep the float formula
         HistogramP16Step,              // 0: P16 threshold tests after each item, not each wave-step
+        PointwiseU8Pairs,              // 0: UInt8 multi-row boxes keep the 8-voxel per-item loop
         Count
     };
     int64_t knob(Knob k);

@@ -19,6 +19,7 @@ vktHipArithmeticRange, ...).  The exchange functions only move bytes and work on
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 from dataclasses import dataclass, field
 from typing import Callable, List, Tuple
@@ -55,6 +56,18 @@ class ResamplePlan:
     local_src: Tuple[int, int]           # planes held in the local source buffer (owned + halo)
     recvs: List[Tuple[int, int, int]] = field(default_factory=list)   # (peer, g0, g1)
     sends: List[Tuple[int, int, int]] = field(default_factory=list)   # (peer, g0, g1)
+    filter_mode: int = 0                 # the filter and chain the plan's source ranges assume
+    chain: bool = False
+
+    def check(self, filter_mode, chain) -> Tuple[int, bool]:
+        """The plan's (filter_mode, chain), or ValueError when a caller passes others: the
+        source sub-views would then miss the z+1 neighbour planes the chain reads."""
+        fm = self.filter_mode if filter_mode is None else filter_mode
+        ch = self.chain if chain is None else bool(chain)
+        if fm != self.filter_mode or ch != self.chain:
+            raise ValueError(f"plan made for filter_mode={self.filter_mode}, chain={self.chain}; "
+                             f"called with filter_mode={fm}, chain={ch}")
+        return fm, ch
 
     @property
     def halo_planes(self) -> int:
@@ -77,7 +90,8 @@ def plan_resample(dst_gdz: int, src_gdz: int, world: int, rank: int, filter_mode
     n = needs[rank]
     lo = min(o[0], n[0]) if n[1] > n[0] else o[0]
     hi = max(o[1], n[1]) if n[1] > n[0] else o[1]
-    plan = ResamplePlan(world, rank, dst_gdz, src_gdz, slab_bounds(dst_gdz, world, rank), o, (lo, hi))
+    plan = ResamplePlan(world, rank, dst_gdz, src_gdz, slab_bounds(dst_gdz, world, rank), o, (lo, hi),
+                        filter_mode=filter_mode, chain=bool(chain))
     for peer in range(world):
         if peer == rank:
             continue
@@ -90,14 +104,35 @@ def plan_resample(dst_gdz: int, src_gdz: int, world: int, rank: int, filter_mode
     return plan
 
 
+@contextlib.contextmanager
+def library_stream(enabled: bool = True):
+    """Make the library's compute stream (vktHipGetComputeStream) torch's current stream for the
+    block.  torch.distributed orders a nccl (RCCL) isend/irecv after the work queued on torch's
+    current stream and a later wait() makes the current stream wait for it; the library's
+    kernels run on its compute stream.  Inside this block the two are one stream, so a send
+    sees the kernels that produced its planes and a kernel enqueued after finish_exchange sees
+    the received planes, whatever stream the caller had current.  No-op when disabled (host
+    tensors, gloo on CPU)."""
+    if not enabled:
+        yield
+        return
+    import torch
+    s = C.c_void_p()
+    if lib.vktHipGetComputeStream(C.byref(s)) != 0:
+        raise RuntimeError(_lib.last_error())
+    with torch.cuda.stream(torch.cuda.ExternalStream(s.value or 0)):
+        yield
+
+
 def start_exchange(plan: ResamplePlan, planes: Callable[[int, int], "torch.Tensor"], group=None):
     """Issue the halo exchange (one batched isend/irecv round) without waiting for it; returns
     the pending round for finish_exchange.  `planes(g0, g1)` returns a writable uint8 tensor
     view of global source planes [g0, g1) in the local buffer.
 
     With the nccl backend (RCCL over xGMI) device planes move device to device on RCCL's own
-    stream, which starts after the work already queued on the current stream; kernels enqueued
-    on the current stream before finish_exchange run concurrently with the transfer.  gloo
+    stream, which starts after the work already queued on torch's current stream; kernels
+    enqueued on that stream before finish_exchange run concurrently with the transfer.  Call it
+    inside library_stream() (resample_slab_overlapped does) so that stream is the library's.  gloo
     moves host tensors only, so device planes are staged through host copies there (CPU tests,
     1-GPU rehearsals)."""
     import torch.distributed as dist
@@ -132,10 +167,12 @@ def exchange_planes(plan: ResamplePlan, planes: Callable[[int, int], "torch.Tens
     finish_exchange(start_exchange(plan, planes, group))
 
 
-def interior_split(plan: ResamplePlan, filter_mode: int, chain: bool) -> int:
+def interior_split(plan: ResamplePlan, filter_mode: int = None, chain: bool = None) -> int:
     """dk such that dst planes [dst0, dk) read only source planes this rank owns (the interior:
     computable while the halo is in flight) and [dk, dst1) read the halo.  dst0 when even the
-    first plane needs a received one; dst1 when nothing is received."""
+    first plane needs a received one; dst1 when nothing is received.  filter_mode / chain
+    default to the plan's (others raise ValueError)."""
+    filter_mode, chain = plan.check(filter_mode, chain)
     d0, d1 = plan.dst
     o0, o1 = plan.owned_src
     if d1 <= d0 or not plan.recvs:
@@ -168,27 +205,32 @@ def sub_view(view, g0: int, g1: int, z0: int):
 
 
 def resample_slab_overlapped(dst_view, src_view, filter_mode: int, plan: ResamplePlan, chain: bool,
-                             planes: Callable[[int, int], "torch.Tensor"], group=None) -> int:
+                             planes: Callable[[int, int], "torch.Tensor"], group=None,
+                             on_library_stream: bool = True) -> int:
     """Halo exchange overlapped with the interior: issue the exchange, resample the dst planes
     that read only owned source planes (source sub-view of exactly those planes, so nothing
     touches the planes in flight), wait for the receives on the stream, then resample the
     boundary planes from the source planes they read.  Each call is a slab resample of its own
-    (the same exact index tables), so the result equals resample_slab's."""
+    (the same exact index tables), so the result equals resample_slab's.  The exchange runs with
+    the library's compute stream as torch's current stream (library_stream; pass
+    on_library_stream=False only for host-tensor planes)."""
+    filter_mode, chain = plan.check(filter_mode, chain)
     d0, d1 = plan.dst
     ls0 = plan.local_src[0]
     if not plan.recvs and not plan.sends:
         return resample_slab(dst_view, src_view, filter_mode, plan)
-    pending = start_exchange(plan, planes, group)
-    dk = interior_split(plan, filter_mode, chain)
-    err = 0
-    for a, b, wait in ((d0, dk, False), (dk, d1, True)):
-        if wait:
-            finish_exchange(pending)
-        if b <= a or err:
-            continue
-        s0, s1 = source_range(plan.dst_gdz, a, b, plan.src_gdz, filter_mode, chain)
-        err = lib.vktHipResampleSlab(sub_view(dst_view, a, b, d0), sub_view(src_view, s0, s1, ls0), filter_mode,
-                                     plan.dst_gdz, a, plan.src_gdz, s0)
+    with library_stream(on_library_stream):
+        pending = start_exchange(plan, planes, group)
+        dk = interior_split(plan, filter_mode, chain)
+        err = 0
+        for a, b, wait in ((d0, dk, False), (dk, d1, True)):
+            if wait:
+                finish_exchange(pending)
+            if b <= a or err:
+                continue
+            s0, s1 = source_range(plan.dst_gdz, a, b, plan.src_gdz, filter_mode, chain)
+            err = lib.vktHipResampleSlab(sub_view(dst_view, a, b, d0), sub_view(src_view, s0, s1, ls0), filter_mode,
+                                         plan.dst_gdz, a, plan.src_gdz, s0)
     return err
 
 
@@ -209,6 +251,131 @@ def resample_slab(dst_view, src_view, filter_mode: int, plan: ResamplePlan) -> i
     """Run the HIP slab resample for this rank (views from StructuredVolume.hip_view())."""
     return lib.vktHipResampleSlab(dst_view, src_view, filter_mode, plan.dst_gdz, plan.dst[0], plan.src_gdz,
                                   plan.local_src[0])
+
+
+# ---- Range calls over Z-slabs (SURVEY.md §8(e): ranges intersected with each slab, planes a
+#      dstOffset.z or a clamped halo moves across slab boundaries sent to their owner) --------------
+FILL, COPY, ARITHMETIC = 0, 1, 2
+
+
+@dataclass
+class Slab:
+    """One rank's part of a Z-slab partitioned volume (include/volkit_hip.h vktHipSlab_t):
+    `view` (HipVolumeView_t, X/Y dims global) holds global planes [z0, z0 + view.dimZ), which
+    include the planes the rank owns in the ceil partition of global_dim_z planes.  `tensor`
+    (optional) is a flat uint8 tensor over the view's bytes -- host memory for gloo on CPU;
+    by default a zero-copy device tensor over view.data."""
+    view: object
+    z0: int
+    global_dim_z: int
+    tensor: object = None
+
+    def c(self):
+        return _lib.HipSlab_t(self.view, self.z0, self.global_dim_z)
+
+    @property
+    def plane_bytes(self) -> int:
+        return self.view.dimX * self.view.dimY * _BYTES_PER_VOXEL[self.view.dataFormat]
+
+    def flat(self):
+        if self.tensor is None:
+            self.tensor = device_tensor(self.view.data, self.plane_bytes * self.view.dimZ)
+        return self.tensor
+
+    def planes(self, g0: int, g1: int):
+        """uint8 tensor view of global planes [g0, g1) of this slab."""
+        if g0 < self.z0 or g1 > self.z0 + self.view.dimZ:
+            raise ValueError(f"slab holds planes [{self.z0}, {self.z0 + self.view.dimZ}), not [{g0}, {g1})")
+        pb = self.plane_bytes
+        return self.flat()[(g0 - self.z0) * pb:(g1 - self.z0) * pb]
+
+
+def range_plan(kind: int, world: int, rank: int, dst_gdz: int, src1_gdz: int, src2_gdz: int, first, last,
+               dst_offset=(0, 0, 0)):
+    """The C plan (vktHipSlabRangePlan): this rank's pieces, its moves in the global order, and
+    the plane counts of its two gather buffers."""
+    args = [kind, world, rank, dst_gdz, src1_gdz, src2_gdz, _lib.Vec3i_t(*first), _lib.Vec3i_t(*last),
+            _lib.Vec3i_t(*dst_offset)]
+    n, m, bp = C.c_int32(), C.c_int32(), (C.c_int32 * 2)()
+    if lib.vktHipSlabRangePlan(*args, None, 0, C.byref(n), None, 0, C.byref(m), bp) != 0:
+        raise RuntimeError(_lib.last_error())
+    pieces, moves = (_lib.HipSlabPiece_t * max(n.value, 1))(), (_lib.HipSlabMove_t * max(m.value, 1))()
+    if lib.vktHipSlabRangePlan(*args, pieces, n.value, C.byref(n), moves, m.value, C.byref(m), bp) != 0:
+        raise RuntimeError(_lib.last_error())
+    return list(pieces[:n.value]), list(moves[:m.value]), (bp[0], bp[1])
+
+
+def _world_rank(group):
+    import torch.distributed as dist
+    if not dist.is_available() or not dist.is_initialized():
+        return 1, 0
+    return dist.get_world_size(group), dist.get_rank(group)
+
+
+def _gpu_pieces(kind, op, world, rank, dst, srcs, first, last, off, value, bufs):
+    s1 = C.byref(srcs[0].c()) if len(srcs) > 0 else None
+    s2 = C.byref(srcs[1].c()) if len(srcs) > 1 else None
+    g = [b.data_ptr() if b is not None else None for b in bufs]
+    return lib.vktHipSlabRangePieces(kind, op, world, rank, dst.c(), s1, s2, _lib.Vec3i_t(*first),
+                                     _lib.Vec3i_t(*last), _lib.Vec3i_t(*off), C.c_float(value), g[0], g[1])
+
+
+def _range(kind, op, dst: Slab, srcs, first, last, off, value, group, run_pieces):
+    import torch
+    import torch.distributed as dist
+
+    world, rank = _world_rank(group)
+    gz = [s.global_dim_z for s in srcs] + [0, 0]
+    pieces, moves, bp = range_plan(kind, world, rank, dst.global_dim_z, gz[0], gz[1], first, last, off)
+    tensors = [dst.flat()] + [s.flat() for s in srcs]
+    on_gpu = any(t.is_cuda for t in tensors)
+    bufs = [None, None]
+    for k, s in enumerate(srcs):
+        if bp[k]:
+            bufs[k] = torch.empty(bp[k] * s.plane_bytes, dtype=torch.uint8, device=s.flat().device)
+    with library_stream(on_gpu):
+        if moves:
+            staged = dist.get_backend(group) == "gloo"
+            ops, landing = [], []
+            for m in moves:
+                s = srcs[m.source]
+                if m.send:
+                    t = s.planes(m.z0, m.z1).contiguous()
+                    ops.append(dist.P2POp(dist.isend, t.cpu() if staged and t.is_cuda else t, m.peer, group))
+                else:
+                    pb = s.plane_bytes
+                    t = bufs[m.source][m.bufPlane * pb:(m.bufPlane + m.z1 - m.z0) * pb]
+                    if staged and t.is_cuda:
+                        host = t.new_empty(t.shape, device="cpu")
+                        landing.append((t, host))
+                        t = host
+                    ops.append(dist.P2POp(dist.irecv, t, m.peer, group))
+            finish_exchange((dist.batch_isend_irecv(ops), landing))
+        err = (run_pieces or _gpu_pieces)(kind, op, world, rank, dst, srcs, first, last, off, value, bufs)
+    if err:
+        raise RuntimeError(_lib.last_error() if err != 0 else "slab range failed")
+    return 0
+
+
+def fill_range(dst: Slab, first, last, value: float, group=None, run_pieces=None) -> int:
+    """FillRange over a Z-slab partitioned volume (global first/last): each rank fills the
+    owned planes of the range; nothing moves."""
+    return _range(FILL, 0, dst, [], first, last, (0, 0, 0), value, group, run_pieces)
+
+
+def copy_range(dst: Slab, src: Slab, first, last, dst_offset=(0, 0, 0), group=None, run_pieces=None) -> int:
+    """CopyRange over Z-slabs (global first/last/dstOffset, source clamped to the global volume,
+    Copy_serial.hpp:38-47): the source planes a rank's dst planes read that other ranks own move
+    to it (one batched isend/irecv round), then the local pieces run."""
+    return _range(COPY, 0, dst, [src], first, last, dst_offset, 0.0, group, run_pieces)
+
+
+def arithmetic_range(op, dst: Slab, s1: Slab, s2: Slab, first, last, dst_offset=(0, 0, 0), group=None,
+                     run_pieces=None) -> int:
+    """{Sum, ..., SafeAbsDiff}Range over Z-slabs (absolute-x reads, dst[x + dstOffset] writes,
+    Arithmetic_serial.hpp:25-41); `op` is an index or a name of _lib.ARITH_OPS."""
+    code = _lib.ARITH_OPS.index(op) if isinstance(op, str) else int(op)
+    return _range(ARITHMETIC, code, dst, [s1, s2], first, last, dst_offset, 0.0, group, run_pieces)
 
 
 # ---- reductions over Z-slabs (SURVEY.md §8(f) F2: the first all-reduce users) -------------------
