@@ -79,7 +79,8 @@ VKTAPI vktError vktHipKernelScopeEnd(vktHipKernelScope scope);
  * tile of 32-bit counters take one pass per tile instead of one pass over packed 16-bit
  * counters), "histogram.mulshift" (1; 0 makes UInt16 histograms whose bins are (code * numBins)
  * >> 16 keep the float bin formula), "histogram.p16_step" (1; 0 runs the packed-16 counters'
- * threshold tests after every item instead of once per wave-step).  For tests and in-process
+ * threshold tests after every item instead of once per wave-step), "render.bricks" (1; 0 makes
+ * MultiScattering sample the dense volume instead of its 8^3-brick copy).  For tests and in-process
  * A/B measurements; unknown names return vktInvalidValue.
  *
  * Writes outside a range box: FillRange / CopyRange / convert and device-functor TransformRange

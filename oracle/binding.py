@@ -227,6 +227,8 @@ class RenderParams(C.Structure):
 
 
 _lib.vko_render.argtypes = [C.POINTER(_Vol), C.POINTER(RenderParams), C.c_void_p, C.c_void_p, C.c_int32]
+_lib.vko_render_window.argtypes = [C.POINTER(_Vol), C.POINTER(RenderParams), C.c_void_p, C.c_void_p, C.c_int32,
+                                   C.c_int32, C.c_int32, C.c_int32, C.c_int32]
 
 
 def render(v: Volume, params: RenderParams, frames: int, accum=None):
@@ -236,3 +238,14 @@ def render(v: Volume, params: RenderParams, frames: int, accum=None):
     col = np.zeros((h, w, 4), np.float32)
     _lib.vko_render(v.ref, C.byref(params), acc.ctypes.data, col.ctypes.data, frames)
     return acc, col
+
+
+def render_window(v: Volume, params: RenderParams, frames: int, window):
+    """Pixels x0 <= x < x1, y0 <= y < y1 of the frame (window = (x0, y0, x1, y1)) from a cleared
+    accumulation -> (accum, color) float32 arrays of shape (y1 - y0, x1 - x0, 4)."""
+    x0, y0, x1, y1 = window
+    h, w = params.height, params.width
+    acc = np.zeros((h, w, 4), np.float32)
+    col = np.zeros((h, w, 4), np.float32)
+    _lib.vko_render_window(v.ref, C.byref(params), acc.ctypes.data, col.ctypes.data, frames, x0, y0, x1, y1)
+    return acc[y0:y1, x0:x1].copy(), col[y0:y1, x0:x1].copy()

@@ -673,10 +673,19 @@ static void r_sample(const vko_volume* v, const vko_render_params* p, int32_t x,
     out[3] = 1.f;
 }
 
-void vko_render(const vko_volume* v, const vko_render_params* p, float* accum, float* color, int32_t num_frames)
+/* Pixels [x0, x1) x [y0, y1) only (accum / color keep the full-viewport layout): full-size
+ * frames (config 5, 1024^2) are checked on windows -- every pixel is independent (its own
+ * random sequence, Render_kernel.hpp per-pixel kernels), so a window equals the same pixels of
+ * the full frame. */
+void vko_render_window(const vko_volume* v, const vko_render_params* p, float* accum, float* color,
+                       int32_t num_frames, int32_t x0, int32_t y0, int32_t x1, int32_t y1)
 {
-    for (int32_t y = 0; y < p->height; ++y)
-        for (int32_t x = 0; x < p->width; ++x) {
+    if (x0 < 0) x0 = 0;
+    if (y0 < 0) y0 = 0;
+    if (x1 > p->width) x1 = p->width;
+    if (y1 > p->height) y1 = p->height;
+    for (int32_t y = y0; y < y1; ++y)
+        for (int32_t x = x0; x < x1; ++x) {
             size_t pix = (size_t)y * (size_t)p->width + (size_t)x;
             float acc[4] = {0.f, 0.f, 0.f, 0.f};
             if (p->frame_begin > 0)
@@ -694,6 +703,11 @@ void vko_render(const vko_volume* v, const vko_render_params* p, float* accum, f
                 color[4 * pix + 3] = acc[3];
             }
         }
+}
+
+void vko_render(const vko_volume* v, const vko_render_params* p, float* accum, float* color, int32_t num_frames)
+{
+    vko_render_window(v, p, accum, color, num_frames, 0, 0, p->width, p->height);
 }
 
 /* ---- synthetic input -------------------------------------------------------------- */

@@ -89,6 +89,8 @@ typedef struct {
 } vko_render_params;
 /* accum / color: width*height*4 floats (row 0 = bottom); accum read when frame_begin > 0 */
 void vko_render(const vko_volume* v, const vko_render_params* p, float* accum, float* color, int32_t num_frames);
+void vko_render_window(const vko_volume* v, const vko_render_params* p, float* accum, float* color,
+                       int32_t num_frames, int32_t x0, int32_t y0, int32_t x1, int32_t y1);
 
 /* Synthetic input shared with the GPU generator (include/volkit_hip.h vktHipSynthesize). */
 uint64_t vko_splitmix64(uint64_t x);

@@ -4,7 +4,10 @@ running the real HIP kernels:
   * slab.aggregates (pass 1 / all_gather / mean / pass 2 / all_gather) == whole-volume oracle;
   * slab.histogram (local counts on the device, all_reduce) == whole-volume oracle, exactly;
   * Float32 "Linear" Resample with the z+1 halo received from the neighbour rank == the
-    rank's slab of the whole-volume oracle resample.
+    rank's slab of the whole-volume oracle resample;
+  * slab.copy_range / slab.arithmetic_range with a dstOffset.z that moves planes across the
+    slab boundary (device slabs, the moved planes staged through gloo) == the rank's planes of
+    one whole-volume oracle call.
 """
 import ctypes as C
 import os
@@ -16,6 +19,8 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 WORLD = 2
+RANGE_COPY = ((1, 2, 3), (30, 18, 20), (0, 1, 4))       # first, last, dstOffset: planes move up 1
+RANGE_ARITH = ((0, 0, 2), (32, 20, 20), (0, 0, -2))     # ... and down 2
 
 
 def _free_port():
@@ -112,6 +117,21 @@ def _worker(rank, port, q):
         torch.cuda.synchronize()
         assert np.array_equal(dst2.to_numpy(), dst.to_numpy()), f"rank {rank}: overlapped != single call (dk={dk})"
         out["split"] = (d0, dk, d1)
+        # Range calls over the slabs: planes cross the rank boundary (dstOffset.z)
+        from volkit_amd import _lib
+
+        def dev_slab(glob):
+            t = torch.from_numpy(np.ascontiguousarray(glob[z0:z1]).view(np.uint8).reshape(-1).copy()).cuda()
+            view = _lib.HipVolumeView_t(t.data_ptr(), gx, gy, z1 - z0, vkt.DataFormat_Float32, 0.0, 1.0)
+            return slab.Slab(view, z0, gz, t)
+
+        a_sl, b_sl = dev_slab(vals), dev_slab(vals[::-1] * 0.5)
+        c_sl, s_sl = dev_slab(np.zeros_like(vals)), dev_slab(np.zeros_like(vals))
+        slab.copy_range(c_sl, a_sl, *RANGE_COPY)
+        slab.arithmetic_range("SafeSum", s_sl, a_sl, b_sl, *RANGE_ARITH)
+        torch.cuda.synchronize()
+        out["range"] = (z0, z1, c_sl.tensor.cpu().numpy().view(np.uint32).copy(),
+                        s_sl.tensor.cpu().numpy().view(np.uint32).copy())
         ep.device = vkt.ExecutionPolicy.Device_CPU
         vkt.SetThreadExecutionPolicy(ep)
         q.put((rank, out, (d0, d1, dst.to_numpy()), plan.halo_planes))
@@ -139,8 +159,17 @@ def test_two_ranks_on_one_gpu():
     vals = _global_volume()
     gz, gy, gx = vals.shape
     whole = ob.Volume(vals.view(np.uint32), 7)
+    whole_b = np.ascontiguousarray(vals[::-1] * 0.5)
+    ref_c = ob.Volume(np.zeros_like(vals).view(np.uint32), 7)
+    ob.copy_range(ref_c, ob.Volume(vals.view(np.uint32), 7), *RANGE_COPY)
+    ref_s = ob.Volume(np.zeros_like(vals).view(np.uint32), 7)
+    ob.arith_range("SafeSum", ref_s, ob.Volume(vals.view(np.uint32), 7), ob.Volume(whole_b.view(np.uint32), 7),
+                   *RANGE_ARITH)
     for r, out, _, halo in res:
         assert not isinstance(out, str), out
+        z0, z1, got_c, got_s = out.pop("range")
+        assert np.array_equal(got_c, ref_c.codes[z0:z1].reshape(-1)), f"rank {r}: slab copy_range differs"
+        assert np.array_equal(got_s, ref_s.codes[z0:z1].reshape(-1)), f"rank {r}: slab arithmetic_range differs"
         d0, dk, d1 = out.pop("split")
         assert d0 < dk < d1 or not halo, (r, d0, dk, d1)   # a rank with a halo has an interior
     for key in res[0][1]:

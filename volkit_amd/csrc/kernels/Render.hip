@@ -492,8 +492,9 @@ vktError vktHipRender(vktHipVolumeView_t volume, vktHipRenderParams_t const* par
     int32_t const nbx = (volume.dimX + 7) / 8, nby = (volume.dimY + 7) / 8, nbz = (volume.dimZ + 7) / 8;
     uint32_t const bpv = codec::bytesPerVoxel(fmt);
     uint64_t const brickRows = static_cast<uint64_t>(nbx) * static_cast<uint64_t>(nby) * static_cast<uint64_t>(nbz) * 64;
-    uint8_t* b = brickRows * 8 * bpv <= kMaxBrickBytes ? static_cast<uint8_t*>(bricks.acquire(brickRows * 8 * bpv, s))
-                                                       : nullptr;
+    uint8_t* b = brickRows * 8 * bpv <= kMaxBrickBytes && rt::knob(rt::Knob::RenderBricks) != 0
+                     ? static_cast<uint8_t*>(bricks.acquire(brickRows * 8 * bpv, s))
+                     : nullptr;
     if (!b)
         (void)hipGetLastError();   // a failed scratch allocation only means: render the dense volume
     if (b)

@@ -83,6 +83,7 @@ namespace rt
         HistogramMulShift,             // 0: UInt16 bins other than code >> s keep the float formula
         HistogramP16Step,              // 0: P16 threshold tests after each item, not each wave-step
         PointwiseU8Pairs,              // 0: UInt8 multi-row boxes keep the 8-voxel per-item loop
+        RenderBricks,                  // 0: multi-scattering samples the dense volume, not an 8^3-brick copy
         Count
     };
     int64_t knob(Knob k);
