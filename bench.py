@@ -21,6 +21,10 @@ them is `value`):
   * f32_linear     -- Float32 "Linear" Resample with the z+1 halo plane exchanged between
                       neighbour ranks over torch.distributed on device tensors (RCCL over
                       xGMI at N>1): per rank 512^3 -> 1024^3 of the same global layout;
+  * config4_2048   -- BASELINE config 4 in its STRONG-scaling form: the fixed global volume
+                      1024^3 -> 2048^3 Resample + SumRange 2048^3 UInt16 Z-slab partitioned over
+                      the N GPUs launched (at N=1 the whole 2048^3 on one GPU, ~50 GiB of
+                      volumes): the denominator and numerator of BASELINE.md §4's speedup;
   * copy_peak      -- the library's own Copy 1024^3 UInt16, the achievable streaming rate;
   * cpu_baseline   -- the oracle port (1 thread) on the full 1024^3 pipeline and on 512^3.
 """
@@ -42,7 +46,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
     # the first ~10-20 ms of sustained streaming run below the steady HBM rate (measured with
-    # tools/libbench.cpp: 1.09 ms per SumRange in the first 10 launches, 1.01 ms after), so the
+    # dev/kbench/libbench.cpp: 1.09 ms per SumRange in the first 10 launches, 1.01 ms after), so the
     # default warm-up covers ~35 ms; an explicit --warmup is honoured as given
     p.add_argument("--warmup", type=int, default=25)
     p.add_argument("--dst", type=int, default=1024, help="per-GPU dst cube edge (source = dst/2)")
@@ -51,6 +55,9 @@ def parse():
     p.add_argument("--no-secondary", action="store_true",
                    help="skip the mapping [-1,3] and Float32-Linear secondary measurements")
     p.add_argument("--cpu-dst", type=int, default=1024, help="dst edge of the CPU-baseline run")
+    p.add_argument("--config4-edge", type=int, default=2048,
+                   help="dst edge of the fixed global config-4 volume (strong scaling; source = edge/2)")
+    p.add_argument("--no-config4", action="store_true", help="skip the strong-scaling config-4 measurement")
     p.add_argument("--layout-gpus", type=int, default=0,
                    help="single process: run rank 0's slab of the M-GPU global layout")
     p.add_argument("--dist-backend", default="nccl",
@@ -272,6 +279,9 @@ def main():
             "traffic": traffic,
             "resample_achieved": gbs(res_bytes, res_ms),
             "pipeline_frac": round(pipe_bytes / ((res_ms + sum_ms) / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+            "resample_note": "resample_achieved = algorithmic bytes (N_src*2 + N_dst*2) / event time, not a "
+                             "sustained HBM rate: each source line is read by several dst rows and can be "
+                             "served from the caches (Infinity Cache hits are counted in FETCH_SIZE too)",
         },
     }
 
@@ -297,6 +307,8 @@ def main():
         # every rank, so no rank is left waiting in a collective)
         out["mapping_m1_3"] = secondary(mapping_m1_3)
         out["f32_linear"] = secondary(lambda: f32_linear(ctx, vkt, slab, lib, args, layout_n, stream))
+    if not args.no_config4:
+        out["config4_2048"] = secondary(lambda: config4_strong(ctx, vkt, slab, lib, args, layout_n, stream))
 
     if not args.no_copy_peak:
         # achievable streaming rate on this box: the library's own CopyRange of one volume
@@ -427,6 +439,74 @@ def f32_linear(ctx, vkt, slab, lib, args, layout_n, stream):
         "resample_frac": round(nbytes / (res_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
     }
     del S, R
+    return out
+
+
+def config4_layout(edge, n, rank):
+    """BASELINE config 4, strong scaling: ONE global volume -- source (edge/2)^3 UInt16, dst and
+    SumRange edge^3 -- Z-slab partitioned over n GPUs.  Returns rank's (dst planes, source planes
+    held, exchange plan); for edge/2 divisible by n every dst slab reads only its own source
+    planes (UInt16 "Linear" = Nearest exactly), so the plan is empty."""
+    from volkit_amd import slab
+    plan = slab.plan_resample(edge, edge // 2, n, rank, 1, chain=False)
+    return plan.dst, plan.local_src, plan
+
+
+def config4_strong(ctx, vkt, slab, lib, args, layout_n, stream):
+    """The fixed config-4 volume over the launched ranks: value = edge^3 dst voxels per step
+    (each rank its slab; max-over-ranks time), so value(N) / value(1) is the strong-scaling
+    speedup BASELINE.md §4 quotes (8.86 ms on 1 GPU vs 1.11 ms per GPU at 8 on A100s)."""
+    torch = ctx.torch
+    rank, world = ctx.rank, ctx.world
+    E = args.config4_edge
+    Sx = E // 2
+    UINT16, LINEAR = vkt.DataFormat_UInt16, vkt.FilterMode_Linear
+    (dz0, dz1), (ls0, ls1), plan = config4_layout(E, layout_n, rank)
+    S = vkt.StructuredVolume(Sx, Sx, ls1 - ls0, UINT16)
+    R = vkt.StructuredVolume(E, E, dz1 - dz0, UINT16)
+    B = vkt.StructuredVolume(E, E, dz1 - dz0, UINT16)
+    D = vkt.StructuredVolume(E, E, dz1 - dz0, UINT16)
+    for k, v in enumerate((S, B)):
+        assert vkt.Synthesize(v, 0x5EED + 40 + k + 1000 * rank) == 0, vkt.last_error()
+    sv, rv, bv, dv = S.hip_view(), R.hip_view(), B.hip_view(), D.hip_view()
+    plane = Sx * Sx * 2
+    first, last, zero = _lib_vec(0, 0, 0), _lib_vec(E, E, dz1 - dz0), _lib_vec(0, 0, 0)
+
+    def planes(g0, g1):
+        return slab.device_tensor(sv.data + (g0 - ls0) * plane, (g1 - g0) * plane)
+
+    def step(ev):
+        if plan.recvs or plan.sends:
+            slab.exchange_planes(plan, planes)
+        if ev:
+            ev[0].record(stream)
+        e1 = lib.vktHipResampleSlab(rv, sv, LINEAR, E, dz0, Sx, ls0)
+        if ev:
+            ev[1].record(stream)
+        e2 = lib.vktHipArithmeticRange(0, dv, rv, bv, first, last, zero)
+        if ev:
+            ev[2].record(stream)
+        if e1 or e2:
+            raise RuntimeError(vkt.last_error())
+
+    steps = max(3, args.steps // 10)
+    elapsed, (res_ms, sum_ms) = ctx.timed(step, steps, 2, 2)
+    ms = elapsed * 1e3 / steps
+    vox = E * E * (dz1 - dz0)
+    nbytes = 2 * Sx * Sx * (ls1 - ls0) + 2 * vox + 6 * vox
+    out = {
+        "workload": f"BASELINE config 4, strong scaling: Resample {Sx}^3->{E}^3 UInt16 Linear + SumRange {E}^3 "
+                    f"UInt16, one fixed global volume Z-slab partitioned over {layout_n} GPU(s)"
+                    + (" (rank 0's slab only, on 1 GPU)" if layout_n != world else ""),
+        "scaling": "strong", "global_dst": [E, E, E], "dst_planes_per_rank": dz1 - dz0,
+        "value": round(vox * world / (ms / 1e3) / 1e9, 3), "unit": "Gvoxels/s", "ms_per_step": round(ms, 4),
+        "kernels_ms": {"Resample": round(res_ms, 4), "SumRange": round(sum_ms, 4)},
+        "pipeline_frac": round(nbytes / ((res_ms + sum_ms) / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+        "halo_planes_per_rank": plan.halo_planes,
+        "note": "speedup at N = config4_2048.value(N) / config4_2048.value(1); per-GPU work shrinks as N grows",
+    }
+    del S, R, B, D
+    torch.cuda.synchronize()
     return out
 
 

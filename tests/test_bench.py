@@ -21,11 +21,43 @@ def test_global_dims_double_one_axis_per_doubling():
     assert bench.global_dims(64, 3) == [64, 64, 192]           # non-powers of two stack in z
 
 
+@pytest.mark.parametrize("n", [1, 2, 4, 8])
+def test_config4_strong_layout(n):
+    """The fixed 2048^3 config-4 volume over n GPUs: dst slabs partition 2048 planes, each rank
+    holds exactly its own source planes (2048 / n dst planes from 1024 / n), nothing moves."""
+    planes = []
+    for rank in range(n):
+        (d0, d1), (s0, s1), plan = bench.config4_layout(2048, n, rank)
+        assert d1 - d0 == 2048 // n and (s0, s1) == (d0 // 2, d1 // 2)
+        assert plan.halo_planes == 0 and not plan.sends and not plan.recvs
+        planes += list(range(d0, d1))
+    assert planes == list(range(2048))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layout", [0, 2, 4])
+def test_bench_config4_layout_rehearsal(layout):
+    """config4_2048 on one GPU: the whole fixed volume (layout 0) or rank 0's slab of the
+    2- / 4-GPU layout, at a reduced edge."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--dst", "128", "--steps", "3", "--warmup", "1",
+           "--no-cpu-baseline", "--no-copy-peak", "--no-secondary", "--config4-edge", "512"]
+    if layout:
+        cmd += ["--layout-gpus", str(layout)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    c4 = out["config4_2048"]
+    assert "error" not in c4, c4
+    assert c4["scaling"] == "strong" and c4["global_dst"] == [512] * 3 and c4["value"] > 0
+    assert c4["dst_planes_per_rank"] == 512 // max(layout, 1) and c4["halo_planes_per_rank"] == 0
+    assert ("rank 0's slab only" in c4["workload"]) == (layout > 1)
+
+
 @pytest.mark.gpu
 def test_bench_small_run_prints_one_contract_line():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dst", "128", "--steps", "3",
-                        "--warmup", "2", "--cpu-dst", "64"], capture_output=True, text=True, timeout=300,
-                       cwd=ROOT)
+                        "--warmup", "2", "--cpu-dst", "64", "--config4-edge", "256"], capture_output=True, text=True,
+                       timeout=300, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout
@@ -44,5 +76,6 @@ def test_bench_small_run_prints_one_contract_line():
     assert fp["value"] > 0 and 0 < fp["SumRange_frac"] < 1.2
     f32 = out["f32_linear"]
     assert f32["value"] > 0 and f32["halo_planes_per_rank"] == 0 and "Float32 Linear" in f32["workload"]
+    assert out["config4_2048"]["value"] > 0 and out["config4_2048"]["scaling"] == "strong"
     cpu = out["cpu_baseline"]
     assert cpu["kind"] == "port" and cpu["cores"] == 1 and cpu["value"] > 0

@@ -78,6 +78,25 @@ def pipelined(fn, reps):
     return a.elapsed_time(b) / reps
 
 
+def table_image(d, s):
+    """Distinct source indices the exact per-axis table s = (int32)((float)x / (float)d * (float)s)
+    of Resample_serial.hpp:26-71 hits for x in [0, d) (float32 arithmetic, as the kernels)."""
+    import numpy as np
+    x = np.arange(d, dtype=np.float32)
+    return int(np.unique((x / np.float32(d) * np.float32(s)).astype(np.int32)).size)
+
+
+def resample_bytes(sdims, ddims, bs, bd, every_row=False):
+    """Bytes a Resample moves: the source rows the dst rows read (whole rows: the gather kernel
+    stages each read row in LDS; the replication kernel reads rows too) x their planes, or every
+    source row when the kernel reads them all (Float32 Linear: unstaged rows are classified for
+    the chain), plus the dst bytes.  Equals the §8(d) N_src*b_s + N_dst*b_d
+    whenever every source row is read (upsampling, same dims)."""
+    sx, sy, sz = sdims
+    rows = sy * sz if every_row else table_image(ddims[1], sy) * table_image(ddims[2], sz)
+    return bs * sx * rows + bd * ddims[0] * ddims[1] * ddims[2]
+
+
 def report(name, ms, nbytes, voxels):
     print(json.dumps({"case": name, "ms": round(ms, 4), "GB/s": round(nbytes / ms / 1e6, 1),
                       "frac_of_8TBs": round(nbytes / ms / 1e6 / 8000, 4),
@@ -257,7 +276,7 @@ def main():
         rng_fill(S, 1024 ** 3)
         Rv = alloc((768,) * 3, 7)
         report("weak Resample 1024^3->768^3 Float32 Linear (gather)", timed(lambda: lib.vktHipResample(Rv, S, 1), R),
-               4 * 1024 ** 3 + 4 * 768 ** 3, 768 ** 3)
+               resample_bytes((1024,) * 3, (768,) * 3, 4, 4, every_row=True), 768 ** 3)
         free(S, Rv)
     if want("general"):
         # boxes the aligned vector path cannot take: operands at different 8-voxel phases,
@@ -323,7 +342,19 @@ def main():
             Rv = alloc((de,) * 3, fmt)
             ms = timed(lambda: lib.vktHipResample(Rv, S, fm), max(3, R // 2))
             report(f"gather Resample {se}^3->{de}^3 fmt{fmt} {'Linear' if fm else 'Nearest'}", ms,
-                   b * se ** 3 + b * de ** 3, de ** 3)
+                   resample_bytes((se,) * 3, (de,) * 3, b, b, every_row=fmt == 7 and fm == 1), de ** 3)
+            free(S, Rv)
+    if want("gpmc"):
+        # one launch per case for FETCH / WRITE passes: the downsampling gathers whose bytes the
+        # table image decides (UInt16: staged rows only; Float32 Linear: every source row)
+        for fmt, b, fm in ((5, 2, 1), (7, 4, 1)):
+            S = alloc((1024,) * 3, fmt, seed=21)
+            if fmt == 7:
+                rng_fill(S, 1024 ** 3)
+            Rv = alloc((768,) * 3, fmt)
+            ms = timed(lambda: lib.vktHipResample(Rv, S, fm), R)
+            report(f"gpmc Resample 1024^3->768^3 fmt{fmt} Linear", ms,
+                   resample_bytes((1024,) * 3, (768,) * 3, b, b, every_row=fmt == 7), 768 ** 3)
             free(S, Rv)
     if want("decompose"):
         # BrickDecompose: 1024^3 UInt16 into 64^3 bricks with a 1-voxel halo
@@ -520,7 +551,7 @@ def main():
                                                           R), 6 * 800 ** 3, 800 ** 3)
     D1000 = alloc((1000, 1000, 1000), 5)
     report("Resample 1024^3->1000^3 UInt16 Nearest (gather)", timed(lambda: lib.vktHipResample(D1000, Rv, 0), R),
-           2 * 1000 ** 3 + 2 * e ** 3, 1000 ** 3)
+           resample_bytes((e,) * 3, (1000,) * 3, 2, 2), 1000 ** 3)
     free(S, Rv, B, D, D1000)
     # per-format streaming rates of the pointwise engine (8-voxel items: 8 B / 16 B / 32 B per lane)
     for fmt, bpv, name in ((4, 1, "UInt8"), (7, 4, "Float32")):

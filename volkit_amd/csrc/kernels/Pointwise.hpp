@@ -102,11 +102,11 @@ namespace hipk
     // stores: every byte is touched once.
     //
     // Quantum per workgroup: ONE wave.  First measured for the 3-stream UInt16 Sum at 1024^3
-    // (tools/kbench7.hip, kbench9.hip): 2 KiB per operand ran 0.98-0.99 ms (6.5 TB/s) against
+    // (dev/kbench/kbench7.hip, kbench9.hip): 2 KiB per operand ran 0.98-0.99 ms (6.5 TB/s) against
     // 1.01-1.08 ms for 4 waves x 4 items (16 KiB per operand): small one-shot workgroups keep
     // more distinct DRAM pages in flight per CU while the moving window stays compact.
     //
-    // Quantum size per stream count, measured with tools/kbench_fill.hip on 2 GiB buffers
+    // Quantum size per stream count, measured with dev/kbench/kbench_fill.hip on 2 GiB buffers
     // (MI355X, one-wave workgroups, 16-B nontemporal accesses): pure stores run best at 4 KiB
     // per workgroup (6.4-6.5 TB/s vs 5.1-5.3 at 2 KiB and 5.7-5.9 at 8 KiB); copies and the
     // 3-stream sum at 1 KiB of each stream (copy 6.82 vs 6.55 TB/s at 2 KiB, sum 6.34 vs 6.14).
