@@ -35,6 +35,7 @@ def main():
         ds = [disp[k] for k in sorted(k for k in disp if k[0] == pname)]
         # drop the input synthesis / setup kernels: keep dispatches of the measured ops
         ds = [d for d in ds if "synthKernel" not in d["kernel"] and "elementwise" not in d["kernel"]
+              and "__amd_rocclr" not in d["kernel"] and "distribution" not in d["kernel"]
               and "fill" not in d["kernel"].lower()[:40]]
         for i, c in enumerate(cases):
             chunk = ds[i * per:(i + 1) * per]

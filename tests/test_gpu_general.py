@@ -207,37 +207,44 @@ def test_multirow_contiguous_lanes(lib, o, fmt, box):
               f"copy fmt={fmt} box={box}")
 
 
-@pytest.mark.parametrize("x0", list(range(16)))
-def test_uint8_pair16_rows(lib, o, x0):
+@pytest.mark.parametrize("x0", list(range(16)) + [37, 50, 63])
+@pytest.mark.parametrize("dims", [(6, 48, 96), (5, 40, 192)], ids=["rows96", "rows192-merge"])
+def test_uint8_pair16_rows(lib, o, x0, dims):
     """UInt8 multi-row boxes on the 16-voxel grid (pair16: one 16-B access per lane for two
     items, byte-range stores at the row ends, kernels/KernelCommon.hpp storeByteRange16): every
     row-start phase x0 mod 16 times row lengths covering every tail length 1..16 and rows shorter
     than one access, for Copy (same offset: the aligned path) and SafeSum / Sum vs the oracle,
-    with the knob pointwise.u8_pairs on and off.  The destination's bytes outside the box must
-    survive (the stores write only the box)."""
+    with the knob pointwise.u8_pairs on and off.  On 192-voxel rows (64-B aligned pitches) boxes
+    with >= 64-B gaps take 64-B sector completion (pairs in the end sectors merged with the
+    destination's own bytes; knob pointwise.merge_sectors = 2 extends it to the arithmetic ops).
+    The destination's bytes outside the box must survive."""
     rng = np.random.default_rng(100 + x0)
-    dims = (6, 48, 96)
+    if x0 >= 16 and dims[2] == 96:
+        pytest.skip("phases past 16 only on the wide rows")
     a = rand_codes(rng, 4, dims)
     b = rand_codes(rng, 4, dims)
     dinit = rand_codes(rng, 4, dims)
+    X = dims[2]
     from volkit_amd._lib import lib as L
     try:
-        for on in (1, 0):
+        for on, mk in ((1, -1), (1, 2), (0, -1)):
             assert L.vktHipSetTuningKnob(b"pointwise.u8_pairs", on) == 0
-            for w in (1, 3, 8, 15, 16, 17, 24, 31, 32, 33, 45, 64, 96 - x0):
-                if x0 + w > 96:
+            assert L.vktHipSetTuningKnob(b"pointwise.merge_sectors", mk) == 0
+            for w in (1, 3, 8, 15, 16, 17, 24, 31, 32, 33, 45, 64, 65, 100, 127, X - x0):
+                if x0 + w > X:
                     continue
-                first, last = (x0, 1, 0), (x0 + w, 47, 6)
+                first, last = (x0, 1, 0), (x0 + w, dims[1] - 1, dims[0])
                 for op in ("SafeSum", "Sum"):
                     da, db, dd = Dev(a, 4), Dev(b, 4), Dev(dinit, 4)
                     assert L.vktHipArithmeticRange(OPS.index(op), dd.view, da.view, db.view, vec(first), vec(last),
                                                    vec((0, 0, 0))) == 0, last_error()
                     ref = o.arith(op, [4] * 3, [(0.0, 1.0)] * 3, a, b, dinit.copy(), first, last, (0, 0, 0))
-                    assert_codes_equal(dd.read(), ref, 4, f"{op} pairs={on} x0={x0} w={w}")
+                    assert_codes_equal(dd.read(), ref, 4, f"{op} pairs={on} merge={mk} x0={x0} w={w}")
                 copy_case(lib, o, 4, 4, (0.0, 1.0), (0.0, 1.0), a, dinit, first, last, first, 0, 0,
-                          f"copy pairs={on} x0={x0} w={w}")
+                          f"copy pairs={on} merge={mk} x0={x0} w={w}")
     finally:
         assert L.vktHipSetTuningKnob(b"pointwise.u8_pairs", -1) == 0
+        assert L.vktHipSetTuningKnob(b"pointwise.merge_sectors", -1) == 0
 
 
 def test_general_knob_matches_scalar_kernel(lib, o):

@@ -217,19 +217,22 @@ def main():
                  ("x 0..800", Vec3i_t(0, 100, 100), Vec3i_t(800, 900, 900)),
                  ("x 0..1024 (planes)", Vec3i_t(0, 100, 100), Vec3i_t(1024, 900, 900)))
         for rnd in range(3):
-            for kv in (0, 1, 2):
-                lib.vktHipSetTuningKnob(b"pointwise.u8_pairs", kv)
+            for kv in ((0, -1), (1, 0), (1, 1), (1, 2), (2, -1)):   # (u8_pairs, merge_sectors)
+                lib.vktHipSetTuningKnob(b"pointwise.u8_pairs", kv[0])
+                lib.vktHipSetTuningKnob(b"pointwise.merge_sectors", kv[1])
                 for lab, f0, f1 in boxes:
                     ab.setdefault(("CopyRange", lab, kv), []).append(
                         timed(lambda: lib.vktHipCopyRange(D, A, f0, f1, f0), R))
                     ab.setdefault(("SumRange", lab, kv), []).append(
                         timed(lambda: lib.vktHipArithmeticRange(0, D, A, B, f0, f1, o), R))
         lib.vktHipSetTuningKnob(b"pointwise.u8_pairs", -1)
+        lib.vktHipSetTuningKnob(b"pointwise.merge_sectors", -1)
         for (op, lab, kv), ts in sorted(ab.items()):
             ts.sort()
             f0, f1 = [(b[1], b[2]) for b in boxes if b[0] == lab][0]
             nv = (f1.x - f0.x) * (f1.y - f0.y) * (f1.z - f0.z)
-            report(f"u8ab {op} {lab} UInt8 u8_pairs={kv} (median of 3 rounds, spread {ts[0]:.4f}-{ts[-1]:.4f})",
+            report(f"u8ab {op} {lab} UInt8 u8_pairs={kv[0]} merge_sectors={kv[1]} (median of 3 rounds, "
+                   f"spread {ts[0]:.4f}-{ts[-1]:.4f})",
                    ts[1], (2 if op == "CopyRange" else 3) * nv, nv)
         free(A, B, D)
     if want("weakspots"):

@@ -289,6 +289,20 @@ namespace hipk
             __builtin_nontemporal_store(static_cast<uint8_t>(at(a)), p + a);
     }
 
+    // Bytes [lo, hi) of v, the others from own (0 <= lo <= hi <= 16; lo == hi: own only).
+    __device__ __forceinline__ u32x4 mergeBytes16(u32x4 v, u32x4 own, int lo, int hi)
+    {
+        auto m = [&](int dw) -> uint32_t {   // byte mask of dword dw: bytes 4dw..4dw+3 in [lo, hi)
+            int const a = lo - 4 * dw, b = hi - 4 * dw;
+            uint32_t const ma = a <= 0 ? 0xFFFFFFFFu : (a >= 4 ? 0u : 0xFFFFFFFFu << (8 * a));
+            uint32_t const mb = b >= 4 ? 0xFFFFFFFFu : (b <= 0 ? 0u : 0xFFFFFFFFu >> (8 * (4 - b)));
+            return ma & mb;
+        };
+        uint32_t const m0 = m(0), m1 = m(1), m2 = m(2), m3 = m(3);
+        return u32x4{(v.x & m0) | (own.x & ~m0), (v.y & m1) | (own.y & ~m1), (v.z & m2) | (own.z & ~m2),
+                     (v.w & m3) | (own.w & ~m3)};
+    }
+
     // XCD-aware block order (guide §5.5 T1): hardware deals workgroups round-robin over the
     // 8 XCDs, so block b and b+8 share an L2.  Remap so each XCD walks one contiguous band of
     // logical blocks -- neighbouring rows then hit the same L2.  Speed only, never correctness.

@@ -125,7 +125,7 @@ namespace hipk
     template <int NS, int BPV, int MODE, class F>
     __device__ __forceinline__ void pointwiseVecItem(Operand const& d, Operand const& s1, Operand const& s2,
                                                      Geom const& g, uint64_t it, uint64_t& o1, uint64_t& o2,
-                                                     uint64_t& od, int64_t* rowX = nullptr)
+                                                     uint64_t& od, int64_t* rowX = nullptr, int64_t span = 8)
     {
         if constexpr (MODE == 0)
         {
@@ -162,7 +162,7 @@ namespace hipk
             {
                 // sector completion: sources only inside the rows' own 8-aligned items
                 int64_t xl = static_cast<int64_t>(x);
-                xl = xl < g.vhead0 ? g.vhead0 : (xl > g.vend0 - 8 ? g.vend0 - 8 : xl);
+                xl = xl < g.vhead0 ? g.vhead0 : (xl > g.vend0 - span ? g.vend0 - span : xl);
                 x = static_cast<uint64_t>(xl);
             }
             o1 = s1.base + k * s1.sz + j * s1.sy + x;
@@ -323,7 +323,7 @@ namespace hipk
                     }
                     else
                         item = beg + static_cast<uint64_t>(u / 2) * 128u + 2u * lane;
-                    pointwiseVecItem<NS, BPV, MODE, F>(d, s1, s2, g, item, o1, o2, od, &xr[u]);
+                    pointwiseVecItem<NS, BPV, MODE, F>(d, s1, s2, g, item, o1, o2, od, &xr[u], BPV == 1 ? 16 : 8);
                     od += sub;
                     o1 += sub;
                     o2 += sub;
@@ -368,6 +368,17 @@ namespace hipk
                     load(s1, o1, a);
                 if constexpr (NS >= 2)
                     load(s2, o2, b);
+                // UInt8 pairs with 64-B sector completion: a pair outside the box row (inside an
+                // end sector) or straddling its end is stored whole, its bytes outside the row
+                // being the destination's own
+                u32x4 own[kUnroll];
+                if constexpr (BPV == 1 && MODE != 0)
+                {
+#pragma unroll
+                    for (int u = 0; u < kUnroll; u += 2)
+                        if (g.merge && (xr[u] < 0 || xr[u] + 16 > g.vnx))
+                            own[u] = *reinterpret_cast<u32x4 const*>(d.data + od[u][0]);
+                }
                 uint32_t o[kUnroll][8];
 #pragma unroll
                 for (int u = 0; u < kUnroll; ++u)
@@ -399,10 +410,16 @@ namespace hipk
                             int64_t const x = xr[u];
                             if (g.padded && (x < 0 || x + 16 > g.vnx))
                             {
-                                // the pair straddles a row end: the row's bytes only
-                                int const lo = x < 0 ? static_cast<int>(-x) : 0;
-                                int const hi = g.vnx - x < 16 ? static_cast<int>(g.vnx - x) : 16;
-                                storeByteRange16(d.data + od[u][0], u32x4{w[0], w[1], w[2], w[3]}, lo, hi);
+                                // the pair straddles a row end (or, merging, lies in an end
+                                // sector): the row's bytes only, or the whole 16 B merged with
+                                // the destination's own bytes
+                                int const lo = x < 0 ? static_cast<int>(x < -16 ? 16 : -x) : 0;
+                                int const hi = g.vnx - x < 16 ? static_cast<int>(g.vnx - x < 0 ? 0 : g.vnx - x) : 16;
+                                if (g.merge)
+                                    __builtin_nontemporal_store(mergeBytes16(u32x4{w[0], w[1], w[2], w[3]}, own[u], lo, hi),
+                                                                reinterpret_cast<u32x4*>(d.data + od[u][0]));
+                                else
+                                    storeByteRange16(d.data + od[u][0], u32x4{w[0], w[1], w[2], w[3]}, lo, hi);
                                 continue;
                             }
                         }
