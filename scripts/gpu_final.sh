@@ -17,7 +17,7 @@ step() {  # name, limit, command...
     tail -n 3 "$O/$name.log"
     return $rc
 }
-B="python3 bench.py --no-cpu-baseline --no-copy-peak"   # the default steps / warm-up of the bench line
+B="python3 bench.py --no-cpu-baseline --no-copy-peak --no-config4"   # the default steps / warm-up of the bench line
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1
 step pytest_gpu 900 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread || exit 1
 step bench 300 python bench.py || exit 1

@@ -134,6 +134,27 @@ def test_brick_decompose_parity(fmt, dims, brick, neg, pos):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("aligned", [1, 2])
+@pytest.mark.parametrize("fmt", [4, 5, 7])
+@pytest.mark.parametrize("dims,brick,neg,pos", LAYOUTS[1:4] + LAYOUTS[6:])
+def test_brick_decompose_aligned_lds_pieces(fmt, dims, brick, neg, pos, aligned):
+    """The staged copy with its row-end words (knob decompose.aligned_lds = 1) or every word
+    (= 2) written to LDS as naturally aligned pieces instead of unaligned 16-B writes / per-voxel
+    loops: the same bricks as the oracle."""
+    rng = np.random.default_rng(fmt * 100 + sum(dims) + aligned)
+    codes = rand_codes(rng, fmt, dims[::-1])
+    assert lib.vktHipSetTuningKnob(b"decompose.aligned_lds", aligned) == 0
+    try:
+        err, got = gpu_decompose(codes, fmt, (0.0, 1.0), brick, neg, pos)
+    finally:
+        assert lib.vktHipSetTuningKnob(b"decompose.aligned_lds", -1) == 0
+    assert err == vkt.NoError, vkt.last_error()
+    ref = ob.brick_decompose(ob.Volume(codes, fmt), brick, neg, pos)
+    for idx, v in ref.items():
+        np.testing.assert_array_equal(got[idx], v.codes, err_msg=f"brick {idx}")
+
+
+@pytest.mark.gpu
 def test_reference_example_decompose():
     """src/examples/Decompose.c:16-88: Fill(.1) on 120x66x49 UInt8, 16^3 bricks with halo 1 --
     every brick voxel (halos clamped at the border) holds the code of 0.1."""

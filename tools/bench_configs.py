@@ -109,6 +109,10 @@ def main():
     ap.add_argument("--big", action="store_true", help="include 2048^3 cases (~50 GB of HBM)")
     ap.add_argument("--only", default="", help="run only cases whose group name contains this")
     args = ap.parse_args()
+    for kv in filter(None, os.environ.get("VKT_KNOBS", "").split(",")):   # "name=value,..." for PMC runs
+        k, v = kv.split("=")
+        if lib.vktHipSetTuningKnob(k.encode(), int(v)) != 0:
+            raise RuntimeError(_lib.last_error())
     torch.cuda.set_device(0)
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
@@ -385,6 +389,58 @@ def main():
             report(f"decompose BrickDecompose 1024^3 UInt16 -> {bs}^3 bricks halo {halo} (back-to-back calls)",
                    ms, 4 * vox, vox)
             del arr, V
+        ep.device = vkt.ExecutionPolicy.Device_CPU
+        vkt.SetThreadExecutionPolicy(ep)
+    if want("decab"):
+        # in-process A/B of the staged copy's LDS writes (knob decompose.aligned_lds: 0 unaligned
+        # 16-B words + per-voxel row ends, 1 row-end words as aligned pieces, 2 every word)
+        import volkit_amd.volkit as vkt
+        ep = vkt.GetThreadExecutionPolicy()
+        ep.device = vkt.ExecutionPolicy.Device_GPU
+        vkt.SetThreadExecutionPolicy(ep)
+        n = 1024
+        V = vkt.StructuredVolume(n, n, n, vkt.DataFormat_UInt16)
+        vkt.Synthesize(V, 77)
+        ab = {}
+        for bs, halo in ((32, (1, 1, 1)), (64, (1, 1, 1)), (128, (0, 0, 0)), (256, (1, 1, 1))):
+            arr = vkt.Array3D_StructuredVolume()
+            b3, h3 = vkt.Vec3i(bs, bs, bs), vkt.Vec3i(*halo)
+            vkt.BrickDecomposeResize(arr, V, b3, h3, h3)
+            vox = sum(arr[(i, j, k)].getSizeInBytes() // 2 for k in range(arr.dims().z)
+                      for j in range(arr.dims().y) for i in range(arr.dims().x))
+            for rnd in range(3):
+                for kv in ((0, 5), (1, 5), (0, 6), (1, 6), (0, 8)):   # (aligned_lds, stage_words)
+                    lib.vktHipSetTuningKnob(b"decompose.aligned_lds", kv[0])
+                    lib.vktHipSetTuningKnob(b"decompose.stage_words", kv[1])
+                    ab.setdefault((bs, halo, kv, vox), []).append(
+                        pipelined(lambda: vkt.BrickDecompose(arr, V, b3, h3, h3), R))
+            del arr
+        lib.vktHipSetTuningKnob(b"decompose.aligned_lds", -1)
+        lib.vktHipSetTuningKnob(b"decompose.stage_words", -1)
+        for (bs, halo, kv, vox), ts in sorted(ab.items()):
+            ts.sort()
+            report(f"decab BrickDecompose 1024^3 UInt16 -> {bs}^3 bricks halo {halo} aligned_lds={kv[0]} "
+                   f"stage_words={kv[1]} "
+                   f"(back-to-back, median of 3 rounds, spread {ts[0]:.4f}-{ts[-1]:.4f})", ts[1], 4 * vox, vox)
+        del V
+        ep.device = vkt.ExecutionPolicy.Device_CPU
+        vkt.SetThreadExecutionPolicy(ep)
+    if want("decpmc"):
+        # one case for PMC passes (VKT_KNOBS picks the variant): 32^3 bricks + halo 1
+        import volkit_amd.volkit as vkt
+        ep = vkt.GetThreadExecutionPolicy()
+        ep.device = vkt.ExecutionPolicy.Device_GPU
+        vkt.SetThreadExecutionPolicy(ep)
+        V = vkt.StructuredVolume(1024, 1024, 1024, vkt.DataFormat_UInt16)
+        vkt.Synthesize(V, 77)
+        arr = vkt.Array3D_StructuredVolume()
+        b3, h3 = vkt.Vec3i(32, 32, 32), vkt.Vec3i(1, 1, 1)
+        vkt.BrickDecomposeResize(arr, V, b3, h3, h3)
+        vox = sum(arr[(i, j, k)].getSizeInBytes() // 2 for k in range(arr.dims().z)
+                  for j in range(arr.dims().y) for i in range(arr.dims().x))
+        report("decpmc BrickDecompose 1024^3 UInt16 -> 32^3 bricks halo 1", timed(
+            lambda: vkt.BrickDecompose(arr, V, b3, h3, h3), R), 4 * vox, vox)
+        del arr, V
         ep.device = vkt.ExecutionPolicy.Device_CPU
         vkt.SetThreadExecutionPolicy(ep)
     if want("reduce"):

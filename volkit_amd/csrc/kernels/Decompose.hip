@@ -86,6 +86,64 @@ namespace hipk
             reinterpret_cast<uint32_t*>(lds)[voxel] = code;
     }
 
+    // Bytes [lo, hi) of the 16-B word v to LDS bytes [a, a + hi - lo) as naturally aligned
+    // 1/2/4/8/16-B writes (leading pieces align the LDS address, trailing pieces finish): no
+    // unaligned LDS write and no per-voxel loop.  (Knob decompose.aligned_lds: 1 for the partial
+    // words at row ends, 2 for every word.)
+    __device__ __forceinline__ void ldsStoreRange(uint8_t* lds, int32_t a, u32x4 v, int lo, int hi)
+    {
+        uint64_t const q0 = static_cast<uint64_t>(v.x) | static_cast<uint64_t>(v.y) << 32;
+        uint64_t const q1 = static_cast<uint64_t>(v.z) | static_cast<uint64_t>(v.w) << 32;
+        auto at = [&](int b) -> uint64_t {   // the (up to) 8 bytes of v starting at byte b
+            uint64_t const l = (b & 8) ? q1 : q0, h = (b & 8) ? 0ull : q1;
+            uint32_t const sh = static_cast<uint32_t>(b & 7) * 8u;
+            return sh ? (l >> sh) | (h << (64u - sh)) : l;
+        };
+        int b = lo, n = hi - lo;
+        if (n == 16 && (a & 15) == 0)
+        {
+            *reinterpret_cast<u32x4*>(lds + a) = v;
+            return;
+        }
+        if ((a & 1) && n >= 1)
+        {
+            lds[a] = static_cast<uint8_t>(at(b));
+            a += 1; b += 1; n -= 1;
+        }
+        if ((a & 2) && n >= 2)
+        {
+            *reinterpret_cast<uint16_t*>(lds + a) = static_cast<uint16_t>(at(b));
+            a += 2; b += 2; n -= 2;
+        }
+        if ((a & 4) && n >= 4)
+        {
+            *reinterpret_cast<uint32_t*>(lds + a) = static_cast<uint32_t>(at(b));
+            a += 4; b += 4; n -= 4;
+        }
+        if ((a & 8) && n >= 8)
+        {
+            *reinterpret_cast<uint64_t*>(lds + a) = at(b);
+            a += 8; b += 8; n -= 8;
+        }
+        if (n >= 8)
+        {
+            *reinterpret_cast<uint64_t*>(lds + a) = at(b);
+            a += 8; b += 8; n -= 8;
+        }
+        if (n >= 4)
+        {
+            *reinterpret_cast<uint32_t*>(lds + a) = static_cast<uint32_t>(at(b));
+            a += 4; b += 4; n -= 4;
+        }
+        if (n >= 2)
+        {
+            *reinterpret_cast<uint16_t*>(lds + a) = static_cast<uint16_t>(at(b));
+            a += 2; b += 2; n -= 2;
+        }
+        if (n >= 1)
+            lds[a] = static_cast<uint8_t>(at(b));
+    }
+
     // LDS-staged copy of one chunk (kBrickChunk 16-byte items = the dst voxels [vStart, vEnd)
     // of a brick stored contiguously).  Phase 1: the rows the chunk touches are read as
     // 16-byte-ALIGNED source words (the hot path: one global_load_dwordx4 per lane) and
@@ -95,9 +153,9 @@ namespace hipk
     // reads, one aligned 16-byte global store per item.  The byte shifting is done by LDS
     // addressing instead of VALU funnel shifts (a 128-bit shift per lane made the kernel VALU
     // bound: 256^3 bricks + halo 1 took 1.15 ms vs 0.75 ms without halo; staged: 0.83 ms).
-    template <int BPV>
+    template <int BPV, int kStageWords>
     __device__ __forceinline__ void brickStaged(BrickDesc const& d, uint32_t base, uint8_t const* src, int32_t sdx,
-                                                int32_t sdy, int32_t sdz)
+                                                int32_t sdy, int32_t sdz, int32_t alignedLds)
     {
         constexpr int32_t V = 16 / BPV;
         __shared__ u32x4 tile[kBrickChunk];   // 16 KiB
@@ -146,7 +204,20 @@ namespace hipk
             if (!w.live)
                 return;
             if (w.whole && w.x0 >= lo && w.x0 + V <= hi && w.li >= 0 && w.li + V <= chunkVox)
-                reinterpret_cast<Unaligned16*>(lds + w.li * BPV)->v = w.v;
+            {
+                if (alignedLds >= 2)
+                    ldsStoreRange(lds, w.li * BPV, w.v, 0, 16);
+                else
+                    reinterpret_cast<Unaligned16*>(lds + w.li * BPV)->v = w.v;
+            }
+            else if (w.whole && alignedLds >= 1)
+            {
+                // the voxels of the word inside the row span and the chunk, as aligned pieces
+                int32_t const k0 = max(max(lo - w.x0, -w.li), 0);
+                int32_t const k1 = min(min(hi - w.x0, chunkVox - w.li), V);
+                if (k1 > k0)
+                    ldsStoreRange(lds, (w.li + k0) * BPV, w.v, k0 * BPV, k1 * BPV);
+            }
             else
             {
 #pragma unroll
@@ -157,8 +228,8 @@ namespace hipk
             }
         };
         // all loads of the first kStageWords rounds in flight before the first LDS write (a
-        // load -> wait -> write loop serialises the memory latency per round)
-        constexpr int kStageWords = 5;
+        // load -> wait -> write loop serialises the memory latency per round; the words left
+        // over after them cost the workgroup a second memory latency)
         Word words[kStageWords];
 #pragma unroll
         for (int k = 0; k < kStageWords; ++k)
@@ -214,10 +285,10 @@ namespace hipk
         }
     }
 
-    template <int BPV>
+    template <int BPV, int kStageWords>
     __global__ __launch_bounds__(kBlock) void brickCopyKernel(BrickDesc const* bricks, FastDiv chunksPerBrick,
                                                              FastDiv groupSize, uint8_t const* src, int32_t sdx,
-                                                             int32_t sdy, int32_t sdz)
+                                                             int32_t sdy, int32_t sdz, int32_t alignedLds)
     {
         constexpr int32_t V = 16 / BPV;
         // blockIdx = (group, chunk, brick in group): consecutive workgroups copy the same rows
@@ -236,7 +307,7 @@ namespace hipk
             return;   // border bricks are smaller than the largest one
         if (d.linear)
         {
-            brickStaged<BPV>(d, base, src, sdx, sdy, sdz);
+            brickStaged<BPV, kStageWords>(d, base, src, sdx, sdy, sdz, alignedLds);
             return;
         }
         uint64_t const pitchY = static_cast<uint64_t>(d.dimX);
@@ -453,15 +524,32 @@ vktError vktHipBrickDecompose(vktHipVolumeView_t source, vktHipBrickRange_t cons
             ++run;
         FastDiv const fdg = makeFastDiv(static_cast<uint32_t>(nFast % run == 0 ? run : 1));
         unsigned const g = static_cast<unsigned>(blocks);
+        int32_t const alignedLds = static_cast<int32_t>(rt::knob(rt::Knob::DecomposeAlignedLds));
+        // words staged per thread: enough that a chunk's source words are all in flight at once
+        // (one memory latency per workgroup): a 16-KiB chunk of 32^3 bricks + halo 1 (68-B rows)
+        // reads ~1450 aligned words = 5.7 per thread.  In-process A/B (profiles/r03/decompose_ab.jsonl,
+        // back-to-back calls): 32^3 + halo 1.256 -> 1.211 ms with 6, 1.218 ms with 8; 64^3 + halo,
+        // 128^3 and 256^3 + halo unchanged within 1 %
+        int64_t const sw = rt::knob(rt::Knob::DecomposeStageWords);
+        auto launch = [&](auto bpvC, auto swC) {
+            constexpr int B = decltype(bpvC)::value, W = decltype(swC)::value;
+            hipLaunchKernelGGL((brickCopyKernel<B, W>), dim3(g), dim3(kBlock), 0, s, dev, fdc, fdg, source.data,
+                               source.dimX, source.dimY, source.dimZ, alignedLds);
+        };
+        auto bySw = [&](auto bpvC) {
+            if (sw <= 5)
+                launch(bpvC, std::integral_constant<int, 5>{});
+            else if (sw == 6)
+                launch(bpvC, std::integral_constant<int, 6>{});
+            else
+                launch(bpvC, std::integral_constant<int, 8>{});
+        };
         if (bpv == 1)
-            hipLaunchKernelGGL(brickCopyKernel<1>, dim3(g), dim3(kBlock), 0, s, dev, fdc, fdg, source.data, source.dimX,
-                               source.dimY, source.dimZ);
+            bySw(std::integral_constant<int, 1>{});
         else if (bpv == 2)
-            hipLaunchKernelGGL(brickCopyKernel<2>, dim3(g), dim3(kBlock), 0, s, dev, fdc, fdg, source.data, source.dimX,
-                               source.dimY, source.dimZ);
+            bySw(std::integral_constant<int, 2>{});
         else
-            hipLaunchKernelGGL(brickCopyKernel<4>, dim3(g), dim3(kBlock), 0, s, dev, fdc, fdg, source.data, source.dimX,
-                               source.dimY, source.dimZ);
+            bySw(std::integral_constant<int, 4>{});
         VKT_HIP_TRY(hipGetLastError());
         VKT_HIP_TRY(hipEventRecord(st.done, s));
         st.pending = true;

@@ -137,8 +137,9 @@ namespace hipk
         // voxels) and a 64-B aligned destination (every sector inside it).  Copies, conversions
         // and fills only: in-process A/B on an 800^3 sub-box of 1024^3 at x0 = 100, CopyRange
         // 0.480 -> 0.422 ms, SafeSumRange 0.627 -> 0.649 ms (its partly read source sectors stay).
-        // Not for UInt8: its per-item loop (8 B per lane) lost the batching of its loads to the
-        // conditional destination-chunk loads -- 800^3 sub-box copy x 0..800 0.250 -> 0.378 ms.
+        // Not for UInt8 here: its per-item loop (8 B per lane) lost the batching of its loads to
+        // the conditional destination-chunk loads -- 800^3 sub-box copy x 0..800 0.250 -> 0.378
+        // ms; UInt8 rows complete their sectors on the 16-voxel pair grid below.
         if (vec && p.g.padded && ns <= 1 && bpv != 1)
         {
             int64_t const bd = bpv;

@@ -84,6 +84,8 @@ namespace rt
         HistogramP16Step,              // 0: P16 threshold tests after each item, not each wave-step
         PointwiseU8Pairs,              // 0: UInt8 multi-row boxes keep the 8-voxel per-item loop
         RenderBricks,                  // 0: multi-scattering samples the dense volume, not an 8^3-brick copy
+        DecomposeAlignedLds,           // 1: partial words as aligned LDS pieces; 2: every word
+        DecomposeStageWords,           // source words per thread in flight in the staged copy (5, 6, 8)
         Count
     };
     int64_t knob(Knob k);
