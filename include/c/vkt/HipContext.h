@@ -1,3 +1,3 @@
-/* HIP context/backend API (design intent of reference include/c/vkt/CudaContext.h). */
+/* HIP context handles: vktHipContext* (reference include/c/vkt/CudaContext.h:17-65, for HIP streams). */
 #pragma once
 #include "../../volkit_hip.h"

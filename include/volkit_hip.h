@@ -50,8 +50,31 @@ VKTAPI vktError vktHipGetAsyncExecution(int32_t* async);
  * NULL restores the backend's own blocking stream. */
 VKTAPI vktError vktHipSetComputeStream(void* hipStream);
 VKTAPI vktError vktHipGetComputeStream(void** hipStream);
+/* Replace the side copy stream of migrate() / streams (NULL restores the backend's own). */
+VKTAPI vktError vktHipSetCopyStream(void* hipStream);
 VKTAPI vktError vktHipGetCopyStream(void** hipStream);
 VKTAPI vktError vktHipSynchronize(void);
+/* Context handles -- the reference's vktCudaContext API (include/c/vkt/CudaContext.h:17-65,
+ * declared there, defined nowhere) for HIP: a context holds numStreams streams (created
+ * blocking and owned by it, or the caller's via SetStream), a compute and a copy stream id and
+ * the async flag.  vktHipContextMakeCurrent(ctx) binds it to the backend (one HIP context per
+ * process): algorithms then run on streams[computeId], migrations on streams[copyId]; setters
+ * on the current context take effect at once.  MakeCurrent(NULL) and destroying the current
+ * context restore the backend's own streams.  A new context has 2 streams, compute 0, copy 1. */
+typedef struct vktHipContext_impl* vktHipContext;
+VKTAPI vktError vktHipContextCreate(vktHipContext* context);
+VKTAPI vktError vktHipContextDestroy(vktHipContext context);
+VKTAPI vktError vktHipContextMakeCurrent(vktHipContext context);
+VKTAPI vktError vktHipContextSetAsyncExecution(vktHipContext context, int32_t async);
+VKTAPI vktError vktHipContextGetAsyncExecution(vktHipContext context, int32_t* async);
+VKTAPI vktError vktHipContextSetNumStreams(vktHipContext context, int32_t numStreams);
+VKTAPI vktError vktHipContextGetNumStreams(vktHipContext context, int32_t* numStreams);
+VKTAPI vktError vktHipContextSetStream(vktHipContext context, int32_t streamId, void* hipStream);
+VKTAPI vktError vktHipContextGetStream(vktHipContext context, int32_t streamId, void** hipStream);
+VKTAPI vktError vktHipContextSetComputeStreamId(vktHipContext context, int32_t streamId);
+VKTAPI vktError vktHipContextGetComputeStreamId(vktHipContext context, int32_t* streamId);
+VKTAPI vktError vktHipContextSetCopyStreamId(vktHipContext context, int32_t streamId);
+VKTAPI vktError vktHipContextGetCopyStreamId(vktHipContext context, int32_t* streamId);
 /* Last HIP error string seen by the backend (thread-local), "" if none. */
 VKTAPI const char* vktHipGetLastErrorString(void);
 /* Milliseconds of the most recent kernel launched by the calling thread, measured with

@@ -206,6 +206,20 @@ SIGNATURES = {
     "vktHipSetComputeStream": (c_err, [C.c_void_p]),
     "vktHipGetComputeStream": (c_err, [P(C.c_void_p)]),
     "vktHipGetCopyStream": (c_err, [P(C.c_void_p)]),
+    "vktHipSetCopyStream": (c_err, [C.c_void_p]),
+    "vktHipContextCreate": (c_err, [P(C.c_void_p)]),
+    "vktHipContextDestroy": (c_err, [C.c_void_p]),
+    "vktHipContextMakeCurrent": (c_err, [C.c_void_p]),
+    "vktHipContextSetAsyncExecution": (c_err, [C.c_void_p, i32]),
+    "vktHipContextGetAsyncExecution": (c_err, [C.c_void_p, P(i32)]),
+    "vktHipContextSetNumStreams": (c_err, [C.c_void_p, i32]),
+    "vktHipContextGetNumStreams": (c_err, [C.c_void_p, P(i32)]),
+    "vktHipContextSetStream": (c_err, [C.c_void_p, i32, C.c_void_p]),
+    "vktHipContextGetStream": (c_err, [C.c_void_p, i32, P(C.c_void_p)]),
+    "vktHipContextSetComputeStreamId": (c_err, [C.c_void_p, i32]),
+    "vktHipContextGetComputeStreamId": (c_err, [C.c_void_p, P(i32)]),
+    "vktHipContextSetCopyStreamId": (c_err, [C.c_void_p, i32]),
+    "vktHipContextGetCopyStreamId": (c_err, [C.c_void_p, P(i32)]),
     "vktHipSynchronize": (c_err, []),
     "vktHipGetLastErrorString": (C.c_char_p, []),
     "vktHipSetKernelTiming": (c_err, [i32]),

@@ -14,7 +14,9 @@
 #include <cstdlib>
 #include <cstring>
 #include <iostream>
+#include <algorithm>
 #include <mutex>
+#include <vector>
 
 namespace vkt
 {
@@ -31,6 +33,8 @@ namespace rt
             hipStream_t userCompute = nullptr;
             bool userStreamSet = false;
             hipStream_t copy = nullptr;
+            hipStream_t userCopy = nullptr;
+            bool userCopySet = false;
             std::atomic<int> async{1};
             std::atomic<int> timing{0};
         };
@@ -94,7 +98,7 @@ namespace rt
         Context& c = ctx();
         std::lock_guard<std::mutex> lock(c.mutex);
         initLocked(c);
-        return c.copy;
+        return c.userCopySet ? c.userCopy : c.copy;
     }
 
     bool asyncExecution() { return ctx().async.load() != 0; }
@@ -304,6 +308,16 @@ vktError vktHipGetComputeStream(void** stream)
     return vktNoError;
 }
 
+vktError vktHipSetCopyStream(void* stream)
+{
+    rt::Context& c = rt::ctx();
+    std::lock_guard<std::mutex> lock(c.mutex);
+    rt::initLocked(c);
+    c.userCopy = static_cast<hipStream_t>(stream);
+    c.userCopySet = stream != nullptr;
+    return vktNoError;
+}
+
 vktError vktHipGetCopyStream(void** stream)
 {
     if (stream == nullptr)
@@ -386,6 +400,199 @@ vktError vktHipSetTuningKnob(char const* name, int64_t value)
 vktError vktHipReportError(char const* message)
 {
     return rt::fail(message != nullptr ? message : "vktHipReportError");
+}
+
+// ---- context handles (reference include/c/vkt/CudaContext.h:17-65, declared there and never
+//      defined): a set of streams + the async flag, bound to the process's backend by
+//      vktHipContextMakeCurrent (one HIP context per process -- the library's model).
+struct vktHipContext_impl
+{
+    std::vector<hipStream_t> streams;
+    std::vector<char> owned;   // created by the context (destroyed with it)
+    int32_t compute = 0, copy = 0;
+    int32_t async = 1;
+};
+
+namespace
+{
+    std::mutex gCtxMutex;
+    vktHipContext gCurrent = nullptr;
+
+    vktError applyLocked(vktHipContext c)
+    {
+        vktHipSetAsyncExecution(c->async);
+        vktError e = vktHipSetComputeStream(c->streams[static_cast<size_t>(c->compute)]);
+        return e != vktNoError ? e : vktHipSetCopyStream(c->streams[static_cast<size_t>(c->copy)]);
+    }
+
+    vktError resize(vktHipContext c, int32_t n)
+    {
+        (void)vkt::rt::device();   // streams of the library's device
+        while (static_cast<int32_t>(c->streams.size()) > n)
+        {
+            if (c->owned.back())
+                VKT_HIP_TRY(hipStreamDestroy(c->streams.back()));
+            c->streams.pop_back();
+            c->owned.pop_back();
+        }
+        while (static_cast<int32_t>(c->streams.size()) < n)
+        {
+            hipStream_t s = nullptr;
+            // blocking streams, like the library's own (ordered with the legacy NULL stream)
+            VKT_HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamDefault));
+            c->streams.push_back(s);
+            c->owned.push_back(1);
+        }
+        c->compute = std::min(c->compute, n - 1);
+        c->copy = std::min(c->copy, n - 1);
+        return vktNoError;
+    }
+
+    vktError changed(vktHipContext c)
+    {
+        return c == gCurrent ? applyLocked(c) : vktNoError;
+    }
+} // namespace
+
+vktError vktHipContextCreate(vktHipContext* context)
+{
+    if (context == nullptr)
+        return rt::fail("vktHipContextCreate: null pointer");
+    auto* c = new vktHipContext_impl;
+    std::lock_guard<std::mutex> lock(gCtxMutex);
+    vktError e = resize(c, 2);   // stream 0: compute, stream 1: copy
+    if (e != vktNoError)
+    {
+        delete c;
+        *context = nullptr;
+        return e;
+    }
+    c->copy = 1;
+    *context = c;
+    return vktNoError;
+}
+
+vktError vktHipContextDestroy(vktHipContext context)
+{
+    if (context == nullptr)
+        return vktNoError;
+    std::lock_guard<std::mutex> lock(gCtxMutex);
+    if (context == gCurrent)
+    {
+        // back to the library's own streams before the context's streams go away
+        VKT_HIP_TRY(hipStreamSynchronize(rt::computeStream()));
+        VKT_HIP_TRY(hipStreamSynchronize(rt::copyStream()));
+        vktHipSetComputeStream(nullptr);
+        vktHipSetCopyStream(nullptr);
+        gCurrent = nullptr;
+    }
+    for (size_t i = 0; i < context->streams.size(); ++i)
+        if (context->owned[i])
+            (void)hipStreamDestroy(context->streams[i]);
+    delete context;
+    return vktNoError;
+}
+
+vktError vktHipContextMakeCurrent(vktHipContext context)
+{
+    std::lock_guard<std::mutex> lock(gCtxMutex);
+    gCurrent = context;
+    if (context == nullptr)
+    {
+        vktHipSetComputeStream(nullptr);
+        return vktHipSetCopyStream(nullptr);
+    }
+    return applyLocked(context);
+}
+
+vktError vktHipContextSetAsyncExecution(vktHipContext context, int32_t async)
+{
+    if (context == nullptr)
+        return rt::fail("vktHipContextSetAsyncExecution: null context");
+    std::lock_guard<std::mutex> lock(gCtxMutex);
+    context->async = async != 0;
+    return changed(context);
+}
+
+vktError vktHipContextGetAsyncExecution(vktHipContext context, int32_t* async)
+{
+    if (context == nullptr || async == nullptr)
+        return rt::fail("vktHipContextGetAsyncExecution: null pointer");
+    *async = context->async;
+    return vktNoError;
+}
+
+vktError vktHipContextSetNumStreams(vktHipContext context, int32_t numStreams)
+{
+    if (context == nullptr || numStreams < 1)
+        return rt::fail("vktHipContextSetNumStreams: null context or numStreams < 1");
+    std::lock_guard<std::mutex> lock(gCtxMutex);
+    vktError e = resize(context, numStreams);
+    return e != vktNoError ? e : changed(context);
+}
+
+vktError vktHipContextGetNumStreams(vktHipContext context, int32_t* numStreams)
+{
+    if (context == nullptr || numStreams == nullptr)
+        return rt::fail("vktHipContextGetNumStreams: null pointer");
+    *numStreams = static_cast<int32_t>(context->streams.size());
+    return vktNoError;
+}
+
+vktError vktHipContextSetStream(vktHipContext context, int32_t streamId, void* stream)
+{
+    if (context == nullptr || streamId < 0 || streamId >= static_cast<int32_t>(context->streams.size()) || !stream)
+        return rt::fail("vktHipContextSetStream: null context / stream or stream id out of range");
+    std::lock_guard<std::mutex> lock(gCtxMutex);
+    size_t const i = static_cast<size_t>(streamId);
+    if (context->owned[i])
+        VKT_HIP_TRY(hipStreamDestroy(context->streams[i]));
+    context->streams[i] = static_cast<hipStream_t>(stream);
+    context->owned[i] = 0;   // the caller's stream: not destroyed by the context
+    return changed(context);
+}
+
+vktError vktHipContextGetStream(vktHipContext context, int32_t streamId, void** stream)
+{
+    if (context == nullptr || stream == nullptr || streamId < 0 ||
+        streamId >= static_cast<int32_t>(context->streams.size()))
+        return rt::fail("vktHipContextGetStream: null pointer or stream id out of range");
+    *stream = context->streams[static_cast<size_t>(streamId)];
+    return vktNoError;
+}
+
+vktError vktHipContextSetComputeStreamId(vktHipContext context, int32_t streamId)
+{
+    if (context == nullptr || streamId < 0 || streamId >= static_cast<int32_t>(context->streams.size()))
+        return rt::fail("vktHipContextSetComputeStreamId: null context or stream id out of range");
+    std::lock_guard<std::mutex> lock(gCtxMutex);
+    context->compute = streamId;
+    return changed(context);
+}
+
+vktError vktHipContextGetComputeStreamId(vktHipContext context, int32_t* streamId)
+{
+    if (context == nullptr || streamId == nullptr)
+        return rt::fail("vktHipContextGetComputeStreamId: null pointer");
+    *streamId = context->compute;
+    return vktNoError;
+}
+
+vktError vktHipContextSetCopyStreamId(vktHipContext context, int32_t streamId)
+{
+    if (context == nullptr || streamId < 0 || streamId >= static_cast<int32_t>(context->streams.size()))
+        return rt::fail("vktHipContextSetCopyStreamId: null context or stream id out of range");
+    std::lock_guard<std::mutex> lock(gCtxMutex);
+    context->copy = streamId;
+    return changed(context);
+}
+
+vktError vktHipContextGetCopyStreamId(vktHipContext context, int32_t* streamId)
+{
+    if (context == nullptr || streamId == nullptr)
+        return rt::fail("vktHipContextGetCopyStreamId: null pointer");
+    *streamId = context->copy;
+    return vktNoError;
 }
 
 } // extern "C"
