@@ -247,6 +247,47 @@ def test_uint8_pair16_rows(lib, o, x0, dims):
         assert L.vktHipSetTuningKnob(b"pointwise.merge_sectors", -1) == 0
 
 
+@pytest.mark.parametrize("sx", [0, 1, 5, 8, 15, 16, 37, 63])
+def test_uint8_wide_general_path(lib, o, sx):
+    """UInt8 boxes on the general path with 16-voxel items (GenGeom::wide: one 16-B store per
+    lane, byte-range or sector-merged row ends): source x phases against destination x phases,
+    widths around the 16- and 64-voxel units, gaps that allow / forbid sector completion (192-
+    voxel rows, 64-B pitches), clamped sources past x = 0 / dimX - 1, and SafeSum / Diff with an
+    x dstOffset -- knob pointwise.u8_wide on and off, vs the oracle."""
+    rng = np.random.default_rng(300 + sx)
+    dims = (5, 24, 192)
+    src = rand_codes(rng, 4, dims)
+    src2 = rand_codes(rng, 4, dims)
+    dinit = rand_codes(rng, 4, dims)
+    from volkit_amd._lib import lib as L
+    try:
+        for on, mk in ((1, -1), (1, 2), (0, -1)):
+            assert L.vktHipSetTuningKnob(b"pointwise.u8_wide", on) == 0
+            assert L.vktHipSetTuningKnob(b"pointwise.merge_sectors", mk) == 0
+            for dx in (0, 3, 16, 17, 64):
+                for w in (1, 7, 16, 17, 33, 64, 100, 128, 150):
+                    if dx + w > 192:
+                        continue
+                    first, last = (sx, 2, 1), (sx + w, 22, 5)
+                    if sx + w <= 192:
+                        copy_case(lib, o, 4, 4, (0.0, 1.0), (0.0, 1.0), src, dinit, first, last, (dx, 1, 0),
+                                  what=f"copy wide={on} sx={sx} dx={dx} w={w}")
+                    # clamped source: starts left of x = 0
+                    copy_case(lib, o, 4, 4, (0.0, 1.0), (0.0, 1.0), src, dinit, (sx - 20, -1, 0), (sx - 20 + w, 22, 4),
+                              (dx, 0, 1), what=f"clamped copy wide={on} sx={sx} dx={dx} w={w}")
+                    if sx + w <= 192 and dx + w <= 192:
+                        off = (dx - sx, 1, 0)
+                        for op in ("SafeSum", "Diff"):
+                            da, db, dd = Dev(src, 4), Dev(src2, 4), Dev(dinit, 4)
+                            assert L.vktHipArithmeticRange(OPS.index(op), dd.view, da.view, db.view, vec(first),
+                                                           vec(last), vec(off)) == 0, last_error()
+                            ref = o.arith(op, [4] * 3, [(0.0, 1.0)] * 3, src, src2, dinit.copy(), first, last, off)
+                            assert_codes_equal(dd.read(), ref, 4, f"{op} wide={on} sx={sx} dx={dx} w={w}")
+    finally:
+        assert L.vktHipSetTuningKnob(b"pointwise.u8_wide", -1) == 0
+        assert L.vktHipSetTuningKnob(b"pointwise.merge_sectors", -1) == 0
+
+
 def test_general_knob_matches_scalar_kernel(lib, o):
     """The same phase-shifted and clamped cases through the general path and, with the knob
     off, through the per-voxel kernel: both equal the oracle."""

@@ -239,6 +239,37 @@ def main():
                    f"spread {ts[0]:.4f}-{ts[-1]:.4f})",
                    ts[1], (2 if op == "CopyRange" else 3) * nv, nv)
         free(A, B, D)
+    if want("u8gen"):
+        # UInt8 general path (source and destination at different phases, 800^3 sub-box of
+        # 1024^3): in-process A/B of 16-voxel items (knob pointwise.u8_wide)
+        m = 1024
+        A, B, D = alloc((m,) * 3, 4, seed=1), alloc((m,) * 3, 4, seed=2), alloc((m,) * 3, 4)
+        ab = {}
+        cases = (("CopyRange x0=100 -> dst 0", lambda: lib.vktHipCopyRange(D, A, Vec3i_t(100, 100, 100),
+                                                                          Vec3i_t(900, 900, 900), o), 2),
+                 ("CopyRange x0=100 -> dst x0=3", lambda: lib.vktHipCopyRange(D, A, Vec3i_t(100, 100, 100),
+                                                                             Vec3i_t(900, 900, 900),
+                                                                             Vec3i_t(3, 100, 100)), 2),
+                 ("CopyRange 1021x1024^2 x0=3 -> 0", lambda: lib.vktHipCopyRange(D, A, Vec3i_t(3, 0, 0),
+                                                                                Vec3i_t(m, m, m), o), 2),
+                 ("SumRange 800^3 x0=100 dstOffset x=-97", lambda: lib.vktHipArithmeticRange(
+                     0, D, A, B, Vec3i_t(100, 100, 100), Vec3i_t(900, 900, 900), Vec3i_t(-97, 0, 0)), 3))
+        kvs = ((0, -1), (1, -1), (1, 2))   # (u8_wide, merge_sectors)
+        for rnd in range(3):
+            for kv in kvs:
+                lib.vktHipSetTuningKnob(b"pointwise.u8_wide", kv[0])
+                lib.vktHipSetTuningKnob(b"pointwise.merge_sectors", kv[1])
+                for lab, fn, _ in cases:
+                    ab.setdefault((lab, kv), []).append(timed(fn, R))
+        lib.vktHipSetTuningKnob(b"pointwise.u8_wide", -1)
+        lib.vktHipSetTuningKnob(b"pointwise.merge_sectors", -1)
+        for lab, fn, streams in cases:
+            nv = 1021 * m * m if "1021" in lab else 800 ** 3
+            for kv in kvs:
+                ts = sorted(ab[(lab, kv)])
+                report(f"u8gen {lab} UInt8 u8_wide={kv[0]} merge_sectors={kv[1]} (median of 3 rounds, "
+                       f"spread {ts[0]:.4f}-{ts[-1]:.4f})", ts[1], streams * nv, nv)
+        free(A, B, D)
     if want("weakspots"):
         # the kernels furthest below the roofline in round 1 (VERDICT r1 "What's weak" 5)
         m = 1024

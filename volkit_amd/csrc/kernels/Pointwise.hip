@@ -267,7 +267,10 @@ namespace hipk
             // (copies, conversions and fills only: a 3-stream op measured slower on this path, an
             // 800^3 SafeSumRange sub-box of 1024^3 at x0 = 100: 0.589 -> 0.634 ms; the aligned
             // path completes sectors on its own, above)
-            bool merge = ns <= 1 && gg.fast && rt::knob(rt::Knob::PointwiseMergeSectors) != 0 &&
+            // (3-stream ops on 1-byte voxels: knob value 2, for the A/B of the 16-voxel items)
+            bool const u8 = p.d.bpv == 1 && (ns < 1 || p.s1.bpv == 1) && (ns < 2 || p.s2.bpv == 1);
+            bool merge = (ns <= 1 || (u8 && rt::knob(rt::Knob::PointwiseMergeSectors) == 2)) && gg.fast &&
+                         rt::knob(rt::Knob::PointwiseMergeSectors) != 0 &&
                          reinterpret_cast<uintptr_t>(p.d.data) % 64 == 0 && dBytes % 64 == 0;
             if (merge && vny > 1)
                 merge = (p.d.sy - vnx) * static_cast<int64_t>(bd) >= 64;
@@ -284,6 +287,23 @@ namespace hipk
                 gg.fast = gg.fast && gg.fast32;
                 gg.merge = gg.fast;
                 gg.divCpr = makeFastDiv(static_cast<uint32_t>(gg.cpr));
+            }
+        }
+        // 1-byte voxels in every operand on the 32-bit path: 16-voxel items (Pointwise.hpp
+        // pointwiseGenSpanFast16); the same row cover and sector completion in 16-voxel units
+        gg.wide = 0;
+        if (gg.fast && p.d.bpv == 1 && (ns < 1 || p.s1.bpv == 1) && (ns < 2 || p.s2.bpv == 1) &&
+            rt::knob(rt::Knob::PointwiseU8Wide) != 0)
+        {
+            uint64_t const cpr = gg.merge ? static_cast<uint64_t>(((vnx + 63 + 63) / 64) * 64 / 16)
+                                          : static_cast<uint64_t>((vnx + 30) / 16);
+            uint64_t const items = rows * cpr;
+            if (items < (1ull << 32))
+            {
+                gg.wide = 1;
+                gg.cpr = cpr;
+                gg.items = items;
+                gg.dph = static_cast<int32_t>(reinterpret_cast<uintptr_t>(p.d.data) & 15u);
             }
         }
         gg.divCpr = makeFastDiv(static_cast<uint32_t>(gg.cpr));

@@ -590,6 +590,8 @@ namespace hipk
         int32_t merge;           // complete the 64-B sectors at the row ends (fast path only)
         int32_t sv;              // voxels per 64-B sector (64 / BD)
         int32_t dph64;           // (d.data / BD) mod sv
+        int32_t wide;            // every operand UInt8-sized, fast path: 16-voxel items
+                                 // (pointwiseGenSpanFast16; cpr / dph in 16-voxel units)
         FastDiv divCpr, divVny;
     };
 
@@ -1173,6 +1175,162 @@ namespace hipk
         }
     }
 
+    // ---- 1-byte voxels, 16-voxel items (GenGeom::wide) ------------------------------------
+    // The 8-voxel items above move 8 B per lane for UInt8 and load a 32-B window per 8 B of
+    // output; here an item is 16 destination voxels (one aligned 16-B store), its source window
+    // the two aligned 16-B words around the 16 source bytes (the same window layout as UInt16
+    // items, Window<1> with hi up to 16) shifted once into 4 dwords.  Row ends: byte-range
+    // stores (storeByteRange16), or with sector completion the whole 16 B merged with the
+    // destination's own bytes (mergeBytes16).
+    __device__ __forceinline__ bool genInterior16(Operand const& o, int32_t x)
+    {
+        return !o.clamp || (o.origin[0] + x >= 0 && o.origin[0] + x + 16 <= o.dims[0]);
+    }
+
+    __device__ __forceinline__ void shiftWindow16(Window<1> const& win, uint32_t (&out)[4])
+    {
+        uint32_t a[6], b[5];
+        shiftSel(win.w, a, (win.s & 8u) != 0, 2, std::make_index_sequence<6>{});
+        shiftSel(a, b, (win.s & 4u) != 0, 1, std::make_index_sequence<5>{});
+        shiftAlign(b, out, win.s & 3u, std::make_index_sequence<4>{});
+    }
+
+    template <int NS, int U, class F>
+    __device__ __forceinline__ void pointwiseGenSpanFast16(Operand const& d, Operand const& s1, Operand const& s2,
+                                                           GenGeom const& g, uint32_t beg, uint32_t end, F const& f)
+    {
+        constexpr bool kPass = NS == 1 && std::is_same<F, PassF>::value;
+        FastOp const fd = fastOp(d), f1 = fastOp(s1), f2 = fastOp(s2);
+        int32_t const vnx = static_cast<int32_t>(g.vnx);
+        Window<1> wa[U];
+        Window<1> wb[NS >= 2 ? U : 1];
+        u32x4 dd[U];
+        int32_t xs[U];
+        int64_t od[U];   // signed: the first item of a row at voxel 0 of a destination view that
+                         // starts inside a 16-B word lies before the view (only its row bytes are stored)
+        uint32_t js[U], ks[U];
+        bool win[U], border[U], pad[U];
+        // items start on 16-voxel (merge: 64-B sector) boundaries of the destination
+        uint32_t const unitMask = g.merge ? 63u : 15u;
+        uint32_t const dphU = static_cast<uint32_t>(g.merge ? g.dph64 : g.dph);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+        {
+            uint32_t const it = beg + threadIdx.x + static_cast<uint32_t>(u) * kVecBlock;
+            bool live = it < end;
+            uint32_t const ii = live ? it : beg;
+            uint32_t const rr = fdiv(ii, g.divCpr);
+            uint32_t const c = ii - rr * g.divCpr.d;
+            uint32_t const k = fdiv(rr, g.divVny);
+            uint32_t const j = rr - k * g.divVny.d;
+            js[u] = j;
+            ks[u] = k;
+            uint32_t const dr = fd.base + __umul24(k, fd.sz) + __umul24(j, fd.sy);
+            int32_t const ps = static_cast<int32_t>((dphU + dr) & unitMask);
+            int32_t const x = static_cast<int32_t>(16 * c) - ps;
+            xs[u] = x;
+            od[u] = static_cast<int64_t>(dr) + x;
+            int32_t const rowEnd = static_cast<int32_t>((static_cast<uint32_t>(ps + vnx) + unitMask) & ~unitMask) - ps;
+            live = live && x < (g.merge ? rowEnd : vnx);
+            bool const boxPart = x + 16 > 0 && x < vnx;
+            pad[u] = live && !boxPart;
+            bool const clampX = NS >= 1 && g.anyClamp && !(genInterior16(s1, x) && (NS < 2 || genInterior16(s2, x)));
+            border[u] = live && boxPart && clampX;
+            win[u] = live && boxPart && !clampX;
+            int32_t const lo = x < 0 ? -x : 0;
+            int32_t const hi = x + 16 > vnx ? vnx - x : 16;
+            if (win[u])
+            {
+                if constexpr (NS >= 1)
+                    loadWindowFast<1>(f1, static_cast<uint32_t>(fastRowStart(s1, f1, j, k)) + static_cast<uint32_t>(x),
+                                      lo, hi, wa[u]);
+                if constexpr (NS >= 2)
+                    loadWindowFast<1>(f2, static_cast<uint32_t>(fastRowStart(s2, f2, j, k)) + static_cast<uint32_t>(x),
+                                      lo, hi, wb[u]);
+            }
+            if (g.merge && live && !(x >= 0 && x + 16 <= vnx))
+                dd[u] = *reinterpret_cast<u32x4 const*>(d.data + od[u]);
+        }
+        auto result = [&](uint32_t const (&a)[4], uint32_t const (&b)[4], u32x4& rd) {
+            if constexpr (kPass)
+                rd = u32x4{a[0], a[1], a[2], a[3]};
+            else
+            {
+                uint32_t r[4];
+#pragma unroll
+                for (int m = 0; m < 4; ++m)
+                {
+                    uint32_t o = 0;
+#pragma unroll
+                    for (int v = 0; v < 4; ++v)
+                        o |= (f(NS >= 1 ? (a[m] >> (8 * v)) & 0xFFu : 0u, NS >= 2 ? (b[m] >> (8 * v)) & 0xFFu : 0u) & 0xFFu)
+                             << (8 * v);
+                    r[m] = o;
+                }
+                rd = u32x4{r[0], r[1], r[2], r[3]};
+            }
+        };
+        auto store = [&](int u, u32x4 const& rd) {
+            uint8_t* const p = d.data + od[u];
+            int32_t const x = xs[u];
+            if (x >= 0 && x + 16 <= vnx)
+                __builtin_nontemporal_store(rd, reinterpret_cast<u32x4*>(p));
+            else
+            {
+                int const lo = x < 0 ? -x : 0;
+                int const hi = x + 16 > vnx ? vnx - x : 16;
+                if (g.merge)
+                    __builtin_nontemporal_store(mergeBytes16(rd, dd[u], lo, hi), reinterpret_cast<u32x4*>(p));
+                else
+                    storeByteRange16(p, rd, lo, hi);
+            }
+        };
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+        {
+            if (pad[u])
+            {
+                __builtin_nontemporal_store(dd[u], reinterpret_cast<u32x4*>(d.data + od[u]));   // sector completion
+                continue;
+            }
+            if (!win[u])
+                continue;
+            uint32_t a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
+            if constexpr (NS >= 1)
+                shiftWindow16(wa[u], a);
+            if constexpr (NS >= 2)
+                shiftWindow16(wb[u], b);
+            u32x4 rd;
+            result(a, b, rd);
+            store(u, rd);
+        }
+        if (!g.anyClamp)
+            return;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+        {
+            if (!border[u])
+                continue;
+            // clamped x border: voxel by voxel (rows as genRowStart: x = 0 of the volume row)
+            int64_t r10 = 0, r20 = 0;
+            int64_t const q1 = genRowStart(s1, js[u], ks[u], r10);
+            int64_t q2 = 0;
+            if constexpr (NS >= 2)
+                q2 = genRowStart(s2, js[u], ks[u], r20);
+            uint32_t a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int v = 0; v < 16; ++v)
+            {
+                a[v / 4] |= genLoadOne<1>(s1, q1, r10, xs[u] + v) << (8 * (v % 4));
+                if constexpr (NS >= 2)
+                    b[v / 4] |= genLoadOne<1>(s2, q2, r20, xs[u] + v) << (8 * (v % 4));
+            }
+            u32x4 rd;
+            result(a, b, rd);
+            store(u, rd);
+        }
+    }
+
     template <int NS, int BD, int B1, int B2, int U, class F>
     __global__ __launch_bounds__(kVecBlock) void pointwiseGenKernel(Operand d, Operand s1, Operand s2, GenGeom g, F f,
                                                                    uint64_t qBase, uint64_t qEnd)
@@ -1184,6 +1342,14 @@ namespace hipk
             if (beg >= g.items)
                 break;
             uint64_t const end = beg + kQ < g.items ? beg + kQ : g.items;
+            if constexpr (BD == 1 && B1 == 1 && (NS < 2 || B2 == 1))
+            {
+                if (g.wide)
+                {
+                    pointwiseGenSpanFast16<NS, U>(d, s1, s2, g, static_cast<uint32_t>(beg), static_cast<uint32_t>(end), f);
+                    continue;
+                }
+            }
             if (g.fast)
                 pointwiseGenSpanFast<NS, BD, B1, B2, U>(d, s1, s2, g, static_cast<uint32_t>(beg),
                                                         static_cast<uint32_t>(end), f);

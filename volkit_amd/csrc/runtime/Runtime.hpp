@@ -86,6 +86,7 @@ namespace rt
         RenderBricks,                  // 0: multi-scattering samples the dense volume, not an 8^3-brick copy
         DecomposeAlignedLds,           // 1: partial words as aligned LDS pieces; 2: every word
         DecomposeStageWords,           // source words per thread in flight in the staged copy (5, 6, 8)
+        PointwiseU8Wide,               // 0: UInt8 general-path boxes keep 8-voxel items
         Count
     };
     int64_t knob(Knob k);
