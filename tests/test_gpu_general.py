@@ -247,6 +247,41 @@ def test_uint8_pair16_rows(lib, o, x0, dims):
         assert L.vktHipSetTuningKnob(b"pointwise.merge_sectors", -1) == 0
 
 
+@pytest.mark.parametrize("fmt", [7, 6])
+@pytest.mark.parametrize("x0", [0, 1, 3, 4, 7, 9, 13, 16])
+def test_float32_padded_rows_halves(lib, o, fmt, x0):
+    """4-byte multi-row boxes with padded rows through the contiguous-lane shape
+    (Geom::f32halves: every 16-B half of an item stored whole, as its row's dwords, or merged
+    with the destination's own dwords under 64-B sector completion): row phases x0 mod 8 and
+    widths covering every tail, on 64-voxel rows (256-B pitches: completion where the gaps
+    allow) -- Copy / SafeSum / Diff, knobs pointwise.f32_halves and merge_sectors on and off."""
+    rng = np.random.default_rng(400 + x0 + fmt)
+    dims = (5, 36, 64)
+    a = rand_codes(rng, fmt, dims)
+    b = rand_codes(rng, fmt, dims)
+    dinit = rand_codes(rng, fmt, dims)
+    from volkit_amd._lib import lib as L
+    try:
+        for on, mk in ((1, -1), (1, 0), (0, -1)):
+            assert L.vktHipSetTuningKnob(b"pointwise.f32_halves", on) == 0
+            assert L.vktHipSetTuningKnob(b"pointwise.merge_sectors", mk) == 0
+            for w in (1, 2, 3, 4, 5, 8, 11, 16, 17, 29, 33, 48, 64 - x0):
+                if x0 + w > 64:
+                    continue
+                first, last = (x0, 1, 0), (x0 + w, 35, 5)
+                for op in ("SafeSum", "Diff"):
+                    da, db, dd = Dev(a, fmt), Dev(b, fmt), Dev(dinit, fmt)
+                    assert L.vktHipArithmeticRange(OPS.index(op), dd.view, da.view, db.view, vec(first), vec(last),
+                                                   vec((0, 0, 0))) == 0, last_error()
+                    ref = o.arith(op, [fmt] * 3, [(0.0, 1.0)] * 3, a, b, dinit.copy(), first, last, (0, 0, 0))
+                    assert_codes_equal(dd.read(), ref, fmt, f"{op} halves={on} merge={mk} x0={x0} w={w}")
+                copy_case(lib, o, fmt, fmt, (0.0, 1.0), (0.0, 1.0), a, dinit, first, last, first, 0, 0,
+                          f"copy halves={on} merge={mk} x0={x0} w={w}")
+    finally:
+        assert L.vktHipSetTuningKnob(b"pointwise.f32_halves", -1) == 0
+        assert L.vktHipSetTuningKnob(b"pointwise.merge_sectors", -1) == 0
+
+
 @pytest.mark.parametrize("sx", [0, 1, 5, 8, 15, 16, 37, 63])
 def test_uint8_wide_general_path(lib, o, sx):
     """UInt8 boxes on the general path with 16-voxel items (GenGeom::wide: one 16-B store per

@@ -270,6 +270,27 @@ def main():
                 report(f"u8gen {lab} UInt8 u8_wide={kv[0]} merge_sectors={kv[1]} (median of 3 rounds, "
                        f"spread {ts[0]:.4f}-{ts[-1]:.4f})", ts[1], streams * nv, nv)
         free(A, B, D)
+    if want("f32ab"):
+        # Float32 padded multi-row boxes: contiguous-lane halves (knob pointwise.f32_halves) A/B
+        m = 1024
+        A, B, D = alloc((m,) * 3, 7, seed=1), alloc((m,) * 3, 7, seed=2), alloc((m,) * 3, 7)
+        boxes = (("x0=100", Vec3i_t(100, 100, 100), Vec3i_t(900, 900, 900)),
+                 ("x0=101", Vec3i_t(101, 100, 100), Vec3i_t(901, 900, 900)))
+        ab = {}
+        for rnd in range(3):
+            for kv in (0, 1):
+                lib.vktHipSetTuningKnob(b"pointwise.f32_halves", kv)
+                for lab, f0, f1 in boxes:
+                    ab.setdefault(("CopyRange", lab, kv), []).append(
+                        timed(lambda: lib.vktHipCopyRange(D, A, f0, f1, f0), R))
+                    ab.setdefault(("SumRange", lab, kv), []).append(
+                        timed(lambda: lib.vktHipArithmeticRange(0, D, A, B, f0, f1, o), R))
+        lib.vktHipSetTuningKnob(b"pointwise.f32_halves", -1)
+        for (op, lab, kv), ts in sorted(ab.items()):
+            ts.sort()
+            report(f"f32ab {op} 800^3 sub-box {lab} Float32 f32_halves={kv} (median of 3 rounds, "
+                   f"spread {ts[0]:.4f}-{ts[-1]:.4f})", ts[1], (8 if op == "CopyRange" else 12) * 800 ** 3, 800 ** 3)
+        free(A, B, D)
     if want("chunked"):
         # metric pipeline scheduled in plane chunks (Resample of dst planes [z0, z1), then SumRange
         # over the same planes): does the R chunk come back from the Infinity Cache?

@@ -174,6 +174,7 @@ namespace hipk
         // Needs every operand's rows at one phase mod 16 and 16-B aligned row supersets (the
         // superset stays inside the volume's row: pitches are multiples of 16).
         p.g.pair16 = 0;
+        p.g.f32halves = bpv == 4 && rt::knob(rt::Knob::PointwiseF32Halves) != 0 ? 1 : 0;
         if (vec && bpv == 1 && vny * vnz > 1 && rt::knob(rt::Knob::PointwisePaddedRows) != 0 &&
             rt::knob(rt::Knob::PointwiseU8Pairs) != 0)
         {

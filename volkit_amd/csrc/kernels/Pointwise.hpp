@@ -65,6 +65,8 @@ namespace hipk
         // its first item starts 16-B aligned, so items 2l, 2l + 1 form one 16-B access (the
         // contiguous-lane shape below) with byte-range stores at the row ends
         int32_t pair16;
+        // 4-byte voxels: padded rows take the contiguous-lane shape too, 16-B halves masked
+        int32_t f32halves;
     };
 
     struct PassF;   // PointwiseOps.hpp: dst = source code (bytewise CopyRange)
@@ -306,16 +308,19 @@ namespace hipk
             // byte-range stores at the row ends (the per-item loop stored a straddling item
             // voxel by voxel: 8 byte stores, 24 store instructions per wave on an 800^3 sub-box
             // at x0 = 100, 0.30 of 8 TB/s)
-            bool const shape = MODE == 0 || (BPV == 4 && !g.padded) || (BPV == 1 && g.pair16);
+            // Float32 rows with padded edges: each 16-B half (4 voxels) is stored whole, as its
+            // row's dwords (storeByteRange16), or -- sector completion -- merged with the
+            // destination's own dwords (g.f32halves, knob pointwise.f32_halves)
+            bool const shape = MODE == 0 || (BPV == 4 && (!g.padded || g.f32halves)) || (BPV == 1 && g.pair16);
             if (end - beg == kQ && shape && aligned(d) && (NS < 1 || aligned(s1)) && (NS < 2 || aligned(s2)))
             {
                 uint32_t a[kUnroll][8], b[kUnroll][8];
-                int64_t xr[kUnroll];
+                int64_t xr[kUnroll][2];   // row-relative x of the lane's access (Float32: of the half)
                 // voxel offsets (d, s1, s2) of the lane's 16-B access number q of block u
                 auto at = [&](int u, int q, uint64_t& od, uint64_t& o1, uint64_t& o2) {
                     uint64_t item;
                     uint64_t sub = 0;
-                    xr[u] = 0;
+                    xr[u][q] = 0;
                     if constexpr (BPV == 4)
                     {
                         item = beg + static_cast<uint64_t>(u) * 64u + 32u * static_cast<uint64_t>(q) + lane / 2;
@@ -323,7 +328,8 @@ namespace hipk
                     }
                     else
                         item = beg + static_cast<uint64_t>(u / 2) * 128u + 2u * lane;
-                    pointwiseVecItem<NS, BPV, MODE, F>(d, s1, s2, g, item, o1, o2, od, &xr[u], BPV == 1 ? 16 : 8);
+                    pointwiseVecItem<NS, BPV, MODE, F>(d, s1, s2, g, item, o1, o2, od, &xr[u][q], BPV == 1 ? 16 : 8);
+                    xr[u][q] += static_cast<int64_t>(sub);
                     od += sub;
                     o1 += sub;
                     o2 += sub;
@@ -371,13 +377,22 @@ namespace hipk
                 // UInt8 pairs with 64-B sector completion: a pair outside the box row (inside an
                 // end sector) or straddling its end is stored whole, its bytes outside the row
                 // being the destination's own
-                u32x4 own[kUnroll];
+                u32x4 own[kUnroll][2];
                 if constexpr (BPV == 1 && MODE != 0)
                 {
 #pragma unroll
                     for (int u = 0; u < kUnroll; u += 2)
-                        if (g.merge && (xr[u] < 0 || xr[u] + 16 > g.vnx))
-                            own[u] = *reinterpret_cast<u32x4 const*>(d.data + od[u][0]);
+                        if (g.merge && (xr[u][0] < 0 || xr[u][0] + 16 > g.vnx))
+                            own[u][0] = *reinterpret_cast<u32x4 const*>(d.data + od[u][0]);
+                }
+                if constexpr (BPV == 4 && MODE != 0)
+                {
+#pragma unroll
+                    for (int u = 0; u < kUnroll; ++u)
+#pragma unroll
+                        for (int q = 0; q < 2; ++q)
+                            if (g.merge && (xr[u][q] < 0 || xr[u][q] + 4 > g.vnx))
+                                own[u][q] = *reinterpret_cast<u32x4 const*>(d.data + od[u][q] * 4u);
                 }
                 uint32_t o[kUnroll][8];
 #pragma unroll
@@ -390,10 +405,29 @@ namespace hipk
                 {
                     if constexpr (BPV == 4)
                     {
-                        __builtin_nontemporal_store(u32x4{o[u][0], o[u][1], o[u][2], o[u][3]},
-                                                    reinterpret_cast<u32x4*>(d.data + od[u][0] * 4u));
-                        __builtin_nontemporal_store(u32x4{o[u][4], o[u][5], o[u][6], o[u][7]},
-                                                    reinterpret_cast<u32x4*>(d.data + od[u][1] * 4u));
+#pragma unroll
+                        for (int q = 0; q < 2; ++q)
+                        {
+                            u32x4 const v{o[u][4 * q], o[u][4 * q + 1], o[u][4 * q + 2], o[u][4 * q + 3]};
+                            uint8_t* const p = d.data + od[u][q] * 4u;
+                            if constexpr (MODE != 0)
+                            {
+                                int64_t const x = xr[u][q];
+                                if (g.padded && (x < 0 || x + 4 > g.vnx))
+                                {
+                                    // a half straddling or outside a row end: the row's dwords
+                                    int const lo = 4 * static_cast<int>(x < 0 ? (x < -4 ? 4 : -x) : 0);
+                                    int const hi = 4 * static_cast<int>(g.vnx - x < 4 ? (g.vnx - x < 0 ? 0 : g.vnx - x) : 4);
+                                    if (g.merge)
+                                        __builtin_nontemporal_store(mergeBytes16(v, own[u][q], lo, hi),
+                                                                    reinterpret_cast<u32x4*>(p));
+                                    else if (hi > lo)
+                                        storeByteRange16(p, v, lo, hi);
+                                    continue;
+                                }
+                            }
+                            __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
+                        }
                     }
                     else if (u % 2 == 0)
                     {
@@ -407,7 +441,7 @@ namespace hipk
                         }
                         if constexpr (MODE != 0)
                         {
-                            int64_t const x = xr[u];
+                            int64_t const x = xr[u][0];
                             if (g.padded && (x < 0 || x + 16 > g.vnx))
                             {
                                 // the pair straddles a row end (or, merging, lies in an end
@@ -416,7 +450,7 @@ namespace hipk
                                 int const lo = x < 0 ? static_cast<int>(x < -16 ? 16 : -x) : 0;
                                 int const hi = g.vnx - x < 16 ? static_cast<int>(g.vnx - x < 0 ? 0 : g.vnx - x) : 16;
                                 if (g.merge)
-                                    __builtin_nontemporal_store(mergeBytes16(u32x4{w[0], w[1], w[2], w[3]}, own[u], lo, hi),
+                                    __builtin_nontemporal_store(mergeBytes16(u32x4{w[0], w[1], w[2], w[3]}, own[u][0], lo, hi),
                                                                 reinterpret_cast<u32x4*>(d.data + od[u][0]));
                                 else
                                     storeByteRange16(d.data + od[u][0], u32x4{w[0], w[1], w[2], w[3]}, lo, hi);

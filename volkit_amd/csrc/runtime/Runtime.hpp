@@ -87,6 +87,7 @@ namespace rt
         DecomposeAlignedLds,           // 1: partial words as aligned LDS pieces; 2: every word
         DecomposeStageWords,           // source words per thread in flight in the staged copy (5, 6, 8)
         PointwiseU8Wide,               // 0: UInt8 general-path boxes keep 8-voxel items
+        PointwiseF32Halves,            // 0: padded 4-byte rows keep the per-item loop
         Count
     };
     int64_t knob(Knob k);
