@@ -282,22 +282,24 @@ def test_float32_padded_rows_halves(lib, o, fmt, x0):
         assert L.vktHipSetTuningKnob(b"pointwise.merge_sectors", -1) == 0
 
 
+@pytest.mark.parametrize("fmt", [4, 7, 6])
 @pytest.mark.parametrize("sx", [0, 1, 5, 8, 15, 16, 37, 63])
-def test_uint8_wide_general_path(lib, o, sx):
-    """UInt8 boxes on the general path with 16-voxel items (GenGeom::wide: one 16-B store per
-    lane, byte-range or sector-merged row ends): source x phases against destination x phases,
-    widths around the 16- and 64-voxel units, gaps that allow / forbid sector completion (192-
-    voxel rows, 64-B pitches), clamped sources past x = 0 / dimX - 1, and SafeSum / Diff with an
-    x dstOffset -- knob pointwise.u8_wide on and off, vs the oracle."""
-    rng = np.random.default_rng(300 + sx)
+def test_uint8_wide_general_path(lib, o, sx, fmt):
+    """1- and 4-byte boxes on the general path with 16-B items (GenGeom::wide: 16 UInt8 / 4
+    Float32 voxels, one 16-B store per lane, byte-range or sector-merged row ends): source x
+    phases against destination x phases, widths around the item and 64-B units, gaps that allow /
+    forbid sector completion (192-voxel rows), clamped sources past x = 0 / dimX - 1, and SafeSum /
+    Diff with an x dstOffset -- knob pointwise.u8_wide / f32_wide on and off, vs the oracle."""
+    rng = np.random.default_rng(300 + sx + fmt)
     dims = (5, 24, 192)
-    src = rand_codes(rng, 4, dims)
-    src2 = rand_codes(rng, 4, dims)
-    dinit = rand_codes(rng, 4, dims)
+    src = rand_codes(rng, fmt, dims)
+    src2 = rand_codes(rng, fmt, dims)
+    dinit = rand_codes(rng, fmt, dims)
+    knob_name = b"pointwise.u8_wide" if fmt == 4 else b"pointwise.f32_wide"
     from volkit_amd._lib import lib as L
     try:
         for on, mk in ((1, -1), (1, 2), (0, -1)):
-            assert L.vktHipSetTuningKnob(b"pointwise.u8_wide", on) == 0
+            assert L.vktHipSetTuningKnob(knob_name, on) == 0
             assert L.vktHipSetTuningKnob(b"pointwise.merge_sectors", mk) == 0
             for dx in (0, 3, 16, 17, 64):
                 for w in (1, 7, 16, 17, 33, 64, 100, 128, 150):
@@ -305,21 +307,21 @@ def test_uint8_wide_general_path(lib, o, sx):
                         continue
                     first, last = (sx, 2, 1), (sx + w, 22, 5)
                     if sx + w <= 192:
-                        copy_case(lib, o, 4, 4, (0.0, 1.0), (0.0, 1.0), src, dinit, first, last, (dx, 1, 0),
+                        copy_case(lib, o, fmt, fmt, (0.0, 1.0), (0.0, 1.0), src, dinit, first, last, (dx, 1, 0),
                                   what=f"copy wide={on} sx={sx} dx={dx} w={w}")
                     # clamped source: starts left of x = 0
-                    copy_case(lib, o, 4, 4, (0.0, 1.0), (0.0, 1.0), src, dinit, (sx - 20, -1, 0), (sx - 20 + w, 22, 4),
-                              (dx, 0, 1), what=f"clamped copy wide={on} sx={sx} dx={dx} w={w}")
+                    copy_case(lib, o, fmt, fmt, (0.0, 1.0), (0.0, 1.0), src, dinit, (sx - 20, -1, 0),
+                              (sx - 20 + w, 22, 4), (dx, 0, 1), what=f"clamped copy wide={on} sx={sx} dx={dx} w={w}")
                     if sx + w <= 192 and dx + w <= 192:
                         off = (dx - sx, 1, 0)
                         for op in ("SafeSum", "Diff"):
-                            da, db, dd = Dev(src, 4), Dev(src2, 4), Dev(dinit, 4)
+                            da, db, dd = Dev(src, fmt), Dev(src2, fmt), Dev(dinit, fmt)
                             assert L.vktHipArithmeticRange(OPS.index(op), dd.view, da.view, db.view, vec(first),
                                                            vec(last), vec(off)) == 0, last_error()
-                            ref = o.arith(op, [4] * 3, [(0.0, 1.0)] * 3, src, src2, dinit.copy(), first, last, off)
-                            assert_codes_equal(dd.read(), ref, 4, f"{op} wide={on} sx={sx} dx={dx} w={w}")
+                            ref = o.arith(op, [fmt] * 3, [(0.0, 1.0)] * 3, src, src2, dinit.copy(), first, last, off)
+                            assert_codes_equal(dd.read(), ref, fmt, f"{op} wide={on} sx={sx} dx={dx} w={w}")
     finally:
-        assert L.vktHipSetTuningKnob(b"pointwise.u8_wide", -1) == 0
+        assert L.vktHipSetTuningKnob(knob_name, -1) == 0
         assert L.vktHipSetTuningKnob(b"pointwise.merge_sectors", -1) == 0
 
 

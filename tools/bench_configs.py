@@ -239,11 +239,13 @@ def main():
                    f"spread {ts[0]:.4f}-{ts[-1]:.4f})",
                    ts[1], (2 if op == "CopyRange" else 3) * nv, nv)
         free(A, B, D)
-    if want("u8gen"):
-        # UInt8 general path (source and destination at different phases, 800^3 sub-box of
-        # 1024^3): in-process A/B of 16-voxel items (knob pointwise.u8_wide)
+    for gname, gfmt, gb, gknob in (("u8gen", 4, 1, b"pointwise.u8_wide"), ("f32gen", 7, 4, b"pointwise.f32_wide")):
+        if not want(gname):
+            continue
+        # general path (source and destination at different phases, 800^3 sub-box of 1024^3):
+        # in-process A/B of 16-B items (knob pointwise.u8_wide / f32_wide)
         m = 1024
-        A, B, D = alloc((m,) * 3, 4, seed=1), alloc((m,) * 3, 4, seed=2), alloc((m,) * 3, 4)
+        A, B, D = alloc((m,) * 3, gfmt, seed=1), alloc((m,) * 3, gfmt, seed=2), alloc((m,) * 3, gfmt)
         ab = {}
         cases = (("CopyRange x0=100 -> dst 0", lambda: lib.vktHipCopyRange(D, A, Vec3i_t(100, 100, 100),
                                                                           Vec3i_t(900, 900, 900), o), 2),
@@ -254,21 +256,21 @@ def main():
                                                                                 Vec3i_t(m, m, m), o), 2),
                  ("SumRange 800^3 x0=100 dstOffset x=-97", lambda: lib.vktHipArithmeticRange(
                      0, D, A, B, Vec3i_t(100, 100, 100), Vec3i_t(900, 900, 900), Vec3i_t(-97, 0, 0)), 3))
-        kvs = ((0, -1), (1, -1), (1, 2))   # (u8_wide, merge_sectors)
+        kvs = ((0, -1), (1, -1), (1, 2))   # (wide, merge_sectors)
         for rnd in range(3):
             for kv in kvs:
-                lib.vktHipSetTuningKnob(b"pointwise.u8_wide", kv[0])
+                lib.vktHipSetTuningKnob(gknob, kv[0])
                 lib.vktHipSetTuningKnob(b"pointwise.merge_sectors", kv[1])
                 for lab, fn, _ in cases:
                     ab.setdefault((lab, kv), []).append(timed(fn, R))
-        lib.vktHipSetTuningKnob(b"pointwise.u8_wide", -1)
+        lib.vktHipSetTuningKnob(gknob, -1)
         lib.vktHipSetTuningKnob(b"pointwise.merge_sectors", -1)
         for lab, fn, streams in cases:
             nv = 1021 * m * m if "1021" in lab else 800 ** 3
             for kv in kvs:
                 ts = sorted(ab[(lab, kv)])
-                report(f"u8gen {lab} UInt8 u8_wide={kv[0]} merge_sectors={kv[1]} (median of 3 rounds, "
-                       f"spread {ts[0]:.4f}-{ts[-1]:.4f})", ts[1], streams * nv, nv)
+                report(f"{gname} {lab} fmt={gfmt} wide={kv[0]} merge_sectors={kv[1]} (median of 3 rounds, "
+                       f"spread {ts[0]:.4f}-{ts[-1]:.4f})", ts[1], streams * nv * gb, nv)
         free(A, B, D)
     if want("f32ab"):
         # Float32 padded multi-row boxes: contiguous-lane halves (knob pointwise.f32_halves) A/B

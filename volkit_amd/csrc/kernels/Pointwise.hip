@@ -290,21 +290,28 @@ namespace hipk
                 gg.divCpr = makeFastDiv(static_cast<uint32_t>(gg.cpr));
             }
         }
-        // 1-byte voxels in every operand on the 32-bit path: 16-voxel items (Pointwise.hpp
-        // pointwiseGenSpanFast16); the same row cover and sector completion in 16-voxel units
+        // 1- or 4-byte voxels in every operand on the 32-bit path: 16-B items of 16 / B voxels
+        // (Pointwise.hpp pointwiseGenSpanFast16); the same row cover and sector completion in
+        // units of 16 / B voxels
         gg.wide = 0;
-        if (gg.fast && p.d.bpv == 1 && (ns < 1 || p.s1.bpv == 1) && (ns < 2 || p.s2.bpv == 1) &&
-            rt::knob(rt::Knob::PointwiseU8Wide) != 0)
         {
-            uint64_t const cpr = gg.merge ? static_cast<uint64_t>(((vnx + 63 + 63) / 64) * 64 / 16)
-                                          : static_cast<uint64_t>((vnx + 30) / 16);
-            uint64_t const items = rows * cpr;
-            if (items < (1ull << 32))
+            uint32_t const B = p.d.bpv;
+            bool const same = (ns < 1 || p.s1.bpv == B) && (ns < 2 || p.s2.bpv == B);
+            bool const on = B == 1 ? rt::knob(rt::Knob::PointwiseU8Wide) != 0
+                                   : B == 4 && rt::knob(rt::Knob::PointwiseF32Wide) != 0;
+            if (gg.fast && same && on)
             {
-                gg.wide = 1;
-                gg.cpr = cpr;
-                gg.items = items;
-                gg.dph = static_cast<int32_t>(reinterpret_cast<uintptr_t>(p.d.data) & 15u);
+                int64_t const V = 16 / B, sv = 64 / B;
+                uint64_t const cpr = gg.merge ? static_cast<uint64_t>(((vnx + sv - 1 + sv - 1) / sv) * sv / V)
+                                              : static_cast<uint64_t>((vnx + 2 * V - 2) / V);
+                uint64_t const items = rows * cpr;
+                if (items < (1ull << 32))
+                {
+                    gg.wide = 1;
+                    gg.cpr = cpr;
+                    gg.items = items;
+                    gg.dph = static_cast<int32_t>((reinterpret_cast<uintptr_t>(p.d.data) / B) & static_cast<uint64_t>(V - 1));
+                }
             }
         }
         gg.divCpr = makeFastDiv(static_cast<uint32_t>(gg.cpr));

@@ -624,8 +624,8 @@ namespace hipk
         int32_t merge;           // complete the 64-B sectors at the row ends (fast path only)
         int32_t sv;              // voxels per 64-B sector (64 / BD)
         int32_t dph64;           // (d.data / BD) mod sv
-        int32_t wide;            // every operand UInt8-sized, fast path: 16-voxel items
-                                 // (pointwiseGenSpanFast16; cpr / dph in 16-voxel units)
+        int32_t wide;            // every operand 1 or every operand 4 B/voxel, fast path: 16-B items
+                                 // (pointwiseGenSpanFast16; cpr / dph in 16/B-voxel units)
         FastDiv divCpr, divVny;
     };
 
@@ -1209,16 +1209,18 @@ namespace hipk
         }
     }
 
-    // ---- 1-byte voxels, 16-voxel items (GenGeom::wide) ------------------------------------
-    // The 8-voxel items above move 8 B per lane for UInt8 and load a 32-B window per 8 B of
-    // output; here an item is 16 destination voxels (one aligned 16-B store), its source window
-    // the two aligned 16-B words around the 16 source bytes (the same window layout as UInt16
-    // items, Window<1> with hi up to 16) shifted once into 4 dwords.  Row ends: byte-range
-    // stores (storeByteRange16), or with sector completion the whole 16 B merged with the
-    // destination's own bytes (mergeBytes16).
-    __device__ __forceinline__ bool genInterior16(Operand const& o, int32_t x)
+    // ---- 16-B items for 1- and 4-byte voxels (GenGeom::wide) ------------------------------
+    // The 8-voxel items above move 8 B per lane for UInt8 (and load a 32-B window per 8 B of
+    // output) and 32 B per lane for 4-byte voxels (each store instruction every other 16 B of
+    // 2 KiB).  Here an item is 16 destination bytes whatever the voxel size -- 16 voxels of
+    // UInt8, 4 of Float32: one aligned 16-B store per lane, its source window the two aligned
+    // 16-B words around the 16 source bytes (the UInt16 item's window) shifted once into four
+    // dwords.  Row ends: byte-range stores (storeByteRange16), or with sector completion the
+    // whole 16 B merged with the destination's own bytes (mergeBytes16).
+    template <int B>
+    __device__ __forceinline__ bool genInteriorW(Operand const& o, int32_t x)
     {
-        return !o.clamp || (o.origin[0] + x >= 0 && o.origin[0] + x + 16 <= o.dims[0]);
+        return !o.clamp || (o.origin[0] + x >= 0 && o.origin[0] + x + 16 / B <= o.dims[0]);
     }
 
     __device__ __forceinline__ void shiftWindow16(Window<1> const& win, uint32_t (&out)[4])
@@ -1229,10 +1231,33 @@ namespace hipk
         shiftAlign(b, out, win.s & 3u, std::make_index_sequence<4>{});
     }
 
-    template <int NS, int U, class F>
+    // the two aligned words around voxels [lo, hi) of the 16 / B voxels at `voxel` (as
+    // loadWindowFast, two words for any voxel size)
+    template <int B>
+    __device__ __forceinline__ void loadWindowFast2(FastOp const& f, uint32_t voxel, int32_t lo, int32_t hi,
+                                                    Window<1>& win)
+    {
+        uint32_t const bo = voxel * B + static_cast<uint32_t>(f.mis);
+        uint32_t const fo = (bo + static_cast<uint32_t>(lo * B)) & ~15u;
+        uint32_t const lw = (bo + static_cast<uint32_t>(hi * B - 1)) & ~15u;
+        int32_t const dw = static_cast<int32_t>((bo & ~15u) - fo);
+        int32_t const span = static_cast<int32_t>(lw - fo);
+        win.s = bo & 15u;
+        auto word = [&](int i) {
+            int32_t const o = min(max(dw + 16 * i, 0), span);
+            return *reinterpret_cast<u32x4 const*>(f.abase + (fo + static_cast<uint32_t>(o)));
+        };
+        u32x4 const v0 = word(0);
+        u32x4 const v1 = word(1);
+        win.w[0] = v0.x; win.w[1] = v0.y; win.w[2] = v0.z; win.w[3] = v0.w;
+        win.w[4] = v1.x; win.w[5] = v1.y; win.w[6] = v1.z; win.w[7] = v1.w;
+    }
+
+    template <int NS, int B, int U, class F>
     __device__ __forceinline__ void pointwiseGenSpanFast16(Operand const& d, Operand const& s1, Operand const& s2,
                                                            GenGeom const& g, uint32_t beg, uint32_t end, F const& f)
     {
+        constexpr int V = 16 / B;   // voxels per item
         constexpr bool kPass = NS == 1 && std::is_same<F, PassF>::value;
         FastOp const fd = fastOp(d), f1 = fastOp(s1), f2 = fastOp(s2);
         int32_t const vnx = static_cast<int32_t>(g.vnx);
@@ -1244,8 +1269,8 @@ namespace hipk
                          // starts inside a 16-B word lies before the view (only its row bytes are stored)
         uint32_t js[U], ks[U];
         bool win[U], border[U], pad[U];
-        // items start on 16-voxel (merge: 64-B sector) boundaries of the destination
-        uint32_t const unitMask = g.merge ? 63u : 15u;
+        // items start on V-voxel (merge: 64-B sector) boundaries of the destination
+        uint32_t const unitMask = g.merge ? static_cast<uint32_t>(64 / B - 1) : static_cast<uint32_t>(V - 1);
         uint32_t const dphU = static_cast<uint32_t>(g.merge ? g.dph64 : g.dph);
 #pragma unroll
         for (int u = 0; u < U; ++u)
@@ -1261,29 +1286,29 @@ namespace hipk
             ks[u] = k;
             uint32_t const dr = fd.base + __umul24(k, fd.sz) + __umul24(j, fd.sy);
             int32_t const ps = static_cast<int32_t>((dphU + dr) & unitMask);
-            int32_t const x = static_cast<int32_t>(16 * c) - ps;
+            int32_t const x = static_cast<int32_t>(V * c) - ps;
             xs[u] = x;
             od[u] = static_cast<int64_t>(dr) + x;
             int32_t const rowEnd = static_cast<int32_t>((static_cast<uint32_t>(ps + vnx) + unitMask) & ~unitMask) - ps;
             live = live && x < (g.merge ? rowEnd : vnx);
-            bool const boxPart = x + 16 > 0 && x < vnx;
+            bool const boxPart = x + V > 0 && x < vnx;
             pad[u] = live && !boxPart;
-            bool const clampX = NS >= 1 && g.anyClamp && !(genInterior16(s1, x) && (NS < 2 || genInterior16(s2, x)));
+            bool const clampX = NS >= 1 && g.anyClamp && !(genInteriorW<B>(s1, x) && (NS < 2 || genInteriorW<B>(s2, x)));
             border[u] = live && boxPart && clampX;
             win[u] = live && boxPart && !clampX;
             int32_t const lo = x < 0 ? -x : 0;
-            int32_t const hi = x + 16 > vnx ? vnx - x : 16;
+            int32_t const hi = x + V > vnx ? vnx - x : V;
             if (win[u])
             {
                 if constexpr (NS >= 1)
-                    loadWindowFast<1>(f1, static_cast<uint32_t>(fastRowStart(s1, f1, j, k)) + static_cast<uint32_t>(x),
-                                      lo, hi, wa[u]);
+                    loadWindowFast2<B>(f1, static_cast<uint32_t>(fastRowStart(s1, f1, j, k)) + static_cast<uint32_t>(x),
+                                       lo, hi, wa[u]);
                 if constexpr (NS >= 2)
-                    loadWindowFast<1>(f2, static_cast<uint32_t>(fastRowStart(s2, f2, j, k)) + static_cast<uint32_t>(x),
-                                      lo, hi, wb[u]);
+                    loadWindowFast2<B>(f2, static_cast<uint32_t>(fastRowStart(s2, f2, j, k)) + static_cast<uint32_t>(x),
+                                       lo, hi, wb[u]);
             }
-            if (g.merge && live && !(x >= 0 && x + 16 <= vnx))
-                dd[u] = *reinterpret_cast<u32x4 const*>(d.data + od[u]);
+            if (g.merge && live && !(x >= 0 && x + V <= vnx))
+                dd[u] = *reinterpret_cast<u32x4 const*>(d.data + od[u] * B);
         }
         auto result = [&](uint32_t const (&a)[4], uint32_t const (&b)[4], u32x4& rd) {
             if constexpr (kPass)
@@ -1294,25 +1319,30 @@ namespace hipk
 #pragma unroll
                 for (int m = 0; m < 4; ++m)
                 {
-                    uint32_t o = 0;
+                    if constexpr (B == 4)
+                        r[m] = f(NS >= 1 ? a[m] : 0u, NS >= 2 ? b[m] : 0u);
+                    else
+                    {
+                        uint32_t o = 0;
 #pragma unroll
-                    for (int v = 0; v < 4; ++v)
-                        o |= (f(NS >= 1 ? (a[m] >> (8 * v)) & 0xFFu : 0u, NS >= 2 ? (b[m] >> (8 * v)) & 0xFFu : 0u) & 0xFFu)
-                             << (8 * v);
-                    r[m] = o;
+                        for (int v = 0; v < 4; ++v)
+                            o |= (f(NS >= 1 ? (a[m] >> (8 * v)) & 0xFFu : 0u, NS >= 2 ? (b[m] >> (8 * v)) & 0xFFu : 0u) &
+                                  0xFFu) << (8 * v);
+                        r[m] = o;
+                    }
                 }
                 rd = u32x4{r[0], r[1], r[2], r[3]};
             }
         };
         auto store = [&](int u, u32x4 const& rd) {
-            uint8_t* const p = d.data + od[u];
+            uint8_t* const p = d.data + od[u] * B;
             int32_t const x = xs[u];
-            if (x >= 0 && x + 16 <= vnx)
+            if (x >= 0 && x + V <= vnx)
                 __builtin_nontemporal_store(rd, reinterpret_cast<u32x4*>(p));
             else
             {
-                int const lo = x < 0 ? -x : 0;
-                int const hi = x + 16 > vnx ? vnx - x : 16;
+                int const lo = B * (x < 0 ? -x : 0);
+                int const hi = B * (x + V > vnx ? vnx - x : V);
                 if (g.merge)
                     __builtin_nontemporal_store(mergeBytes16(rd, dd[u], lo, hi), reinterpret_cast<u32x4*>(p));
                 else
@@ -1324,7 +1354,7 @@ namespace hipk
         {
             if (pad[u])
             {
-                __builtin_nontemporal_store(dd[u], reinterpret_cast<u32x4*>(d.data + od[u]));   // sector completion
+                __builtin_nontemporal_store(dd[u], reinterpret_cast<u32x4*>(d.data + od[u] * B));   // sector completion
                 continue;
             }
             if (!win[u])
@@ -1353,11 +1383,12 @@ namespace hipk
                 q2 = genRowStart(s2, js[u], ks[u], r20);
             uint32_t a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
 #pragma unroll
-            for (int v = 0; v < 16; ++v)
+            for (int v = 0; v < V; ++v)
             {
-                a[v / 4] |= genLoadOne<1>(s1, q1, r10, xs[u] + v) << (8 * (v % 4));
+                constexpr int kBits = 8 * B;
+                a[(v * B) / 4] |= genLoadOne<B>(s1, q1, r10, xs[u] + v) << ((v * kBits) % 32);
                 if constexpr (NS >= 2)
-                    b[v / 4] |= genLoadOne<1>(s2, q2, r20, xs[u] + v) << (8 * (v % 4));
+                    b[(v * B) / 4] |= genLoadOne<B>(s2, q2, r20, xs[u] + v) << ((v * kBits) % 32);
             }
             u32x4 rd;
             result(a, b, rd);
@@ -1376,11 +1407,12 @@ namespace hipk
             if (beg >= g.items)
                 break;
             uint64_t const end = beg + kQ < g.items ? beg + kQ : g.items;
-            if constexpr (BD == 1 && B1 == 1 && (NS < 2 || B2 == 1))
+            if constexpr ((BD == 1 || BD == 4) && B1 == BD && (NS < 2 || B2 == BD))
             {
                 if (g.wide)
                 {
-                    pointwiseGenSpanFast16<NS, U>(d, s1, s2, g, static_cast<uint32_t>(beg), static_cast<uint32_t>(end), f);
+                    pointwiseGenSpanFast16<NS, BD, U>(d, s1, s2, g, static_cast<uint32_t>(beg), static_cast<uint32_t>(end),
+                                                      f);
                     continue;
                 }
             }
@@ -1441,10 +1473,9 @@ namespace hipk
     };
 
     // General vector path launch (operand voxel sizes BD, B1, B2 fixed at compile time).
-    template <int NS, int BD, int B1, int B2, class F>
-    vktError launchGen(PwPlan const& p, F const& f, hipStream_t stream)
+    template <int NS, int BD, int B1, int B2, int U, class F>
+    vktError launchGenU(PwPlan const& p, F const& f, hipStream_t stream)
     {
-        constexpr int U = NS == 0 ? 2 : vecUnroll<NS, BD>();
         constexpr uint64_t kQ = static_cast<uint64_t>(kVecBlock) * U;
         // (measured and rejected: one row segment per workgroup, row coordinates on the scalar
         // unit -- 1021-voxel rows split into two 65-chunk segments, SumRange with dstOffset x = 3
@@ -1461,6 +1492,18 @@ namespace hipk
             q0 += n;
         } while (q0 < quanta);
         return vktNoError;
+    }
+
+    template <int NS, int BD, int B1, int B2, class F>
+    vktError launchGen(PwPlan const& p, F const& f, hipStream_t stream)
+    {
+        constexpr int U = NS == 0 ? 2 : vecUnroll<NS, BD>();
+        // 16-B items of 4-byte voxels are half the 8-voxel items: twice the items per lane
+        // keep the bytes in flight
+        if constexpr (BD == 4 && B1 == 4 && (NS < 2 || B2 == 4))
+            if (p.gg.wide)
+                return launchGenU<NS, BD, B1, B2, 2 * U>(p, f, stream);
+        return launchGenU<NS, BD, B1, B2, U>(p, f, stream);
     }
 
     // Builds the plan for `ns` sources over a box of extent n (all > 0).

@@ -88,6 +88,7 @@ namespace rt
         DecomposeStageWords,           // source words per thread in flight in the staged copy (5, 6, 8)
         PointwiseU8Wide,               // 0: UInt8 general-path boxes keep 8-voxel items
         PointwiseF32Halves,            // 0: padded 4-byte rows keep the per-item loop
+        PointwiseF32Wide,              // 1: 4-byte general-path boxes use 16-B items (measured neutral; off)
         Count
     };
     int64_t knob(Knob k);
