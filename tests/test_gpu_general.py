@@ -247,6 +247,32 @@ def test_uint8_pair16_rows(lib, o, x0, dims):
         assert L.vktHipSetTuningKnob(b"pointwise.merge_sectors", -1) == 0
 
 
+@pytest.mark.parametrize("x0", [0, 3, 4, 13, 37])
+def test_three_stream_sector_completion(lib, o, x0):
+    """pointwise.merge_sectors = 2: 64-B sector completion for the 3-stream ops on the aligned
+    path (UInt16 packed functor, Float32 halves, UInt8 pairs): SafeSum / Sum over padded rows
+    with >= 64-B gaps vs the oracle; bytes outside the box keep their values."""
+    from volkit_amd._lib import lib as L
+    try:
+        assert L.vktHipSetTuningKnob(b"pointwise.merge_sectors", 2) == 0
+        for fmt, X in ((5, 128), (7, 64), (4, 256)):
+            rng = np.random.default_rng(500 + x0 + fmt)
+            dims = (4, 20, X)
+            a, b, dinit = rand_codes(rng, fmt, dims), rand_codes(rng, fmt, dims), rand_codes(rng, fmt, dims)
+            for w in (1, 5, 17, X // 2, X - x0 - 40):
+                if w <= 0 or x0 + w > X:
+                    continue
+                first, last = (x0, 1, 0), (x0 + w, 19, 4)
+                for op in ("SafeSum", "Sum"):
+                    da, db, dd = Dev(a, fmt), Dev(b, fmt), Dev(dinit, fmt)
+                    assert L.vktHipArithmeticRange(OPS.index(op), dd.view, da.view, db.view, vec(first), vec(last),
+                                                   vec((0, 0, 0))) == 0, last_error()
+                    ref = o.arith(op, [fmt] * 3, [(0.0, 1.0)] * 3, a, b, dinit.copy(), first, last, (0, 0, 0))
+                    assert_codes_equal(dd.read(), ref, fmt, f"{op} fmt={fmt} x0={x0} w={w}")
+    finally:
+        assert L.vktHipSetTuningKnob(b"pointwise.merge_sectors", -1) == 0
+
+
 @pytest.mark.parametrize("fmt", [7, 6])
 @pytest.mark.parametrize("x0", [0, 1, 3, 4, 7, 9, 13, 16])
 def test_float32_padded_rows_halves(lib, o, fmt, x0):

@@ -293,6 +293,26 @@ def main():
             report(f"f32ab {op} 800^3 sub-box {lab} Float32 f32_halves={kv} (median of 3 rounds, "
                    f"spread {ts[0]:.4f}-{ts[-1]:.4f})", ts[1], (8 if op == "CopyRange" else 12) * 800 ** 3, 800 ** 3)
         free(A, B, D)
+    if want("u16merge"):
+        # 3-stream UInt16 / Float32 ops on padded sub-boxes: sector completion (merge_sectors = 2)
+        for fmt, bpv in ((5, 2), (7, 4)):
+            m = 1024
+            A, B, D = alloc((m,) * 3, fmt, seed=1), alloc((m,) * 3, fmt, seed=2), alloc((m,) * 3, fmt)
+            ab = {}
+            for rnd in range(3):
+                for kv in (1, 2):
+                    lib.vktHipSetTuningKnob(b"pointwise.merge_sectors", kv)
+                    for lab, f0, f1 in (("x0=100", Vec3i_t(100, 100, 100), Vec3i_t(900, 900, 900)),):
+                        ab.setdefault((lab, kv, 5), []).append(
+                            timed(lambda: lib.vktHipArithmeticRange(5, D, A, B, f0, f1, o), R))
+                        ab.setdefault((lab, kv, 0), []).append(
+                            timed(lambda: lib.vktHipArithmeticRange(0, D, A, B, f0, f1, o), R))
+            lib.vktHipSetTuningKnob(b"pointwise.merge_sectors", -1)
+            for (lab, kv, op), ts in sorted(ab.items()):
+                ts.sort()
+                report(f"u16merge {'SafeSum' if op == 5 else 'Sum'}Range 800^3 sub-box {lab} fmt={fmt} merge_sectors={kv} "
+                       f"(median of 3 rounds, spread {ts[0]:.4f}-{ts[-1]:.4f})", ts[1], 3 * bpv * 800 ** 3, 800 ** 3)
+            free(A, B, D)
     if want("chunked"):
         # metric pipeline scheduled in plane chunks (Resample of dst planes [z0, z1), then SumRange
         # over the same planes): does the R chunk come back from the Infinity Cache?

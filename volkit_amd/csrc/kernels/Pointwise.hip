@@ -140,7 +140,12 @@ namespace hipk
         // Not for UInt8 here: its per-item loop (8 B per lane) lost the batching of its loads to
         // the conditional destination-chunk loads -- 800^3 sub-box copy x 0..800 0.250 -> 0.378
         // ms; UInt8 rows complete their sectors on the 16-voxel pair grid below.
-        if (vec && p.g.padded && ns <= 1 && bpv != 1)
+        // (3-stream ops: 4-byte voxels on the contiguous-lane halves only -- 800^3 sub-box of
+        // 1024^3 at x0 = 100, Float32 SumRange 1.218 -> 1.147 ms, while UInt16 lost again, 0.624 ->
+        // 0.645 ms, profiles/r03/merge3_ab.jsonl; knob value 2 forces it for A/B)
+        bool const merge3 = rt::knob(rt::Knob::PointwiseMergeSectors) == 2 ||
+                            (bpv == 4 && rt::knob(rt::Knob::PointwiseF32Halves) != 0);
+        if (vec && p.g.padded && (ns <= 1 || merge3) && bpv != 1)
         {
             int64_t const bd = bpv;
             int64_t const sv = 64 / bd;
