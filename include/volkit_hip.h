@@ -275,6 +275,13 @@ VKTAPI vktError vktHipSlabArithmeticRange(vktHipComm_t comm, vktHipArithmeticOp 
                                           vktHipSlab_t const* dest, vktHipSlab_t const* source1,
                                           vktHipSlab_t const* source2, vktVec3i_t first, vktVec3i_t last,
                                           vktVec3i_t dstOffset);
+/* TransformRange with a host callback over a Z-slab partitioned volume (Transform shards with
+ * no exchange): rank `rank` of nranks transforms the planes it owns of the GLOBAL
+ * range [first, last) of its slab; the callback sees global coordinates, in the serial order
+ * within the rank (ranks 0..n-1 called in turn reproduce the whole serial loop).  Device
+ * functors: vkt::TransformRangeSlab (include/volkit_transform.hpp). */
+VKTAPI vktError vktHipSlabTransformRange1(int32_t nranks, int32_t rank, vktHipSlab_t slab, vktVec3i_t first,
+                                          vktVec3i_t last, vktTransformUnaryOp unaryOp);
 /* The local half of a Range call whose moves the CALLER carried out (volkit_amd/slab.py moves
  * them over torch.distributed): runs rank `rank`'s pieces, reading remote source planes from
  * gather1 / gather2 (device buffers holding bufPlanes[0] / bufPlanes[1] planes of source 1 / 2

@@ -31,6 +31,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <type_traits>
 
@@ -693,5 +694,40 @@ namespace transform_detail
     Error Transform(StructuredVolume& volume1, StructuredVolume& volume2, Op op)
     {
         return TransformRange(volume1, volume2, Vec3i{0, 0, 0}, volume1.getDims(), op);
+    }
+
+    //! A functor seen through a Z shift: z + dz is passed on (a slab's first global plane).
+    template <class Op>
+    struct ZShifted
+    {
+        Op op;
+        int32_t dz;
+        __device__ void operator()(int32_t x, int32_t y, int32_t z, VoxelView voxel) { op(x, y, z + dz, voxel); }
+    };
+
+    //! TransformRange with a device functor over a Z-slab partitioned volume (Transform shards
+    //! with no exchange).  `slab` holds global planes [z0, z0 + dimZ) of a volume
+    //! globalDimZ deep, split over nranks by the ceil partition of vktHipSlabExchangeHalo; rank
+    //! `rank` transforms the planes it OWNS of the GLOBAL range [first, last), and the functor
+    //! sees global coordinates.  Host-callback twin: vktHipSlabTransformRange1.
+    template <class Op, EnableIfDeviceOp<Op> = 0>
+    Error TransformRangeSlab(int32_t nranks, int32_t rank, StructuredVolume& slab, int32_t z0, int32_t globalDimZ,
+                             Vec3i first, Vec3i last, Op op)
+    {
+        if (nranks <= 0 || rank < 0 || rank >= nranks || globalDimZ < 0)
+            return static_cast<Error>(vktHipReportError("TransformRangeSlab: invalid rank / nranks"));
+        if (last.x <= first.x || last.y <= first.y || last.z <= first.z)
+            return NoError;
+        if (first.z < 0 || last.z > globalDimZ)
+            return static_cast<Error>(vktHipReportError("TransformRangeSlab: range outside the volume"));
+        int64_t const size = (static_cast<int64_t>(globalDimZ) + nranks - 1) / nranks;
+        int64_t const d0 = std::min<int64_t>(rank * size, globalDimZ), d1 = std::min<int64_t>(d0 + size, globalDimZ);
+        int64_t const zb = std::max<int64_t>(first.z, d0), ze = std::min<int64_t>(last.z, d1);
+        if (ze <= zb)
+            return NoError;
+        if (zb < z0 || ze > static_cast<int64_t>(z0) + slab.getDims().z)
+            return static_cast<Error>(vktHipReportError("TransformRangeSlab: slab does not hold its owned planes"));
+        return TransformRange(slab, Vec3i{first.x, first.y, static_cast<int32_t>(zb - z0)},
+                              Vec3i{last.x, last.y, static_cast<int32_t>(ze - z0)}, ZShifted<Op>{op, z0});
     }
 } // vkt

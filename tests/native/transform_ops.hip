@@ -181,6 +181,33 @@ int vktt_run_unary(int op, void* data, int dx, int dy, int dz, int fmt, float lo
     return rc;
 }
 
+// Z-slab TransformRange: the global volume (host bytes, updated in place) is cut into nranks
+// slabs of the ceil partition, each slab (its owned planes only) gets TransformRangeSlab.
+int vktt_run_unary_slab(int op, void* data, int dx, int dy, int dz, int fmt, float lo, float hi, int nranks, int fx,
+                        int fy, int fz, int lx, int ly, int lz)
+{
+    GpuPolicy gpu;
+    size_t const plane = static_cast<size_t>(dx) * dy * vkt::codec::bytesPerVoxel(fmt);
+    int const size = (dz + nranks - 1) / nranks;
+    for (int r = 0; r < nranks; ++r)
+    {
+        int const z0 = std::min(r * size, dz), z1 = std::min(z0 + size, dz);
+        if (z1 <= z0)
+            continue;
+        uint8_t* host = static_cast<uint8_t*>(data) + plane * z0;
+        vkt::StructuredVolume v(dx, dy, z1 - z0, static_cast<vkt::DataFormat>(fmt), 1.f, 1.f, 1.f, lo, hi);
+        upload(v, host);
+        int rc = withUnary(op, [&](auto f) {
+            return static_cast<int>(
+                vkt::TransformRangeSlab(nranks, r, v, z0, dz, vkt::Vec3i{fx, fy, fz}, vkt::Vec3i{lx, ly, lz}, f));
+        });
+        download(host, v);
+        if (rc != 0)
+            return rc;
+    }
+    return 0;
+}
+
 // Whole-volume Transform (the reference's vkt::Transform(volume, op) entry).
 int vktt_run_unary_whole(int op, void* data, int dx, int dy, int dz, int fmt, float lo, float hi)
 {

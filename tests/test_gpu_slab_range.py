@@ -217,3 +217,48 @@ def test_slab_py_executor_one_rank(L):
     slab.copy_range(slab.Slab(D.view, 0, 14), slab.Slab(S.view, 0, 11), (3, -1, -2), (45, 11, 10), (0, 0, 2))
     torch.cuda.synchronize()
     assert np.array_equal(D.read(), ref.codes)
+
+
+@pytest.mark.parametrize("nslabs", [1, 3, 4])
+def test_slab_transform_host_callback(L, nslabs):
+    """vktHipSlabTransformRange1 (and slab.transform_range for one rank): each slab runs the
+    host callback over its owned planes of the global range with global z; the slabs put
+    together equal the whole-volume oracle TransformRange_serial (Transform_serial.hpp:15-48),
+    halo planes untouched."""
+    from volkit_amd import _lib, slab
+    from volkit_amd.volkit import VoxelView
+    rng = np.random.default_rng(nslabs)
+    G, y, x = 11, 6, 13
+    glob = rng.integers(0, 256, (G, y, x), dtype=np.uint8)
+    first, last = (2, 1, 1), (12, 6, 10)
+
+    def op(xx, yy, zz, v):
+        v.bytes[0] = (v.bytes[0] ^ (xx + 3 * yy + 17 * zz)) & 0xFF
+
+    def oracle_op(xx, yy, zz, b, fmt, lo, hi):
+        b[0] = (b[0] ^ (xx + 3 * yy + 17 * zz)) & 0xFF
+
+    ref = ob.Volume(glob.copy(), 4, 0.0, 1.0)
+    ob.transform_range1(ref, first, last, oracle_op)
+    slabs = [DevSlab(glob, 4, nslabs, r, halo=1) for r in range(nslabs)]
+    seen = []
+
+    def record(xx, yy, zz, v):
+        seen.append(zz)
+        op(xx, yy, zz, v)
+    cb = _lib.UnaryOp(lambda xx, yy, zz, v: record(xx, yy, zz, VoxelView(v)))
+    for r, s in enumerate(slabs):
+        assert L.vktHipSlabTransformRange1(nslabs, r, s.slab, _lib.Vec3i_t(*first), _lib.Vec3i_t(*last), cb) == 0, err(L)
+    assert seen == sorted(seen)            # ranks 0..n-1 in turn: the serial z order
+    for s in slabs:
+        got, o0, o1 = s.read(), *s.owned
+        np.testing.assert_array_equal(got[o0 - s.z0:o1 - s.z0], ref.codes[o0:o1])
+        keep = np.ones(got.shape[0], bool)
+        keep[o0 - s.z0:o1 - s.z0] = False
+        np.testing.assert_array_equal(got[keep], s.before[keep])
+    if nslabs == 1:
+        s = DevSlab(glob, 4, 1, 0)
+        slab.transform_range(slab.Slab(s.view, s.z0, G), first, last, op)
+        np.testing.assert_array_equal(s.read(), ref.codes)
+    bad = slabs[0]
+    assert L.vktHipSlabTransformRange1(nslabs, 0, bad.slab, _lib.Vec3i_t(0, 0, 0), _lib.Vec3i_t(x, y, G + 1), cb) != 0

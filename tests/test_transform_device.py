@@ -34,6 +34,7 @@ def t():
     i, f, p = C.c_int, C.c_float, C.c_void_p
     lib.vktt_run_unary.argtypes = [i, p, i, i, i, i, f, f, i, i, i, i, i, i]
     lib.vktt_run_unary_whole.argtypes = [i, p, i, i, i, i, f, f]
+    lib.vktt_run_unary_slab.argtypes = [i, p, i, i, i, i, f, f, i, i, i, i, i, i, i]
     lib.vktt_run_binary.argtypes = [i, i, p, i, i, i, i, f, f, p, i, i, i, i, f, f, i, i, i, i, i, i]
     lib.vktt_host_unary.restype = p
     lib.vktt_host_unary.argtypes = [i]
@@ -106,6 +107,25 @@ def test_unary_functor_vs_oracle(t, op, fmt):
             out = gpu_unary(t, op, codes, fmt, mapping, first, last)
             ref = oracle_unary(t, op, codes, fmt, mapping, first, last)
             assert_codes_equal(out, ref, fmt, f"{UNARY_OPS[op]} fmt={fmt} map={mapping} {dims} {first}->{last}")
+
+
+@pytest.mark.parametrize("nranks", [1, 2, 3, 5, 8])
+@pytest.mark.parametrize("fmt", [4, 5, 7])
+def test_unary_functor_slabs(t, nranks, fmt):
+    """vkt::TransformRangeSlab: the volume cut into nranks Z-slabs (ceil partition, empty
+    trailing slabs for 8 ranks over 5..11 planes), each slab transforms the owned planes of the
+    GLOBAL range with the functor seeing global z: the slabs put together equal one
+    whole-volume oracle call.  Checkered<3> and Diagonal read z, so a missed shift shows."""
+    rng = np.random.default_rng(31 * nranks + fmt)
+    for op in (0, 2, 4):
+        for dims, first, last in RANGES[2:6] + [((40, 9, 5), (0, 0, 0), (40, 9, 5))]:
+            codes = rand_codes(rng, fmt, dims[::-1])
+            out = np.ascontiguousarray(codes.copy())
+            z, y, x = out.shape
+            rc = t.vktt_run_unary_slab(op, out.ctypes.data, x, y, z, fmt, 0.0, 1.0, nranks, *first, *last)
+            assert rc == 0, rc
+            ref = oracle_unary(t, op, codes, fmt, (0.0, 1.0), first, last)
+            assert_codes_equal(out, ref, fmt, f"slabs={nranks} {UNARY_OPS[op]} fmt={fmt} {dims} {first}->{last}")
 
 
 @pytest.mark.parametrize("op", [0, 2, 3])

@@ -254,6 +254,7 @@ SIGNATURES = {
     "vktHipSlabCopyRange": (c_err, [c_comm, i32, P(HipSlab_t), P(HipSlab_t), Vec3i_t, Vec3i_t, Vec3i_t]),
     "vktHipSlabArithmeticRange": (c_err, [c_comm, C.c_int, i32, P(HipSlab_t), P(HipSlab_t), P(HipSlab_t), Vec3i_t,
                                           Vec3i_t, Vec3i_t]),
+    "vktHipSlabTransformRange1": (c_err, [i32, i32, HipSlab_t, Vec3i_t, Vec3i_t, UnaryOp]),
     "vktHipSlabRangePieces": (c_err, [C.c_int, C.c_int, i32, i32, HipSlab_t, P(HipSlab_t), P(HipSlab_t), Vec3i_t,
                                       Vec3i_t, Vec3i_t, f32, C.c_void_p, C.c_void_p]),
     "vktHipTransformRange1": (c_err, [HipVolumeView_t, Vec3i_t, Vec3i_t, UnaryOp]),

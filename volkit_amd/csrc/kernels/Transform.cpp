@@ -56,13 +56,22 @@ namespace hipk
 } // hipk
 } // vkt
 
+namespace vkt
+{
+namespace hipk
+{
+    // The unary host-callback transform; the callback sees z + zShift (a Z-slab of a larger
+    // volume passes its first global plane, runtime/Slab.cpp).
+    vktError transformRange1Shifted(vktHipVolumeView_t volume, vktVec3i_t first, vktVec3i_t last,
+                                    vktTransformUnaryOp unaryOp, int32_t zShift);
+} // hipk
+} // vkt
+
 using namespace vkt;
 using namespace vkt::hipk;
 
-extern "C" {
-
-vktError vktHipTransformRange1(vktHipVolumeView_t volume, vktVec3i_t first, vktVec3i_t last,
-                               vktTransformUnaryOp unaryOp)
+vktError vkt::hipk::transformRange1Shifted(vktHipVolumeView_t volume, vktVec3i_t first, vktVec3i_t last,
+                                           vktTransformUnaryOp unaryOp, int32_t zShift)
 {
     if (!validView(volume) || unaryOp == nullptr)
         return rt::fail("vktHipTransformRange1: invalid arguments");
@@ -88,10 +97,18 @@ vktError vktHipTransformRange1(vktHipVolumeView_t volume, vktVec3i_t first, vktV
                 std::memcpy(bytes, p, bpv);
                 vktVoxelView_t vv{bytes, static_cast<vktDataFormat>(volume.dataFormat), volume.mappingLo,
                                   volume.mappingHi};
-                unaryOp(x, y, z, vv);
+                unaryOp(x, y, z + zShift, vv);
                 std::memcpy(p, bytes, bpv);
             }
     return s.store();
+}
+
+extern "C" {
+
+vktError vktHipTransformRange1(vktHipVolumeView_t volume, vktVec3i_t first, vktVec3i_t last,
+                               vktTransformUnaryOp unaryOp)
+{
+    return transformRange1Shifted(volume, first, last, unaryOp, 0);
 }
 
 vktError vktHipTransformRange2(vktHipVolumeView_t volume1, vktHipVolumeView_t volume2, vktVec3i_t first,

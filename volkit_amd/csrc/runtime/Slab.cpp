@@ -28,6 +28,11 @@
 
 namespace vkt
 {
+namespace hipk
+{
+    vktError transformRange1Shifted(vktHipVolumeView_t volume, vktVec3i_t first, vktVec3i_t last,
+                                    vktTransformUnaryOp unaryOp, int32_t zShift);
+}
 namespace
 {
     struct Move
@@ -461,6 +466,32 @@ vktError vktHipSlabRangePieces(vktHipSlabOpKind kind, vktHipArithmeticOp op, int
         src[k] = *srcs[k];
     e = runPieces(a, op, dst, src, buf, ps, first, last, dstOffset, value);
     return e != vktNoError ? e : rt::finishLaunch(what);
+}
+
+vktError vktHipSlabTransformRange1(int32_t nranks, int32_t rank, vktHipSlab_t slab, vktVec3i_t first, vktVec3i_t last,
+                                   vktTransformUnaryOp unaryOp)
+{
+    char const* what = "vktHipSlabTransformRange1";
+    if (unaryOp == nullptr)
+        return rt::fail("vktHipSlabTransformRange1: null operation");
+    if (nranks <= 0 || rank < 0 || rank >= nranks)
+        return rt::fail("vktHipSlabTransformRange1: invalid rank / nranks");
+    // the owned planes of the range: the Fill plan (no sources, nothing moves)
+    Args a{vktHipSlabFill, nranks, slab.globalDimZ, {0, 0}, first.z, last.z, 0};
+    vktError e = validate(a, what);
+    if (e != vktNoError || last.x <= first.x || last.y <= first.y || last.z <= first.z)
+        return e;
+    if ((e = checkSlabs(a, rank, 1, &slab, nullptr, what)) != vktNoError)
+        return e;
+    std::vector<vktHipSlabPiece_t> ps;
+    int32_t bp[2];
+    planRank(a, rank, ps, bp);
+    for (vktHipSlabPiece_t const& p : ps)
+        if ((e = hipk::transformRange1Shifted(slab.view, vktVec3i_t{first.x, first.y, p.zBegin - slab.z0},
+                                              vktVec3i_t{last.x, last.y, p.zEnd - slab.z0}, unaryOp, slab.z0)) !=
+            vktNoError)
+            return e;
+    return vktNoError;
 }
 
 vktError vktHipSlabFillRange(vktHipComm_t comm, int32_t numSlabs, vktHipSlab_t const* dst, vktVec3i_t first,

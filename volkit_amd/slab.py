@@ -378,6 +378,18 @@ def arithmetic_range(op, dst: Slab, s1: Slab, s2: Slab, first, last, dst_offset=
     return _range(ARITHMETIC, code, dst, [s1, s2], first, last, dst_offset, 0.0, group, run_pieces)
 
 
+def transform_range(dst: Slab, first, last, fn, group=None) -> int:
+    """TransformRange with a host callback over Z-slabs (Transform shards with no exchange):
+    each rank runs fn(x, y, z, VoxelView) over the owned planes of the global range, z global
+    (vktHipSlabTransformRange1; Transform_serial.hpp:15-48 per slab)."""
+    from .volkit import VoxelView
+    world, rank = _world_rank(group)
+    cb = _lib.UnaryOp(lambda x, y, z, v: fn(x, y, z, VoxelView(v)))
+    if lib.vktHipSlabTransformRange1(world, rank, dst.c(), _lib.Vec3i_t(*first), _lib.Vec3i_t(*last), cb) != 0:
+        raise RuntimeError(_lib.last_error())
+    return 0
+
+
 # ---- reductions over Z-slabs (SURVEY.md §8(f) F2: the first all-reduce users) -------------------
 PARTIAL_BYTES = C.sizeof(_lib.HipAggregatePartial_t)
 
