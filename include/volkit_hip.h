@@ -103,8 +103,14 @@ VKTAPI vktError vktHipKernelScopeEnd(vktHipKernelScope scope);
  * counters), "histogram.mulshift" (1; 0 makes UInt16 histograms whose bins are (code * numBins)
  * >> 16 keep the float bin formula), "histogram.p16_step" (1; 0 runs the packed-16 counters'
  * threshold tests after every item instead of once per wave-step), "render.bricks" (1; 0 makes
- * MultiScattering sample the dense volume instead of its 8^3-brick copy).  For tests and in-process
- * A/B measurements; unknown names return vktInvalidValue.
+ * MultiScattering sample the dense volume instead of its 8^3-brick copy), "decompose.aligned_lds"
+ * (0; 1 / 2 write the row-end / every staged word to LDS as aligned pieces), "decompose.stage_words"
+ * (6; 5 or 8 source words in flight per thread), "pointwise.u8_wide" (1; 0 keeps UInt8 boxes of the
+ * general path on 8-voxel items), "pointwise.f32_halves" (1; 0 keeps 4-byte padded multi-row boxes
+ * on the per-item loop), "pointwise.f32_wide" (0; 1 gives 4-byte general-path boxes 16-B items),
+ * "aggregates.codes" (1; 0 makes UInt8 ComputeAggregates take the two float passes instead of one
+ * pass of code counts).  For tests and in-process A/B measurements; unknown names return
+ * vktInvalidValue.
  *
  * Writes outside a range box: FillRange / CopyRange / convert and device-functor TransformRange
  * may rewrite, with the destination's own unchanged bytes, up to one 64-B sector around each row

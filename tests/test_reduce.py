@@ -406,6 +406,61 @@ def test_aggregates_integer_pass_unit_mapping(fmt):
     assert abs(got.prod - ref.prod) <= codes.size * EPS * exact_prod
 
 
+def check_aggregates(got, codes, fmt, mapping, first, last, what):
+    ref = ob.aggregates_range(ob.Volume(codes, fmt, *mapping), first, last)
+    assert (got.min, got.max) == (ref.min, ref.max), what
+    assert tuple(got.argmin) == tuple(ref.argmin) and tuple(got.argmax) == tuple(ref.argmax), what
+    vals = values_of(codes, fmt, *mapping)[first[2]:last[2], first[1]:last[1], first[0]:last[0]].reshape(-1)
+    n, nall = vals.size, codes.size
+    check_float("sum", got.sum, ref.sum, float(np.sum(vals, dtype=np.float64)),
+                float(np.sum(np.abs(vals), dtype=np.float64)), n)
+    assert got.mean == np.float32(np.float64(np.float32(got.sum)) / nall), what
+    d = (vals - np.float32(got.mean)).astype(np.float32)
+    d2 = (d * d).astype(np.float32)
+    exact_var = float(np.float32(np.float64(np.float32(np.sum(d2, dtype=np.float64))) / nall))
+    assert abs(got.var - exact_var) <= float(np.spacing(np.float32(exact_var))), what
+    assert got.stddev == np.float32(np.sqrt(np.float32(got.var))), what
+    return ref
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mapping", [(0.0, 1.0), (3.0, -1.0), (-2.0, 5.0), (1000.0, 1000.001), (0.25, 0.25)])
+def test_aggregates_uint8_code_counts(mapping):
+    """UInt8 ComputeAggregates from one pass of code counts (knob aggregates.codes):
+    increasing and decreasing mappings (the value minimum is then the LARGEST code), a mapping
+    that rounds neighbouring codes to one value and a constant one (extremes held by several
+    codes: the library reruns the two float passes), tied extremes across lanes, waves and
+    padded end items; equal to the oracle and to the two-pass path (knob 0)."""
+    rng = np.random.default_rng(17)
+    cases = [((24, 40, 1040), (0, 0, 0), (1040, 40, 24)),      # one span
+             ((24, 40, 1040), (3, 1, 2), (1037, 39, 23)),       # padded rows
+             ((10, 64, 256), (8, 3, 2), (200, 60, 9))]          # strided box
+    for dims, first, last in cases:
+        codes = rng.integers(2, 254, dims, dtype=np.uint8)
+        for z, y, x in ((5, 7, 9), (2, 3, 1000 % dims[2]), (8, 30, 40)):
+            codes[z, y, x] = 1
+        for z, y, x in ((6, 1, 511 % dims[2]), (6, 1, 13), (9, 38, 8)):
+            codes[z, y, x] = 254
+        runs = []
+        for k in (1, 0):
+            lib.vktHipSetTuningKnob(b"aggregates.codes", k)
+            try:
+                got = gpu_aggregates(codes, 4, *mapping, first, last)
+            finally:
+                lib.vktHipSetTuningKnob(b"aggregates.codes", -1)
+            check_aggregates(got, codes, 4, mapping, first, last, f"map={mapping} {first}->{last} knob={k}")
+            runs.append(got)
+        a, b = runs
+        assert (a.min, a.max, tuple(a.argmin), tuple(a.argmax), a.mean) == (b.min, b.max, tuple(b.argmin),
+                                                                          tuple(b.argmax), b.mean)
+    # product through value^count: 256 voxels of 1.01 (code 255 under (0, 1.01)), ~12.8
+    codes = np.full((2, 2, 64), 255, np.uint8)
+    got = gpu_aggregates(codes, 4, 0.0, 1.01, (0, 0, 0), (64, 2, 2))
+    v = float(values_of(codes[:1, :1, :1], 4, 0.0, 1.01).reshape(-1)[0])
+    exact = v ** codes.size
+    assert abs(got.prod - exact) <= codes.size * EPS * exact, (got.prod, exact)
+
+
 @pytest.mark.gpu
 def test_aggregates_ties_specials_and_whole_volume_mean():
     # duplicate minima / maxima: first occurrence in z, y, x order; NaN never min / max;

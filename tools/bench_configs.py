@@ -591,7 +591,12 @@ def main():
             report(f"reduce Histogram 1024^3 {name} 256 bins", ms, bpv * n ** 3, n ** 3)
             aggW = _lib.Aggregates_t()
             ms = timed(lambda: lib.vktHipAggregatesRange(W, o, last, C.byref(aggW)), R)
-            report(f"reduce Aggregates 1024^3 {name} (2 passes, incl. D2H of the result)", ms, 2 * bpv * n ** 3, n ** 3)
+            if fmt == 4:   # one pass of code counts (knob aggregates.codes)
+                report(f"reduce Aggregates 1024^3 {name} (1 pass of code counts, incl. D2H of the result)", ms,
+                       bpv * n ** 3, n ** 3)
+            else:
+                report(f"reduce Aggregates 1024^3 {name} (2 passes, incl. D2H of the result)", ms, 2 * bpv * n ** 3,
+                       n ** 3)
             free(W)
         Vc = alloc((n,) * 3, 5)
         lib.vktHipFillRange(Vc, o, last, C.c_float(0.5))
@@ -605,6 +610,24 @@ def main():
         report("reduce Aggregates 1024^3 UInt16 (2 passes, incl. D2H of the result)", ms, 2 * 2 * n ** 3, n ** 3)
         free(V, Vc)
         lib.vktHipFree(bins)
+    if want("aggcodes"):
+        # UInt8 ComputeAggregates: one pass of code counts vs the two float passes (knob
+        # aggregates.codes), whole volume and the 800^3 sub-box at x0 = 100 (padded rows)
+        n = 1024
+        W = alloc((n,) * 3, 4, seed=12)
+        last = Vec3i_t(n, n, n)
+        u0, u1 = Vec3i_t(100, 100, 100), Vec3i_t(900, 900, 900)
+        agg = _lib.Aggregates_t()
+        for k in (1, 0):
+            lib.vktHipSetTuningKnob(b"aggregates.codes", k)
+            passes = 1 if k else 2
+            ms = timed(lambda: lib.vktHipAggregatesRange(W, o, last, C.byref(agg)), R)
+            report(f"aggcodes Aggregates 1024^3 UInt8 [codes={k}, {passes} pass(es)]", ms, passes * n ** 3, n ** 3)
+            ms = timed(lambda: lib.vktHipAggregatesRange(W, u0, u1, C.byref(agg)), R)
+            report(f"aggcodes Aggregates UInt8 800^3 sub-box at x0=100 [codes={k}, {passes} pass(es)]", ms,
+                   passes * 800 ** 3, 800 ** 3)
+        lib.vktHipSetTuningKnob(b"aggregates.codes", -1)
+        free(W)
     if want("config5"):
         # BASELINE config 5: 1024^3 UInt8 multi-scattering, 1024^2 viewport (headless frames)
         import volkit_amd.volkit as vkt

@@ -756,15 +756,32 @@ namespace hipk
     // exact whatever the schedule.  Sums accumulate per lane in double, then the fixed
     // shuffle / LDS / partials tree (deterministic for a given grid).
     // UNIT: the mapping is the unit mapping (+0, 1), decode without the lerp (codec::decodeUnit).
-    template <int PASS, int FMT, bool CONTIG, bool UNIT = false>
+    // CODES (UInt8, pass 1): no decode and no float terms at all -- every voxel of a UInt8 volume
+    // has one of 256 values, so the kernel counts CODES (LDS counters, 2^rShift copies, flushed to
+    // the 256 u64 bins h.bins) and tracks the first occurrence of the smallest and largest code per
+    // lane (integer compares; minValue / maxValue of the partial hold the codes).  The sums, the
+    // product and the second pass's sum of squares follow from the 256 counts
+    // (aggregatesCodesFinalKernel): one pass over the data instead of two.
+    template <int PASS, int FMT, bool CONTIG, bool UNIT = false, bool CODES = false>
     __global__ __launch_bounds__(kBlock) void aggregatesFastKernel(FastHistArgs h, float const* meanPtr,
                                                                   float meanValue, vktHipAggregatePartial_t* partials)
     {
         constexpr int BPV = FMT == codec::FmtUInt8 ? 1 : FMT == codec::FmtUInt16 ? 2 : 4;
         constexpr int U = 4;
+        static_assert(!CODES || (PASS == 1 && FMT == codec::FmtUInt8), "code counts: UInt8 pass 1");
         float const mean = PASS == 2 ? (meanPtr ? *meanPtr : meanValue) : 0.f;
         vktHipAggregatePartial_t p = emptyPartial();
         uint32_t const lane = threadIdx.x & 63;
+        extern __shared__ uint32_t codeCnt[];
+        uint32_t const rowShift = h.rShift + 2;
+        char* const cLane = reinterpret_cast<char*>(codeCnt) + ((lane & ((1u << h.rShift) - 1u)) << 2);
+        int32_t cmin = 256, cmax = -1;   // CODES: this lane's smallest / largest code so far
+        if constexpr (CODES)
+        {
+            for (uint32_t i = threadIdx.x; i < (256u << h.rShift); i += kBlock)
+                codeCnt[i] = 0;
+            __syncthreads();
+        }
         uint64_t const px = static_cast<uint64_t>(h.dimX), py = static_cast<uint64_t>(h.dimY);
         // global linear index of voxel j of item `item`
         auto globalIndex = [&](uint64_t item, int j) -> uint64_t {
@@ -791,6 +808,42 @@ namespace hipk
                     return h.giBase + hb * 8 + 4 * lane + (j < 4 ? static_cast<uint64_t>(j) : 252ull + j);
                 return globalIndex(item, j);
             };
+            if constexpr (CODES)
+            {
+                int32_t lo = 256, hi = -1;
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    if ((m >> j) & 1u)
+                    {
+                        atomicAdd(reinterpret_cast<uint32_t*>(cLane + (c[j] << rowShift)), 1u);
+                        lo = min(lo, static_cast<int32_t>(c[j]));
+                        hi = max(hi, static_cast<int32_t>(c[j]));
+                    }
+                if (lo < cmin || hi > cmax)   // rare after the first items: voxel order only then
+                {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j)
+                    {
+                        int32_t const cj = static_cast<int32_t>(c[j]);
+                        if (((m >> j) & 1u) && (cj < cmin || cj > cmax))
+                        {
+                            uint64_t const gi = gIndex(j);
+                            if (cj < cmin)
+                            {
+                                cmin = cj;
+                                p.minIndex = gi;
+                            }
+                            if (cj > cmax)
+                            {
+                                cmax = cj;
+                                p.maxIndex = gi;
+                            }
+                        }
+                    }
+                }
+                p.count += __builtin_popcount(m);
+                return;
+            }
             // pass 1 over spans: one test per item (its min / max against the lane's) instead of
             // one branch per voxel; the voxel-by-voxel strict updates run in order only when it
             // holds.  1024^3 UInt8 pass 1 272 -> 248 us; padded rows (non-CONTIG) lost 300 ->
@@ -908,9 +961,130 @@ namespace hipk
             load8<BPV, true>(h.data, spanVoxel<CONTIG>(h, it), c);
             visit8(c, it);
         }
+        if constexpr (CODES)
+        {
+            if (cmin <= 255)
+                p.minValue = static_cast<float>(cmin);
+            if (cmax >= 0)
+                p.maxValue = static_cast<float>(cmax);
+            __syncthreads();
+            uint32_t const R = 1u << h.rShift;
+            for (uint32_t b = threadIdx.x; b < 256u; b += kBlock)
+            {
+                uint32_t sum = 0;
+                for (uint32_t r = 0; r < R; ++r)
+                    sum += codeCnt[(b << h.rShift) + ((r + b) & (R - 1))];
+                if (sum)
+                    atomicAdd(&h.bins[b], static_cast<unsigned long long>(sum));
+            }
+        }
         blockReduce(p);
         if (threadIdx.x == 0)
             partials[blockIdx.x] = p;
+    }
+
+    // UInt8 aggregates from the code counts of aggregatesFastKernel<CODES>: one workgroup, thread
+    // c = code c.  Each present code contributes count * its value to the sum, value^count to the
+    // product and count * (float)((value - mean)^2) to the sum of squares -- the per-voxel float
+    // terms of Aggregates_serial.hpp:37-80, summed in double in another order (the same parity
+    // bound as the streaming passes).  min / max are the extreme VALUES among the present codes;
+    // argmin / argmax the first occurrence of the code holding each, which the data pass tracked
+    // for the smallest and the largest code.  res[1].count = 1 when that holds: every present
+    // value finite and below FLT_MAX in magnitude, each extreme held by ONE code (a mapping that
+    // rounds two codes to one value, or a decreasing one with ties, makes the caller rerun the
+    // two float passes), and that code the smallest or the largest present one; 0 otherwise.
+    __global__ __launch_bounds__(kBlock) void aggregatesCodesFinalKernel(vktHipAggregatePartial_t const* partials,
+                                                                        uint32_t n, unsigned long long const* counts,
+                                                                        float lo, float hi, double numElems,
+                                                                        vktHipAggregatePartial_t* res)
+    {
+        vktHipAggregatePartial_t p = emptyPartial();
+        for (uint32_t i = threadIdx.x; i < n; i += blockDim.x)
+        {
+            vktHipAggregatePartial_t const& o = partials[i];
+            minCombine(p.minValue, p.minIndex, o.minValue, o.minIndex);
+            maxCombine(p.maxValue, p.maxIndex, o.maxValue, o.maxIndex);
+        }
+        blockReduce(p);
+        __shared__ float sLoCode, sHiCode, sVmin, sVmax, sMean;
+        __shared__ uint64_t sLoIdx, sHiIdx;
+        __shared__ int32_t sNmin, sNmax, sCmin, sCmax, sBad;
+        if (threadIdx.x == 0)
+        {
+            sLoCode = p.minValue;
+            sHiCode = p.maxValue;
+            sLoIdx = p.minIndex;
+            sHiIdx = p.maxIndex;
+            sNmin = sNmax = sBad = 0;
+            sCmin = sCmax = -1;
+        }
+        __syncthreads();
+        uint32_t const c = threadIdx.x;   // kBlock == 256: one code per thread
+        unsigned long long const cnt = c < 256u ? counts[c] : 0ull;
+        float const v = codec::decode(c, codec::FmtUInt8, lo, hi);
+        bool const present = cnt != 0ull;
+        vktHipAggregatePartial_t q = emptyPartial();
+        if (present)
+        {
+            if (!(fabsf(v) < FLT_MAX))
+                atomicOr(&sBad, 1);
+            q.minValue = q.maxValue = v;
+            q.minIndex = q.maxIndex = c;
+            double const dv = static_cast<double>(v), dn = static_cast<double>(cnt);
+            q.sum = dn * dv;
+            q.prod = pow(dv, dn);
+            q.count = cnt;
+        }
+        blockReduce(q);
+        __syncthreads();
+        vktHipAggregatePartial_t& r = q;   // thread 0: sum / prod / count / value extremes
+        if (threadIdx.x == 0)
+        {
+            sVmin = r.minValue;
+            sVmax = r.maxValue;
+            sMean = static_cast<float>(static_cast<double>(static_cast<float>(r.sum)) / numElems);
+        }
+        __syncthreads();
+        if (present && v == sVmin)
+        {
+            atomicAdd(&sNmin, 1);
+            sCmin = static_cast<int32_t>(c);
+        }
+        if (present && v == sVmax)
+        {
+            atomicAdd(&sNmax, 1);
+            sCmax = static_cast<int32_t>(c);
+        }
+        vktHipAggregatePartial_t t = emptyPartial();
+        if (present)
+        {
+            float const d = v - sMean;
+            float const d2 = d * d;
+            t.sumSq = static_cast<double>(cnt) * static_cast<double>(d2);
+        }
+        blockReduce(t);
+        __syncthreads();
+        if (threadIdx.x == 0)
+        {
+            auto indexOf = [&](int32_t code, bool& ok) -> uint64_t {
+                if (code >= 0 && static_cast<float>(code) == sLoCode)
+                    return sLoIdx;
+                if (code >= 0 && static_cast<float>(code) == sHiCode)
+                    return sHiIdx;
+                ok = false;
+                return kNoIndex;
+            };
+            bool ok = sBad == 0 && sNmin == 1 && sNmax == 1;
+            vktHipAggregatePartial_t out = r;
+            out.sumSq = 0.0;
+            out.minIndex = indexOf(sCmin, ok);
+            out.maxIndex = indexOf(sCmax, ok);
+            res[0] = out;
+            vktHipAggregatePartial_t two = emptyPartial();
+            two.sumSq = t.sumSq;
+            two.count = ok ? 1u : 0u;
+            res[1] = two;
+        }
     }
 
     __global__ void zeroU64Kernel(unsigned long long* p, uint64_t n)
@@ -1271,6 +1445,43 @@ namespace hipk
         return s;
     }
 
+    // UInt8 aggregates in one data pass (aggregatesFastKernel<CODES> + aggregatesCodesFinalKernel
+    // into res[0], res[1]); false when the range does not take the streaming walk.
+    bool launchCodeAggregates(BoxArgs const& a, hipStream_t s, double numElems, void* scratch, unsigned g,
+                              vktHipAggregatePartial_t* res)
+    {
+        FastHistArgs h;
+        bool contig;
+        if (!makeSpanArgs(a, h, contig))
+            return false;
+        auto* partials = static_cast<vktHipAggregatePartial_t*>(scratch);
+        h.bins = reinterpret_cast<unsigned long long*>(partials + g);
+        h.rShift = 5;   // 32 copies of each counter: lane groups never share a bank (as the histogram)
+        size_t const lds = 256u << (h.rShift + 2);
+        if (hipMemsetAsync(h.bins, 0, 256 * sizeof(unsigned long long), s) != hipSuccess)
+            return false;
+        if (contig)
+            hipLaunchKernelGGL((aggregatesFastKernel<1, codec::FmtUInt8, true, false, true>), dim3(g), dim3(kBlock), lds,
+                               s, h, static_cast<float const*>(nullptr), 0.f, partials);
+        else
+            hipLaunchKernelGGL((aggregatesFastKernel<1, codec::FmtUInt8, false, false, true>), dim3(g), dim3(kBlock), lds,
+                               s, h, static_cast<float const*>(nullptr), 0.f, partials);
+        hipLaunchKernelGGL(aggregatesCodesFinalKernel, dim3(1), dim3(kBlock), 0, s, partials, g, h.bins, a.lo, a.hi,
+                           numElems, res);
+        return true;
+    }
+
+    // Grid of the code-count pass: 32 KiB of counters per workgroup, 4 workgroups per CU; 0 when
+    // the range does not take it.
+    unsigned codeAggGrid(BoxArgs const& a)
+    {
+        FastHistArgs h;
+        bool contig;
+        if (a.fmt != codec::FmtUInt8 || rt::knob(rt::Knob::AggregatesCodes) == 0 || !makeSpanArgs(a, h, contig))
+            return 0;
+        return streamingGrid(h.items, 64u * 4u * (kBlock / 64), 4);
+    }
+
 } // hipk
 } // vkt
 
@@ -1393,7 +1604,50 @@ vktError vktHipAggregatesRange(vktHipVolumeView_t volume, vktVec3i_t first, vktV
                               static_cast<uint64_t>(volume.dimZ > 0 ? volume.dimZ : 0);
     BoxArgs a{};
     vktError e;
-    if (makeBox(volume, first, last, 0, a, "vktHipAggregatesRange: invalid volume view", e))
+    bool done = false;
+    unsigned const gc = makeBox(volume, first, last, 0, a, "vktHipAggregatesRange: invalid volume view", e)
+                            ? codeAggGrid(a)
+                            : 0u;
+    if (gc != 0)
+    {
+        // UInt8: one pass of code counts; the two float passes below only when the counts cannot
+        // give the first occurrence of an extreme (aggregatesCodesFinalKernel)
+        hipStream_t s = rt::computeStream();
+        AggScratch& sc = aggScratch();
+        size_t const bytes = (static_cast<size_t>(gc) + 2) * sizeof(vktHipAggregatePartial_t) +
+                             256 * sizeof(unsigned long long) + 16;
+        auto* partials = static_cast<vktHipAggregatePartial_t*>(sc.dev.acquire(bytes, s));
+        if (!partials)
+            return vktInvalidValue;
+        if (!sc.host && rt::check(hipHostMalloc(reinterpret_cast<void**>(&sc.host),
+                                                2 * sizeof(vktHipAggregatePartial_t)),
+                                  "hipHostMalloc") != vktNoError)
+        {
+            sc.dev.release(s);
+            return vktInvalidValue;
+        }
+        // layout: gc partials, 256 code counts, then the two results
+        auto* res = reinterpret_cast<vktHipAggregatePartial_t*>(
+            reinterpret_cast<unsigned long long*>(partials + gc) + 256);
+        bool const launched = launchCodeAggregates(a, s, static_cast<double>(numElems), partials, gc, res);
+        e = launched ? rt::check(hipMemcpyAsync(sc.host, res, 2 * sizeof(vktHipAggregatePartial_t),
+                                                hipMemcpyDeviceToHost, s),
+                                 "hipMemcpyAsync(aggregates)")
+                     : rt::fail("vktHipAggregatesRange: code-count launch failed");
+        sc.dev.release(s);
+        if (e != vktNoError)
+            return e;
+        VKT_HIP_TRY(hipStreamSynchronize(s));
+        if ((e = rt::finishLaunch("AggregatesRange_hip")) != vktNoError)
+            return e;
+        if (sc.host[1].count == 1u)
+        {
+            p1 = sc.host[0];
+            p2 = sc.host[1];
+            done = true;
+        }
+    }
+    if (!done && makeBox(volume, first, last, 0, a, "vktHipAggregatesRange: invalid volume view", e))
     {
         // both passes and the mean stay on the device: one host round trip at the end
         hipStream_t s = rt::computeStream();
@@ -1430,7 +1684,7 @@ vktError vktHipAggregatesRange(vktHipVolumeView_t volume, vktVec3i_t first, vktV
         if (e != vktNoError)
             return e;
     }
-    else if (e != vktNoError)
+    else if (!done && e != vktNoError)
         return e;
     return vktHipAggregatesFinish(&p1, &p2, numElems, volume.dimX, volume.dimY, out);
 }
