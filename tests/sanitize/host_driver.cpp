@@ -6,6 +6,9 @@
 // tests/sanitize/Makefile: AddressSanitizer + UBSan (host code of libvolkit instrumented with
 // -Xarch_host -fsanitize=...) and ThreadSanitizer.  Exit status = number of failed checks.
 #include "volkit_c.h"
+#include "runtime/HostPool.hpp"
+
+#include <atomic>
 
 #include <cmath>
 #include <cstdio>
@@ -269,6 +272,42 @@ static void threads()
         th.join();
 }
 
+// rt::parallelFor (BrickDecompose's host planning): every item visited exactly once, many jobs
+// back to back (no worker may straddle two), concurrent callers (one runs on the pool, the
+// others serially) and a nested call from inside a job.
+static void hostPool()
+{
+    for (int job = 0; job < 200; ++job)
+    {
+        size_t const n = 1000 + 997 * static_cast<size_t>(job);
+        std::vector<int> hits(n, 0);
+        vkt::rt::parallelFor(n, 64, [&](size_t b, size_t e) {
+            for (size_t i = b; i < e; ++i)
+                hits[i] += 1;
+        });
+        bool once = true;
+        for (int h : hits)
+            once = once && h == 1;
+        CHECK(once);
+    }
+    std::vector<std::thread> callers;
+    std::atomic<long> total{0};
+    for (int t = 0; t < 4; ++t)
+        callers.emplace_back([&] {
+            for (int r = 0; r < 20; ++r)
+                vkt::rt::parallelFor(50000, 256, [&](size_t b, size_t e) {
+                    long local = 0;
+                    for (size_t i = b; i < e; ++i)
+                        local += static_cast<long>(i);
+                    vkt::rt::parallelFor(4, 1, [&](size_t, size_t) {});   // nested: serial
+                    total += local;
+                });
+        });
+    for (auto& th : callers)
+        th.join();
+    CHECK(total.load() == 4L * 20L * (50000L * 49999L / 2));
+}
+
 int main(int argc, char** argv)
 {
     char const* dir = argc > 1 ? argv[1] : "/tmp";
@@ -280,6 +319,7 @@ int main(int argc, char** argv)
     algorithmsRefuseCpuPolicy();
     streams(dir);
     threads();
+    hostPool();
     std::printf("host_driver: %d failed checks\n", g_fails);
     return g_fails;
 }

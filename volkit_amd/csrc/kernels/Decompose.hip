@@ -19,6 +19,7 @@
 // interior, counted as in SURVEY.md §8(d): b_src + b_dst per voxel in range).
 
 #include "KernelCommon.hpp"
+#include "../runtime/HostPool.hpp"
 #include "../runtime/Runtime.hpp"
 #include "volkit_hip.h"
 
@@ -438,73 +439,108 @@ vktError vktHipBrickDecompose(vktHipVolumeView_t source, vktHipBrickRange_t cons
     if (!st.done)
         VKT_HIP_TRY(hipEventCreateWithFlags(&st.done, hipEventDisableTiming));
     BrickDesc* const fast = st.host;
-    size_t nFast = 0;
-    std::vector<int32_t> slow;
-    uint32_t maxItems = 0;
-    // bricks of a decomposition share a few sizes: reuse the last divisor of each kind (each
-    // makeFastDiv costs a 64-bit division; 32^3 bricks of 1024^3 are 32 768 descriptors)
-    struct LastDiv
-    {
-        FastDiv f{0u, 0u, 0u};
-        bool valid = false;
-        FastDiv operator()(uint32_t d)
-        {
-            if (!valid || f.d != d)
-            {
-                f = makeFastDiv(d);
-                valid = true;
-            }
-            return f;
-        }
-    } divSeg, divX, divWpr, divY;
     int64_t const V = 16 / bpv;                            // voxels per 16-B segment
     uint32_t const vShift = bpv == 1 ? 4u : bpv == 2 ? 3u : 2u;
     bool const srcAligned = source.dimX >= V && reinterpret_cast<uintptr_t>(source.data) % 16 == 0;
-    for (int32_t i = 0; i < numBricks; ++i)
-    {
-        vktHipBrickRange_t const& br = bricks[i];
-        if (!validView(br.brick))
-            return rt::fail("vktHipBrickDecompose: invalid brick view");
-        int64_t nx = int64_t(br.last.x) - br.first.x, ny = int64_t(br.last.y) - br.first.y;
-        int64_t nz = int64_t(br.last.z) - br.first.z;
-        if (nx <= 0 || ny <= 0 || nz <= 0)
-            continue;
-        if (nx > br.brick.dimX || ny > br.brick.dimY || nz > br.brick.dimZ)
-            return rt::fail("vktHipBrickDecompose: brick smaller than its range (reference writes out of bounds)");
-        if (overlaps(br.brick, source))
-            return rt::fail("vktHipBrickDecompose: brick aliases the source");
-        bool bytewise = br.brick.dataFormat == source.dataFormat && br.brick.mappingLo == source.mappingLo &&
-                        br.brick.mappingHi == source.mappingHi;   // Copy_serial.hpp:21-22
-        uint64_t nv = static_cast<uint64_t>(nx) * static_cast<uint64_t>(ny) * static_cast<uint64_t>(nz);
-        if (!bytewise || nv >= (1ull << 31))
+    // One descriptor per brick, at the brick's own index (a brick with an empty range or one that
+    // needs unmap -> map gets nitems = 0 and its workgroups return at once), built in parallel
+    // chunks on the host pool: 262 144 bricks of 16^3 cost ~9 ns each serially.
+    std::mutex merge;
+    std::vector<int32_t> slow;
+    uint32_t maxItems = 0;
+    int32_t errBrick = numBricks;
+    char const* errWhat = nullptr;
+    rt::parallelFor(static_cast<size_t>(numBricks), 4096, [&](size_t b, size_t e) {
+        // bricks of a decomposition share a few sizes: reuse the last divisor of each kind (each
+        // makeFastDiv costs a 64-bit division)
+        struct LastDiv
         {
-            slow.push_back(i);
-            continue;
-        }
-        BrickDesc& d = fast[nFast++];
-        d = BrickDesc{};
-        d.dst = br.brick.data;
-        d.dimX = br.brick.dimX;
-        d.dimY = br.brick.dimY;
-        d.fx = br.first.x;
-        d.fy = br.first.y;
-        d.fz = br.first.z;
-        uint32_t const seg = static_cast<uint32_t>((nx + V - 1) >> vShift);   // 16-B segments per row
-        d.nx = static_cast<int32_t>(nx);
-        d.nvox = static_cast<uint32_t>(nv);
-        d.linear = nx == br.brick.dimX && ny == br.brick.dimY && nx >= V && srcAligned &&
-                   reinterpret_cast<uintptr_t>(br.brick.data) % 16 == 0;
-        d.nitems = d.linear ? static_cast<uint32_t>((nv + V - 1) >> vShift) : static_cast<uint32_t>(ny * nz) * seg;
-        d.fseg = divSeg(seg);
-        d.fdx = divX(static_cast<uint32_t>(nx));
+            FastDiv f{0u, 0u, 0u};
+            bool valid = false;
+            FastDiv operator()(uint32_t d)
+            {
+                if (!valid || f.d != d)
+                {
+                    f = makeFastDiv(d);
+                    valid = true;
+                }
+                return f;
+            }
+        } divSeg, divX, divWpr, divY;
+        std::vector<int32_t> mySlow;
+        uint32_t myMax = 0;
+        int32_t myErr = numBricks;
+        char const* myWhat = nullptr;
+        for (size_t ii = b; ii < e; ++ii)
         {
-            int64_t const span = std::min<int64_t>(br.first.x + nx, source.dimX) - std::max<int32_t>(br.first.x, 0);
-            d.fwpr = divWpr(span > 0 ? static_cast<uint32_t>((span * bpv + 15) / 16 + 1) : 0u);
+            int32_t const i = static_cast<int32_t>(ii);
+            vktHipBrickRange_t const& br = bricks[i];
+            BrickDesc& d = fast[i];
+            d = BrickDesc{};
+            d.fx = br.first.x;
+            d.fy = br.first.y;
+            d.fz = br.first.z;
+            if (!validView(br.brick))
+            {
+                myErr = i;
+                myWhat = "vktHipBrickDecompose: invalid brick view";
+                break;
+            }
+            int64_t nx = int64_t(br.last.x) - br.first.x, ny = int64_t(br.last.y) - br.first.y;
+            int64_t nz = int64_t(br.last.z) - br.first.z;
+            if (nx <= 0 || ny <= 0 || nz <= 0)
+                continue;
+            if (nx > br.brick.dimX || ny > br.brick.dimY || nz > br.brick.dimZ)
+            {
+                myErr = i;
+                myWhat = "vktHipBrickDecompose: brick smaller than its range (reference writes out of bounds)";
+                break;
+            }
+            if (overlaps(br.brick, source))
+            {
+                myErr = i;
+                myWhat = "vktHipBrickDecompose: brick aliases the source";
+                break;
+            }
+            bool bytewise = br.brick.dataFormat == source.dataFormat && br.brick.mappingLo == source.mappingLo &&
+                            br.brick.mappingHi == source.mappingHi;   // Copy_serial.hpp:21-22
+            uint64_t nv = static_cast<uint64_t>(nx) * static_cast<uint64_t>(ny) * static_cast<uint64_t>(nz);
+            if (!bytewise || nv >= (1ull << 31))
+            {
+                mySlow.push_back(i);
+                continue;
+            }
+            d.dst = br.brick.data;
+            d.dimX = br.brick.dimX;
+            d.dimY = br.brick.dimY;
+            uint32_t const seg = static_cast<uint32_t>((nx + V - 1) >> vShift);   // 16-B segments per row
+            d.nx = static_cast<int32_t>(nx);
+            d.nvox = static_cast<uint32_t>(nv);
+            d.linear = nx == br.brick.dimX && ny == br.brick.dimY && nx >= V && srcAligned &&
+                       reinterpret_cast<uintptr_t>(br.brick.data) % 16 == 0;
+            d.nitems = d.linear ? static_cast<uint32_t>((nv + V - 1) >> vShift) : static_cast<uint32_t>(ny * nz) * seg;
+            d.fseg = divSeg(seg);
+            d.fdx = divX(static_cast<uint32_t>(nx));
+            {
+                int64_t const span = std::min<int64_t>(br.first.x + nx, source.dimX) - std::max<int32_t>(br.first.x, 0);
+                d.fwpr = divWpr(span > 0 ? static_cast<uint32_t>((span * bpv + 15) / 16 + 1) : 0u);
+            }
+            d.fdy = divY(static_cast<uint32_t>(ny));
+            myMax = d.nitems > myMax ? d.nitems : myMax;
         }
-        d.fdy = divY(static_cast<uint32_t>(ny));
-        maxItems = d.nitems > maxItems ? d.nitems : maxItems;
-    }
-
+        std::lock_guard<std::mutex> g(merge);
+        slow.insert(slow.end(), mySlow.begin(), mySlow.end());
+        maxItems = std::max(maxItems, myMax);
+        if (myErr < errBrick)
+        {
+            errBrick = myErr;
+            errWhat = myWhat;
+        }
+    });
+    if (errWhat != nullptr)   // the first bad brick in list order, before anything launched
+        return rt::fail(errWhat);
+    std::sort(slow.begin(), slow.end());
+    size_t const nFast = maxItems > 0 ? static_cast<size_t>(numBricks) : 0;
     hipStream_t s = rt::computeStream();
     if (nFast > 0)
     {
