@@ -471,7 +471,7 @@ def main():
         ep.device = vkt.ExecutionPolicy.Device_GPU
         vkt.SetThreadExecutionPolicy(ep)
         n = 1024
-        cases = [(64, (1, 1, 1)), (128, (0, 0, 0)), (32, (1, 1, 1))]
+        cases = [(64, (1, 1, 1)), (128, (0, 0, 0)), (32, (1, 1, 1)), (16, (1, 1, 1))]
         if os.environ.get("VKT_DECOMP_CASES"):   # "bs:hx,hy,hz;..."
             cases = [(int(c.split(":")[0]), tuple(int(h) for h in c.split(":")[1].split(",")))
                      for c in os.environ["VKT_DECOMP_CASES"].split(";")]

@@ -145,7 +145,7 @@ int hostThreads()
                 return std::min(v, 64);
         }
         unsigned const hw = std::thread::hardware_concurrency();
-        return static_cast<int>(std::max(1u, std::min(8u, hw)));
+        return static_cast<int>(std::max(1u, std::min(16u, hw)));
     }();
     return n;
 }

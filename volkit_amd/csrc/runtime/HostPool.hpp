@@ -16,7 +16,7 @@ namespace rt
     // the calling thread.  Worker threads start with the calling thread's HIP device.
     void parallelFor(size_t n, size_t minChunk, std::function<void(size_t, size_t)> const& fn);
 
-    // Threads parallelFor uses: VKT_HOST_THREADS if set (1 = serial), else min(8, cores).
+    // Threads parallelFor uses: VKT_HOST_THREADS if set (1 = serial), else min(16, cores).
     int hostThreads();
 } // rt
 } // vkt

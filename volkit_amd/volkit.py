@@ -120,7 +120,7 @@ class StructuredVolume:
         lib.vktStructuredVolumeCreateCopy(C.byref(h), other._h)
         return cls(_handle=h)
 
-    def __del__(self):
+    def __del__(self, lib=lib):   # bound now: module globals are gone at interpreter exit
         h = getattr(self, "_h", None)
         if h is not None and h.value and getattr(self, "_owner", None) is None:
             lib.vktStructuredVolumeDestroy(h)
@@ -391,7 +391,7 @@ class Array3D_StructuredVolume:
             lib.vktArray3D_vktStructuredVolume_Create(C.byref(h), Vec3i_t(*_ints([dims], 3)))
         self._h = h
 
-    def __del__(self):
+    def __del__(self, lib=lib):   # bound now: module globals are gone at interpreter exit
         h = getattr(self, "_h", None)
         if h is not None and h.value:
             lib.vktArray3D_vktStructuredVolume_Destroy(h)
@@ -490,7 +490,7 @@ class Histogram:
         lib.vktHistogramCreate(C.byref(h), int(numBins))
         self._h = h
 
-    def __del__(self):
+    def __del__(self, lib=lib):   # bound now: module globals are gone at interpreter exit
         h = getattr(self, "_h", None)
         if h is not None and h.value:
             lib.vktHistogramDestroy(h)
@@ -537,7 +537,7 @@ class RawFile:
         lib.vktRawFileCreateS(C.byref(h), self._name, mode.encode())
         self._h = h
 
-    def __del__(self):
+    def __del__(self, lib=lib):   # bound now: module globals are gone at interpreter exit
         h = getattr(self, "_h", None)
         if h is not None and h.value:
             lib.vktRawFileDestroy(h)
@@ -574,7 +574,7 @@ class InputStream:
         lib.vktInputStreamCreate(C.byref(h), source.base())
         self._h, self._source = h, source
 
-    def __del__(self):
+    def __del__(self, lib=lib):   # bound now: module globals are gone at interpreter exit
         h = getattr(self, "_h", None)
         if h is not None and h.value:
             lib.vktInputStreamDestroy(h)
@@ -596,7 +596,7 @@ class OutputStream:
         lib.vktOutputStreamCreate(C.byref(h), source.base())
         self._h, self._source = h, source
 
-    def __del__(self):
+    def __del__(self, lib=lib):   # bound now: module globals are gone at interpreter exit
         h = getattr(self, "_h", None)
         if h is not None and h.value:
             lib.vktOutputStreamDestroy(h)
@@ -641,7 +641,7 @@ class LookupTable:
         lib.vktLookupTableCreate(C.byref(h), int(dimX), int(dimY), int(dimZ), int(colorFormat))
         self._h = h
 
-    def __del__(self):
+    def __del__(self, lib=lib):   # bound now: module globals are gone at interpreter exit
         h = getattr(self, "_h", None)
         if h is not None and h.value:
             lib.vktLookupTableDestroy(h)
