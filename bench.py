@@ -477,7 +477,8 @@ def config4_strong(ctx, vkt, slab, lib, args, layout_n, stream):
 
     def step(ev):
         if plan.recvs or plan.sends:
-            slab.exchange_planes(plan, planes)
+            with slab.library_stream():   # the halo moves in order with the library's kernels
+                slab.exchange_planes(plan, planes)
         if ev:
             ev[0].record(stream)
         e1 = lib.vktHipResampleSlab(rv, sv, LINEAR, E, dz0, Sx, ls0)
