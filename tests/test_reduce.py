@@ -453,6 +453,14 @@ def test_aggregates_uint8_code_counts(mapping):
         a, b = runs
         assert (a.min, a.max, tuple(a.argmin), tuple(a.argmax), a.mean) == (b.min, b.max, tuple(b.argmin),
                                                                           tuple(b.argmax), b.mean)
+    # extremes that first occur after the first 512 Ki voxels of the range (the whole-grid
+    # second stage of the first-occurrence search), once in a span and once in a padded box
+    codes = rng.integers(2, 254, (16, 64, 1024), dtype=np.uint8)
+    codes[12, 5, 700] = codes[14, 0, 3] = 1
+    codes[15, 63, 1000] = codes[13, 9, 9] = 254
+    for first, last in (((0, 0, 0), (1024, 64, 16)), ((3, 1, 0), (1021, 64, 16))):
+        got = gpu_aggregates(codes, 4, *mapping, first, last)
+        check_aggregates(got, codes, 4, mapping, first, last, f"late extremes map={mapping} {first}->{last}")
     # product through value^count: 256 voxels of 1.01 (code 255 under (0, 1.01)), ~12.8
     codes = np.full((2, 2, 64), 255, np.uint8)
     got = gpu_aggregates(codes, 4, 0.0, 1.01, (0, 0, 0), (64, 2, 2))

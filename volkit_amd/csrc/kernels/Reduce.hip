@@ -756,12 +756,13 @@ namespace hipk
     // exact whatever the schedule.  Sums accumulate per lane in double, then the fixed
     // shuffle / LDS / partials tree (deterministic for a given grid).
     // UNIT: the mapping is the unit mapping (+0, 1), decode without the lerp (codec::decodeUnit).
-    // CODES (UInt8, pass 1): no decode and no float terms at all -- every voxel of a UInt8 volume
-    // has one of 256 values, so the kernel counts CODES (LDS counters, 2^rShift copies, flushed to
-    // the 256 u64 bins h.bins) and tracks the first occurrence of the smallest and largest code per
-    // lane (integer compares; minValue / maxValue of the partial hold the codes).  The sums, the
-    // product and the second pass's sum of squares follow from the 256 counts
-    // (aggregatesCodesFinalKernel): one pass over the data instead of two.
+    // CODES (UInt8, pass 1): no decode, no float terms and no compares -- every voxel of a UInt8
+    // volume has one of 256 values, so the kernel only counts CODES (LDS counters, 2^rShift
+    // copies, flushed to the 256 u64 bins h.bins; no partials).  The sums, the product, the second
+    // pass's sum of squares and the extreme values follow from the 256 counts
+    // (aggregatesCodesFinalKernel); the first occurrence of each extreme's code is searched from
+    // the start of the range (aggregatesFindHeadKernel, which stops early): one pass over the
+    // data instead of two.
     template <int PASS, int FMT, bool CONTIG, bool UNIT = false, bool CODES = false>
     __global__ __launch_bounds__(kBlock) void aggregatesFastKernel(FastHistArgs h, float const* meanPtr,
                                                                   float meanValue, vktHipAggregatePartial_t* partials)
@@ -775,7 +776,6 @@ namespace hipk
         extern __shared__ uint32_t codeCnt[];
         uint32_t const rowShift = h.rShift + 2;
         char* const cLane = reinterpret_cast<char*>(codeCnt) + ((lane & ((1u << h.rShift) - 1u)) << 2);
-        int32_t cmin = 256, cmax = -1;   // CODES: this lane's smallest / largest code so far
         if constexpr (CODES)
         {
             for (uint32_t i = threadIdx.x; i < (256u << h.rShift); i += kBlock)
@@ -810,38 +810,10 @@ namespace hipk
             };
             if constexpr (CODES)
             {
-                int32_t lo = 256, hi = -1;
 #pragma unroll
                 for (int j = 0; j < 8; ++j)
                     if ((m >> j) & 1u)
-                    {
                         atomicAdd(reinterpret_cast<uint32_t*>(cLane + (c[j] << rowShift)), 1u);
-                        lo = min(lo, static_cast<int32_t>(c[j]));
-                        hi = max(hi, static_cast<int32_t>(c[j]));
-                    }
-                if (lo < cmin || hi > cmax)   // rare after the first items: voxel order only then
-                {
-#pragma unroll
-                    for (int j = 0; j < 8; ++j)
-                    {
-                        int32_t const cj = static_cast<int32_t>(c[j]);
-                        if (((m >> j) & 1u) && (cj < cmin || cj > cmax))
-                        {
-                            uint64_t const gi = gIndex(j);
-                            if (cj < cmin)
-                            {
-                                cmin = cj;
-                                p.minIndex = gi;
-                            }
-                            if (cj > cmax)
-                            {
-                                cmax = cj;
-                                p.maxIndex = gi;
-                            }
-                        }
-                    }
-                }
-                p.count += __builtin_popcount(m);
                 return;
             }
             // pass 1 over spans: one test per item (its min / max against the lane's) instead of
@@ -963,10 +935,6 @@ namespace hipk
         }
         if constexpr (CODES)
         {
-            if (cmin <= 255)
-                p.minValue = static_cast<float>(cmin);
-            if (cmax >= 0)
-                p.maxValue = static_cast<float>(cmax);
             __syncthreads();
             uint32_t const R = 1u << h.rShift;
             for (uint32_t b = threadIdx.x; b < 256u; b += kBlock)
@@ -977,6 +945,7 @@ namespace hipk
                 if (sum)
                     atomicAdd(&h.bins[b], static_cast<unsigned long long>(sum));
             }
+            return;
         }
         blockReduce(p);
         if (threadIdx.x == 0)
@@ -988,33 +957,20 @@ namespace hipk
     // product and count * (float)((value - mean)^2) to the sum of squares -- the per-voxel float
     // terms of Aggregates_serial.hpp:37-80, summed in double in another order (the same parity
     // bound as the streaming passes).  min / max are the extreme VALUES among the present codes;
-    // argmin / argmax the first occurrence of the code holding each, which the data pass tracked
-    // for the smallest and the largest code.  res[1].count = 1 when that holds: every present
-    // value finite and below FLT_MAX in magnitude, each extreme held by ONE code (a mapping that
-    // rounds two codes to one value, or a decreasing one with ties, makes the caller rerun the
-    // two float passes), and that code the smallest or the largest present one; 0 otherwise.
-    __global__ __launch_bounds__(kBlock) void aggregatesCodesFinalKernel(vktHipAggregatePartial_t const* partials,
-                                                                        uint32_t n, unsigned long long const* counts,
-                                                                        float lo, float hi, double numElems,
-                                                                        vktHipAggregatePartial_t* res)
+    // targets[0] / [1] the code holding each, whose first occurrence aggregatesFindHead/TailKernel
+    // then write to res[0].minIndex / maxIndex.  res[1].count = 1 when the counts determine the
+    // result: every present value finite and below FLT_MAX in magnitude and each extreme held by
+    // ONE code (a mapping that rounds two present codes onto an extreme makes the caller rerun
+    // the two float passes); 0 otherwise (targets -1).
+    __global__ __launch_bounds__(kBlock) void aggregatesCodesFinalKernel(unsigned long long const* counts, float lo,
+                                                                        float hi, double numElems,
+                                                                        vktHipAggregatePartial_t* res,
+                                                                        int32_t* targets)
     {
-        vktHipAggregatePartial_t p = emptyPartial();
-        for (uint32_t i = threadIdx.x; i < n; i += blockDim.x)
-        {
-            vktHipAggregatePartial_t const& o = partials[i];
-            minCombine(p.minValue, p.minIndex, o.minValue, o.minIndex);
-            maxCombine(p.maxValue, p.maxIndex, o.maxValue, o.maxIndex);
-        }
-        blockReduce(p);
-        __shared__ float sLoCode, sHiCode, sVmin, sVmax, sMean;
-        __shared__ uint64_t sLoIdx, sHiIdx;
+        __shared__ float sVmin, sVmax, sMean;
         __shared__ int32_t sNmin, sNmax, sCmin, sCmax, sBad;
         if (threadIdx.x == 0)
         {
-            sLoCode = p.minValue;
-            sHiCode = p.maxValue;
-            sLoIdx = p.minIndex;
-            sHiIdx = p.maxIndex;
             sNmin = sNmax = sBad = 0;
             sCmin = sCmax = -1;
         }
@@ -1066,25 +1022,115 @@ namespace hipk
         __syncthreads();
         if (threadIdx.x == 0)
         {
-            auto indexOf = [&](int32_t code, bool& ok) -> uint64_t {
-                if (code >= 0 && static_cast<float>(code) == sLoCode)
-                    return sLoIdx;
-                if (code >= 0 && static_cast<float>(code) == sHiCode)
-                    return sHiIdx;
-                ok = false;
-                return kNoIndex;
-            };
-            bool ok = sBad == 0 && sNmin == 1 && sNmax == 1;
+            bool const ok = sBad == 0 && sNmin == 1 && sNmax == 1;
             vktHipAggregatePartial_t out = r;
             out.sumSq = 0.0;
-            out.minIndex = indexOf(sCmin, ok);
-            out.maxIndex = indexOf(sCmax, ok);
+            out.minIndex = kNoIndex;   // set by aggregatesFindHead/TailKernel
+            out.maxIndex = kNoIndex;
             res[0] = out;
             vktHipAggregatePartial_t two = emptyPartial();
             two.sumSq = t.sumSq;
             two.count = ok ? 1u : 0u;
             res[1] = two;
+            targets[0] = ok ? sCmin : -1;
+            targets[1] = ok ? sCmax : -1;
         }
+    }
+
+    // global linear index of voxel j of 8-voxel item `item` of a span walk (FastHistArgs)
+    template <bool CONTIG>
+    __device__ __forceinline__ uint64_t spanGlobalIndex(FastHistArgs const& h, uint64_t item, int j)
+    {
+        if constexpr (CONTIG)
+            return h.giBase + item * 8 + static_cast<uint64_t>(j);
+        else
+        {
+            uint32_t const i = static_cast<uint32_t>(item);
+            uint32_t const r = fdiv(i, h.fdIpr);
+            uint32_t const xi = i - r * h.fdIpr.d;
+            uint32_t const zr = fdiv(r, h.fdNy);
+            uint32_t const yr = r - zr * h.fdNy.d;
+            return (static_cast<uint64_t>(h.fz + zr + h.zGlobal) * static_cast<uint64_t>(h.dimY) +
+                    static_cast<uint64_t>(h.fy + yr)) *
+                       static_cast<uint64_t>(h.dimX) +
+                   static_cast<uint64_t>(h.px0) + 8ull * xi + static_cast<uint64_t>(j);
+        }
+    }
+
+    // The first voxels of item `item` holding codes tmin / tmax, folded into *bMin / *bMax with
+    // atomicMin (LDS or global).
+    template <bool CONTIG>
+    __device__ __forceinline__ void findCodes(FastHistArgs const& h, uint64_t item, int32_t tmin, int32_t tmax,
+                                              unsigned long long* bMin, unsigned long long* bMax)
+    {
+        uint32_t c[8];
+        load8<1, true>(h.data, spanVoxel<CONTIG>(h, item), c);
+        uint32_t const m = itemMask<CONTIG>(h, item);
+        int jMin = 8, jMax = 8;
+#pragma unroll
+        for (int j = 7; j >= 0; --j)
+            if ((m >> j) & 1u)
+            {
+                jMin = static_cast<int32_t>(c[j]) == tmin ? j : jMin;
+                jMax = static_cast<int32_t>(c[j]) == tmax ? j : jMax;
+            }
+        if (jMin < 8)
+            atomicMin(bMin, static_cast<unsigned long long>(spanGlobalIndex<CONTIG>(h, item, jMin)));
+        if (jMax < 8)
+            atomicMin(bMax, static_cast<unsigned long long>(spanGlobalIndex<CONTIG>(h, item, jMax)));
+    }
+
+    // First occurrence of codes targets[0] / targets[1] (the extremes' codes), stage 1: ONE
+    // workgroup walks the first `headItems` items of the range in order, 1024 items per step,
+    // with LDS atomics, and stops at the first step after which both are known (on varied data,
+    // the first step: 8 Ki voxels).  Writes res[0].minIndex / maxIndex (kNoIndex if not found).
+    // One workgroup, because many waves folding into one global word serialise on it (a
+    // whole-grid version with global atomics and early exit took 0.35 ms).
+    template <bool CONTIG>
+    __global__ __launch_bounds__(1024) void aggregatesFindHeadKernel(FastHistArgs h, int32_t const* targets,
+                                                                    vktHipAggregatePartial_t* res, uint64_t headItems)
+    {
+        int32_t const tmin = targets[0], tmax = targets[1];
+        if (tmin < 0 || tmax < 0)
+            return;
+        __shared__ unsigned long long sMin, sMax;
+        if (threadIdx.x == 0)
+            sMin = sMax = kNoIndex;
+        __syncthreads();
+        uint64_t const end = headItems < h.items ? headItems : h.items;
+        for (uint64_t base = 0; base < end; base += blockDim.x)
+        {
+            uint64_t const item = base + threadIdx.x;
+            if (item < end)
+                findCodes<CONTIG>(h, item, tmin, tmax, &sMin, &sMax);
+            __syncthreads();
+            bool const done = sMin != kNoIndex && sMax != kNoIndex;
+            __syncthreads();   // every thread has read before the next step's atomics
+            if (done)
+                break;
+        }
+        if (threadIdx.x == 0)
+        {
+            res[0].minIndex = sMin;
+            res[0].maxIndex = sMax;
+        }
+    }
+
+    // Stage 2, the whole grid over the items after the head -- only when stage 1 left a code
+    // unfound (it then occurs rarely, so few lanes fold into the global words).
+    template <bool CONTIG>
+    __global__ __launch_bounds__(kBlock) void aggregatesFindTailKernel(FastHistArgs h, int32_t const* targets,
+                                                                      vktHipAggregatePartial_t* res, uint64_t headItems)
+    {
+        int32_t const tmin = targets[0], tmax = targets[1];
+        if (tmin < 0 || tmax < 0 || (res[0].minIndex != kNoIndex && res[0].maxIndex != kNoIndex))
+            return;   // (stage 1's stores are visible: a kernel boundary lies between)
+        auto* const bMin = reinterpret_cast<unsigned long long*>(&res[0].minIndex);
+        auto* const bMax = reinterpret_cast<unsigned long long*>(&res[0].maxIndex);
+        uint64_t const stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+        for (uint64_t item = headItems + static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; item < h.items;
+             item += stride)
+            findCodes<CONTIG>(h, item, tmin, tmax, bMin, bMax);
     }
 
     __global__ void zeroU64Kernel(unsigned long long* p, uint64_t n)
@@ -1445,8 +1491,9 @@ namespace hipk
         return s;
     }
 
-    // UInt8 aggregates in one data pass (aggregatesFastKernel<CODES> + aggregatesCodesFinalKernel
-    // into res[0], res[1]); false when the range does not take the streaming walk.
+    // UInt8 aggregates in one data pass (aggregatesFastKernel<CODES>, aggregatesCodesFinalKernel,
+    // aggregatesFind{Head,Tail}Kernel into res[0], res[1]); false when the range does not take the
+    // streaming walk.  scratch: 256 code counts, then 2 target codes.
     bool launchCodeAggregates(BoxArgs const& a, hipStream_t s, double numElems, void* scratch, unsigned g,
                               vktHipAggregatePartial_t* res)
     {
@@ -1454,20 +1501,33 @@ namespace hipk
         bool contig;
         if (!makeSpanArgs(a, h, contig))
             return false;
-        auto* partials = static_cast<vktHipAggregatePartial_t*>(scratch);
-        h.bins = reinterpret_cast<unsigned long long*>(partials + g);
+        h.bins = static_cast<unsigned long long*>(scratch);
+        auto* const targets = reinterpret_cast<int32_t*>(h.bins + 256);
         h.rShift = 5;   // 32 copies of each counter: lane groups never share a bank (as the histogram)
         size_t const lds = 256u << (h.rShift + 2);
         if (hipMemsetAsync(h.bins, 0, 256 * sizeof(unsigned long long), s) != hipSuccess)
             return false;
+        auto* const none = static_cast<vktHipAggregatePartial_t*>(nullptr);
         if (contig)
             hipLaunchKernelGGL((aggregatesFastKernel<1, codec::FmtUInt8, true, false, true>), dim3(g), dim3(kBlock), lds,
-                               s, h, static_cast<float const*>(nullptr), 0.f, partials);
+                               s, h, static_cast<float const*>(nullptr), 0.f, none);
         else
             hipLaunchKernelGGL((aggregatesFastKernel<1, codec::FmtUInt8, false, false, true>), dim3(g), dim3(kBlock), lds,
-                               s, h, static_cast<float const*>(nullptr), 0.f, partials);
-        hipLaunchKernelGGL(aggregatesCodesFinalKernel, dim3(1), dim3(kBlock), 0, s, partials, g, h.bins, a.lo, a.hi,
-                           numElems, res);
+                               s, h, static_cast<float const*>(nullptr), 0.f, none);
+        hipLaunchKernelGGL(aggregatesCodesFinalKernel, dim3(1), dim3(kBlock), 0, s, h.bins, a.lo, a.hi, numElems, res,
+                           targets);
+        uint64_t const head = 64u * 1024u;   // stage 1 covers the first 512 Ki voxels at most
+        unsigned const gf = std::max(1u, std::min(g, static_cast<unsigned>((h.items + kBlock - 1) / kBlock)));
+        if (contig)
+        {
+            hipLaunchKernelGGL((aggregatesFindHeadKernel<true>), dim3(1), dim3(1024), 0, s, h, targets, res, head);
+            hipLaunchKernelGGL((aggregatesFindTailKernel<true>), dim3(gf), dim3(kBlock), 0, s, h, targets, res, head);
+        }
+        else
+        {
+            hipLaunchKernelGGL((aggregatesFindHeadKernel<false>), dim3(1), dim3(1024), 0, s, h, targets, res, head);
+            hipLaunchKernelGGL((aggregatesFindTailKernel<false>), dim3(gf), dim3(kBlock), 0, s, h, targets, res, head);
+        }
         return true;
     }
 
@@ -1614,10 +1674,9 @@ vktError vktHipAggregatesRange(vktHipVolumeView_t volume, vktVec3i_t first, vktV
         // give the first occurrence of an extreme (aggregatesCodesFinalKernel)
         hipStream_t s = rt::computeStream();
         AggScratch& sc = aggScratch();
-        size_t const bytes = (static_cast<size_t>(gc) + 2) * sizeof(vktHipAggregatePartial_t) +
-                             256 * sizeof(unsigned long long) + 16;
-        auto* partials = static_cast<vktHipAggregatePartial_t*>(sc.dev.acquire(bytes, s));
-        if (!partials)
+        size_t const bytes = 2 * sizeof(vktHipAggregatePartial_t) + 256 * sizeof(unsigned long long) + 16;
+        auto* res = static_cast<vktHipAggregatePartial_t*>(sc.dev.acquire(bytes, s));
+        if (!res)
             return vktInvalidValue;
         if (!sc.host && rt::check(hipHostMalloc(reinterpret_cast<void**>(&sc.host),
                                                 2 * sizeof(vktHipAggregatePartial_t)),
@@ -1626,10 +1685,8 @@ vktError vktHipAggregatesRange(vktHipVolumeView_t volume, vktVec3i_t first, vktV
             sc.dev.release(s);
             return vktInvalidValue;
         }
-        // layout: gc partials, 256 code counts, then the two results
-        auto* res = reinterpret_cast<vktHipAggregatePartial_t*>(
-            reinterpret_cast<unsigned long long*>(partials + gc) + 256);
-        bool const launched = launchCodeAggregates(a, s, static_cast<double>(numElems), partials, gc, res);
+        // layout: the two results, then 256 code counts and the 2 target codes
+        bool const launched = launchCodeAggregates(a, s, static_cast<double>(numElems), res + 2, gc, res);
         e = launched ? rt::check(hipMemcpyAsync(sc.host, res, 2 * sizeof(vktHipAggregatePartial_t),
                                                 hipMemcpyDeviceToHost, s),
                                  "hipMemcpyAsync(aggregates)")
