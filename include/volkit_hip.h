@@ -108,8 +108,8 @@ VKTAPI vktError vktHipKernelScopeEnd(vktHipKernelScope scope);
  * (6; 5 or 8 source words in flight per thread), "pointwise.u8_wide" (1; 0 keeps UInt8 boxes of the
  * general path on 8-voxel items), "pointwise.f32_halves" (1; 0 keeps 4-byte padded multi-row boxes
  * on the per-item loop), "pointwise.f32_wide" (0; 1 gives 4-byte general-path boxes 16-B items),
- * "aggregates.codes" (1; 0 makes UInt8 ComputeAggregates take the two float passes instead of one
- * pass of code counts).  For tests and in-process A/B measurements; unknown names return
+ * "aggregates.codes" (3; bit 0 UInt8, bit 1 UInt16: ComputeAggregates from one pass of code counts
+ * instead of the two float passes).  For tests and in-process A/B measurements; unknown names return
  * vktInvalidValue.
  *
  * Writes outside a range box: FillRange / CopyRange / convert and device-functor TransformRange
@@ -351,6 +351,27 @@ VKTAPI vktError vktHipAggregatesPass(vktHipVolumeView_t volume, vktVec3i_t first
                                      vktHipAggregatePartial_t* partial);
 VKTAPI vktError vktHipAggregatesFinish(vktHipAggregatePartial_t const* pass1, vktHipAggregatePartial_t const* pass2,
                                        uint64_t numElems, int32_t dimX, int32_t dimY, vktAggregates_t* aggregates);
+/* UInt8 / UInt16 slabs in ONE pass (the code-count form of vktHipAggregatesRange, DESIGN.md
+ * §4.8): every rank counts the codes of its range (vktHipAggregateCodeCounts: a DEVICE array of
+ * 256 / 65 536 uint64 counters, overwritten); the counts are summed over the ranks (one
+ * all-reduce); vktHipAggregatesFromCodes turns the global counts into pass 1 (sum, prod, count,
+ * min / max values; indices ~0) and pass 2 (sumSq) and names the code holding each extreme
+ * (codes[0] min, codes[1] max; -1 when the counts cannot tell which voxel comes first: a mapping
+ * that rounds two present codes onto an extreme or a non-finite value -- then use the two
+ * passes); each rank searches its range for the first voxels with those codes
+ * (vktHipAggregateFirstCodes, global indices as vktHipAggregatesPass, ~0 = none), the minimum
+ * over ranks fills pass1.minIndex / maxIndex, and vktHipAggregatesFinish completes.
+ * vktHipAggregateCodesSupported: 1 when the range takes the code-count walk (a 16-B aligned
+ * volume with dimX % 8 == 0; empty ranges too), else 0. */
+VKTAPI int32_t vktHipAggregateCodesSupported(vktHipVolumeView_t volume, vktVec3i_t first, vktVec3i_t last);
+VKTAPI vktError vktHipAggregateCodeCounts(vktHipVolumeView_t volume, vktVec3i_t first, vktVec3i_t last,
+                                          uint64_t* counts);
+VKTAPI vktError vktHipAggregatesFromCodes(uint64_t const* counts, int32_t dataFormat, float mappingLo, float mappingHi,
+                                          uint64_t numElems, vktHipAggregatePartial_t* pass1,
+                                          vktHipAggregatePartial_t* pass2, int32_t* codes);
+VKTAPI vktError vktHipAggregateFirstCodes(vktHipVolumeView_t volume, vktVec3i_t first, vktVec3i_t last,
+                                          int32_t zGlobalOffset, int32_t minCode, int32_t maxCode,
+                                          uint64_t* indices);
 
 /* replaces ComputeHistogramRange_cuda (reference src/vkt/Histogram_cuda.cu:45-76, which
  * ignores `first`); semantics of ComputeHistogramRange_serial (src/vkt/Histogram_serial.hpp:

@@ -2,6 +2,8 @@
 exchange -- the driver's 8-GPU node uses RCCL), each holding only its own Z-slab in HBM and
 running the real HIP kernels:
   * slab.aggregates (pass 1 / all_gather / mean / pass 2 / all_gather) == whole-volume oracle;
+    on UInt8 / UInt16 slabs the one-pass code-count form (all_reduce of the code counts, first-
+    occurrence search per slab, all_reduce MIN of the indices), also == the oracle;
   * slab.histogram (local counts on the device, all_reduce) == whole-volume oracle, exactly;
   * Float32 "Linear" Resample with the z+1 halo received from the neighbour rank == the
     rank's slab of the whole-volume oracle resample;
@@ -36,6 +38,15 @@ def _global_volume():
     return vals
 
 
+def _code_volume(fmt):
+    top = 255 if fmt == 4 else 65535
+    rng = np.random.default_rng(31 + fmt)
+    codes = rng.integers(2, top - 1, (20, 24, 64)).astype(np.uint8 if fmt == 4 else np.uint16)
+    codes[15, 3, 9] = codes[18, 0, 0] = 1              # the minimum only in the second slab
+    codes[4, 20, 60] = codes[14, 2, 2] = top - 1
+    return codes
+
+
 def _worker(rank, port, q):
     try:
         os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -64,6 +75,18 @@ def _worker(rank, port, q):
             out[(first, last)] = ((a.min, a.max, (a.argmin.x, a.argmin.y, a.argmin.z),
                                    (a.argmax.x, a.argmax.y, a.argmax.z), a.sum, a.mean, a.var),
                                   bins.cpu().numpy().copy())
+        # UInt8 / UInt16 slabs: the one-pass code-count form (counts on the device, all_reduce,
+        # first-occurrence search per slab, all_reduce MIN of the indices)
+        for fmt, mapping in ((5, (-1.0, 3.0)), (4, (0.0, 1.0)), (4, (3.0, -1.0))):
+            codes = _code_volume(fmt)
+            cz, cy, cx = codes.shape
+            c0, c1 = slab.slab_bounds(cz, WORLD, rank)
+            cv = vkt.StructuredVolume(cx, cy, c1 - c0, fmt, 1.0, 1.0, 1.0, *mapping)
+            cv.from_numpy(np.ascontiguousarray(codes[c0:c1]))
+            for first, last in (((0, 0, 0), (cx, cy, cz)), ((3, 1, 2), (cx - 5, cy, cz - 1))):
+                a = slab.aggregates(cv.hip_view(), (cx, cy, cz), c0, first, last, device="cuda")
+                out[("codes", fmt, mapping, first, last)] = (a.min, a.max, (a.argmin.x, a.argmin.y, a.argmin.z),
+                                                             (a.argmax.x, a.argmax.y, a.argmax.z), a.sum, a.mean, a.var)
         # Float32 Linear resample 2x with the halo exchanged over the process group
         dz = 2 * gz
         plan = slab.plan_resample(dz, gz, WORLD, rank, vkt.FilterMode_Linear, chain=True)
@@ -172,6 +195,16 @@ def test_two_ranks_on_one_gpu():
         assert np.array_equal(got_s, ref_s.codes[z0:z1].reshape(-1)), f"rank {r}: slab arithmetic_range differs"
         d0, dk, d1 = out.pop("split")
         assert d0 < dk < d1 or not halo, (r, d0, dk, d1)   # a rank with a halo has an interior
+    for key in [k for k in res[0][1] if k[0] == "codes"]:
+        _, fmt, mapping, first, last = key
+        codes = _code_volume(fmt)
+        ref = ob.aggregates_range(ob.Volume(codes, fmt, *mapping), first, last)
+        for r, out, _, _ in res:
+            mn, mx, amin, amax, s, mean, var = out.pop(key)
+            assert (mn, mx, amin, amax) == (ref.min, ref.max, tuple(ref.argmin), tuple(ref.argmax)), (r, key)
+            n = np.prod(np.subtract(last, first))
+            assert abs(s - ref.sum) <= n * 2.0 ** -24 * abs(ref.sum) + 1e-6, (r, key)
+            assert abs(var - ref.var) <= 4 * n * 2.0 ** -24 * abs(ref.var) + 1e-7, (r, key)
     for key in res[0][1]:
         first, last = key
         ref = ob.aggregates_range(whole, first, last)

@@ -424,47 +424,49 @@ def check_aggregates(got, codes, fmt, mapping, first, last, what):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("fmt", [4, 5])
 @pytest.mark.parametrize("mapping", [(0.0, 1.0), (3.0, -1.0), (-2.0, 5.0), (1000.0, 1000.001), (0.25, 0.25)])
-def test_aggregates_uint8_code_counts(mapping):
-    """UInt8 ComputeAggregates from one pass of code counts (knob aggregates.codes):
+def test_aggregates_code_counts(fmt, mapping):
+    """UInt8 / UInt16 ComputeAggregates from one pass of code counts (knob aggregates.codes):
     increasing and decreasing mappings (the value minimum is then the LARGEST code), a mapping
     that rounds neighbouring codes to one value and a constant one (extremes held by several
     codes: the library reruns the two float passes), tied extremes across lanes, waves and
     padded end items; equal to the oracle and to the two-pass path (knob 0)."""
-    rng = np.random.default_rng(17)
+    rng = np.random.default_rng(17 + fmt)
+    top, dt = (255, np.uint8) if fmt == 4 else (65535, np.uint16)
     cases = [((24, 40, 1040), (0, 0, 0), (1040, 40, 24)),      # one span
              ((24, 40, 1040), (3, 1, 2), (1037, 39, 23)),       # padded rows
              ((10, 64, 256), (8, 3, 2), (200, 60, 9))]          # strided box
     for dims, first, last in cases:
-        codes = rng.integers(2, 254, dims, dtype=np.uint8)
+        codes = rng.integers(2, top - 1, dims, dtype=dt)
         for z, y, x in ((5, 7, 9), (2, 3, 1000 % dims[2]), (8, 30, 40)):
             codes[z, y, x] = 1
         for z, y, x in ((6, 1, 511 % dims[2]), (6, 1, 13), (9, 38, 8)):
-            codes[z, y, x] = 254
+            codes[z, y, x] = top - 1
         runs = []
-        for k in (1, 0):
+        for k in (3, 0):
             lib.vktHipSetTuningKnob(b"aggregates.codes", k)
             try:
-                got = gpu_aggregates(codes, 4, *mapping, first, last)
+                got = gpu_aggregates(codes, fmt, *mapping, first, last)
             finally:
                 lib.vktHipSetTuningKnob(b"aggregates.codes", -1)
-            check_aggregates(got, codes, 4, mapping, first, last, f"map={mapping} {first}->{last} knob={k}")
+            check_aggregates(got, codes, fmt, mapping, first, last, f"fmt={fmt} map={mapping} {first}->{last} knob={k}")
             runs.append(got)
         a, b = runs
         assert (a.min, a.max, tuple(a.argmin), tuple(a.argmax), a.mean) == (b.min, b.max, tuple(b.argmin),
                                                                           tuple(b.argmax), b.mean)
     # extremes that first occur after the first 512 Ki voxels of the range (the whole-grid
     # second stage of the first-occurrence search), once in a span and once in a padded box
-    codes = rng.integers(2, 254, (16, 64, 1024), dtype=np.uint8)
+    codes = rng.integers(2, top - 1, (16, 64, 1024), dtype=dt)
     codes[12, 5, 700] = codes[14, 0, 3] = 1
-    codes[15, 63, 1000] = codes[13, 9, 9] = 254
+    codes[15, 63, 1000] = codes[13, 9, 9] = top - 1
     for first, last in (((0, 0, 0), (1024, 64, 16)), ((3, 1, 0), (1021, 64, 16))):
-        got = gpu_aggregates(codes, 4, *mapping, first, last)
-        check_aggregates(got, codes, 4, mapping, first, last, f"late extremes map={mapping} {first}->{last}")
-    # product through value^count: 256 voxels of 1.01 (code 255 under (0, 1.01)), ~12.8
-    codes = np.full((2, 2, 64), 255, np.uint8)
-    got = gpu_aggregates(codes, 4, 0.0, 1.01, (0, 0, 0), (64, 2, 2))
-    v = float(values_of(codes[:1, :1, :1], 4, 0.0, 1.01).reshape(-1)[0])
+        got = gpu_aggregates(codes, fmt, *mapping, first, last)
+        check_aggregates(got, codes, fmt, mapping, first, last, f"late extremes map={mapping} {first}->{last}")
+    # product through value^count: 256 voxels of ~1.01 (the top code under (0, 1.01)), ~12.8
+    codes = np.full((2, 2, 64), top, dt)
+    got = gpu_aggregates(codes, fmt, 0.0, 1.01, (0, 0, 0), (64, 2, 2))
+    v = float(values_of(codes[:1, :1, :1], fmt, 0.0, 1.01).reshape(-1)[0])
     exact = v ** codes.size
     assert abs(got.prod - exact) <= codes.size * EPS * exact, (got.prod, exact)
 

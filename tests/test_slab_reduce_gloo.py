@@ -126,3 +126,135 @@ def test_slab_reductions_match_whole_volume(world, case):
     assert abs(var - ref.var) <= 4 * n * 2.0 ** -24 * abs(ref.var) + 1e-7
     for r, _, b in res:
         np.testing.assert_array_equal(b, ref_bins.astype(np.int64))
+
+
+# ---- UInt8 / UInt16 slabs in one data pass (slab._aggregates_codes) ------------------------------
+class NumpyCodeSlab(NumpySlab):
+    """A UInt8 / UInt16 slab: .codes (z, y, x), .vals their oracle-decoded float32 values (for the
+    two-pass fallback), and the view fields the code-count form reads."""
+
+    def __init__(self, codes, fmt, lo, hi, values):
+        super().__init__(values)
+        self.codes = codes
+        self.dataFormat, self.mappingLo, self.mappingHi = fmt, lo, hi
+
+
+def code_values(fmt, lo, hi, ncodes):
+    from oracle import binding as ob
+    return np.array([ob.unmap_voxel(int(c).to_bytes(ob.BPV[fmt], "little"), fmt, lo, hi) for c in range(ncodes)],
+                    dtype=np.float32)
+
+
+class NumpyCodeFns:
+    """numpy restatement of the three GPU steps (vktHipAggregateCodeCounts, vktHipAggregatesFrom-
+    Codes -- aggregatesCodesFinalKernel's float terms --, vktHipAggregateFirstCodes)."""
+
+    @staticmethod
+    def supported(view, first, last):
+        return True
+
+    @staticmethod
+    def count(view, first, last, counts):
+        box = view.codes[first[2]:last[2], first[1]:last[1], first[0]:last[0]]
+        counts.copy_(torch.from_numpy(np.bincount(box.reshape(-1).astype(np.int64), minlength=counts.numel())))
+
+    @staticmethod
+    def from_codes(counts, fmt, lo, hi, n):
+        from volkit_amd import _lib
+        from volkit_amd._lib import lib
+        cnt = counts.numpy().astype(np.float64)
+        v = code_values(fmt, lo, hi, cnt.size)
+        present = cnt > 0
+        p1, p2 = _lib.HipAggregatePartial_t(), _lib.HipAggregatePartial_t()
+        lib.vktHipAggregatePartialInit(C.byref(p1))
+        lib.vktHipAggregatePartialInit(C.byref(p2))
+        vp, cp = v[present], cnt[present]
+        p1.sum = float(np.sum(cp * vp.astype(np.float64)))
+        p1.prod = float(np.prod(vp.astype(np.float64) ** cp))
+        p1.count = int(cp.sum())
+        p1.minValue, p1.maxValue = float(vp.min()), float(vp.max())
+        mean = np.float32(np.float64(np.float32(p1.sum)) / n)
+        d = (vp - mean).astype(np.float32)
+        p2.sumSq = float(np.sum(cp * (d * d).astype(np.float32).astype(np.float64)))
+        codes = np.nonzero(present)[0]
+        lo_c, hi_c = codes[vp == vp.min()], codes[vp == vp.max()]
+        ok = len(lo_c) == 1 and len(hi_c) == 1 and np.all(np.abs(vp) < np.float32(FLT_MAX))
+        return p1, p2, ((int(lo_c[0]), int(hi_c[0])) if ok else (-1, -1))
+
+    @staticmethod
+    def first_codes(view, first, last, z0, cmin, cmax):
+        box = view.codes[first[2]:last[2], first[1]:last[1], first[0]:last[0]]
+        gy, gx = view.codes.shape[1], view.codes.shape[2]
+        out = []
+        for c in (cmin, cmax):
+            hits = np.argwhere(box == c)   # z, y, x in row-major (serial) order
+            if len(hits) == 0:
+                out.append((1 << 64) - 1)
+            else:
+                z, y, x = hits[0]
+                out.append(int(((z + first[2] + z0) * gy + (y + first[1])) * gx + (x + first[0])))
+        return tuple(out)
+
+
+def _codes_volume(fmt, dims):
+    gx, gy, gz = dims
+    top = 255 if fmt == 4 else 65535
+    rng = np.random.default_rng(7 + fmt)
+    codes = rng.integers(3, top - 2, (gz, gy, gx)).astype(np.uint8 if fmt == 4 else np.uint16)
+    codes[2, 1, 3] = codes[gz - 2, 0, 1] = 1           # tied minima in different slabs
+    codes[gz - 1, gy - 1, gx - 1] = codes[5, 4, 4] = top - 1
+    return codes
+
+
+def _codes_worker(rank, world, port, case, q):
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from volkit_amd import slab
+        fmt, (lo, hi), dims, first, last = case
+        codes = _codes_volume(fmt, dims)
+        vals = code_values(fmt, lo, hi, 256 if fmt == 4 else 65536)[codes.astype(np.int64)]
+        z0, z1 = slab.slab_bounds(dims[2], world, rank)
+        view = NumpyCodeSlab(codes[z0:z1], fmt, lo, hi, vals[z0:z1])
+        agg = slab.aggregates(view, dims, z0, first, last, pass_fn=numpy_pass, code_fns=NumpyCodeFns)
+        q.put((rank, (agg.min, agg.max, (agg.argmin.x, agg.argmin.y, agg.argmin.z),
+                      (agg.argmax.x, agg.argmax.y, agg.argmax.z), agg.sum, agg.mean, agg.var)))
+        dist.destroy_process_group()
+    except Exception:   # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("case", [(4, (0.0, 1.0), (12, 9, 10), (0, 0, 0), (12, 9, 10)),
+                                  (4, (3.0, -1.0), (12, 9, 10), (2, 1, 3), (11, 9, 9)),
+                                  (5, (-1.0, 3.0), (12, 9, 10), (1, 0, 1), (12, 8, 10)),
+                                  (4, (0.25, 0.25), (12, 9, 10), (0, 0, 0), (12, 9, 10))])   # -> two passes
+def test_slab_code_count_aggregates(world, case):
+    """slab.aggregates on UInt8 / UInt16 slabs: local code counts, one all_reduce(SUM), the
+    aggregates from the global counts, first-occurrence search per slab + all_reduce(MIN) of the
+    indices == the whole-volume oracle (a constant mapping falls back to the two passes)."""
+    from oracle import binding as ob
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_codes_worker, args=(r, world, port, case, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for r, agg in res:
+        assert not isinstance(agg, str), agg
+    fmt, (lo, hi), dims, first, last = case
+    codes = _codes_volume(fmt, dims)
+    ref = ob.aggregates_range(ob.Volume(codes, fmt, lo, hi), first, last)
+    aggs = {r: a for r, a in res}
+    assert len(set(aggs.values())) == 1
+    mn, mx, amin, amax, s, mean, var = aggs[0]
+    assert (mn, mx, amin, amax) == (ref.min, ref.max, tuple(ref.argmin), tuple(ref.argmax))
+    n = (last[0] - first[0]) * (last[1] - first[1]) * (last[2] - first[2])
+    assert abs(s - ref.sum) <= n * 2.0 ** -24 * abs(ref.sum) + 1e-6
+    assert abs(mean - ref.mean) <= n * 2.0 ** -24 * abs(ref.mean) + 1e-7
+    assert abs(var - ref.var) <= 4 * n * 2.0 ** -24 * abs(ref.var) + 1e-7

@@ -626,8 +626,18 @@ def main():
             ms = timed(lambda: lib.vktHipAggregatesRange(W, u0, u1, C.byref(agg)), R)
             report(f"aggcodes Aggregates UInt8 800^3 sub-box at x0=100 [codes={k}, {passes} pass(es)]", ms,
                    passes * 800 ** 3, 800 ** 3)
-        lib.vktHipSetTuningKnob(b"aggregates.codes", -1)
         free(W)
+        V = alloc((n,) * 3, 5, seed=11)
+        for k in (3, 1):
+            lib.vktHipSetTuningKnob(b"aggregates.codes", k)
+            passes = 1 if k & 2 else 2
+            ms = timed(lambda: lib.vktHipAggregatesRange(V, o, last, C.byref(agg)), R)
+            report(f"aggcodes Aggregates 1024^3 UInt16 [codes={k}, {passes} pass(es)]", ms, passes * 2 * n ** 3, n ** 3)
+            ms = timed(lambda: lib.vktHipAggregatesRange(V, u0, u1, C.byref(agg)), R)
+            report(f"aggcodes Aggregates UInt16 800^3 sub-box at x0=100 [codes={k}, {passes} pass(es)]", ms,
+                   passes * 2 * 800 ** 3, 800 ** 3)
+        lib.vktHipSetTuningKnob(b"aggregates.codes", -1)
+        free(V)
     if want("config5"):
         # BASELINE config 5: 1024^3 UInt8 multi-scattering, 1024^2 viewport (headless frames)
         import volkit_amd.volkit as vkt

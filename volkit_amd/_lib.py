@@ -294,6 +294,11 @@ SIGNATURES = {
     "vktHipAggregatePartialCombine": (c_err, [P(HipAggregatePartial_t), P(HipAggregatePartial_t)]),
     "vktHipAggregatesMean": (f32, [P(HipAggregatePartial_t), u64]),
     "vktHipAggregatesPass": (c_err, [HipVolumeView_t, Vec3i_t, Vec3i_t, i32, i32, f32, P(HipAggregatePartial_t)]),
+    "vktHipAggregateCodesSupported": (i32, [HipVolumeView_t, Vec3i_t, Vec3i_t]),
+    "vktHipAggregateCodeCounts": (c_err, [HipVolumeView_t, Vec3i_t, Vec3i_t, C.c_void_p]),
+    "vktHipAggregatesFromCodes": (c_err, [C.c_void_p, i32, f32, f32, u64, P(HipAggregatePartial_t),
+                                          P(HipAggregatePartial_t), P(i32)]),
+    "vktHipAggregateFirstCodes": (c_err, [HipVolumeView_t, Vec3i_t, Vec3i_t, i32, i32, i32, P(u64)]),
     "vktHipAggregatesFinish": (c_err, [P(HipAggregatePartial_t), P(HipAggregatePartial_t), u64, i32, i32,
                                        P(Aggregates_t)]),
     "vktHipHistogramRange": (c_err, [HipVolumeView_t, Vec3i_t, Vec3i_t, C.c_void_p, u64, i32]),

@@ -132,7 +132,9 @@ namespace hipk
         return (static_cast<uint64_t>(hi) << 32) | lo;
     }
 
-    // Whole-wave / workgroup reduction of a partial (lane 0 of the block ends with it).
+    // Whole-wave / workgroup reduction of a partial (lane 0 of the block ends with it); WAVES =
+    // the workgroup's waves.
+    template <int WAVES = kBlock / 64>
     __device__ void blockReduce(vktHipAggregatePartial_t& p)
     {
         for (int m = 32; m >= 1; m >>= 1)
@@ -148,7 +150,7 @@ namespace hipk
             p.sumSq += s2;
             p.count += c;
         }
-        __shared__ vktHipAggregatePartial_t lds[kBlock / 64];
+        __shared__ vktHipAggregatePartial_t lds[WAVES];
         int const wave = threadIdx.x >> 6;
         if ((threadIdx.x & 63) == 0)
             lds[wave] = p;
@@ -962,11 +964,16 @@ namespace hipk
     // result: every present value finite and below FLT_MAX in magnitude and each extreme held by
     // ONE code (a mapping that rounds two present codes onto an extreme makes the caller rerun
     // the two float passes); 0 otherwise (targets -1).
-    __global__ __launch_bounds__(kBlock) void aggregatesCodesFinalKernel(unsigned long long const* counts, float lo,
-                                                                        float hi, double numElems,
-                                                                        vktHipAggregatePartial_t* res,
-                                                                        int32_t* targets)
+    // FMT UInt8 (256 codes, 256 threads: one code each) or UInt16 (65 536 codes, 1024 threads: 64
+    // each, strided so a wave reads consecutive counts).
+    template <int FMT>
+    __global__ __launch_bounds__(FMT == codec::FmtUInt8 ? 256 : 1024) void aggregatesCodesFinalKernel(
+        unsigned long long const* counts, float lo, float hi, double numElems, vktHipAggregatePartial_t* res,
+        int32_t* targets)
     {
+        constexpr uint32_t kCodes = FMT == codec::FmtUInt8 ? 256u : 65536u;
+        constexpr uint32_t kThreads = FMT == codec::FmtUInt8 ? 256u : 1024u;
+        constexpr int kWaves = static_cast<int>(kThreads / 64);
         __shared__ float sVmin, sVmax, sMean;
         __shared__ int32_t sNmin, sNmax, sCmin, sCmax, sBad;
         if (threadIdx.x == 0)
@@ -975,23 +982,23 @@ namespace hipk
             sCmin = sCmax = -1;
         }
         __syncthreads();
-        uint32_t const c = threadIdx.x;   // kBlock == 256: one code per thread
-        unsigned long long const cnt = c < 256u ? counts[c] : 0ull;
-        float const v = codec::decode(c, codec::FmtUInt8, lo, hi);
-        bool const present = cnt != 0ull;
         vktHipAggregatePartial_t q = emptyPartial();
-        if (present)
+        for (uint32_t c = threadIdx.x; c < kCodes; c += kThreads)
         {
+            unsigned long long const cnt = counts[c];
+            if (cnt == 0ull)
+                continue;
+            float const v = codec::decode(c, FMT, lo, hi);
             if (!(fabsf(v) < FLT_MAX))
                 atomicOr(&sBad, 1);
-            q.minValue = q.maxValue = v;
-            q.minIndex = q.maxIndex = c;
+            minCombine(q.minValue, q.minIndex, v, c);
+            maxCombine(q.maxValue, q.maxIndex, v, c);
             double const dv = static_cast<double>(v), dn = static_cast<double>(cnt);
-            q.sum = dn * dv;
-            q.prod = pow(dv, dn);
-            q.count = cnt;
+            q.sum += dn * dv;
+            q.prod *= cnt == 1ull ? dv : pow(dv, dn);
+            q.count += cnt;
         }
-        blockReduce(q);
+        blockReduce<kWaves>(q);
         __syncthreads();
         vktHipAggregatePartial_t& r = q;   // thread 0: sum / prod / count / value extremes
         if (threadIdx.x == 0)
@@ -1001,24 +1008,28 @@ namespace hipk
             sMean = static_cast<float>(static_cast<double>(static_cast<float>(r.sum)) / numElems);
         }
         __syncthreads();
-        if (present && v == sVmin)
-        {
-            atomicAdd(&sNmin, 1);
-            sCmin = static_cast<int32_t>(c);
-        }
-        if (present && v == sVmax)
-        {
-            atomicAdd(&sNmax, 1);
-            sCmax = static_cast<int32_t>(c);
-        }
         vktHipAggregatePartial_t t = emptyPartial();
-        if (present)
+        for (uint32_t c = threadIdx.x; c < kCodes; c += kThreads)
         {
+            unsigned long long const cnt = counts[c];
+            if (cnt == 0ull)
+                continue;
+            float const v = codec::decode(c, FMT, lo, hi);
+            if (v == sVmin)
+            {
+                atomicAdd(&sNmin, 1);
+                sCmin = static_cast<int32_t>(c);
+            }
+            if (v == sVmax)
+            {
+                atomicAdd(&sNmax, 1);
+                sCmax = static_cast<int32_t>(c);
+            }
             float const d = v - sMean;
             float const d2 = d * d;
-            t.sumSq = static_cast<double>(cnt) * static_cast<double>(d2);
+            t.sumSq += static_cast<double>(cnt) * static_cast<double>(d2);
         }
-        blockReduce(t);
+        blockReduce<kWaves>(t);
         __syncthreads();
         if (threadIdx.x == 0)
         {
@@ -1059,12 +1070,12 @@ namespace hipk
 
     // The first voxels of item `item` holding codes tmin / tmax, folded into *bMin / *bMax with
     // atomicMin (LDS or global).
-    template <bool CONTIG>
+    template <int BPV, bool CONTIG>
     __device__ __forceinline__ void findCodes(FastHistArgs const& h, uint64_t item, int32_t tmin, int32_t tmax,
                                               unsigned long long* bMin, unsigned long long* bMax)
     {
         uint32_t c[8];
-        load8<1, true>(h.data, spanVoxel<CONTIG>(h, item), c);
+        load8<BPV, true>(h.data, spanVoxel<CONTIG>(h, item), c);
         uint32_t const m = itemMask<CONTIG>(h, item);
         int jMin = 8, jMax = 8;
 #pragma unroll
@@ -1086,7 +1097,7 @@ namespace hipk
     // the first step: 8 Ki voxels).  Writes res[0].minIndex / maxIndex (kNoIndex if not found).
     // One workgroup, because many waves folding into one global word serialise on it (a
     // whole-grid version with global atomics and early exit took 0.35 ms).
-    template <bool CONTIG>
+    template <int BPV, bool CONTIG>
     __global__ __launch_bounds__(1024) void aggregatesFindHeadKernel(FastHistArgs h, int32_t const* targets,
                                                                     vktHipAggregatePartial_t* res, uint64_t headItems)
     {
@@ -1102,7 +1113,7 @@ namespace hipk
         {
             uint64_t const item = base + threadIdx.x;
             if (item < end)
-                findCodes<CONTIG>(h, item, tmin, tmax, &sMin, &sMax);
+                findCodes<BPV, CONTIG>(h, item, tmin, tmax, &sMin, &sMax);
             __syncthreads();
             bool const done = sMin != kNoIndex && sMax != kNoIndex;
             __syncthreads();   // every thread has read before the next step's atomics
@@ -1118,7 +1129,7 @@ namespace hipk
 
     // Stage 2, the whole grid over the items after the head -- only when stage 1 left a code
     // unfound (it then occurs rarely, so few lanes fold into the global words).
-    template <bool CONTIG>
+    template <int BPV, bool CONTIG>
     __global__ __launch_bounds__(kBlock) void aggregatesFindTailKernel(FastHistArgs h, int32_t const* targets,
                                                                       vktHipAggregatePartial_t* res, uint64_t headItems)
     {
@@ -1130,7 +1141,7 @@ namespace hipk
         uint64_t const stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
         for (uint64_t item = headItems + static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; item < h.items;
              item += stride)
-            findCodes<CONTIG>(h, item, tmin, tmax, bMin, bMax);
+            findCodes<BPV, CONTIG>(h, item, tmin, tmax, bMin, bMax);
     }
 
     __global__ void zeroU64Kernel(unsigned long long* p, uint64_t n)
@@ -1491,9 +1502,85 @@ namespace hipk
         return s;
     }
 
-    // UInt8 aggregates in one data pass (aggregatesFastKernel<CODES>, aggregatesCodesFinalKernel,
-    // aggregatesFind{Head,Tail}Kernel into res[0], res[1]); false when the range does not take the
-    // streaming walk.  scratch: 256 code counts, then 2 target codes.
+    // Code counts of a span walk into the device array h.bins (256 or 65 536 u64, zeroed here):
+    // UInt8 aggregatesFastKernel<CODES>; UInt16 the histogram kernel's one-pass packed-16
+    // counters with bin = code.  g: codeAggGrid.
+    bool launchCodeCounts(FastHistArgs h, bool contig, int32_t fmt, unsigned g, hipStream_t s)
+    {
+        bool const u8 = fmt == codec::FmtUInt8;
+        uint32_t const codes = u8 ? 256u : 65536u;
+        if (hipMemsetAsync(h.bins, 0, codes * sizeof(unsigned long long), s) != hipSuccess)
+            return false;
+        auto* const none = static_cast<vktHipAggregatePartial_t*>(nullptr);
+        if (u8)
+        {
+            h.rShift = 5;   // 32 copies of each counter: lane groups never share a bank (as the histogram)
+            size_t const lds = 256u << (h.rShift + 2);
+            if (contig)
+                hipLaunchKernelGGL((aggregatesFastKernel<1, codec::FmtUInt8, true, false, true>), dim3(g), dim3(kBlock),
+                                   lds, s, h, static_cast<float const*>(nullptr), 0.f, none);
+            else
+                hipLaunchKernelGGL((aggregatesFastKernel<1, codec::FmtUInt8, false, false, true>), dim3(g), dim3(kBlock),
+                                   lds, s, h, static_cast<float const*>(nullptr), 0.f, none);
+        }
+        else
+        {
+            // bin = (code * 1) >> 0 over 65 536 bins in one tile of packed 16-bit counters
+            h.nb = 65536u;
+            h.nbf = 65536.0f;
+            h.binShift = 0u;
+            h.binMul = 1u;
+            h.rShift = 0;
+            h.tileBase = 0;
+            h.tileBins = 65536u;
+            h.p16Step = rt::knob(rt::Knob::HistogramP16Step) != 0 ? 1u : 0u;
+            size_t const lds = 32768u * 4u;
+            if (contig)
+                hipLaunchKernelGGL((histogramFastKernel<codec::FmtUInt16, true, true, kTileBlock, true, true>), dim3(g),
+                                   dim3(kTileBlock), lds, s, h);
+            else
+                hipLaunchKernelGGL((histogramFastKernel<codec::FmtUInt16, false, true, kTileBlock, true, true>), dim3(g),
+                                   dim3(kTileBlock), lds, s, h);
+        }
+        return true;
+    }
+
+    void launchCodesFinal(unsigned long long const* counts, int32_t fmt, float lo, float hi, double numElems,
+                          vktHipAggregatePartial_t* res, int32_t* targets, hipStream_t s)
+    {
+        if (fmt == codec::FmtUInt8)
+            hipLaunchKernelGGL((aggregatesCodesFinalKernel<codec::FmtUInt8>), dim3(1), dim3(256), 0, s, counts, lo, hi,
+                               numElems, res, targets);
+        else
+            hipLaunchKernelGGL((aggregatesCodesFinalKernel<codec::FmtUInt16>), dim3(1), dim3(1024), 0, s, counts, lo, hi,
+                               numElems, res, targets);
+    }
+
+    // First occurrences of codes targets[0] / [1] in the walk h into res[0].minIndex / maxIndex.
+    void launchFindCodes(FastHistArgs const& h, bool contig, int32_t fmt, int32_t const* targets,
+                         vktHipAggregatePartial_t* res, hipStream_t s)
+    {
+        uint64_t const head = 64u * 1024u;   // stage 1 covers the first 512 Ki voxels at most
+        unsigned const gf = static_cast<unsigned>(std::max<uint64_t>(1, std::min<uint64_t>(2048, (h.items + kBlock - 1) / kBlock)));
+#define VKT_FIND(B, CT)                                                                                          \
+    do {                                                                                                         \
+        hipLaunchKernelGGL((aggregatesFindHeadKernel<B, CT>), dim3(1), dim3(1024), 0, s, h, targets, res, head);   \
+        hipLaunchKernelGGL((aggregatesFindTailKernel<B, CT>), dim3(gf), dim3(kBlock), 0, s, h, targets, res, head); \
+    } while (0)
+        if (fmt == codec::FmtUInt8)
+        {
+            if (contig) VKT_FIND(1, true); else VKT_FIND(1, false);
+        }
+        else
+        {
+            if (contig) VKT_FIND(2, true); else VKT_FIND(2, false);
+        }
+#undef VKT_FIND
+    }
+
+    // UInt8 / UInt16 aggregates in one data pass: code counts, aggregatesCodesFinalKernel, then the
+    // first-occurrence search, into res[0], res[1]; false when the range does not take the
+    // streaming walk.  scratch: the code counts (256 or 65 536), then 2 target codes.
     bool launchCodeAggregates(BoxArgs const& a, hipStream_t s, double numElems, void* scratch, unsigned g,
                               vktHipAggregatePartial_t* res)
     {
@@ -1501,45 +1588,30 @@ namespace hipk
         bool contig;
         if (!makeSpanArgs(a, h, contig))
             return false;
+        uint32_t const codes = a.fmt == codec::FmtUInt8 ? 256u : 65536u;
         h.bins = static_cast<unsigned long long*>(scratch);
-        auto* const targets = reinterpret_cast<int32_t*>(h.bins + 256);
-        h.rShift = 5;   // 32 copies of each counter: lane groups never share a bank (as the histogram)
-        size_t const lds = 256u << (h.rShift + 2);
-        if (hipMemsetAsync(h.bins, 0, 256 * sizeof(unsigned long long), s) != hipSuccess)
+        auto* const targets = reinterpret_cast<int32_t*>(h.bins + codes);
+        if (!launchCodeCounts(h, contig, a.fmt, g, s))
             return false;
-        auto* const none = static_cast<vktHipAggregatePartial_t*>(nullptr);
-        if (contig)
-            hipLaunchKernelGGL((aggregatesFastKernel<1, codec::FmtUInt8, true, false, true>), dim3(g), dim3(kBlock), lds,
-                               s, h, static_cast<float const*>(nullptr), 0.f, none);
-        else
-            hipLaunchKernelGGL((aggregatesFastKernel<1, codec::FmtUInt8, false, false, true>), dim3(g), dim3(kBlock), lds,
-                               s, h, static_cast<float const*>(nullptr), 0.f, none);
-        hipLaunchKernelGGL(aggregatesCodesFinalKernel, dim3(1), dim3(kBlock), 0, s, h.bins, a.lo, a.hi, numElems, res,
-                           targets);
-        uint64_t const head = 64u * 1024u;   // stage 1 covers the first 512 Ki voxels at most
-        unsigned const gf = std::max(1u, std::min(g, static_cast<unsigned>((h.items + kBlock - 1) / kBlock)));
-        if (contig)
-        {
-            hipLaunchKernelGGL((aggregatesFindHeadKernel<true>), dim3(1), dim3(1024), 0, s, h, targets, res, head);
-            hipLaunchKernelGGL((aggregatesFindTailKernel<true>), dim3(gf), dim3(kBlock), 0, s, h, targets, res, head);
-        }
-        else
-        {
-            hipLaunchKernelGGL((aggregatesFindHeadKernel<false>), dim3(1), dim3(1024), 0, s, h, targets, res, head);
-            hipLaunchKernelGGL((aggregatesFindTailKernel<false>), dim3(gf), dim3(kBlock), 0, s, h, targets, res, head);
-        }
+        launchCodesFinal(h.bins, a.fmt, a.lo, a.hi, numElems, res, targets, s);
+        launchFindCodes(h, contig, a.fmt, targets, res, s);
         return true;
     }
 
-    // Grid of the code-count pass: 32 KiB of counters per workgroup, 4 workgroups per CU; 0 when
-    // the range does not take it.
+    // Grid of the code-count pass (0 when the range does not take it): UInt8 32 KiB of counters
+    // per workgroup, 4 per CU; UInt16 the packed-16 histogram's one 1024-thread workgroup per CU.
+    // Knob aggregates.codes: bit 0 UInt8, bit 1 UInt16.
     unsigned codeAggGrid(BoxArgs const& a)
     {
         FastHistArgs h;
         bool contig;
-        if (a.fmt != codec::FmtUInt8 || rt::knob(rt::Knob::AggregatesCodes) == 0 || !makeSpanArgs(a, h, contig))
+        int64_t const k = rt::knob(rt::Knob::AggregatesCodes);
+        bool const on = (a.fmt == codec::FmtUInt8 && (k & 1)) || (a.fmt == codec::FmtUInt16 && (k & 2));
+        if (!on || !makeSpanArgs(a, h, contig))
             return 0;
-        return streamingGrid(h.items, 64u * 4u * (kBlock / 64), 4);
+        if (a.fmt == codec::FmtUInt8)
+            return streamingGrid(h.items, 64u * 4u * (kBlock / 64), 4);
+        return streamingGrid(h.items, 64u * 4u * (kTileBlock / 64), 1);
     }
 
 } // hipk
@@ -1670,11 +1742,11 @@ vktError vktHipAggregatesRange(vktHipVolumeView_t volume, vktVec3i_t first, vktV
                             : 0u;
     if (gc != 0)
     {
-        // UInt8: one pass of code counts; the two float passes below only when the counts cannot
-        // give the first occurrence of an extreme (aggregatesCodesFinalKernel)
+        // UInt8 / UInt16: one pass of code counts; the two float passes below only when the
+        // counts cannot give the first occurrence of an extreme (aggregatesCodesFinalKernel)
         hipStream_t s = rt::computeStream();
         AggScratch& sc = aggScratch();
-        size_t const bytes = 2 * sizeof(vktHipAggregatePartial_t) + 256 * sizeof(unsigned long long) + 16;
+        size_t const bytes = 2 * sizeof(vktHipAggregatePartial_t) + 65536 * sizeof(unsigned long long) + 16;
         auto* res = static_cast<vktHipAggregatePartial_t*>(sc.dev.acquire(bytes, s));
         if (!res)
             return vktInvalidValue;
@@ -1685,7 +1757,7 @@ vktError vktHipAggregatesRange(vktHipVolumeView_t volume, vktVec3i_t first, vktV
             sc.dev.release(s);
             return vktInvalidValue;
         }
-        // layout: the two results, then 256 code counts and the 2 target codes
+        // layout: the two results, then the code counts and the 2 target codes
         bool const launched = launchCodeAggregates(a, s, static_cast<double>(numElems), res + 2, gc, res);
         e = launched ? rt::check(hipMemcpyAsync(sc.host, res, 2 * sizeof(vktHipAggregatePartial_t),
                                                 hipMemcpyDeviceToHost, s),
@@ -1744,6 +1816,125 @@ vktError vktHipAggregatesRange(vktHipVolumeView_t volume, vktVec3i_t first, vktV
     else if (!done && e != vktNoError)
         return e;
     return vktHipAggregatesFinish(&p1, &p2, numElems, volume.dimX, volume.dimY, out);
+}
+
+vktError vktHipAggregateCodeCounts(vktHipVolumeView_t volume, vktVec3i_t first, vktVec3i_t last, uint64_t* counts)
+{
+    if (counts == nullptr)
+        return rt::fail("vktHipAggregateCodeCounts: null counts");
+    if (volume.dataFormat != codec::FmtUInt8 && volume.dataFormat != codec::FmtUInt16)
+        return rt::fail("vktHipAggregateCodeCounts: UInt8 / UInt16 volumes only");
+    uint32_t const codes = volume.dataFormat == codec::FmtUInt8 ? 256u : 65536u;
+    hipStream_t s = rt::computeStream();
+    BoxArgs a{};
+    vktError e;
+    if (!makeBox(volume, first, last, 0, a, "vktHipAggregateCodeCounts: invalid volume view", e))
+    {
+        if (e != vktNoError)
+            return e;
+        VKT_HIP_TRY(hipMemsetAsync(counts, 0, codes * sizeof(uint64_t), s));   // empty range
+        return rt::finishLaunch("AggregateCodeCounts_hip");
+    }
+    FastHistArgs h;
+    bool contig;
+    if (!makeSpanArgs(a, h, contig))
+        return rt::fail("vktHipAggregateCodeCounts: the range does not take the code-count walk (16-B aligned volume "
+                        "with dimX % 8 == 0 needed)");
+    h.bins = reinterpret_cast<unsigned long long*>(counts);
+    unsigned const g = a.fmt == codec::FmtUInt8 ? streamingGrid(h.items, 64u * 4u * (kBlock / 64), 4)
+                                                : streamingGrid(h.items, 64u * 4u * (kTileBlock / 64), 1);
+    if (!launchCodeCounts(h, contig, a.fmt, g, s))
+        return rt::check(hipGetLastError(), "vktHipAggregateCodeCounts");
+    return rt::finishLaunch("AggregateCodeCounts_hip");
+}
+
+int32_t vktHipAggregateCodesSupported(vktHipVolumeView_t volume, vktVec3i_t first, vktVec3i_t last)
+{
+    if (volume.dataFormat != codec::FmtUInt8 && volume.dataFormat != codec::FmtUInt16)
+        return 0;
+    BoxArgs a{};
+    vktError e;
+    if (!makeBox(volume, first, last, 0, a, "vktHipAggregateCodesSupported: invalid volume view", e))
+        return e == vktNoError ? 1 : 0;   // an empty range counts nothing
+    FastHistArgs h;
+    bool contig;
+    return makeSpanArgs(a, h, contig) ? 1 : 0;
+}
+
+vktError vktHipAggregatesFromCodes(uint64_t const* counts, int32_t dataFormat, float mappingLo, float mappingHi,
+                                   uint64_t numElems, vktHipAggregatePartial_t* pass1, vktHipAggregatePartial_t* pass2,
+                                   int32_t* codes)
+{
+    if (counts == nullptr || pass1 == nullptr || pass2 == nullptr || codes == nullptr)
+        return rt::fail("vktHipAggregatesFromCodes: null pointer");
+    if (dataFormat != codec::FmtUInt8 && dataFormat != codec::FmtUInt16)
+        return rt::fail("vktHipAggregatesFromCodes: UInt8 / UInt16 only");
+    hipStream_t s = rt::computeStream();
+    AggScratch& sc = aggScratch();
+    size_t const bytes = 2 * sizeof(vktHipAggregatePartial_t) + 16;
+    auto* res = static_cast<vktHipAggregatePartial_t*>(sc.dev.acquire(bytes, s));
+    if (!res)
+        return vktInvalidValue;
+    auto* targets = reinterpret_cast<int32_t*>(res + 2);
+    launchCodesFinal(reinterpret_cast<unsigned long long const*>(counts), dataFormat, mappingLo, mappingHi,
+                     static_cast<double>(numElems), res, targets, s);
+    struct
+    {
+        vktHipAggregatePartial_t r[2];
+        int32_t t[2];
+    } host;
+    vktError e = rt::check(hipMemcpyAsync(&host, res, sizeof(host.r), hipMemcpyDeviceToHost, s), "hipMemcpyAsync");
+    if (e == vktNoError)
+        e = rt::check(hipMemcpyAsync(host.t, targets, sizeof(host.t), hipMemcpyDeviceToHost, s), "hipMemcpyAsync");
+    sc.dev.release(s);
+    if (e != vktNoError)
+        return e;
+    VKT_HIP_TRY(hipStreamSynchronize(s));
+    *pass1 = host.r[0];
+    *pass2 = host.r[1];
+    pass2->count = 0;
+    codes[0] = host.t[0];
+    codes[1] = host.t[1];
+    return rt::finishLaunch("AggregatesFromCodes_hip");
+}
+
+vktError vktHipAggregateFirstCodes(vktHipVolumeView_t volume, vktVec3i_t first, vktVec3i_t last, int32_t zGlobalOffset,
+                                   int32_t minCode, int32_t maxCode, uint64_t* indices)
+{
+    if (indices == nullptr)
+        return rt::fail("vktHipAggregateFirstCodes: null indices");
+    indices[0] = indices[1] = kNoIndex;
+    if (minCode < 0 || maxCode < 0)
+        return rt::fail("vktHipAggregateFirstCodes: negative code");
+    BoxArgs a{};
+    vktError e;
+    if (!makeBox(volume, first, last, zGlobalOffset, a, "vktHipAggregateFirstCodes: invalid volume view", e))
+        return e;
+    FastHistArgs h;
+    bool contig;
+    if ((a.fmt != codec::FmtUInt8 && a.fmt != codec::FmtUInt16) || !makeSpanArgs(a, h, contig))
+        return rt::fail("vktHipAggregateFirstCodes: the range does not take the code-count walk");
+    hipStream_t s = rt::computeStream();
+    AggScratch& sc = aggScratch();
+    size_t const bytes = 2 * sizeof(vktHipAggregatePartial_t) + 16;
+    auto* res = static_cast<vktHipAggregatePartial_t*>(sc.dev.acquire(bytes, s));
+    if (!res)
+        return vktInvalidValue;
+    auto* targets = reinterpret_cast<int32_t*>(res + 2);
+    int32_t const t[2] = {minCode, maxCode};
+    e = rt::check(hipMemcpyAsync(targets, t, sizeof(t), hipMemcpyHostToDevice, s), "hipMemcpyAsync");
+    if (e == vktNoError)
+        launchFindCodes(h, contig, a.fmt, targets, res, s);
+    uint64_t out[2] = {kNoIndex, kNoIndex};
+    if (e == vktNoError)
+        e = rt::check(hipMemcpyAsync(out, &res[0].minIndex, sizeof(out), hipMemcpyDeviceToHost, s), "hipMemcpyAsync");
+    sc.dev.release(s);
+    if (e != vktNoError)
+        return e;
+    VKT_HIP_TRY(hipStreamSynchronize(s));
+    indices[0] = out[0];
+    indices[1] = out[1];
+    return rt::finishLaunch("AggregateFirstCodes_hip");
 }
 
 vktError vktHipHistogramRange(vktHipVolumeView_t volume, vktVec3i_t first, vktVec3i_t last, uint64_t* bins,

@@ -205,7 +205,7 @@ namespace rt
             {"pointwise.u8_wide", 1},
             {"pointwise.f32_halves", 1},
             {"pointwise.f32_wide", 0},
-            {"aggregates.codes", 1},
+            {"aggregates.codes", 3},
         };
         static_assert(sizeof(kKnobs) / sizeof(kKnobs[0]) == static_cast<size_t>(Knob::Count), "knob table");
         std::atomic<int64_t> gKnobs[static_cast<int>(Knob::Count)] = {{kKnobs[0].def}, {kKnobs[1].def},

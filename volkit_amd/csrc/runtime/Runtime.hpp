@@ -89,7 +89,7 @@ namespace rt
         PointwiseU8Wide,               // 0: UInt8 general-path boxes keep 8-voxel items
         PointwiseF32Halves,            // 0: padded 4-byte rows keep the per-item loop
         PointwiseF32Wide,              // 1: 4-byte general-path boxes use 16-B items (measured neutral; off)
-        AggregatesCodes,               // 1: UInt8 ComputeAggregates from one pass of code counts (else 2 passes)
+        AggregatesCodes,               // bit 0 UInt8, bit 1 UInt16: ComputeAggregates from one pass of code counts
         Count
     };
     int64_t knob(Knob k);

@@ -435,14 +435,103 @@ def combine_partials(parts):
     return acc
 
 
-def aggregates(view, global_dims, z0: int, first, last, group=None, device=None, pass_fn=None):
+def _all_reduce(t, op, group=None):
+    """all_reduce of a (device or host) tensor; gloo reduces a host copy of a device tensor."""
+    import torch.distributed as dist
+    if t.is_cuda and dist.get_backend(group) == "gloo":
+        host = t.cpu()
+        dist.all_reduce(host, op=op, group=group)
+        t.copy_(host)
+    else:
+        dist.all_reduce(t, op=op, group=group)
+    return t
+
+
+NO_INDEX = (1 << 64) - 1
+_I64_MAX = (1 << 63) - 1
+
+
+class GpuCodeFns:
+    """The code-count form's per-rank steps on the GPU (include/volkit_hip.h)."""
+
+    @staticmethod
+    def supported(view, first, last) -> bool:
+        return bool(lib.vktHipAggregateCodesSupported(view, _lib.Vec3i_t(*first), _lib.Vec3i_t(*last)))
+
+    @staticmethod
+    def count(view, first, last, counts) -> None:
+        if lib.vktHipAggregateCodeCounts(view, _lib.Vec3i_t(*first), _lib.Vec3i_t(*last),
+                                         C.c_void_p(counts.data_ptr())) != 0:
+            raise RuntimeError(_lib.last_error())
+
+    @staticmethod
+    def from_codes(counts, fmt, lo, hi, n):
+        p1, p2, codes = _lib.HipAggregatePartial_t(), _lib.HipAggregatePartial_t(), (C.c_int32 * 2)()
+        if lib.vktHipAggregatesFromCodes(C.c_void_p(counts.data_ptr()), fmt, C.c_float(lo), C.c_float(hi), n,
+                                         C.byref(p1), C.byref(p2), codes) != 0:
+            raise RuntimeError(_lib.last_error())
+        return p1, p2, (codes[0], codes[1])
+
+    @staticmethod
+    def first_codes(view, first, last, z0, cmin, cmax):
+        idx = (C.c_uint64 * 2)()
+        if lib.vktHipAggregateFirstCodes(view, _lib.Vec3i_t(*first), _lib.Vec3i_t(*last), z0, cmin, cmax, idx) != 0:
+            raise RuntimeError(_lib.last_error())
+        return idx[0], idx[1]
+
+
+def _aggregates_codes(view, global_dims, z0, rng, group, device, fns):
+    """UInt8 / UInt16 slabs in one data pass: local code counts, ONE all_reduce(SUM) of them, the
+    aggregates from the global counts (identical on every rank), a first-occurrence search of
+    the two extremes' codes in each slab and an all_reduce(MIN) of the indices.  None when the
+    counts cannot tell which voxel comes first (the caller runs the two passes; every rank
+    reaches the same answer, from the same counts)."""
+    import torch
+    import torch.distributed as dist
+
+    gx, gy, gz = global_dims
+    ncodes = 256 if view.dataFormat == 4 else 65536
+    dev = device if device is not None else "cpu"
+    counts = torch.zeros(ncodes, dtype=torch.int64, device=dev)
+    if rng:
+        fns.count(view, rng[0], rng[1], counts)
+    _all_reduce(counts, dist.ReduceOp.SUM, group)
+    p1, p2, (cmin, cmax) = fns.from_codes(counts, view.dataFormat, view.mappingLo, view.mappingHi, gx * gy * gz)
+    if cmin < 0 or cmax < 0:
+        return None
+    imin, imax = fns.first_codes(view, rng[0], rng[1], z0, cmin, cmax) if rng else (NO_INDEX, NO_INDEX)
+    idx = torch.tensor([min(imin, _I64_MAX), min(imax, _I64_MAX)], dtype=torch.int64, device=dev)
+    _all_reduce(idx, dist.ReduceOp.MIN, group)
+    imin, imax = (int(i) if int(i) != _I64_MAX else NO_INDEX for i in idx.cpu())
+    p1.minIndex, p1.maxIndex = imin, imax
+    out = _lib.Aggregates_t()
+    lib.vktHipAggregatesFinish(C.byref(p1), C.byref(p2), gx * gy * gz, gx, gy, C.byref(out))
+    return out
+
+
+def aggregates(view, global_dims, z0: int, first, last, group=None, device=None, pass_fn=None, code_fns=None):
     """ComputeAggregatesRange over a Z-slab partitioned volume: each rank reduces its planes
     (pass 1), partials are all-gathered and combined in rank order (deterministic), the
     reference's float mean of the WHOLE volume follows, then pass 2 and a second exchange.
+    UInt8 / UInt16 volumes whose every slab takes the code-count walk use ONE data pass
+    instead (_aggregates_codes; `code_fns` replaces the GPU steps, e.g. in CPU tests; a custom
+    `pass_fn` alone keeps the two passes).
     `view` is this rank's slab (global planes [z0, z0 + view.dimZ)); returns Aggregates_t."""
-    pass_fn = pass_fn or _gpu_pass
+    import torch
+    import torch.distributed as dist
+
     gx, gy, gz = global_dims
     rng = slab_range(first, last, z0, z0 + view.dimZ)
+    if getattr(view, "dataFormat", None) in (4, 5) and (code_fns is not None or pass_fn is None):
+        fns = code_fns or GpuCodeFns
+        ok = torch.tensor([1 if fns.supported(view, *(rng or (first, first))) else 0], dtype=torch.int64,
+                          device=device if device is not None else "cpu")
+        _all_reduce(ok, dist.ReduceOp.MIN, group)
+        if int(ok.item()):
+            out = _aggregates_codes(view, global_dims, z0, rng, group, device, fns)
+            if out is not None:
+                return out
+    pass_fn = pass_fn or _gpu_pass
     empty = _lib.HipAggregatePartial_t()
     lib.vktHipAggregatePartialInit(C.byref(empty))
     p1 = pass_fn(view, *rng, z0, 1, 0.0) if rng else empty
