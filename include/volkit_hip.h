@@ -109,7 +109,9 @@ VKTAPI vktError vktHipKernelScopeEnd(vktHipKernelScope scope);
  * general path on 8-voxel items), "pointwise.f32_halves" (1; 0 keeps 4-byte padded multi-row boxes
  * on the per-item loop), "pointwise.f32_wide" (0; 1 gives 4-byte general-path boxes 16-B items),
  * "aggregates.codes" (3; bit 0 UInt8, bit 1 UInt16: ComputeAggregates from one pass of code counts
- * instead of the two float passes).  For tests and in-process A/B measurements; unknown names return
+ * instead of the two float passes), "reduce.u8_rows16" (1; UInt8 code counts over range rows on 16-voxel
+ * items, row-end bytes subtracted inside the main loop; 2 subtracts them in a row walk after it;
+ * 0 keeps the 8-voxel item walk).  For tests and in-process A/B measurements; unknown names return
  * vktInvalidValue.
  *
  * Writes outside a range box: FillRange / CopyRange / convert and device-functor TransformRange

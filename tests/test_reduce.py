@@ -545,3 +545,62 @@ def test_aggregate_slab_partials_combine_to_the_whole(nx):
     assert (out.argmin.x, out.argmin.y, out.argmin.z) == tuple(whole.argmin)
     assert (out.argmax.x, out.argmax.y, out.argmax.z) == tuple(whole.argmax)
     assert out.mean == whole.mean and abs(out.var - whole.var) <= float(np.spacing(np.float32(whole.var)))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows16", [1, 2, 0])
+def test_u8_code_counts_over_rows_exact(rows16):
+    """UInt8 code counts over range rows (vktHipAggregateCodeCounts): the 16-voxel
+    row walk counts every byte of each row's 16-aligned cover and subtracts the bytes outside
+    the range again, inside the main loop (knob reduce.u8_rows16 = 1; rows of >= 9 items) or in
+    a row walk after it (2); the 8-voxel walk masks them (0).  Exact against
+    np.bincount of the box: row starts and ends at every phase mod 16, boxes touching x = 0 and
+    x = dimX, one-row / one-plane boxes, rows of fewer than 16 voxels inside one item, a volume
+    whose dimX is a multiple of 8 but not 16 (8-voxel walk either way), and ranges whose item
+    count leaves a partial wave-step."""
+    import torch
+    rng = np.random.default_rng(71)
+    vols = {(12, 21, 256): None, (9, 7, 1040): None, (5, 6, 200): None}
+    boxes = {(12, 21, 256): [((100, 3, 1), (228, 20, 12)), ((0, 0, 0), (256, 21, 12)), ((1, 0, 0), (255, 21, 12)),
+                             ((15, 2, 3), (17, 3, 4)), ((16, 5, 2), (32, 6, 11)), ((33, 4, 4), (47, 16, 9)),
+                             ((241, 0, 0), (256, 21, 12)), ((0, 7, 5), (1, 8, 6))],
+             (9, 7, 1040): [((3, 1, 2), (1037, 6, 8)), ((17, 0, 0), (1039, 7, 9)), ((0, 3, 4), (1040, 4, 5))],
+             (5, 6, 200): [((3, 1, 1), (197, 5, 4)), ((8, 0, 0), (200, 6, 5))]}
+    for dims, bl in boxes.items():
+        codes = rng.integers(0, 256, dims, dtype=np.uint8)
+        v = gpu_volume(codes, 4, 0.0, 1.0)
+        set_device(vkt.ExecutionPolicy.Device_GPU)
+        lib.vktHipSetTuningKnob(b"reduce.u8_rows16", rows16)
+        try:
+            for first, last in bl:
+                counts = torch.zeros(256, dtype=torch.int64, device="cuda")
+                err = lib.vktHipAggregateCodeCounts(v.hip_view(), _lib.Vec3i_t(*first), _lib.Vec3i_t(*last),
+                                                    C.c_void_p(counts.data_ptr()))
+                assert err == 0, _lib.last_error()
+                box = codes[first[2]:last[2], first[1]:last[1], first[0]:last[0]]
+                want = np.bincount(box.reshape(-1), minlength=256)
+                got = counts.cpu().numpy()
+                assert np.array_equal(got, want), (dims, first, last, np.nonzero(got != want)[0][:8])
+        finally:
+            lib.vktHipSetTuningKnob(b"reduce.u8_rows16", -1)
+            set_device(vkt.ExecutionPolicy.Device_CPU)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows16", [1, 2, 0])
+def test_u8_histogram_over_rows_from_code_counts(rows16):
+    """UInt8 histograms over range rows from the 16-voxel code counts folded into the bins with
+    the streaming kernel's bin formula (knob reduce.u8_rows16 1 / 2; 0 = the 8-voxel item walk):
+    padded and unpadded rows of >= 9 items (end bytes subtracted inside the main loop), bin
+    counts below, at and above 256, and mappings that drop codes outside [0, numBins)."""
+    rng = np.random.default_rng(5 + rows16)
+    codes = rng.integers(0, 256, (8, 20, 320), dtype=np.uint8)
+    lib.vktHipSetTuningKnob(b"reduce.u8_rows16", rows16)
+    try:
+        for first, last in (((3, 1, 1), (317, 19, 7)), ((16, 0, 0), (304, 20, 8)), ((100, 2, 3), (250, 3, 8))):
+            for mapping, nbins in (((0.0, 1.0), 256), ((0.0, 1.0), 7), ((-1.0, 3.0), 1000), ((0.25, 0.75), 64)):
+                got = gpu_histogram(codes, 4, *mapping, first, last, nbins)
+                ref, _ = ob.histogram_range(ob.Volume(codes, 4, *mapping), first, last, nbins)
+                np.testing.assert_array_equal(got, ref, err_msg=f"{first}->{last} map={mapping} nbins={nbins}")
+    finally:
+        lib.vktHipSetTuningKnob(b"reduce.u8_rows16", -1)

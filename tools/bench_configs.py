@@ -626,6 +626,25 @@ def main():
             ms = timed(lambda: lib.vktHipAggregatesRange(W, u0, u1, C.byref(agg)), R)
             report(f"aggcodes Aggregates UInt8 800^3 sub-box at x0=100 [codes={k}, {passes} pass(es)]", ms,
                    passes * 800 ** 3, 800 ** 3)
+        lib.vktHipSetTuningKnob(b"aggregates.codes", -1)
+        # the code-count walk over range rows: 16-voxel items + row-end subtraction vs 8-voxel items
+        hb = C.c_void_p()
+        if lib.vktHipAllocate(C.byref(hb), 256 * 8) != 0:
+            raise RuntimeError(_lib.last_error())
+        hbins = C.c_void_p(hb.value)
+        for k in (1, 2, 0):
+            lib.vktHipSetTuningKnob(b"reduce.u8_rows16", k)
+            for (a0, a1, what) in ((u0, u1, "800^3 sub-box at x0=100"),
+                                   (Vec3i_t(0, 100, 100), Vec3i_t(800, 900, 900), "800^3 sub-box x 0..800"),
+                                   (Vec3i_t(3, 0, 0), Vec3i_t(1021, n, n), "1018x1024^2 x 3..1021"),
+                                   (Vec3i_t(3, 0, 0), Vec3i_t(67, 64, 64), "64^3 box (fixed cost)")):
+                nv = (a1.x - a0.x) * (a1.y - a0.y) * (a1.z - a0.z)
+                ms = timed(lambda: lib.vktHipAggregatesRange(W, a0, a1, C.byref(agg)), R)
+                report(f"aggcodes Aggregates UInt8 {what} [rows16={k}]", ms, nv, nv)
+                ms = timed(lambda: lib.vktHipHistogramRange(W, a0, a1, hbins, 256, 0), R)
+                report(f"aggcodes Histogram UInt8 {what}, 256 bins [rows16={k}]", ms, nv, nv)
+        lib.vktHipSetTuningKnob(b"reduce.u8_rows16", -1)
+        lib.vktHipFree(hb)
         free(W)
         V = alloc((n,) * 3, 5, seed=11)
         for k in (3, 1):

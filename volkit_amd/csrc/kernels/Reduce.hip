@@ -381,6 +381,7 @@ namespace hipk
         // from px0 = fx & ~7 to the 8-aligned end; voxels outside [rx0, rx1) are not visited
         int32_t px0, rx0, rx1;
         uint32_t padded;
+        uint32_t rows;              // codeCountsU8RowsKernel: range rows (ny * nz)
     };
 
     typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -954,6 +955,157 @@ namespace hipk
             partials[blockIdx.x] = p;
     }
 
+    // UInt8 code counts over range ROWS (the non-CONTIG form of aggregatesFastKernel<CODES>):
+    // 16-voxel items, one aligned 16-B load per lane, covering each row from h.px0 = fx & ~15 to
+    // the 16-aligned end (h.fdIpr = items per row; dimX % 16 == 0, 16-B aligned volume).  Counts
+    // need no order and no mask: every loaded byte is counted, then the bytes of each row outside
+    // [rx0, rx1) (at most 15 + 15, at the same offsets in every row) are subtracted again.  The
+    // 8-voxel walk spent 3 fast divisions, a mask and 8 branches per 8 bytes, with 8-B loads:
+    // an 800^3 sub-box of 1024^3 took longer than the whole 1024^3 volume.
+    // INLOOP (rows of >= 9 items): each wave-step also subtracts the end bytes of the rows whose
+    // first / last item lies in its 256 items -- lane l re-reads the first (l < 32) or last item
+    // of row rA + l % 32, lines the step has just fetched; else a row walk after the main loop
+    // (its end items are separate sectors fetched again from HBM: 800^3 sub-box at x0 = 100,
+    // 139 us against 103 us for the same box at x0 = 0).
+    // Counters: 32 copies (h.rShift = 5) as in aggregatesFastKernel; a workgroup's net count of a
+    // code may be negative (its subtracted rows are not its counted items): the copies are summed
+    // mod 2^32 and flushed sign-extended.
+    template <bool INLOOP>
+    __global__ __launch_bounds__(kBlock) void codeCountsU8RowsKernel(FastHistArgs h)
+    {
+        constexpr int U = 4;
+        constexpr uint32_t kRowShift = 7;   // byte offset of a code's 32 counter copies
+        extern __shared__ uint32_t codeCnt[];
+        uint32_t const lane = threadIdx.x & 63;
+        char* const cLane = reinterpret_cast<char*>(codeCnt) + ((lane & 31u) << 2);
+        for (uint32_t i = threadIdx.x; i < (256u << 5); i += kBlock)
+            codeCnt[i] = 0;
+        __syncthreads();
+        auto rowStart = [&](uint32_t r) -> uint8_t const* {
+            uint32_t const zr = fdiv(r, h.fdNy);
+            uint32_t const yr = r - zr * h.fdNy.d;
+            return h.data + ((static_cast<uint64_t>(h.fz + zr) * static_cast<uint64_t>(h.dimY) + (h.fy + yr)) *
+                                 static_cast<uint64_t>(h.dimX) +
+                             static_cast<uint64_t>(h.px0));
+        };
+        auto itemPtr = [&](uint32_t i) -> uint8_t const* {
+            uint32_t const r = fdiv(i, h.fdIpr);
+            return rowStart(r) + 16u * (i - r * h.fdIpr.d);
+        };
+        auto addByte = [&](uint32_t c, uint32_t v) {
+            atomicAdd(reinterpret_cast<uint32_t*>(cLane + (c << kRowShift)), v);
+        };
+        auto count16 = [&](u32x4 const& x) {
+            uint32_t const w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    addByte(__builtin_amdgcn_ubfe(w[q], 8 * b, 8), 1u);
+        };
+        uint32_t const items = static_cast<uint32_t>(h.items);
+        uint32_t const wave = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+        uint32_t const waves = gridDim.x * (kBlock / 64);
+        int32_t const head = h.rx0 - h.px0;   // bytes [0, head) of a row's first item are outside
+        int32_t const tail = h.rx1 - h.px0 - 16 * static_cast<int32_t>(h.fdIpr.d - 1);   // [tail, 16) of its last
+        uint32_t const lastItem = 16u * (h.fdIpr.d - 1);
+        if constexpr (INLOOP)
+        {
+            // every step whole-wave: the last one's items past the range are not counted
+            uint32_t const steps = (items + 64 * U - 1) / (64 * U);
+            bool const tailSide = lane >= 32;
+            for (uint32_t st = wave; st < steps; st += waves)
+            {
+                uint32_t const s0 = st * (64 * U), s1 = min(s0 + 64 * U, items);
+                u32x4 x[U];
+#pragma unroll
+                for (int k = 0; k < U; ++k)
+                    x[k] = loadVec<u32x4, true>(itemPtr(min(s0 + k * 64 + lane, items - 1)));
+                // the end items of this step's rows (first / last item inside [s0, s1))
+                uint32_t const rA = fdiv(s0, h.fdIpr), rB = fdiv(s1 - 1, h.fdIpr);
+                uint32_t const row = rA + (lane & 31u);
+                uint32_t const ie = row * h.fdIpr.d + (tailSide ? h.fdIpr.d - 1 : 0u);
+                bool const edge = row <= rB && ie >= s0 && ie < s1 && (tailSide ? tail < 16 : head > 0);
+                u32x4 ex = {0u, 0u, 0u, 0u};
+                if (edge)
+                    ex = loadVec<u32x4, false>(rowStart(row) + (tailSide ? lastItem : 0u));
+#pragma unroll
+                for (int k = 0; k < U; ++k)
+                    if (s0 + k * 64 + lane < s1)
+                        count16(x[k]);
+                uint32_t const w[4] = {ex.x, ex.y, ex.z, ex.w};
+#pragma unroll
+                for (int b = 0; b < 16; ++b)
+                {
+                    bool const out = tailSide ? b >= tail : b < head;
+                    if (edge && out)
+                        addByte(__builtin_amdgcn_ubfe(w[b / 4], 8 * (b % 4), 8), ~0u);
+                }
+            }
+        }
+        else
+        {
+            uint32_t const steps = items / (64 * U);
+            for (uint32_t st = wave; st < steps; st += waves)
+            {
+                u32x4 x[U];
+#pragma unroll
+                for (int k = 0; k < U; ++k)
+                    x[k] = loadVec<u32x4, true>(itemPtr(st * (64 * U) + k * 64 + lane));
+#pragma unroll
+                for (int k = 0; k < U; ++k)
+                    count16(x[k]);
+            }
+            for (uint32_t it = steps * (64 * U) + wave * 64 + lane; it < items; it += waves * 64)
+                count16(loadVec<u32x4, true>(itemPtr(it)));
+        }
+        if (!INLOOP && h.padded)
+        {
+            // subtract each row's bytes outside the range: bytes [0, head) of its first item and
+            // [tail, 16) of its last -- the same offsets in every row (uniform branches); the two
+            // items of RU rows are loaded before the first subtraction
+            constexpr int RU = 4;
+            uint32_t const rows = h.rows, stride = gridDim.x * kBlock;
+            auto sub16 = [&](u32x4 const& x, int32_t b0, int32_t b1) {   // bytes [b0, b1) of x
+                uint32_t const w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+                for (int b = 0; b < 16; ++b)
+                    if (b >= b0 && b < b1)
+                        addByte(__builtin_amdgcn_ubfe(w[b / 4], 8 * (b % 4), 8), ~0u);
+            };
+            for (uint32_t r0 = blockIdx.x * kBlock + threadIdx.x; r0 < rows; r0 += RU * stride)
+            {
+                u32x4 hx[RU], tx[RU];
+                bool live[RU];
+#pragma unroll
+                for (int u = 0; u < RU; ++u)
+                {
+                    uint32_t const r = r0 + u * stride;
+                    live[u] = r < rows;
+                    uint8_t const* const p = rowStart(live[u] ? r : r0);
+                    hx[u] = loadVec<u32x4, true>(p);
+                    tx[u] = loadVec<u32x4, true>(p + lastItem);
+                }
+#pragma unroll
+                for (int u = 0; u < RU; ++u)
+                    if (live[u])
+                    {
+                        sub16(hx[u], 0, head);
+                        sub16(tx[u], tail, 16);
+                    }
+            }
+        }
+        __syncthreads();
+        for (uint32_t c = threadIdx.x; c < 256u; c += kBlock)
+        {
+            uint32_t sum = 0;
+            for (uint32_t r = 0; r < 32u; ++r)
+                sum += codeCnt[(c << 5) + ((r + c) & 31u)];
+            if (sum)
+                atomicAdd(&h.bins[c], static_cast<unsigned long long>(static_cast<int64_t>(static_cast<int32_t>(sum))));
+        }
+    }
+
     // UInt8 aggregates from the code counts of aggregatesFastKernel<CODES>: one workgroup, thread
     // c = code c.  Each present code contributes count * its value to the sum, value^count to the
     // product and count * (float)((value - mean)^2) to the sum of squares -- the per-voxel float
@@ -964,52 +1116,135 @@ namespace hipk
     // result: every present value finite and below FLT_MAX in magnitude and each extreme held by
     // ONE code (a mapping that rounds two present codes onto an extreme makes the caller rerun
     // the two float passes); 0 otherwise (targets -1).
-    // FMT UInt8 (256 codes, 256 threads: one code each) or UInt16 (65 536 codes, 1024 threads: 64
-    // each, strided so a wave reads consecutive counts).
-    template <int FMT>
+    // PHASE 0: one workgroup runs both loops (UInt8: 256 threads, one code each).  UInt16 (65 536
+    // codes) splits them over kCodeFinalBlocks workgroups of 1024 threads, one code each, in two
+    // launches: PHASE 1 the first loop, PHASE 2 the second (it needs the mean and the value
+    // extremes of all codes); in each, every workgroup publishes a partial and the LAST one to
+    // finish (work->ticket) combines them in block order (deterministic).  One 1024-thread
+    // workgroup running both loops over 65 536 codes (pow() per present code) took 139 us, the
+    // multi-workgroup first loop with the second in the last workgroup 44 us.  work->ticket /
+    // work->bad must be 0 at the PHASE 1 launch (PHASE 2's last workgroup leaves them 0).
+    constexpr uint32_t kCodeFinalBlocks = 64;
+    struct CodeFinalWork
+    {
+        uint32_t ticket, bad;
+        float vmin, vmax, mean, pad[3];
+        vktHipAggregatePartial_t parts[kCodeFinalBlocks];
+        struct Second
+        {
+            double sumSq;
+            int32_t nmin, nmax, cmin, cmax;
+        } parts2[kCodeFinalBlocks];
+    };
+
+    // thread 0 of the last workgroup to arrive (after every workgroup's thread 0 published)
+    __device__ __forceinline__ bool lastBlock(uint32_t* ticket, int32_t* sLast)
+    {
+        if (threadIdx.x == 0)
+        {
+            __threadfence();
+            *sLast = atomicAdd(ticket, 1u) == gridDim.x - 1 ? 1 : 0;
+        }
+        __syncthreads();
+        if (!*sLast)
+            return false;
+        __threadfence();
+        return true;
+    }
+
+    template <int FMT, int PHASE>
     __global__ __launch_bounds__(FMT == codec::FmtUInt8 ? 256 : 1024) void aggregatesCodesFinalKernel(
         unsigned long long const* counts, float lo, float hi, double numElems, vktHipAggregatePartial_t* res,
-        int32_t* targets)
+        int32_t* targets, CodeFinalWork* work)
     {
         constexpr uint32_t kCodes = FMT == codec::FmtUInt8 ? 256u : 65536u;
         constexpr uint32_t kThreads = FMT == codec::FmtUInt8 ? 256u : 1024u;
         constexpr int kWaves = static_cast<int>(kThreads / 64);
+        static_assert(PHASE == 0 || FMT == codec::FmtUInt16, "UInt16 splits the loops");
         __shared__ float sVmin, sVmax, sMean;
-        __shared__ int32_t sNmin, sNmax, sCmin, sCmax, sBad;
+        __shared__ int32_t sNmin, sNmax, sCmin, sCmax, sBad, sLast;
         if (threadIdx.x == 0)
         {
             sNmin = sNmax = sBad = 0;
             sCmin = sCmax = -1;
         }
         __syncthreads();
+        uint32_t const c0 = blockIdx.x * kThreads + threadIdx.x, cStride = gridDim.x * kThreads;
         vktHipAggregatePartial_t q = emptyPartial();
-        for (uint32_t c = threadIdx.x; c < kCodes; c += kThreads)
+        if constexpr (PHASE != 2)
         {
-            unsigned long long const cnt = counts[c];
-            if (cnt == 0ull)
-                continue;
-            float const v = codec::decode(c, FMT, lo, hi);
-            if (!(fabsf(v) < FLT_MAX))
-                atomicOr(&sBad, 1);
-            minCombine(q.minValue, q.minIndex, v, c);
-            maxCombine(q.maxValue, q.maxIndex, v, c);
-            double const dv = static_cast<double>(v), dn = static_cast<double>(cnt);
-            q.sum += dn * dv;
-            q.prod *= cnt == 1ull ? dv : pow(dv, dn);
-            q.count += cnt;
+            for (uint32_t c = c0; c < kCodes; c += cStride)
+            {
+                unsigned long long const cnt = counts[c];
+                if (cnt == 0ull)
+                    continue;
+                float const v = codec::decode(c, FMT, lo, hi);
+                if (!(fabsf(v) < FLT_MAX))
+                    atomicOr(&sBad, 1);
+                minCombine(q.minValue, q.minIndex, v, c);
+                maxCombine(q.maxValue, q.maxIndex, v, c);
+                double const dv = static_cast<double>(v), dn = static_cast<double>(cnt);
+                q.sum += dn * dv;
+                q.prod *= cnt == 1ull ? dv : pow(dv, dn);
+                q.count += cnt;
+            }
+            if constexpr (PHASE == 1)
+            {
+                blockReduce<kWaves>(q);
+                if (threadIdx.x == 0)
+                {
+                    work->parts[blockIdx.x] = q;
+                    if (sBad)
+                        atomicOr(&work->bad, 1u);
+                }
+                if (!lastBlock(&work->ticket, &sLast))
+                    return;
+                q = emptyPartial();
+                if (threadIdx.x < gridDim.x)
+                {
+                    // (other workgroups' stores: read past this CU's L1)
+                    vktHipAggregatePartial_t const volatile& o = work->parts[threadIdx.x];
+                    q.sum = o.sum;
+                    q.prod = o.prod;
+                    q.count = o.count;
+                    q.minValue = o.minValue;
+                    q.maxValue = o.maxValue;
+                    q.minIndex = o.minIndex;
+                    q.maxIndex = o.maxIndex;
+                }
+            }
+            blockReduce<kWaves>(q);
+            __syncthreads();
+            if (threadIdx.x == 0)
+            {
+                sVmin = q.minValue;
+                sVmax = q.maxValue;
+                sMean = static_cast<float>(static_cast<double>(static_cast<float>(q.sum)) / numElems);
+                vktHipAggregatePartial_t out = q;   // thread 0: sum / prod / count / value extremes
+                out.sumSq = 0.0;
+                out.minIndex = kNoIndex;   // set by aggregatesFindHead/TailKernel
+                out.maxIndex = kNoIndex;
+                res[0] = out;
+                if constexpr (PHASE == 1)
+                {
+                    work->vmin = sVmin;
+                    work->vmax = sVmax;
+                    work->mean = sMean;
+                    work->ticket = 0u;
+                }
+            }
+            if constexpr (PHASE == 1)
+                return;
         }
-        blockReduce<kWaves>(q);
-        __syncthreads();
-        vktHipAggregatePartial_t& r = q;   // thread 0: sum / prod / count / value extremes
-        if (threadIdx.x == 0)
+        else if (threadIdx.x == 0)
         {
-            sVmin = r.minValue;
-            sVmax = r.maxValue;
-            sMean = static_cast<float>(static_cast<double>(static_cast<float>(r.sum)) / numElems);
+            sVmin = work->vmin;   // (PHASE 1's stores: a kernel boundary lies between)
+            sVmax = work->vmax;
+            sMean = work->mean;
         }
         __syncthreads();
         vktHipAggregatePartial_t t = emptyPartial();
-        for (uint32_t c = threadIdx.x; c < kCodes; c += kThreads)
+        for (uint32_t c = PHASE == 2 ? c0 : threadIdx.x; c < kCodes; c += PHASE == 2 ? cStride : kThreads)
         {
             unsigned long long const cnt = counts[c];
             if (cnt == 0ull)
@@ -1031,14 +1266,43 @@ namespace hipk
         }
         blockReduce<kWaves>(t);
         __syncthreads();
+        if constexpr (PHASE == 2)
+        {
+            if (threadIdx.x == 0)
+                work->parts2[blockIdx.x] = CodeFinalWork::Second{t.sumSq, sNmin, sNmax, sCmin, sCmax};
+            if (!lastBlock(&work->ticket, &sLast))
+                return;
+            // every partial loaded at once (one volatile load after another from thread 0 cost a
+            // memory latency each: 47 us), then summed in block order by thread 0
+            __shared__ CodeFinalWork::Second sParts[kCodeFinalBlocks];
+            if (threadIdx.x < gridDim.x)
+            {
+                CodeFinalWork::Second const volatile& o = work->parts2[threadIdx.x];
+                sParts[threadIdx.x] = CodeFinalWork::Second{o.sumSq, o.nmin, o.nmax, o.cmin, o.cmax};
+            }
+            __syncthreads();
+            if (threadIdx.x == 0)
+            {
+                t.sumSq = 0.0;
+                sNmin = sNmax = 0;
+                sCmin = sCmax = -1;
+                for (uint32_t b = 0; b < gridDim.x; ++b)
+                {
+                    CodeFinalWork::Second const& o = sParts[b];
+                    t.sumSq += o.sumSq;
+                    sNmin += o.nmin;
+                    sNmax += o.nmax;
+                    sCmin = o.cmin >= 0 ? o.cmin : sCmin;
+                    sCmax = o.cmax >= 0 ? o.cmax : sCmax;
+                }
+                sBad = static_cast<int32_t>(*static_cast<uint32_t volatile*>(&work->bad));
+                work->ticket = 0u;
+                work->bad = 0u;
+            }
+        }
         if (threadIdx.x == 0)
         {
             bool const ok = sBad == 0 && sNmin == 1 && sNmax == 1;
-            vktHipAggregatePartial_t out = r;
-            out.sumSq = 0.0;
-            out.minIndex = kNoIndex;   // set by aggregatesFindHead/TailKernel
-            out.maxIndex = kNoIndex;
-            res[0] = out;
             vktHipAggregatePartial_t two = emptyPartial();
             two.sumSq = t.sumSq;
             two.count = ok ? 1u : 0u;
@@ -1091,12 +1355,15 @@ namespace hipk
             atomicMin(bMax, static_cast<unsigned long long>(spanGlobalIndex<CONTIG>(h, item, jMax)));
     }
 
-    // First occurrence of codes targets[0] / targets[1] (the extremes' codes), stage 1: ONE
-    // workgroup walks the first `headItems` items of the range in order, 1024 items per step,
-    // with LDS atomics, and stops at the first step after which both are known (on varied data,
-    // the first step: 8 Ki voxels).  Writes res[0].minIndex / maxIndex (kNoIndex if not found).
-    // One workgroup, because many waves folding into one global word serialise on it (a
-    // whole-grid version with global atomics and early exit took 0.35 ms).
+    // First occurrence of codes targets[0] / targets[1] (the extremes' codes), stage 1: the first
+    // `headItems` items of the range, one 1024-item step per workgroup (kFindHeadBlocks of them,
+    // all in flight at once), each workgroup folding its first hits in LDS and then with one
+    // global atomicMin per code into res[0].minIndex / maxIndex (kNoIndex before the launch).  On
+    // varied data the codes occur in the first step.  (One workgroup walking the head in order
+    // stopped early but paid one memory latency per step: 22-43 us for UInt16, whose extreme
+    // codes first occur ~65 Ki voxels in; a whole-grid walk with global atomics and early exit
+    // took 0.35 ms -- many waves folding into one global word serialise on it.)
+    constexpr uint32_t kFindHeadBlocks = 64;
     template <int BPV, bool CONTIG>
     __global__ __launch_bounds__(1024) void aggregatesFindHeadKernel(FastHistArgs h, int32_t const* targets,
                                                                     vktHipAggregatePartial_t* res, uint64_t headItems)
@@ -1109,21 +1376,18 @@ namespace hipk
             sMin = sMax = kNoIndex;
         __syncthreads();
         uint64_t const end = headItems < h.items ? headItems : h.items;
-        for (uint64_t base = 0; base < end; base += blockDim.x)
-        {
-            uint64_t const item = base + threadIdx.x;
-            if (item < end)
-                findCodes<BPV, CONTIG>(h, item, tmin, tmax, &sMin, &sMax);
-            __syncthreads();
-            bool const done = sMin != kNoIndex && sMax != kNoIndex;
-            __syncthreads();   // every thread has read before the next step's atomics
-            if (done)
-                break;
-        }
+        uint64_t const item = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+        if (item < end)
+            findCodes<BPV, CONTIG>(h, item, tmin, tmax, &sMin, &sMax);
+        __syncthreads();
         if (threadIdx.x == 0)
         {
-            res[0].minIndex = sMin;
-            res[0].maxIndex = sMax;
+            auto* const bMin = reinterpret_cast<unsigned long long*>(&res[0].minIndex);
+            auto* const bMax = reinterpret_cast<unsigned long long*>(&res[0].maxIndex);
+            if (sMin != kNoIndex)
+                atomicMin(bMin, sMin);
+            if (sMax != kNoIndex)
+                atomicMin(bMax, sMax);
         }
     }
 
@@ -1307,6 +1571,46 @@ namespace hipk
         return ok;
     }
 
+    // UInt8 code counts of a non-CONTIG span walk h added into h.bins (256 u64) by
+    // codeCountsU8RowsKernel (16-voxel items over the rows); false (nothing launched) when the
+    // volume's rows are not on the 16-voxel grid or knob reduce.u8_rows16 is 0.
+    bool launchU8RowCounts(FastHistArgs const& h, hipStream_t s)
+    {
+        int64_t const k = rt::knob(rt::Knob::ReduceU8Rows16);
+        if (h.dimX % 16 != 0 || k == 0)
+            return false;
+        uint64_t const rows = h.items / h.fdIpr.d;
+        int32_t const px0 = h.rx0 & ~15, px1 = (h.rx1 + 15) & ~15;
+        uint64_t const ipr = static_cast<uint64_t>(px1 - px0) / 16;
+        FastHistArgs r = h;
+        r.px0 = px0;
+        r.fdIpr = makeFastDiv(static_cast<uint32_t>(ipr));
+        r.items = ipr * rows;
+        r.rows = static_cast<uint32_t>(rows);
+        r.padded = px0 != h.rx0 || px1 != h.rx1 ? 1u : 0u;
+        unsigned const g = streamingGrid(r.items, 64u * 4u * (kBlock / 64), 4);
+        size_t const lds = 256u << 7;   // 32 copies of 256 counters
+        // end bytes subtracted inside the main loop needs <= 32 rows per 256-item step
+        if (r.padded && ipr >= 9 && k == 1)
+            hipLaunchKernelGGL(codeCountsU8RowsKernel<true>, dim3(g), dim3(kBlock), lds, s, r);
+        else
+            hipLaunchKernelGGL(codeCountsU8RowsKernel<false>, dim3(g), dim3(kBlock), lds, s, r);
+        return true;
+    }
+
+    // UInt8 histogram from code counts: bins[bin(c)] += counts[c] with the streaming kernel's own
+    // bin formula (codes outside [0, numBins) dropped, as its trash row)
+    __global__ __launch_bounds__(256) void histogramFromCodesKernel(unsigned long long const* counts, float lo,
+                                                                  float hi, float scale, uint32_t nb,
+                                                                  unsigned long long* bins)
+    {
+        uint32_t const c = threadIdx.x;
+        float const v = codec::decode(c, codec::FmtUInt8, lo, hi);
+        uint32_t const b = fastBin((v - lo) * scale, static_cast<float>(nb), nb);
+        if (b < nb && counts[c] != 0ull)
+            atomicAdd(&bins[b], counts[c]);
+    }
+
     // Launches histogramFastKernel when the range qualifies (see its comment); false otherwise.
     bool launchFastHistogram(BoxArgs const& a, HistArgs const& hh, hipStream_t s)
     {
@@ -1351,6 +1655,25 @@ namespace hipk
                     shift = hostBinU8(c, a.lo, a.hi, hh.scale, static_cast<float>(hh.numBins), hh.numBins) == (c >> sh);
                 h.binShift = sh;
             }
+        }
+        if (fmt == codec::FmtUInt8 && !contig && h.dimX % 16 == 0 && rt::knob(rt::Knob::ReduceU8Rows16) != 0)
+        {
+            // range rows: count the 256 codes with the 16-voxel row walk, then fold the counts
+            // into the bins (800^3 sub-box of 1024^3 at x0 = 100, 256 bins: DESIGN §4.8)
+            static rt::StreamScratch scratch;
+            auto* const counts = static_cast<unsigned long long*>(scratch.acquire(256 * sizeof(unsigned long long), s));
+            if (!counts)
+                return false;
+            FastHistArgs c = h;
+            c.bins = counts;
+            bool const ok = hipMemsetAsync(counts, 0, 256 * sizeof(unsigned long long), s) == hipSuccess &&
+                            launchU8RowCounts(c, s);
+            if (ok)
+                hipLaunchKernelGGL(histogramFromCodesKernel, dim3(1), dim3(256), 0, s, counts, a.lo, a.hi, h.scale, h.nb,
+                                   h.bins);
+            scratch.release(s);
+            if (ok)
+                return true;
         }
 #define VKT_FAST_HIST(FMT, TILED, BLOCK, G, LDS)                                                                   \
     do {                                                                                                           \
@@ -1519,7 +1842,7 @@ namespace hipk
             if (contig)
                 hipLaunchKernelGGL((aggregatesFastKernel<1, codec::FmtUInt8, true, false, true>), dim3(g), dim3(kBlock),
                                    lds, s, h, static_cast<float const*>(nullptr), 0.f, none);
-            else
+            else if (!launchU8RowCounts(h, s))
                 hipLaunchKernelGGL((aggregatesFastKernel<1, codec::FmtUInt8, false, false, true>), dim3(g), dim3(kBlock),
                                    lds, s, h, static_cast<float const*>(nullptr), 0.f, none);
         }
@@ -1545,26 +1868,35 @@ namespace hipk
         return true;
     }
 
-    void launchCodesFinal(unsigned long long const* counts, int32_t fmt, float lo, float hi, double numElems,
-                          vktHipAggregatePartial_t* res, int32_t* targets, hipStream_t s)
+    // work: device scratch of sizeof(CodeFinalWork) bytes (UInt16; its ticket is zeroed here)
+    bool launchCodesFinal(unsigned long long const* counts, int32_t fmt, float lo, float hi, double numElems,
+                          vktHipAggregatePartial_t* res, int32_t* targets, CodeFinalWork* work, hipStream_t s)
     {
         if (fmt == codec::FmtUInt8)
-            hipLaunchKernelGGL((aggregatesCodesFinalKernel<codec::FmtUInt8>), dim3(1), dim3(256), 0, s, counts, lo, hi,
-                               numElems, res, targets);
+            hipLaunchKernelGGL((aggregatesCodesFinalKernel<codec::FmtUInt8, 0>), dim3(1), dim3(256), 0, s, counts, lo,
+                               hi, numElems, res, targets, work);
         else
-            hipLaunchKernelGGL((aggregatesCodesFinalKernel<codec::FmtUInt16>), dim3(1), dim3(1024), 0, s, counts, lo, hi,
-                               numElems, res, targets);
+        {
+            if (hipMemsetAsync(work, 0, 8, s) != hipSuccess)
+                return false;
+            hipLaunchKernelGGL((aggregatesCodesFinalKernel<codec::FmtUInt16, 1>), dim3(kCodeFinalBlocks), dim3(1024), 0,
+                               s, counts, lo, hi, numElems, res, targets, work);
+            hipLaunchKernelGGL((aggregatesCodesFinalKernel<codec::FmtUInt16, 2>), dim3(kCodeFinalBlocks), dim3(1024), 0,
+                               s, counts, lo, hi, numElems, res, targets, work);
+        }
+        return true;
     }
 
     // First occurrences of codes targets[0] / [1] in the walk h into res[0].minIndex / maxIndex.
     void launchFindCodes(FastHistArgs const& h, bool contig, int32_t fmt, int32_t const* targets,
                          vktHipAggregatePartial_t* res, hipStream_t s)
     {
-        uint64_t const head = 64u * 1024u;   // stage 1 covers the first 512 Ki voxels at most
+        uint64_t const head = 1024u * kFindHeadBlocks;   // stage 1 covers the first 512 Ki voxels at most
         unsigned const gf = static_cast<unsigned>(std::max<uint64_t>(1, std::min<uint64_t>(2048, (h.items + kBlock - 1) / kBlock)));
+        unsigned const gh = static_cast<unsigned>(std::max<uint64_t>(1, (std::min<uint64_t>(head, h.items) + 1023) / 1024));
 #define VKT_FIND(B, CT)                                                                                          \
     do {                                                                                                         \
-        hipLaunchKernelGGL((aggregatesFindHeadKernel<B, CT>), dim3(1), dim3(1024), 0, s, h, targets, res, head);   \
+        hipLaunchKernelGGL((aggregatesFindHeadKernel<B, CT>), dim3(gh), dim3(1024), 0, s, h, targets, res, head);  \
         hipLaunchKernelGGL((aggregatesFindTailKernel<B, CT>), dim3(gf), dim3(kBlock), 0, s, h, targets, res, head); \
     } while (0)
         if (fmt == codec::FmtUInt8)
@@ -1580,7 +1912,8 @@ namespace hipk
 
     // UInt8 / UInt16 aggregates in one data pass: code counts, aggregatesCodesFinalKernel, then the
     // first-occurrence search, into res[0], res[1]; false when the range does not take the
-    // streaming walk.  scratch: the code counts (256 or 65 536), then 2 target codes.
+    // streaming walk.  scratch: the code counts (256 or 65 536), 2 target codes
+    // + 8 B, then the final kernel's CodeFinalWork.
     bool launchCodeAggregates(BoxArgs const& a, hipStream_t s, double numElems, void* scratch, unsigned g,
                               vktHipAggregatePartial_t* res)
     {
@@ -1591,9 +1924,11 @@ namespace hipk
         uint32_t const codes = a.fmt == codec::FmtUInt8 ? 256u : 65536u;
         h.bins = static_cast<unsigned long long*>(scratch);
         auto* const targets = reinterpret_cast<int32_t*>(h.bins + codes);
+        auto* const work = reinterpret_cast<CodeFinalWork*>(targets + 4);
         if (!launchCodeCounts(h, contig, a.fmt, g, s))
             return false;
-        launchCodesFinal(h.bins, a.fmt, a.lo, a.hi, numElems, res, targets, s);
+        if (!launchCodesFinal(h.bins, a.fmt, a.lo, a.hi, numElems, res, targets, work, s))
+            return false;
         launchFindCodes(h, contig, a.fmt, targets, res, s);
         return true;
     }
@@ -1746,7 +2081,8 @@ vktError vktHipAggregatesRange(vktHipVolumeView_t volume, vktVec3i_t first, vktV
         // counts cannot give the first occurrence of an extreme (aggregatesCodesFinalKernel)
         hipStream_t s = rt::computeStream();
         AggScratch& sc = aggScratch();
-        size_t const bytes = 2 * sizeof(vktHipAggregatePartial_t) + 65536 * sizeof(unsigned long long) + 16;
+        size_t const bytes = 2 * sizeof(vktHipAggregatePartial_t) + 65536 * sizeof(unsigned long long) + 16 +
+                             sizeof(CodeFinalWork);
         auto* res = static_cast<vktHipAggregatePartial_t*>(sc.dev.acquire(bytes, s));
         if (!res)
             return vktInvalidValue;
@@ -1871,13 +2207,17 @@ vktError vktHipAggregatesFromCodes(uint64_t const* counts, int32_t dataFormat, f
         return rt::fail("vktHipAggregatesFromCodes: UInt8 / UInt16 only");
     hipStream_t s = rt::computeStream();
     AggScratch& sc = aggScratch();
-    size_t const bytes = 2 * sizeof(vktHipAggregatePartial_t) + 16;
+    size_t const bytes = 2 * sizeof(vktHipAggregatePartial_t) + 16 + sizeof(CodeFinalWork);
     auto* res = static_cast<vktHipAggregatePartial_t*>(sc.dev.acquire(bytes, s));
     if (!res)
         return vktInvalidValue;
     auto* targets = reinterpret_cast<int32_t*>(res + 2);
-    launchCodesFinal(reinterpret_cast<unsigned long long const*>(counts), dataFormat, mappingLo, mappingHi,
-                     static_cast<double>(numElems), res, targets, s);
+    if (!launchCodesFinal(reinterpret_cast<unsigned long long const*>(counts), dataFormat, mappingLo, mappingHi,
+                          static_cast<double>(numElems), res, targets, reinterpret_cast<CodeFinalWork*>(targets + 4), s))
+    {
+        sc.dev.release(s);
+        return rt::check(hipGetLastError(), "vktHipAggregatesFromCodes");
+    }
     struct
     {
         vktHipAggregatePartial_t r[2];
@@ -1922,7 +2262,10 @@ vktError vktHipAggregateFirstCodes(vktHipVolumeView_t volume, vktVec3i_t first, 
         return vktInvalidValue;
     auto* targets = reinterpret_cast<int32_t*>(res + 2);
     int32_t const t[2] = {minCode, maxCode};
+    uint64_t const none[2] = {kNoIndex, kNoIndex};   // the search folds into them with atomicMin
     e = rt::check(hipMemcpyAsync(targets, t, sizeof(t), hipMemcpyHostToDevice, s), "hipMemcpyAsync");
+    if (e == vktNoError)
+        e = rt::check(hipMemcpyAsync(&res[0].minIndex, none, sizeof(none), hipMemcpyHostToDevice, s), "hipMemcpyAsync");
     if (e == vktNoError)
         launchFindCodes(h, contig, a.fmt, targets, res, s);
     uint64_t out[2] = {kNoIndex, kNoIndex};

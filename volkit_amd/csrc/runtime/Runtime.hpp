@@ -90,6 +90,7 @@ namespace rt
         PointwiseF32Halves,            // 0: padded 4-byte rows keep the per-item loop
         PointwiseF32Wide,              // 1: 4-byte general-path boxes use 16-B items (measured neutral; off)
         AggregatesCodes,               // bit 0 UInt8, bit 1 UInt16: ComputeAggregates from one pass of code counts
+        ReduceU8Rows16,                // UInt8 code counts over range rows with 16-voxel items (codeCountsU8RowsKernel)
         Count
     };
     int64_t knob(Knob k);
