@@ -111,7 +111,8 @@ VKTAPI vktError vktHipKernelScopeEnd(vktHipKernelScope scope);
  * "aggregates.codes" (3; bit 0 UInt8, bit 1 UInt16: ComputeAggregates from one pass of code counts
  * instead of the two float passes), "reduce.u8_rows16" (1; UInt8 code counts over range rows on 16-voxel
  * items, row-end bytes subtracted inside the main loop; 2 subtracts them in a row walk after it;
- * 0 keeps the 8-voxel item walk).  For tests and in-process A/B measurements; unknown names return
+ * 0 keeps the 8-voxel item walk), "decompose.grid" (1; 0 makes uniform brick grids load a
+ * per-brick descriptor instead of deriving it from the brick index).  For tests and in-process A/B measurements; unknown names return
  * vktInvalidValue.
  *
  * Writes outside a range box: FillRange / CopyRange / convert and device-functor TransformRange

@@ -134,6 +134,25 @@ def test_brick_decompose_parity(fmt, dims, brick, neg, pos):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("fmt", [4, 5, 7])
+@pytest.mark.parametrize("dims,brick,neg,pos", LAYOUTS)
+def test_brick_decompose_descriptor_table(fmt, dims, brick, neg, pos):
+    """Knob decompose.grid = 0: uniform brick grids load one descriptor per brick instead of
+    deriving it from the brick index (the default, tested by test_brick_decompose_parity)."""
+    rng = np.random.default_rng(fmt * 100 + sum(dims) + 7)
+    codes = rand_codes(rng, fmt, dims[::-1])
+    assert lib.vktHipSetTuningKnob(b"decompose.grid", 0) == 0
+    try:
+        err, got = gpu_decompose(codes, fmt, (0.0, 1.0), brick, neg, pos)
+    finally:
+        assert lib.vktHipSetTuningKnob(b"decompose.grid", -1) == 0
+    assert err == vkt.NoError, vkt.last_error()
+    ref = ob.brick_decompose(ob.Volume(codes, fmt), brick, neg, pos)
+    for idx, v in ref.items():
+        np.testing.assert_array_equal(got[idx], v.codes, err_msg=f"brick {idx}")
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("aligned", [1, 2])
 @pytest.mark.parametrize("fmt", [4, 5, 7])
 @pytest.mark.parametrize("dims,brick,neg,pos", LAYOUTS[1:4] + LAYOUTS[6:])

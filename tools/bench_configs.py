@@ -526,6 +526,39 @@ def main():
         del V
         ep.device = vkt.ExecutionPolicy.Device_CPU
         vkt.SetThreadExecutionPolicy(ep)
+    if want("decgrid"):
+        # in-process A/B of grid-derived brick descriptors (knob decompose.grid): back-to-back and
+        # single synchronised calls, median of 3 rounds
+        import volkit_amd.volkit as vkt
+        ep = vkt.GetThreadExecutionPolicy()
+        ep.device = vkt.ExecutionPolicy.Device_GPU
+        vkt.SetThreadExecutionPolicy(ep)
+        n = 1024
+        V = vkt.StructuredVolume(n, n, n, vkt.DataFormat_UInt16)
+        vkt.Synthesize(V, 77)
+        ab = {}
+        for bs, halo in ((16, (1, 1, 1)), (32, (1, 1, 1)), (64, (1, 1, 1)), (128, (0, 0, 0))):
+            arr = vkt.Array3D_StructuredVolume()
+            b3, h3 = vkt.Vec3i(bs, bs, bs), vkt.Vec3i(*halo)
+            vkt.BrickDecomposeResize(arr, V, b3, h3, h3)
+            vox = sum(arr[(i, j, k)].getSizeInBytes() // 2 for k in range(arr.dims().z)
+                      for j in range(arr.dims().y) for i in range(arr.dims().x))
+            for rnd in range(3):
+                for k in (1, 0):
+                    lib.vktHipSetTuningKnob(b"decompose.grid", k)
+                    ab.setdefault((bs, halo, k, "back-to-back", vox), []).append(
+                        pipelined(lambda: vkt.BrickDecompose(arr, V, b3, h3, h3), R))
+                    ab.setdefault((bs, halo, k, "incl. host planning", vox), []).append(
+                        timed(lambda: vkt.BrickDecompose(arr, V, b3, h3, h3), R))
+            del arr
+        lib.vktHipSetTuningKnob(b"decompose.grid", -1)
+        for (bs, halo, k, how, vox), ts in sorted(ab.items()):
+            ts.sort()
+            report(f"decgrid BrickDecompose 1024^3 UInt16 -> {bs}^3 bricks halo {halo} grid={k} ({how}, median of 3 "
+                   f"rounds, spread {ts[0]:.4f}-{ts[-1]:.4f})", ts[1], 4 * vox, vox)
+        del V
+        ep.device = vkt.ExecutionPolicy.Device_CPU
+        vkt.SetThreadExecutionPolicy(ep)
     if want("decpmc"):
         # one case for PMC passes (VKT_KNOBS picks the variant): 32^3 bricks + halo 1
         import volkit_amd.volkit as vkt

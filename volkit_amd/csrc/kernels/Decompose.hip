@@ -24,6 +24,7 @@
 #include "volkit_hip.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <mutex>
 #include <vector>
@@ -286,10 +287,38 @@ namespace hipk
         }
     }
 
-    template <int BPV, int kStageWords>
-    __global__ __launch_bounds__(kBlock) void brickCopyKernel(BrickDesc const* bricks, FastDiv chunksPerBrick,
-                                                             FastDiv groupSize, uint8_t const* src, int32_t sdx,
-                                                             int32_t sdy, int32_t sdz, int32_t alignedLds)
+    // A uniform brick grid (what BrickDecompose builds: brick (ix, iy, iz) at index ix + nbx * (iy
+    // + nby * iz), box = the grid cell extended by the halo, every brick linear): descriptors are
+    // derived from the brick index and three classes per axis (first, interior, last brick), so a
+    // workgroup loads only its brick's data pointer -- needed no earlier than its stores -- instead
+    // of waiting for a 96-B descriptor before its first source load.
+    struct BrickGrid
+    {
+        uint8_t* const* dst;                   // data pointer of brick b
+        FastDiv fnbx, fnby;                    // bricks per grid row / per grid plane (y)
+        int32_t nbx, nby, nbz;
+        int32_t fx0, fy0, fz0;                 // box start of brick (0, 0, 0) (= -halo)
+        int32_t bx, by, bz;                    // brick size (grid step)
+        int32_t nx[3], ny[3], nz[3];           // box extent per class: 0 first, 1 interior, 2 last
+        FastDiv fdx[3], fwpr[3], fdy[3];       // divisors of nx, the source words per row, ny
+    };
+
+    __device__ __forceinline__ int gridClass(int32_t i, int32_t n)
+    {
+        return i == n - 1 ? 2 : (i == 0 ? 0 : 1);
+    }
+
+    template <class T>
+    __device__ __forceinline__ T pick3(T const (&a)[3], int c)
+    {
+        return c == 0 ? a[0] : (c == 1 ? a[1] : a[2]);
+    }
+
+    template <int BPV, int kStageWords, bool GRID>
+    __global__ __launch_bounds__(kBlock) void brickCopyKernel(BrickDesc const* bricks, BrickGrid grid,
+                                                             FastDiv chunksPerBrick, FastDiv groupSize,
+                                                             uint8_t const* src, int32_t sdx, int32_t sdy, int32_t sdz,
+                                                             int32_t alignedLds)
     {
         constexpr int32_t V = 16 / BPV;
         // blockIdx = (group, chunk, brick in group): consecutive workgroups copy the same rows
@@ -302,11 +331,35 @@ namespace hipk
         uint32_t const grp = fdiv(rest, chunksPerBrick);
         uint32_t const chunk = __builtin_amdgcn_readfirstlane(rest - grp * chunksPerBrick.d);
         uint32_t const b = __builtin_amdgcn_readfirstlane(grp * groupSize.d + ig);
-        BrickDesc const d = bricks[b];
+        BrickDesc d;
+        if constexpr (GRID)
+        {
+            uint32_t const yz = fdiv(b, grid.fnbx);
+            int32_t const ix = static_cast<int32_t>(b - yz * grid.fnbx.d);
+            uint32_t const izu = fdiv(yz, grid.fnby);
+            int32_t const iy = static_cast<int32_t>(yz - izu * grid.fnby.d), iz = static_cast<int32_t>(izu);
+            int const cx = gridClass(ix, grid.nbx), cy = gridClass(iy, grid.nby), cz = gridClass(iz, grid.nbz);
+            d.dst = grid.dst[b];
+            d.fx = grid.fx0 + ix * grid.bx;
+            d.fy = grid.fy0 + iy * grid.by;
+            d.fz = grid.fz0 + iz * grid.bz;
+            d.nx = pick3(grid.nx, cx);
+            int32_t const ny = pick3(grid.ny, cy), nz = pick3(grid.nz, cz);
+            d.dimX = d.nx;
+            d.dimY = ny;
+            d.nvox = static_cast<uint32_t>(d.nx) * static_cast<uint32_t>(ny) * static_cast<uint32_t>(nz);
+            d.nitems = (d.nvox + V - 1) / V;
+            d.linear = 1;
+            d.fdx = pick3(grid.fdx, cx);
+            d.fwpr = pick3(grid.fwpr, cx);
+            d.fdy = pick3(grid.fdy, cy);
+        }
+        else
+            d = bricks[b];
         uint32_t const base = chunk * kBrickChunk;
         if (base >= d.nitems)
             return;   // border bricks are smaller than the largest one
-        if (d.linear)
+        if (GRID || d.linear)
         {
             brickStaged<BPV, kStageWords>(d, base, src, sdx, sdy, sdz, alignedLds);
             return;
@@ -370,6 +423,8 @@ namespace hipk
     {
         BrickDesc* host = nullptr;
         BrickDesc* dev = nullptr;
+        uint8_t** hostPtr = nullptr;   // brick data pointers (uniform grids, BrickGrid::dst)
+        uint8_t** devPtr = nullptr;
         size_t cap = 0;
         hipEvent_t done = nullptr;
         hipEvent_t copied = nullptr;   // the table's upload (copy stream) finished
@@ -388,6 +443,85 @@ namespace hipk
     {
         static DescRing r;
         return r;
+    }
+
+    // Uniform brick grid inferred from the range list (BrickGrid): nbx = the leading run of ranges
+    // on one y/z box, nby = the rows of the first plane; the grid step from the neighbours of
+    // range 0; the box extents of each axis class from one range each.  False when the list does
+    // not factor into nbx * nby * nbz.  Each range is then checked against the pattern inside the
+    // descriptor loop (gridMatches) -- one pass over the bricks, no second walk.
+    struct GridGuess
+    {
+        BrickGrid g{};
+        size_t pz = 0;
+        bool ok = false;
+    };
+
+    GridGuess inferGrid(vktHipBrickRange_t const* r, size_t n)
+    {
+        GridGuess q;
+        if (n == 0 || n >= (1ull << 31))
+            return q;
+        auto sameYZ = [&](size_t i) { return r[i].first.y == r[0].first.y && r[i].first.z == r[0].first.z; };
+        size_t nbx = 1;
+        while (nbx < n && sameYZ(nbx))
+            ++nbx;
+        size_t nby = 1;
+        while ((nby + 1) * nbx <= n && r[nby * nbx].first.z == r[0].first.z && r[nby * nbx].first.y != r[(nby - 1) * nbx].first.y)
+            ++nby;
+        if (n % (nbx * nby) != 0)
+            return q;
+        size_t const nbz = n / (nbx * nby), pz = nbx * nby;
+        BrickGrid& g = q.g;
+        g.nbx = static_cast<int32_t>(nbx);
+        g.nby = static_cast<int32_t>(nby);
+        g.nbz = static_cast<int32_t>(nbz);
+        g.fnbx = makeFastDiv(static_cast<uint32_t>(nbx));
+        g.fnby = makeFastDiv(static_cast<uint32_t>(nby));
+        g.fx0 = r[0].first.x;
+        g.fy0 = r[0].first.y;
+        g.fz0 = r[0].first.z;
+        g.bx = nbx > 1 ? r[1].first.x - r[0].first.x : 0;
+        g.by = nby > 1 ? r[nbx].first.y - r[0].first.y : 0;
+        g.bz = nbz > 1 ? r[pz].first.z - r[0].first.z : 0;
+        auto rep = [](int c, size_t nb) -> size_t { return c == 0 ? 0 : (c == 1 ? (nb > 2 ? 1 : 0) : nb - 1); };
+        for (int c = 0; c < 3; ++c)
+        {
+            g.nx[c] = r[rep(c, nbx)].last.x - r[rep(c, nbx)].first.x;
+            g.ny[c] = r[rep(c, nby) * nbx].last.y - r[rep(c, nby) * nbx].first.y;
+            g.nz[c] = r[rep(c, nbz) * pz].last.z - r[rep(c, nbz) * pz].first.z;
+        }
+        q.pz = pz;
+        q.ok = true;
+        return q;
+    }
+
+    // range i (its descriptor d) at its place in the inferred grid, a linear brick
+    bool gridMatches(GridGuess const& q, vktHipBrickRange_t const& r, BrickDesc const& d, size_t i)
+    {
+        BrickGrid const& g = q.g;
+        int32_t const ix = static_cast<int32_t>(i % static_cast<size_t>(g.nbx));
+        int32_t const iy = static_cast<int32_t>((i / static_cast<size_t>(g.nbx)) % static_cast<size_t>(g.nby));
+        int32_t const iz = static_cast<int32_t>(i / q.pz);
+        auto cls = [](int32_t k, int32_t nb) { return k == nb - 1 ? 2 : (k == 0 ? 0 : 1); };
+        int32_t const nx = g.nx[cls(ix, g.nbx)], ny = g.ny[cls(iy, g.nby)], nz = g.nz[cls(iz, g.nbz)];
+        return d.linear && r.first.x == g.fx0 + ix * g.bx && r.first.y == g.fy0 + iy * g.by &&
+               r.first.z == g.fz0 + iz * g.bz && r.last.x - r.first.x == nx && r.last.y - r.first.y == ny &&
+               r.last.z - r.first.z == nz;
+    }
+
+    // The class divisors from one descriptor of each class (every brick of a class has the same
+    // box extent and source span, so the same divisors: gridMatches held for all of them).
+    void gridDivisors(GridGuess& q, BrickDesc const* d)
+    {
+        BrickGrid& g = q.g;
+        auto rep = [](int c, int32_t nb) -> size_t { return c == 0 ? 0 : (c == 1 ? (nb > 2 ? 1 : 0) : nb - 1); };
+        for (int c = 0; c < 3; ++c)
+        {
+            g.fdx[c] = d[rep(c, g.nbx)].fdx;
+            g.fwpr[c] = d[rep(c, g.nbx)].fwpr;
+            g.fdy[c] = d[rep(c, g.nby) * static_cast<size_t>(g.nbx)].fdy;
+        }
     }
 
 } // hipk
@@ -430,11 +564,19 @@ vktError vktHipBrickDecompose(vktHipVolumeView_t source, vktHipBrickRange_t cons
             VKT_HIP_TRY(hipHostFree(st.host));
         if (st.dev)
             VKT_HIP_TRY(hipFree(st.dev));
+        if (st.hostPtr)
+            VKT_HIP_TRY(hipHostFree(st.hostPtr));
+        if (st.devPtr)
+            VKT_HIP_TRY(hipFree(st.devPtr));
         st.host = nullptr;
         st.dev = nullptr;
+        st.hostPtr = nullptr;
+        st.devPtr = nullptr;
         st.cap = 0;
         VKT_HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&st.host), need * sizeof(BrickDesc)));
         VKT_HIP_TRY(hipMalloc(reinterpret_cast<void**>(&st.dev), need * sizeof(BrickDesc)));
+        VKT_HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&st.hostPtr), need * sizeof(uint8_t*)));
+        VKT_HIP_TRY(hipMalloc(reinterpret_cast<void**>(&st.devPtr), need * sizeof(uint8_t*)));
         st.cap = need;
     }
     if (!st.done)
@@ -448,6 +590,11 @@ vktError vktHipBrickDecompose(vktHipVolumeView_t source, vktHipBrickRange_t cons
     // One descriptor per brick, at the brick's own index (a brick with an empty range or one that
     // needs unmap -> map gets nitems = 0 and its workgroups return at once), built in parallel
     // chunks on the host pool: 262 144 bricks of 16^3 cost ~9 ns each serially.
+    // uniform grid (BrickGrid): inferred from the ranges, each range checked in the loop below
+    GridGuess guess = rt::knob(rt::Knob::DecomposeGrid) != 0 ? inferGrid(bricks, static_cast<size_t>(numBricks))
+                                                            : GridGuess{};
+    std::atomic<bool> gridOk{guess.ok};
+    uint8_t** const ptrs = st.hostPtr;
     std::mutex merge;
     std::vector<int32_t> slow;
     uint32_t maxItems = 0;
@@ -471,6 +618,7 @@ vktError vktHipBrickDecompose(vktHipVolumeView_t source, vktHipBrickRange_t cons
             }
         } divSeg, divX, divWpr, divY;
         std::vector<int32_t> mySlow;
+        bool myGrid = guess.ok && gridOk.load(std::memory_order_relaxed);
         uint32_t myMax = 0;
         int32_t myErr = numBricks;
         char const* myWhat = nullptr;
@@ -492,7 +640,10 @@ vktError vktHipBrickDecompose(vktHipVolumeView_t source, vktHipBrickRange_t cons
             int64_t nx = int64_t(br.last.x) - br.first.x, ny = int64_t(br.last.y) - br.first.y;
             int64_t nz = int64_t(br.last.z) - br.first.z;
             if (nx <= 0 || ny <= 0 || nz <= 0)
+            {
+                myGrid = false;   // (the grid kernel would copy a box for it)
                 continue;
+            }
             if (nx > br.brick.dimX || ny > br.brick.dimY || nz > br.brick.dimZ)
             {
                 myErr = i;
@@ -530,7 +681,14 @@ vktError vktHipBrickDecompose(vktHipVolumeView_t source, vktHipBrickRange_t cons
             }
             d.fdy = divY(static_cast<uint32_t>(ny));
             myMax = d.nitems > myMax ? d.nitems : myMax;
+            if (myGrid)
+            {
+                myGrid = gridMatches(guess, br, d, ii);
+                ptrs[i] = d.dst;
+            }
         }
+        if (!myGrid)
+            gridOk.store(false, std::memory_order_relaxed);
         std::lock_guard<std::mutex> g(merge);
         slow.insert(slow.end(), mySlow.begin(), mySlow.end());
         maxItems = std::max(maxItems, myMax);
@@ -553,20 +711,31 @@ vktError vktHipBrickDecompose(vktHipVolumeView_t source, vktHipBrickRange_t cons
             return rt::fail("vktHipBrickDecompose: too many bricks for one launch");
         ring.next = (ring.next + 1) % kDescSlots;
         BrickDesc* dev = st.dev;
-        // the table goes up on the copy stream, so it overlaps the previous call's kernel
-        // (262 144 descriptors of 16^3 bricks are 25 MB, 0.59 ms of PCIe); the kernel waits for it.
-        // The slot's previous kernel has finished (st.done above), so its buffers are free.
-        hipStream_t const cs = rt::copyStream();
-        VKT_HIP_TRY(hipMemcpyAsync(dev, st.host, nFast * sizeof(BrickDesc), hipMemcpyHostToDevice, cs));
-        VKT_HIP_TRY(hipEventRecord(st.copied, cs));
-        VKT_HIP_TRY(hipStreamWaitEvent(s, st.copied, 0));
-        FastDiv const fdc = makeFastDiv(static_cast<uint32_t>(chunks));
         // group = the run of leading bricks with the same y/z box (one brick row of an
         // Array3D).  Any group size dividing the brick count maps blocks 1:1 onto (brick,
         // chunk); it only changes the order in which bricks are visited.
         size_t run = 1;
         while (run < nFast && fast[run].fy == fast[0].fy && fast[run].fz == fast[0].fz)
             ++run;
+        bool const useGrid = slow.empty() && guess.ok && gridOk.load() && nFast == static_cast<size_t>(numBricks);
+        if (useGrid)
+            gridDivisors(guess, fast);
+        BrickGrid grid = guess.g;
+        // the table goes up on the copy stream, so it overlaps the previous call's kernel
+        // (262 144 descriptors of 16^3 bricks are 25 MB, 0.59 ms of PCIe; their data pointers
+        // 2 MB); the kernel waits for it.  The slot's previous kernel has finished (st.done
+        // above), so its buffers are free.
+        hipStream_t const cs = rt::copyStream();
+        if (useGrid)
+        {
+            VKT_HIP_TRY(hipMemcpyAsync(st.devPtr, st.hostPtr, nFast * sizeof(uint8_t*), hipMemcpyHostToDevice, cs));
+            grid.dst = st.devPtr;
+        }
+        else
+            VKT_HIP_TRY(hipMemcpyAsync(dev, st.host, nFast * sizeof(BrickDesc), hipMemcpyHostToDevice, cs));
+        VKT_HIP_TRY(hipEventRecord(st.copied, cs));
+        VKT_HIP_TRY(hipStreamWaitEvent(s, st.copied, 0));
+        FastDiv const fdc = makeFastDiv(static_cast<uint32_t>(chunks));
         FastDiv const fdg = makeFastDiv(static_cast<uint32_t>(nFast % run == 0 ? run : 1));
         unsigned const g = static_cast<unsigned>(blocks);
         int32_t const alignedLds = static_cast<int32_t>(rt::knob(rt::Knob::DecomposeAlignedLds));
@@ -578,8 +747,12 @@ vktError vktHipBrickDecompose(vktHipVolumeView_t source, vktHipBrickRange_t cons
         int64_t const sw = rt::knob(rt::Knob::DecomposeStageWords);
         auto launch = [&](auto bpvC, auto swC) {
             constexpr int B = decltype(bpvC)::value, W = decltype(swC)::value;
-            hipLaunchKernelGGL((brickCopyKernel<B, W>), dim3(g), dim3(kBlock), 0, s, dev, fdc, fdg, source.data,
-                               source.dimX, source.dimY, source.dimZ, alignedLds);
+            if (useGrid)
+                hipLaunchKernelGGL((brickCopyKernel<B, W, true>), dim3(g), dim3(kBlock), 0, s, dev, grid, fdc, fdg,
+                                   source.data, source.dimX, source.dimY, source.dimZ, alignedLds);
+            else
+                hipLaunchKernelGGL((brickCopyKernel<B, W, false>), dim3(g), dim3(kBlock), 0, s, dev, grid, fdc, fdg,
+                                   source.data, source.dimX, source.dimY, source.dimZ, alignedLds);
         };
         auto bySw = [&](auto bpvC) {
             if (sw <= 5)

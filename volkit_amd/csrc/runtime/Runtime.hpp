@@ -91,6 +91,7 @@ namespace rt
         PointwiseF32Wide,              // 1: 4-byte general-path boxes use 16-B items (measured neutral; off)
         AggregatesCodes,               // bit 0 UInt8, bit 1 UInt16: ComputeAggregates from one pass of code counts
         ReduceU8Rows16,                // UInt8 code counts over range rows with 16-voxel items (codeCountsU8RowsKernel)
+        DecomposeGrid,                 // 0: uniform brick grids keep the per-brick descriptor table
         Count
     };
     int64_t knob(Knob k);
