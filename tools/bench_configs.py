@@ -614,7 +614,9 @@ def main():
         ms = timed(lambda: lib.vktHipHistogramRange(V, u0, u1, bins, 256, 0), R)
         report("reduce Histogram UInt16 800^3 sub-box of 1024^3 at x0=100, 256 bins", ms, 2 * 800 ** 3, 800 ** 3)
         agg0 = _lib.Aggregates_t()
+        lib.vktHipSetTuningKnob(b"aggregates.codes", 1)   # UInt16: the two float passes
         ms = timed(lambda: lib.vktHipAggregatesRange(V, u0, u1, C.byref(agg0)), R)
+        lib.vktHipSetTuningKnob(b"aggregates.codes", -1)
         report("reduce Aggregates UInt16 800^3 sub-box of 1024^3 at x0=100 (2 passes)", ms, 2 * 2 * 800 ** 3, 800 ** 3)
         for fmt, bpv, name in ((4, 1, "UInt8"), (7, 4, "Float32")):
             W = alloc((n,) * 3, fmt, seed=12 if fmt != 7 else None)
@@ -639,7 +641,9 @@ def main():
             ms = timed(lambda: lib.vktHipHistogramRange(Vc, o, last, bins, nb, 0), R)
             report(f"reduce Histogram 1024^3 UInt16 {nb} bins, constant volume", ms, 2 * n ** 3, n ** 3)
         agg = _lib.Aggregates_t()
+        lib.vktHipSetTuningKnob(b"aggregates.codes", 1)   # UInt16: the two float passes
         ms = timed(lambda: lib.vktHipAggregatesRange(V, o, last, C.byref(agg)), R)
+        lib.vktHipSetTuningKnob(b"aggregates.codes", -1)
         report("reduce Aggregates 1024^3 UInt16 (2 passes, incl. D2H of the result)", ms, 2 * 2 * n ** 3, n ** 3)
         free(V, Vc)
         lib.vktHipFree(bins)
