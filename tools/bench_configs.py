@@ -503,7 +503,11 @@ def main():
         V = vkt.StructuredVolume(n, n, n, vkt.DataFormat_UInt16)
         vkt.Synthesize(V, 77)
         ab = {}
-        for bs, halo in ((32, (1, 1, 1)), (64, (1, 1, 1)), (128, (0, 0, 0)), (256, (1, 1, 1))):
+        cases = ((16, (1, 1, 1)), (32, (1, 1, 1)), (64, (1, 1, 1)), (128, (0, 0, 0)), (256, (1, 1, 1)))
+        if os.environ.get("VKT_DECAB_SIZES"):   # e.g. "16,32"
+            keep = {int(x) for x in os.environ["VKT_DECAB_SIZES"].split(",")}
+            cases = tuple(c for c in cases if c[0] in keep)
+        for bs, halo in cases:
             arr = vkt.Array3D_StructuredVolume()
             b3, h3 = vkt.Vec3i(bs, bs, bs), vkt.Vec3i(*halo)
             vkt.BrickDecomposeResize(arr, V, b3, h3, h3)
@@ -691,6 +695,10 @@ def main():
             report(f"aggcodes Aggregates 1024^3 UInt16 [codes={k}, {passes} pass(es)]", ms, passes * 2 * n ** 3, n ** 3)
             ms = timed(lambda: lib.vktHipAggregatesRange(V, u0, u1, C.byref(agg)), R)
             report(f"aggcodes Aggregates UInt16 800^3 sub-box at x0=100 [codes={k}, {passes} pass(es)]", ms,
+                   passes * 2 * 800 ** 3, 800 ** 3)
+            a0, a1 = Vec3i_t(0, 100, 100), Vec3i_t(800, 900, 900)
+            ms = timed(lambda: lib.vktHipAggregatesRange(V, a0, a1, C.byref(agg)), R)
+            report(f"aggcodes Aggregates UInt16 800^3 sub-box x 0..800 [codes={k}, {passes} pass(es)]", ms,
                    passes * 2 * 800 ** 3, 800 ** 3)
         lib.vktHipSetTuningKnob(b"aggregates.codes", -1)
         free(V)
