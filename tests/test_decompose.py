@@ -30,6 +30,8 @@ LAYOUTS = [
     ((131, 9, 4), (64, 4, 4), (5, 0, 0), (7, 0, 0)),
     # bricks of many 16-KiB workgroup chunks, chunk boundaries inside rows
     ((150, 97, 61), (64, 48, 40), (1, 1, 1), (2, 1, 3)),
+    # halos wider than a brick: interior bricks clamped at the x ends (no uniform-grid descriptors)
+    ((70, 20, 10), (8, 8, 8), (10, 1, 0), (12, 0, 1)),
 ]
 
 

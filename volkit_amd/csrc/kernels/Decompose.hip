@@ -496,8 +496,10 @@ namespace hipk
         return q;
     }
 
-    // range i (its descriptor d) at its place in the inferred grid, a linear brick
-    bool gridMatches(GridGuess const& q, vktHipBrickRange_t const& r, BrickDesc const& d, size_t i)
+    // range i (its descriptor d) at its place in the inferred grid, a linear brick.  Interior
+    // bricks along x must not be clamped at the volume's x ends (a halo wider than a brick): their
+    // source words per row (fwpr) would differ from the class representative's.
+    bool gridMatches(GridGuess const& q, vktHipBrickRange_t const& r, BrickDesc const& d, size_t i, int32_t sdx)
     {
         BrickGrid const& g = q.g;
         int32_t const ix = static_cast<int32_t>(i % static_cast<size_t>(g.nbx));
@@ -505,6 +507,8 @@ namespace hipk
         int32_t const iz = static_cast<int32_t>(i / q.pz);
         auto cls = [](int32_t k, int32_t nb) { return k == nb - 1 ? 2 : (k == 0 ? 0 : 1); };
         int32_t const nx = g.nx[cls(ix, g.nbx)], ny = g.ny[cls(iy, g.nby)], nz = g.nz[cls(iz, g.nbz)];
+        if (cls(ix, g.nbx) == 1 && (r.first.x < 0 || r.first.x + nx > sdx))
+            return false;
         return d.linear && r.first.x == g.fx0 + ix * g.bx && r.first.y == g.fy0 + iy * g.by &&
                r.first.z == g.fz0 + iz * g.bz && r.last.x - r.first.x == nx && r.last.y - r.first.y == ny &&
                r.last.z - r.first.z == nz;
@@ -683,7 +687,7 @@ vktError vktHipBrickDecompose(vktHipVolumeView_t source, vktHipBrickRange_t cons
             myMax = d.nitems > myMax ? d.nitems : myMax;
             if (myGrid)
             {
-                myGrid = gridMatches(guess, br, d, ii);
+                myGrid = gridMatches(guess, br, d, ii, source.dimX);
                 ptrs[i] = d.dst;
             }
         }
