@@ -213,7 +213,8 @@ def main():
             free(A, B, D)
     if want("u8ab"):
         # in-process A/B of the UInt8 16-voxel pair grid (knob pointwise.u8_pairs: 0 off, 1
-        # default rule, 2 forced), alternating on the same allocations
+        # default rule, 2 forced, 3 the general path's wide items), alternating on the same
+        # allocations (VKT_U8AB_GEN=1: default vs general path only)
         m = 1024
         A, B, D = alloc((m,) * 3, 4, seed=1), alloc((m,) * 3, 4, seed=2), alloc((m,) * 3, 4)
         ab = {}
@@ -221,7 +222,8 @@ def main():
                  ("x 0..800", Vec3i_t(0, 100, 100), Vec3i_t(800, 900, 900)),
                  ("x 0..1024 (planes)", Vec3i_t(0, 100, 100), Vec3i_t(1024, 900, 900)))
         for rnd in range(3):
-            for kv in ((0, -1), (1, 0), (1, 1), (1, 2), (2, -1)):   # (u8_pairs, merge_sectors)
+            for kv in ((1, -1), (3, -1), (3, 2)) if os.environ.get("VKT_U8AB_GEN") else \
+                    ((0, -1), (1, 0), (1, 1), (1, 2), (2, -1)):   # (u8_pairs, merge_sectors)
                 lib.vktHipSetTuningKnob(b"pointwise.u8_pairs", kv[0])
                 lib.vktHipSetTuningKnob(b"pointwise.merge_sectors", kv[1])
                 for lab, f0, f1 in boxes:

@@ -321,6 +321,10 @@ namespace hipk
         }
         gg.divCpr = makeFastDiv(static_cast<uint32_t>(gg.cpr));
         gg.divVny = makeFastDiv(static_cast<uint32_t>(vny));
+        // (knob pointwise.u8_pairs = 3, A/B only: UInt8 multi-row boxes on the general path's wide
+        // items instead of the aligned path)
+        if (vec && bpv == 1 && vny * vnz > 1 && gg.wide && rt::knob(rt::Knob::PointwiseU8Pairs) == 3)
+            vec = false;
         p.vec = vec;
         p.gen = gen && !vec && rt::knob(rt::Knob::PointwiseGeneral) != 0;
         p.uniform = uniform;
