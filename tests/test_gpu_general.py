@@ -615,3 +615,26 @@ def test_random_geometry_fuzz(lib, o, seed):
     finally:
         for kname, _ in knobs:
             lib.vktHipSetTuningKnob(kname, -1)
+
+
+@pytest.mark.parametrize("k", [1, 2, 3])
+def test_uint8_long_edge_free_rows_on_the_general_path(lib, o, k):
+    """UInt8 copies over multi-row boxes of long rows without row edges (whole-x planes of a y
+    sub-range: rows merge to >= 4096 voxels per plane) take the general path's wide items by
+    default (knob pointwise.u8_pairs = 1), the pair grid with 2, the general path for every
+    UInt8 multi-row box with 3: same bytes as the oracle, including shorter rows and row edges."""
+    from volkit_amd._lib import lib as L
+    rng = np.random.default_rng(91 + k)
+    dims = (6, 40, 256)
+    a = rand_codes(rng, 4, dims)
+    dinit = rand_codes(rng, 4, dims)
+    L.vktHipSetTuningKnob(b"pointwise.u8_pairs", k)
+    try:
+        for first, last in (((0, 3, 1), (256, 37, 5)), ((0, 0, 0), (256, 40, 6)), ((0, 5, 0), (256, 6, 6)),
+                            ((16, 2, 1), (240, 39, 5)), ((3, 2, 1), (250, 39, 5))):
+            copy_case(lib, o, 4, 4, (0.0, 1.0), (0.0, 1.0), a, dinit, first, last, (0, 0, 0), 0, 0,
+                      f"u8 copy k={k} {first}->{last}")
+            copy_case(lib, o, 4, 4, (0.0, 1.0), (0.0, 1.0), a, dinit, first, last, (0, 0, 0), 0, 64,
+                      f"u8 copy k={k} {first}->{last} dst+64")
+    finally:
+        L.vktHipSetTuningKnob(b"pointwise.u8_pairs", -1)

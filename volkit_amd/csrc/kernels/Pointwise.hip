@@ -321,10 +321,17 @@ namespace hipk
         }
         gg.divCpr = makeFastDiv(static_cast<uint32_t>(gg.cpr));
         gg.divVny = makeFastDiv(static_cast<uint32_t>(vny));
-        // (knob pointwise.u8_pairs = 3, A/B only: UInt8 multi-row boxes on the general path's wide
-        // items instead of the aligned path)
-        if (vec && bpv == 1 && vny * vnz > 1 && gg.wide && rt::knob(rt::Knob::PointwiseU8Pairs) == 3)
-            vec = false;
+        // UInt8 copies / fills over multi-row boxes of long rows without row edges (e.g. whole-x
+        // planes of a y sub-range) run faster on the general path's wide items than on the pair
+        // grid: 800 planes of 1024 x 800 voxels 0.254 -> 0.226 ms, while 800-voxel rows lost 3 %
+        // and rows with edges tied (profiles/r03/u8_general_ab.jsonl; the 3-stream ops lost on the
+        // general path everywhere).  Knob pointwise.u8_pairs = 3 sends every UInt8 multi-row box there (A/B).
+        {
+            int64_t const k = rt::knob(rt::Knob::PointwiseU8Pairs);
+            bool const edgeFreeLong = ns <= 1 && (ops[0]->base & 15) == 0 && vnx % 16 == 0 && vnx >= 4096;
+            if (vec && bpv == 1 && vny * vnz > 1 && gg.wide && (k == 3 || (k == 1 && edgeFreeLong)))
+                vec = false;
+        }
         p.vec = vec;
         p.gen = gen && !vec && rt::knob(rt::Knob::PointwiseGeneral) != 0;
         p.uniform = uniform;
