@@ -430,6 +430,40 @@ namespace hipk
         return m;
     }
 
+    // spanVoxel and itemMask of one item from ONE row division (the two computed apart divided the
+    // item index twice per item on the non-CONTIG walks)
+    template <bool CONTIG>
+    __device__ __forceinline__ uint64_t spanVoxelMask(FastHistArgs const& h, uint64_t item, uint32_t& mask)
+    {
+        if constexpr (CONTIG)
+        {
+            mask = 0xFFu;
+            return item * 8;
+        }
+        else
+        {
+            uint32_t const i = static_cast<uint32_t>(item);
+            uint32_t const r = fdiv(i, h.fdIpr);
+            uint32_t const xi = i - r * h.fdIpr.d;
+            uint32_t const zr = fdiv(r, h.fdNy);
+            uint32_t const yr = r - zr * h.fdNy.d;
+            int32_t const x0 = h.px0 + 8 * static_cast<int32_t>(xi);
+            uint32_t m = 0xFFu;
+            if (h.padded && !(x0 >= h.rx0 && x0 + 8 <= h.rx1))
+            {
+                m = 0;
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    m |= (x0 + j >= h.rx0 && x0 + j < h.rx1) ? 1u << j : 0u;
+            }
+            mask = m;
+            return ((static_cast<uint64_t>(h.fz + zr) * static_cast<uint64_t>(h.dimY) + (h.fy + yr)) *
+                        static_cast<uint64_t>(h.dimX) +
+                    static_cast<uint64_t>(h.px0)) +
+                   8ull * xi;
+        }
+    }
+
     // SHIFT: the bin of every code is code >> binShift, so one shift replaces the decode, the
     // range test and the conversion (UInt16) or the LDS table read (UInt8).  UInt16: taken
     // for the unit mapping (+0, 1) and numBins = 2^k, k <= 16, where decode(c) = c * 2^-16
@@ -487,7 +521,6 @@ namespace hipk
         // this lane's copy of counter row 0; row b is at + (b << rowShift) (one v_lshl_add)
         char* const cLane = reinterpret_cast<char*>(cnt) + (TILED ? 0u : (lane & ((1u << h.rShift) - 1u)) << 2);
 
-        auto voxelOf = [&](uint64_t item) { return spanVoxel<CONTIG>(h, item); };
         uint32_t runBin = ~0u, runCount = 0u;   // TILED: the wave's run of uniform voxels
         auto add = [&](uint32_t b) {
             if constexpr (TILED)
@@ -660,14 +693,14 @@ namespace hipk
         };
         // P16, one wave-step of U items: every item's returning adds are in flight before the
         // (rare) threshold tests, which wait for the returns only once per step
-        auto countStepP16 = [&](uint32_t const (&c)[U][8], uint64_t item0) {
+        auto countStepP16 = [&](uint32_t const (&c)[U][8], uint32_t const (&msk)[U]) {
             uint32_t b[U][8], old[U][8];
             bool uni[U];
             uint32_t any = 0;
 #pragma unroll
             for (int k = 0; k < U; ++k)
             {
-                bins8(c[k], itemMask<CONTIG>(h, item0 + k * 64), b[k]);
+                bins8(c[k], msk[k], b[k]);
                 uni[k] = takeUniform(b[k]);
                 if (!uni[k])
                     any |= p16Adds(b[k], old[k]);
@@ -703,26 +736,30 @@ namespace hipk
                     c[k][4] = y.x; c[k][5] = y.y; c[k][6] = y.z; c[k][7] = y.w;
                 }
             }
-            else
+            uint32_t msk[U];
+#pragma unroll
+            for (int k = 0; k < U; ++k)
+                msk[k] = 0xFFu;
+            if (!halves)
             {
 #pragma unroll
                 for (int k = 0; k < U; ++k)
-                    load8<BPV, true>(h.data, voxelOf(st * (64 * U) + k * 64 + lane), c[k]);
+                    load8<BPV, true>(h.data, spanVoxelMask<CONTIG>(h, st * (64 * U) + k * 64 + lane, msk[k]), c[k]);
             }
             if (P16 && h.p16Step)
-                countStepP16(c, st * (64 * U) + lane);
+                countStepP16(c, msk);
             else
             {
 #pragma unroll
                 for (int k = 0; k < U; ++k)
-                    count8(c[k], itemMask<CONTIG>(h, st * (64 * U) + k * 64 + lane));
+                    count8(c[k], msk[k]);
             }
         }
         for (uint64_t it = steps * (64 * U) + wave * 64 + lane; it < h.items; it += waves * 64)
         {
-            uint32_t c[8];
-            load8<BPV, true>(h.data, voxelOf(it), c);
-            count8(c, itemMask<CONTIG>(h, it));
+            uint32_t c[8], m;
+            load8<BPV, true>(h.data, spanVoxelMask<CONTIG>(h, it, m), c);
+            count8(c, m);
         }
         if constexpr (TILED)
             flushRun();   // (every lane reconverged; lane 0 holds the run)
@@ -804,8 +841,8 @@ namespace hipk
         // hb (Float32 spans, `halves`): c holds the halves at 4l and 256 + 4l of the 64-item block
         // starting at item hb -- still in increasing index order per lane, which the first-
         // occurrence tie-break of argmin / argmax relies on
-        auto visit8 = [&](uint32_t const (&c)[8], uint64_t item, uint64_t hb = ~0ull) {
-            uint32_t const m = itemMask<CONTIG>(h, item);
+        auto visit8 = [&](uint32_t const (&c)[8], uint64_t item, uint64_t hb = ~0ull, uint32_t mIn = 0x100u) {
+            uint32_t const m = mIn != 0x100u ? mIn : itemMask<CONTIG>(h, item);
             auto gIndex = [&](int j) -> uint64_t {
                 if (CONTIG && hb != ~0ull)
                     return h.giBase + hb * 8 + 4 * lane + (j < 4 ? static_cast<uint64_t>(j) : 252ull + j);
@@ -922,19 +959,20 @@ namespace hipk
             }
             else
             {
+                uint32_t msk[U];
 #pragma unroll
                 for (int k = 0; k < U; ++k)
-                    load8<BPV, true>(h.data, spanVoxel<CONTIG>(h, st * (64 * U) + k * 64 + lane), c[k]);
+                    load8<BPV, true>(h.data, spanVoxelMask<CONTIG>(h, st * (64 * U) + k * 64 + lane, msk[k]), c[k]);
 #pragma unroll
                 for (int k = 0; k < U; ++k)
-                    visit8(c[k], st * (64 * U) + k * 64 + lane);
+                    visit8(c[k], st * (64 * U) + k * 64 + lane, ~0ull, msk[k]);
             }
         }
         for (uint64_t it = steps * (64 * U) + wave * 64 + lane; it < h.items; it += waves * 64)
         {
-            uint32_t c[8];
-            load8<BPV, true>(h.data, spanVoxel<CONTIG>(h, it), c);
-            visit8(c, it);
+            uint32_t c[8], m;
+            load8<BPV, true>(h.data, spanVoxelMask<CONTIG>(h, it, m), c);
+            visit8(c, it, ~0ull, m);
         }
         if constexpr (CODES)
         {
