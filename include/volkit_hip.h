@@ -112,7 +112,8 @@ VKTAPI vktError vktHipKernelScopeEnd(vktHipKernelScope scope);
  * instead of the two float passes), "reduce.u8_rows16" (1; UInt8 code counts over range rows on 16-voxel
  * items, row-end bytes subtracted inside the main loop; 2 subtracts them in a row walk after it;
  * 0 keeps the 8-voxel item walk), "decompose.grid" (1; 0 makes uniform brick grids load a
- * per-brick descriptor instead of deriving it from the brick index).  For tests and in-process A/B measurements; unknown names return
+ * per-brick descriptor instead of deriving it from the brick index), "memory.pool" (1; 0 gives every
+ * device buffer of <= 4 MiB its own hipMalloc instead of a 256-B class of a 64-MiB pooled chunk).  For tests and in-process A/B measurements; unknown names return
  * vktInvalidValue.
  *
  * Writes outside a range box: FillRange / CopyRange / convert and device-functor TransformRange

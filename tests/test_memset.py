@@ -114,3 +114,50 @@ def test_managed_buffer_fill(fx, psize):
         out = np.zeros(count * psize, np.uint8)
         assert fx.vktt_managed_fill(psize, count, pattern.ctypes.data, out.ctypes.data) == 0
         assert np.array_equal(out, np.resize(pattern, count * psize)), (psize, count)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pool", [1, 0])
+def test_small_device_buffers_pooled_and_reused(pool):
+    """Device buffers of <= 4 MiB come from pooled 64-MiB chunks in 256-B classes (knob
+    memory.pool; 0 = one hipMalloc each).  Many small volumes of two sizes, filled with distinct
+    values, half of them freed while kernels on the others are queued, then new ones allocated
+    (reusing the freed blocks after the pool's one device synchronisation) and filled: every
+    volume reads back its own value; a >4 MiB volume is unaffected."""
+    import volkit_amd.volkit as vkt
+    from volkit_amd._lib import lib as L
+
+    def policy(dev):
+        ep = vkt.GetThreadExecutionPolicy()
+        ep.device = dev
+        vkt.SetThreadExecutionPolicy(ep)
+
+    L.vktHipSetTuningKnob(b"memory.pool", pool)
+    try:
+        policy(vkt.ExecutionPolicy.Device_GPU)
+        vols = []
+        for i in range(600):
+            d = (18, 18, 18) if i % 2 else (16, 20, 9)
+            v = vkt.StructuredVolume(*d, vkt.DataFormat_UInt16)
+            assert vkt.Fill(v, (i % 1000) / 1000.0) == vkt.NoError
+            vols.append((i, v))
+        big = vkt.StructuredVolume(256, 128, 80, vkt.DataFormat_UInt16)   # 5 MiB: own hipMalloc
+        assert vkt.Fill(big, 0.25) == vkt.NoError
+        for i, v in vols[::2]:
+            assert vkt.Fill(v, 0.999) == vkt.NoError   # queued work on blocks about to be freed
+        vols = vols[1::2]
+        for i in range(600, 900):
+            d = (18, 18, 18) if i % 2 else (16, 20, 9)
+            v = vkt.StructuredVolume(*d, vkt.DataFormat_UInt16)
+            assert vkt.Fill(v, (i % 1000) / 1000.0) == vkt.NoError
+            vols.append((i, v))
+        policy(vkt.ExecutionPolicy.Device_CPU)
+        for i, v in vols:
+            want = int(np.frombuffer(vkt.MapVoxel((i % 1000) / 1000.0, vkt.DataFormat_UInt16), np.uint16)[0])
+            got = v.to_numpy()
+            assert (got == want).all(), (i, np.unique(got)[:4], want)
+        want = int(np.frombuffer(vkt.MapVoxel(0.25, vkt.DataFormat_UInt16), np.uint16)[0])
+        assert (big.to_numpy() == want).all()
+    finally:
+        policy(vkt.ExecutionPolicy.Device_CPU)
+        L.vktHipSetTuningKnob(b"memory.pool", -1)

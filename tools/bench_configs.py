@@ -565,6 +565,51 @@ def main():
         del V
         ep.device = vkt.ExecutionPolicy.Device_CPU
         vkt.SetThreadExecutionPolicy(ep)
+    if want("memresize"):
+        # BrickDecomposeResize (one StructuredVolume per brick, allocated on the device) with the
+        # small-buffer pool on / off (knob memory.pool): host wall time of the resize, and of a
+        # second resize over the same array (the first one's bricks freed, their blocks reused)
+        import time
+        import volkit_amd.volkit as vkt
+        ep = vkt.GetThreadExecutionPolicy()
+        ep.device = vkt.ExecutionPolicy.Device_GPU
+        vkt.SetThreadExecutionPolicy(ep)
+        n = 1024
+        V = vkt.StructuredVolume(n, n, n, vkt.DataFormat_UInt16)
+        vkt.Synthesize(V, 77)
+        arrs = {}
+        for bs in (32, 16):
+            for k in (1, 0):
+                lib.vktHipSetTuningKnob(b"memory.pool", k)
+                arr = vkt.Array3D_StructuredVolume()
+                b3, h3 = vkt.Vec3i(bs, bs, bs), vkt.Vec3i(1, 1, 1)
+                t0 = time.perf_counter()
+                vkt.BrickDecomposeResize(arr, V, b3, h3, h3)
+                torch.cuda.synchronize()
+                t1 = time.perf_counter()
+                vkt.BrickDecomposeResize(arr, V, b3, h3, h3)
+                torch.cuda.synchronize()
+                t2 = time.perf_counter()
+                nb = arr.dims().x * arr.dims().y * arr.dims().z
+                print(json.dumps({"case": f"memresize BrickDecomposeResize 1024^3 -> {bs}^3 bricks halo 1 pool={k}",
+                                  "bricks": nb, "first_ms": round((t1 - t0) * 1e3, 2),
+                                  "again_ms": round((t2 - t1) * 1e3, 2)}), flush=True)
+                arrs[(bs, k)] = arr
+            # the decomposition into bricks from the pool vs from one hipMalloc each, alternating
+            b3, h3 = vkt.Vec3i(bs, bs, bs), vkt.Vec3i(1, 1, 1)
+            ts = {}
+            for rnd in range(3):
+                for k in (1, 0):
+                    ts.setdefault(k, []).append(pipelined(lambda: vkt.BrickDecompose(arrs[(bs, k)], V, b3, h3, h3), R))
+            for k, v in ts.items():
+                v.sort()
+                print(json.dumps({"case": f"memresize BrickDecompose into {bs}^3 bricks halo 1 pool={k} (back-to-back, "
+                                  f"median of 3 rounds, spread {v[0]:.4f}-{v[-1]:.4f})", "ms": round(v[1], 4)}), flush=True)
+            arrs.clear()
+        lib.vktHipSetTuningKnob(b"memory.pool", -1)
+        del V
+        ep.device = vkt.ExecutionPolicy.Device_CPU
+        vkt.SetThreadExecutionPolicy(ep)
     if want("decpmc"):
         # one case for PMC passes (VKT_KNOBS picks the variant): 32^3 bricks + halo 1
         import volkit_amd.volkit as vkt

@@ -208,6 +208,7 @@ namespace rt
             {"aggregates.codes", 3},
             {"reduce.u8_rows16", 1},
             {"decompose.grid", 1},
+            {"memory.pool", 1},
         };
         static_assert(sizeof(kKnobs) / sizeof(kKnobs[0]) == static_cast<size_t>(Knob::Count), "knob table");
         std::atomic<int64_t> gKnobs[static_cast<int>(Knob::Count)] = {{kKnobs[0].def}, {kKnobs[1].def},
@@ -218,7 +219,8 @@ namespace rt
                                                                   {kKnobs[10].def}, {kKnobs[11].def},
                                                                   {kKnobs[12].def}, {kKnobs[13].def},
                                                                   {kKnobs[14].def}, {kKnobs[15].def},
-                                                                  {kKnobs[16].def}, {kKnobs[17].def}};
+                                                                  {kKnobs[16].def}, {kKnobs[17].def},
+                                                                  {kKnobs[18].def}};
     } // namespace
 
     int64_t knob(Knob k) { return gKnobs[static_cast<int>(k)].load(std::memory_order_relaxed); }

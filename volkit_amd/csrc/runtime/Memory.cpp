@@ -20,7 +20,9 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <unordered_map>
 #include <unordered_set>
+#include <vector>
 
 namespace vkt
 {
@@ -42,6 +44,97 @@ namespace
     {
         static auto* s = new std::unordered_set<void*>;
         return *s;
+    }
+
+    // Small device allocations (<= kPoolMax bytes: bricks, lookup tables, small volumes) come from
+    // 64-MiB hipMalloc chunks in 256-B size classes instead of one hipMalloc each: a
+    // BrickDecomposeResize of a 1024^3 volume into 16^3 bricks makes 262 144 allocations.  Freed
+    // blocks wait on a pending list; the first allocation that would reuse one synchronises the
+    // device once for the whole batch (the guarantee hipFree gave: no kernel or copy still uses
+    // the block), then serves them.  Chunks are kept for the process (like a caching allocator);
+    // knob memory.pool = 0 allocates every buffer with hipMalloc.
+    constexpr std::size_t kPoolMax = 4u << 20;
+    constexpr std::size_t kPoolChunk = 64u << 20;
+    constexpr std::size_t kPoolAlign = 256;
+
+    struct DevicePool
+    {
+        std::unordered_map<std::size_t, std::vector<void*>> freeBlocks;   // by class
+        std::unordered_map<std::size_t, std::vector<void*>> pending;      // by class: freed, not yet synchronised
+        char* bump = nullptr;
+        std::size_t left = 0;
+    };
+
+    struct Pools
+    {
+        std::mutex m;
+        std::unordered_map<int, DevicePool> byDevice;
+        std::unordered_map<void*, std::pair<int, std::size_t>> owner;   // block -> (device, class)
+    };
+
+    Pools& pools()
+    {
+        static auto* p = new Pools;   // (never destroyed: frees may run during static destruction)
+        return *p;
+    }
+
+    void* poolAllocate(std::size_t bytes)
+    {
+        std::size_t const cls = (bytes + kPoolAlign - 1) / kPoolAlign * kPoolAlign;
+        int const dev = rt::device();
+        Pools& P = pools();
+        std::lock_guard<std::mutex> lock(P.m);
+        DevicePool& d = P.byDevice[dev];
+        auto reuse = [&]() -> void* {
+            auto it = d.freeBlocks.find(cls);
+            if (it == d.freeBlocks.end() || it->second.empty())
+                return nullptr;
+            void* b = it->second.back();
+            it->second.pop_back();
+            return b;
+        };
+        void* b = reuse();
+        auto mine = d.pending.find(cls);
+        if (!b && mine != d.pending.end() && !mine->second.empty() &&
+            rt::check(hipDeviceSynchronize(), "hipDeviceSynchronize(pool)") == vktNoError)
+        {
+            for (auto& q : d.pending)   // every class: the one synchronisation covers them all
+            {
+                auto& f = d.freeBlocks[q.first];
+                f.insert(f.end(), q.second.begin(), q.second.end());
+                q.second.clear();
+            }
+            b = reuse();
+        }
+        if (!b)
+        {
+            if (d.left < cls)
+            {
+                void* c = nullptr;
+                if (rt::check(hipMalloc(&c, kPoolChunk), "hipMalloc(pool chunk)") != vktNoError)
+                    return nullptr;
+                d.bump = static_cast<char*>(c);
+                d.left = kPoolChunk;
+            }
+            b = d.bump;
+            d.bump += cls;
+            d.left -= cls;
+        }
+        P.owner[b] = {dev, cls};
+        return b;
+    }
+
+    // true when p is a pool block (then it is queued for reuse)
+    bool poolFree(void* p)
+    {
+        Pools& P = pools();
+        std::lock_guard<std::mutex> lock(P.m);
+        auto it = P.owner.find(p);
+        if (it == P.owner.end())
+            return false;
+        P.byDevice[it->second.first].pending[it->second.second].push_back(p);
+        P.owner.erase(it);
+        return true;
     }
 
 } // namespace
@@ -88,6 +181,8 @@ namespace detail
         if (onGpu(owner))
         {
             (void)rt::device();   // bind the context's device before allocating
+            if (bytes <= kPoolMax && rt::knob(rt::Knob::MemoryPool) != 0)
+                return poolAllocate(bytes);
             void* p = nullptr;
             if (rt::check(hipMalloc(&p, bytes), "hipMalloc") != vktNoError)
                 return nullptr;
@@ -115,7 +210,8 @@ namespace detail
             return;
         if (onGpu(owner))
         {
-            (void)rt::check(hipFree(data), "hipFree");
+            if (!poolFree(data))
+                (void)rt::check(hipFree(data), "hipFree");
             return;
         }
         {
@@ -234,6 +330,8 @@ vktError vktHipAllocate(void** ptr, size_t size)
 vktError vktHipFree(void* ptr)
 {
     if (ptr == nullptr)
+        return vktNoError;
+    if (vkt::poolFree(ptr))
         return vktNoError;
     return vkt::rt::check(hipFree(ptr), "hipFree");
 }

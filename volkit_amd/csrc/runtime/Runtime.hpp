@@ -92,6 +92,7 @@ namespace rt
         AggregatesCodes,               // bit 0 UInt8, bit 1 UInt16: ComputeAggregates from one pass of code counts
         ReduceU8Rows16,                // UInt8 code counts over range rows with 16-voxel items (codeCountsU8RowsKernel)
         DecomposeGrid,                 // 0: uniform brick grids keep the per-brick descriptor table
+        MemoryPool,                    // 0: every device buffer from its own hipMalloc (no small-block pool)
         Count
     };
     int64_t knob(Knob k);
