@@ -127,7 +127,9 @@ VKTAPI vktError vktHipSetTuningKnob(const char* name, int64_t value);
 VKTAPI vktError vktHipReportError(const char* message);
 
 /* ---- memory: replaces Allocate_cuda/Free_cuda/MemsetRange_cuda
- *      (reference src/vkt/Memory_cuda.hpp:16-31) and the cudaMemcpy of src/vkt/Memory.cpp:40-75 */
+ *      (reference src/vkt/Memory_cuda.hpp:16-31) and the cudaMemcpy of src/vkt/Memory.cpp:40-75
+ * Buffers of <= 4 MiB are blocks of pooled chunks (knob "memory.pool"): release every pointer
+ * from vktHipAllocate / vktAllocate with vktHipFree / vktFree, never with hipFree. */
 VKTAPI vktError vktHipAllocate(void** ptr, size_t size);
 VKTAPI vktError vktHipFree(void* ptr);
 VKTAPI vktError vktHipMemcpy(void* dst, void const* src, size_t size, vktCopyKind ck);
