@@ -113,7 +113,8 @@ VKTAPI vktError vktHipKernelScopeEnd(vktHipKernelScope scope);
  * items, row-end bytes subtracted inside the main loop; 2 subtracts them in a row walk after it;
  * 0 keeps the 8-voxel item walk), "decompose.grid" (1; 0 makes uniform brick grids load a
  * per-brick descriptor instead of deriving it from the brick index), "memory.pool" (1; 0 gives every
- * device buffer of <= 4 MiB its own hipMalloc instead of a 256-B class of a 64-MiB pooled chunk).  For tests and in-process A/B measurements; unknown names return
+ * device buffer of <= 4 MiB its own hipMalloc instead of a 256-B class of a 64-MiB pooled chunk), "memory.arena" (1; 0 gives every larger buffer its
+ * own hipMalloc instead of a 2-MiB aligned block of a >= 16-GiB arena chunk).  For tests and in-process A/B measurements; unknown names return
  * vktInvalidValue.
  *
  * Writes outside a range box: FillRange / CopyRange / convert and device-functor TransformRange
@@ -128,7 +129,7 @@ VKTAPI vktError vktHipReportError(const char* message);
 
 /* ---- memory: replaces Allocate_cuda/Free_cuda/MemsetRange_cuda
  *      (reference src/vkt/Memory_cuda.hpp:16-31) and the cudaMemcpy of src/vkt/Memory.cpp:40-75
- * Buffers of <= 4 MiB are blocks of pooled chunks (knob "memory.pool"): release every pointer
+ * Device buffers are blocks of pooled / arena chunks (knobs "memory.pool", "memory.arena"): release every pointer
  * from vktHipAllocate / vktAllocate with vktHipFree / vktFree, never with hipFree. */
 VKTAPI vktError vktHipAllocate(void** ptr, size_t size);
 VKTAPI vktError vktHipFree(void* ptr);

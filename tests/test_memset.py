@@ -161,3 +161,45 @@ def test_small_device_buffers_pooled_and_reused(pool):
     finally:
         policy(vkt.ExecutionPolicy.Device_CPU)
         L.vktHipSetTuningKnob(b"memory.pool", -1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("arena", [1, 0])
+def test_large_device_buffers_from_arena_chunks(arena):
+    """Device buffers above 4 MiB are 2-MiB aligned blocks carved first-fit from >= 16-GiB arena
+    chunks (knob memory.arena; 0 = one hipMalloc each).  Volumes of three sizes, filled with
+    distinct values; every other one freed while work on it is queued, then new ones allocated
+    (the freed blocks return after the arena's one device synchronisation, holes coalesce) and
+    filled: every live volume reads back its own value."""
+    import volkit_amd.volkit as vkt
+    from volkit_amd._lib import lib as L
+
+    def policy(dev):
+        ep = vkt.GetThreadExecutionPolicy()
+        ep.device = dev
+        vkt.SetThreadExecutionPolicy(ep)
+
+    dims = [(256, 128, 80), (512, 512, 33), (300, 301, 97)]     # 5, 17, 17.5 MB of UInt16
+    L.vktHipSetTuningKnob(b"memory.arena", arena)
+    try:
+        policy(vkt.ExecutionPolicy.Device_GPU)
+        vols = []
+        for i in range(24):
+            v = vkt.StructuredVolume(*dims[i % 3], vkt.DataFormat_UInt16)
+            assert vkt.Fill(v, (i + 1) / 100.0) == vkt.NoError
+            vols.append((i, v))
+        for i, v in vols[::2]:
+            assert vkt.Fill(v, 0.999) == vkt.NoError
+        vols = vols[1::2]
+        for i in range(24, 40):
+            v = vkt.StructuredVolume(*dims[(i * 7) % 3], vkt.DataFormat_UInt16)
+            assert vkt.Fill(v, (i + 1) / 100.0) == vkt.NoError
+            vols.append((i, v))
+        policy(vkt.ExecutionPolicy.Device_CPU)
+        for i, v in vols:
+            want = int(np.frombuffer(vkt.MapVoxel((i + 1) / 100.0, vkt.DataFormat_UInt16), np.uint16)[0])
+            got = v.to_numpy()
+            assert (got == want).all(), (i, np.unique(got)[:4], want)
+    finally:
+        policy(vkt.ExecutionPolicy.Device_CPU)
+        L.vktHipSetTuningKnob(b"memory.arena", -1)

@@ -25,6 +25,14 @@ o, last = Vec3i_t(0, 0, 0), Vec3i_t(n, n, n)
 
 
 def alloc(mode):
+    if mode in ("library", "library0"):   # vktHipAllocate (arena on / off: knob memory.arena)
+        lib.vktHipSetTuningKnob(b"memory.arena", 1 if mode == "library" else 0)
+        ptrs = []
+        for _ in range(3):
+            p = C.c_void_p()
+            assert lib.vktHipAllocate(C.byref(p), nb) == 0
+            ptrs.append(p.value)
+        return ptrs, [("lib", q) for q in ptrs]
     if mode == "block":
         p = C.c_void_p()
         assert hip.hipMalloc(C.byref(p), 3 * nb + 4096) == 0
@@ -62,5 +70,8 @@ for it in range(int(os.environ.get("PROBE_ITERS", "5"))):
         print(it, mode, round(ms, 4), flush=True)
         torch.cuda.synchronize()
         for p in frees:
-            hip.hipFree(C.c_void_p(p))
+            if isinstance(p, tuple):
+                lib.vktHipFree(C.c_void_p(p[1]))
+            else:
+                hip.hipFree(C.c_void_p(p))
 print({k: sorted(v) for k, v in res.items()})

@@ -209,6 +209,7 @@ namespace rt
             {"reduce.u8_rows16", 1},
             {"decompose.grid", 1},
             {"memory.pool", 1},
+            {"memory.arena", 1},
         };
         static_assert(sizeof(kKnobs) / sizeof(kKnobs[0]) == static_cast<size_t>(Knob::Count), "knob table");
         std::atomic<int64_t> gKnobs[static_cast<int>(Knob::Count)] = {{kKnobs[0].def}, {kKnobs[1].def},
@@ -220,7 +221,7 @@ namespace rt
                                                                   {kKnobs[12].def}, {kKnobs[13].def},
                                                                   {kKnobs[14].def}, {kKnobs[15].def},
                                                                   {kKnobs[16].def}, {kKnobs[17].def},
-                                                                  {kKnobs[18].def}};
+                                                                  {kKnobs[18].def}, {kKnobs[19].def}};
     } // namespace
 
     int64_t knob(Knob k) { return gKnobs[static_cast<int>(k)].load(std::memory_order_relaxed); }

@@ -93,6 +93,7 @@ namespace rt
         ReduceU8Rows16,                // UInt8 code counts over range rows with 16-voxel items (codeCountsU8RowsKernel)
         DecomposeGrid,                 // 0: uniform brick grids keep the per-brick descriptor table
         MemoryPool,                    // 0: every device buffer from its own hipMalloc (no small-block pool)
+        MemoryArena,                   // 0: buffers > 4 MiB from their own hipMalloc (no arena chunks)
         Count
     };
     int64_t knob(Knob k);
