@@ -25,14 +25,18 @@ them is `value`):
                       1024^3 -> 2048^3 Resample + SumRange 2048^3 UInt16 Z-slab partitioned over
                       the N GPUs launched (at N=1 the whole 2048^3 on one GPU, ~50 GiB of
                       volumes): the denominator and numerator of BASELINE.md §4's speedup;
+  * migrate        -- ManagedBuffer::migrate() host<->HBM GB/s of one 2 GiB UInt16 volume, pageable
+                      and pinned host memory (N=1; SURVEY §8(a) A2, reported apart from the roofline);
   * copy_peak      -- the library's own Copy 1024^3 UInt16, the achievable streaming rate;
   * cpu_baseline   -- the oracle port (1 thread) on the full 1024^3 pipeline and on 512^3.
 """
 import argparse
 import ctypes as C
+import datetime
 import json
 import os
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -58,12 +62,18 @@ def parse():
     p.add_argument("--config4-edge", type=int, default=2048,
                    help="dst edge of the fixed global config-4 volume (strong scaling; source = edge/2)")
     p.add_argument("--no-config4", action="store_true", help="skip the strong-scaling config-4 measurement")
+    p.add_argument("--no-migrate", action="store_true", help="skip the host<->HBM migrate() measurement (N=1 only)")
     p.add_argument("--layout-gpus", type=int, default=0,
                    help="single process: run rank 0's slab of the M-GPU global layout")
     p.add_argument("--dist-backend", default="nccl",
                    help="torch.distributed backend for N>1 (nccl = RCCL over xGMI; gloo only for rehearsal)")
     p.add_argument("--rehearse-one-device", action="store_true",
                    help="put every rank on device 0 (multi-rank rehearsal on a 1-GPU box, with --dist-backend gloo)")
+    p.add_argument("--dist-timeout", type=float, default=300.0,
+                   help="seconds: torch.distributed process-group timeout (collectives and p2p waits)")
+    p.add_argument("--secondary-timeout", type=float, default=120.0,
+                   help="seconds one secondary measurement may take before the watchdog prints the line "
+                        "with that field {'error': 'timeout'} and exits non-zero")
     return p.parse_args()
 
 
@@ -150,10 +160,15 @@ def main():
         local = 0
     torch.cuda.set_device(local)
     if world > 1:
+        # a dead or diverged peer fails the collective after --dist-timeout instead of hanging;
+        # the secondaries' watchdog (below) fires first and still reports the headline
+        pg_timeout = datetime.timedelta(seconds=args.dist_timeout)
         if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=pg_timeout)
         else:
-            dist.init_process_group(args.dist_backend)
+            dist.init_process_group(args.dist_backend, timeout=pg_timeout)
+        from volkit_amd import slab as _slab
+        _slab.set_exchange_timeout(args.dist_timeout)
 
     import volkit_amd.volkit as vkt
     from volkit_amd import slab
@@ -304,11 +319,19 @@ def main():
             }
         # a failing secondary measurement is recorded in the line instead of losing the headline
         # (the failures these guard against -- a library error, an allocation -- are the same on
-        # every rank, so no rank is left waiting in a collective)
-        out["mapping_m1_3"] = secondary(mapping_m1_3)
-        out["f32_linear"] = secondary(lambda: f32_linear(ctx, vkt, slab, lib, args, layout_n, stream))
+        # every rank, so no rank is left waiting in a collective); one that overruns (a peer that
+        # never arrives in an exchange) trips the watchdog, which prints the line and exits
+        out["mapping_m1_3"] = guarded(out, "mapping_m1_3", mapping_m1_3, args.secondary_timeout, rank)
+        out["f32_linear"] = guarded(out, "f32_linear",
+                                    lambda: f32_linear(ctx, vkt, slab, lib, args, layout_n, stream),
+                                    args.secondary_timeout, rank)
     if not args.no_config4:
-        out["config4_2048"] = secondary(lambda: config4_strong(ctx, vkt, slab, lib, args, layout_n, stream))
+        out["config4_2048"] = guarded(out, "config4_2048",
+                                      lambda: config4_strong(ctx, vkt, slab, lib, args, layout_n, stream),
+                                      args.secondary_timeout, rank)
+
+    if not args.no_migrate and world == 1:
+        out["migrate"] = guarded(out, "migrate", lambda: migrate_rates(vkt, lib, args.dst), args.secondary_timeout, rank)
 
     if not args.no_copy_peak:
         # achievable streaming rate on this box: the library's own CopyRange of one volume
@@ -364,6 +387,36 @@ def secondary(fn):
     except Exception as e:   # noqa: BLE001 -- reported, not swallowed
         print(f"bench: secondary measurement failed: {e!r}", file=sys.stderr, flush=True)
         return {"error": repr(e)[:300]}
+
+
+WATCHDOG_EXIT = 3
+
+
+def guarded(out, name, fn, seconds, rank, exit_fn=None):
+    """secondary(fn) under a watchdog: if it has not returned after `seconds` (a peer that never
+    joins an exchange or collective blocks every rank), the watchdog thread sets out[name] to
+    {"error": "timeout"}, has rank 0 print the line as it stands -- the headline is measured
+    before any secondary -- and ends the process with WATCHDOG_EXIT (no re-exec; exit_fn for
+    tests).  Fires before the process-group timeout (--dist-timeout), whose handler would abort
+    the process without a line."""
+    fired = threading.Event()
+
+    def fire():
+        fired.set()
+        out[name] = {"error": "timeout", "seconds": seconds,
+                     "note": "watchdog: the measurement did not finish; line printed, process ended"}
+        if rank == 0:
+            print(json.dumps(out), flush=True)
+        print(f"bench: watchdog: secondary '{name}' exceeded {seconds} s", file=sys.stderr, flush=True)
+        (exit_fn or os._exit)(WATCHDOG_EXIT)
+
+    t = threading.Timer(seconds, fire)
+    t.daemon = True
+    t.start()
+    try:
+        return secondary(fn)
+    finally:
+        t.cancel()
 
 
 def f32_linear(ctx, vkt, slab, lib, args, layout_n, stream):
@@ -440,6 +493,59 @@ def f32_linear(ctx, vkt, slab, lib, args, layout_n, stream):
     }
     del S, R
     return out
+
+
+PCIE_PEAK_GBS = 63.0   # MI355X host link, PCIe Gen5 x16 per direction (MI355X_MICROARCH.md)
+
+
+def migrate_rates(vkt, lib, edge, reps=3):
+    """SURVEY §8(a) A2, reported apart from the kernel roofline: ManagedBuffer::migrate of one
+    UInt16 edge^3 volume (2 GiB at 1024^3) between host memory and HBM at a device flip of the
+    thread policy (reference include/cpp/vkt/ManagedBuffer.hpp:168-198 -> runtime/Memory.cpp
+    MigrateBuffer: allocate on the new side, one copy on the side copy stream, free the old side).
+    Pageable host buffers (malloc, the reference's behaviour) and pinned ones
+    (vktHipSetPinnedHostAllocation).  H2D: the host volume (pages written) to HBM; D2H: back into a
+    FRESH host allocation (its pages are first touched by the copy -- part of the flow's cost).
+    Best of `reps` round trips; GB/s of the volume's bytes."""
+    import numpy as np
+    cpu, gpu = vkt.ExecutionPolicy.Device_CPU, vkt.ExecutionPolicy.Device_GPU
+
+    def policy(dev):
+        ep = vkt.GetThreadExecutionPolicy()
+        ep.device = dev
+        vkt.SetThreadExecutionPolicy(ep)
+
+    res = {"volume": f"{edge}^3 UInt16", "bytes": 2 * edge ** 3, "pcie_peak_GBs": PCIE_PEAK_GBS,
+           "note": "host<->HBM migrate() over PCIe; not part of value (inputs are device-resident)"}
+    try:
+        for pinned in (False, True):
+            lib.vktHipSetPinnedHostAllocation(1 if pinned else 0)
+            policy(cpu)
+            v = vkt.StructuredVolume(edge, edge, edge, vkt.DataFormat_UInt16)
+            v.from_numpy(np.full((edge, edge, edge), 0x1234, np.uint16))
+            nbytes = v.getSizeInBytes()
+            h2d, d2h = [], []
+            for _ in range(reps):
+                policy(gpu)
+                t0 = time.perf_counter()
+                v.migrate()
+                if lib.vktHipSynchronize() != 0:
+                    raise RuntimeError(vkt.last_error())
+                h2d.append(time.perf_counter() - t0)
+                policy(cpu)
+                t0 = time.perf_counter()
+                v.migrate()
+                d2h.append(time.perf_counter() - t0)
+            if v.getValue(3, 2, 1) != 0x1234 / 65536.0:
+                raise RuntimeError("migrate round trip changed the data")
+            del v
+            key = "pinned" if pinned else "pageable"
+            res[key] = {"H2D_GBs": round(nbytes / min(h2d) / 1e9, 2), "D2H_GBs": round(nbytes / min(d2h) / 1e9, 2),
+                        "H2D_ms": round(min(h2d) * 1e3, 2), "D2H_ms": round(min(d2h) * 1e3, 2)}
+    finally:
+        lib.vktHipSetPinnedHostAllocation(0)
+        policy(gpu)
+    return res
 
 
 def config4_layout(edge, n, rank):

@@ -114,7 +114,10 @@ VKTAPI vktError vktHipKernelScopeEnd(vktHipKernelScope scope);
  * 0 keeps the 8-voxel item walk), "decompose.grid" (1; 0 makes uniform brick grids load a
  * per-brick descriptor instead of deriving it from the brick index), "memory.pool" (1; 0 gives every
  * device buffer of <= 4 MiB its own hipMalloc instead of a 256-B class of a 64-MiB pooled chunk), "memory.arena" (1; 0 gives every larger buffer its
- * own hipMalloc instead of a 2-MiB aligned block of a >= 16-GiB arena chunk).  For tests and in-process A/B measurements; unknown names return
+ * own hipMalloc instead of a 2-MiB aligned block of an arena chunk), "memory.arena_chunk_mib" (0; > 0 makes
+ * new arena chunks exactly max(request, value MiB): tests), "aggregates.moments" (1; bit 0: UInt16
+ * ComputeAggregates under the unit mapping from one pass of exact integer moments instead of
+ * "aggregates.codes").  For tests and in-process A/B measurements; unknown names return
  * vktInvalidValue.
  *
  * Writes outside a range box: FillRange / CopyRange / convert and device-functor TransformRange
@@ -133,6 +136,12 @@ VKTAPI vktError vktHipReportError(const char* message);
  * from vktHipAllocate / vktAllocate with vktHipFree / vktFree, never with hipFree. */
 VKTAPI vktError vktHipAllocate(void** ptr, size_t size);
 VKTAPI vktError vktHipFree(void* ptr);
+/* The library caches device memory (pool chunks of small buffers; arena chunks of large ones,
+ * sized for a group of like buffers -- four times the request, at least 64 MiB -- and returned to
+ * HIP as soon as their last buffer is freed).  This call waits for the library's streams, then
+ * returns every chunk that holds no live buffer to HIP; *releasedBytes (may be NULL) receives the
+ * bytes released.  A device allocation that fails does the same and retries once. */
+VKTAPI vktError vktHipReleaseCachedMemory(size_t* releasedBytes);
 VKTAPI vktError vktHipMemcpy(void* dst, void const* src, size_t size, vktCopyKind ck);
 /* Host buffers allocated under the CPU policy from now on are page-locked (hipHostMalloc),
  * so migrate() DMAs directly to/from them (default 0: malloc, as the reference). */
@@ -208,10 +217,18 @@ typedef struct vktHipComm_impl* vktHipComm_t;
 VKTAPI vktError vktHipCommGetUniqueId(vktHipCommId_t* id);
 VKTAPI vktError vktHipCommInitRank(vktHipComm_t* comm, int32_t nranks, vktHipCommId_t id, int32_t rank);
 VKTAPI vktError vktHipCommDestroy(vktHipComm_t comm);
+/* Failure detection: every RCCL round the library issues on `comm` (halo
+ * exchange, slab Range moves) waits on the host up to `milliseconds` for its transfers, polling
+ * ncclCommGetAsyncError; a peer that never joins, or an asynchronous RCCL error, aborts the
+ * communicator and the call returns vktInvalidValue (later calls on it fail at once) instead of
+ * hanging every rank.  0: a round returns once enqueued (no host wait).  Default 300 000 ms, or
+ * the environment variable VKT_COMM_TIMEOUT_MS at vktHipCommInitRank. */
+VKTAPI vktError vktHipCommSetTimeout(vktHipComm_t comm, int64_t milliseconds);
 /* `localSrc` holds global source planes [localZ0, localZ0 + localSrc.dimZ) (X/Y dims global).
  * Sends the owned planes the peers' dst slabs read and receives this rank's halo planes into
  * the buffer: one ncclGroupStart .. ncclGroupEnd round of ncclSend / ncclRecv on the compute
- * stream, so a vktHipResampleSlab enqueued next reads the halo.  Returns once enqueued. */
+ * stream, so a vktHipResampleSlab enqueued next reads the halo.  Returns once the round has
+ * completed, or once enqueued with a timeout of 0 (vktHipCommSetTimeout). */
 VKTAPI vktError vktHipSlabExchangeHalo(vktHipComm_t comm, vktHipVolumeView_t localSrc, int32_t localZ0,
                                        int32_t dstGlobalDimZ, int32_t srcGlobalDimZ, vktFilterMode fm,
                                        int32_t needsNeighbours);

@@ -12,7 +12,9 @@ for g in "$@"; do
   B="python3 tools/bench_configs.py --only $g --reps 2"
   timeout -k 10 200 python3 tools/bench_configs.py --only $g --reps 2 > $O/$g.pmc_cases.log 2>&1 || exit 1
   i=0
-  for pass in FETCH_SIZE WRITE_SIZE "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_BUSY_CYCLES SQ_WAIT_INST_ANY"; do
+  PASSES=("FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_BUSY_CYCLES SQ_WAIT_INST_ANY")
+  [ -n "${PMC_EXTRA:-}" ] && PASSES+=("$PMC_EXTRA")   # one more pass (<= 8 SQ counters)
+  for pass in "${PASSES[@]}"; do
     timeout -s KILL 120 rocprofv3 --pmc $pass -d $O/$g/p$i -o run --output-format csv -- $B > $O/$g.p$i.log 2>&1 || { tail -20 $O/$g.p$i.log; exit 1; }
     i=$((i+1))
   done

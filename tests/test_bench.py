@@ -77,5 +77,9 @@ def test_bench_small_run_prints_one_contract_line():
     f32 = out["f32_linear"]
     assert f32["value"] > 0 and f32["halo_planes_per_rank"] == 0 and "Float32 Linear" in f32["workload"]
     assert out["config4_2048"]["value"] > 0 and out["config4_2048"]["scaling"] == "strong"
+    mig = out["migrate"]
+    assert "error" not in mig, mig
+    for kind in ("pageable", "pinned"):
+        assert mig[kind]["H2D_GBs"] > 0 and mig[kind]["D2H_GBs"] > 0, mig
     cpu = out["cpu_baseline"]
     assert cpu["kind"] == "port" and cpu["cores"] == 1 and cpu["value"] > 0

@@ -73,6 +73,7 @@ def test_plan_errors_are_returned():
     assert "too small" in _lib.last_error()
     assert lib.vktHipSlabExchangeHalo(None, HipVolumeView_t(), 0, 64, 32, LINEAR, 1) != 0
     assert "null communicator" in _lib.last_error()
+    assert lib.vktHipCommSetTimeout(None, 1000) != 0
 
 
 @pytest.mark.gpu
@@ -84,6 +85,8 @@ def test_one_rank_communicator():
     comm = C.c_void_p()
     assert lib.vktHipCommInitRank(C.byref(comm), 1, uid, 0) == 0, _lib.last_error()
     try:
+        assert lib.vktHipCommSetTimeout(comm, -1) != 0
+        assert lib.vktHipCommSetTimeout(comm, 5000) == 0, _lib.last_error()
         buf = torch.zeros(16 * 16 * 8 * 2, dtype=torch.uint8, device="cuda")
         view = HipVolumeView_t(buf.data_ptr(), 16, 16, 8, 5, 0.0, 1.0)
         # one rank owns every plane: nothing to move

@@ -91,3 +91,42 @@ def test_context_argument_checks():
         assert (cid.value, pid.value) == (0, 0)
     finally:
         _ok(lib.vktHipContextDestroy(ctx))
+
+
+def test_shrinking_the_current_context_with_work_queued():
+    """SetNumStreams on the CURRENT context while kernels are queued on the compute stream it
+    removes (and SetStream replacing a bound owned stream): the backend is rebound to a surviving
+    stream and the old one is synchronised before it is destroyed, so the queued work finishes and
+    later calls run on a live stream."""
+    import torch
+    torch.cuda.set_device(0)
+    ctx = C.c_void_p()
+    _ok(lib.vktHipContextCreate(C.byref(ctx)))
+    n = 256
+    t = torch.zeros(n * n * n, dtype=torch.uint16, device="cuda")
+    torch.cuda.synchronize()
+    v = _lib.HipVolumeView_t(t.data_ptr(), n, n, n, 5, 0.0, 1.0)
+    o, last = _lib.Vec3i_t(0, 0, 0), _lib.Vec3i_t(n, n, n)
+    try:
+        _ok(lib.vktHipContextSetNumStreams(ctx, 4))
+        _ok(lib.vktHipContextSetComputeStreamId(ctx, 3))
+        _ok(lib.vktHipContextMakeCurrent(ctx))
+        for k in range(40):   # queued on stream 3, asynchronously
+            _ok(lib.vktHipFillRange(v, o, last, C.c_float((k + 1) / 65536.0)))
+        _ok(lib.vktHipContextSetNumStreams(ctx, 2))        # stream 3 goes: rebind, sync, destroy
+        cs, s1 = C.c_void_p(), C.c_void_p()
+        _ok(lib.vktHipGetComputeStream(C.byref(cs)))
+        _ok(lib.vktHipContextGetStream(ctx, 1, C.byref(s1)))
+        assert cs.value == s1.value
+        _ok(lib.vktHipFillRange(v, o, last, C.c_float(41 / 65536.0)))   # on the new stream
+        for k in range(10):
+            _ok(lib.vktHipFillRange(v, o, last, C.c_float((k + 100) / 65536.0)))
+        user = torch.cuda.Stream()
+        _ok(lib.vktHipContextSetStream(ctx, 1, C.c_void_p(user.cuda_stream)))   # replaces the bound stream
+        _ok(lib.vktHipGetComputeStream(C.byref(cs)))
+        assert cs.value == user.cuda_stream
+        _ok(lib.vktHipFillRange(v, o, last, C.c_float(7 / 65536.0)))
+        _ok(lib.vktHipSynchronize())
+        assert (t.cpu().numpy() == 7).all()
+    finally:
+        _ok(lib.vktHipContextDestroy(ctx))

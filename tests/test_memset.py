@@ -203,3 +203,98 @@ def test_large_device_buffers_from_arena_chunks(arena):
     finally:
         policy(vkt.ExecutionPolicy.Device_CPU)
         L.vktHipSetTuningKnob(b"memory.arena", -1)
+
+
+@pytest.mark.gpu
+def test_arena_is_proportionate_and_returns_memory():
+    """A 5 MiB device buffer reserves at most 64 MiB of HBM (an arena chunk sized for a group of
+    like buffers, not a fixed 16-GiB chunk), freeing it returns the chunk to HIP at once, and
+    vktHipReleaseCachedMemory returns the cached pool chunks."""
+    import torch
+    from volkit_amd import _lib
+    from volkit_amd._lib import lib
+    torch.cuda.set_device(0)
+    lib.vktHipReleaseCachedMemory(None)
+    torch.cuda.synchronize()
+    free0, _ = torch.cuda.mem_get_info()
+    p = C.c_void_p()
+    assert lib.vktHipAllocate(C.byref(p), 5 << 20) == 0, _lib.last_error()
+    free1, _ = torch.cuda.mem_get_info()
+    assert 0 < free0 - free1 <= (64 << 20) + (2 << 20), (free0 - free1) / 2 ** 20
+    assert lib.vktHipFree(p) == 0
+    free2, _ = torch.cuda.mem_get_info()
+    assert free2 >= free0 - (2 << 20), (free0 - free2) / 2 ** 20      # the empty chunk went back
+    # small buffers: a cached pool chunk until the trim call
+    q = C.c_void_p()
+    assert lib.vktHipAllocate(C.byref(q), 4096) == 0
+    assert lib.vktHipFree(q) == 0
+    released = C.c_size_t(0)
+    assert lib.vktHipReleaseCachedMemory(C.byref(released)) == 0
+    assert released.value >= 64 << 20
+    free3, _ = torch.cuda.mem_get_info()
+    assert free3 >= free0 - (2 << 20)
+    # a group of large buffers shares one chunk: the second and third follow the first
+    vols = []
+    for _ in range(3):
+        r = C.c_void_p()
+        assert lib.vktHipAllocate(C.byref(r), 256 << 20) == 0
+        vols.append(r.value)
+    assert vols[1] - vols[0] == 256 << 20 and vols[2] - vols[1] == 256 << 20, [hex(v) for v in vols]
+    for r in vols:
+        assert lib.vktHipFree(C.c_void_p(r)) == 0
+    free4, _ = torch.cuda.mem_get_info()
+    assert free4 >= free0 - (2 << 20)
+
+
+@pytest.mark.gpu
+def test_arena_exhaustion_coalesces_freed_neighbours():
+    """Force the arena's reuse path with 64-MiB chunks (knob memory.arena_chunk_mib): a full chunk,
+    two freed neighbours in the middle (pending until the drain), an allocation of their combined
+    size must wait for the drain and land at the first one's address; the untouched neighbours keep
+    their contents; a larger request opens a new chunk."""
+    import torch
+    from volkit_amd import _lib
+    from volkit_amd._lib import lib
+    torch.cuda.set_device(0)
+    mib = 1 << 20
+    lib.vktHipSetTuningKnob(b"memory.arena_chunk_mib", 64)
+    try:
+        blocks = []
+        for k in range(4):
+            p = C.c_void_p()
+            assert lib.vktHipAllocate(C.byref(p), 16 * mib) == 0, _lib.last_error()
+            blocks.append(p.value)
+        assert all(blocks[k + 1] - blocks[k] == 16 * mib for k in range(3)), [hex(b) for b in blocks]
+        ends = []
+        for k in (0, 3):   # patterns that must survive the reuse of the middle
+            t = torch.full((16 * mib,), k + 1, dtype=torch.uint8, device="cuda")
+            assert lib.vktHipMemcpy(C.c_void_p(blocks[k]), C.c_void_p(t.data_ptr()), 16 * mib, 3) == 0
+            ends.append(t)
+        # queued work on the library's stream that still reads block 1 while it is freed
+        src = _lib.HipVolumeView_t(blocks[1], 1024, 1024, 8, 5, 0.0, 1.0)
+        dst = _lib.HipVolumeView_t(blocks[3], 1024, 1024, 8, 5, 0.0, 1.0)
+        o, last = _lib.Vec3i_t(0, 0, 0), _lib.Vec3i_t(1024, 1024, 8)
+        assert lib.vktHipFillRange(src, o, last, C.c_float(4 / 65536.0)) == 0
+        for _ in range(20):
+            assert lib.vktHipCopyRange(dst, src, o, last, o) == 0
+        assert lib.vktHipFree(C.c_void_p(blocks[1])) == 0
+        assert lib.vktHipFree(C.c_void_p(blocks[2])) == 0
+        p = C.c_void_p()
+        assert lib.vktHipAllocate(C.byref(p), 32 * mib) == 0
+        assert p.value == blocks[1], (hex(p.value), hex(blocks[1]))   # the two holes merged
+        got3 = torch.empty(16 * mib, dtype=torch.uint8, device="cuda")
+        assert lib.vktHipMemcpy(C.c_void_p(got3.data_ptr()), C.c_void_p(blocks[3]), 16 * mib, 3) == 0
+        torch.cuda.synchronize()
+        # block 3 holds the copies of block 1's fill (code 4), completed before the reuse
+        assert (got3.view(torch.int16) == 4).all()
+        got0 = torch.empty(16 * mib, dtype=torch.uint8, device="cuda")
+        assert lib.vktHipMemcpy(C.c_void_p(got0.data_ptr()), C.c_void_p(blocks[0]), 16 * mib, 3) == 0
+        torch.cuda.synchronize()
+        assert (got0 == 1).all()
+        q = C.c_void_p()
+        assert lib.vktHipAllocate(C.byref(q), 48 * mib) == 0        # no room left: a new chunk
+        assert not (blocks[0] <= q.value < blocks[0] + 64 * mib)
+        for b in (blocks[0], p.value, blocks[3], q.value):
+            assert lib.vktHipFree(C.c_void_p(b)) == 0
+    finally:
+        lib.vktHipSetTuningKnob(b"memory.arena_chunk_mib", -1)

@@ -8,6 +8,11 @@ Parity contract:
       |gpu - exact| <= 1 ulp(exact) + 2^-24 * sum|terms| * 1e-6     (GPU is accurate)
       |gpu - oracle| <= n * 2^-24 * sum|terms| + 1 ulp                (serial error bound)
     where exact is a float64 sum of the same float32 terms.
+  * var under the UInt16 unit-mapping moments path (knob aggregates.moments): the
+    sum of squares is the EXACT sum (v - m)^2 from integer moments, not a sum of float terms;
+    each float term fl(fl(v - m)^2) lies within 3 * 2^-24 of (v - m)^2, so
+      |var - var_terms| <= 3 * 2^-24 * var_terms + 2 ulp(var_terms)
+    (var_terms: the float-terms value above); far inside the serial bound.
 The oracle itself is pinned here against numpy's sequential float32 accumulation
 (np.add.accumulate is strictly left-to-right) and a float32 restatement of the bin formula.
 """
@@ -317,6 +322,18 @@ def test_histogram_packed16_matches_tiled_passes(fmt):
     np.testing.assert_array_equal(runs[0], ref)
 
 
+def takes_moments(fmt, mapping):
+    """UInt16 under the unit mapping (+0, 1) takes the integer-moments path (aggregates.moments)."""
+    return fmt == 5 and mapping[1] == 1.0 and mapping[0] == 0.0 and np.copysign(1.0, mapping[0]) > 0
+
+
+def check_var(got_var, var_terms, moments, what=""):
+    """var against the float-terms value: 1 ulp, or the moments bound (module docstring)."""
+    ulp = float(np.spacing(np.float32(abs(var_terms))))
+    bound = 3 * EPS * abs(var_terms) + 2 * ulp if moments else ulp
+    assert abs(got_var - var_terms) <= bound, f"var {got_var} vs {var_terms} {what}"
+
+
 def check_float(name, gpu, oracle, exact, terms_abs_sum, n):
     ulp = float(np.spacing(np.float32(abs(exact)))) if np.isfinite(exact) else 0.0
     assert abs(gpu - exact) <= ulp + 1e-6 * EPS * terms_abs_sum, f"{name}: gpu {gpu} vs exact {exact}"
@@ -344,7 +361,7 @@ def test_aggregates_parity(fmt, mapping):
         d = (vals - np.float32(got.mean)).astype(np.float32)
         d2 = (d * d).astype(np.float32)
         exact_var = float(np.float32(np.float64(np.float32(np.sum(d2, dtype=np.float64))) / nall))
-        assert abs(got.var - exact_var) <= float(np.spacing(np.float32(exact_var))), what
+        check_var(got.var, exact_var, takes_moments(fmt, mapping), what)
         assert abs(got.var - ref.var) <= n * EPS * 4 * (abs(ref.var) + 1e-30) + float(np.spacing(np.float32(ref.var)))
         assert got.stddev == np.float32(np.sqrt(np.float32(got.var))), what
 
@@ -418,9 +435,17 @@ def check_aggregates(got, codes, fmt, mapping, first, last, what):
     d = (vals - np.float32(got.mean)).astype(np.float32)
     d2 = (d * d).astype(np.float32)
     exact_var = float(np.float32(np.float64(np.float32(np.sum(d2, dtype=np.float64))) / nall))
-    assert abs(got.var - exact_var) <= float(np.spacing(np.float32(exact_var))), what
+    moments = takes_moments(fmt, mapping) and lib_knob_moments_on()
+    check_var(got.var, exact_var, moments, what)
     assert got.stddev == np.float32(np.sqrt(np.float32(got.var))), what
     return ref
+
+
+_MOMENTS_OFF = []
+
+
+def lib_knob_moments_on():
+    return not _MOMENTS_OFF
 
 
 @pytest.mark.gpu
@@ -604,3 +629,88 @@ def test_u8_histogram_over_rows_from_code_counts(rows16):
                 np.testing.assert_array_equal(got, ref, err_msg=f"{first}->{last} map={mapping} nbins={nbins}")
     finally:
         lib.vktHipSetTuningKnob(b"reduce.u8_rows16", -1)
+
+
+@pytest.mark.gpu
+def test_aggregates_uint16_moments():
+    """UInt16 ComputeAggregates under the unit mapping from one pass of exact integer moments
+    (knob aggregates.moments) against the oracle and against the code-count path
+    (knob 0): every code once (min 0 / max 65535 at known places), random codes over spans,
+    padded rows (row ends at every phase mod 8, masked end items), strided boxes, ranges with a
+    partial wave-step, tied extremes across lanes / waves / steps, extremes first occurring late,
+    constant volumes (var exactly 0, as the float terms give), a constant volume whose first voxel
+    differs (the cancellation case of a float moment form), a product that stays above 0.
+    min / max / arg / sum / mean are identical to the code-count path; var within the stated bound."""
+    rng = np.random.default_rng(2024)
+    every = rng.permutation(np.arange(65536, dtype=np.uint16)).reshape(16, 16, 256)
+    rand = rng.integers(0, 65536, (24, 40, 1040), dtype=np.uint16)
+    for z, y, x in ((5, 7, 9), (2, 3, 1000), (20, 30, 40), (23, 39, 1039)):
+        rand[z, y, x] = 7          # tied small codes (the minimum of rand below 7 is overwritten)
+    rand[rand < 7] = 8
+    for z, y, x in ((6, 1, 511), (6, 1, 513), (22, 38, 8)):
+        rand[z, y, x] = 65535
+    const = np.full((10, 20, 64), 40000, np.uint16)
+    outlier = const.copy()
+    outlier[0, 0, 0] = 1
+    late = rng.integers(100, 60000, (16, 64, 1024), dtype=np.uint16)
+    late[12, 5, 700] = late[14, 0, 3] = 3
+    late[15, 63, 1000] = late[13, 9, 9] = 65000
+    cases = [(every, [((0, 0, 0), (256, 16, 16)), ((3, 1, 2), (253, 15, 14)), ((8, 0, 0), (16, 16, 16))]),
+             (rand, [((0, 0, 0), (1040, 40, 24)), ((3, 1, 2), (1037, 39, 23)), ((1, 0, 0), (2, 40, 24)),
+                     ((9, 5, 3), (1031, 6, 4)), ((0, 0, 5), (1040, 40, 6)), ((512, 3, 3), (520, 9, 20))]),
+             (const, [((0, 0, 0), (64, 20, 10)), ((5, 3, 1), (61, 19, 9))]),
+             (outlier, [((0, 0, 0), (64, 20, 10))]),
+             (late, [((0, 0, 0), (1024, 64, 16)), ((3, 1, 0), (1021, 64, 16))])]
+    for codes, boxes in cases:
+        for first, last in boxes:
+            what = f"dims={codes.shape} {first}->{last}"
+            got = gpu_aggregates(codes, 5, 0.0, 1.0, first, last)
+            check_aggregates(got, codes, 5, (0.0, 1.0), first, last, what)
+            lib.vktHipSetTuningKnob(b"aggregates.moments", 0)
+            _MOMENTS_OFF.append(1)
+            try:
+                two = gpu_aggregates(codes, 5, 0.0, 1.0, first, last)
+                check_aggregates(two, codes, 5, (0.0, 1.0), first, last, what + " knob=0")
+            finally:
+                _MOMENTS_OFF.clear()
+                lib.vktHipSetTuningKnob(b"aggregates.moments", -1)
+            assert (got.min, got.max, tuple(got.argmin), tuple(got.argmax), got.sum, got.mean) == \
+                (two.min, two.max, tuple(two.argmin), tuple(two.argmax), two.sum, two.mean), what
+            if codes is const:
+                assert got.var == 0.0 and two.var == 0.0, what
+    # product through the pair products: all-top volume, (1 - 2^-16)^n stays far from 0
+    codes = np.full((4, 8, 64), 65535, np.uint16)
+    got = gpu_aggregates(codes, 5, 0.0, 1.0, (0, 0, 0), (64, 8, 4))
+    exact = (65535 / 65536) ** codes.size
+    assert got.prod != 0.0 and abs(got.prod - exact) <= codes.size * EPS * exact, (got.prod, exact)
+
+
+@pytest.mark.gpu
+def test_aggregates_uint16_moments_sum_of_squares_beyond_2_64():
+    """The code sum of squares of > 2^32 voxels of code 65535 exceeds 2^64: the 128-bit combine of
+    the workgroup partials (aggregatesMomentsU16FinalKernel).  Constant volume of 2048 x 2048 x
+    1025 voxels (8.6 GB): sum = n * 65535 * 2^-16 exactly rounded, var = the float mean's offset
+    from the value squared, as the float terms of the reference give it."""
+    import torch
+    dims = (2048, 2048, 1025)
+    n = dims[0] * dims[1] * dims[2]
+    t = torch.empty((2 * n,), dtype=torch.uint8, device="cuda")
+    view = _lib.HipVolumeView_t(t.data_ptr(), dims[0], dims[1], dims[2], 5, 0.0, 1.0)
+    out = _lib.Aggregates_t()
+    try:
+        assert lib.vktHipFillRange(view, _lib.Vec3i_t(0, 0, 0), _lib.Vec3i_t(*dims), C.c_float(65535 / 65536)) == 0
+        assert lib.vktHipAggregatesRange(view, _lib.Vec3i_t(0, 0, 0), _lib.Vec3i_t(*dims), C.byref(out)) == 0, \
+            _lib.last_error()
+    finally:
+        del t
+        torch.cuda.empty_cache()
+    v = np.float32(65535 / 65536)
+    s = np.float32(n * (65535 / 65536))
+    assert out.sum == s
+    m = np.float32(np.float64(s) / n)
+    assert out.mean == m
+    d = np.float32(v - m)
+    var_terms = float(np.float32(np.float64(np.float32(np.float64(d * d) * n)) / n))
+    check_var(out.var, var_terms, True, "2^32+ voxels")
+    assert (out.min, out.max) == (v, v)
+    assert (out.argmin.x, out.argmin.y, out.argmin.z) == (0, 0, 0) == (out.argmax.x, out.argmax.y, out.argmax.z)

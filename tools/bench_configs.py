@@ -211,6 +211,46 @@ def main():
                 report(f"{grp} SumRange {lab} {name}",
                        timed(lambda: lib.vktHipArithmeticRange(0, D, A, B, f0, f1, o), R), 3 * bpv * nv, nv)
             free(A, B, D)
+    if want("f32shift"):
+        # one launch per case (PMC passes): the Float32 general path with a
+        # phase shift, and UInt8 SumRange on the 800^3 sub-box at x0 = 100, default knobs
+        m = 1024
+        for fmt, bpv, name in ((7, 4, "Float32"), (4, 1, "UInt8")):
+            A, B, D = alloc((m,) * 3, fmt, seed=1), alloc((m,) * 3, fmt, seed=2), alloc((m,) * 3, fmt)
+            f0, f1 = Vec3i_t(100, 100, 100), Vec3i_t(900, 900, 900)
+            nv = 800 ** 3
+            if fmt == 7:
+                report(f"f32shift CopyRange 800^3 x0=100 -> dst 0 {name}",
+                       timed(lambda: lib.vktHipCopyRange(D, A, f0, f1, o), R), 2 * bpv * nv, nv)
+                report(f"f32shift CopyRange 800^3 x0=100 -> dst x0=3 {name}",
+                       timed(lambda: lib.vktHipCopyRange(D, A, f0, f1, Vec3i_t(3, 100, 100)), R), 2 * bpv * nv, nv)
+                report(f"f32shift SumRange 800^3 x0=100 dstOffset x=-97 {name}",
+                       timed(lambda: lib.vktHipArithmeticRange(0, D, A, B, f0, f1, Vec3i_t(-97, 0, 0)), R),
+                       3 * bpv * nv, nv)
+                report(f"f32shift CopyRange 800^3 x0=100 same offset {name}",
+                       timed(lambda: lib.vktHipCopyRange(D, A, f0, f1, f0), R), 2 * bpv * nv, nv)
+            else:
+                report(f"f32shift SumRange 800^3 x0=100 {name}",
+                       timed(lambda: lib.vktHipArithmeticRange(0, D, A, B, f0, f1, o), R), 3 * bpv * nv, nv)
+                report(f"f32shift CopyRange 800^3 x0=100 same offset {name}",
+                       timed(lambda: lib.vktHipCopyRange(D, A, f0, f1, f0), R), 2 * bpv * nv, nv)
+            free(A, B, D)
+    if want("p16"):
+        # the 65 536-bin UInt16 histogram (packed 16-bit LDS counters), one launch per case
+        # (accumulate: no zeroing kernel) -- the code-count kernel of the UInt16 aggregates too
+        n = 1024
+        V = alloc((n,) * 3, 5, seed=11)
+        hb = C.c_void_p()
+        if lib.vktHipAllocate(C.byref(hb), 65536 * 8) != 0:
+            raise RuntimeError(_lib.last_error())
+        bins = C.c_void_p(hb.value)
+        last = Vec3i_t(n, n, n)
+        report("p16 Histogram 1024^3 UInt16 65536 bins (P16)",
+               timed(lambda: lib.vktHipHistogramRange(V, o, last, bins, 65536, 1), R), 2 * n ** 3, n ** 3)
+        report("p16 Histogram 1024^3 UInt16 256 bins (replicated counters)",
+               timed(lambda: lib.vktHipHistogramRange(V, o, last, bins, 256, 1), R), 2 * n ** 3, n ** 3)
+        lib.vktHipFree(hb)
+        free(V)
     if want("u8ab"):
         # in-process A/B of the UInt8 16-voxel pair grid (knob pointwise.u8_pairs: 0 off, 1
         # default rule, 2 forced, 3 the general path's wide items), alternating on the same
@@ -747,6 +787,27 @@ def main():
             ms = timed(lambda: lib.vktHipAggregatesRange(V, a0, a1, C.byref(agg)), R)
             report(f"aggcodes Aggregates UInt16 800^3 sub-box x 0..800 [codes={k}, {passes} pass(es)]", ms,
                    passes * 2 * 800 ** 3, 800 ** 3)
+        lib.vktHipSetTuningKnob(b"aggregates.codes", -1)
+        free(V)
+    if want("moments"):
+        # UInt16 ComputeAggregates under the unit mapping: one pass of integer moments (knob
+        # aggregates.moments) vs the packed-16 code counts vs the two float passes; per call,
+        # incl. the D2H of the result.  Bytes: one read of the range.
+        n = 1024
+        V = alloc((n,) * 3, 5, seed=11)
+        last = Vec3i_t(n, n, n)
+        agg = _lib.Aggregates_t()
+        boxes = ((o, last, "1024^3"), (Vec3i_t(100, 100, 100), Vec3i_t(900, 900, 900), "800^3 sub-box at x0=100"),
+                 (Vec3i_t(0, 100, 100), Vec3i_t(800, 900, 900), "800^3 sub-box x 0..800"),
+                 (Vec3i_t(3, 0, 0), Vec3i_t(67, 64, 64), "64^3 box (fixed cost)"))
+        for mom, codes, what in ((1, 3, "moments"), (0, 3, "code counts"), (0, 1, "2 float passes")):
+            lib.vktHipSetTuningKnob(b"aggregates.moments", mom)
+            lib.vktHipSetTuningKnob(b"aggregates.codes", codes)
+            for a0, a1, box in boxes:
+                nv = (a1.x - a0.x) * (a1.y - a0.y) * (a1.z - a0.z)
+                ms = timed(lambda: lib.vktHipAggregatesRange(V, a0, a1, C.byref(agg)), R)
+                report(f"moments Aggregates UInt16 {box} [{what}]", ms, 2 * nv, nv)
+        lib.vktHipSetTuningKnob(b"aggregates.moments", -1)
         lib.vktHipSetTuningKnob(b"aggregates.codes", -1)
         free(V)
     if want("config5"):

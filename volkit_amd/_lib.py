@@ -230,6 +230,7 @@ SIGNATURES = {
     "vktHipSetTuningKnob": (c_err, [C.c_char_p, C.c_int64]),
     "vktHipAllocate": (c_err, [P(C.c_void_p), C.c_size_t]),
     "vktHipFree": (c_err, [C.c_void_p]),
+    "vktHipReleaseCachedMemory": (c_err, [P(C.c_size_t)]),
     "vktHipMemcpy": (c_err, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]),
     "vktHipMemsetRange": (c_err, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_size_t]),
     "vktHipSetPinnedHostAllocation": (c_err, [i32]),
@@ -246,6 +247,7 @@ SIGNATURES = {
     "vktHipCommGetUniqueId": (c_err, [P(HipCommId_t)]),
     "vktHipCommInitRank": (c_err, [P(c_comm), i32, HipCommId_t, i32]),
     "vktHipCommDestroy": (c_err, [c_comm]),
+    "vktHipCommSetTimeout": (c_err, [c_comm, C.c_int64]),
     "vktHipSlabExchangeHalo": (c_err, [c_comm, HipVolumeView_t, i32, i32, i32, C.c_int, i32]),
     "vktHipSlabExchangeHaloLocal": (c_err, [i32, P(HipVolumeView_t), P(i32), i32, i32, C.c_int, i32]),
     "vktHipSlabRangePlan": (c_err, [C.c_int, i32, i32, i32, i32, i32, Vec3i_t, Vec3i_t, Vec3i_t, P(HipSlabPiece_t),

@@ -1370,6 +1370,270 @@ namespace hipk
         }
     }
 
+    // ---- Aggregates in ONE pass of exact integer moments (UInt16, unit mapping) ----------------
+    // Under the unit mapping (+0, 1) a UInt16 voxel's value is v = c * 2^-16 exactly
+    // (codec::decodeUnit), so everything Aggregates_serial.hpp:37-80 derives from the values
+    // follows from integer sums over the codes, exactly: sum = Sc * 2^-16, and the second pass's
+    // sum of squares about the float mean m is
+    //     S = 2^-32 * sum (c - mu)^2 = 2^-32 * ((n Sc2 - Sc^2) + (Sc - n mu)^2) / n,   mu = m * 2^16,
+    // with Sc = sum c (u64) and Sc2 = sum c^2 (128-bit), so the data is read once.  min / max /
+    // argmin / argmax follow the codes (v is strictly increasing in c), first occurrence exact as in
+    // aggregatesFastKernel (a lane visits its voxels in increasing index order, the combines
+    // tie-break on the index).  prod multiplies the values in double as the other paths do.
+    // Per lane and 16-B item (8 codes in 4 dwords w):
+    //  * Sc: v_dot2_u32_u16(w, {1, 1}) -- 1 instruction per 2 codes;
+    //  * Sc2: c^2 = 2^16 h^2 + r with h = c >> 8, r = 512 h l + l^2 < 2^25: per dword
+    //    H += dot2(hb, hb) (hb = the two high bytes) and Q += dot2(w, w) mod 2^32; per wave-step
+    //    (32 codes) R = Q - 2^16 H mod 2^32 is the exact sum of the r (< 2^30), so
+    //    Sc2 += 2^16 H + R -- 3 instructions per 2 codes, exact;
+    //  * extremes: v_pk_min/max_u16 over the 4 dwords, the in-order per-voxel update only when the
+    //    item can improve the lane's (rare after the first items);
+    //  * prod: (c0 c1) exact in v_mul_u32_u24, four pair products in double scaled by 2^-128 --
+    //    skipped once every lane's product is +0 (it stays 0: the values are finite).
+    // Items outside the range in padded rows' end items (mask m != 0xFF) go voxel by voxel.
+    // The float paths needed a decode, two double adds / multiplies and float min/max per voxel,
+    // plus either a second pass over the data or a 65 536-code LDS count.
+    struct MomentPartialU16
+    {
+        uint64_t count, sumC, sumSqLo, sumSqHi;
+        double prod;
+        uint32_t cmin;     // 0x10000: none
+        int32_t cmax;      // -1: none
+        uint64_t minIndex, maxIndex;
+    };
+
+    typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
+
+    __device__ __forceinline__ u16x2 asU16x2(uint32_t w) { return __builtin_bit_cast(u16x2, w); }
+
+    __device__ __forceinline__ void momentCombine(MomentPartialU16& p, MomentPartialU16 const& o)
+    {
+        uint64_t const lo = p.sumSqLo + o.sumSqLo;
+        p.sumSqHi += o.sumSqHi + (lo < p.sumSqLo ? 1u : 0u);
+        p.sumSqLo = lo;
+        p.count += o.count;
+        p.sumC += o.sumC;
+        p.prod *= o.prod;
+        if (o.cmin < p.cmin || (o.cmin == p.cmin && o.minIndex < p.minIndex))
+        {
+            p.cmin = o.cmin;
+            p.minIndex = o.minIndex;
+        }
+        if (o.cmax > p.cmax || (o.cmax == p.cmax && o.maxIndex < p.maxIndex))
+        {
+            p.cmax = o.cmax;
+            p.maxIndex = o.maxIndex;
+        }
+    }
+
+    __device__ __forceinline__ MomentPartialU16 shflXorMoment(MomentPartialU16 const& p, int m)
+    {
+        MomentPartialU16 o;
+        o.count = shflXorU(p.count, m);
+        o.sumC = shflXorU(p.sumC, m);
+        o.sumSqLo = shflXorU(p.sumSqLo, m);
+        o.sumSqHi = shflXorU(p.sumSqHi, m);
+        o.prod = shflXorD(p.prod, m);
+        o.cmin = __shfl_xor(p.cmin, m);
+        o.cmax = __shfl_xor(p.cmax, m);
+        o.minIndex = shflXorU(p.minIndex, m);
+        o.maxIndex = shflXorU(p.maxIndex, m);
+        return o;
+    }
+
+    // wave butterfly, then the workgroup's waves in order through LDS (thread 0 ends with it)
+    template <int WAVES>
+    __device__ void momentBlockReduce(MomentPartialU16& p)
+    {
+        for (int m = 32; m >= 1; m >>= 1)
+            momentCombine(p, shflXorMoment(p, m));
+        __shared__ MomentPartialU16 lds[WAVES];
+        if ((threadIdx.x & 63) == 0)
+            lds[threadIdx.x >> 6] = p;
+        __syncthreads();
+        if (threadIdx.x == 0)
+            for (int w = 1; w < WAVES; ++w)
+                momentCombine(p, lds[w]);
+    }
+
+    template <bool CONTIG>
+    __global__ __launch_bounds__(kBlock) void aggregatesMomentsU16Kernel(FastHistArgs h, MomentPartialU16* partials)
+    {
+        constexpr int U = 4;
+        uint32_t const lane = threadIdx.x & 63;
+        MomentPartialU16 p;
+        p.count = p.sumC = p.sumSqLo = p.sumSqHi = 0;
+        p.prod = 1.0;
+        p.cmin = 0x10000u;
+        p.cmax = -1;
+        p.minIndex = p.maxIndex = kNoIndex;
+        uint32_t sc = 0, hq = 0, q = 0;   // this step's Sc, H and Q (see above)
+        auto addSq = [&](uint64_t x) {
+            uint64_t const lo = p.sumSqLo + x;
+            p.sumSqHi += lo < x ? 1u : 0u;
+            p.sumSqLo = lo;
+        };
+        auto flushStep = [&] {
+            uint32_t const r = q - (hq << 16);   // exact: the r of <= 32 codes sum to < 2^30
+            addSq((static_cast<uint64_t>(hq) << 16) + r);
+            p.sumC += sc;
+            sc = hq = q = 0;
+        };
+        // in-order strict updates of the lane's extremes over the valid voxels of one item
+        auto extremes = [&](uint32_t const (&w)[4], uint32_t m, uint64_t item) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+            {
+                uint32_t const c = (w[j / 2] >> (16 * (j % 2))) & 0xFFFFu;
+                if (((m >> j) & 1u) && (c < p.cmin || static_cast<int32_t>(c) > p.cmax))
+                {
+                    uint64_t const gi = spanGlobalIndex<CONTIG>(h, item, j);
+                    if (c < p.cmin)
+                    {
+                        p.cmin = c;
+                        p.minIndex = gi;
+                    }
+                    if (static_cast<int32_t>(c) > p.cmax)
+                    {
+                        p.cmax = static_cast<int32_t>(c);
+                        p.maxIndex = gi;
+                    }
+                }
+            }
+        };
+        auto item8 = [&](uint32_t const (&w)[4], uint32_t m, uint64_t item, bool prodLive) {
+            if (m == 0xFFu)
+            {
+                u16x2 const one = {1, 1};
+                u16x2 mn = asU16x2(w[0]), mx = mn;
+#pragma unroll
+                for (int d = 0; d < 4; ++d)
+                {
+                    u16x2 const x = asU16x2(w[d]);
+                    if (d)
+                    {
+                        mn = __builtin_elementwise_min(mn, x);
+                        mx = __builtin_elementwise_max(mx, x);
+                    }
+                    sc = __builtin_amdgcn_udot2(x, one, sc, false);
+                    // the two high bytes as u16 (v_perm_b32: bytes 1, 3 of w, zeros above)
+                    u16x2 const hb = asU16x2(__builtin_amdgcn_perm(0u, w[d], 0x0C030C01u));
+                    hq = __builtin_amdgcn_udot2(hb, hb, hq, false);
+                    q = __builtin_amdgcn_udot2(x, x, q, false);
+                }
+                uint32_t const imin = mn.x < mn.y ? mn.x : mn.y, imax = mx.x > mx.y ? mx.x : mx.y;
+                if (imin < p.cmin || static_cast<int32_t>(imax) > p.cmax)
+                    extremes(w, 0xFFu, item);
+                if (prodLive)
+                {
+                    double pr[4];
+#pragma unroll
+                    for (int d = 0; d < 4; ++d)
+                        pr[d] = static_cast<double>(static_cast<uint32_t>(__umul24(w[d] & 0xFFFFu, w[d] >> 16)));
+                    p.prod *= ((pr[0] * pr[1]) * (pr[2] * pr[3])) * 0x1p-128;
+                }
+                p.count += 8;
+            }
+            else
+            {
+                // padded row end item: voxel by voxel, outside-range voxels skipped
+                extremes(w, m, item);
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                {
+                    uint32_t const c = (w[j / 2] >> (16 * (j % 2))) & 0xFFFFu;
+                    if ((m >> j) & 1u)
+                    {
+                        p.sumC += c;
+                        addSq(static_cast<uint64_t>(c) * c);
+                        p.prod *= static_cast<double>(c) * 0x1p-16;
+                        p.count += 1;
+                    }
+                }
+            }
+        };
+        uint64_t const wave = static_cast<uint64_t>(blockIdx.x) * (kBlock / 64) + (threadIdx.x >> 6);
+        uint64_t const waves = static_cast<uint64_t>(gridDim.x) * (kBlock / 64);
+        uint64_t const steps = h.items / (64 * U);
+        for (uint64_t st = wave; st < steps; st += waves)
+        {
+            uint32_t w[U][4], msk[U];
+#pragma unroll
+            for (int k = 0; k < U; ++k)
+            {
+                u32x4 const x = loadVec<u32x4, true>(
+                    h.data + 2 * spanVoxelMask<CONTIG>(h, st * (64 * U) + k * 64 + lane, msk[k]));
+                w[k][0] = x.x; w[k][1] = x.y; w[k][2] = x.z; w[k][3] = x.w;
+            }
+            bool const prodLive = __any(p.prod != 0.0);   // wave-uniform
+#pragma unroll
+            for (int k = 0; k < U; ++k)
+                item8(w[k], msk[k], st * (64 * U) + k * 64 + lane, prodLive);
+            flushStep();
+        }
+        for (uint64_t it = steps * (64 * U) + wave * 64 + lane; it < h.items; it += waves * 64)
+        {
+            uint32_t w[4], m;
+            u32x4 const x = loadVec<u32x4, true>(h.data + 2 * spanVoxelMask<CONTIG>(h, it, m));
+            w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w;
+            item8(w, m, it, true);
+            flushStep();
+        }
+        momentBlockReduce<kBlock / 64>(p);
+        if (threadIdx.x == 0)
+            partials[blockIdx.x] = p;
+    }
+
+    // One workgroup: the n partials of aggregatesMomentsU16Kernel (thread t combines t, t + 256,
+    // ... in order, then the fixed tree) -> res[0] (pass-1 fields) and res[1].sumSq = S with
+    // res[1].count = 1 (the result is complete: no fallback).  numElems: voxels of the WHOLE
+    // volume (the reference divides by it, Aggregates_serial.hpp:61-63).
+    __global__ __launch_bounds__(kBlock) void aggregatesMomentsU16FinalKernel(MomentPartialU16 const* partials,
+                                                                             uint32_t n, double numElems,
+                                                                             vktHipAggregatePartial_t* res)
+    {
+        MomentPartialU16 p;
+        p.count = p.sumC = p.sumSqLo = p.sumSqHi = 0;
+        p.prod = 1.0;
+        p.cmin = 0x10000u;
+        p.cmax = -1;
+        p.minIndex = p.maxIndex = kNoIndex;
+        for (uint32_t i = threadIdx.x; i < n; i += kBlock)
+            momentCombine(p, partials[i]);
+        momentBlockReduce<kBlock / 64>(p);
+        if (threadIdx.x != 0)
+            return;
+        vktHipAggregatePartial_t one = emptyPartial();
+        one.count = p.count;
+        one.sum = static_cast<double>(p.sumC) * 0x1p-16;   // exact (Sc < 2^53)
+        one.prod = p.prod;
+        if (p.cmin <= 0xFFFFu)
+        {
+            one.minValue = static_cast<float>(p.cmin) * 0x1p-16f;
+            one.minIndex = p.minIndex;
+        }
+        if (p.cmax >= 0)
+        {
+            one.maxValue = static_cast<float>(p.cmax) * 0x1p-16f;
+            one.maxIndex = p.maxIndex;
+        }
+        // the reference's float mean (Aggregates_serial.hpp:61-63, as vktHipAggregatesFinish)
+        float const m = static_cast<float>(static_cast<double>(static_cast<float>(one.sum)) / numElems);
+        double const mu = static_cast<double>(m) * 65536.0;
+        unsigned __int128 const sc2 = (static_cast<unsigned __int128>(p.sumSqHi) << 64) | p.sumSqLo;
+        unsigned __int128 const t = static_cast<unsigned __int128>(p.count) * sc2 -
+                                    static_cast<unsigned __int128>(p.sumC) * p.sumC;   // n Sc2 - Sc^2 >= 0
+        double const td = static_cast<double>(static_cast<uint64_t>(t >> 64)) * 0x1p64 +
+                          static_cast<double>(static_cast<uint64_t>(t));
+        double const dn = static_cast<double>(p.count);
+        double const r = fma(-dn, mu, static_cast<double>(p.sumC));   // Sc - n mu, one rounding
+        vktHipAggregatePartial_t two = emptyPartial();
+        two.sumSq = p.count ? (td + r * r) / dn * 0x1p-32 : 0.0;
+        two.count = 1u;
+        res[0] = one;
+        res[1] = two;
+    }
+
     // The first voxels of item `item` holding codes tmin / tmax, folded into *bMin / *bMax with
     // atomicMin (LDS or global).
     template <int BPV, bool CONTIG>
@@ -1971,6 +2235,28 @@ namespace hipk
         return true;
     }
 
+    // UInt16 under the unit mapping: ComputeAggregates from one pass of integer moments
+    // (aggregatesMomentsU16Kernel + its final kernel) into res[0], res[1]; 0 when the range does
+    // not take it, else the number of partials (scratch: that many MomentPartialU16).
+    // Knob aggregates.moments, bit 0.
+    unsigned momentGridU16(BoxArgs const& a, FastHistArgs& h, bool& contig)
+    {
+        if (a.fmt != codec::FmtUInt16 || !codec::isUnitMapping(a.lo, a.hi) ||
+            (rt::knob(rt::Knob::AggregatesMoments) & 1) == 0 || !makeSpanArgs(a, h, contig))
+            return 0;
+        return streamingGrid(h.items, 64u * 4u * (kBlock / 64), 8);
+    }
+
+    void launchMomentsU16(FastHistArgs const& h, bool contig, unsigned g, double numElems, MomentPartialU16* parts,
+                          vktHipAggregatePartial_t* res, hipStream_t s)
+    {
+        if (contig)
+            hipLaunchKernelGGL(aggregatesMomentsU16Kernel<true>, dim3(g), dim3(kBlock), 0, s, h, parts);
+        else
+            hipLaunchKernelGGL(aggregatesMomentsU16Kernel<false>, dim3(g), dim3(kBlock), 0, s, h, parts);
+        hipLaunchKernelGGL(aggregatesMomentsU16FinalKernel, dim3(1), dim3(kBlock), 0, s, parts, g, numElems, res);
+    }
+
     // Grid of the code-count pass (0 when the range does not take it): UInt8 32 KiB of counters
     // per workgroup, 4 per CU; UInt16 the packed-16 histogram's one 1024-thread workgroup per CU.
     // Knob aggregates.codes: bit 0 UInt8, bit 1 UInt16.
@@ -2110,10 +2396,42 @@ vktError vktHipAggregatesRange(vktHipVolumeView_t volume, vktVec3i_t first, vktV
     BoxArgs a{};
     vktError e;
     bool done = false;
-    unsigned const gc = makeBox(volume, first, last, 0, a, "vktHipAggregatesRange: invalid volume view", e)
-                            ? codeAggGrid(a)
-                            : 0u;
-    if (gc != 0)
+    bool const boxed = makeBox(volume, first, last, 0, a, "vktHipAggregatesRange: invalid volume view", e);
+    FastHistArgs hm;
+    bool contigM = false;
+    unsigned const gm = boxed ? momentGridU16(a, hm, contigM) : 0u;
+    unsigned const gc = boxed && gm == 0 ? codeAggGrid(a) : 0u;
+    if (gm != 0)
+    {
+        // UInt16, unit mapping: one pass of exact integer moments, complete (no fallback)
+        hipStream_t s = rt::computeStream();
+        AggScratch& sc = aggScratch();
+        size_t const bytes = 2 * sizeof(vktHipAggregatePartial_t) + static_cast<size_t>(gm) * sizeof(MomentPartialU16);
+        auto* res = static_cast<vktHipAggregatePartial_t*>(sc.dev.acquire(bytes, s));
+        if (!res)
+            return vktInvalidValue;
+        if (!sc.host && rt::check(hipHostMalloc(reinterpret_cast<void**>(&sc.host),
+                                                2 * sizeof(vktHipAggregatePartial_t)),
+                                  "hipHostMalloc") != vktNoError)
+        {
+            sc.dev.release(s);
+            return vktInvalidValue;
+        }
+        launchMomentsU16(hm, contigM, gm, static_cast<double>(numElems), reinterpret_cast<MomentPartialU16*>(res + 2),
+                         res, s);
+        e = rt::check(hipMemcpyAsync(sc.host, res, 2 * sizeof(vktHipAggregatePartial_t), hipMemcpyDeviceToHost, s),
+                      "hipMemcpyAsync(aggregates)");
+        sc.dev.release(s);
+        if (e != vktNoError)
+            return e;
+        VKT_HIP_TRY(hipStreamSynchronize(s));
+        if ((e = rt::finishLaunch("AggregatesRange_hip")) != vktNoError)
+            return e;
+        p1 = sc.host[0];
+        p2 = sc.host[1];
+        done = true;
+    }
+    else if (gc != 0)
     {
         // UInt8 / UInt16: one pass of code counts; the two float passes below only when the
         // counts cannot give the first occurrence of an extreme (aggregatesCodesFinalKernel)

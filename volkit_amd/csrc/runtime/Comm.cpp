@@ -15,9 +15,12 @@
 #include <dlfcn.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <type_traits>
 #include <vector>
 
@@ -41,6 +44,8 @@ namespace
         decltype(&::ncclSend) send = nullptr;
         decltype(&::ncclRecv) recv = nullptr;
         decltype(&::ncclGetErrorString) errorString = nullptr;
+        decltype(&::ncclCommGetAsyncError) getAsyncError = nullptr;   // optional (deadline only without it)
+        decltype(&::ncclCommAbort) abort = nullptr;
         bool ok = false;
     };
 
@@ -63,7 +68,8 @@ namespace
             r.ok = sym(r.getUniqueId, "ncclGetUniqueId") && sym(r.commInitRank, "ncclCommInitRank") &&
                    sym(r.commDestroy, "ncclCommDestroy") && sym(r.groupStart, "ncclGroupStart") &&
                    sym(r.groupEnd, "ncclGroupEnd") && sym(r.send, "ncclSend") && sym(r.recv, "ncclRecv") &&
-                   sym(r.errorString, "ncclGetErrorString");
+                   sym(r.errorString, "ncclGetErrorString") && sym(r.abort, "ncclCommAbort");
+            sym(r.getAsyncError, "ncclCommGetAsyncError");
         });
         return r;
     }
@@ -165,12 +171,64 @@ namespace comm
         return vktNoError;
     }
 
+    // Aborts the communicator after a failed / timed-out round (its kernels exit; every later
+    // call on it fails fast).
+    vktError abortComm(vktHipComm_t c, std::string const& why)
+    {
+        if (!c->aborted && c->comm != nullptr)
+            (void)rccl().abort(c->comm);
+        c->aborted = true;
+        c->comm = nullptr;
+        return rt::fail((why + " (communicator aborted)").c_str());
+    }
+
+    // Host wait for the round just enqueued on `stream`, under c->timeoutMs.
+    vktError waitRound(vktHipComm_t c, hipStream_t stream, char const* what)
+    {
+        hipEvent_t ev = nullptr;
+        VKT_HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        vktError e = rt::check(hipEventRecord(ev, stream), "hipEventRecord(rcclRound)");
+        auto const t0 = std::chrono::steady_clock::now();
+        for (uint32_t polls = 0; e == vktNoError; ++polls)
+        {
+            hipError_t const q = hipEventQuery(ev);
+            if (q == hipSuccess)
+                break;
+            if (q != hipErrorNotReady)
+            {
+                e = rt::check(q, what);
+                break;
+            }
+            ncclResult_t as = ncclSuccess;
+            if (rccl().getAsyncError != nullptr && rccl().getAsyncError(c->comm, &as) == ncclSuccess &&
+                as != ncclSuccess && as != ncclInProgress)
+            {
+                e = abortComm(c, std::string(what) + ": RCCL asynchronous error: " + rccl().errorString(as));
+                break;
+            }
+            auto const ms = std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0);
+            if (ms.count() >= c->timeoutMs)
+            {
+                e = abortComm(c, std::string(what) + ": a peer did not complete its side of the round within " +
+                                     std::to_string(c->timeoutMs) + " ms");
+                break;
+            }
+            // spin briefly (a halo round on xGMI takes tens of microseconds), then back off
+            if (polls > 256)
+                std::this_thread::sleep_for(std::chrono::microseconds(polls > 4096 ? 1000 : 50));
+        }
+        (void)hipEventDestroy(ev);
+        return e;
+    }
+
     vktError rcclRound(vktHipComm_t c, std::vector<Xfer> const& xs, hipStream_t stream, char const* what)
     {
         if (xs.empty())
             return vktNoError;
         if (!rccl().ok)
             return noRccl(what);
+        if (c->aborted)
+            return rt::fail((std::string(what) + ": the communicator was aborted after an earlier failure").c_str());
         ncclResult_t r = rccl().groupStart();
         if (r != ncclSuccess)
             return ncclFail((std::string(what) + ": ncclGroupStart").c_str(), r);
@@ -186,8 +244,8 @@ namespace comm
         }
         r = rccl().groupEnd();
         if (r != ncclSuccess)
-            return ncclFail((std::string(what) + ": ncclGroupEnd").c_str(), r);
-        return vktNoError;
+            return abortComm(c, std::string(what) + ": ncclGroupEnd: " + rccl().errorString(r));
+        return c->timeoutMs > 0 ? waitRound(c, stream, what) : vktNoError;
     }
 
     vktError localMove(uint8_t* dst, uint8_t const* src, size_t bytes, hipStream_t stream, char const* what)
@@ -258,7 +316,18 @@ vktError vktHipCommInitRank(vktHipComm_t* comm, int32_t nranks, vktHipCommId_t i
     }
     c->rank = rank;
     c->nranks = nranks;
+    // default round deadline: VKT_COMM_TIMEOUT_MS (0 = rounds return once enqueued), else 300 s
+    char const* env = std::getenv("VKT_COMM_TIMEOUT_MS");
+    c->timeoutMs = env != nullptr ? std::max<int64_t>(0, std::strtoll(env, nullptr, 10)) : 300000;
     *comm = c;
+    return vktNoError;
+}
+
+vktError vktHipCommSetTimeout(vktHipComm_t comm, int64_t milliseconds)
+{
+    if (comm == nullptr || milliseconds < 0)
+        return rt::fail("vktHipCommSetTimeout: null communicator or negative timeout");
+    comm->timeoutMs = milliseconds;
     return vktNoError;
 }
 
@@ -266,7 +335,7 @@ vktError vktHipCommDestroy(vktHipComm_t comm)
 {
     if (comm == nullptr)
         return vktNoError;
-    ncclResult_t const r = rccl().commDestroy(comm->comm);
+    ncclResult_t const r = comm->aborted ? ncclSuccess : rccl().commDestroy(comm->comm);
     delete comm;
     return r == ncclSuccess ? vktNoError : ncclFail("vktHipCommDestroy", r);
 }

@@ -15,6 +15,10 @@ struct vktHipComm_impl
 {
     ncclComm_t comm = nullptr;
     int32_t rank = 0, nranks = 0;
+    // rcclRound waits (host) up to timeoutMs for each round, polling ncclCommGetAsyncError;
+    // 0: returns once the round is enqueued (vktHipCommSetTimeout, VKT_COMM_TIMEOUT_MS)
+    int64_t timeoutMs = 0;
+    bool aborted = false;   // a round failed or timed out: the communicator was aborted
 };
 
 namespace vkt
@@ -42,7 +46,10 @@ namespace comm
     };
 
     // The moves as ONE ncclGroupStart .. ncclGroupEnd round of ncclSend / ncclRecv on `stream`
-    // (pairs of ranks match their moves in issue order).
+    // (pairs of ranks match their moves in issue order).  With comm->timeoutMs > 0 the host then
+    // waits for the round under that deadline, polling ncclCommGetAsyncError: a peer that never
+    // joins, or an asynchronous RCCL error, aborts the communicator and returns vktInvalidValue
+    // instead of leaving every later call on the stream hanging (SURVEY §5 failure detection).
     vktError rcclRound(vktHipComm_t comm, std::vector<Xfer> const& xs, hipStream_t stream, char const* what);
 
     // A device-to-device copy on `stream` (the in-process transport: every slab of a

@@ -210,6 +210,8 @@ namespace rt
             {"decompose.grid", 1},
             {"memory.pool", 1},
             {"memory.arena", 1},
+            {"aggregates.moments", 1},
+            {"memory.arena_chunk_mib", 0},
         };
         static_assert(sizeof(kKnobs) / sizeof(kKnobs[0]) == static_cast<size_t>(Knob::Count), "knob table");
         std::atomic<int64_t> gKnobs[static_cast<int>(Knob::Count)] = {{kKnobs[0].def}, {kKnobs[1].def},
@@ -221,7 +223,8 @@ namespace rt
                                                                   {kKnobs[12].def}, {kKnobs[13].def},
                                                                   {kKnobs[14].def}, {kKnobs[15].def},
                                                                   {kKnobs[16].def}, {kKnobs[17].def},
-                                                                  {kKnobs[18].def}, {kKnobs[19].def}};
+                                                                  {kKnobs[18].def}, {kKnobs[19].def},
+                                                                  {kKnobs[20].def}, {kKnobs[21].def}};
     } // namespace
 
     int64_t knob(Knob k) { return gKnobs[static_cast<int>(k)].load(std::memory_order_relaxed); }
@@ -302,14 +305,37 @@ vktError vktHipGetAsyncExecution(int32_t* async)
     return vktNoError;
 }
 
+namespace
+{
+    // Work queued on the stream being replaced stays ordered before everything queued on its
+    // successor (the successor waits for the old tail): the library's later calls, its allocator's
+    // reuse of freed buffers (runtime/Memory.cpp drains on the current streams) and a context
+    // destroying the old stream all see it finished.
+    vktError chainStreams(hipStream_t from, hipStream_t to)
+    {
+        if (from == to)
+            return vktNoError;
+        hipEvent_t ev = nullptr;
+        VKT_HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        vktError e = rt::check(hipEventRecord(ev, from), "hipEventRecord(stream switch)");
+        if (e == vktNoError)
+            e = rt::check(hipStreamWaitEvent(to, ev, 0), "hipStreamWaitEvent(stream switch)");
+        (void)hipEventDestroy(ev);
+        return e;
+    }
+} // namespace
+
 vktError vktHipSetComputeStream(void* stream)
 {
     rt::Context& c = rt::ctx();
     std::lock_guard<std::mutex> lock(c.mutex);
     rt::initLocked(c);
+    hipStream_t const old = c.userStreamSet ? c.userCompute : c.ownCompute;
+    hipStream_t const next = stream != nullptr ? static_cast<hipStream_t>(stream) : c.ownCompute;
+    vktError const e = chainStreams(old, next);
     c.userCompute = static_cast<hipStream_t>(stream);
     c.userStreamSet = stream != nullptr;
-    return vktNoError;
+    return e;
 }
 
 vktError vktHipGetComputeStream(void** stream)
@@ -325,9 +351,12 @@ vktError vktHipSetCopyStream(void* stream)
     rt::Context& c = rt::ctx();
     std::lock_guard<std::mutex> lock(c.mutex);
     rt::initLocked(c);
+    hipStream_t const old = c.userCopySet ? c.userCopy : c.copy;
+    hipStream_t const next = stream != nullptr ? static_cast<hipStream_t>(stream) : c.copy;
+    vktError const e = chainStreams(old, next);
     c.userCopy = static_cast<hipStream_t>(stream);
     c.userCopySet = stream != nullptr;
-    return vktNoError;
+    return e;
 }
 
 vktError vktHipGetCopyStream(void** stream)
@@ -437,15 +466,37 @@ namespace
         return e != vktNoError ? e : vktHipSetCopyStream(c->streams[static_cast<size_t>(c->copy)]);
     }
 
+    vktError changed(vktHipContext c);
+
+    // Destroys an owned stream the context no longer uses: when the context is current it is
+    // first unbound (the backend rebound to the context's remaining ids, which also orders its
+    // queued work before theirs) and synchronised, so no caller enqueues on a destroyed handle
+    // (ADVICE r3).
+    vktError retire(hipStream_t s, bool owned)
+    {
+        if (!owned)
+            return vktNoError;
+        VKT_HIP_TRY(hipStreamSynchronize(s));
+        VKT_HIP_TRY(hipStreamDestroy(s));
+        return vktNoError;
+    }
+
     vktError resize(vktHipContext c, int32_t n)
     {
         (void)vkt::rt::device();   // streams of the library's device
-        while (static_cast<int32_t>(c->streams.size()) > n)
+        if (static_cast<int32_t>(c->streams.size()) > n)
         {
-            if (c->owned.back())
-                VKT_HIP_TRY(hipStreamDestroy(c->streams.back()));
-            c->streams.pop_back();
-            c->owned.pop_back();
+            std::vector<hipStream_t> doomed(c->streams.begin() + n, c->streams.end());
+            std::vector<char> owned(c->owned.begin() + n, c->owned.end());
+            c->compute = std::min(c->compute, n - 1);
+            c->copy = std::min(c->copy, n - 1);
+            vktError e = changed(c);   // rebind to surviving streams first
+            for (size_t i = 0; i < doomed.size() && e == vktNoError; ++i)
+                e = retire(doomed[i], owned[i] != 0);
+            c->streams.resize(static_cast<size_t>(n));
+            c->owned.resize(static_cast<size_t>(n));
+            if (e != vktNoError)
+                return e;
         }
         while (static_cast<int32_t>(c->streams.size()) < n)
         {
@@ -557,11 +608,13 @@ vktError vktHipContextSetStream(vktHipContext context, int32_t streamId, void* s
         return rt::fail("vktHipContextSetStream: null context / stream or stream id out of range");
     std::lock_guard<std::mutex> lock(gCtxMutex);
     size_t const i = static_cast<size_t>(streamId);
-    if (context->owned[i])
-        VKT_HIP_TRY(hipStreamDestroy(context->streams[i]));
+    hipStream_t const old = context->streams[i];
+    bool const owned = context->owned[i] != 0;
     context->streams[i] = static_cast<hipStream_t>(stream);
     context->owned[i] = 0;   // the caller's stream: not destroyed by the context
-    return changed(context);
+    vktError const e = changed(context);   // rebind (current context) before the old one goes
+    vktError const r = old != context->streams[i] ? retire(old, owned) : vktNoError;
+    return e != vktNoError ? e : r;
 }
 
 vktError vktHipContextGetStream(vktHipContext context, int32_t streamId, void** stream)

@@ -16,6 +16,7 @@
 #include "Runtime.hpp"
 #include "volkit_hip.h"
 
+#include <algorithm>
 #include <atomic>
 #include <cstdlib>
 #include <cstring>
@@ -48,141 +49,88 @@ namespace
         return *s;
     }
 
-    // Small device allocations (<= kPoolMax bytes: bricks, lookup tables, small volumes) come from
-    // 64-MiB hipMalloc chunks in 256-B size classes instead of one hipMalloc each: a
-    // BrickDecomposeResize of a 1024^3 volume into 16^3 bricks makes 262 144 allocations.  Freed
-    // blocks wait on a pending list; the first allocation that would reuse one synchronises the
-    // device once for the whole batch (the guarantee hipFree gave: no kernel or copy still uses
-    // the block), then serves them.  Chunks are kept for the process (like a caching allocator);
-    // knob memory.pool = 0 allocates every buffer with hipMalloc.
+    // ---- device heap: the library's caching allocator for GPU buffers ----------------------
+    // Small buffers (<= kPoolMax bytes: bricks, lookup tables, small volumes) come from 64-MiB
+    // pool chunks in 256-B size classes instead of one hipMalloc each: a BrickDecomposeResize of a
+    // 1024^3 volume into 16^3 bricks makes 262 144 allocations.  Larger buffers are carved
+    // first-fit, 2-MiB aligned, from arena chunks: a 1024^3 UInt16 SumRange over three separately
+    // allocated volumes ran in one of two placement states (0.98-1.00 ms or 1.04-1.07 ms, ~40 % of
+    // allocations), over three volumes carved from one block at 0.99-1.01 ms every time
+    // (tools/alloc_probe.py).  An arena chunk is sized for a group of like buffers
+    // (kArenaGroup times the request: the src / dst / operand volumes of one pipeline land in one
+    // chunk), at least kArenaMin, growing geometrically (twice the previous chunk, up to
+    // kArenaGrowCap) for runs of smaller buffers, and never more than 3/4 of the device's free
+    // memory beyond the request -- a 5 MiB buffer reserves 64 MiB, not a 16-GiB chunk.
+    // Freed blocks are not reusable at once (a queued kernel or copy may still use them): they
+    // wait on a pending list until a drain records one event on each of the library's streams
+    // (compute, copy) and waits for the two -- the guarantee hipFree gave, without stalling
+    // torch's or RCCL's streams as a hipDeviceSynchronize did.  A pool allocation drains when a
+    // pending block of its class exists; an arena allocation when nothing fits; a free that
+    // leaves an arena chunk without live blocks drains and returns the chunk to HIP.  Pool chunks
+    // are cached; vktHipReleaseCachedMemory (and any allocation that fails) drains and releases
+    // every empty chunk.  Knobs: memory.pool / memory.arena = 0 give those buffers their own
+    // hipMalloc; memory.arena_chunk_mib (tests) fixes the arena chunk size.
     constexpr std::size_t kPoolMax = 4u << 20;
     constexpr std::size_t kPoolChunk = 64u << 20;
     constexpr std::size_t kPoolAlign = 256;
-
-    struct DevicePool
-    {
-        std::unordered_map<std::size_t, std::vector<void*>> freeBlocks;   // by class
-        std::unordered_map<std::size_t, std::vector<void*>> pending;      // by class: freed, not yet synchronised
-        char* bump = nullptr;
-        std::size_t left = 0;
-    };
-
-    struct Pools
-    {
-        std::mutex m;
-        std::unordered_map<int, DevicePool> byDevice;
-        std::unordered_map<void*, std::pair<int, std::size_t>> owner;   // block -> (device, class)
-    };
-
-    Pools& pools()
-    {
-        static auto* p = new Pools;   // (never destroyed: frees may run during static destruction)
-        return *p;
-    }
-
-    void* poolAllocate(std::size_t bytes)
-    {
-        std::size_t const cls = (bytes + kPoolAlign - 1) / kPoolAlign * kPoolAlign;
-        int const dev = rt::device();
-        Pools& P = pools();
-        std::lock_guard<std::mutex> lock(P.m);
-        DevicePool& d = P.byDevice[dev];
-        auto reuse = [&]() -> void* {
-            auto it = d.freeBlocks.find(cls);
-            if (it == d.freeBlocks.end() || it->second.empty())
-                return nullptr;
-            void* b = it->second.back();
-            it->second.pop_back();
-            return b;
-        };
-        void* b = reuse();
-        auto mine = d.pending.find(cls);
-        if (!b && mine != d.pending.end() && !mine->second.empty() &&
-            rt::check(hipDeviceSynchronize(), "hipDeviceSynchronize(pool)") == vktNoError)
-        {
-            for (auto& q : d.pending)   // every class: the one synchronisation covers them all
-            {
-                auto& f = d.freeBlocks[q.first];
-                f.insert(f.end(), q.second.begin(), q.second.end());
-                q.second.clear();
-            }
-            b = reuse();
-        }
-        if (!b)
-        {
-            if (d.left < cls)
-            {
-                void* c = nullptr;
-                if (rt::check(hipMalloc(&c, kPoolChunk), "hipMalloc(pool chunk)") != vktNoError)
-                    return nullptr;
-                d.bump = static_cast<char*>(c);
-                d.left = kPoolChunk;
-            }
-            b = d.bump;
-            d.bump += cls;
-            d.left -= cls;
-        }
-        P.owner[b] = {dev, cls};
-        return b;
-    }
-
-    // true when p is a pool block (then it is queued for reuse)
-    bool poolFree(void* p)
-    {
-        Pools& P = pools();
-        std::lock_guard<std::mutex> lock(P.m);
-        auto it = P.owner.find(p);
-        if (it == P.owner.end())
-            return false;
-        P.byDevice[it->second.first].pending[it->second.second].push_back(p);
-        P.owner.erase(it);
-        return true;
-    }
-
-    // Large device buffers (> kPoolMax) are carved first-fit from arena chunks of at least
-    // kArenaChunk bytes, 2-MiB aligned, instead of one hipMalloc each: a 1024^3 UInt16 SumRange
-    // over three separately allocated volumes ran in one of two placement states (0.98-1.00 ms or
-    // 1.04-1.07 ms, ~40 % of allocations), over three volumes carved from one block at 0.99-1.01 ms
-    // every time (tools/alloc_probe.py).  Freed blocks wait on a pending list; an
-    // allocation that finds no room synchronises the device once, returns them (coalescing) and
-    // releases chunks left empty (hipFree), then retries; a chunk that cannot be allocated falls
-    // back to a plain hipMalloc of the request.  Knob memory.arena = 0: one hipMalloc per buffer.
-    constexpr std::size_t kArenaChunk = std::size_t(16) << 30;
     constexpr std::size_t kArenaAlign = std::size_t(2) << 20;
+    constexpr std::size_t kArenaMin = std::size_t(64) << 20;
+    constexpr std::size_t kArenaGroup = 4;
+    constexpr std::size_t kArenaGrowCap = std::size_t(1) << 30;
+
+    struct PoolChunk
+    {
+        char* base = nullptr;
+        std::size_t bump = 0;   // bytes handed out from the start (never given back but by release)
+        std::size_t live = 0;   // blocks currently allocated (not freed)
+    };
 
     struct ArenaChunk
     {
         char* base = nullptr;
-        std::size_t size = 0, used = 0;
+        std::size_t size = 0, used = 0;             // used: carved bytes (live + pending)
+        std::size_t live = 0;                        // live bytes (not freed)
         std::map<std::size_t, std::size_t> holes;   // offset -> length, coalesced
     };
 
-    struct ArenaBlock
+    struct HeapBlock
     {
-        ArenaChunk* chunk;
-        std::size_t off, len;
+        int dev;
+        bool arena;
+        std::size_t len;   // pool: class; arena: carved length
+        PoolChunk* pc;
+        ArenaChunk* ac;
+        std::size_t off;
     };
 
-    struct Arenas
+    struct DeviceHeap
+    {
+        std::vector<PoolChunk*> poolChunks;
+        std::unordered_map<std::size_t, std::vector<std::pair<void*, PoolChunk*>>> poolFree;   // by class
+        std::unordered_map<std::size_t, std::size_t> pendingByClass;    // pool classes on the pending list
+        std::vector<ArenaChunk*> arenaChunks;
+        std::size_t lastArenaChunk = 0;
+        std::vector<void*> pending;   // freed, not yet known idle
+        hipEvent_t evCompute = nullptr, evCopy = nullptr;
+    };
+
+    struct Heaps
     {
         std::mutex m;
-        std::unordered_map<int, std::vector<ArenaChunk*>> chunks;
-        std::unordered_map<int, std::vector<ArenaBlock>> pending;
-        std::unordered_map<void*, std::pair<int, ArenaBlock>> owner;
+        std::unordered_map<int, DeviceHeap> byDevice;
+        std::unordered_map<void*, HeapBlock> owner;   // live and pending blocks
     };
 
-    Arenas& arenas()
+    Heaps& heaps()
     {
-        static auto* a = new Arenas;   // (never destroyed: frees may run during static destruction)
-        return *a;
+        static auto* h = new Heaps;   // (never destroyed: frees may run during static destruction)
+        return *h;
     }
 
-    void arenaRelease(ArenaBlock const& b)
+    void arenaRelease(ArenaChunk& c, std::size_t off, std::size_t len)
     {
-        ArenaChunk& c = *b.chunk;
-        c.used -= b.len;
-        auto next = c.holes.lower_bound(b.off);
-        std::size_t off = b.off, len = b.len;
+        c.used -= len;
+        auto next = c.holes.lower_bound(off);
         if (next != c.holes.begin())
         {
             auto prev = std::prev(next);
@@ -201,9 +149,146 @@ namespace
         c.holes[off] = len;
     }
 
-    void* arenaCarve(std::vector<ArenaChunk*>& list, std::size_t len, int dev, Arenas& A)
+    // Waits until no queued work of the library's streams can use a pending block, then makes
+    // them reusable (H.m held).  Blocks of another device than the context's: a device
+    // synchronisation of that device (rare).
+    void drain(DeviceHeap& d, int dev, Heaps& H)
     {
-        for (ArenaChunk* c : list)
+        if (d.pending.empty())
+            return;
+        bool idle = false;
+        if (dev == rt::device())
+        {
+            if (!d.evCompute && (hipEventCreateWithFlags(&d.evCompute, hipEventDisableTiming) != hipSuccess ||
+                                 hipEventCreateWithFlags(&d.evCopy, hipEventDisableTiming) != hipSuccess))
+                (void)hipGetLastError();
+            idle = d.evCopy && hipEventRecord(d.evCompute, rt::computeStream()) == hipSuccess &&
+                   hipEventRecord(d.evCopy, rt::copyStream()) == hipSuccess &&
+                   hipEventSynchronize(d.evCompute) == hipSuccess && hipEventSynchronize(d.evCopy) == hipSuccess;
+        }
+        if (!idle)
+        {
+            int cur = 0;
+            idle = hipGetDevice(&cur) == hipSuccess && hipSetDevice(dev) == hipSuccess &&
+                   hipDeviceSynchronize() == hipSuccess;
+            (void)hipSetDevice(cur);
+        }
+        if (!idle)
+        {
+            (void)hipGetLastError();
+            return;   // keep them pending: never hand out a block that may still be in use
+        }
+        for (void* p : d.pending)
+        {
+            auto it = H.owner.find(p);
+            HeapBlock const b = it->second;
+            H.owner.erase(it);
+            if (b.arena)
+                arenaRelease(*b.ac, b.off, b.len);
+            else
+                d.poolFree[b.len].push_back({p, b.pc});
+        }
+        d.pending.clear();
+        d.pendingByClass.clear();
+    }
+
+    // Returns arena chunks without carved blocks to HIP; with `pools`, also pool chunks without
+    // live blocks (their free blocks leave the class lists).  Bytes released.
+    std::size_t releaseEmpty(DeviceHeap& d, bool pools)
+    {
+        std::size_t freed = 0;
+        for (auto it = d.arenaChunks.begin(); it != d.arenaChunks.end();)
+            if ((*it)->used == 0)
+            {
+                (void)hipFree((*it)->base);
+                freed += (*it)->size;
+                delete *it;
+                it = d.arenaChunks.erase(it);
+            }
+            else
+                ++it;
+        if (!pools)
+            return freed;
+        std::vector<PoolChunk*> keep, gone;
+        for (PoolChunk* c : d.poolChunks)
+            (c->live == 0 && d.pendingByClass.empty() ? gone : keep).push_back(c);
+        if (gone.empty())
+            return freed;
+        auto inGone = [&](std::pair<void*, PoolChunk*> const& f) {
+            return std::find(gone.begin(), gone.end(), f.second) != gone.end();
+        };
+        for (auto& f : d.poolFree)
+            f.second.erase(std::remove_if(f.second.begin(), f.second.end(), inGone), f.second.end());
+        for (PoolChunk* c : gone)
+        {
+            (void)hipFree(c->base);
+            freed += kPoolChunk;
+            delete c;
+        }
+        d.poolChunks = keep;
+        return freed;
+    }
+
+    // hipMalloc; on failure drain + release every empty chunk of the device, then once more
+    void* deviceMalloc(std::size_t bytes, DeviceHeap& d, int dev, Heaps& H, bool quiet)
+    {
+        void* p = nullptr;
+        if (hipMalloc(&p, bytes) == hipSuccess)
+            return p;
+        (void)hipGetLastError();
+        drain(d, dev, H);
+        releaseEmpty(d, true);
+        if (hipMalloc(&p, bytes) == hipSuccess)
+            return p;
+        if (quiet)
+            (void)hipGetLastError();
+        else
+            (void)rt::check(hipErrorOutOfMemory, "hipMalloc");
+        return nullptr;
+    }
+
+    void* poolAllocate(std::size_t bytes, DeviceHeap& d, int dev, Heaps& H)
+    {
+        std::size_t const cls = (bytes + kPoolAlign - 1) / kPoolAlign * kPoolAlign;
+        PoolChunk* pc = nullptr;
+        auto reuse = [&]() -> void* {
+            auto it = d.poolFree.find(cls);
+            if (it == d.poolFree.end() || it->second.empty())
+                return nullptr;
+            auto const f = it->second.back();
+            it->second.pop_back();
+            pc = f.second;
+            return f.first;
+        };
+        void* b = reuse();
+        if (!b && d.pendingByClass.count(cls))
+        {
+            drain(d, dev, H);   // one wait covers every pending block of every class
+            b = reuse();
+        }
+        if (!b)
+        {
+            pc = d.poolChunks.empty() ? nullptr : d.poolChunks.back();
+            if (!pc || kPoolChunk - pc->bump < cls)
+            {
+                void* base = deviceMalloc(kPoolChunk, d, dev, H, false);
+                if (!base)
+                    return nullptr;
+                pc = new PoolChunk;
+                pc->base = static_cast<char*>(base);
+                d.poolChunks.push_back(pc);
+            }
+            b = pc->base + pc->bump;
+            pc->bump += cls;
+        }
+        pc->live += 1;
+        H.owner[b] = HeapBlock{dev, false, cls, pc, nullptr, 0};
+        return b;
+    }
+
+    void* arenaCarve(DeviceHeap& d, std::size_t len, int dev, Heaps& H)
+    {
+        for (ArenaChunk* c : d.arenaChunks)
             for (auto it = c->holes.begin(); it != c->holes.end(); ++it)
                 if (it->second >= len)
                 {
@@ -212,66 +297,116 @@ namespace
                     if (rest > 0)
                         c->holes[off + len] = rest;
                     c->used += len;
+                    c->live += len;
                     void* p = c->base + off;
-                    A.owner[p] = {dev, ArenaBlock{c, off, len}};
+                    H.owner[p] = HeapBlock{dev, true, len, nullptr, c, off};
                     return p;
                 }
         return nullptr;
     }
 
+    // size of a new arena chunk for a request of len bytes (see above)
+    std::size_t arenaChunkSize(DeviceHeap const& d, std::size_t len)
+    {
+        int64_t const fixed = rt::knob(rt::Knob::MemoryArenaChunkMiB);
+        if (fixed > 0)
+            return std::max(len, static_cast<std::size_t>(fixed) << 20);
+        std::size_t want = std::max(kArenaMin, kArenaGroup * len);
+        want = std::max(want, std::min(2 * d.lastArenaChunk, kArenaGrowCap));
+        std::size_t freeB = 0, totalB = 0;
+        if (want > len && hipMemGetInfo(&freeB, &totalB) == hipSuccess && freeB > len)
+            want = std::min(want, len + (freeB - len) / 4 * 3);
+        else
+            (void)hipGetLastError();
+        return (std::max(want, len) + kArenaAlign - 1) / kArenaAlign * kArenaAlign;
+    }
+
     // nullptr: the caller allocates the buffer with its own hipMalloc
-    void* arenaAllocate(std::size_t bytes)
+    void* arenaAllocate(std::size_t bytes, DeviceHeap& d, int dev, Heaps& H)
     {
         std::size_t const len = (bytes + kArenaAlign - 1) / kArenaAlign * kArenaAlign;
-        int const dev = rt::device();
-        Arenas& A = arenas();
-        std::lock_guard<std::mutex> lock(A.m);
-        std::vector<ArenaChunk*>& list = A.chunks[dev];
-        if (void* p = arenaCarve(list, len, dev, A))
+        if (void* p = arenaCarve(d, len, dev, H))
             return p;
-        std::vector<ArenaBlock>& pend = A.pending[dev];
-        if (!pend.empty() && hipDeviceSynchronize() == hipSuccess)
+        if (!d.pending.empty())
         {
-            for (ArenaBlock const& b : pend)
-                arenaRelease(b);
-            pend.clear();
-            for (auto it = list.begin(); it != list.end();)
-                if ((*it)->used == 0)
-                {
-                    (void)hipFree((*it)->base);
-                    delete *it;
-                    it = list.erase(it);
-                }
-                else
-                    ++it;
-            if (void* p = arenaCarve(list, len, dev, A))
+            drain(d, dev, H);
+            releaseEmpty(d, false);
+            if (void* p = arenaCarve(d, len, dev, H))
                 return p;
         }
-        std::size_t const size = len > kArenaChunk ? len : kArenaChunk;
+        std::size_t size = arenaChunkSize(d, len);
         void* base = nullptr;
         if (hipMalloc(&base, size) != hipSuccess)
         {
-            (void)hipGetLastError();   // (the request alone may still fit: plain hipMalloc)
-            return nullptr;
+            (void)hipGetLastError();
+            size = len;   // the group does not fit: a chunk of the request alone
+            if (!(base = deviceMalloc(size, d, dev, H, true)))
+                return nullptr;
         }
         auto* c = new ArenaChunk;
         c->base = static_cast<char*>(base);
         c->size = size;
         c->holes[0] = size;
-        list.push_back(c);
-        return arenaCarve(list, len, dev, A);
+        d.arenaChunks.push_back(c);
+        d.lastArenaChunk = size;
+        return arenaCarve(d, len, dev, H);
     }
 
-    bool arenaFree(void* p)
+    void* heapAllocate(std::size_t bytes)
     {
-        Arenas& A = arenas();
-        std::lock_guard<std::mutex> lock(A.m);
-        auto it = A.owner.find(p);
-        if (it == A.owner.end())
+        int const dev = rt::device();
+        Heaps& H = heaps();
+        std::lock_guard<std::mutex> lock(H.m);
+        DeviceHeap& d = H.byDevice[dev];
+        if (bytes <= kPoolMax && rt::knob(rt::Knob::MemoryPool) != 0)
+            return poolAllocate(bytes, d, dev, H);
+        if (bytes > kPoolMax && rt::knob(rt::Knob::MemoryArena) != 0)
+            if (void* p = arenaAllocate(bytes, d, dev, H))
+                return p;
+        return deviceMalloc(bytes, d, dev, H, false);   // a plain buffer (freed with hipFree)
+    }
+
+    // true when p is a heap block (then it is queued for reuse)
+    bool heapFree(void* p)
+    {
+        Heaps& H = heaps();
+        std::lock_guard<std::mutex> lock(H.m);
+        auto it = H.owner.find(p);
+        if (it == H.owner.end())
             return false;
-        A.pending[it->second.first].push_back(it->second.second);
-        A.owner.erase(it);
+        HeapBlock const& b = it->second;
+        DeviceHeap& d = H.byDevice[b.dev];
+        d.pending.push_back(p);
+        if (b.arena)
+        {
+            b.ac->live -= b.len;
+            if (b.ac->live == 0)
+            {
+                // the chunk's last live block: drain now and give the chunk back to HIP
+                int const dev = b.dev;
+                drain(d, dev, H);
+                releaseEmpty(d, false);
+            }
+        }
+        else
+        {
+            b.pc->live -= 1;
+            d.pendingByClass[b.len] += 1;
+        }
         return true;
+    }
+
+    std::size_t heapReleaseCached()
+    {
+        Heaps& H = heaps();
+        std::lock_guard<std::mutex> lock(H.m);
+        std::size_t freed = 0;
+        for (auto& kv : H.byDevice)
+        {
+            drain(kv.second, kv.first, H);
+            freed += releaseEmpty(kv.second, true);
+        }
+        return freed;
     }
 
 } // namespace
@@ -318,15 +453,7 @@ namespace detail
         if (onGpu(owner))
         {
             (void)rt::device();   // bind the context's device before allocating
-            if (bytes <= kPoolMax && rt::knob(rt::Knob::MemoryPool) != 0)
-                return poolAllocate(bytes);
-            if (bytes > kPoolMax && rt::knob(rt::Knob::MemoryArena) != 0)
-                if (void* a = arenaAllocate(bytes))
-                    return a;
-            void* p = nullptr;
-            if (rt::check(hipMalloc(&p, bytes), "hipMalloc") != vktNoError)
-                return nullptr;
-            return p;
+            return heapAllocate(bytes);
         }
         if (gPinnedHost.load())
         {
@@ -350,7 +477,7 @@ namespace detail
             return;
         if (onGpu(owner))
         {
-            if (!poolFree(data) && !arenaFree(data))
+            if (!heapFree(data))
                 (void)rt::check(hipFree(data), "hipFree");
             return;
         }
@@ -471,9 +598,17 @@ vktError vktHipFree(void* ptr)
 {
     if (ptr == nullptr)
         return vktNoError;
-    if (vkt::poolFree(ptr) || vkt::arenaFree(ptr))
+    if (vkt::heapFree(ptr))
         return vktNoError;
     return vkt::rt::check(hipFree(ptr), "hipFree");
+}
+
+vktError vktHipReleaseCachedMemory(size_t* releasedBytes)
+{
+    std::size_t const n = vkt::heapReleaseCached();
+    if (releasedBytes != nullptr)
+        *releasedBytes = n;
+    return vktNoError;
 }
 
 vktError vktHipMemcpy(void* dst, void const* src, size_t size, vktCopyKind ck)

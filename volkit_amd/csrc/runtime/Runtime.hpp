@@ -94,6 +94,8 @@ namespace rt
         DecomposeGrid,                 // 0: uniform brick grids keep the per-brick descriptor table
         MemoryPool,                    // 0: every device buffer from its own hipMalloc (no small-block pool)
         MemoryArena,                   // 0: buffers > 4 MiB from their own hipMalloc (no arena chunks)
+        AggregatesMoments,             // bit 0: UInt16 unit-mapping ComputeAggregates from one pass of integer moments
+        MemoryArenaChunkMiB,           // > 0: arena chunks of exactly max(request, this many MiB) (tests)
         Count
     };
     int64_t knob(Knob k);

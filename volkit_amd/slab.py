@@ -152,12 +152,40 @@ def start_exchange(plan: ResamplePlan, planes: Callable[[int, int], "torch.Tenso
     return (dist.batch_isend_irecv(ops) if ops else [], landing)
 
 
+_EXCHANGE_TIMEOUT_S = None
+
+
+def set_exchange_timeout(seconds) -> None:
+    """Bound every wait of an exchange round (finish_exchange, the Range calls' moves) to
+    `seconds` (None: the backend's default -- the process group's timeout for gloo; a
+    stream-ordered wait for nccl).  A peer that never joins its side of a round then raises
+    RuntimeError on the waiting rank instead of hanging it (SURVEY §5 failure detection; with
+    nccl the wait also blocks the host until the receives land or the deadline passes)."""
+    global _EXCHANGE_TIMEOUT_S
+    _EXCHANGE_TIMEOUT_S = None if seconds is None else float(seconds)
+
+
+def _wait(req) -> None:
+    if _EXCHANGE_TIMEOUT_S is None:
+        req.wait()
+        return
+    import datetime
+    try:
+        ok = req.wait(datetime.timedelta(seconds=_EXCHANGE_TIMEOUT_S))
+    except RuntimeError as e:
+        raise RuntimeError(f"slab exchange: a peer did not complete its side within {_EXCHANGE_TIMEOUT_S} s: "
+                           f"{e}") from e
+    if ok is False:
+        raise RuntimeError(f"slab exchange: a peer did not complete its side within {_EXCHANGE_TIMEOUT_S} s")
+
+
 def finish_exchange(pending) -> None:
     """Wait for a round from start_exchange: with RCCL the current stream waits for the
-    receives (the host does not block), so a kernel enqueued next reads the halo."""
+    receives (the host does not block unless set_exchange_timeout bounds the wait), so a kernel
+    enqueued next reads the halo."""
     reqs, landing = pending
     for req in reqs:
-        req.wait()
+        _wait(req)
     for dev, host in landing:
         dev.copy_(host)
 
