@@ -155,6 +155,28 @@ def test_brick_decompose_descriptor_table(fmt, dims, brick, neg, pos):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("grid", [1, 0])
+@pytest.mark.parametrize("fmt", [4, 5, 7])
+@pytest.mark.parametrize("dims,brick,neg,pos", LAYOUTS)
+def test_brick_decompose_128_thread_workgroups(fmt, dims, brick, neg, pos, grid):
+    """Knob decompose.block = 128: each 16-KiB chunk copied by 128 threads (twice the items and
+    staged words per thread), with grid-derived descriptors and with the descriptor table."""
+    rng = np.random.default_rng(fmt * 100 + sum(dims) + 11)
+    codes = rand_codes(rng, fmt, dims[::-1])
+    assert lib.vktHipSetTuningKnob(b"decompose.block", 128) == 0
+    assert lib.vktHipSetTuningKnob(b"decompose.grid", grid) == 0
+    try:
+        err, got = gpu_decompose(codes, fmt, (0.0, 1.0), brick, neg, pos)
+    finally:
+        assert lib.vktHipSetTuningKnob(b"decompose.block", -1) == 0
+        assert lib.vktHipSetTuningKnob(b"decompose.grid", -1) == 0
+    assert err == vkt.NoError, vkt.last_error()
+    ref = ob.brick_decompose(ob.Volume(codes, fmt), brick, neg, pos)
+    for idx, v in ref.items():
+        np.testing.assert_array_equal(got[idx], v.codes, err_msg=f"brick {idx}")
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("aligned", [1, 2])
 @pytest.mark.parametrize("fmt", [4, 5, 7])
 @pytest.mark.parametrize("dims,brick,neg,pos", LAYOUTS[1:4] + LAYOUTS[6:])

@@ -8,9 +8,9 @@ Parity contract:
       |gpu - exact| <= 1 ulp(exact) + 2^-24 * sum|terms| * 1e-6     (GPU is accurate)
       |gpu - oracle| <= n * 2^-24 * sum|terms| + 1 ulp                (serial error bound)
     where exact is a float64 sum of the same float32 terms.
-  * var under the UInt16 unit-mapping moments path (knob aggregates.moments): the
-    sum of squares is the EXACT sum (v - m)^2 from integer moments, not a sum of float terms;
-    each float term fl(fl(v - m)^2) lies within 3 * 2^-24 of (v - m)^2, so
+  * var under the one-pass moments paths (knob aggregates.moments, DESIGN §4.8: UInt16, Float32):
+    the sum of squares is the EXACT sum (v - m)^2 (integer moments; float moments to ~2^-50), not
+    a sum of float terms; each float term fl(fl(v - m)^2) lies within 3 * 2^-24 of (v - m)^2, so
       |var - var_terms| <= 3 * 2^-24 * var_terms + 2 ulp(var_terms)
     (var_terms: the float-terms value above); far inside the serial bound.
 The oracle itself is pinned here against numpy's sequential float32 accumulation
@@ -323,8 +323,9 @@ def test_histogram_packed16_matches_tiled_passes(fmt):
 
 
 def takes_moments(fmt, mapping):
-    """UInt16 under the unit mapping (+0, 1) takes the integer-moments path (aggregates.moments)."""
-    return fmt == 5 and mapping[1] == 1.0 and mapping[0] == 0.0 and np.copysign(1.0, mapping[0]) > 0
+    """UInt16 (integer moments under the unit mapping, float moments otherwise) and Float32 (float
+    moments) take the one-pass moments paths (aggregates.moments)."""
+    return fmt in (5, 7)
 
 
 def check_var(got_var, var_terms, moments, what=""):
@@ -569,7 +570,8 @@ def test_aggregate_slab_partials_combine_to_the_whole(nx):
     assert (out.min, out.max) == (whole.min, whole.max)
     assert (out.argmin.x, out.argmin.y, out.argmin.z) == tuple(whole.argmin)
     assert (out.argmax.x, out.argmax.y, out.argmax.z) == tuple(whole.argmax)
-    assert out.mean == whole.mean and abs(out.var - whole.var) <= float(np.spacing(np.float32(whole.var)))
+    assert out.mean == whole.mean
+    check_var(whole.var, out.var, True, "whole (moments) vs slab partials (two passes)")
 
 
 @pytest.mark.gpu
@@ -638,7 +640,7 @@ def test_aggregates_uint16_moments():
     (knob 0): every code once (min 0 / max 65535 at known places), random codes over spans,
     padded rows (row ends at every phase mod 8, masked end items), strided boxes, ranges with a
     partial wave-step, tied extremes across lanes / waves / steps, extremes first occurring late,
-    constant volumes (var exactly 0, as the float terms give), a constant volume whose first voxel
+    constant volumes (var exactly 0 over the whole volume, as the float terms give), a constant volume whose first voxel
     differs (the cancellation case of a float moment form), a product that stays above 0.
     min / max / arg / sum / mean are identical to the code-count path; var within the stated bound."""
     rng = np.random.default_rng(2024)
@@ -676,8 +678,8 @@ def test_aggregates_uint16_moments():
                 lib.vktHipSetTuningKnob(b"aggregates.moments", -1)
             assert (got.min, got.max, tuple(got.argmin), tuple(got.argmax), got.sum, got.mean) == \
                 (two.min, two.max, tuple(two.argmin), tuple(two.argmax), two.sum, two.mean), what
-            if codes is const:
-                assert got.var == 0.0 and two.var == 0.0, what
+            if codes is const and last == codes.shape[::-1] and first == (0, 0, 0):
+                assert got.var == 0.0 and two.var == 0.0, what   # (a sub-box's mean divides by the whole count)
     # product through the pair products: all-top volume, (1 - 2^-16)^n stays far from 0
     codes = np.full((4, 8, 64), 65535, np.uint16)
     got = gpu_aggregates(codes, 5, 0.0, 1.0, (0, 0, 0), (64, 8, 4))
@@ -714,3 +716,56 @@ def test_aggregates_uint16_moments_sum_of_squares_beyond_2_64():
     check_var(out.var, var_terms, True, "2^32+ voxels")
     assert (out.min, out.max) == (v, v)
     assert (out.argmin.x, out.argmin.y, out.argmin.z) == (0, 0, 0) == (out.argmax.x, out.argmax.y, out.argmax.z)
+
+
+@pytest.mark.gpu
+def test_aggregates_float_moments_and_fallbacks():
+    """UInt16 under other mappings and Float32 from one pass of floating-point moments (knob
+    aggregates.moments bit 1): against the oracle and the two-pass path (knob 0) over
+    spans, padded rows and strided boxes, a narrow mapping (1000, 1000.001) whose values sit far
+    from 0 relative to their spread, and a first lane value far from the rest (the pivot case).
+    Volumes whose float terms may leave the normal float range must give the two-pass result
+    exactly: NaN / Inf voxels, |v - m| beyond 2^62 (3e30), values with a nonzero |v| < 2^-40
+    (1e-20, denormals), and a UInt16 mapping whose codes decode to such tiny values."""
+    rng = np.random.default_rng(99)
+    boxes = [((0, 0, 0), (520, 24, 12)), ((3, 1, 2), (517, 23, 11)), ((8, 3, 2), (200, 20, 9))]
+
+    def both(codes, fmt, mapping, first, last):
+        got = gpu_aggregates(codes, fmt, *mapping, first, last)
+        lib.vktHipSetTuningKnob(b"aggregates.moments", 0)
+        try:
+            two = gpu_aggregates(codes, fmt, *mapping, first, last)
+        finally:
+            lib.vktHipSetTuningKnob(b"aggregates.moments", -1)
+        return got, two
+
+    for fmt, mapping in ((5, (-1.0, 3.0)), (5, (1000.0, 1000.001)), (5, (3.0, -1.0)), (7, (0.0, 1.0))):
+        codes = rand_codes(rng, fmt, (12, 24, 520))
+        if fmt == 7:
+            vals = codes.view(np.float32)
+            vals[0, 0, 0] = 2.0e6      # the first lane's pivot far from its other values
+        for first, last in boxes:
+            what = f"fmt={fmt} map={mapping} {first}->{last}"
+            got, two = both(codes, fmt, mapping, first, last)
+            check_aggregates(got, codes, fmt, mapping, first, last, what)
+            assert (got.min, got.max, tuple(got.argmin), tuple(got.argmax)) == \
+                (two.min, two.max, tuple(two.argmin), tuple(two.argmax)), what
+    # fallbacks: bit-identical to the two passes
+    base = rng.uniform(-1.0, 1.0, (8, 16, 256)).astype(np.float32)
+    specials = {"nan": np.nan, "inf": np.inf, "huge": 3.0e30, "tiny": 1.0e-20, "denormal": 1.0e-40}
+    for name, val in specials.items():
+        vals = base.copy()
+        vals[3, 5, 100] = val
+        codes = vals.view(np.uint32)
+        for first, last in ((((0, 0, 0), (256, 16, 8))), (((3, 1, 1), (250, 15, 7)))):
+            got, two = both(codes, 7, (0.0, 1.0), first, last)
+            for f in ("min", "max", "sum", "mean", "var", "stddev", "prod"):
+                a, b = getattr(got, f), getattr(two, f)
+                assert (a == b) or (np.isnan(a) and np.isnan(b)), (name, f, a, b)
+            assert tuple(got.argmin) == tuple(two.argmin) and tuple(got.argmax) == tuple(two.argmax)
+    # a UInt16 mapping with codes decoding to tiny nonzero values: (-2^-41 * 65536 ... ) around 0
+    codes = rng.integers(0, 65536, (8, 16, 256), dtype=np.uint16)
+    tiny_map = (-1.0e-13, 1.0e-13)
+    got, two = both(codes, 5, tiny_map, (0, 0, 0), (256, 16, 8))
+    for f in ("min", "max", "sum", "mean", "var", "prod"):
+        assert getattr(got, f) == getattr(two, f), f

@@ -19,7 +19,7 @@ torch.cuda.set_device(0)
 stream = torch.cuda.Stream()
 torch.cuda.set_stream(stream)
 lib.vktHipSetComputeStream(C.c_void_p(stream.cuda_stream))
-n = 1024
+n = int(os.environ.get("PROBE_EDGE", "1024"))   # 2048: the config-4 volumes (16 GiB each)
 nb = 2 * n ** 3
 o, last = Vec3i_t(0, 0, 0), Vec3i_t(n, n, n)
 
@@ -75,3 +75,5 @@ for it in range(int(os.environ.get("PROBE_ITERS", "5"))):
             else:
                 hip.hipFree(C.c_void_p(p))
 print({k: sorted(v) for k, v in res.items()})
+for k, v in res.items():
+    print(k, "spread", round((max(v) - min(v)) / min(v) * 100, 2), "%", flush=True)

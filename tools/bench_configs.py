@@ -534,6 +534,39 @@ def main():
             del arr, V
         ep.device = vkt.ExecutionPolicy.Device_CPU
         vkt.SetThreadExecutionPolicy(ep)
+    if want("decblk"):
+        # in-process A/B of the threads per BrickDecompose workgroup (knob decompose.block: 256, 128
+        # -- the same 16-KiB chunk, twice the items and staged words per thread with 128)
+        import volkit_amd.volkit as vkt
+        ep = vkt.GetThreadExecutionPolicy()
+        ep.device = vkt.ExecutionPolicy.Device_GPU
+        vkt.SetThreadExecutionPolicy(ep)
+        n = 1024
+        V = vkt.StructuredVolume(n, n, n, vkt.DataFormat_UInt16)
+        vkt.Synthesize(V, 77)
+        ab = {}
+        for bs, halo in ((16, (1, 1, 1)), (32, (1, 1, 1)), (64, (1, 1, 1))):
+            arr = vkt.Array3D_StructuredVolume()
+            b3, h3 = vkt.Vec3i(bs, bs, bs), vkt.Vec3i(*halo)
+            vkt.BrickDecomposeResize(arr, V, b3, h3, h3)
+            vox = sum(arr[(i, j, k)].getSizeInBytes() // 2 for k in range(arr.dims().z)
+                      for j in range(arr.dims().y) for i in range(arr.dims().x))
+            for rnd in range(3):
+                for kv in (256, 128):
+                    lib.vktHipSetTuningKnob(b"decompose.block", kv)
+                    ab.setdefault((bs, halo, kv, vox, "back-to-back"), []).append(
+                        pipelined(lambda: vkt.BrickDecompose(arr, V, b3, h3, h3), R))
+                    ab.setdefault((bs, halo, kv, vox, "incl. host planning"), []).append(
+                        timed(lambda: vkt.BrickDecompose(arr, V, b3, h3, h3), R))
+            del arr
+        lib.vktHipSetTuningKnob(b"decompose.block", -1)
+        for (bs, halo, kv, vox, how), ts in sorted(ab.items()):
+            ts.sort()
+            report(f"decblk BrickDecompose 1024^3 UInt16 -> {bs}^3 bricks halo {halo} block={kv} ({how}; median of 3 "
+                   f"rounds, spread {ts[0]:.4f}-{ts[-1]:.4f})", ts[1], 4 * vox, vox)
+        del V
+        ep.device = vkt.ExecutionPolicy.Device_CPU
+        vkt.SetThreadExecutionPolicy(ep)
     if want("decab"):
         # in-process A/B of the staged copy's LDS writes (knob decompose.aligned_lds: 0 unaligned
         # 16-B words + per-voxel row ends, 1 row-end words as aligned pieces, 2 every word)

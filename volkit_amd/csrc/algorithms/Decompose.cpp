@@ -82,10 +82,22 @@ namespace
         if (ranges.size() < total)
             ranges.resize(total);
         vktHipBrickRange_t* const out = ranges.data();
+        vktHipVolumeView_t const src = brickView(source);
+        // Many small bricks: the ranges are planned and handed to the backend in batches of whole
+        // brick planes (~16 Ki bricks, at most kMaxBatches), so the host plans batch k + 1 -- the
+        // views here, the descriptors in the backend -- while the GPU copies batch k: a
+        // synchronised call costs about one batch of planning plus the copies instead of all the
+        // planning plus the copies.  Each batch is a uniform brick grid of its own (the backend
+        // infers and checks it per call), the copies are the same.
+        constexpr size_t kBatchBricks = 16384, kMaxBatches = 8;
+        size_t const nzb = static_cast<size_t>(std::max(0, arrDims.z)), plane = nx * ny;
+        size_t batches = std::min(kMaxBatches, std::max<size_t>(1, total / kBatchBricks));
+        batches = std::min(batches, std::max<size_t>(1, nzb));
+        size_t const planesPer = nzb > 0 ? (nzb + batches - 1) / batches : 0;
         // one view per brick (getData() migrates a brick that lives elsewhere): ~16 ns per brick,
         // 4 ms for the 262 144 bricks of 16^3 over 1024^3 serially -- split over the host pool,
         // each worker under the caller's policy (and device: HostPool)
-        rt::parallelFor(total, 4096, [&](size_t b, size_t e) {
+        auto plan = [&](size_t b, size_t e) {
             ExecutionPolicy const saved = GetThreadExecutionPolicy();
             SetThreadExecutionPolicy(ep);
             constexpr size_t kAhead = 16;
@@ -106,9 +118,18 @@ namespace
                 r.brick = brickView(brickAt(i));
             }
             SetThreadExecutionPolicy(saved);
-        });
-        vktHipVolumeView_t src = brickView(source);
-        return static_cast<Error>(vktHipBrickDecompose(src, out, static_cast<int32_t>(total)));
+        };
+        if (total == 0 || planesPer == 0)
+            return static_cast<Error>(vktHipBrickDecompose(src, out, 0));
+        for (size_t z0 = 0; z0 < nzb; z0 += planesPer)
+        {
+            size_t const b0 = z0 * plane, b1 = std::min(nzb, z0 + planesPer) * plane;
+            rt::parallelFor(b1 - b0, 4096, [&](size_t b, size_t e) { plan(b0 + b, b0 + e); });
+            vktError const e = vktHipBrickDecompose(src, out + b0, static_cast<int32_t>(b1 - b0));
+            if (e != vktNoError)
+                return static_cast<Error>(e);
+        }
+        return NoError;
     }
 } // namespace
 

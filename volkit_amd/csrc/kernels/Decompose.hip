@@ -54,8 +54,9 @@ namespace hipk
     // 16-byte store out of the LDS tile the workgroup assembled (brickStaged).  Row mode (a
     // brick larger than its range): item = a 16-byte segment of one box row, one unaligned
     // 16-byte load and store, row tails and clamped segments voxel by voxel.
-    constexpr int kBrickPerThread = 4;
-    constexpr uint32_t kBrickChunk = kBlock * kBrickPerThread;   // segments per workgroup
+    constexpr uint32_t kBrickChunk = 1024;   // 16-B items (16 KiB) per workgroup
+    // threads per workgroup NT (kBlock = 256, or 128 for small bricks: knob decompose.block) and
+    // items per thread kBrickChunk / NT
 
     struct __attribute__((packed, aligned(1))) Unaligned16
     {
@@ -155,7 +156,7 @@ namespace hipk
     // reads, one aligned 16-byte global store per item.  The byte shifting is done by LDS
     // addressing instead of VALU funnel shifts (a 128-bit shift per lane made the kernel VALU
     // bound: 256^3 bricks + halo 1 took 1.15 ms vs 0.75 ms without halo; staged: 0.83 ms).
-    template <int BPV, int kStageWords>
+    template <int BPV, int kStageWords, int NT>
     __device__ __forceinline__ void brickStaged(BrickDesc const& d, uint32_t base, uint8_t const* src, int32_t sdx,
                                                 int32_t sdy, int32_t sdz, int32_t alignedLds)
     {
@@ -235,11 +236,11 @@ namespace hipk
         Word words[kStageWords];
 #pragma unroll
         for (int k = 0; k < kStageWords; ++k)
-            locate(threadIdx.x + k * kBlock, words[k]);
+            locate(threadIdx.x + k * NT, words[k]);
 #pragma unroll
         for (int k = 0; k < kStageWords; ++k)
             place(words[k]);
-        for (uint32_t t = threadIdx.x + kStageWords * kBlock; t < total; t += kBlock)
+        for (uint32_t t = threadIdx.x + kStageWords * NT; t < total; t += NT)
         {
             Word w;
             locate(t, w);
@@ -247,7 +248,7 @@ namespace hipk
         }
         if (d.fx < 0 || d.fx + d.nx > sdx)   // clamped halo voxels (border bricks only)
         {
-            for (int32_t q = threadIdx.x; q < nRows; q += kBlock)
+            for (int32_t q = threadIdx.x; q < nRows; q += NT)
             {
                 int32_t const r = rA + q;
                 uint64_t const rb = rowBase(r);
@@ -270,9 +271,9 @@ namespace hipk
         }
         __syncthreads();
 #pragma unroll
-        for (int u = 0; u < kBrickPerThread; ++u)
+        for (int u = 0; u < static_cast<int>(kBrickChunk) / NT; ++u)
         {
-            int32_t const t = u * kBlock + static_cast<int32_t>(threadIdx.x);
+            int32_t const t = u * NT + static_cast<int32_t>(threadIdx.x);
             int32_t const lv = t * V;
             uint8_t* const out = d.dst + static_cast<uint64_t>(vStart + lv) * BPV;
             // global address space named (the brick pointer comes from the descriptor table; a
@@ -314,8 +315,8 @@ namespace hipk
         return c == 0 ? a[0] : (c == 1 ? a[1] : a[2]);
     }
 
-    template <int BPV, int kStageWords, bool GRID>
-    __global__ __launch_bounds__(kBlock) void brickCopyKernel(BrickDesc const* bricks, BrickGrid grid,
+    template <int BPV, int kStageWords, bool GRID, int NT = kBlock>
+    __global__ __launch_bounds__(NT) void brickCopyKernel(BrickDesc const* bricks, BrickGrid grid,
                                                              FastDiv chunksPerBrick, FastDiv groupSize,
                                                              uint8_t const* src, int32_t sdx, int32_t sdy, int32_t sdz,
                                                              int32_t alignedLds)
@@ -361,20 +362,21 @@ namespace hipk
             return;   // border bricks are smaller than the largest one
         if (GRID || d.linear)
         {
-            brickStaged<BPV, kStageWords>(d, base, src, sdx, sdy, sdz, alignedLds);
+            brickStaged<BPV, kStageWords, NT>(d, base, src, sdx, sdy, sdz, alignedLds);
             return;
         }
         uint64_t const pitchY = static_cast<uint64_t>(d.dimX);
         uint64_t const pitchZ = pitchY * static_cast<uint64_t>(d.dimY);
         uint64_t const spY = static_cast<uint64_t>(sdx), spZ = spY * static_cast<uint64_t>(sdy);
-        u32x4 vals[kBrickPerThread];
-        uint64_t srow[kBrickPerThread], drow[kBrickPerThread];
-        int32_t sx0[kBrickPerThread], cnt[kBrickPerThread];
-        bool fast[kBrickPerThread];
+        constexpr int kPer = static_cast<int>(kBrickChunk) / NT;
+        u32x4 vals[kPer];
+        uint64_t srow[kPer], drow[kPer];
+        int32_t sx0[kPer], cnt[kPer];
+        bool fast[kPer];
 #pragma unroll
-        for (int u = 0; u < kBrickPerThread; ++u)
+        for (int u = 0; u < kPer; ++u)
         {
-            uint32_t const i = base + u * kBlock + threadIdx.x;
+            uint32_t const i = base + u * NT + threadIdx.x;
             bool const live = i < d.nitems;
             uint32_t const ii = live ? i : 0;
             uint32_t const row = fdiv(ii, d.fseg);
@@ -394,7 +396,7 @@ namespace hipk
                 vals[u] = reinterpret_cast<Unaligned16 const*>(src + (srow[u] + sx0[u]) * BPV)->v;
         }
 #pragma unroll
-        for (int u = 0; u < kBrickPerThread; ++u)
+        for (int u = 0; u < kPer; ++u)
         {
             if (fast[u])
             {
@@ -749,9 +751,21 @@ vktError vktHipBrickDecompose(vktHipVolumeView_t source, vktHipBrickRange_t cons
         // back-to-back calls): 32^3 + halo 1.256 -> 1.211 ms with 6, 1.218 ms with 8; 64^3 + halo,
         // 128^3 and 256^3 + halo unchanged within 1 %
         int64_t const sw = rt::knob(rt::Knob::DecomposeStageWords);
+        // threads per workgroup (knob decompose.block): 128 gives each thread twice the items and
+        // staged words of a 256-thread workgroup over the same 16-KiB chunk
+        bool const half = rt::knob(rt::Knob::DecomposeBlock) == 128;
         auto launch = [&](auto bpvC, auto swC) {
             constexpr int B = decltype(bpvC)::value, W = decltype(swC)::value;
-            if (useGrid)
+            if (half)
+            {
+                if (useGrid)
+                    hipLaunchKernelGGL((brickCopyKernel<B, 2 * W, true, 128>), dim3(g), dim3(128), 0, s, dev, grid, fdc,
+                                       fdg, source.data, source.dimX, source.dimY, source.dimZ, alignedLds);
+                else
+                    hipLaunchKernelGGL((brickCopyKernel<B, 2 * W, false, 128>), dim3(g), dim3(128), 0, s, dev, grid, fdc,
+                                       fdg, source.data, source.dimX, source.dimY, source.dimZ, alignedLds);
+            }
+            else if (useGrid)
                 hipLaunchKernelGGL((brickCopyKernel<B, W, true>), dim3(g), dim3(kBlock), 0, s, dev, grid, fdc, fdg,
                                    source.data, source.dimX, source.dimY, source.dimZ, alignedLds);
             else

@@ -1634,6 +1634,271 @@ namespace hipk
         res[1] = two;
     }
 
+    // ---- Aggregates in ONE pass of floating-point moments (UInt16 other mappings, Float32) ----
+    // The values are not integers here, so the sum of squares about the float mean m comes from
+    // per-lane moments about a pivot K (the lane's first value): S1 = sum (v - K), S2 = sum
+    // (v - K)^2 in double (v - K is exact in double for floats), per lane mean = K + S1/n and
+    // M2 = S2 - S1^2/n, combined across lanes / waves / workgroups with the pairwise update
+    // (Chan et al.): M2 = M2a + M2b + delta^2 na nb / n -- no cancellation beyond one lane's
+    // values.  Then S = M2 + n (mean - m)^2: the EXACT sum (v - m)^2 to ~2^-50, where the
+    // reference's float terms fl(fl(v - m)^2) each lie within 3 * 2^-24 of (v - m)^2 (the bound
+    // tests/test_reduce.py states).  The float terms can differ by more than that only when a term
+    // leaves the normal float range: (v - m)^2 above FLT_MAX (|v - m| >= 2^62 checked from the
+    // extremes) or subnormal (a nonzero |v| or |m| below 2^-40: flagged per voxel for Float32,
+    // per code on the host for UInt16); and NaN / +-Inf make every sum non-finite.  In those cases
+    // res[1].count = 0 and the caller runs the two float passes.  min / max / arg, the extremes
+    // filter, prod and the in-order first occurrence as aggregatesFastKernel.
+    struct MomentPartialF
+    {
+        uint64_t count;
+        double mean, m2, sum, prod;
+        float minValue, maxValue;
+        uint64_t minIndex, maxIndex;
+        uint32_t flags;   // bit 0: a non-finite value; bit 1: a nonzero |v| < 2^-40
+        uint32_t pad;
+    };
+
+    constexpr float kTinyValue = 0x1p-40f;
+
+    __device__ __forceinline__ void momentCombineF(MomentPartialF& p, MomentPartialF const& o)
+    {
+        if (o.count != 0)
+        {
+            if (p.count == 0)
+            {
+                p.mean = o.mean;
+                p.m2 = o.m2;
+            }
+            else
+            {
+                double const na = static_cast<double>(p.count), nb = static_cast<double>(o.count);
+                double const n = na + nb, delta = o.mean - p.mean;
+                p.mean += delta * (nb / n);
+                p.m2 += o.m2 + delta * delta * (na * nb / n);
+            }
+        }
+        p.count += o.count;
+        p.sum += o.sum;
+        p.prod *= o.prod;
+        p.flags |= o.flags;
+        minCombine(p.minValue, p.minIndex, o.minValue, o.minIndex);
+        maxCombine(p.maxValue, p.maxIndex, o.maxValue, o.maxIndex);
+    }
+
+    __device__ __forceinline__ MomentPartialF shflXorMomentF(MomentPartialF const& p, int m)
+    {
+        MomentPartialF o;
+        o.count = shflXorU(p.count, m);
+        o.mean = shflXorD(p.mean, m);
+        o.m2 = shflXorD(p.m2, m);
+        o.sum = shflXorD(p.sum, m);
+        o.prod = shflXorD(p.prod, m);
+        o.minValue = __shfl_xor(p.minValue, m);
+        o.maxValue = __shfl_xor(p.maxValue, m);
+        o.minIndex = shflXorU(p.minIndex, m);
+        o.maxIndex = shflXorU(p.maxIndex, m);
+        o.flags = __shfl_xor(p.flags, m);
+        o.pad = 0;
+        return o;
+    }
+
+    template <int WAVES>
+    __device__ void momentBlockReduceF(MomentPartialF& p)
+    {
+        for (int m = 32; m >= 1; m >>= 1)
+            momentCombineF(p, shflXorMomentF(p, m));
+        __shared__ MomentPartialF lds[WAVES];
+        if ((threadIdx.x & 63) == 0)
+            lds[threadIdx.x >> 6] = p;
+        __syncthreads();
+        if (threadIdx.x == 0)
+            for (int w = 1; w < WAVES; ++w)
+                momentCombineF(p, lds[w]);
+    }
+
+    __device__ __forceinline__ MomentPartialF emptyMomentF()
+    {
+        MomentPartialF p;
+        p.count = 0;
+        p.mean = p.m2 = p.sum = 0.0;
+        p.prod = 1.0;
+        p.minValue = FLT_MAX;
+        p.maxValue = -FLT_MAX;
+        p.minIndex = p.maxIndex = kNoIndex;
+        p.flags = 0;
+        p.pad = 0;
+        return p;
+    }
+
+    // FMT UInt16 (any mapping but the unit one, which takes the integer kernel) or Float32.
+    template <int FMT, bool CONTIG>
+    __global__ __launch_bounds__(kBlock) void aggregatesMomentsFKernel(FastHistArgs h, MomentPartialF* partials)
+    {
+        constexpr int BPV = FMT == codec::FmtUInt16 ? 2 : 4;
+        constexpr int U = 4;
+        uint32_t const lane = threadIdx.x & 63;
+        MomentPartialF p = emptyMomentF();
+        double K = 0.0, s1 = 0.0, s2 = 0.0;
+        uint32_t n = 0;   // this lane's voxels (< 2^32: a lane visits far fewer)
+        bool bad = false, tiny = false;
+        auto decodeV = [&](uint32_t c) -> float {
+            if constexpr (FMT == codec::FmtFloat32)
+                return codec::bitsToFloat(c);
+            else
+                return codec::decode(c, FMT, h.lo, h.hi);
+        };
+        auto visit8 = [&](uint32_t const (&c)[8], uint64_t item, uint64_t hb, uint32_t m, bool prodLive) {
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                v[j] = decodeV(c[j]);
+            auto gIndex = [&](int j) -> uint64_t {
+                if (CONTIG && hb != ~0ull)
+                    return h.giBase + hb * 8 + 4 * lane + (j < 4 ? static_cast<uint64_t>(j) : 252ull + j);
+                return spanGlobalIndex<CONTIG>(h, item, j);
+            };
+            // the lane's pivot: its first valid value (0 when that is not finite: the result then
+            // falls back anyway)
+            if (n == 0)
+            {
+                float k0 = 0.f;
+#pragma unroll
+                for (int j = 7; j >= 0; --j)
+                    k0 = (m >> j) & 1u ? v[j] : k0;
+                K = fabsf(k0) <= FLT_MAX ? static_cast<double>(k0) : 0.0;
+            }
+            float lo = FLT_MAX, hi = -FLT_MAX;
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+            {
+                float const x = (m >> j) & 1u ? v[j] : p.minValue;
+                lo = fminf(lo, x);   // (NaN never qualifies: minNum / maxNum skip it)
+                hi = fmaxf(hi, x);
+            }
+            if (lo < p.minValue || hi > p.maxValue)
+            {
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                {
+                    if (!((m >> j) & 1u))
+                        continue;
+                    if (v[j] < p.minValue)
+                    {
+                        p.minValue = v[j];
+                        p.minIndex = gIndex(j);
+                    }
+                    if (v[j] > p.maxValue)
+                    {
+                        p.maxValue = v[j];
+                        p.maxIndex = gIndex(j);
+                    }
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+            {
+                if (!((m >> j) & 1u))
+                    continue;
+                double const x = static_cast<double>(v[j]);
+                double const d = x - K;
+                s1 += d;
+                s2 = fma(d, d, s2);
+                if (prodLive)
+                    p.prod *= x;
+                float const a = fabsf(v[j]);
+                bad = bad || !(a <= FLT_MAX);
+                if constexpr (FMT == codec::FmtFloat32)
+                    tiny = tiny || (a < kTinyValue && a != 0.f);
+            }
+            n += static_cast<uint32_t>(__builtin_popcount(m));
+        };
+        uint64_t const wave = static_cast<uint64_t>(blockIdx.x) * (kBlock / 64) + (threadIdx.x >> 6);
+        uint64_t const waves = static_cast<uint64_t>(gridDim.x) * (kBlock / 64);
+        uint64_t const steps = h.items / (64 * U);
+        bool const halves = CONTIG && BPV == 4 && (reinterpret_cast<uintptr_t>(h.data) & 15u) == 0;
+        for (uint64_t st = wave; st < steps; st += waves)
+        {
+            uint32_t c[U][8], msk[U];
+            if (halves)   // contiguous 16-B lanes (as aggregatesFastKernel)
+            {
+#pragma unroll
+                for (int k = 0; k < U; ++k)
+                {
+                    uint8_t const* q = h.data + ((st * (64 * U) + k * 64) * 8 + 4 * lane) * 4;
+                    u32x4 const x = loadVec<u32x4, true>(q), y = loadVec<u32x4, true>(q + 1024);
+                    c[k][0] = x.x; c[k][1] = x.y; c[k][2] = x.z; c[k][3] = x.w;
+                    c[k][4] = y.x; c[k][5] = y.y; c[k][6] = y.z; c[k][7] = y.w;
+                    msk[k] = 0xFFu;
+                }
+            }
+            else
+            {
+#pragma unroll
+                for (int k = 0; k < U; ++k)
+                    load8<BPV, true>(h.data, spanVoxelMask<CONTIG>(h, st * (64 * U) + k * 64 + lane, msk[k]), c[k]);
+            }
+            bool const prodLive = __any(p.prod != 0.0);   // wave-uniform: 0 stays 0 (finite values)
+#pragma unroll
+            for (int k = 0; k < U; ++k)
+                visit8(c[k], st * (64 * U) + k * 64 + lane, halves ? st * (64 * U) + k * 64 : ~0ull, msk[k], prodLive);
+        }
+        for (uint64_t it = steps * (64 * U) + wave * 64 + lane; it < h.items; it += waves * 64)
+        {
+            uint32_t c[8], m;
+            load8<BPV, true>(h.data, spanVoxelMask<CONTIG>(h, it, m), c);
+            visit8(c, it, ~0ull, m, true);
+        }
+        if (n != 0)
+        {
+            double const dn = static_cast<double>(n);
+            p.count = n;
+            p.mean = K + s1 / dn;
+            p.m2 = fmax(s2 - s1 * (s1 / dn), 0.0);
+            p.sum = fma(dn, K, s1);
+        }
+        p.flags = (bad ? 1u : 0u) | (tiny ? 2u : 0u);
+        momentBlockReduceF<kBlock / 64>(p);
+        if (threadIdx.x == 0)
+            partials[blockIdx.x] = p;
+    }
+
+    // One workgroup: the n partials of aggregatesMomentsFKernel -> res[0] (pass-1 fields) and
+    // res[1].sumSq = S with res[1].count = 1, or res[1].count = 0 when the float terms may differ
+    // from the exact form (see above; the caller runs the two passes).  tinyCodes: the host found a
+    // code of the volume's format whose value is a nonzero |v| < 2^-40 (UInt16).
+    __global__ __launch_bounds__(kBlock) void aggregatesMomentsFFinalKernel(MomentPartialF const* partials, uint32_t n,
+                                                                           double numElems, uint32_t tinyCodes,
+                                                                           vktHipAggregatePartial_t* res)
+    {
+        MomentPartialF p = emptyMomentF();
+        for (uint32_t i = threadIdx.x; i < n; i += kBlock)
+            momentCombineF(p, partials[i]);
+        momentBlockReduceF<kBlock / 64>(p);
+        if (threadIdx.x != 0)
+            return;
+        vktHipAggregatePartial_t one = emptyPartial();
+        one.count = p.count;
+        one.sum = p.sum;
+        one.prod = p.prod;
+        one.minValue = p.minValue;
+        one.minIndex = p.minIndex;
+        one.maxValue = p.maxValue;
+        one.maxIndex = p.maxIndex;
+        float const m = static_cast<float>(static_cast<double>(static_cast<float>(p.sum)) / numElems);
+        double const dm = static_cast<double>(m);
+        bool ok = (p.flags & 1u) == 0 && fabs(p.sum) <= DBL_MAX && p.m2 <= DBL_MAX;
+        ok = ok && (p.flags & 2u) == 0 && tinyCodes == 0 && (m == 0.f || fabsf(m) >= kTinyValue);
+        if (p.count != 0)
+            ok = ok && fabs(static_cast<double>(p.maxValue) - dm) < 0x1p62 &&
+                 fabs(static_cast<double>(p.minValue) - dm) < 0x1p62;
+        double const dd = p.mean - dm;
+        vktHipAggregatePartial_t two = emptyPartial();
+        two.sumSq = p.count ? p.m2 + static_cast<double>(p.count) * dd * dd : 0.0;
+        two.count = ok ? 1u : 0u;
+        res[0] = one;
+        res[1] = two;
+    }
+
     // The first voxels of item `item` holding codes tmin / tmax, folded into *bMin / *bMax with
     // atomicMin (LDS or global).
     template <int BPV, bool CONTIG>
@@ -2247,6 +2512,55 @@ namespace hipk
         return streamingGrid(h.items, 64u * 4u * (kBlock / 64), 8);
     }
 
+    // UInt16 under any other mapping and Float32: one pass of floating-point moments
+    // (aggregatesMomentsFKernel); knob aggregates.moments bit 1.  0 when the range does not take
+    // it, else the number of partials.  tiny: some UInt16 code decodes to a nonzero |v| < 2^-40.
+    unsigned momentGridF(BoxArgs const& a, FastHistArgs& h, bool& contig, uint32_t& tiny)
+    {
+        tiny = 0;
+        bool const fmtOk = (a.fmt == codec::FmtUInt16 && !codec::isUnitMapping(a.lo, a.hi)) || a.fmt == codec::FmtFloat32;
+        if (!fmtOk || (rt::knob(rt::Knob::AggregatesMoments) & 2) == 0 || !makeSpanArgs(a, h, contig))
+            return 0;
+        if (a.fmt == codec::FmtUInt16)
+        {
+            // every code's value once on the host (kept per thread for the last mapping)
+            thread_local uint64_t lastKey = ~0ull;
+            thread_local uint32_t lastTiny = 0;
+            uint64_t const key = static_cast<uint64_t>(codec::floatToBits(a.lo)) << 32 | codec::floatToBits(a.hi);
+            if (key != lastKey)
+            {
+                uint32_t t = 0;
+                for (uint32_t c = 0; c < 65536u && !t; ++c)
+                {
+                    float const v = std::fabs(codec::decode(c, codec::FmtUInt16, a.lo, a.hi));
+                    t = v != 0.f && v < 0x1p-40f ? 1u : 0u;
+                }
+                lastKey = key;
+                lastTiny = t;
+            }
+            tiny = lastTiny;
+        }
+        return streamingGrid(h.items, 64u * 4u * (kBlock / 64), 8);
+    }
+
+    void launchMomentsF(FastHistArgs const& h, bool contig, int32_t fmt, unsigned g, double numElems, uint32_t tiny,
+                        MomentPartialF* parts, vktHipAggregatePartial_t* res, hipStream_t s)
+    {
+        if (fmt == codec::FmtUInt16)
+        {
+            if (contig)
+                hipLaunchKernelGGL((aggregatesMomentsFKernel<codec::FmtUInt16, true>), dim3(g), dim3(kBlock), 0, s, h, parts);
+            else
+                hipLaunchKernelGGL((aggregatesMomentsFKernel<codec::FmtUInt16, false>), dim3(g), dim3(kBlock), 0, s, h,
+                                   parts);
+        }
+        else if (contig)
+            hipLaunchKernelGGL((aggregatesMomentsFKernel<codec::FmtFloat32, true>), dim3(g), dim3(kBlock), 0, s, h, parts);
+        else
+            hipLaunchKernelGGL((aggregatesMomentsFKernel<codec::FmtFloat32, false>), dim3(g), dim3(kBlock), 0, s, h, parts);
+        hipLaunchKernelGGL(aggregatesMomentsFFinalKernel, dim3(1), dim3(kBlock), 0, s, parts, g, numElems, tiny, res);
+    }
+
     void launchMomentsU16(FastHistArgs const& h, bool contig, unsigned g, double numElems, MomentPartialU16* parts,
                           vktHipAggregatePartial_t* res, hipStream_t s)
     {
@@ -2399,14 +2713,19 @@ vktError vktHipAggregatesRange(vktHipVolumeView_t volume, vktVec3i_t first, vktV
     bool const boxed = makeBox(volume, first, last, 0, a, "vktHipAggregatesRange: invalid volume view", e);
     FastHistArgs hm;
     bool contigM = false;
+    uint32_t tiny = 0;
     unsigned const gm = boxed ? momentGridU16(a, hm, contigM) : 0u;
-    unsigned const gc = boxed && gm == 0 ? codeAggGrid(a) : 0u;
-    if (gm != 0)
+    unsigned const gf = boxed && gm == 0 ? momentGridF(a, hm, contigM, tiny) : 0u;
+    unsigned const gc = boxed && gm == 0 && gf == 0 ? codeAggGrid(a) : 0u;
+    if (gm != 0 || gf != 0)
     {
-        // UInt16, unit mapping: one pass of exact integer moments, complete (no fallback)
+        // UInt16 under the unit mapping: one pass of exact integer moments, complete; other
+        // mappings / Float32: one pass of float moments, the two passes below when it says so
         hipStream_t s = rt::computeStream();
         AggScratch& sc = aggScratch();
-        size_t const bytes = 2 * sizeof(vktHipAggregatePartial_t) + static_cast<size_t>(gm) * sizeof(MomentPartialU16);
+        size_t const bytes = 2 * sizeof(vktHipAggregatePartial_t) +
+                             std::max(static_cast<size_t>(gm) * sizeof(MomentPartialU16),
+                                      static_cast<size_t>(gf) * sizeof(MomentPartialF));
         auto* res = static_cast<vktHipAggregatePartial_t*>(sc.dev.acquire(bytes, s));
         if (!res)
             return vktInvalidValue;
@@ -2417,8 +2736,12 @@ vktError vktHipAggregatesRange(vktHipVolumeView_t volume, vktVec3i_t first, vktV
             sc.dev.release(s);
             return vktInvalidValue;
         }
-        launchMomentsU16(hm, contigM, gm, static_cast<double>(numElems), reinterpret_cast<MomentPartialU16*>(res + 2),
-                         res, s);
+        if (gm != 0)
+            launchMomentsU16(hm, contigM, gm, static_cast<double>(numElems),
+                             reinterpret_cast<MomentPartialU16*>(res + 2), res, s);
+        else
+            launchMomentsF(hm, contigM, a.fmt, gf, static_cast<double>(numElems), tiny,
+                           reinterpret_cast<MomentPartialF*>(res + 2), res, s);
         e = rt::check(hipMemcpyAsync(sc.host, res, 2 * sizeof(vktHipAggregatePartial_t), hipMemcpyDeviceToHost, s),
                       "hipMemcpyAsync(aggregates)");
         sc.dev.release(s);
@@ -2427,9 +2750,12 @@ vktError vktHipAggregatesRange(vktHipVolumeView_t volume, vktVec3i_t first, vktV
         VKT_HIP_TRY(hipStreamSynchronize(s));
         if ((e = rt::finishLaunch("AggregatesRange_hip")) != vktNoError)
             return e;
-        p1 = sc.host[0];
-        p2 = sc.host[1];
-        done = true;
+        if (sc.host[1].count == 1u)
+        {
+            p1 = sc.host[0];
+            p2 = sc.host[1];
+            done = true;
+        }
     }
     else if (gc != 0)
     {

@@ -210,8 +210,9 @@ namespace rt
             {"decompose.grid", 1},
             {"memory.pool", 1},
             {"memory.arena", 1},
-            {"aggregates.moments", 1},
+            {"aggregates.moments", 3},
             {"memory.arena_chunk_mib", 0},
+            {"decompose.block", 256},
         };
         static_assert(sizeof(kKnobs) / sizeof(kKnobs[0]) == static_cast<size_t>(Knob::Count), "knob table");
         std::atomic<int64_t> gKnobs[static_cast<int>(Knob::Count)] = {{kKnobs[0].def}, {kKnobs[1].def},
@@ -224,7 +225,8 @@ namespace rt
                                                                   {kKnobs[14].def}, {kKnobs[15].def},
                                                                   {kKnobs[16].def}, {kKnobs[17].def},
                                                                   {kKnobs[18].def}, {kKnobs[19].def},
-                                                                  {kKnobs[20].def}, {kKnobs[21].def}};
+                                                                  {kKnobs[20].def}, {kKnobs[21].def},
+                                                                  {kKnobs[22].def}};
     } // namespace
 
     int64_t knob(Knob k) { return gKnobs[static_cast<int>(k)].load(std::memory_order_relaxed); }

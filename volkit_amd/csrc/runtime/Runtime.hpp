@@ -94,8 +94,9 @@ namespace rt
         DecomposeGrid,                 // 0: uniform brick grids keep the per-brick descriptor table
         MemoryPool,                    // 0: every device buffer from its own hipMalloc (no small-block pool)
         MemoryArena,                   // 0: buffers > 4 MiB from their own hipMalloc (no arena chunks)
-        AggregatesMoments,             // bit 0: UInt16 unit-mapping ComputeAggregates from one pass of integer moments
+        AggregatesMoments,             // ComputeAggregates in one pass of moments: bit 0 UInt16 unit mapping (integer), bit 1 UInt16 other mappings / Float32 (float)
         MemoryArenaChunkMiB,           // > 0: arena chunks of exactly max(request, this many MiB) (tests)
+        DecomposeBlock,                // threads per BrickDecompose workgroup over one 16-KiB chunk: 256 or 128
         Count
     };
     int64_t knob(Knob k);

@@ -358,10 +358,12 @@ def _range(kind, op, dst: Slab, srcs, first, last, off, value, group, run_pieces
     tensors = [dst.flat()] + [s.flat() for s in srcs]
     on_gpu = any(t.is_cuda for t in tensors)
     bufs = [None, None]
-    for k, s in enumerate(srcs):
-        if bp[k]:
-            bufs[k] = torch.empty(bp[k] * s.plane_bytes, dtype=torch.uint8, device=s.flat().device)
     with library_stream(on_gpu):
+        # gather buffers allocated on the library's stream: torch returns their blocks to that
+        # stream, so no later user reuses them while the library's kernels still read them
+        for k, s in enumerate(srcs):
+            if bp[k]:
+                bufs[k] = torch.empty(bp[k] * s.plane_bytes, dtype=torch.uint8, device=s.flat().device)
         if moves:
             staged = dist.get_backend(group) == "gloo"
             ops, landing = [], []
@@ -520,17 +522,21 @@ def _aggregates_codes(view, global_dims, z0, rng, group, device, fns):
     gx, gy, gz = global_dims
     ncodes = 256 if view.dataFormat == 4 else 65536
     dev = device if device is not None else "cpu"
-    counts = torch.zeros(ncodes, dtype=torch.int64, device=dev)
-    if rng:
-        fns.count(view, rng[0], rng[1], counts)
-    _all_reduce(counts, dist.ReduceOp.SUM, group)
-    p1, p2, (cmin, cmax) = fns.from_codes(counts, view.dataFormat, view.mappingLo, view.mappingHi, gx * gy * gz)
-    if cmin < 0 or cmax < 0:
-        return None
-    imin, imax = fns.first_codes(view, rng[0], rng[1], z0, cmin, cmax) if rng else (NO_INDEX, NO_INDEX)
-    idx = torch.tensor([min(imin, _I64_MAX), min(imax, _I64_MAX)], dtype=torch.int64, device=dev)
-    _all_reduce(idx, dist.ReduceOp.MIN, group)
-    imin, imax = (int(i) if int(i) != _I64_MAX else NO_INDEX for i in idx.cpu())
+    # the library writes `counts` on its compute stream and the collectives run after torch's
+    # current stream: inside library_stream the two are one stream, whatever the caller has
+    # current; the tensors are allocated there too, so their memory is tied to it
+    with library_stream(torch.device(dev).type == "cuda"):
+        counts = torch.zeros(ncodes, dtype=torch.int64, device=dev)
+        if rng:
+            fns.count(view, rng[0], rng[1], counts)
+        _all_reduce(counts, dist.ReduceOp.SUM, group)
+        p1, p2, (cmin, cmax) = fns.from_codes(counts, view.dataFormat, view.mappingLo, view.mappingHi, gx * gy * gz)
+        if cmin < 0 or cmax < 0:
+            return None
+        imin, imax = fns.first_codes(view, rng[0], rng[1], z0, cmin, cmax) if rng else (NO_INDEX, NO_INDEX)
+        idx = torch.tensor([min(imin, _I64_MAX), min(imax, _I64_MAX)], dtype=torch.int64, device=dev)
+        _all_reduce(idx, dist.ReduceOp.MIN, group)
+        imin, imax = (int(i) if int(i) != _I64_MAX else NO_INDEX for i in idx.cpu())
     p1.minIndex, p1.maxIndex = imin, imax
     out = _lib.Aggregates_t()
     lib.vktHipAggregatesFinish(C.byref(p1), C.byref(p2), gx * gy * gz, gx, gy, C.byref(out))
@@ -588,14 +594,15 @@ def histogram(view, z0: int, first, last, bins, num_bins: int, group=None, count
     import torch.distributed as dist
 
     rng = slab_range(first, last, z0, z0 + view.dimZ)
-    if rng:
-        (count_fn or _gpu_count)(view, rng[0], rng[1], bins, num_bins)
-    else:
-        bins.zero_()
-    if bins.is_cuda and dist.get_backend(group) == "gloo":
-        host = bins.cpu()
-        dist.all_reduce(host, op=dist.ReduceOp.SUM, group=group)
-        bins.copy_(host)
-    else:
-        dist.all_reduce(bins, op=dist.ReduceOp.SUM, group=group)
+    with library_stream(bins.is_cuda):   # the counting kernel and the all_reduce on one stream
+        if rng:
+            (count_fn or _gpu_count)(view, rng[0], rng[1], bins, num_bins)
+        else:
+            bins.zero_()
+        if bins.is_cuda and dist.get_backend(group) == "gloo":
+            host = bins.cpu()
+            dist.all_reduce(host, op=dist.ReduceOp.SUM, group=group)
+            bins.copy_(host)
+        else:
+            dist.all_reduce(bins, op=dist.ReduceOp.SUM, group=group)
     return bins
