@@ -398,6 +398,33 @@ VKTAPI vktError vktHipAggregatesFromCodes(uint64_t const* counts, int32_t dataFo
 VKTAPI vktError vktHipAggregateFirstCodes(vktHipVolumeView_t volume, vktVec3i_t first, vktVec3i_t last,
                                           int32_t zGlobalOffset, int32_t minCode, int32_t maxCode,
                                           uint64_t* indices);
+/* Slabs in ONE pass of moments (the moments forms of vktHipAggregatesRange, DESIGN.md §4.8:
+ * UInt16 -- exact integer moments under the unit mapping, float moments otherwise -- and
+ * Float32): every rank reduces its range to one vktHipMomentPartial_t (vktHipAggregateMoments;
+ * global indices as vktHipAggregatesPass; an empty range gives count 0), the partials are
+ * exchanged (e.g. one all-gather of sizeof(vktHipMomentPartial_t) bytes per rank) and
+ * vktHipAggregatesFromMoments combines them IN THE ORDER GIVEN (rank order: deterministic) and
+ * finishes the aggregates of the whole volume.  *complete = 0 when the float form's terms may
+ * leave the normal float range (non-finite / huge / tiny values: use the two passes, as
+ * vktHipAggregatesRange does); every rank gets the same answer from the same partials.
+ * vktHipAggregateMoments returns vktInvalidValue for a format / range that takes no moments
+ * form (vktHipAggregateMomentsSupported: 1 when it does, empty ranges included). */
+typedef struct {
+    uint64_t count;
+    uint64_t codeSum, codeSumSqLo, codeSumSqHi;   /* form 1: sum of the codes, 128-bit sum of their squares */
+    double mean, m2;                             /* form 2: mean, sum of squared deviations of the values */
+    double sum, prod;                            /* form 2: sum; both forms: product of the values */
+    float minValue, maxValue;
+    uint64_t minIndex, maxIndex;                 /* global linear indices, ~0 = none */
+    int32_t form;                                /* 1 integer (UInt16, unit mapping), 2 float */
+    uint32_t flags;                              /* form 2: bit 0 non-finite value, bit 1 tiny value */
+} vktHipMomentPartial_t;
+VKTAPI int32_t vktHipAggregateMomentsSupported(vktHipVolumeView_t volume, vktVec3i_t first, vktVec3i_t last);
+VKTAPI vktError vktHipAggregateMoments(vktHipVolumeView_t volume, vktVec3i_t first, vktVec3i_t last,
+                                       int32_t zGlobalOffset, vktHipMomentPartial_t* partial);
+VKTAPI vktError vktHipAggregatesFromMoments(vktHipMomentPartial_t const* partials, int32_t numPartials,
+                                            uint64_t numElems, int32_t dimX, int32_t dimY,
+                                            vktAggregates_t* aggregates, int32_t* complete);
 
 /* replaces ComputeHistogramRange_cuda (reference src/vkt/Histogram_cuda.cu:45-76, which
  * ignores `first`); semantics of ComputeHistogramRange_serial (src/vkt/Histogram_serial.hpp:

@@ -77,7 +77,8 @@ def _worker(rank, port, q):
                                   bins.cpu().numpy().copy())
         # UInt8 / UInt16 slabs: the one-pass code-count form (counts on the device, all_reduce,
         # first-occurrence search per slab, all_reduce MIN of the indices)
-        for fmt, mapping in ((5, (-1.0, 3.0)), (4, (0.0, 1.0)), (4, (3.0, -1.0))):
+        # (UInt16 / Float32 take the one-pass moments form: one all_gather of moment partials)
+        for fmt, mapping in ((5, (-1.0, 3.0)), (5, (0.0, 1.0)), (4, (0.0, 1.0)), (4, (3.0, -1.0))):
             codes = _code_volume(fmt)
             cz, cy, cx = codes.shape
             c0, c1 = slab.slab_bounds(cz, WORLD, rank)

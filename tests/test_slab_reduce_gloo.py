@@ -258,3 +258,126 @@ def test_slab_code_count_aggregates(world, case):
     assert abs(s - ref.sum) <= n * 2.0 ** -24 * abs(ref.sum) + 1e-6
     assert abs(mean - ref.mean) <= n * 2.0 ** -24 * abs(ref.mean) + 1e-7
     assert abs(var - ref.var) <= 4 * n * 2.0 ** -24 * abs(ref.var) + 1e-7
+
+
+# ---- UInt16 / Float32 slabs in one pass of moments (slab._aggregates_moments) --------------------
+class NumpyMomentFns:
+    """numpy restatement of the per-rank step vktHipAggregateMoments (aggregatesMomentsU16Kernel /
+    aggregatesMomentsFKernel + their combine): form 1 exact integer sums of the UInt16 codes under the
+    unit mapping, form 2 the mean and the sum of squared deviations of the values (float64), min / max
+    with first-occurrence global indices; the combine across ranks and the finish are the library's
+    own host code (vktHipAggregatesFromMoments)."""
+
+    @staticmethod
+    def supported(view, first, last):
+        return True
+
+    @staticmethod
+    def moments(view, first, last, z0):
+        from volkit_amd import _lib
+        p = _lib.HipMomentPartial_t()
+        unit = view.dataFormat == 5 and view.mappingLo == 0.0 and view.mappingHi == 1.0 \
+            and np.copysign(1.0, view.mappingLo) > 0
+        p.form = 1 if unit else 2
+        p.prod, p.minValue, p.maxValue = 1.0, FLT_MAX, -FLT_MAX
+        p.minIndex = p.maxIndex = (1 << 64) - 1
+        if first == last or any(a >= b for a, b in zip(first, last)):
+            return p
+        box = view.vals[first[2]:last[2], first[1]:last[1], first[0]:last[0]]
+        v = box.reshape(-1)
+        gy, gx = view.vals.shape[1], view.vals.shape[2]
+        zz, yy, xx = np.meshgrid(np.arange(first[2], last[2]) + z0, np.arange(first[1], last[1]),
+                                 np.arange(first[0], last[0]), indexing="ij")
+        gidx = ((zz.astype(np.uint64) * gy + yy) * gx + xx).reshape(-1)
+        p.count = v.size
+        m = v.min()
+        p.minValue, p.minIndex = float(m), int(gidx[np.argmax(v == m)])
+        m = v.max()
+        p.maxValue, p.maxIndex = float(m), int(gidx[np.argmax(v == m)])
+        p.prod = float(np.prod(v.astype(np.float64)))
+        if unit:
+            c = view.codes[first[2]:last[2], first[1]:last[1], first[0]:last[0]].reshape(-1).astype(object)
+            s2 = int(sum(int(x) * int(x) for x in c))
+            p.codeSum = int(sum(int(x) for x in c))
+            p.codeSumSqLo, p.codeSumSqHi = s2 & ((1 << 64) - 1), s2 >> 64
+        else:
+            d = v.astype(np.float64)
+            p.mean = float(d.mean())
+            p.m2 = float(np.sum((d - p.mean) ** 2))
+            p.sum = float(np.sum(d))
+            a = np.abs(v)
+            p.flags = (1 if not np.all(np.isfinite(v)) else 0) | (2 if np.any((a < 2.0 ** -40) & (a != 0)) else 0)
+        return p
+
+
+def _moments_worker(rank, world, port, case, q):
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from volkit_amd import slab
+        fmt, (lo, hi), dims, first, last = case
+        gx, gy, gz = dims
+        if fmt == 7:
+            codes = np.random.default_rng(5).uniform(-2.0, 3.0, (gz, gy, gx)).astype(np.float32)
+            codes[2, 1, 3] = codes[gz - 2, 0, 1] = -2.5
+            vals = codes
+        else:
+            codes = _codes_volume(fmt, dims)
+            vals = code_values(fmt, lo, hi, 65536)[codes.astype(np.int64)]
+        z0, z1 = slab.slab_bounds(gz, world, rank)
+        view = NumpyCodeSlab(codes[z0:z1], fmt, lo, hi, vals[z0:z1])
+        agg = slab.aggregates(view, dims, z0, first, last, pass_fn=numpy_pass, moment_fns=NumpyMomentFns)
+        q.put((rank, (agg.min, agg.max, (agg.argmin.x, agg.argmin.y, agg.argmin.z),
+                      (agg.argmax.x, agg.argmax.y, agg.argmax.z), agg.sum, agg.mean, agg.var)))
+        dist.destroy_process_group()
+    except Exception:   # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("case", [(5, (0.0, 1.0), (12, 9, 10), (0, 0, 0), (12, 9, 10)),     # integer form
+                                  (5, (0.0, 1.0), (12, 9, 10), (2, 1, 3), (11, 9, 9)),
+                                  (5, (-1.0, 3.0), (12, 9, 10), (1, 0, 1), (12, 8, 10)),    # float form
+                                  (7, (0.0, 1.0), (12, 9, 10), (0, 0, 0), (12, 9, 10)),
+                                  (7, (0.0, 1.0), (12, 9, 10), (3, 0, 8), (9, 9, 10))])     # a rank with none
+def test_slab_moment_aggregates(world, case):
+    """slab.aggregates on UInt16 / Float32 slabs: per-rank moment partials, ONE all_gather, the
+    library's in-order combine and finish (vktHipAggregatesFromMoments, host code) == the
+    whole-volume oracle; var within the moments bound of tests/test_reduce.py."""
+    from oracle import binding as ob
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_moments_worker, args=(r, world, port, case, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for r, agg in res:
+        assert not isinstance(agg, str), agg
+    fmt, (lo, hi), dims, first, last = case
+    gx, gy, gz = dims
+    if fmt == 7:
+        codes = np.random.default_rng(5).uniform(-2.0, 3.0, (gz, gy, gx)).astype(np.float32)
+        codes[2, 1, 3] = codes[gz - 2, 0, 1] = -2.5
+        ref = ob.aggregates_range(ob.Volume(codes.view(np.uint32), 7), first, last)
+        vals = codes
+    else:
+        codes = _codes_volume(fmt, dims)
+        ref = ob.aggregates_range(ob.Volume(codes, fmt, lo, hi), first, last)
+        vals = code_values(fmt, lo, hi, 65536)[codes.astype(np.int64)]
+    aggs = {r: a for r, a in res}
+    assert len(set(aggs.values())) == 1
+    mn, mx, amin, amax, s, mean, var = aggs[0]
+    assert (mn, mx, amin, amax) == (ref.min, ref.max, tuple(ref.argmin), tuple(ref.argmax))
+    box = vals[first[2]:last[2], first[1]:last[1], first[0]:last[0]].reshape(-1)
+    n, nall = box.size, codes.size
+    assert abs(s - ref.sum) <= n * 2.0 ** -24 * float(np.sum(np.abs(box), dtype=np.float64)) + 1e-6
+    assert mean == np.float32(np.float64(np.float32(s)) / nall)
+    d = (box - np.float32(mean)).astype(np.float32)
+    var_terms = float(np.float32(np.float64(np.float32(np.sum((d * d).astype(np.float32), dtype=np.float64))) / nall))
+    ulp = float(np.spacing(np.float32(var_terms)))
+    assert abs(var - var_terms) <= 3 * 2.0 ** -24 * var_terms + 2 * ulp, (var, var_terms)

@@ -102,6 +102,13 @@ class HipAggregatePartial_t(C.Structure):
     _fields_ = [("sum", C.c_double), ("prod", C.c_double), ("sumSq", C.c_double), ("minValue", f32),
                 ("maxValue", f32), ("minIndex", u64), ("maxIndex", u64), ("count", u64)]
 
+class HipMomentPartial_t(C.Structure):
+    _fields_ = [("count", u64), ("codeSum", u64), ("codeSumSqLo", u64), ("codeSumSqHi", u64),
+                ("mean", C.c_double), ("m2", C.c_double), ("sum", C.c_double), ("prod", C.c_double),
+                ("minValue", f32), ("maxValue", f32), ("minIndex", u64), ("maxIndex", u64),
+                ("form", i32), ("flags", C.c_uint32)]
+
+
 class Vec3fC_t(C.Structure):
     _fields_ = [("x", C.c_float), ("y", C.c_float), ("z", C.c_float)]
 
@@ -293,6 +300,9 @@ SIGNATURES = {
     "vktComputeHistogramRangeSV": (c_err, [c_vol, c_hist, i32, i32, i32, i32, i32, i32]),
     "vktHipAggregatesRange": (c_err, [HipVolumeView_t, Vec3i_t, Vec3i_t, P(Aggregates_t)]),
     "vktHipAggregatePartialInit": (c_err, [P(HipAggregatePartial_t)]),
+    "vktHipAggregateMomentsSupported": (i32, [HipVolumeView_t, Vec3i_t, Vec3i_t]),
+    "vktHipAggregateMoments": (c_err, [HipVolumeView_t, Vec3i_t, Vec3i_t, i32, P(HipMomentPartial_t)]),
+    "vktHipAggregatesFromMoments": (c_err, [P(HipMomentPartial_t), i32, u64, i32, i32, P(Aggregates_t), P(i32)]),
     "vktHipAggregatePartialCombine": (c_err, [P(HipAggregatePartial_t), P(HipAggregatePartial_t)]),
     "vktHipAggregatesMean": (f32, [P(HipAggregatePartial_t), u64]),
     "vktHipAggregatesPass": (c_err, [HipVolumeView_t, Vec3i_t, Vec3i_t, i32, i32, f32, P(HipAggregatePartial_t)]),

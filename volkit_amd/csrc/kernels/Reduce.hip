@@ -1899,6 +1899,36 @@ namespace hipk
         res[1] = two;
     }
 
+    // One workgroup: the n partials of a moments kernel combined (same order and tree as the
+    // final kernels) into out[0], not finished -- one rank's part of a Z-slab volume
+    // (vktHipAggregateMoments).
+    __global__ __launch_bounds__(kBlock) void momentsCombineU16Kernel(MomentPartialU16 const* partials, uint32_t n,
+                                                                     MomentPartialU16* out)
+    {
+        MomentPartialU16 p;
+        p.count = p.sumC = p.sumSqLo = p.sumSqHi = 0;
+        p.prod = 1.0;
+        p.cmin = 0x10000u;
+        p.cmax = -1;
+        p.minIndex = p.maxIndex = kNoIndex;
+        for (uint32_t i = threadIdx.x; i < n; i += kBlock)
+            momentCombine(p, partials[i]);
+        momentBlockReduce<kBlock / 64>(p);
+        if (threadIdx.x == 0)
+            *out = p;
+    }
+
+    __global__ __launch_bounds__(kBlock) void momentsCombineFKernel(MomentPartialF const* partials, uint32_t n,
+                                                                   MomentPartialF* out)
+    {
+        MomentPartialF p = emptyMomentF();
+        for (uint32_t i = threadIdx.x; i < n; i += kBlock)
+            momentCombineF(p, partials[i]);
+        momentBlockReduceF<kBlock / 64>(p);
+        if (threadIdx.x == 0)
+            *out = p;
+    }
+
     // The first voxels of item `item` holding codes tmin / tmax, folded into *bMin / *bMax with
     // atomicMin (LDS or global).
     template <int BPV, bool CONTIG>
@@ -2512,6 +2542,27 @@ namespace hipk
         return streamingGrid(h.items, 64u * 4u * (kBlock / 64), 8);
     }
 
+    // 1 when some UInt16 code decodes to a nonzero |v| < 2^-40 under (lo, hi): every code once on
+    // the host, the answer kept per thread for the last mapping
+    uint32_t tinyCodesU16(float lo, float hi)
+    {
+        thread_local uint64_t lastKey = ~0ull;
+        thread_local uint32_t lastTiny = 0;
+        uint64_t const key = static_cast<uint64_t>(codec::floatToBits(lo)) << 32 | codec::floatToBits(hi);
+        if (key != lastKey)
+        {
+            uint32_t t = 0;
+            for (uint32_t c = 0; c < 65536u && !t; ++c)
+            {
+                float const v = std::fabs(codec::decode(c, codec::FmtUInt16, lo, hi));
+                t = v != 0.f && v < 0x1p-40f ? 1u : 0u;
+            }
+            lastKey = key;
+            lastTiny = t;
+        }
+        return lastTiny;
+    }
+
     // UInt16 under any other mapping and Float32: one pass of floating-point moments
     // (aggregatesMomentsFKernel); knob aggregates.moments bit 1.  0 when the range does not take
     // it, else the number of partials.  tiny: some UInt16 code decodes to a nonzero |v| < 2^-40.
@@ -2522,24 +2573,7 @@ namespace hipk
         if (!fmtOk || (rt::knob(rt::Knob::AggregatesMoments) & 2) == 0 || !makeSpanArgs(a, h, contig))
             return 0;
         if (a.fmt == codec::FmtUInt16)
-        {
-            // every code's value once on the host (kept per thread for the last mapping)
-            thread_local uint64_t lastKey = ~0ull;
-            thread_local uint32_t lastTiny = 0;
-            uint64_t const key = static_cast<uint64_t>(codec::floatToBits(a.lo)) << 32 | codec::floatToBits(a.hi);
-            if (key != lastKey)
-            {
-                uint32_t t = 0;
-                for (uint32_t c = 0; c < 65536u && !t; ++c)
-                {
-                    float const v = std::fabs(codec::decode(c, codec::FmtUInt16, a.lo, a.hi));
-                    t = v != 0.f && v < 0x1p-40f ? 1u : 0u;
-                }
-                lastKey = key;
-                lastTiny = t;
-            }
-            tiny = lastTiny;
-        }
+            tiny = tinyCodesU16(a.lo, a.hi);
         return streamingGrid(h.items, 64u * 4u * (kBlock / 64), 8);
     }
 
@@ -2834,6 +2868,225 @@ vktError vktHipAggregatesRange(vktHipVolumeView_t volume, vktVec3i_t first, vktV
     else if (!done && e != vktNoError)
         return e;
     return vktHipAggregatesFinish(&p1, &p2, numElems, volume.dimX, volume.dimY, out);
+}
+
+int32_t vktHipAggregateMomentsSupported(vktHipVolumeView_t volume, vktVec3i_t first, vktVec3i_t last)
+{
+    if (volume.dataFormat != codec::FmtUInt16 && volume.dataFormat != codec::FmtFloat32)
+        return 0;
+    BoxArgs a{};
+    vktError e;
+    if (!makeBox(volume, first, last, 0, a, "vktHipAggregateMomentsSupported: invalid volume view", e))
+        return e == vktNoError ? 1 : 0;   // an empty range: count 0
+    FastHistArgs h;
+    bool contig;
+    return makeSpanArgs(a, h, contig) ? 1 : 0;
+}
+
+vktError vktHipAggregateMoments(vktHipVolumeView_t volume, vktVec3i_t first, vktVec3i_t last, int32_t zGlobalOffset,
+                                vktHipMomentPartial_t* partial)
+{
+    if (partial == nullptr)
+        return rt::fail("vktHipAggregateMoments: null partial");
+    if (volume.dataFormat != codec::FmtUInt16 && volume.dataFormat != codec::FmtFloat32)
+        return rt::fail("vktHipAggregateMoments: UInt16 / Float32 volumes only");
+    bool const integer = volume.dataFormat == codec::FmtUInt16 && codec::isUnitMapping(volume.mappingLo, volume.mappingHi);
+    vktHipMomentPartial_t& o = *partial;
+    std::memset(&o, 0, sizeof(o));
+    o.prod = 1.0;
+    o.minValue = FLT_MAX;
+    o.maxValue = -FLT_MAX;
+    o.minIndex = o.maxIndex = kNoIndex;
+    o.form = integer ? 1 : 2;
+    o.flags = !integer && volume.dataFormat == codec::FmtUInt16 && tinyCodesU16(volume.mappingLo, volume.mappingHi)
+                  ? 2u
+                  : 0u;
+    BoxArgs a{};
+    vktError e;
+    if (!makeBox(volume, first, last, zGlobalOffset, a, "vktHipAggregateMoments: invalid volume view", e))
+        return e;   // empty range: the empty partial
+    FastHistArgs h;
+    bool contig;
+    if (!makeSpanArgs(a, h, contig))
+        return rt::fail("vktHipAggregateMoments: the range does not take the moments walk (16-B aligned volume with "
+                        "dimX % 8 == 0 needed)");
+    unsigned const g = streamingGrid(h.items, 64u * 4u * (kBlock / 64), 8);
+    hipStream_t s = rt::computeStream();
+    AggScratch& sc = aggScratch();
+    size_t const unit = std::max(sizeof(MomentPartialU16), sizeof(MomentPartialF));
+    auto* parts = static_cast<uint8_t*>(sc.dev.acquire((static_cast<size_t>(g) + 1) * unit, s));
+    if (!parts)
+        return vktInvalidValue;
+    union
+    {
+        MomentPartialU16 u;
+        MomentPartialF f;
+    } host;
+    if (integer)
+    {
+        auto* pp = reinterpret_cast<MomentPartialU16*>(parts);
+        if (contig)
+            hipLaunchKernelGGL(aggregatesMomentsU16Kernel<true>, dim3(g), dim3(kBlock), 0, s, h, pp);
+        else
+            hipLaunchKernelGGL(aggregatesMomentsU16Kernel<false>, dim3(g), dim3(kBlock), 0, s, h, pp);
+        hipLaunchKernelGGL(momentsCombineU16Kernel, dim3(1), dim3(kBlock), 0, s, pp, g, pp + g);
+        e = rt::check(hipMemcpyAsync(&host.u, pp + g, sizeof(host.u), hipMemcpyDeviceToHost, s), "hipMemcpyAsync");
+    }
+    else
+    {
+        auto* pp = reinterpret_cast<MomentPartialF*>(parts);
+        if (a.fmt == codec::FmtUInt16)
+        {
+            if (contig)
+                hipLaunchKernelGGL((aggregatesMomentsFKernel<codec::FmtUInt16, true>), dim3(g), dim3(kBlock), 0, s, h, pp);
+            else
+                hipLaunchKernelGGL((aggregatesMomentsFKernel<codec::FmtUInt16, false>), dim3(g), dim3(kBlock), 0, s, h,
+                                   pp);
+        }
+        else if (contig)
+            hipLaunchKernelGGL((aggregatesMomentsFKernel<codec::FmtFloat32, true>), dim3(g), dim3(kBlock), 0, s, h, pp);
+        else
+            hipLaunchKernelGGL((aggregatesMomentsFKernel<codec::FmtFloat32, false>), dim3(g), dim3(kBlock), 0, s, h, pp);
+        hipLaunchKernelGGL(momentsCombineFKernel, dim3(1), dim3(kBlock), 0, s, pp, g, pp + g);
+        e = rt::check(hipMemcpyAsync(&host.f, pp + g, sizeof(host.f), hipMemcpyDeviceToHost, s), "hipMemcpyAsync");
+    }
+    sc.dev.release(s);
+    if (e != vktNoError)
+        return e;
+    VKT_HIP_TRY(hipStreamSynchronize(s));
+    if (integer)
+    {
+        MomentPartialU16 const& u = host.u;
+        o.count = u.count;
+        o.codeSum = u.sumC;
+        o.codeSumSqLo = u.sumSqLo;
+        o.codeSumSqHi = u.sumSqHi;
+        o.prod = u.prod;
+        if (u.cmin <= 0xFFFFu)
+        {
+            o.minValue = static_cast<float>(u.cmin) * 0x1p-16f;
+            o.minIndex = u.minIndex;
+        }
+        if (u.cmax >= 0)
+        {
+            o.maxValue = static_cast<float>(u.cmax) * 0x1p-16f;
+            o.maxIndex = u.maxIndex;
+        }
+    }
+    else
+    {
+        MomentPartialF const& f = host.f;
+        o.count = f.count;
+        o.mean = f.mean;
+        o.m2 = f.m2;
+        o.sum = f.sum;
+        o.prod = f.prod;
+        o.minValue = f.minValue;
+        o.maxValue = f.maxValue;
+        o.minIndex = f.minIndex;
+        o.maxIndex = f.maxIndex;
+        o.flags |= f.flags;
+    }
+    return rt::finishLaunch("AggregateMoments_hip");
+}
+
+// Host combine of rank partials in the given order + the finish of the final kernels
+// (aggregatesMomentsU16FinalKernel / aggregatesMomentsFFinalKernel: the same formulas).
+vktError vktHipAggregatesFromMoments(vktHipMomentPartial_t const* partials, int32_t numPartials, uint64_t numElems,
+                                     int32_t dimX, int32_t dimY, vktAggregates_t* aggregates, int32_t* complete)
+{
+    if (partials == nullptr || aggregates == nullptr || complete == nullptr || numPartials <= 0)
+        return rt::fail("vktHipAggregatesFromMoments: null pointer or no partials");
+    int32_t const form = partials[0].form;
+    if (form != 1 && form != 2)
+        return rt::fail("vktHipAggregatesFromMoments: unknown partial form");
+    vktHipAggregatePartial_t one, two;
+    vktHipAggregatePartialInit(&one);
+    vktHipAggregatePartialInit(&two);
+    double const N = static_cast<double>(numElems);
+    uint64_t count = 0;
+    bool ok = true;
+    auto extremes = [&](vktHipMomentPartial_t const& q) {
+        if (q.minIndex != kNoIndex &&
+            (q.minValue < one.minValue || (q.minValue == one.minValue && q.minIndex < one.minIndex)))
+        {
+            one.minValue = q.minValue;
+            one.minIndex = q.minIndex;
+        }
+        if (q.maxIndex != kNoIndex &&
+            (q.maxValue > one.maxValue || (q.maxValue == one.maxValue && q.maxIndex < one.maxIndex)))
+        {
+            one.maxValue = q.maxValue;
+            one.maxIndex = q.maxIndex;
+        }
+    };
+    if (form == 1)
+    {
+        uint64_t sc = 0;
+        unsigned __int128 sc2 = 0;
+        for (int32_t i = 0; i < numPartials; ++i)
+        {
+            vktHipMomentPartial_t const& q = partials[i];
+            if (q.form != form)
+                return rt::fail("vktHipAggregatesFromMoments: partials of different forms");
+            count += q.count;
+            sc += q.codeSum;
+            sc2 += (static_cast<unsigned __int128>(q.codeSumSqHi) << 64) | q.codeSumSqLo;
+            one.prod *= q.prod;
+            extremes(q);
+        }
+        one.sum = static_cast<double>(sc) * 0x1p-16;
+        float const m = static_cast<float>(static_cast<double>(static_cast<float>(one.sum)) / N);
+        double const mu = static_cast<double>(m) * 65536.0;
+        unsigned __int128 const t = static_cast<unsigned __int128>(count) * sc2 - static_cast<unsigned __int128>(sc) * sc;
+        double const td = static_cast<double>(static_cast<uint64_t>(t >> 64)) * 0x1p64 + static_cast<double>(static_cast<uint64_t>(t));
+        double const dn = static_cast<double>(count);
+        double const r = std::fma(-dn, mu, static_cast<double>(sc));
+        two.sumSq = count ? (td + r * r) / dn * 0x1p-32 : 0.0;
+    }
+    else
+    {
+        double mean = 0.0, m2 = 0.0;
+        uint32_t flags = 0;
+        for (int32_t i = 0; i < numPartials; ++i)
+        {
+            vktHipMomentPartial_t const& q = partials[i];
+            if (q.form != form)
+                return rt::fail("vktHipAggregatesFromMoments: partials of different forms");
+            flags |= q.flags;
+            if (q.count != 0)
+            {
+                if (count == 0)
+                {
+                    mean = q.mean;
+                    m2 = q.m2;
+                }
+                else
+                {
+                    double const na = static_cast<double>(count), nb = static_cast<double>(q.count);
+                    double const n = na + nb, delta = q.mean - mean;
+                    mean += delta * (nb / n);
+                    m2 += q.m2 + delta * delta * (na * nb / n);
+                }
+            }
+            count += q.count;
+            one.sum += q.sum;
+            one.prod *= q.prod;
+            extremes(q);
+        }
+        float const m = static_cast<float>(static_cast<double>(static_cast<float>(one.sum)) / N);
+        double const dm = static_cast<double>(m);
+        ok = (flags & 1u) == 0 && std::fabs(one.sum) <= DBL_MAX && m2 <= DBL_MAX && (flags & 2u) == 0 &&
+             (m == 0.f || std::fabs(m) >= 0x1p-40f);
+        if (count != 0)
+            ok = ok && std::fabs(static_cast<double>(one.maxValue) - dm) < 0x1p62 &&
+                 std::fabs(static_cast<double>(one.minValue) - dm) < 0x1p62;
+        double const dd = mean - dm;
+        two.sumSq = count ? m2 + static_cast<double>(count) * dd * dd : 0.0;
+    }
+    one.count = count;
+    *complete = ok ? 1 : 0;
+    return vktHipAggregatesFinish(&one, &two, numElems, dimX, dimY, aggregates);
 }
 
 vktError vktHipAggregateCodeCounts(vktHipVolumeView_t volume, vktVec3i_t first, vktVec3i_t last, uint64_t* counts)

@@ -443,8 +443,8 @@ def _gpu_pass(view, first, last, z0, pass_no, mean):
 
 
 def _allgather_partials(p, group=None, device=None):
-    """Every rank's partial, in rank order (one all_gather of PARTIAL_BYTES per rank; on a
-    device tensor for nccl, a host tensor for gloo)."""
+    """Every rank's partial (a ctypes structure), in rank order (one all_gather of its bytes per
+    rank; on a device tensor for nccl, a host tensor for gloo)."""
     import torch
     import torch.distributed as dist
 
@@ -454,7 +454,7 @@ def _allgather_partials(p, group=None, device=None):
     world = dist.get_world_size(group)
     out = [torch.empty_like(mine) for _ in range(world)]
     dist.all_gather(out, mine, group=group)
-    return [_lib.HipAggregatePartial_t.from_buffer_copy(bytes(t.cpu().numpy())) for t in out]
+    return [type(p).from_buffer_copy(bytes(t.cpu().numpy())) for t in out]
 
 
 def combine_partials(parts):
@@ -510,6 +510,37 @@ class GpuCodeFns:
         return idx[0], idx[1]
 
 
+class GpuMomentFns:
+    """The moments form's per-rank steps on the GPU (include/volkit_hip.h vktHipAggregateMoments)."""
+
+    @staticmethod
+    def supported(view, first, last) -> bool:
+        return bool(lib.vktHipAggregateMomentsSupported(view, _lib.Vec3i_t(*first), _lib.Vec3i_t(*last)))
+
+    @staticmethod
+    def moments(view, first, last, z0):
+        p = _lib.HipMomentPartial_t()
+        if lib.vktHipAggregateMoments(view, _lib.Vec3i_t(*first), _lib.Vec3i_t(*last), z0, C.byref(p)) != 0:
+            raise RuntimeError(_lib.last_error())
+        return p
+
+
+def _aggregates_moments(view, global_dims, z0, first, last, rng, group, device, fns):
+    """UInt16 / Float32 slabs in one data pass: every rank's 128-byte moments partial (exact
+    integer sums under the UInt16 unit mapping, float moments otherwise), ONE all_gather, combined
+    in rank order (deterministic, identical on every rank) and finished on the host.  None when
+    the float form says its terms may leave the float range (the caller runs the two passes; every
+    rank reaches the same answer from the same partials)."""
+    gx, gy, gz = global_dims
+    p = fns.moments(view, *(rng or (first, first)), z0)
+    parts = _allgather_partials(p, group, device)
+    arr = (_lib.HipMomentPartial_t * len(parts))(*parts)
+    out, complete = _lib.Aggregates_t(), C.c_int32(0)
+    if lib.vktHipAggregatesFromMoments(arr, len(parts), gx * gy * gz, gx, gy, C.byref(out), C.byref(complete)) != 0:
+        raise RuntimeError(_lib.last_error())
+    return out if complete.value else None
+
+
 def _aggregates_codes(view, global_dims, z0, rng, group, device, fns):
     """UInt8 / UInt16 slabs in one data pass: local code counts, ONE all_reduce(SUM) of them, the
     aggregates from the global counts (identical on every rank), a first-occurrence search of
@@ -543,20 +574,32 @@ def _aggregates_codes(view, global_dims, z0, rng, group, device, fns):
     return out
 
 
-def aggregates(view, global_dims, z0: int, first, last, group=None, device=None, pass_fn=None, code_fns=None):
+def aggregates(view, global_dims, z0: int, first, last, group=None, device=None, pass_fn=None, code_fns=None,
+               moment_fns=None):
     """ComputeAggregatesRange over a Z-slab partitioned volume: each rank reduces its planes
     (pass 1), partials are all-gathered and combined in rank order (deterministic), the
     reference's float mean of the WHOLE volume follows, then pass 2 and a second exchange.
-    UInt8 / UInt16 volumes whose every slab takes the code-count walk use ONE data pass
-    instead (_aggregates_codes; `code_fns` replaces the GPU steps, e.g. in CPU tests; a custom
-    `pass_fn` alone keeps the two passes).
-    `view` is this rank's slab (global planes [z0, z0 + view.dimZ)); returns Aggregates_t."""
+    UInt16 / Float32 volumes whose every slab takes the moments walk use ONE data pass and one
+    all_gather of 128-byte moment partials (_aggregates_moments; `moment_fns` replaces the GPU
+    steps), UInt8 (and UInt16 when that is off) one pass of code counts (_aggregates_codes;
+    `code_fns` replaces the GPU steps, e.g. in CPU tests); a custom `pass_fn` alone keeps the two
+    passes.  `view` is this rank's slab (global planes [z0, z0 + view.dimZ)); returns Aggregates_t."""
     import torch
     import torch.distributed as dist
 
     gx, gy, gz = global_dims
     rng = slab_range(first, last, z0, z0 + view.dimZ)
-    if getattr(view, "dataFormat", None) in (4, 5) and (code_fns is not None or pass_fn is None):
+    fmt = getattr(view, "dataFormat", None)
+    if fmt in (5, 7) and (moment_fns is not None or (code_fns is None and pass_fn is None)):
+        fns = moment_fns or GpuMomentFns
+        ok = torch.tensor([1 if fns.supported(view, *(rng or (first, first))) else 0], dtype=torch.int64,
+                          device=device if device is not None else "cpu")
+        _all_reduce(ok, dist.ReduceOp.MIN, group)
+        if int(ok.item()):
+            out = _aggregates_moments(view, global_dims, z0, first, last, rng, group, device, fns)
+            if out is not None:
+                return out
+    if fmt in (4, 5) and (code_fns is not None or pass_fn is None):
         fns = code_fns or GpuCodeFns
         ok = torch.tensor([1 if fns.supported(view, *(rng or (first, first))) else 0], dtype=torch.int64,
                           device=device if device is not None else "cpu")
