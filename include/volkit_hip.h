@@ -116,7 +116,8 @@ VKTAPI vktError vktHipKernelScopeEnd(vktHipKernelScope scope);
  * device buffer of <= 4 MiB its own hipMalloc instead of a 256-B class of a 64-MiB pooled chunk), "memory.arena" (1; 0 gives every larger buffer its
  * own hipMalloc instead of a 2-MiB aligned block of an arena chunk), "memory.arena_chunk_mib" (0; > 0 makes
  * new arena chunks exactly max(request, value MiB): tests), "decompose.block" (256; 128 copies each
- * 16-KiB BrickDecompose chunk with 128 threads), "aggregates.moments" (3; bit 0: UInt16
+ * 16-KiB BrickDecompose chunk with 128 threads), "pointwise.dword_shift" (1; 0 keeps the byte-align
+ * stage of the general path's window shift for 4-byte voxels at 4-B aligned addresses), "aggregates.moments" (3; bit 0: UInt16
  * ComputeAggregates under the unit mapping from one pass of exact integer moments, bit 1: UInt16
  * under other mappings and Float32 from one pass of floating-point moments -- both instead of
  * "aggregates.codes" / the two float passes).  For tests and in-process A/B measurements; unknown names return

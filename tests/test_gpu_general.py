@@ -638,3 +638,37 @@ def test_uint8_long_edge_free_rows_on_the_general_path(lib, o, k):
                       f"u8 copy k={k} {first}->{last} dst+64")
     finally:
         L.vktHipSetTuningKnob(b"pointwise.u8_pairs", -1)
+
+
+@pytest.mark.parametrize("dword", [1, 0])
+@pytest.mark.parametrize("wide", [0, 1])
+def test_float32_dword_shift(lib, o, dword, wide):
+    """4-byte voxels at 4-B aligned addresses shift their windows by whole dwords (knob
+    pointwise.dword_shift: the byte-align stage skipped), on the 8-voxel and the 16-B item layouts
+    (knob pointwise.f32_wide): copies at every source x phase against several destination phases,
+    an arithmetic dstOffset, 4-B aligned but not 16-B aligned view pointers (and, byte-offset
+    pointers, which must keep the byte-align stage)."""
+    rng = np.random.default_rng(5 + dword + 2 * wide)
+    src = rand_codes(rng, 7, (4, 6, 45))
+    b2 = rand_codes(rng, 7, (4, 6, 45))
+    dinit = rand_codes(rng, 7, (5, 7, 53))
+    assert lib.vktHipSetTuningKnob(b"pointwise.dword_shift", dword) == 0
+    assert lib.vktHipSetTuningKnob(b"pointwise.f32_wide", wide) == 0
+    try:
+        for spad, dpad in ((0, 0), (4, 0), (0, 12), (8, 4)):
+            for sx in range(5):
+                for dx in (0, 1, 3, 6):
+                    copy_case(lib, o, 7, 7, (0.0, 1.0), (0.0, 1.0), src, dinit, (sx, 1, 0), (sx + 37, 6, 4), (dx, 0, 1),
+                              spad, dpad, what=f"dword={dword} wide={wide} pads {spad},{dpad} sx={sx} dx={dx}")
+        for spad in (1, 2):   # byte-offset views (not 4-B aligned): the byte-align stage runs
+            copy_case(lib, o, 7, 7, (0.0, 1.0), (0.0, 1.0), src, dinit, (3, 0, 0), (40, 6, 4), (0, 0, 0), spad, 0,
+                      what=f"dword={dword} byte pad {spad}")
+        for dx in range(8):
+            da, db, dd = Dev(src, 7), Dev(b2, 7, pad=4), Dev(dinit, 7)
+            assert lib.vktHipArithmeticRange(0, dd.view, da.view, db.view, vec((3, 1, 1)), vec((40, 5, 3)),
+                                             vec((dx, 1, 1))) == 0
+            ref = o.arith("Sum", [7] * 3, [(0.0, 1.0)] * 3, src, b2, dinit.copy(), (3, 1, 1), (40, 5, 3), (dx, 1, 1))
+            assert_codes_equal(dd.read(), ref, 7, f"Sum dword={dword} wide={wide} dx={dx}")
+    finally:
+        lib.vktHipSetTuningKnob(b"pointwise.dword_shift", -1)
+        lib.vktHipSetTuningKnob(b"pointwise.f32_wide", -1)

@@ -235,6 +235,32 @@ def main():
                 report(f"f32shift CopyRange 800^3 x0=100 same offset {name}",
                        timed(lambda: lib.vktHipCopyRange(D, A, f0, f1, f0), R), 2 * bpv * nv, nv)
             free(A, B, D)
+    if want("f32dw"):
+        # in-process A/B: whole-dword window shifts (knob pointwise.dword_shift) x 16-B items
+        # (pointwise.f32_wide) on the Float32 general path, 800^3 sub-box of 1024^3
+        m = 1024
+        A, B, D = alloc((m,) * 3, 7, seed=1), alloc((m,) * 3, 7, seed=2), alloc((m,) * 3, 7)
+        f0, f1 = Vec3i_t(100, 100, 100), Vec3i_t(900, 900, 900)
+        cases = (("CopyRange 800^3 x0=100 -> dst 0", lambda: lib.vktHipCopyRange(D, A, f0, f1, o), 2),
+                 ("CopyRange 800^3 x0=100 -> dst x0=3", lambda: lib.vktHipCopyRange(D, A, f0, f1, Vec3i_t(3, 100, 100)), 2),
+                 ("SumRange 800^3 x0=100 dstOffset x=-97",
+                  lambda: lib.vktHipArithmeticRange(0, D, A, B, f0, f1, Vec3i_t(-97, 0, 0)), 3))
+        kvs = ((1, 0), (0, 0), (1, 1), (0, 1))   # (dword_shift, f32_wide)
+        ab = {}
+        for rnd in range(3):
+            for kv in kvs:
+                lib.vktHipSetTuningKnob(b"pointwise.dword_shift", kv[0])
+                lib.vktHipSetTuningKnob(b"pointwise.f32_wide", kv[1])
+                for lab, fn, _ in cases:
+                    ab.setdefault((lab, kv), []).append(timed(fn, R))
+        lib.vktHipSetTuningKnob(b"pointwise.dword_shift", -1)
+        lib.vktHipSetTuningKnob(b"pointwise.f32_wide", -1)
+        for lab, fn, streams in cases:
+            for kv in kvs:
+                ts = sorted(ab[(lab, kv)])
+                report(f"f32dw {lab} Float32 dword_shift={kv[0]} f32_wide={kv[1]} (median of 3 rounds, "
+                       f"spread {ts[0]:.4f}-{ts[-1]:.4f})", ts[1], streams * 4 * 800 ** 3, 800 ** 3)
+        free(A, B, D)
     if want("p16"):
         # the 65 536-bin UInt16 histogram (packed 16-bit LDS counters), one launch per case
         # (accumulate: no zeroing kernel) -- the code-count kernel of the UInt16 aggregates too

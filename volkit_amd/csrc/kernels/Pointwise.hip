@@ -321,6 +321,13 @@ namespace hipk
         }
         gg.divCpr = makeFastDiv(static_cast<uint32_t>(gg.cpr));
         gg.divVny = makeFastDiv(static_cast<uint32_t>(vny));
+        // whole-dword window offsets (4-byte voxels at 4-B aligned addresses; knob pointwise.dword_shift)
+        {
+            bool dw = p.d.bpv == 4 && rt::knob(rt::Knob::PointwiseDwordShift) != 0;
+            for (int i = 0; i < nops && dw; ++i)
+                dw = ops[i]->bpv == 4 && reinterpret_cast<uintptr_t>(ops[i]->data) % 4 == 0;
+            gg.dword = dw ? 1 : 0;
+        }
         // UInt8 copies / fills over multi-row boxes of long rows without row edges (e.g. whole-x
         // planes of a y sub-range) run faster on the general path's wide items than on the pair
         // grid: 800 planes of 1024 x 800 voxels 0.254 -> 0.226 ms, while 800-voxel rows lost 3 %

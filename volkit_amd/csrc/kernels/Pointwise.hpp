@@ -626,6 +626,8 @@ namespace hipk
         int32_t dph64;           // (d.data / BD) mod sv
         int32_t wide;            // every operand 1 or every operand 4 B/voxel, fast path: 16-B items
                                  // (pointwiseGenSpanFast16; cpr / dph in 16/B-voxel units)
+        int32_t dword;           // every operand 4 B/voxel at a 4-B aligned address: every window
+                                 // offset is a whole dword, the byte-align stage is the identity
         FastDiv divCpr, divVny;
     };
 
@@ -689,14 +691,23 @@ namespace hipk
         }
     }
 
+    // dword (GenGeom::dword, 4-byte voxels only): the offset is a multiple of 4, the two dword
+    // selects finish the shift (wave-uniform branch around the v_alignbyte stage)
     template <int B>
-    __device__ __forceinline__ void shiftWindow(Window<B> const& win, uint32_t (&out)[2 * B])
+    __device__ __forceinline__ void shiftWindow(Window<B> const& win, uint32_t (&out)[2 * B], bool dword = false)
     {
         constexpr int NO = 2 * B;   // output dwords
         uint32_t a[NO + 2], b[NO + 1];
         shiftSel(win.w, a, (win.s & 8u) != 0, 2, std::make_index_sequence<NO + 2>{});
         shiftSel(a, b, (win.s & 4u) != 0, 1, std::make_index_sequence<NO + 1>{});
-        shiftAlign(b, out, win.s & 3u, std::make_index_sequence<NO>{});
+        if (B == 4 && dword)
+        {
+#pragma unroll
+            for (int i = 0; i < NO; ++i)
+                out[i] = b[i];
+        }
+        else
+            shiftAlign(b, out, win.s & 3u, std::make_index_sequence<NO>{});
     }
 
     template <int B>
@@ -1168,9 +1179,9 @@ namespace hipk
                 continue;
             uint32_t a[2 * B1], b[2 * (NS >= 2 ? B2 : 1)], rd[2 * BD];
             if constexpr (NS >= 1)
-                shiftWindow<B1>(wa[u], a);
+                shiftWindow<B1>(wa[u], a, g.dword != 0);
             if constexpr (NS >= 2)
-                shiftWindow<B2>(wb[u], b);
+                shiftWindow<B2>(wb[u], b, g.dword != 0);
             result(a, b, rd);
             store(u, rd);
         }
@@ -1223,12 +1234,19 @@ namespace hipk
         return !o.clamp || (o.origin[0] + x >= 0 && o.origin[0] + x + 16 / B <= o.dims[0]);
     }
 
-    __device__ __forceinline__ void shiftWindow16(Window<1> const& win, uint32_t (&out)[4])
+    __device__ __forceinline__ void shiftWindow16(Window<1> const& win, uint32_t (&out)[4], bool dword = false)
     {
         uint32_t a[6], b[5];
         shiftSel(win.w, a, (win.s & 8u) != 0, 2, std::make_index_sequence<6>{});
         shiftSel(a, b, (win.s & 4u) != 0, 1, std::make_index_sequence<5>{});
-        shiftAlign(b, out, win.s & 3u, std::make_index_sequence<4>{});
+        if (dword)
+        {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                out[i] = b[i];
+        }
+        else
+            shiftAlign(b, out, win.s & 3u, std::make_index_sequence<4>{});
     }
 
     // the two aligned words around voxels [lo, hi) of the 16 / B voxels at `voxel` (as
@@ -1361,9 +1379,9 @@ namespace hipk
                 continue;
             uint32_t a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
             if constexpr (NS >= 1)
-                shiftWindow16(wa[u], a);
+                shiftWindow16(wa[u], a, B == 4 && g.dword != 0);
             if constexpr (NS >= 2)
-                shiftWindow16(wb[u], b);
+                shiftWindow16(wb[u], b, B == 4 && g.dword != 0);
             u32x4 rd;
             result(a, b, rd);
             store(u, rd);

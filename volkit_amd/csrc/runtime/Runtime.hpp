@@ -97,6 +97,7 @@ namespace rt
         AggregatesMoments,             // ComputeAggregates in one pass of moments: bit 0 UInt16 unit mapping (integer), bit 1 UInt16 other mappings / Float32 (float)
         MemoryArenaChunkMiB,           // > 0: arena chunks of exactly max(request, this many MiB) (tests)
         DecomposeBlock,                // threads per BrickDecompose workgroup over one 16-KiB chunk: 256 or 128
+        PointwiseDwordShift,           // 0: 4-byte general-path windows keep the byte-align stage (whole-dword offsets)
         Count
     };
     int64_t knob(Knob k);
