@@ -242,6 +242,14 @@ VKTAPI vktError vktHipSlabExchangeHalo(vktHipComm_t comm, vktHipVolumeView_t loc
 VKTAPI vktError vktHipSlabExchangeHaloLocal(int32_t numSlabs, vktHipVolumeView_t const* localSrc,
                                             int32_t const* localZ0, int32_t dstGlobalDimZ, int32_t srcGlobalDimZ,
                                             vktFilterMode fm, int32_t needsNeighbours);
+/* The same for slabs on SEVERAL devices of this process (slab r on HIP device devices[r]; the
+ * multi-device single-process model of the reference's CudaContext, include/c/vkt/CudaContext.h:
+ * 41-65): every receive is a hipMemcpyPeerAsync into the receiving slab's device (peer access
+ * enabled where the devices support it), ordered after the library's compute stream for its own
+ * device; returns once every plane has landed. */
+VKTAPI vktError vktHipSlabExchangeHaloPeer(int32_t numSlabs, vktHipVolumeView_t const* localSrc,
+                                           int32_t const* localZ0, int32_t const* devices, int32_t dstGlobalDimZ,
+                                           int32_t srcGlobalDimZ, vktFilterMode fm, int32_t needsNeighbours);
 
 /* ---- Range calls over Z-slab partitioned volumes (no reference counterpart)
  * A volume of global depth globalDimZ is split over nranks ranks by the ceil partition: rank r

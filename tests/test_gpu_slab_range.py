@@ -80,10 +80,13 @@ def same_codes(got, want, fmt):
     return np.array_equal(got, want)
 
 
+@pytest.mark.parametrize("transport", ["local", "peer"])
 @pytest.mark.parametrize("nslabs", [4, 8])
 @pytest.mark.parametrize("sdims,ddims", [((40, 24, 32), (80, 48, 64)), ((37, 19, 29), (64, 40, 53)),
                                          ((32, 16, 64), (16, 16, 21))])
-def test_local_halo_exchange_linear_chain(L, nslabs, sdims, ddims):
+def test_local_halo_exchange_linear_chain(L, nslabs, sdims, ddims, transport):
+    """vktHipSlabExchangeHaloLocal (device copies) and vktHipSlabExchangeHaloPeer (peer copies into
+    each slab's device; every slab on device 0 of the one-GPU pool) deliver every rank's halo."""
     from volkit_amd import _lib, slab
     sx, sy, sz = sdims
     dx, dy, dz = ddims
@@ -106,7 +109,11 @@ def test_local_halo_exchange_linear_chain(L, nslabs, sdims, ddims):
     assert moved > 0, "the chain must exchange planes"
     views = (_lib.HipVolumeView_t * nslabs)(*[s.view for s in srcs])
     z0s = (C.c_int32 * nslabs)(*[s.z0 for s in srcs])
-    assert L.vktHipSlabExchangeHaloLocal(nslabs, views, z0s, dz, sz, 1, 1) == 0, err(L)
+    if transport == "local":
+        assert L.vktHipSlabExchangeHaloLocal(nslabs, views, z0s, dz, sz, 1, 1) == 0, err(L)
+    else:
+        devs = (C.c_int32 * nslabs)(*([0] * nslabs))
+        assert L.vktHipSlabExchangeHaloPeer(nslabs, views, z0s, devs, dz, sz, 1, 1) == 0, err(L)
     for r, (p, s) in enumerate(zip(plans, srcs)):
         l0, l1 = p.local_src
         assert np.array_equal(s.read(), glob[l0:l1]), f"slab {r}: halo planes not delivered"
@@ -128,6 +135,10 @@ def test_local_halo_exchange_rejects_short_buffers(L):
     z0s = (C.c_int32 * 2)(0, 4)
     # slab 0 holds planes [0, 4) but must also hold plane 4 (the chain's z+1 neighbour)
     assert L.vktHipSlabExchangeHaloLocal(2, views, z0s, 16, 8, 1, 1) != 0
+    devs = (C.c_int32 * 2)(0, 0)
+    assert L.vktHipSlabExchangeHaloPeer(2, views, z0s, devs, 16, 8, 1, 1) != 0
+    bad = (C.c_int32 * 2)(0, 99)
+    assert L.vktHipSlabExchangeHaloPeer(2, views, z0s, bad, 16, 8, 1, 1) != 0   # no such device
 
 
 @pytest.mark.parametrize("nslabs", [1, 2, 3, 4, 8])

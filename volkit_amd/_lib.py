@@ -257,6 +257,7 @@ SIGNATURES = {
     "vktHipCommSetTimeout": (c_err, [c_comm, C.c_int64]),
     "vktHipSlabExchangeHalo": (c_err, [c_comm, HipVolumeView_t, i32, i32, i32, C.c_int, i32]),
     "vktHipSlabExchangeHaloLocal": (c_err, [i32, P(HipVolumeView_t), P(i32), i32, i32, C.c_int, i32]),
+    "vktHipSlabExchangeHaloPeer": (c_err, [i32, P(HipVolumeView_t), P(i32), P(i32), i32, i32, C.c_int, i32]),
     "vktHipSlabRangePlan": (c_err, [C.c_int, i32, i32, i32, i32, i32, Vec3i_t, Vec3i_t, Vec3i_t, P(HipSlabPiece_t),
                                     i32, P(i32), P(HipSlabMove_t), i32, P(i32), P(i32)]),
     "vktHipSlabFillRange": (c_err, [c_comm, i32, P(HipSlab_t), Vec3i_t, Vec3i_t, f32]),

@@ -402,4 +402,99 @@ vktError vktHipSlabExchangeHaloLocal(int32_t numSlabs, vktHipVolumeView_t const*
     return rt::finishLaunch("SlabExchangeHaloLocal_hip");
 }
 
+vktError vktHipSlabExchangeHaloPeer(int32_t numSlabs, vktHipVolumeView_t const* localSrc, int32_t const* localZ0,
+                                    int32_t const* devices, int32_t dstGlobalDimZ, int32_t srcGlobalDimZ,
+                                    vktFilterMode fm, int32_t needsNeighbours)
+{
+    if (numSlabs <= 0 || localSrc == nullptr || localZ0 == nullptr || devices == nullptr)
+        return rt::fail("vktHipSlabExchangeHaloPeer: invalid slab arrays");
+    int32_t nDev = 0;
+    VKT_HIP_TRY(hipGetDeviceCount(&nDev));
+    for (int32_t r = 0; r < numSlabs; ++r)
+        if (devices[r] < 0 || devices[r] >= nDev)
+            return rt::fail("vktHipSlabExchangeHaloPeer: device id out of range");
+    // every receive of the plan as a peer copy into the receiving slab's device, on a stream of
+    // that device (the library's compute stream for its own device); each device's copies are
+    // ordered after the work already queued on the library's compute stream (for the library's
+    // device) and the call returns once every plane has landed
+    int const libDev = rt::device();
+    int cur = 0;
+    VKT_HIP_TRY(hipGetDevice(&cur));
+    std::vector<hipStream_t> streams(static_cast<size_t>(nDev), nullptr);
+    std::vector<char> owned(static_cast<size_t>(nDev), 0);
+    vktError e = vktNoError;
+    auto streamOf = [&](int dev) -> hipStream_t {
+        if (dev == libDev)
+            return rt::computeStream();
+        if (!streams[static_cast<size_t>(dev)])
+        {
+            if (rt::check(hipSetDevice(dev), "hipSetDevice") == vktNoError &&
+                rt::check(hipStreamCreateWithFlags(&streams[static_cast<size_t>(dev)], hipStreamNonBlocking),
+                          "hipStreamCreate") == vktNoError)
+                owned[static_cast<size_t>(dev)] = 1;
+            (void)hipSetDevice(cur);
+        }
+        return streams[static_cast<size_t>(dev)];
+    };
+    for (int32_t r = 0; r < numSlabs && e == vktNoError; ++r)
+    {
+        int32_t lo, hi;
+        std::vector<vktHipSlabTransfer_t> xs;
+        e = plan(dstGlobalDimZ, srcGlobalDimZ, numSlabs, r, fm, needsNeighbours, lo, hi, xs);
+        for (size_t k = 0; k < xs.size() && e == vktNoError; ++k)
+        {
+            vktHipSlabTransfer_t const& x = xs[k];
+            if (x.send)
+                continue;
+            uint8_t *to, *from;
+            size_t n, m;
+            e = comm::planeSpan(localSrc[r], localZ0[r], x.z0, x.z1, "vktHipSlabExchangeHaloPeer", to, n);
+            if (e == vktNoError)
+                e = comm::planeSpan(localSrc[x.peer], localZ0[x.peer], x.z0, x.z1, "vktHipSlabExchangeHaloPeer", from, m);
+            if (e == vktNoError && n != m)
+                e = rt::fail("vktHipSlabExchangeHaloPeer: slabs of different plane sizes");
+            if (e != vktNoError)
+                break;
+            int const dd = devices[r], sd = devices[x.peer];
+            hipStream_t const st = streamOf(dd);
+            if (!st)
+            {
+                e = rt::fail("vktHipSlabExchangeHaloPeer: no stream on the receiving device");
+                break;
+            }
+            if (dd != sd)
+            {
+                int can = 0;
+                if (hipDeviceCanAccessPeer(&can, dd, sd) == hipSuccess && can)
+                {
+                    (void)hipSetDevice(dd);
+                    hipError_t const pe = hipDeviceEnablePeerAccess(sd, 0);
+                    if (pe != hipSuccess && pe != hipErrorPeerAccessAlreadyEnabled)
+                        (void)hipGetLastError();
+                    else if (pe == hipErrorPeerAccessAlreadyEnabled)
+                        (void)hipGetLastError();
+                    (void)hipSetDevice(cur);
+                }
+            }
+            e = rt::check(hipMemcpyPeerAsync(to, dd, from, sd, n, st), "vktHipSlabExchangeHaloPeer: hipMemcpyPeerAsync");
+        }
+    }
+    // every plane landed before the call returns (the slabs' owners may read them on any stream)
+    for (int d = 0; d < nDev; ++d)
+        if (streams[static_cast<size_t>(d)])
+        {
+            if (e == vktNoError)
+                e = rt::check(hipStreamSynchronize(streams[static_cast<size_t>(d)]), "hipStreamSynchronize");
+            if (owned[static_cast<size_t>(d)])
+            {
+                (void)hipSetDevice(d);
+                (void)hipStreamDestroy(streams[static_cast<size_t>(d)]);
+            }
+        }
+    (void)hipSetDevice(cur);
+    if (e == vktNoError)
+        e = rt::check(hipStreamSynchronize(rt::computeStream()), "hipStreamSynchronize");
+    return e != vktNoError ? e : rt::finishLaunch("SlabExchangeHaloPeer_hip");
+}
+
 } // extern "C"
