@@ -58,8 +58,8 @@ namespace
     // allocations), over three volumes carved from one block at 0.99-1.01 ms every time
     // (tools/alloc_probe.py).  An arena chunk is sized for a group of like buffers
     // (kArenaGroup times the request: the src / dst / operand volumes of one pipeline land in one
-    // chunk), at least kArenaMin, growing geometrically (twice the previous chunk, up to
-    // kArenaGrowCap) for runs of smaller buffers, and never more than 3/4 of the device's free
+    // chunk), at least kArenaMin, growing geometrically (twice the newest chunk while it is
+    // allocated, up to kArenaGrowCap) for runs of like-sized smaller buffers, and never more than 3/4 of the device's free
     // memory beyond the request -- a 5 MiB buffer reserves 64 MiB, not a 16-GiB chunk.
     // Freed blocks are not reusable at once (a queued kernel or copy may still use them): they
     // wait on a pending list until a drain records one event on each of the library's streams
@@ -109,7 +109,8 @@ namespace
         std::unordered_map<std::size_t, std::vector<std::pair<void*, PoolChunk*>>> poolFree;   // by class
         std::unordered_map<std::size_t, std::size_t> pendingByClass;    // pool classes on the pending list
         std::vector<ArenaChunk*> arenaChunks;
-        std::size_t lastArenaChunk = 0;
+        ArenaChunk* lastChunk = nullptr;   // the newest arena chunk while it exists, and its request
+        std::size_t lastReq = 0;
         std::vector<void*> pending;   // freed, not yet known idle
         hipEvent_t evCompute = nullptr, evCopy = nullptr;
     };
@@ -202,6 +203,8 @@ namespace
             {
                 (void)hipFree((*it)->base);
                 freed += (*it)->size;
+                if (*it == d.lastChunk)
+                    d.lastChunk = nullptr;   // (a later burst starts small again)
                 delete *it;
                 it = d.arenaChunks.erase(it);
             }
@@ -312,7 +315,9 @@ namespace
         if (fixed > 0)
             return std::max(len, static_cast<std::size_t>(fixed) << 20);
         std::size_t want = std::max(kArenaMin, kArenaGroup * len);
-        want = std::max(want, std::min(2 * d.lastArenaChunk, kArenaGrowCap));
+        // a run of like buffers that outgrew the newest chunk (still allocated): twice its size
+        if (d.lastChunk && d.lastReq <= 2 * len && 2 * d.lastReq >= len)
+            want = std::max(want, std::min(2 * d.lastChunk->size, kArenaGrowCap));
         std::size_t freeB = 0, totalB = 0;
         if (want > len && hipMemGetInfo(&freeB, &totalB) == hipSuccess && freeB > len)
             want = std::min(want, len + (freeB - len) / 4 * 3);
@@ -348,7 +353,8 @@ namespace
         c->size = size;
         c->holes[0] = size;
         d.arenaChunks.push_back(c);
-        d.lastArenaChunk = size;
+        d.lastChunk = c;
+        d.lastReq = len;
         return arenaCarve(d, len, dev, H);
     }
 
