@@ -18,5 +18,5 @@ for g in "$@"; do
     timeout -s KILL 120 rocprofv3 --pmc $pass -d $O/$g/p$i -o run --output-format csv -- $B > $O/$g.p$i.log 2>&1 || { tail -20 $O/$g.p$i.log; exit 1; }
     i=$((i+1))
   done
-  python3 scripts/pmc_dispatch.py $O/$g $O/$g.pmc_cases.log 3 > $O/$g.pmc.jsonl && cat $O/$g.pmc.jsonl
+  python3 scripts/pmc_dispatch.py $O/$g $O/$g.pmc_cases.log 3 ${PMC_KERNEL:-} > $O/$g.pmc.jsonl && cat $O/$g.pmc.jsonl
 done

@@ -1,7 +1,9 @@
 """Per-dispatch PMC table from rocprofv3 counter CSVs (one directory per pass), in dispatch
 order, joined with the case lines a bench printed.
 
-  python3 scripts/pmc_dispatch.py <dir with p0/ p1/ ...> <bench log with JSON case lines> <launches per case>
+  python3 scripts/pmc_dispatch.py <dir with p0/ p1/ ...> <bench log with JSON case lines> <launches per case> [kernel]
+
+(kernel: only dispatches whose kernel name contains it -- ops that launch several kernels)
 
 Each case of tools/bench_configs.py runs `reps + 1` launches (one warm-up); a case's value is
 the median over its launches.  FETCH_SIZE is doubled (gfx950: a wide coalesced read is
@@ -19,6 +21,7 @@ from collections import defaultdict
 
 def main():
     root, log, per = sys.argv[1], sys.argv[2], int(sys.argv[3])
+    only = sys.argv[4] if len(sys.argv) > 4 else None   # keep dispatches whose kernel name holds this
     disp = defaultdict(dict)   # (pass, dispatch) -> {counter: value}, kernel
     for p in sorted(glob.glob(os.path.join(root, "p*"))):
         if not os.path.isdir(p):
@@ -37,6 +40,8 @@ def main():
         ds = [d for d in ds if "synthKernel" not in d["kernel"] and "elementwise" not in d["kernel"]
               and "__amd_rocclr" not in d["kernel"] and "distribution" not in d["kernel"]
               and "fill" not in d["kernel"].lower()[:40]]
+        if only:
+            ds = [d for d in ds if only in d["kernel"]]
         for i, c in enumerate(cases):
             chunk = ds[i * per:(i + 1) * per]
             if not chunk:

@@ -189,6 +189,43 @@ def test_fill_and_copy_1024(hip):
     W.free()
 
 
+def test_float32_4gib_operands_shifted_parity(hip):
+    """1024^3 Float32 operands are exactly 4 GiB: the general path's 32-bit addressing admits
+    them (byte offsets from the 16-B aligned base <= 2^32).  Phase-shifted CopyRange and an
+    arithmetic dstOffset on the 800^3 sub-box at x0 = 100 (the f32shift bench cases, whose last
+    rows end at the volume's last bytes when shifted to the far corner), bit-exact vs the oracle."""
+    import torch
+    e = 1024
+    A, B, D = (DevVol(hip, (e, e, e), 7) for _ in range(3))
+    gen = torch.Generator(device="cuda").manual_seed(11)
+    for v in (A, B, D):
+        t = torch.rand((e, e, e), device="cuda", dtype=torch.float32, generator=gen)
+        assert hip.lib.vktHipMemcpy(v.ptr, t.data_ptr(), v.nbytes, 3) == 0
+        del t
+    assert hip.lib.vktHipSynchronize() == 0
+    a, b, d0 = A.download(), B.download(), D.download()
+    f0, f1 = (100, 100, 100), (900, 900, 900)
+    cases = (("copy dst 0", None, (0, 0, 0)), ("copy dst x0=3", None, (3, 100, 100)),
+             ("copy to the volume end", None, (224, 224, 224)), ("Sum dstOffset x=-97", 0, (-97, 0, 0)),
+             ("Sum dstOffset to the end", 0, (124, 124, 124)))
+    for what, op, off in cases:
+        assert hip.lib.vktHipMemcpy(D.ptr, d0.ctypes.data, D.nbytes, 1) == 0
+        if op is None:
+            rc = hip.lib.vktHipCopyRange(D.view, A.view, v3(*f0, hip), v3(*f1, hip), v3(*off, hip))
+            ref = ob.Volume(d0.copy(), 7)
+            ob.copy_range(ref, ob.Volume(a, 7), f0, f1, off)
+        else:
+            rc = hip.lib.vktHipArithmeticRange(op, D.view, A.view, B.view, v3(*f0, hip), v3(*f1, hip), v3(*off, hip))
+            ref = ob.Volume(d0.copy(), 7)
+            ob.arith_range("Sum", ref, ob.Volume(a, 7), ob.Volume(b, 7), f0, f1, off)
+        assert rc == 0, hip.last_error()
+        got = D.download()
+        assert np.array_equal(got, ref.codes), what
+        del got, ref
+    for v in (A, B, D):
+        v.free()
+
+
 @pytest.mark.parametrize("world", [2, 3])
 @pytest.mark.parametrize("fmt,fm", [(5, 1), (7, 1), (4, 0)])
 @pytest.mark.parametrize("sdims,ddims", [((64, 48, 40), (128, 96, 80)), ((37, 23, 29), (64, 40, 53)),

@@ -869,6 +869,78 @@ def main():
         lib.vktHipSetTuningKnob(b"aggregates.moments", -1)
         lib.vktHipSetTuningKnob(b"aggregates.codes", -1)
         free(V)
+    if want("mompipe"):
+        # in-process A/B of the integer-moments kernel variants (knob aggregates.moments_pipe: 0
+        # one buffer x 4 items, 1 two buffers x 4 items, 2 two buffers x 8 items), per call incl.
+        # the D2H of the result, median of 3 rounds
+        n = 1024
+        V = alloc((n,) * 3, 5, seed=11)
+        agg = _lib.Aggregates_t()
+        boxes = ((o, Vec3i_t(n, n, n), "1024^3"), (Vec3i_t(100, 100, 100), Vec3i_t(900, 900, 900), "800^3 sub-box at x0=100"),
+                 (Vec3i_t(0, 100, 100), Vec3i_t(800, 900, 900), "800^3 sub-box x 0..800"))
+        ab = {}
+        for rnd in range(3):
+            for pv in (0, 1, 2, 3, 4):
+                lib.vktHipSetTuningKnob(b"aggregates.moments_pipe", pv)
+                for a0, a1, box in boxes:
+                    ab.setdefault((box, pv), []).append(
+                        timed(lambda: lib.vktHipAggregatesRange(V, a0, a1, C.byref(agg)), R))
+        lib.vktHipSetTuningKnob(b"aggregates.moments_pipe", -1)
+        for a0, a1, box in boxes:
+            nv = (a1.x - a0.x) * (a1.y - a0.y) * (a1.z - a0.z)
+            for pv in (0, 1, 2, 3, 4):
+                ts = sorted(ab[(box, pv)])
+                report(f"mompipe Aggregates UInt16 {box} moments_pipe={pv} (median of 3 rounds, spread "
+                       f"{ts[0]:.4f}-{ts[-1]:.4f})", ts[1], 2 * nv, nv)
+        free(V)
+    if want("mom1"):
+        # integer-moments variants, one ComputeAggregates per case (PMC passes:
+        # PMC_KERNEL=aggregatesMomentsU16Kernel scripts/gpu_pmc_groups.sh)
+        n = 1024
+        V = alloc((n,) * 3, 5, seed=11)
+        agg = _lib.Aggregates_t()
+        for pv in (0, 1, 3, 4):
+            lib.vktHipSetTuningKnob(b"aggregates.moments_pipe", pv)
+            for a0, a1, box in ((o, Vec3i_t(n, n, n), "1024^3"),
+                                (Vec3i_t(100, 100, 100), Vec3i_t(900, 900, 900), "800^3 sub-box at x0=100")):
+                nv = (a1.x - a0.x) * (a1.y - a0.y) * (a1.z - a0.z)
+                report(f"mom1 Aggregates UInt16 {box} moments_pipe={pv}",
+                       timed(lambda: lib.vktHipAggregatesRange(V, a0, a1, C.byref(agg)), R), 2 * nv, nv)
+        lib.vktHipSetTuningKnob(b"aggregates.moments_pipe", -1)
+        free(V)
+    if want("decbatch"):
+        # in-process A/B of BrickDecompose's batched planning (knob decompose.batch: 1 up to 8
+        # batches of brick planes, planning batch k + 1 while the GPU copies batch k; 0 one batch)
+        import volkit_amd.volkit as vkt
+        ep = vkt.GetThreadExecutionPolicy()
+        ep.device = vkt.ExecutionPolicy.Device_GPU
+        vkt.SetThreadExecutionPolicy(ep)
+        n = 1024
+        V = vkt.StructuredVolume(n, n, n, vkt.DataFormat_UInt16)
+        vkt.Synthesize(V, 77)
+        ab = {}
+        for bs, halo in ((16, (1, 1, 1)), (16, (0, 0, 0)), (32, (1, 1, 1))):
+            arr = vkt.Array3D_StructuredVolume()
+            b3, h3 = vkt.Vec3i(bs, bs, bs), vkt.Vec3i(*halo)
+            vkt.BrickDecomposeResize(arr, V, b3, h3, h3)
+            vox = sum(arr[(i, j, k)].getSizeInBytes() // 2 for k in range(arr.dims().z)
+                      for j in range(arr.dims().y) for i in range(arr.dims().x))
+            for rnd in range(3):
+                for kv in (1, 0):
+                    lib.vktHipSetTuningKnob(b"decompose.batch", kv)
+                    ab.setdefault((bs, halo, kv, vox, "back-to-back"), []).append(
+                        pipelined(lambda: vkt.BrickDecompose(arr, V, b3, h3, h3), R))
+                    ab.setdefault((bs, halo, kv, vox, "incl. host planning"), []).append(
+                        timed(lambda: vkt.BrickDecompose(arr, V, b3, h3, h3), R))
+            del arr
+        lib.vktHipSetTuningKnob(b"decompose.batch", -1)
+        for (bs, halo, kv, vox, how), ts in sorted(ab.items()):
+            ts.sort()
+            report(f"decbatch BrickDecompose 1024^3 UInt16 -> {bs}^3 bricks halo {halo} batch={kv} ({how}; median of "
+                   f"3 rounds, spread {ts[0]:.4f}-{ts[-1]:.4f})", ts[1], 4 * vox, vox)
+        del V
+        ep.device = vkt.ExecutionPolicy.Device_CPU
+        vkt.SetThreadExecutionPolicy(ep)
     if want("config5"):
         # BASELINE config 5: 1024^3 UInt8 multi-scattering, 1024^2 viewport (headless frames)
         import volkit_amd.volkit as vkt

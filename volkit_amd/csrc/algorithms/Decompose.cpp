@@ -83,15 +83,18 @@ namespace
             ranges.resize(total);
         vktHipBrickRange_t* const out = ranges.data();
         vktHipVolumeView_t const src = brickView(source);
-        // Many small bricks: the ranges are planned and handed to the backend in batches of whole
-        // brick planes (~16 Ki bricks, at most kMaxBatches), so the host plans batch k + 1 -- the
-        // views here, the descriptors in the backend -- while the GPU copies batch k: a
-        // synchronised call costs about one batch of planning plus the copies instead of all the
-        // planning plus the copies.  Each batch is a uniform brick grid of its own (the backend
-        // infers and checks it per call), the copies are the same.
+        // Knob decompose.batch 1: the ranges are planned and handed to the backend in batches of
+        // whole brick planes (~16 Ki bricks, at most kMaxBatches), so the host plans batch k + 1
+        // while the GPU copies batch k.  Measured on MI355X (profiles/r04/decbatch.jsonl) it is
+        // SLOWER: 16^3 bricks + halo 1 of 1024^3 UInt16 back-to-back 2.61 ms batched vs 1.54 ms
+        // in one batch, incl. planning 2.80 vs 2.61 -- eight small copy launches fill the GPU
+        // worse than one, and the per-call descriptor upload and grid inference repeat -- so the
+        // default is one batch.
         constexpr size_t kBatchBricks = 16384, kMaxBatches = 8;
         size_t const nzb = static_cast<size_t>(std::max(0, arrDims.z)), plane = nx * ny;
-        size_t batches = std::min(kMaxBatches, std::max<size_t>(1, total / kBatchBricks));
+        size_t batches = rt::knob(rt::Knob::DecomposeBatch) != 0
+                             ? std::min(kMaxBatches, std::max<size_t>(1, total / kBatchBricks))
+                             : 1;   // (knob decompose.batch 0: one batch, for the A/B)
         batches = std::min(batches, std::max<size_t>(1, nzb));
         size_t const planesPer = nzb > 0 ? (nzb + batches - 1) / batches : 0;
         // one view per brick (getData() migrates a brick that lives elsewhere): ~16 ns per brick,

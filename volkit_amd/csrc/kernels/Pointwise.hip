@@ -243,8 +243,12 @@ namespace hipk
         gg.dph = static_cast<int32_t>((reinterpret_cast<uintptr_t>(p.d.data) / p.d.bpv) & 7);
         gg.fast32 = gg.items < (1ull << 32) ? 1 : 0;
         gg.anyClamp = anyClamp ? 1 : 0;
-        // 32-bit addressing: byte offsets from each operand's 16-B aligned base < 2^31, pitches
-        // and box extents fit the 24-bit multiplies, items < 2^32
+        // 32-bit addressing: every byte of each operand at an offset < 2^32 from its 16-B aligned
+        // base (the window words, merged chunks and stores address only valid voxels' words; voxel
+        // indices times B stay < 2^32), pitches and box extents fit the 24-bit multiplies, items
+        // < 2^32.  A 4 GiB operand (1024^3 Float32) qualifies when 16-B aligned: it had been sent to
+        // the 64-bit path (~2.5x the VALU, per-voxel row-end stores, no sector completion) by a
+        // 64-B margin no access needs.
         {
             bool fast = gg.items < (1ull << 32) && vny < (1ll << 24) && vnz < (1ll << 24);
             for (int i = 0; i < nops && fast; ++i)
@@ -252,7 +256,8 @@ namespace hipk
                 Operand const& o = *ops[i];
                 uint64_t const bytes = static_cast<uint64_t>(o.dims[0]) * static_cast<uint64_t>(o.dims[1]) *
                                        static_cast<uint64_t>(o.dims[2]) * o.bpv;
-                fast = bytes + 64 < (1ull << 32) && (o.clamp || o.base >= 0) &&
+                uint64_t const mis = reinterpret_cast<uintptr_t>(o.data) & 15u;
+                fast = mis + bytes <= (1ull << 32) && (o.clamp || o.base >= 0) &&
                        (vny <= 1 || (o.sy < (1ll << 24) && o.dims[0] < (1 << 24))) &&
                        (vnz <= 1 || o.sz < (1ll << 24)) && (!o.clamp || static_cast<int64_t>(o.dims[0]) * o.dims[1] < (1ll << 24));
             }

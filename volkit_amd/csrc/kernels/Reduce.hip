@@ -32,6 +32,8 @@
 #include <cmath>
 #include <algorithm>
 #include <cstring>
+#include <mutex>
+#include <unordered_map>
 
 namespace vkt
 {
@@ -1390,7 +1392,8 @@ namespace hipk
     //    item can improve the lane's (rare after the first items);
     //  * prod: (c0 c1) exact in v_mul_u32_u24, four pair products in double scaled by 2^-128 --
     //    skipped once every lane's product is +0 (it stays 0: the values are finite).
-    // Items outside the range in padded rows' end items (mask m != 0xFF) go voxel by voxel.
+    // Voxels outside the range in padded rows' end items (mask m != 0xFF) are masked in the
+    // packed words (0 for the sums, 0xFFFF for the min bound, code 2^16 = value 1 for prod).
     // The float paths needed a decode, two double adds / multiplies and float min/max per voxel,
     // plus either a second pass over the data or a 65 536-code LDS count.
     struct MomentPartialU16
@@ -1456,10 +1459,12 @@ namespace hipk
                 momentCombine(p, lds[w]);
     }
 
-    template <bool CONTIG>
+    // U items per lane and wave-step; PIPE: the next step's loads are issued before this step's
+    // arithmetic (two register buffers), so a wave keeps 16 U bytes per lane in flight while it
+    // computes -- without it the loads of a step wait behind the previous step's ALU work.
+    template <bool CONTIG, int U, bool PIPE>
     __global__ __launch_bounds__(kBlock) void aggregatesMomentsU16Kernel(FastHistArgs h, MomentPartialU16* partials)
     {
-        constexpr int U = 4;
         uint32_t const lane = threadIdx.x & 63;
         MomentPartialU16 p;
         p.count = p.sumC = p.sumSqLo = p.sumSqHi = 0;
@@ -1467,17 +1472,18 @@ namespace hipk
         p.cmin = 0x10000u;
         p.cmax = -1;
         p.minIndex = p.maxIndex = kNoIndex;
-        uint32_t sc = 0, hq = 0, q = 0;   // this step's Sc, H and Q (see above)
+        uint32_t sc = 0, hq = 0, q = 0, cnt = 0;   // this step's Sc, H, Q and count (see above)
         auto addSq = [&](uint64_t x) {
             uint64_t const lo = p.sumSqLo + x;
             p.sumSqHi += lo < x ? 1u : 0u;
             p.sumSqLo = lo;
         };
         auto flushStep = [&] {
-            uint32_t const r = q - (hq << 16);   // exact: the r of <= 32 codes sum to < 2^30
+            uint32_t const r = q - (hq << 16);   // exact: the r of <= 8 U codes sum to < 2^30
             addSq((static_cast<uint64_t>(hq) << 16) + r);
             p.sumC += sc;
-            sc = hq = q = 0;
+            p.count += cnt;
+            sc = hq = q = cnt = 0;
         };
         // in-order strict updates of the lane's extremes over the valid voxels of one item
         auto extremes = [&](uint32_t const (&w)[4], uint32_t m, uint64_t item) {
@@ -1501,82 +1507,124 @@ namespace hipk
                 }
             }
         };
-        auto item8 = [&](uint32_t const (&w)[4], uint32_t m, uint64_t item, bool prodLive) {
+        // one item's sums; mn / mx collect the step's packed extremes bounds.  Voxels outside the
+        // range (padded row ends, mask m != 0xFF) enter the sums as 0, the min bound as 0xFFFF
+        // and the product as 1 (code 2^16): the same packed instructions for every item.
+        auto item8 = [&](uint32_t const (&w)[4], uint32_t m, bool prodLive, u16x2& mn, u16x2& mx) {
+            u16x2 const one = {1, 1};
+            uint32_t xs[4], xm[4];
+            double pf = 1.0;
             if (m == 0xFFu)
             {
-                u16x2 const one = {1, 1};
-                u16x2 mn = asU16x2(w[0]), mx = mn;
 #pragma unroll
                 for (int d = 0; d < 4; ++d)
-                {
-                    u16x2 const x = asU16x2(w[d]);
-                    if (d)
-                    {
-                        mn = __builtin_elementwise_min(mn, x);
-                        mx = __builtin_elementwise_max(mx, x);
-                    }
-                    sc = __builtin_amdgcn_udot2(x, one, sc, false);
-                    // the two high bytes as u16 (v_perm_b32: bytes 1, 3 of w, zeros above)
-                    u16x2 const hb = asU16x2(__builtin_amdgcn_perm(0u, w[d], 0x0C030C01u));
-                    hq = __builtin_amdgcn_udot2(hb, hb, hq, false);
-                    q = __builtin_amdgcn_udot2(x, x, q, false);
-                }
-                uint32_t const imin = mn.x < mn.y ? mn.x : mn.y, imax = mx.x > mx.y ? mx.x : mx.y;
-                if (imin < p.cmin || static_cast<int32_t>(imax) > p.cmax)
-                    extremes(w, 0xFFu, item);
+                    xs[d] = xm[d] = w[d];
                 if (prodLive)
                 {
                     double pr[4];
 #pragma unroll
                     for (int d = 0; d < 4; ++d)
                         pr[d] = static_cast<double>(static_cast<uint32_t>(__umul24(w[d] & 0xFFFFu, w[d] >> 16)));
-                    p.prod *= ((pr[0] * pr[1]) * (pr[2] * pr[3])) * 0x1p-128;
+                    pf = ((pr[0] * pr[1]) * (pr[2] * pr[3])) * 0x1p-128;
                 }
-                p.count += 8;
             }
             else
             {
-                // padded row end item: voxel by voxel, outside-range voxels skipped
-                extremes(w, m, item);
+                double pr[4];
 #pragma unroll
-                for (int j = 0; j < 8; ++j)
+                for (int d = 0; d < 4; ++d)
                 {
-                    uint32_t const c = (w[j / 2] >> (16 * (j % 2))) & 0xFFFFu;
-                    if ((m >> j) & 1u)
-                    {
-                        p.sumC += c;
-                        addSq(static_cast<uint64_t>(c) * c);
-                        p.prod *= static_cast<double>(c) * 0x1p-16;
-                        p.count += 1;
-                    }
+                    bool const kl = (m >> (2 * d)) & 1u, kh = (m >> (2 * d + 1)) & 1u;
+                    uint32_t const keep = (kl ? 0xFFFFu : 0u) | (kh ? 0xFFFF0000u : 0u);
+                    xs[d] = w[d] & keep;
+                    xm[d] = w[d] | ~keep;
+                    uint32_t const lo = kl ? (w[d] & 0xFFFFu) : 0x10000u, hi = kh ? (w[d] >> 16) : 0x10000u;
+                    pr[d] = static_cast<double>(lo) * static_cast<double>(hi);   // exact (< 2^33)
                 }
+                if (prodLive)
+                    pf = ((pr[0] * pr[1]) * (pr[2] * pr[3])) * 0x1p-128;
+            }
+#pragma unroll
+            for (int d = 0; d < 4; ++d)
+            {
+                u16x2 const x = asU16x2(xs[d]);
+                mn = __builtin_elementwise_min(mn, asU16x2(xm[d]));
+                mx = __builtin_elementwise_max(mx, x);
+                sc = __builtin_amdgcn_udot2(x, one, sc, false);
+                // the two high bytes as u16 (v_perm_b32: bytes 1, 3 of the dword, zeros above)
+                u16x2 const hb = asU16x2(__builtin_amdgcn_perm(0u, xs[d], 0x0C030C01u));
+                hq = __builtin_amdgcn_udot2(hb, hb, hq, false);
+                q = __builtin_amdgcn_udot2(x, x, q, false);
+            }
+            if (prodLive)
+                p.prod *= pf;
+            cnt += CONTIG ? 8u : static_cast<uint32_t>(__popc(m));
+        };
+        // a wave-step of U items: sums, then -- only when the step's packed bounds can improve
+        // the lane's extremes (rare after the first steps) -- the in-order per-voxel updates
+        auto doStep = [&](uint32_t const (&w)[U][4], uint32_t const (&msk)[U], uint64_t base, bool prodLive) {
+            u16x2 mn = {0xFFFFu, 0xFFFFu}, mx = {0, 0};
+#pragma unroll
+            for (int k = 0; k < U; ++k)
+                item8(w[k], msk[k], prodLive, mn, mx);
+            uint32_t const imin = mn.x < mn.y ? mn.x : mn.y, imax = mx.x > mx.y ? mx.x : mx.y;
+            if ((imin < p.cmin) | (static_cast<int32_t>(imax) > p.cmax))
+            {
+#pragma unroll
+                for (int k = 0; k < U; ++k)
+                    extremes(w[k], msk[k], base + k * 64 + lane);
+            }
+            flushStep();
+        };
+        auto loadStep = [&](uint64_t base, uint32_t (&w)[U][4], uint32_t (&msk)[U]) {
+#pragma unroll
+            for (int k = 0; k < U; ++k)
+            {
+                u32x4 const x = loadVec<u32x4, true>(h.data + 2 * spanVoxelMask<CONTIG>(h, base + k * 64 + lane, msk[k]));
+                w[k][0] = x.x; w[k][1] = x.y; w[k][2] = x.z; w[k][3] = x.w;
             }
         };
         uint64_t const wave = static_cast<uint64_t>(blockIdx.x) * (kBlock / 64) + (threadIdx.x >> 6);
         uint64_t const waves = static_cast<uint64_t>(gridDim.x) * (kBlock / 64);
         uint64_t const steps = h.items / (64 * U);
-        for (uint64_t st = wave; st < steps; st += waves)
+        if constexpr (PIPE)
         {
-            uint32_t w[U][4], msk[U];
-#pragma unroll
-            for (int k = 0; k < U; ++k)
+            uint32_t wa[U][4], ma[U], wb[U][4], mb[U];
+            uint64_t st = wave;
+            if (st < steps)
+                loadStep(st * (64 * U), wa, ma);
+            while (st < steps)   // wave-uniform
             {
-                u32x4 const x = loadVec<u32x4, true>(
-                    h.data + 2 * spanVoxelMask<CONTIG>(h, st * (64 * U) + k * 64 + lane, msk[k]));
-                w[k][0] = x.x; w[k][1] = x.y; w[k][2] = x.z; w[k][3] = x.w;
+                uint64_t const s1 = st + waves;
+                if (s1 < steps)
+                    loadStep(s1 * (64 * U), wb, mb);
+                doStep(wa, ma, st * (64 * U), __any(p.prod != 0.0));
+                if (s1 >= steps)
+                    break;
+                uint64_t const s2 = s1 + waves;
+                if (s2 < steps)
+                    loadStep(s2 * (64 * U), wa, ma);
+                doStep(wb, mb, s1 * (64 * U), __any(p.prod != 0.0));
+                st = s2;
             }
-            bool const prodLive = __any(p.prod != 0.0);   // wave-uniform
-#pragma unroll
-            for (int k = 0; k < U; ++k)
-                item8(w[k], msk[k], st * (64 * U) + k * 64 + lane, prodLive);
-            flushStep();
+        }
+        else
+        {
+            for (uint64_t st = wave; st < steps; st += waves)
+            {
+                uint32_t w[U][4], msk[U];
+                loadStep(st * (64 * U), w, msk);
+                doStep(w, msk, st * (64 * U), __any(p.prod != 0.0));
+            }
         }
         for (uint64_t it = steps * (64 * U) + wave * 64 + lane; it < h.items; it += waves * 64)
         {
-            uint32_t w[4], m;
-            u32x4 const x = loadVec<u32x4, true>(h.data + 2 * spanVoxelMask<CONTIG>(h, it, m));
-            w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w;
-            item8(w, m, it, true);
+            uint32_t w[1][4], m[1];
+            u32x4 const x = loadVec<u32x4, true>(h.data + 2 * spanVoxelMask<CONTIG>(h, it, m[0]));
+            w[0][0] = x.x; w[0][1] = x.y; w[0][2] = x.z; w[0][3] = x.w;
+            u16x2 mn = {0xFFFFu, 0xFFFFu}, mx = {0, 0};
+            item8(w[0], m[0], true, mn, mx);
+            extremes(w[0], m[0], it);
             flushStep();
         }
         momentBlockReduce<kBlock / 64>(p);
@@ -2530,6 +2578,65 @@ namespace hipk
         return true;
     }
 
+    // The integer-moments kernel variant (knob aggregates.moments_pipe: 0 one buffer, 4 items per
+    // lane and step; 1 two buffers (next step's loads in flight during this step's arithmetic),
+    // 4 items; 2 two buffers, 8 items; 3 one buffer, 8 items; 4 two buffers, 2 items) and its grid: as many workgroups as the variant keeps
+    // resident on every CU (hipOccupancyMaxActiveBlocksPerMultiprocessor, at most 8) -- a grid-
+    // stride walk with more would leave a second partial wave of workgroups running alone.
+    using MomentKernelU16 = void (*)(FastHistArgs, MomentPartialU16*);
+
+    template <bool CONTIG>
+    MomentKernelU16 momentKernelU16(int64_t v, int& itemsPerLane)
+    {
+        switch (v)
+        {
+        case 1: itemsPerLane = 4; return aggregatesMomentsU16Kernel<CONTIG, 4, true>;
+        case 2: itemsPerLane = 8; return aggregatesMomentsU16Kernel<CONTIG, 8, true>;
+        case 3: itemsPerLane = 8; return aggregatesMomentsU16Kernel<CONTIG, 8, false>;
+        case 4: itemsPerLane = 2; return aggregatesMomentsU16Kernel<CONTIG, 2, true>;
+        default: itemsPerLane = 4; return aggregatesMomentsU16Kernel<CONTIG, 4, false>;
+        }
+    }
+
+    MomentKernelU16 momentKernelU16(bool contig, int& itemsPerLane)
+    {
+        int64_t const v = rt::knob(rt::Knob::AggregatesMomentsPipe);
+        return contig ? momentKernelU16<true>(v, itemsPerLane) : momentKernelU16<false>(v, itemsPerLane);
+    }
+
+    unsigned residentBlocksPerCU(void const* fn)
+    {
+        static std::mutex mu;
+        static std::unordered_map<void const*, unsigned> cache;
+        std::lock_guard<std::mutex> lock(mu);
+        auto it = cache.find(fn);
+        if (it != cache.end())
+            return it->second;
+        int n = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, kBlock, 0) != hipSuccess || n < 1)
+        {
+            (void)hipGetLastError();
+            n = 4;
+        }
+        unsigned const r = static_cast<unsigned>(std::min(n, 8));
+        cache.emplace(fn, r);
+        return r;
+    }
+
+    unsigned momentGridItemsU16(uint64_t items, bool contig)
+    {
+        int u = 4;
+        MomentKernelU16 const k = momentKernelU16(contig, u);
+        return streamingGrid(items, 64u * static_cast<unsigned>(u) * (kBlock / 64),
+                             residentBlocksPerCU(reinterpret_cast<void const*>(k)));
+    }
+
+    void launchMomentsU16Kernel(FastHistArgs const& h, bool contig, unsigned g, MomentPartialU16* parts, hipStream_t s)
+    {
+        int u = 4;
+        hipLaunchKernelGGL(momentKernelU16(contig, u), dim3(g), dim3(kBlock), 0, s, h, parts);
+    }
+
     // UInt16 under the unit mapping: ComputeAggregates from one pass of integer moments
     // (aggregatesMomentsU16Kernel + its final kernel) into res[0], res[1]; 0 when the range does
     // not take it, else the number of partials (scratch: that many MomentPartialU16).
@@ -2539,7 +2646,7 @@ namespace hipk
         if (a.fmt != codec::FmtUInt16 || !codec::isUnitMapping(a.lo, a.hi) ||
             (rt::knob(rt::Knob::AggregatesMoments) & 1) == 0 || !makeSpanArgs(a, h, contig))
             return 0;
-        return streamingGrid(h.items, 64u * 4u * (kBlock / 64), 8);
+        return momentGridItemsU16(h.items, contig);
     }
 
     // 1 when some UInt16 code decodes to a nonzero |v| < 2^-40 under (lo, hi): every code once on
@@ -2598,10 +2705,7 @@ namespace hipk
     void launchMomentsU16(FastHistArgs const& h, bool contig, unsigned g, double numElems, MomentPartialU16* parts,
                           vktHipAggregatePartial_t* res, hipStream_t s)
     {
-        if (contig)
-            hipLaunchKernelGGL(aggregatesMomentsU16Kernel<true>, dim3(g), dim3(kBlock), 0, s, h, parts);
-        else
-            hipLaunchKernelGGL(aggregatesMomentsU16Kernel<false>, dim3(g), dim3(kBlock), 0, s, h, parts);
+        launchMomentsU16Kernel(h, contig, g, parts, s);
         hipLaunchKernelGGL(aggregatesMomentsU16FinalKernel, dim3(1), dim3(kBlock), 0, s, parts, g, numElems, res);
     }
 
@@ -2910,7 +3014,7 @@ vktError vktHipAggregateMoments(vktHipVolumeView_t volume, vktVec3i_t first, vkt
     if (!makeSpanArgs(a, h, contig))
         return rt::fail("vktHipAggregateMoments: the range does not take the moments walk (16-B aligned volume with "
                         "dimX % 8 == 0 needed)");
-    unsigned const g = streamingGrid(h.items, 64u * 4u * (kBlock / 64), 8);
+    unsigned const g = integer ? momentGridItemsU16(h.items, contig) : streamingGrid(h.items, 64u * 4u * (kBlock / 64), 8);
     hipStream_t s = rt::computeStream();
     AggScratch& sc = aggScratch();
     size_t const unit = std::max(sizeof(MomentPartialU16), sizeof(MomentPartialF));
@@ -2925,10 +3029,7 @@ vktError vktHipAggregateMoments(vktHipVolumeView_t volume, vktVec3i_t first, vkt
     if (integer)
     {
         auto* pp = reinterpret_cast<MomentPartialU16*>(parts);
-        if (contig)
-            hipLaunchKernelGGL(aggregatesMomentsU16Kernel<true>, dim3(g), dim3(kBlock), 0, s, h, pp);
-        else
-            hipLaunchKernelGGL(aggregatesMomentsU16Kernel<false>, dim3(g), dim3(kBlock), 0, s, h, pp);
+        launchMomentsU16Kernel(h, contig, g, pp, s);
         hipLaunchKernelGGL(momentsCombineU16Kernel, dim3(1), dim3(kBlock), 0, s, pp, g, pp + g);
         e = rt::check(hipMemcpyAsync(&host.u, pp + g, sizeof(host.u), hipMemcpyDeviceToHost, s), "hipMemcpyAsync");
     }

@@ -214,6 +214,8 @@ namespace rt
             {"memory.arena_chunk_mib", 0},
             {"decompose.block", 256},
             {"pointwise.dword_shift", 1},
+            {"aggregates.moments_pipe", 0},
+            {"decompose.batch", 0},
         };
         static_assert(sizeof(kKnobs) / sizeof(kKnobs[0]) == static_cast<size_t>(Knob::Count), "knob table");
         std::atomic<int64_t> gKnobs[static_cast<int>(Knob::Count)] = {{kKnobs[0].def}, {kKnobs[1].def},
@@ -227,7 +229,8 @@ namespace rt
                                                                   {kKnobs[16].def}, {kKnobs[17].def},
                                                                   {kKnobs[18].def}, {kKnobs[19].def},
                                                                   {kKnobs[20].def}, {kKnobs[21].def},
-                                                                  {kKnobs[22].def}, {kKnobs[23].def}};
+                                                                  {kKnobs[22].def}, {kKnobs[23].def},
+                                                                  {kKnobs[24].def}, {kKnobs[25].def}};
     } // namespace
 
     int64_t knob(Knob k) { return gKnobs[static_cast<int>(k)].load(std::memory_order_relaxed); }
