@@ -96,7 +96,7 @@ VKTAPI vktError vktHipKernelScopeEnd(vktHipKernelScope scope);
  * aligned vector path cannot take to the per-voxel kernel), "pointwise.merge_sectors" (1; 0 stops
  * the general path from completing the 64-B sectors at the row ends of a box by rewriting the
  * destination's own bytes around it), "pointwise.general_32bit" (1; 0 makes the general path use
- * its 64-bit addressing, otherwise taken only for operands of 4 GiB and more), "pointwise.u8_pairs"
+ * its 64-bit addressing, otherwise taken only for operands beyond 4 GiB from their 16-B aligned base), "pointwise.u8_pairs"
  * (1; 0 keeps UInt8 multi-row boxes on the 8-voxel per-item loop instead of 16-B accesses on a
  * 16-voxel row grid), "histogram.packed16" (1; 0 makes histograms with more bins than one LDS
  * tile of 32-bit counters take one pass per tile instead of one pass over packed 16-bit
@@ -120,7 +120,11 @@ VKTAPI vktError vktHipKernelScopeEnd(vktHipKernelScope scope);
  * stage of the general path's window shift for 4-byte voxels at 4-B aligned addresses), "aggregates.moments" (3; bit 0: UInt16
  * ComputeAggregates under the unit mapping from one pass of exact integer moments, bit 1: UInt16
  * under other mappings and Float32 from one pass of floating-point moments -- both instead of
- * "aggregates.codes" / the two float passes).  For tests and in-process A/B measurements; unknown names return
+ * "aggregates.codes" / the two float passes), "aggregates.moments_pipe" (1; integer-moments kernel
+ * variant: 0 one register buffer of 4 items per lane and wave-step, 1 two buffers of 4 (the next
+ * step's loads in flight during this step's arithmetic), 2 two of 8, 3 one of 8, 4 two of 2),
+ * "decompose.batch" (0; 1 plans and copies BrickDecompose in up to 8 batches of brick planes).
+ * For tests and in-process A/B measurements; unknown names return
  * vktInvalidValue.
  *
  * Writes outside a range box: FillRange / CopyRange / convert and device-functor TransformRange

@@ -769,3 +769,54 @@ def test_aggregates_float_moments_and_fallbacks():
     got, two = both(codes, 5, tiny_map, (0, 0, 0), (256, 16, 8))
     for f in ("min", "max", "sum", "mean", "var", "prod"):
         assert getattr(got, f) == getattr(two, f), f
+
+
+@pytest.mark.gpu
+def test_moments_first_occurrence_across_wave_steps():
+    """The moment kernels keep each lane's extremes per wave-step and look up the first voxel of
+    the extreme code in its step after the walk.  Volumes large enough that every wave walks many
+    steps, with the extreme values repeated at scattered positions (ties within and across steps,
+    lanes and workgroups), +0 / -0 both minimal for Float32: arg positions are the first
+    occurrences in linear order and min keeps the first zero's sign -- as the reference's strict
+    in-order updates (Aggregates_serial.hpp:40-49).  Spans and a padded sub-box."""
+    rng = np.random.default_rng(4242)
+    shape = (128, 256, 1024)   # (z, y, x): 32 Mi voxels, ~4 Mi items, many steps per wave
+    n = shape[0] * shape[1] * shape[2]
+
+    def first_xyz(flat, idx_box):
+        z, y, x = np.unravel_index(flat, idx_box)
+        return int(x), int(y), int(z)
+
+    # UInt16, unit mapping (integer moments): codes in [1, 65534], then 0 and 65535 at 300
+    # random places each
+    codes = rng.integers(1, 65535, shape, dtype=np.uint16)
+    flat = codes.reshape(-1)
+    flat[rng.choice(n, 300, replace=False)] = 0
+    flat[rng.choice(n, 300, replace=False)] = 65535
+    for first, last in (((0, 0, 0), (1024, 256, 128)), ((100, 3, 5), (900, 250, 120))):
+        (x0, y0, z0), (x1, y1, z1) = first, last
+        sub = codes[z0:z1, y0:y1, x0:x1]
+        a = gpu_aggregates(codes, 5, 0.0, 1.0, first, last)
+        lo, hi = np.argmin(sub), np.argmax(sub)
+        ex, ey, ez = first_xyz(lo, sub.shape)
+        assert tuple(a.argmin) == (ex + x0, ey + y0, ez + z0), (first, "argmin")
+        ex, ey, ez = first_xyz(hi, sub.shape)
+        assert tuple(a.argmax) == (ex + x0, ey + y0, ez + z0), (first, "argmax")
+        assert a.min == 0.0 and a.max == np.float32(65535 / 65536)
+    # Float32 (float moments): values in [1, 2), zeros of random sign and a repeated maximum 5.0
+    vals = rng.uniform(1.0, 2.0, shape).astype(np.float32)
+    fv = vals.reshape(-1)
+    zeros = rng.choice(n, 200, replace=False)
+    fv[zeros] = np.where(rng.random(200) < 0.5, np.float32(0.0), np.float32(-0.0))
+    fv[rng.choice(n, 200, replace=False)] = 5.0
+    for first, last in (((0, 0, 0), (1024, 256, 128)), ((100, 3, 5), (900, 250, 120))):
+        (x0, y0, z0), (x1, y1, z1) = first, last
+        sub = vals[z0:z1, y0:y1, x0:x1]
+        a = gpu_aggregates(vals.view(np.uint32), 7, 0.0, 1.0, first, last)
+        lo, hi = np.argmin(sub), np.argmax(sub)
+        ex, ey, ez = first_xyz(lo, sub.shape)
+        assert tuple(a.argmin) == (ex + x0, ey + y0, ez + z0), (first, "argmin f32")
+        assert np.signbit(np.float32(a.min)) == np.signbit(sub.reshape(-1)[lo]), (first, "sign of the first zero")
+        ex, ey, ez = first_xyz(hi, sub.shape)
+        assert tuple(a.argmax) == (ex + x0, ey + y0, ez + z0), (first, "argmax f32")
+        assert a.max == 5.0

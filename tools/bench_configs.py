@@ -908,6 +908,24 @@ def main():
                        timed(lambda: lib.vktHipAggregatesRange(V, a0, a1, C.byref(agg)), R), 2 * nv, nv)
         lib.vktHipSetTuningKnob(b"aggregates.moments_pipe", -1)
         free(V)
+    if want("momf"):
+        # float moments (knob aggregates.moments bit 1: UInt16 under another mapping, Float32) vs
+        # the two float passes, per call incl. the D2H of the result
+        n = 1024
+        agg = _lib.Aggregates_t()
+        for fmt, bpv, lo, hi, name in ((7, 4, 0.0, 1.0, "Float32"), (5, 2, -1.0, 3.0, "UInt16 mapping [-1,3]")):
+            V = alloc((n,) * 3, fmt, lo, hi, seed=12)
+            if fmt == 7:   # finite values (random bits would hold NaNs: the moments fall back)
+                rng_fill(V, n ** 3)
+            for mom, what in ((3, "moments"), (1, "2 float passes")):
+                lib.vktHipSetTuningKnob(b"aggregates.moments", mom)
+                for a0, a1, box in ((o, Vec3i_t(n, n, n), "1024^3"),
+                                    (Vec3i_t(100, 100, 100), Vec3i_t(900, 900, 900), "800^3 sub-box at x0=100")):
+                    nv = (a1.x - a0.x) * (a1.y - a0.y) * (a1.z - a0.z)
+                    report(f"momf Aggregates {name} {box} [{what}]",
+                           timed(lambda: lib.vktHipAggregatesRange(V, a0, a1, C.byref(agg)), R), bpv * nv, nv)
+            lib.vktHipSetTuningKnob(b"aggregates.moments", -1)
+            free(V)
     if want("decbatch"):
         # in-process A/B of BrickDecompose's batched planning (knob decompose.batch: 1 up to 8
         # batches of brick planes, planning batch k + 1 while the GPU copies batch k; 0 one batch)

@@ -606,104 +606,146 @@ vktError vktHipBrickDecompose(vktHipVolumeView_t source, vktHipBrickRange_t cons
     uint32_t maxItems = 0;
     int32_t errBrick = numBricks;
     char const* errWhat = nullptr;
-    rt::parallelFor(static_cast<size_t>(numBricks), 4096, [&](size_t b, size_t e) {
-        // bricks of a decomposition share a few sizes: reuse the last divisor of each kind (each
-        // makeFastDiv costs a 64-bit division)
-        struct LastDiv
-        {
-            FastDiv f{0u, 0u, 0u};
-            bool valid = false;
-            FastDiv operator()(uint32_t d)
+    // A uniform grid (the usual BrickDecompose list) uploads only the brick pointers: the pass
+    // validates every range and builds its descriptor on the stack, storing no table (262 144
+    // descriptors of 16^3 bricks are 25 MB of host writes per call).  When the grid does not hold
+    // (or was not guessed), a second pass -- or the only one -- writes the table.
+    auto pass = [&](bool writeTable) {
+        rt::parallelFor(static_cast<size_t>(numBricks), 4096, [&](size_t b, size_t e) {
+            // bricks of a decomposition share a few sizes: reuse the last divisor of each kind
+            // (each makeFastDiv costs a 64-bit division)
+            struct LastDiv
             {
-                if (!valid || f.d != d)
+                FastDiv f{0u, 0u, 0u};
+                bool valid = false;
+                FastDiv operator()(uint32_t d)
                 {
-                    f = makeFastDiv(d);
-                    valid = true;
+                    if (!valid || f.d != d)
+                    {
+                        f = makeFastDiv(d);
+                        valid = true;
+                    }
+                    return f;
                 }
-                return f;
+            } divSeg, divX, divWpr, divY;
+            std::vector<int32_t> mySlow;
+            bool myGrid = !writeTable && guess.ok && gridOk.load(std::memory_order_relaxed);
+            uint32_t myMax = 0;
+            int32_t myErr = numBricks;
+            char const* myWhat = nullptr;
+            BrickDesc local;
+            for (size_t ii = b; ii < e; ++ii)
+            {
+                int32_t const i = static_cast<int32_t>(ii);
+                vktHipBrickRange_t const& br = bricks[i];
+                BrickDesc& d = writeTable ? fast[i] : local;
+                d = BrickDesc{};
+                d.fx = br.first.x;
+                d.fy = br.first.y;
+                d.fz = br.first.z;
+                if (!validView(br.brick))
+                {
+                    myErr = i;
+                    myWhat = "vktHipBrickDecompose: invalid brick view";
+                    break;
+                }
+                int64_t nx = int64_t(br.last.x) - br.first.x, ny = int64_t(br.last.y) - br.first.y;
+                int64_t nz = int64_t(br.last.z) - br.first.z;
+                if (nx <= 0 || ny <= 0 || nz <= 0)
+                {
+                    myGrid = false;   // (the grid kernel would copy a box for it)
+                    continue;
+                }
+                if (nx > br.brick.dimX || ny > br.brick.dimY || nz > br.brick.dimZ)
+                {
+                    myErr = i;
+                    myWhat = "vktHipBrickDecompose: brick smaller than its range (reference writes out of bounds)";
+                    break;
+                }
+                if (overlaps(br.brick, source))
+                {
+                    myErr = i;
+                    myWhat = "vktHipBrickDecompose: brick aliases the source";
+                    break;
+                }
+                bool bytewise = br.brick.dataFormat == source.dataFormat && br.brick.mappingLo == source.mappingLo &&
+                                br.brick.mappingHi == source.mappingHi;   // Copy_serial.hpp:21-22
+                uint64_t nv = static_cast<uint64_t>(nx) * static_cast<uint64_t>(ny) * static_cast<uint64_t>(nz);
+                if (!bytewise || nv >= (1ull << 31))
+                {
+                    mySlow.push_back(i);
+                    myGrid = false;
+                    continue;
+                }
+                d.dst = br.brick.data;
+                d.dimX = br.brick.dimX;
+                d.dimY = br.brick.dimY;
+                uint32_t const seg = static_cast<uint32_t>((nx + V - 1) >> vShift);   // 16-B segments per row
+                d.nx = static_cast<int32_t>(nx);
+                d.nvox = static_cast<uint32_t>(nv);
+                d.linear = nx == br.brick.dimX && ny == br.brick.dimY && nx >= V && srcAligned &&
+                           reinterpret_cast<uintptr_t>(br.brick.data) % 16 == 0;
+                d.nitems = d.linear ? static_cast<uint32_t>((nv + V - 1) >> vShift) : static_cast<uint32_t>(ny * nz) * seg;
+                d.fseg = divSeg(seg);
+                d.fdx = divX(static_cast<uint32_t>(nx));
+                {
+                    int64_t const span = std::min<int64_t>(br.first.x + nx, source.dimX) - std::max<int32_t>(br.first.x, 0);
+                    d.fwpr = divWpr(span > 0 ? static_cast<uint32_t>((span * bpv + 15) / 16 + 1) : 0u);
+                }
+                d.fdy = divY(static_cast<uint32_t>(ny));
+                myMax = d.nitems > myMax ? d.nitems : myMax;
+                if (myGrid)
+                {
+                    myGrid = gridMatches(guess, br, d, ii, source.dimX);
+                    ptrs[i] = d.dst;
+                }
             }
-        } divSeg, divX, divWpr, divY;
-        std::vector<int32_t> mySlow;
-        bool myGrid = guess.ok && gridOk.load(std::memory_order_relaxed);
-        uint32_t myMax = 0;
-        int32_t myErr = numBricks;
-        char const* myWhat = nullptr;
-        for (size_t ii = b; ii < e; ++ii)
+            if (!myGrid)
+                gridOk.store(false, std::memory_order_relaxed);
+            std::lock_guard<std::mutex> g(merge);
+            if (writeTable || !guess.ok)
+                slow.insert(slow.end(), mySlow.begin(), mySlow.end());
+            maxItems = std::max(maxItems, myMax);
+            if (myErr < errBrick)
+            {
+                errBrick = myErr;
+                errWhat = myWhat;
+            }
+        });
+    };
+    if (guess.ok)
+    {
+        pass(false);
+        if (errWhat == nullptr && !gridOk.load())
         {
-            int32_t const i = static_cast<int32_t>(ii);
-            vktHipBrickRange_t const& br = bricks[i];
-            BrickDesc& d = fast[i];
-            d = BrickDesc{};
-            d.fx = br.first.x;
-            d.fy = br.first.y;
-            d.fz = br.first.z;
-            if (!validView(br.brick))
+            maxItems = 0;
+            pass(true);   // the grid failed somewhere: the descriptor table after all
+        }
+        else if (errWhat == nullptr)
+        {
+            // the class representatives' descriptors (gridDivisors) and the brick-row run below
+            auto rep = [](int c, int32_t nb) -> size_t { return c == 0 ? 0 : (c == 1 ? (nb > 2 ? 1 : 0) : nb - 1); };
+            std::vector<size_t> reps;
+            for (int c = 0; c < 3; ++c)
             {
-                myErr = i;
-                myWhat = "vktHipBrickDecompose: invalid brick view";
-                break;
+                reps.push_back(rep(c, guess.g.nbx));
+                reps.push_back(rep(c, guess.g.nby) * static_cast<size_t>(guess.g.nbx));
             }
-            int64_t nx = int64_t(br.last.x) - br.first.x, ny = int64_t(br.last.y) - br.first.y;
-            int64_t nz = int64_t(br.last.z) - br.first.z;
-            if (nx <= 0 || ny <= 0 || nz <= 0)
+            for (size_t r : reps)
             {
-                myGrid = false;   // (the grid kernel would copy a box for it)
-                continue;
-            }
-            if (nx > br.brick.dimX || ny > br.brick.dimY || nz > br.brick.dimZ)
-            {
-                myErr = i;
-                myWhat = "vktHipBrickDecompose: brick smaller than its range (reference writes out of bounds)";
-                break;
-            }
-            if (overlaps(br.brick, source))
-            {
-                myErr = i;
-                myWhat = "vktHipBrickDecompose: brick aliases the source";
-                break;
-            }
-            bool bytewise = br.brick.dataFormat == source.dataFormat && br.brick.mappingLo == source.mappingLo &&
-                            br.brick.mappingHi == source.mappingHi;   // Copy_serial.hpp:21-22
-            uint64_t nv = static_cast<uint64_t>(nx) * static_cast<uint64_t>(ny) * static_cast<uint64_t>(nz);
-            if (!bytewise || nv >= (1ull << 31))
-            {
-                mySlow.push_back(i);
-                continue;
-            }
-            d.dst = br.brick.data;
-            d.dimX = br.brick.dimX;
-            d.dimY = br.brick.dimY;
-            uint32_t const seg = static_cast<uint32_t>((nx + V - 1) >> vShift);   // 16-B segments per row
-            d.nx = static_cast<int32_t>(nx);
-            d.nvox = static_cast<uint32_t>(nv);
-            d.linear = nx == br.brick.dimX && ny == br.brick.dimY && nx >= V && srcAligned &&
-                       reinterpret_cast<uintptr_t>(br.brick.data) % 16 == 0;
-            d.nitems = d.linear ? static_cast<uint32_t>((nv + V - 1) >> vShift) : static_cast<uint32_t>(ny * nz) * seg;
-            d.fseg = divSeg(seg);
-            d.fdx = divX(static_cast<uint32_t>(nx));
-            {
+                vktHipBrickRange_t const& br = bricks[r];
+                BrickDesc& d = fast[r];
+                d = BrickDesc{};
+                int64_t const nx = int64_t(br.last.x) - br.first.x, ny = int64_t(br.last.y) - br.first.y;
                 int64_t const span = std::min<int64_t>(br.first.x + nx, source.dimX) - std::max<int32_t>(br.first.x, 0);
-                d.fwpr = divWpr(span > 0 ? static_cast<uint32_t>((span * bpv + 15) / 16 + 1) : 0u);
-            }
-            d.fdy = divY(static_cast<uint32_t>(ny));
-            myMax = d.nitems > myMax ? d.nitems : myMax;
-            if (myGrid)
-            {
-                myGrid = gridMatches(guess, br, d, ii, source.dimX);
-                ptrs[i] = d.dst;
+                d.fdx = makeFastDiv(static_cast<uint32_t>(nx));
+                d.fwpr = makeFastDiv(span > 0 ? static_cast<uint32_t>((span * bpv + 15) / 16 + 1) : 0u);
+                d.fdy = makeFastDiv(static_cast<uint32_t>(ny));
             }
         }
-        if (!myGrid)
-            gridOk.store(false, std::memory_order_relaxed);
-        std::lock_guard<std::mutex> g(merge);
-        slow.insert(slow.end(), mySlow.begin(), mySlow.end());
-        maxItems = std::max(maxItems, myMax);
-        if (myErr < errBrick)
-        {
-            errBrick = myErr;
-            errWhat = myWhat;
-        }
-    });
+    }
+    else
+        pass(true);
     if (errWhat != nullptr)   // the first bad brick in list order, before anything launched
         return rt::fail(errWhat);
     std::sort(slow.begin(), slow.end());
@@ -721,7 +763,7 @@ vktError vktHipBrickDecompose(vktHipVolumeView_t source, vktHipBrickRange_t cons
         // Array3D).  Any group size dividing the brick count maps blocks 1:1 onto (brick,
         // chunk); it only changes the order in which bricks are visited.
         size_t run = 1;
-        while (run < nFast && fast[run].fy == fast[0].fy && fast[run].fz == fast[0].fz)
+        while (run < nFast && bricks[run].first.y == bricks[0].first.y && bricks[run].first.z == bricks[0].first.z)
             ++run;
         bool const useGrid = slow.empty() && guess.ok && gridOk.load() && nFast == static_cast<size_t>(numBricks);
         if (useGrid)

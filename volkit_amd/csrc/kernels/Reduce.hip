@@ -1462,8 +1462,15 @@ namespace hipk
     // U items per lane and wave-step; PIPE: the next step's loads are issued before this step's
     // arithmetic (two register buffers), so a wave keeps 16 U bytes per lane in flight while it
     // computes -- without it the loads of a step wait behind the previous step's ALU work.
+    // waves per SIMD each variant is built for (without a bound the one-buffer 4-item span kernel
+    // took 76 VGPRs: 6 waves; bound to 8 it fits 56 with no spill; the row form spills at 8)
+    constexpr int momentWaves(bool contig, int u, bool pipe)
+    {
+        return pipe ? 4 : u <= 4 ? (contig ? 8 : 6) : (contig ? 6 : 4);
+    }
+
     template <bool CONTIG, int U, bool PIPE>
-    __global__ __launch_bounds__(kBlock) void aggregatesMomentsU16Kernel(FastHistArgs h, MomentPartialU16* partials)
+    __global__ __launch_bounds__(kBlock, momentWaves(CONTIG, U, PIPE)) void aggregatesMomentsU16Kernel(FastHistArgs h, MomentPartialU16* partials)
     {
         uint32_t const lane = threadIdx.x & 63;
         MomentPartialU16 p;
@@ -1562,19 +1569,42 @@ namespace hipk
         };
         // a wave-step of U items: sums, then -- only when the step's packed bounds can improve
         // the lane's extremes (rare after the first steps) -- the in-order per-voxel updates
-        auto doStep = [&](uint32_t const (&w)[U][4], uint32_t const (&msk)[U], uint64_t base, bool prodLive) {
+        // The lane's extremes per wave-step, branch-free: a step that holds a new strict minimum
+        // (maximum) records its code and the step's base item; the first voxel of that code in
+        // that step -- the lane's first occurrence, every earlier step held only larger (smaller)
+        // codes -- is looked up once after the walk (resolveStep).  Every item holds a voxel of the
+        // range, so the masked packed bounds are the step's true extremes.  (Per-voxel updates
+        // inside the step cost ~3x the step's sums: with 64 lanes some lane improves in most
+        // of a wave's few dozen steps, and the whole wave runs the divergent branch.)
+        uint32_t minStep = ~0u, maxStep = ~0u;   // (steps < 2^32: 2^32 steps would be >= 16 TiB of codes)
+        auto doStep = [&](uint32_t const (&w)[U][4], uint32_t const (&msk)[U], uint32_t st, bool prodLive) {
             u16x2 mn = {0xFFFFu, 0xFFFFu}, mx = {0, 0};
 #pragma unroll
             for (int k = 0; k < U; ++k)
                 item8(w[k], msk[k], prodLive, mn, mx);
             uint32_t const imin = mn.x < mn.y ? mn.x : mn.y, imax = mx.x > mx.y ? mx.x : mx.y;
-            if ((imin < p.cmin) | (static_cast<int32_t>(imax) > p.cmax))
-            {
-#pragma unroll
-                for (int k = 0; k < U; ++k)
-                    extremes(w[k], msk[k], base + k * 64 + lane);
-            }
+            bool const lower = imin < p.cmin, higher = static_cast<int32_t>(imax) > p.cmax;
+            p.cmin = lower ? imin : p.cmin;
+            minStep = lower ? st : minStep;
+            p.cmax = higher ? static_cast<int32_t>(imax) : p.cmax;
+            maxStep = higher ? st : maxStep;
             flushStep();
+        };
+        // index of the first voxel with code c in step st (its items reloaded)
+        auto resolveStep = [&](uint32_t st, uint32_t c) -> uint64_t {
+            uint64_t const base = static_cast<uint64_t>(st) * (64 * U);
+            uint64_t at = kNoIndex;
+            for (int k = U - 1; k >= 0; --k)
+            {
+                uint32_t m;
+                uint64_t const item = base + static_cast<uint64_t>(k) * 64 + lane;
+                u32x4 const x = loadVec<u32x4, false>(h.data + 2 * spanVoxelMask<CONTIG>(h, item, m));
+                uint32_t const w[4] = {x.x, x.y, x.z, x.w};
+                for (int j = 7; j >= 0; --j)
+                    if (((m >> j) & 1u) && ((w[j / 2] >> (16 * (j % 2))) & 0xFFFFu) == c)
+                        at = spanGlobalIndex<CONTIG>(h, item, j);
+            }
+            return at;
         };
         auto loadStep = [&](uint64_t base, uint32_t (&w)[U][4], uint32_t (&msk)[U]) {
 #pragma unroll
@@ -1598,13 +1628,13 @@ namespace hipk
                 uint64_t const s1 = st + waves;
                 if (s1 < steps)
                     loadStep(s1 * (64 * U), wb, mb);
-                doStep(wa, ma, st * (64 * U), __any(p.prod != 0.0));
+                doStep(wa, ma, static_cast<uint32_t>(st), __any(p.prod != 0.0));
                 if (s1 >= steps)
                     break;
                 uint64_t const s2 = s1 + waves;
                 if (s2 < steps)
                     loadStep(s2 * (64 * U), wa, ma);
-                doStep(wb, mb, s1 * (64 * U), __any(p.prod != 0.0));
+                doStep(wb, mb, static_cast<uint32_t>(s1), __any(p.prod != 0.0));
                 st = s2;
             }
         }
@@ -1614,9 +1644,13 @@ namespace hipk
             {
                 uint32_t w[U][4], msk[U];
                 loadStep(st * (64 * U), w, msk);
-                doStep(w, msk, st * (64 * U), __any(p.prod != 0.0));
+                doStep(w, msk, static_cast<uint32_t>(st), __any(p.prod != 0.0));
             }
         }
+        if (minStep != ~0u)
+            p.minIndex = resolveStep(minStep, p.cmin);
+        if (maxStep != ~0u)
+            p.maxIndex = resolveStep(maxStep, static_cast<uint32_t>(p.cmax));
         for (uint64_t it = steps * (64 * U) + wave * 64 + lane; it < h.items; it += waves * 64)
         {
             uint32_t w[1][4], m[1];
@@ -1795,16 +1829,20 @@ namespace hipk
             else
                 return codec::decode(c, FMT, h.lo, h.hi);
         };
-        auto visit8 = [&](uint32_t const (&c)[8], uint64_t item, uint64_t hb, uint32_t m, bool prodLive) {
+        auto gIndexOf = [&](uint64_t item, uint64_t hb, int j) -> uint64_t {
+            if (CONTIG && hb != ~0ull)
+                return h.giBase + hb * 8 + 4 * lane + (j < 4 ? static_cast<uint64_t>(j) : 252ull + j);
+            return spanGlobalIndex<CONTIG>(h, item, j);
+        };
+        // STEP: the extremes are the wave-step's (slo / shi, resolved after the walk as in
+        // aggregatesMomentsU16Kernel); otherwise (tail items) the in-order per-voxel updates
+        auto visit8 = [&](uint32_t const (&c)[8], uint64_t item, uint64_t hb, uint32_t m, bool prodLive, bool step,
+                          float& slo, float& shi) {
             float v[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j)
                 v[j] = decodeV(c[j]);
-            auto gIndex = [&](int j) -> uint64_t {
-                if (CONTIG && hb != ~0ull)
-                    return h.giBase + hb * 8 + 4 * lane + (j < 4 ? static_cast<uint64_t>(j) : 252ull + j);
-                return spanGlobalIndex<CONTIG>(h, item, j);
-            };
+            auto gIndex = [&](int j) -> uint64_t { return gIndexOf(item, hb, j); };
             // the lane's pivot: its first valid value (0 when that is not finite: the result then
             // falls back anyway)
             if (n == 0)
@@ -1819,11 +1857,16 @@ namespace hipk
 #pragma unroll
             for (int j = 0; j < 8; ++j)
             {
-                float const x = (m >> j) & 1u ? v[j] : p.minValue;
-                lo = fminf(lo, x);   // (NaN never qualifies: minNum / maxNum skip it)
-                hi = fmaxf(hi, x);
+                bool const in = (m >> j) & 1u;   // voxels outside the range never qualify
+                lo = fminf(lo, in ? v[j] : FLT_MAX);   // (NaN never qualifies: minNum / maxNum skip it)
+                hi = fmaxf(hi, in ? v[j] : -FLT_MAX);
             }
-            if (lo < p.minValue || hi > p.maxValue)
+            if (step)
+            {
+                slo = fminf(slo, lo);
+                shi = fmaxf(shi, hi);
+            }
+            else if (lo < p.minValue || hi > p.maxValue)
             {
 #pragma unroll
                 for (int j = 0; j < 8; ++j)
@@ -1864,6 +1907,7 @@ namespace hipk
         uint64_t const waves = static_cast<uint64_t>(gridDim.x) * (kBlock / 64);
         uint64_t const steps = h.items / (64 * U);
         bool const halves = CONTIG && BPV == 4 && (reinterpret_cast<uintptr_t>(h.data) & 15u) == 0;
+        uint32_t minStep = ~0u, maxStep = ~0u;   // the steps of the lane's extremes (as the integer kernel)
         for (uint64_t st = wave; st < steps; st += waves)
         {
             uint32_t c[U][8], msk[U];
@@ -1886,15 +1930,57 @@ namespace hipk
                     load8<BPV, true>(h.data, spanVoxelMask<CONTIG>(h, st * (64 * U) + k * 64 + lane, msk[k]), c[k]);
             }
             bool const prodLive = __any(p.prod != 0.0);   // wave-uniform: 0 stays 0 (finite values)
+            float slo = FLT_MAX, shi = -FLT_MAX;
 #pragma unroll
             for (int k = 0; k < U; ++k)
-                visit8(c[k], st * (64 * U) + k * 64 + lane, halves ? st * (64 * U) + k * 64 : ~0ull, msk[k], prodLive);
+                visit8(c[k], st * (64 * U) + k * 64 + lane, halves ? st * (64 * U) + k * 64 : ~0ull, msk[k], prodLive,
+                       true, slo, shi);
+            // strict: a later step reaching the same value keeps the earlier one (first occurrence)
+            bool const lower = slo < p.minValue, higher = shi > p.maxValue;
+            p.minValue = lower ? slo : p.minValue;
+            minStep = lower ? static_cast<uint32_t>(st) : minStep;
+            p.maxValue = higher ? shi : p.maxValue;
+            maxStep = higher ? static_cast<uint32_t>(st) : maxStep;
         }
+        // the first voxel of the lane's extreme value in its step (reloaded); the value is taken
+        // from that voxel (of +0 / -0, the first one's sign, as the strict in-order updates)
+        auto resolveStep = [&](uint32_t st, float value, uint64_t& index, float& out) {
+            uint64_t const base = static_cast<uint64_t>(st) * (64 * U);
+            for (int k = U - 1; k >= 0; --k)
+            {
+                uint32_t cc[8], m = 0xFFu;
+                uint64_t const item = base + static_cast<uint64_t>(k) * 64 + lane;
+                uint64_t const hb = halves ? base + static_cast<uint64_t>(k) * 64 : ~0ull;
+                if (halves)
+                {
+                    uint8_t const* q = h.data + ((base + k * 64) * 8 + 4 * lane) * 4;
+                    u32x4 const x = loadVec<u32x4, false>(q), y = loadVec<u32x4, false>(q + 1024);
+                    cc[0] = x.x; cc[1] = x.y; cc[2] = x.z; cc[3] = x.w;
+                    cc[4] = y.x; cc[5] = y.y; cc[6] = y.z; cc[7] = y.w;
+                }
+                else
+                    load8<BPV, false>(h.data, spanVoxelMask<CONTIG>(h, item, m), cc);
+                for (int j = 7; j >= 0; --j)
+                {
+                    float const v = decodeV(cc[j]);
+                    if (((m >> j) & 1u) && v == value)
+                    {
+                        index = gIndexOf(item, hb, j);
+                        out = v;
+                    }
+                }
+            }
+        };
+        if (minStep != ~0u)
+            resolveStep(minStep, p.minValue, p.minIndex, p.minValue);
+        if (maxStep != ~0u)
+            resolveStep(maxStep, p.maxValue, p.maxIndex, p.maxValue);
         for (uint64_t it = steps * (64 * U) + wave * 64 + lane; it < h.items; it += waves * 64)
         {
             uint32_t c[8], m;
             load8<BPV, true>(h.data, spanVoxelMask<CONTIG>(h, it, m), c);
-            visit8(c, it, ~0ull, m, true);
+            float slo = FLT_MAX, shi = -FLT_MAX;
+            visit8(c, it, ~0ull, m, true, false, slo, shi);
         }
         if (n != 0)
         {

@@ -214,7 +214,7 @@ namespace rt
             {"memory.arena_chunk_mib", 0},
             {"decompose.block", 256},
             {"pointwise.dword_shift", 1},
-            {"aggregates.moments_pipe", 0},
+            {"aggregates.moments_pipe", 1},
             {"decompose.batch", 0},
         };
         static_assert(sizeof(kKnobs) / sizeof(kKnobs[0]) == static_cast<size_t>(Knob::Count), "knob table");

@@ -98,7 +98,7 @@ namespace rt
         MemoryArenaChunkMiB,           // > 0: arena chunks of exactly max(request, this many MiB) (tests)
         DecomposeBlock,                // threads per BrickDecompose workgroup over one 16-KiB chunk: 256 or 128
         PointwiseDwordShift,           // 0: 4-byte general-path windows keep the byte-align stage (whole-dword offsets)
-        AggregatesMomentsPipe,         // integer moments: 0 one buffer x 4 items, 1 / 2 / 4 two buffers x 4 / 8 / 2 items, 3 one buffer x 8
+        AggregatesMomentsPipe,         // integer moments: 0 one buffer x 4 items, 1 (default) / 2 / 4 two buffers x 4 / 8 / 2 items, 3 one buffer x 8
         DecomposeBatch,                // 1: BrickDecompose plans / copies in up to 8 batches of brick planes (measured slower: off)
         Count
     };
