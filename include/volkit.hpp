@@ -200,6 +200,9 @@ namespace vkt
 
         ResourceHandle getResourceHandle() const { return resourceHandle_; }
 
+        //! True when the bytes already live on `ep`'s device (no migration pending for it).
+        bool residentOn(ExecutionPolicy const& ep) const { return ep.device == lastAllocationPolicy_.device; }
+
         //! If the thread's device changed since the last allocation, move the bytes there.
         void migrate()
         {
@@ -297,6 +300,10 @@ namespace vkt
         void getVoxelMapping(float& lo, float& hi);
         void setVoxelMapping(Vec2f mapping);
         Vec2f getVoxelMapping() const;
+
+        //! getData() for a caller that runs under `ep` (its thread's policy), without looking the
+        //! policy up when the bytes already live there (per-brick walks of BrickDecompose).
+        uint8_t* getDataFor(ExecutionPolicy const& ep) { return residentOn(ep) ? data_ : getData(); }
 
         Box3f getDomainBounds() const;
         Box3f getObjectBounds() const;

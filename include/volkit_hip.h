@@ -360,6 +360,29 @@ typedef struct {
 VKTAPI vktError vktHipBrickDecompose(vktHipVolumeView_t source, vktHipBrickRange_t const* bricks,
                                      int32_t numBricks);
 
+/* A uniform brick grid: numBricks = ceil(source dims / brickSize) per axis (reference
+ * Decompose.cpp:103-121); brick (ix, iy, iz), linear index ix + nbx * (iy + nby * iz), holds the
+ * source box [c - haloNeg, c + size + haloPos), c = (ix, iy, iz) * brickSize, size = brickSize
+ * except the last brick of an axis (the remainder). */
+typedef struct vktHipBrickGrid_t
+{
+    vktVec3i_t numBricks;
+    vktVec3i_t brickSize;
+    vktVec3i_t haloNeg;
+    vktVec3i_t haloPos;
+} vktHipBrickGrid_t;
+
+/* BrickDecompose of a uniform grid whose bricks are allocated exactly at their box size in the
+ * source's data format and voxel mapping (what BrickDecomposeResize builds), brick i's voxels
+ * at brickData[i] on the device.  The CALLER guarantees those dims / formats / mappings (the
+ * C / C++ front-ends check them per brick and otherwise call vktHipBrickDecompose); this checks
+ * the grid against the source, the pointers (non-null, none inside the source) and copies from
+ * the brick index alone -- no per-brick range list, no descriptor table: one pass over the
+ * bricks on the host instead of two (same bytes as vktHipBrickDecompose on the equivalent
+ * ranges; grids the index-derived kernel cannot take go through that path internally).
+ * brickData is read before the call returns. */
+VKTAPI vktError vktHipBrickDecomposeGrid(vktHipVolumeView_t source, vktHipBrickGrid_t grid, uint8_t* const* brickData);
+
 /* ---- reductions --------------------------------------------------
  * replaces ComputeAggregatesRange_cuda (declared by reference src/vkt/Aggregates_cuda.hpp,
  * never implemented); semantics of ComputeAggregatesRange_serial

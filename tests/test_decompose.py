@@ -316,3 +316,53 @@ def test_brick_decompose_narrow_rows(fmt):
     ref = ob.brick_decompose(ob.Volume(codes, fmt), (8, 64, 64), (0, 0, 0), (0, 0, 0))
     for idx, v in ref.items():
         np.testing.assert_array_equal(got[idx], v.codes, err_msg=f"brick {idx}")
+
+
+@pytest.mark.gpu
+def test_grid_entry_point_parity_and_validation():
+    """vktHipBrickDecomposeGrid (the front-ends' path for BrickDecomposeResize-shaped arrays)
+    through the C ABI: a 37x23x19 UInt16 source, 8^3 bricks with halos (2,1,0)/(1,2,3), bricks
+    allocated at their box sizes, bit-exact vs the oracle; a halo wider than a brick takes the
+    range path inside the call (same bytes); a null brick pointer, a brick inside the source and
+    a brick count that is not ceil(dims / brickSize) are refused before any copy."""
+    from volkit_amd import _lib as L
+    rng = np.random.default_rng(77)
+    dims = (37, 23, 19)
+    codes = rand_codes(rng, 5, dims[::-1])
+    nbytes = codes.nbytes
+    p = C.c_void_p()
+    assert lib.vktHipAllocate(C.byref(p), nbytes) == 0
+    src_ptr = p.value
+    assert lib.vktHipMemcpy(C.c_void_p(src_ptr), codes.ctypes.data, nbytes, 1) == 0
+    src = L.HipVolumeView_t(src_ptr, *dims, 5, 0.0, 1.0)
+    for brick, neg, pos in (((8, 8, 8), (2, 1, 0), (1, 2, 3)), ((4, 4, 4), (6, 1, 1), (5, 0, 2))):
+        ref = ob.brick_decompose(ob.Volume(codes, 5), brick, neg, pos)
+        nb = tuple(-(-d // b) for d, b in zip(dims, brick))
+        ptrs, shapes = [], []
+        for k in range(nb[2]):
+            for j in range(nb[1]):
+                for i in range(nb[0]):
+                    shape = ref[(i, j, k)].codes.shape
+                    q = C.c_void_p()
+                    assert lib.vktHipAllocate(C.byref(q), int(np.prod(shape)) * 2) == 0
+                    ptrs.append(q.value)
+                    shapes.append(((i, j, k), shape))
+        arr = (C.c_void_p * len(ptrs))(*ptrs)
+        grid = L.HipBrickGrid_t(L.Vec3i_t(*nb), L.Vec3i_t(*brick), L.Vec3i_t(*neg), L.Vec3i_t(*pos))
+        assert lib.vktHipBrickDecomposeGrid(src, grid, arr) == 0, L.last_error()
+        assert lib.vktHipSynchronize() == 0
+        for q, (idx, shape) in zip(ptrs, shapes):
+            got = np.empty(shape, np.uint16)
+            assert lib.vktHipMemcpy(got.ctypes.data, C.c_void_p(q), got.nbytes, 2) == 0
+            np.testing.assert_array_equal(got, ref[idx].codes, err_msg=f"{brick} {neg} {pos} brick {idx}")
+        bad = list(ptrs)
+        bad[3] = None
+        assert lib.vktHipBrickDecomposeGrid(src, grid, (C.c_void_p * len(bad))(*bad)) != 0
+        bad[3] = src_ptr + 64
+        assert lib.vktHipBrickDecomposeGrid(src, grid, (C.c_void_p * len(bad))(*bad)) != 0
+        wrong = L.HipBrickGrid_t(L.Vec3i_t(nb[0] + 1, nb[1], nb[2]), L.Vec3i_t(*brick), L.Vec3i_t(*neg),
+                                 L.Vec3i_t(*pos))
+        assert lib.vktHipBrickDecomposeGrid(src, wrong, arr) != 0
+        for q in ptrs:
+            lib.vktHipFree(C.c_void_p(q))
+    lib.vktHipFree(C.c_void_p(src_ptr))

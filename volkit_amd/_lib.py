@@ -67,6 +67,10 @@ class HipBrickRange_t(C.Structure):
     _fields_ = [("brick", HipVolumeView_t), ("first", Vec3i_t), ("last", Vec3i_t)]
 
 
+class HipBrickGrid_t(C.Structure):
+    _fields_ = [("numBricks", Vec3i_t), ("brickSize", Vec3i_t), ("haloNeg", Vec3i_t), ("haloPos", Vec3i_t)]
+
+
 class HipSlabTransfer_t(C.Structure):
     _fields_ = [("peer", i32), ("z0", i32), ("z1", i32), ("send", i32)]
 
@@ -271,6 +275,7 @@ SIGNATURES = {
     "vktHipTransformRange2": (c_err, [HipVolumeView_t, HipVolumeView_t, Vec3i_t, Vec3i_t, Vec3i_t, BinaryOp]),
     "vktHipSynthesize": (c_err, [HipVolumeView_t, u64]),
     "vktHipBrickDecompose": (c_err, [HipVolumeView_t, P(HipBrickRange_t), i32]),
+    "vktHipBrickDecomposeGrid": (c_err, [HipVolumeView_t, HipBrickGrid_t, P(C.c_void_p)]),
     # Array3D.h (vktStructuredVolume instantiation) / Decompose.h
     "vktArray3D_vktStructuredVolume_CreateEmpty": (None, [P(c_arr)]),
     "vktArray3D_vktStructuredVolume_Create": (None, [P(c_arr), Vec3i_t]),

@@ -427,7 +427,7 @@ namespace hipk
         BrickDesc* dev = nullptr;
         uint8_t** hostPtr = nullptr;   // brick data pointers (uniform grids, BrickGrid::dst)
         uint8_t** devPtr = nullptr;
-        size_t cap = 0;
+        size_t capDesc = 0, capPtr = 0;
         hipEvent_t done = nullptr;
         hipEvent_t copied = nullptr;   // the table's upload (copy stream) finished
         bool pending = false;
@@ -530,6 +530,124 @@ namespace hipk
         }
     }
 
+    vktError prepareSlot(DescTable& st, size_t descs, size_t ptrs)
+    {
+        if (st.pending)
+        {
+            VKT_HIP_TRY(hipEventSynchronize(st.done));
+            st.pending = false;
+        }
+        if (st.capDesc < descs)
+        {
+            if (st.host)
+                VKT_HIP_TRY(hipHostFree(st.host));
+            if (st.dev)
+                VKT_HIP_TRY(hipFree(st.dev));
+            st.host = nullptr;
+            st.dev = nullptr;
+            st.capDesc = 0;
+            VKT_HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&st.host), descs * sizeof(BrickDesc)));
+            VKT_HIP_TRY(hipMalloc(reinterpret_cast<void**>(&st.dev), descs * sizeof(BrickDesc)));
+            st.capDesc = descs;
+        }
+        if (st.capPtr < ptrs)
+        {
+            if (st.hostPtr)
+                VKT_HIP_TRY(hipHostFree(st.hostPtr));
+            if (st.devPtr)
+                VKT_HIP_TRY(hipFree(st.devPtr));
+            st.hostPtr = nullptr;
+            st.devPtr = nullptr;
+            st.capPtr = 0;
+            VKT_HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&st.hostPtr), ptrs * sizeof(uint8_t*)));
+            VKT_HIP_TRY(hipMalloc(reinterpret_cast<void**>(&st.devPtr), ptrs * sizeof(uint8_t*)));
+            st.capPtr = ptrs;
+        }
+        if (!st.done)
+            VKT_HIP_TRY(hipEventCreateWithFlags(&st.done, hipEventDisableTiming));
+        if (!st.copied)
+            VKT_HIP_TRY(hipEventCreateWithFlags(&st.copied, hipEventDisableTiming));
+        return vktNoError;
+    }
+
+    // Upload the slot's table (descriptors, or the brick pointers of a uniform grid) on the copy
+    // stream and launch the copy of nFast bricks (groups of `run` bricks along x, chunks of up to
+    // maxItems 16-B items).  Caller holds the ring lock.
+    vktError launchBricks(DescRing& ring, DescTable& st, bool useGrid, BrickGrid grid, size_t nFast, size_t run,
+                          uint32_t maxItems, vktHipVolumeView_t const& source, uint32_t bpv)
+    {
+        hipStream_t s = rt::computeStream();
+        uint64_t const chunks = (maxItems + kBrickChunk - 1) / kBrickChunk;
+        uint64_t const blocks = chunks * nFast;
+        if (blocks >= (1ull << 32))
+            return rt::fail("BrickDecompose: too many bricks for one launch");
+        ring.next = (ring.next + 1) % kDescSlots;
+        BrickDesc* dev = st.dev;
+        // the table goes up on the copy stream, so it overlaps the previous call's kernel
+        // (262 144 descriptors of 16^3 bricks are 25 MB, 0.59 ms of PCIe; their data pointers
+        // 2 MB); the kernel waits for it.  The slot's previous kernel has finished (st.done
+        // above), so its buffers are free.
+        hipStream_t const cs = rt::copyStream();
+        if (useGrid)
+        {
+            VKT_HIP_TRY(hipMemcpyAsync(st.devPtr, st.hostPtr, nFast * sizeof(uint8_t*), hipMemcpyHostToDevice, cs));
+            grid.dst = st.devPtr;
+        }
+        else
+            VKT_HIP_TRY(hipMemcpyAsync(dev, st.host, nFast * sizeof(BrickDesc), hipMemcpyHostToDevice, cs));
+        VKT_HIP_TRY(hipEventRecord(st.copied, cs));
+        VKT_HIP_TRY(hipStreamWaitEvent(s, st.copied, 0));
+        FastDiv const fdc = makeFastDiv(static_cast<uint32_t>(chunks));
+        FastDiv const fdg = makeFastDiv(static_cast<uint32_t>(nFast % run == 0 ? run : 1));
+        unsigned const g = static_cast<unsigned>(blocks);
+        int32_t const alignedLds = static_cast<int32_t>(rt::knob(rt::Knob::DecomposeAlignedLds));
+        // words staged per thread: enough that a chunk's source words are all in flight at once
+        // (one memory latency per workgroup): a 16-KiB chunk of 32^3 bricks + halo 1 (68-B rows)
+        // reads ~1450 aligned words = 5.7 per thread.  In-process A/B (profiles/r03/decompose_ab.jsonl,
+        // back-to-back calls): 32^3 + halo 1.256 -> 1.211 ms with 6, 1.218 ms with 8; 64^3 + halo,
+        // 128^3 and 256^3 + halo unchanged within 1 %
+        int64_t const sw = rt::knob(rt::Knob::DecomposeStageWords);
+        // threads per workgroup (knob decompose.block): 128 gives each thread twice the items and
+        // staged words of a 256-thread workgroup over the same 16-KiB chunk
+        bool const half = rt::knob(rt::Knob::DecomposeBlock) == 128;
+        auto launch = [&](auto bpvC, auto swC) {
+            constexpr int B = decltype(bpvC)::value, W = decltype(swC)::value;
+            if (half)
+            {
+                if (useGrid)
+                    hipLaunchKernelGGL((brickCopyKernel<B, 2 * W, true, 128>), dim3(g), dim3(128), 0, s, dev, grid, fdc,
+                                       fdg, source.data, source.dimX, source.dimY, source.dimZ, alignedLds);
+                else
+                    hipLaunchKernelGGL((brickCopyKernel<B, 2 * W, false, 128>), dim3(g), dim3(128), 0, s, dev, grid, fdc,
+                                       fdg, source.data, source.dimX, source.dimY, source.dimZ, alignedLds);
+            }
+            else if (useGrid)
+                hipLaunchKernelGGL((brickCopyKernel<B, W, true>), dim3(g), dim3(kBlock), 0, s, dev, grid, fdc, fdg,
+                                   source.data, source.dimX, source.dimY, source.dimZ, alignedLds);
+            else
+                hipLaunchKernelGGL((brickCopyKernel<B, W, false>), dim3(g), dim3(kBlock), 0, s, dev, grid, fdc, fdg,
+                                   source.data, source.dimX, source.dimY, source.dimZ, alignedLds);
+        };
+        auto bySw = [&](auto bpvC) {
+            if (sw <= 5)
+                launch(bpvC, std::integral_constant<int, 5>{});
+            else if (sw == 6)
+                launch(bpvC, std::integral_constant<int, 6>{});
+            else
+                launch(bpvC, std::integral_constant<int, 8>{});
+        };
+        if (bpv == 1)
+            bySw(std::integral_constant<int, 1>{});
+        else if (bpv == 2)
+            bySw(std::integral_constant<int, 2>{});
+        else
+            bySw(std::integral_constant<int, 4>{});
+        VKT_HIP_TRY(hipGetLastError());
+        VKT_HIP_TRY(hipEventRecord(st.done, s));
+        st.pending = true;
+        return vktNoError;
+    }
+
 } // hipk
 } // vkt
 
@@ -558,37 +676,9 @@ vktError vktHipBrickDecompose(vktHipVolumeView_t source, vktHipBrickRange_t cons
     DescRing& ring = descRing();
     std::unique_lock<std::mutex> lock(ring.m);
     DescTable& st = ring.slot[ring.next];
-    if (st.pending)
-    {
-        VKT_HIP_TRY(hipEventSynchronize(st.done));
-        st.pending = false;
-    }
     size_t const need = static_cast<size_t>(numBricks);
-    if (st.cap < need)
-    {
-        if (st.host)
-            VKT_HIP_TRY(hipHostFree(st.host));
-        if (st.dev)
-            VKT_HIP_TRY(hipFree(st.dev));
-        if (st.hostPtr)
-            VKT_HIP_TRY(hipHostFree(st.hostPtr));
-        if (st.devPtr)
-            VKT_HIP_TRY(hipFree(st.devPtr));
-        st.host = nullptr;
-        st.dev = nullptr;
-        st.hostPtr = nullptr;
-        st.devPtr = nullptr;
-        st.cap = 0;
-        VKT_HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&st.host), need * sizeof(BrickDesc)));
-        VKT_HIP_TRY(hipMalloc(reinterpret_cast<void**>(&st.dev), need * sizeof(BrickDesc)));
-        VKT_HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&st.hostPtr), need * sizeof(uint8_t*)));
-        VKT_HIP_TRY(hipMalloc(reinterpret_cast<void**>(&st.devPtr), need * sizeof(uint8_t*)));
-        st.cap = need;
-    }
-    if (!st.done)
-        VKT_HIP_TRY(hipEventCreateWithFlags(&st.done, hipEventDisableTiming));
-    if (!st.copied)
-        VKT_HIP_TRY(hipEventCreateWithFlags(&st.copied, hipEventDisableTiming));
+    if (vktError const e = prepareSlot(st, need, need); e != vktNoError)
+        return e;
     BrickDesc* const fast = st.host;
     int64_t const V = 16 / bpv;                            // voxels per 16-B segment
     uint32_t const vShift = bpv == 1 ? 4u : bpv == 2 ? 3u : 2u;
@@ -750,15 +840,8 @@ vktError vktHipBrickDecompose(vktHipVolumeView_t source, vktHipBrickRange_t cons
         return rt::fail(errWhat);
     std::sort(slow.begin(), slow.end());
     size_t const nFast = maxItems > 0 ? static_cast<size_t>(numBricks) : 0;
-    hipStream_t s = rt::computeStream();
     if (nFast > 0)
     {
-        uint64_t const chunks = (maxItems + kBrickChunk - 1) / kBrickChunk;
-        uint64_t const blocks = chunks * nFast;
-        if (blocks >= (1ull << 32))
-            return rt::fail("vktHipBrickDecompose: too many bricks for one launch");
-        ring.next = (ring.next + 1) % kDescSlots;
-        BrickDesc* dev = st.dev;
         // group = the run of leading bricks with the same y/z box (one brick row of an
         // Array3D).  Any group size dividing the brick count maps blocks 1:1 onto (brick,
         // chunk); it only changes the order in which bricks are visited.
@@ -768,69 +851,9 @@ vktError vktHipBrickDecompose(vktHipVolumeView_t source, vktHipBrickRange_t cons
         bool const useGrid = slow.empty() && guess.ok && gridOk.load() && nFast == static_cast<size_t>(numBricks);
         if (useGrid)
             gridDivisors(guess, fast);
-        BrickGrid grid = guess.g;
-        // the table goes up on the copy stream, so it overlaps the previous call's kernel
-        // (262 144 descriptors of 16^3 bricks are 25 MB, 0.59 ms of PCIe; their data pointers
-        // 2 MB); the kernel waits for it.  The slot's previous kernel has finished (st.done
-        // above), so its buffers are free.
-        hipStream_t const cs = rt::copyStream();
-        if (useGrid)
-        {
-            VKT_HIP_TRY(hipMemcpyAsync(st.devPtr, st.hostPtr, nFast * sizeof(uint8_t*), hipMemcpyHostToDevice, cs));
-            grid.dst = st.devPtr;
-        }
-        else
-            VKT_HIP_TRY(hipMemcpyAsync(dev, st.host, nFast * sizeof(BrickDesc), hipMemcpyHostToDevice, cs));
-        VKT_HIP_TRY(hipEventRecord(st.copied, cs));
-        VKT_HIP_TRY(hipStreamWaitEvent(s, st.copied, 0));
-        FastDiv const fdc = makeFastDiv(static_cast<uint32_t>(chunks));
-        FastDiv const fdg = makeFastDiv(static_cast<uint32_t>(nFast % run == 0 ? run : 1));
-        unsigned const g = static_cast<unsigned>(blocks);
-        int32_t const alignedLds = static_cast<int32_t>(rt::knob(rt::Knob::DecomposeAlignedLds));
-        // words staged per thread: enough that a chunk's source words are all in flight at once
-        // (one memory latency per workgroup): a 16-KiB chunk of 32^3 bricks + halo 1 (68-B rows)
-        // reads ~1450 aligned words = 5.7 per thread.  In-process A/B (profiles/r03/decompose_ab.jsonl,
-        // back-to-back calls): 32^3 + halo 1.256 -> 1.211 ms with 6, 1.218 ms with 8; 64^3 + halo,
-        // 128^3 and 256^3 + halo unchanged within 1 %
-        int64_t const sw = rt::knob(rt::Knob::DecomposeStageWords);
-        // threads per workgroup (knob decompose.block): 128 gives each thread twice the items and
-        // staged words of a 256-thread workgroup over the same 16-KiB chunk
-        bool const half = rt::knob(rt::Knob::DecomposeBlock) == 128;
-        auto launch = [&](auto bpvC, auto swC) {
-            constexpr int B = decltype(bpvC)::value, W = decltype(swC)::value;
-            if (half)
-            {
-                if (useGrid)
-                    hipLaunchKernelGGL((brickCopyKernel<B, 2 * W, true, 128>), dim3(g), dim3(128), 0, s, dev, grid, fdc,
-                                       fdg, source.data, source.dimX, source.dimY, source.dimZ, alignedLds);
-                else
-                    hipLaunchKernelGGL((brickCopyKernel<B, 2 * W, false, 128>), dim3(g), dim3(128), 0, s, dev, grid, fdc,
-                                       fdg, source.data, source.dimX, source.dimY, source.dimZ, alignedLds);
-            }
-            else if (useGrid)
-                hipLaunchKernelGGL((brickCopyKernel<B, W, true>), dim3(g), dim3(kBlock), 0, s, dev, grid, fdc, fdg,
-                                   source.data, source.dimX, source.dimY, source.dimZ, alignedLds);
-            else
-                hipLaunchKernelGGL((brickCopyKernel<B, W, false>), dim3(g), dim3(kBlock), 0, s, dev, grid, fdc, fdg,
-                                   source.data, source.dimX, source.dimY, source.dimZ, alignedLds);
-        };
-        auto bySw = [&](auto bpvC) {
-            if (sw <= 5)
-                launch(bpvC, std::integral_constant<int, 5>{});
-            else if (sw == 6)
-                launch(bpvC, std::integral_constant<int, 6>{});
-            else
-                launch(bpvC, std::integral_constant<int, 8>{});
-        };
-        if (bpv == 1)
-            bySw(std::integral_constant<int, 1>{});
-        else if (bpv == 2)
-            bySw(std::integral_constant<int, 2>{});
-        else
-            bySw(std::integral_constant<int, 4>{});
-        VKT_HIP_TRY(hipGetLastError());
-        VKT_HIP_TRY(hipEventRecord(st.done, s));
-        st.pending = true;
+        if (vktError const e = launchBricks(ring, st, useGrid, guess.g, nFast, run, maxItems, source, bpv);
+            e != vktNoError)
+            return e;
     }
     lock.unlock();
     // bricks that need the unmap -> map conversion: one CopyRange each
@@ -841,6 +864,134 @@ vktError vktHipBrickDecompose(vktHipVolumeView_t source, vktHipBrickRange_t cons
         if (e != vktNoError)
             return e;
     }
+    return rt::finishLaunch("BrickDecompose_hip");
+}
+
+vktError vktHipBrickDecomposeGrid(vktHipVolumeView_t source, vktHipBrickGrid_t grid, uint8_t* const* brickData)
+{
+    if (!validView(source) || source.dimX <= 0 || source.dimY <= 0 || source.dimZ <= 0)
+        return rt::fail("vktHipBrickDecomposeGrid: invalid source view");
+    uint32_t const bpv = codec::bytesPerVoxel(source.dataFormat);
+    if (bpv != 1 && bpv != 2 && bpv != 4)
+        return rt::fail("vktHipBrickDecomposeGrid: unsupported data format");
+    int32_t const sd[3] = {source.dimX, source.dimY, source.dimZ};
+    int32_t const nb[3] = {grid.numBricks.x, grid.numBricks.y, grid.numBricks.z};
+    int32_t const bs[3] = {grid.brickSize.x, grid.brickSize.y, grid.brickSize.z};
+    int32_t const hn[3] = {grid.haloNeg.x, grid.haloNeg.y, grid.haloNeg.z};
+    int32_t const hp[3] = {grid.haloPos.x, grid.haloPos.y, grid.haloPos.z};
+    // box extent per axis and class (0 first brick, 1 interior, 2 last -- gridClass; a single
+    // brick is class 2), and the x of the representative brick of each class
+    int32_t ext[3][3], fxc[3];
+    for (int a = 0; a < 3; ++a)
+    {
+        if (bs[a] <= 0 || hn[a] < 0 || hp[a] < 0 || nb[a] != (sd[a] + bs[a] - 1) / bs[a])
+            return rt::fail("vktHipBrickDecomposeGrid: grid does not match the source (numBricks = ceil(dims / "
+                            "brickSize), halos >= 0)");
+        int32_t const border = sd[a] - (nb[a] - 1) * bs[a];
+        ext[a][0] = hn[a] + (nb[a] > 1 ? bs[a] : border) + hp[a];
+        ext[a][1] = hn[a] + bs[a] + hp[a];
+        ext[a][2] = hn[a] + border + hp[a];
+    }
+    if (brickData == nullptr)
+        return rt::fail("vktHipBrickDecomposeGrid: null brick pointer list");
+    size_t const n = static_cast<size_t>(nb[0]) * static_cast<size_t>(nb[1]) * static_cast<size_t>(nb[2]);
+    if (n >= (1ull << 31))
+        return rt::fail("vktHipBrickDecomposeGrid: too many bricks");
+    fxc[0] = -hn[0];
+    fxc[1] = bs[0] - hn[0];
+    fxc[2] = (nb[0] - 1) * bs[0] - hn[0];
+    int32_t const V = 16 / static_cast<int32_t>(bpv);
+    int64_t const maxVox = static_cast<int64_t>(std::max({ext[0][0], ext[0][1], ext[0][2]})) *
+                           std::max({ext[1][0], ext[1][1], ext[1][2]}) * std::max({ext[2][0], ext[2][1], ext[2][2]});
+    // what the index-derived (grid) kernel needs: linear bricks (rows of >= 16 B, 16-B aligned
+    // source), interior bricks along x never clamped (one source span per class), boxes < 2^31
+    bool ok = source.dimX >= V && reinterpret_cast<uintptr_t>(source.data) % 16 == 0 && maxVox < (1ll << 31) &&
+              rt::knob(rt::Knob::DecomposeGrid) != 0;
+    for (int c = 0; c < 3; ++c)
+        ok = ok && ext[0][c] >= V;
+    if (nb[0] > 2)
+        ok = ok && fxc[1] >= 0 && (nb[0] - 2) * bs[0] - hn[0] + ext[0][1] <= sd[0];
+    auto boxOf = [&](size_t i, vktHipBrickRange_t& r) {
+        int32_t const ix = static_cast<int32_t>(i % static_cast<size_t>(nb[0]));
+        int32_t const iy = static_cast<int32_t>((i / static_cast<size_t>(nb[0])) % static_cast<size_t>(nb[1]));
+        int32_t const iz = static_cast<int32_t>(i / (static_cast<size_t>(nb[0]) * static_cast<size_t>(nb[1])));
+        int32_t const c[3] = {ix * bs[0], iy * bs[1], iz * bs[2]};
+        r.first = {c[0] - hn[0], c[1] - hn[1], c[2] - hn[2]};
+        r.last = {std::min(c[0] + bs[0], sd[0]) + hp[0], std::min(c[1] + bs[1], sd[1]) + hp[1],
+                  std::min(c[2] + bs[2], sd[2]) + hp[2]};
+        r.brick = source;
+        r.brick.data = brickData[i];
+        r.brick.dimX = r.last.x - r.first.x;
+        r.brick.dimY = r.last.y - r.first.y;
+        r.brick.dimZ = r.last.z - r.first.z;
+    };
+    if (!ok)
+    {
+        // the general path on the equivalent range list
+        thread_local std::vector<vktHipBrickRange_t> ranges;
+        ranges.resize(n);
+        rt::parallelFor(n, 4096, [&](size_t b, size_t e) {
+            for (size_t i = b; i < e; ++i)
+                boxOf(i, ranges[i]);
+        });
+        return vktHipBrickDecompose(source, ranges.data(), static_cast<int32_t>(n));
+    }
+    DescRing& ring = descRing();
+    std::unique_lock<std::mutex> lock(ring.m);
+    DescTable& st = ring.slot[ring.next];
+    if (vktError const e = prepareSlot(st, 0, n); e != vktNoError)
+        return e;
+    // the pointers into the pinned table; each checked: non-null, not inside the source
+    uint8_t const* const s0 = source.data;
+    uint8_t const* const s1 = s0 + static_cast<uint64_t>(sd[0]) * sd[1] * sd[2] * bpv;
+    std::atomic<int64_t> bad{-1};
+    uint8_t** const ptrs = st.hostPtr;
+    rt::parallelFor(n, 8192, [&](size_t b, size_t e) {
+        auto cls = [](size_t k, int32_t nbk) { return k == static_cast<size_t>(nbk - 1) ? 2 : (k == 0 ? 0 : 1); };
+        for (size_t i = b; i < e; ++i)
+        {
+            uint8_t* const p = brickData[i];
+            ptrs[i] = p;
+            size_t const ix = i % static_cast<size_t>(nb[0]), yz = i / static_cast<size_t>(nb[0]);
+            size_t const iy = yz % static_cast<size_t>(nb[1]), iz = yz / static_cast<size_t>(nb[1]);
+            uint64_t const bytes = static_cast<uint64_t>(ext[0][cls(ix, nb[0])]) * ext[1][cls(iy, nb[1])] *
+                                   ext[2][cls(iz, nb[2])] * bpv;
+            if (p == nullptr || (p < s1 && p + bytes > s0))
+            {
+                int64_t expect = -1;
+                bad.compare_exchange_strong(expect, static_cast<int64_t>(i));
+            }
+        }
+    });
+    if (bad.load() >= 0)
+        return rt::fail("vktHipBrickDecomposeGrid: a brick pointer is null or inside the source");
+    BrickGrid g{};
+    g.nbx = nb[0];
+    g.nby = nb[1];
+    g.nbz = nb[2];
+    g.fnbx = makeFastDiv(static_cast<uint32_t>(nb[0]));
+    g.fnby = makeFastDiv(static_cast<uint32_t>(nb[1]));
+    g.fx0 = -hn[0];
+    g.fy0 = -hn[1];
+    g.fz0 = -hn[2];
+    g.bx = nb[0] > 1 ? bs[0] : 0;
+    g.by = nb[1] > 1 ? bs[1] : 0;
+    g.bz = nb[2] > 1 ? bs[2] : 0;
+    for (int c = 0; c < 3; ++c)
+    {
+        g.nx[c] = ext[0][c];
+        g.ny[c] = ext[1][c];
+        g.nz[c] = ext[2][c];
+        g.fdx[c] = makeFastDiv(static_cast<uint32_t>(ext[0][c]));
+        g.fdy[c] = makeFastDiv(static_cast<uint32_t>(ext[1][c]));
+        int64_t const span = std::min<int64_t>(fxc[c] + ext[0][c], sd[0]) - std::max<int32_t>(fxc[c], 0);
+        g.fwpr[c] = makeFastDiv(span > 0 ? static_cast<uint32_t>((span * bpv + 15) / 16 + 1) : 1u);
+    }
+    uint32_t const maxItems = static_cast<uint32_t>((maxVox + V - 1) / V);
+    if (vktError const e = launchBricks(ring, st, true, g, n, static_cast<size_t>(nb[0]), maxItems, source, bpv);
+        e != vktNoError)
+        return e;
+    lock.unlock();
     return rt::finishLaunch("BrickDecompose_hip");
 }
 
