@@ -366,3 +366,22 @@ def test_grid_entry_point_parity_and_validation():
         for q in ptrs:
             lib.vktHipFree(C.c_void_p(q))
     lib.vktHipFree(C.c_void_p(src_ptr))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fmt", [4, 5, 7])
+@pytest.mark.parametrize("dims,brick,neg,pos", LAYOUTS)
+def test_brick_decompose_staged_grid_kernel(fmt, dims, brick, neg, pos):
+    """Knob decompose.gather = 0: uniform grids keep the staged kernel (source words scattered
+    into the brick layout in LDS) instead of the gather kernel (the default, tested above)."""
+    rng = np.random.default_rng(fmt * 100 + sum(dims) + 11)
+    codes = rand_codes(rng, fmt, dims[::-1])
+    assert lib.vktHipSetTuningKnob(b"decompose.gather", 0) == 0
+    try:
+        err, got = gpu_decompose(codes, fmt, (0.0, 1.0), brick, neg, pos)
+    finally:
+        assert lib.vktHipSetTuningKnob(b"decompose.gather", -1) == 0
+    assert err == vkt.NoError, vkt.last_error()
+    ref = ob.brick_decompose(ob.Volume(codes, fmt), brick, neg, pos)
+    for idx, v in ref.items():
+        np.testing.assert_array_equal(got[idx], v.codes, err_msg=f"brick {idx}")

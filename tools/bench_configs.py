@@ -615,7 +615,7 @@ def main():
             vox = sum(arr[(i, j, k)].getSizeInBytes() // 2 for k in range(arr.dims().z)
                       for j in range(arr.dims().y) for i in range(arr.dims().x))
             for rnd in range(3):
-                for kv in ((0, 5), (1, 5), (0, 6), (1, 6), (0, 8)):   # (aligned_lds, stage_words)
+                for kv in ((0, 5), (1, 5), (0, 6), (1, 6), (2, 6), (0, 8)):   # (aligned_lds, stage_words)
                     lib.vktHipSetTuningKnob(b"decompose.aligned_lds", kv[0])
                     lib.vktHipSetTuningKnob(b"decompose.stage_words", kv[1])
                     ab.setdefault((bs, halo, kv, vox), []).append(
@@ -926,6 +926,59 @@ def main():
                            timed(lambda: lib.vktHipAggregatesRange(V, a0, a1, C.byref(agg)), R), bpv * nv, nv)
             lib.vktHipSetTuningKnob(b"aggregates.moments", -1)
             free(V)
+    if want("dec16"):
+        # BrickDecompose of 1024^3 UInt16 into small bricks, one call per case (PMC passes)
+        import volkit_amd.volkit as vkt
+        ep = vkt.GetThreadExecutionPolicy()
+        ep.device = vkt.ExecutionPolicy.Device_GPU
+        vkt.SetThreadExecutionPolicy(ep)
+        n = 1024
+        V = vkt.StructuredVolume(n, n, n, vkt.DataFormat_UInt16)
+        vkt.Synthesize(V, 77)
+        for bs, halo in ((16, (1, 1, 1)), (16, (0, 0, 0)), (32, (1, 1, 1))):
+            arr = vkt.Array3D_StructuredVolume()
+            b3, h3 = vkt.Vec3i(bs, bs, bs), vkt.Vec3i(*halo)
+            vkt.BrickDecomposeResize(arr, V, b3, h3, h3)
+            vox = (n // bs) ** 3 * (bs + halo[0] + halo[0]) ** 3
+            report(f"dec16 BrickDecompose 1024^3 UInt16 -> {bs}^3 bricks halo {halo}",
+                   timed(lambda: vkt.BrickDecompose(arr, V, b3, h3, h3), R), 4 * vox, vox)
+            del arr
+        del V
+        ep.device = vkt.ExecutionPolicy.Device_CPU
+        vkt.SetThreadExecutionPolicy(ep)
+    if want("decpipe"):
+        # in-process A/B of the uniform-grid copy kernels (knob decompose.pipe: 1 resident grid
+        # loading chunk k + 1 while storing chunk k, 0 one workgroup per chunk; the gather form,
+        # knob decompose.gather, measured no faster: profiles/r04/decgather.jsonl)
+        import volkit_amd.volkit as vkt
+        ep = vkt.GetThreadExecutionPolicy()
+        ep.device = vkt.ExecutionPolicy.Device_GPU
+        vkt.SetThreadExecutionPolicy(ep)
+        n = 1024
+        V = vkt.StructuredVolume(n, n, n, vkt.DataFormat_UInt16)
+        vkt.Synthesize(V, 77)
+        ab = {}
+        for bs, halo in ((16, (1, 1, 1)), (16, (0, 0, 0)), (32, (1, 1, 1)), (64, (1, 1, 1)), (256, (1, 1, 1))):
+            arr = vkt.Array3D_StructuredVolume()
+            b3, h3 = vkt.Vec3i(bs, bs, bs), vkt.Vec3i(*halo)
+            vkt.BrickDecomposeResize(arr, V, b3, h3, h3)
+            vox = (n // bs) ** 3 * (bs + 2 * halo[0]) ** 3
+            for rnd in range(3):
+                for kv in (1, 0):
+                    lib.vktHipSetTuningKnob(b"decompose.pipe", kv)
+                    ab.setdefault((bs, halo, kv, vox, "back-to-back"), []).append(
+                        pipelined(lambda: vkt.BrickDecompose(arr, V, b3, h3, h3), R))
+                    ab.setdefault((bs, halo, kv, vox, "incl. host planning"), []).append(
+                        timed(lambda: vkt.BrickDecompose(arr, V, b3, h3, h3), R))
+            del arr
+        lib.vktHipSetTuningKnob(b"decompose.pipe", -1)
+        for (bs, halo, kv, vox, how), ts in sorted(ab.items()):
+            ts.sort()
+            report(f"decpipe BrickDecompose 1024^3 UInt16 -> {bs}^3 bricks halo {halo} pipe={kv} ({how}; median of "
+                   f"3 rounds, spread {ts[0]:.4f}-{ts[-1]:.4f})", ts[1], 4 * vox, vox)
+        del V
+        ep.device = vkt.ExecutionPolicy.Device_CPU
+        vkt.SetThreadExecutionPolicy(ep)
     if want("decbatch"):
         # in-process A/B of BrickDecompose's batched planning (knob decompose.batch: 1 up to 8
         # batches of brick planes, planning batch k + 1 while the GPU copies batch k; 0 one batch)

@@ -414,6 +414,417 @@ namespace hipk
         }
     }
 
+    // ---- Persistent, software-pipelined staged copy of a uniform grid (knob decompose.pipe) ----
+    // The staged kernel above runs one workgroup per 16-KiB chunk: a small brick (16^3 + halo 1 =
+    // 11.7 KB) is one short-lived workgroup whose loads, LDS pass and stores run back to back, so
+    // the chip holds few bytes in flight (measured 4.2 TB/s of HBM traffic for 16^3 + halo).
+    // Here a grid of resident workgroups walks the chunks (item = blockIdx + k * gridDim, the same
+    // (brick row, chunk, brick) order and XCD grouping), with two LDS tiles: the source words of
+    // chunk k + 1 are loaded while chunk k is stored from the other tile.
+    template <int BPV, int W, int NT>
+    __global__ __launch_bounds__(NT) void brickPipeKernel(BrickGrid grid, FastDiv chunksPerBrick, FastDiv groupSize,
+                                                          uint32_t items, uint8_t const* src, int32_t sdx, int32_t sdy,
+                                                          int32_t sdz, int32_t alignedLds)
+    {
+        constexpr int32_t V = 16 / BPV;
+        __shared__ u32x4 tile[2][kBrickChunk];   // 32 KiB
+        uint64_t const spY = static_cast<uint64_t>(sdx), spZ = spY * static_cast<uint64_t>(sdy);
+        uint64_t const srcBytes = spZ * static_cast<uint64_t>(sdz) * BPV;
+        struct Geom
+        {
+            uint8_t* dst;
+            int32_t fx, fy, fz, nx, vStart, chunkVox, rA, nRows, lo, hi;
+            uint32_t wpr, total;
+            FastDiv fdx, fwpr, fdy;
+            bool live;
+        };
+        auto geom = [&](uint32_t item) -> Geom {
+            Geom g{};
+            uint32_t const lb = xcdSwizzle(item, items);
+            uint32_t const rest = fdiv(lb, groupSize);
+            uint32_t const ig = lb - rest * groupSize.d;
+            uint32_t const grp = fdiv(rest, chunksPerBrick);
+            uint32_t const chunk = __builtin_amdgcn_readfirstlane(rest - grp * chunksPerBrick.d);
+            uint32_t const b = __builtin_amdgcn_readfirstlane(grp * groupSize.d + ig);
+            uint32_t const yz = fdiv(b, grid.fnbx);
+            int32_t const ix = static_cast<int32_t>(b - yz * grid.fnbx.d);
+            uint32_t const izu = fdiv(yz, grid.fnby);
+            int32_t const iy = static_cast<int32_t>(yz - izu * grid.fnby.d), iz = static_cast<int32_t>(izu);
+            int const cx = gridClass(ix, grid.nbx), cy = gridClass(iy, grid.nby), cz = gridClass(iz, grid.nbz);
+            g.fx = grid.fx0 + ix * grid.bx;
+            g.fy = grid.fy0 + iy * grid.by;
+            g.fz = grid.fz0 + iz * grid.bz;
+            g.nx = pick3(grid.nx, cx);
+            int32_t const nvox = g.nx * pick3(grid.ny, cy) * pick3(grid.nz, cz);
+            g.fdx = pick3(grid.fdx, cx);
+            g.fwpr = pick3(grid.fwpr, cx);
+            g.fdy = pick3(grid.fdy, cy);
+            uint32_t const base = chunk * kBrickChunk;
+            g.live = base < static_cast<uint32_t>((nvox + V - 1) / V);
+            if (!g.live)
+                return g;
+            g.dst = grid.dst[b];
+            g.vStart = static_cast<int32_t>(base) * V;
+            int32_t const vEnd = min(g.vStart + static_cast<int32_t>(kBrickChunk) * V, nvox);
+            g.chunkVox = vEnd - g.vStart;
+            g.rA = static_cast<int32_t>(fdiv(static_cast<uint32_t>(g.vStart), g.fdx));
+            g.nRows = static_cast<int32_t>(fdiv(static_cast<uint32_t>(vEnd - 1), g.fdx)) - g.rA + 1;
+            g.lo = max(g.fx, 0);
+            g.hi = min(g.fx + g.nx, sdx);
+            g.wpr = g.fwpr.d;
+            g.total = static_cast<uint32_t>(g.nRows) * g.wpr;
+            return g;
+        };
+        auto rowBase = [&](Geom const& g, int32_t r) -> uint64_t {
+            uint32_t const z = fdiv(static_cast<uint32_t>(r), g.fdy);
+            uint32_t const y = static_cast<uint32_t>(r) - z * g.fdy.d;
+            return static_cast<uint64_t>(clampi(g.fz + static_cast<int32_t>(z), sdz - 1)) * spZ +
+                   static_cast<uint64_t>(clampi(g.fy + static_cast<int32_t>(y), sdy - 1)) * spY;
+        };
+        struct Word
+        {
+            uint64_t rb;
+            int32_t x0, li;
+            bool live, whole;
+            u32x4 v;
+        };
+        auto locate = [&](Geom const& g, uint32_t t, Word& w) {
+            w.live = t < g.total;
+            uint32_t const tt = w.live ? t : 0u;
+            uint32_t const q = fdiv(tt, g.fwpr);
+            int32_t const r = g.rA + static_cast<int32_t>(q);
+            w.rb = rowBase(g, r);
+            uint64_t const startByte =
+                (((w.rb + static_cast<uint64_t>(g.lo)) * BPV) & ~uint64_t(15)) + 16ull * (tt - q * g.wpr);
+            w.live = w.live && startByte < (w.rb + static_cast<uint64_t>(g.hi)) * BPV;
+            w.x0 = static_cast<int32_t>(startByte / BPV - w.rb);
+            w.li = r * g.nx + (w.x0 - g.fx) - g.vStart;
+            w.whole = startByte + 16 <= srcBytes;
+            w.v = u32x4{0u, 0u, 0u, 0u};
+            if (w.live && w.whole)
+                w.v = *reinterpret_cast<u32x4 const*>(src + startByte);
+        };
+        auto place = [&](Geom const& g, uint8_t* lds, Word const& w) {
+            if (!w.live)
+                return;
+            if (w.whole && w.x0 >= g.lo && w.x0 + V <= g.hi && w.li >= 0 && w.li + V <= g.chunkVox)
+            {
+                if (alignedLds >= 2)
+                    ldsStoreRange(lds, w.li * BPV, w.v, 0, 16);
+                else
+                    reinterpret_cast<Unaligned16*>(lds + w.li * BPV)->v = w.v;
+            }
+            else if (w.whole && alignedLds >= 1)
+            {
+                int32_t const k0 = max(max(g.lo - w.x0, -w.li), 0);
+                int32_t const k1 = min(min(g.hi - w.x0, g.chunkVox - w.li), V);
+                if (k1 > k0)
+                    ldsStoreRange(lds, (w.li + k0) * BPV, w.v, k0 * BPV, k1 * BPV);
+            }
+            else
+            {
+#pragma unroll
+                for (int k = 0; k < V; ++k)
+                    if (w.x0 + k >= g.lo && w.x0 + k < g.hi && w.li + k >= 0 && w.li + k < g.chunkVox)
+                        ldsStoreCode<BPV>(lds, w.li + k,
+                                          w.whole ? wordCode<BPV>(w.v, k) : loadCode<BPV>(src, w.rb + w.x0 + k));
+            }
+        };
+        // the words beyond the first W rounds, then the clamped x halo voxels (border bricks)
+        auto stageRest = [&](Geom const& g, uint8_t* lds) {
+            for (uint32_t t = threadIdx.x + W * NT; t < g.total; t += NT)
+            {
+                Word w;
+                locate(g, t, w);
+                place(g, lds, w);
+            }
+            if (g.fx < 0 || g.fx + g.nx > sdx)
+            {
+                for (int32_t q = threadIdx.x; q < g.nRows; q += NT)
+                {
+                    int32_t const r = g.rA + q;
+                    uint64_t const rb = rowBase(g, r);
+                    int32_t const rowL = r * g.nx - g.fx - g.vStart;
+                    if (g.fx < 0)
+                    {
+                        uint32_t const c = loadCode<BPV>(src, rb);
+                        for (int32_t x = g.fx; x < min(0, g.fx + g.nx); ++x)
+                            if (rowL + x >= 0 && rowL + x < g.chunkVox)
+                                ldsStoreCode<BPV>(lds, rowL + x, c);
+                    }
+                    if (g.fx + g.nx > sdx)
+                    {
+                        uint32_t const c = loadCode<BPV>(src, rb + static_cast<uint64_t>(sdx - 1));
+                        for (int32_t x = max(sdx, g.fx); x < g.fx + g.nx; ++x)
+                            if (rowL + x >= 0 && rowL + x < g.chunkVox)
+                                ldsStoreCode<BPV>(lds, rowL + x, c);
+                    }
+                }
+            }
+        };
+        auto storeOut = [&](Geom const& g, u32x4 const* t, uint8_t const* lds) {
+#pragma unroll
+            for (int u = 0; u < static_cast<int>(kBrickChunk) / NT; ++u)
+            {
+                int32_t const it = u * NT + static_cast<int32_t>(threadIdx.x);
+                int32_t const lv = it * V;
+                uint8_t* const out = g.dst + static_cast<uint64_t>(g.vStart + lv) * BPV;
+                if (lv + V <= g.chunkVox)
+                    __builtin_nontemporal_store(t[it], (__attribute__((address_space(1))) u32x4*)(out));
+                else
+                {
+                    for (int32_t k = 0; k < V && lv + k < g.chunkVox; ++k)
+                        storeCode<BPV>(out, k, loadCode<BPV>(lds, lv + k));
+                }
+            }
+        };
+        uint32_t item = blockIdx.x;
+        if (item >= items)
+            return;   // (whole workgroup)
+        Geom cur = geom(item);
+        Word words[W];
+        int p = 0;
+        if (cur.live)
+        {
+#pragma unroll
+            for (int k = 0; k < W; ++k)
+                locate(cur, threadIdx.x + k * NT, words[k]);
+#pragma unroll
+            for (int k = 0; k < W; ++k)
+                place(cur, reinterpret_cast<uint8_t*>(tile[0]), words[k]);
+            stageRest(cur, reinterpret_cast<uint8_t*>(tile[0]));
+        }
+        __syncthreads();
+        while (true)   // item and every branch below are workgroup-uniform
+        {
+            uint32_t const nitem = item + gridDim.x;
+            bool const more = nitem < items;
+            Geom nxt{};
+            if (more)
+            {
+                nxt = geom(nitem);
+                if (nxt.live)
+                {
+#pragma unroll
+                    for (int k = 0; k < W; ++k)
+                        locate(nxt, threadIdx.x + k * NT, words[k]);
+                }
+            }
+            if (cur.live)
+                storeOut(cur, tile[p], reinterpret_cast<uint8_t const*>(tile[p]));
+            if (!more)
+                break;
+            if (nxt.live)
+            {
+                uint8_t* const lds = reinterpret_cast<uint8_t*>(tile[p ^ 1]);
+#pragma unroll
+                for (int k = 0; k < W; ++k)
+                    place(nxt, lds, words[k]);
+                stageRest(nxt, lds);
+            }
+            __syncthreads();   // tile[p ^ 1] complete, and every wave is done reading tile[p]
+            cur = nxt;
+            p ^= 1;
+            item = nitem;
+        }
+    }
+
+    // ---- Gather form of the uniform-grid copy (knob decompose.gather) ------------------------
+    // Phase 1 stages the source rows a chunk touches in LDS as ALIGNED 16-B words -- row q of the
+    // chunk at q * P bytes, P = the class's source words per row * 16 -- with aligned LDS writes
+    // only; phase 2 assembles each 16-B output item with one unaligned ds_read_b128 from its row,
+    // or two merged by a byte mask for an item that crosses a brick row end; only items with
+    // clamped (x halo) voxels and a brick's last partial item go voxel by voxel.  The staged form
+    // above scatters source words into the brick layout, the words cut by a row end voxel by
+    // voxel: for 16^3 bricks + halo 1 (36-B rows: 2 of 4 words partial) that took ~550 VALU + ~560
+    // SALU instructions per wave (profiles/r04/dec16.pmc.jsonl).  LDS: dynamic, (rows a chunk
+    // touches) x P, sized on the host per launch.
+    __device__ __forceinline__ u32x4 ldsRead16(uint8_t const* lds, uint32_t a)
+    {
+        return reinterpret_cast<Unaligned16 const*>(lds + a)->v;
+    }
+
+    // bytes [0, cb) from a, the rest from b (0 < cb < 16)
+    __device__ __forceinline__ u32x4 mergeBytes(u32x4 a, u32x4 b, int32_t cb)
+    {
+        auto m = [&](int i) -> uint32_t {
+            int32_t const n = min(max(cb - 4 * i, 0), 4);
+            return n >= 4 ? ~0u : (1u << (8 * n)) - 1u;
+        };
+        uint32_t const m0 = m(0), m1 = m(1), m2 = m(2), m3 = m(3);
+        return u32x4{(a.x & m0) | (b.x & ~m0), (a.y & m1) | (b.y & ~m1), (a.z & m2) | (b.z & ~m2),
+                     (a.w & m3) | (b.w & ~m3)};
+    }
+
+    template <int BPV, int kStageWords, int NT>
+    __global__ __launch_bounds__(NT) void brickGatherKernel(BrickGrid grid, FastDiv chunksPerBrick, FastDiv groupSize,
+                                                            uint8_t const* src, int32_t sdx, int32_t sdy, int32_t sdz)
+    {
+        constexpr int32_t V = 16 / BPV;
+        extern __shared__ u32x4 stage[];
+        uint8_t* const lds = reinterpret_cast<uint8_t*>(stage);
+        uint32_t const lb = xcdSwizzle(blockIdx.x, gridDim.x);
+        uint32_t const rest = fdiv(lb, groupSize);
+        uint32_t const ig = lb - rest * groupSize.d;
+        uint32_t const grp = fdiv(rest, chunksPerBrick);
+        uint32_t const chunk = __builtin_amdgcn_readfirstlane(rest - grp * chunksPerBrick.d);
+        uint32_t const b = __builtin_amdgcn_readfirstlane(grp * groupSize.d + ig);
+        uint32_t const yz = fdiv(b, grid.fnbx);
+        int32_t const ix = static_cast<int32_t>(b - yz * grid.fnbx.d);
+        uint32_t const izu = fdiv(yz, grid.fnby);
+        int32_t const iy = static_cast<int32_t>(yz - izu * grid.fnby.d), iz = static_cast<int32_t>(izu);
+        int const cx = gridClass(ix, grid.nbx), cy = gridClass(iy, grid.nby), cz = gridClass(iz, grid.nbz);
+        int32_t const fx = grid.fx0 + ix * grid.bx, fy = grid.fy0 + iy * grid.by, fz = grid.fz0 + iz * grid.bz;
+        int32_t const nx = pick3(grid.nx, cx), ny = pick3(grid.ny, cy), nz = pick3(grid.nz, cz);
+        FastDiv const fdx = pick3(grid.fdx, cx), fwpr = pick3(grid.fwpr, cx), fdy = pick3(grid.fdy, cy);
+        int32_t const nvox = nx * ny * nz;
+        uint32_t const base = chunk * kBrickChunk;
+        if (base >= static_cast<uint32_t>((nvox + V - 1) / V))
+            return;   // border bricks are smaller than the largest one
+        uint8_t* const dst = grid.dst[b];
+        uint64_t const spY = static_cast<uint64_t>(sdx), spZ = spY * static_cast<uint64_t>(sdy);
+        uint64_t const srcBytes = spZ * static_cast<uint64_t>(sdz) * BPV;
+        int32_t const vStart = static_cast<int32_t>(base) * V;
+        int32_t const vEnd = min(vStart + static_cast<int32_t>(kBrickChunk) * V, nvox);
+        int32_t const chunkVox = vEnd - vStart;
+        int32_t const rA = static_cast<int32_t>(fdiv(static_cast<uint32_t>(vStart), fdx));
+        int32_t const rB = static_cast<int32_t>(fdiv(static_cast<uint32_t>(vEnd - 1), fdx));
+        int32_t const nRows = rB - rA + 1;
+        int32_t const lo = max(fx, 0), hi = min(fx + nx, sdx);   // in-volume x span of a row
+        uint32_t const wpr = fwpr.d, P = wpr * 16u;
+        auto rowBase = [&](int32_t r) -> uint64_t {   // source voxel index of x = 0 of brick row r
+            uint32_t const z = fdiv(static_cast<uint32_t>(r), fdy);
+            uint32_t const y = static_cast<uint32_t>(r) - z * fdy.d;
+            return static_cast<uint64_t>(clampi(fz + static_cast<int32_t>(z), sdz - 1)) * spZ +
+                   static_cast<uint64_t>(clampi(fy + static_cast<int32_t>(y), sdy - 1)) * spY;
+        };
+        // phase 1: word k of staged row q = the aligned source word k of the row's x span
+        uint32_t const total = static_cast<uint32_t>(nRows) * wpr;
+        // source byte offset of staged word t; ~0: nothing to load (past the row's span, where a
+        // class's longest row has more words); the volume's last word, cut by the end of the
+        // source allocation, is loaded byte by byte after the batch (cutWord)
+        auto wordStart = [&](uint32_t t) -> uint64_t {
+            uint32_t const q = fdiv(t, fwpr);
+            uint32_t const k = t - q * wpr;
+            uint64_t const rb = rowBase(rA + static_cast<int32_t>(q));
+            uint64_t const start = (((rb + static_cast<uint64_t>(lo)) * BPV) & ~uint64_t(15)) + 16ull * k;
+            return start < (rb + static_cast<uint64_t>(hi)) * BPV ? start : ~0ull;
+        };
+        auto cutWord = [&](uint32_t t, uint64_t start) {
+            uint32_t w[4] = {0u, 0u, 0u, 0u};
+            for (uint64_t i = start; i < srcBytes; ++i)
+                w[(i - start) / 4] |= static_cast<uint32_t>(src[i]) << (8 * ((i - start) % 4));
+            stage[t] = u32x4{w[0], w[1], w[2], w[3]};
+        };
+        for (uint32_t t0 = 0; t0 < total; t0 += kStageWords * NT)
+        {
+            u32x4 w[kStageWords];
+            uint64_t at[kStageWords];
+#pragma unroll
+            for (int k = 0; k < kStageWords; ++k)
+            {
+                uint32_t const t = t0 + threadIdx.x + static_cast<uint32_t>(k * NT);
+                at[k] = t < total ? wordStart(t) : ~0ull;
+                w[k] = u32x4{0u, 0u, 0u, 0u};
+                if (at[k] != ~0ull && at[k] + 16 <= srcBytes)
+                    w[k] = *reinterpret_cast<u32x4 const*>(src + at[k]);
+            }
+#pragma unroll
+            for (int k = 0; k < kStageWords; ++k)
+            {
+                uint32_t const t = t0 + threadIdx.x + static_cast<uint32_t>(k * NT);
+                if (t < total)
+                {
+                    if (at[k] != ~0ull && at[k] + 16 > srcBytes)
+                        cutWord(t, at[k]);
+                    else
+                        stage[t] = w[k];
+                }
+            }
+        }
+        __syncthreads();
+        // LDS byte of source x (in [lo, hi)) in staged row q whose x = 0 is source voxel rb
+        auto ldsAt = [&](int32_t q, uint64_t rb, int32_t sx) -> uint32_t {
+            uint32_t const m = static_cast<uint32_t>(((rb + static_cast<uint64_t>(lo)) * BPV) & 15u);
+            return static_cast<uint32_t>(q) * P + m + static_cast<uint32_t>((sx - lo) * BPV);
+        };
+#pragma unroll 1
+        for (int u = 0; u < static_cast<int>(kBrickChunk) / NT; ++u)
+        {
+            int32_t const lv = (u * NT + static_cast<int32_t>(threadIdx.x)) * V;
+            if (lv >= chunkVox)
+                continue;
+            int32_t const v = vStart + lv;
+            int32_t const r = static_cast<int32_t>(fdiv(static_cast<uint32_t>(v), fdx));
+            int32_t const x = v - r * nx;
+            int32_t const q = r - rA;
+            int32_t const c = nx - x;                 // voxels of the item left in row r
+            uint64_t const rb = rowBase(r);
+            uint8_t* const out = dst + static_cast<uint64_t>(v) * BPV;
+            bool const whole = lv + V <= chunkVox;
+            if (whole && c >= V && fx + x >= lo && fx + x + V <= hi)
+            {
+                __builtin_nontemporal_store(ldsRead16(lds, ldsAt(q, rb, fx + x)),
+                                            (__attribute__((address_space(1))) u32x4*)(out));
+                continue;
+            }
+            if (whole && c < V && fx + x >= lo && fx + nx <= hi && fx >= lo && fx + (V - c) <= hi)
+            {
+                // row r's tail, then row r + 1 from its x = 0 (read from V - c voxels before it)
+                uint64_t const rb2 = rowBase(r + 1);
+                u32x4 const a = ldsRead16(lds, ldsAt(q, rb, fx + x));
+                u32x4 const bb = ldsRead16(lds, ldsAt(q + 1, rb2, fx) - static_cast<uint32_t>(c * BPV));
+                __builtin_nontemporal_store(mergeBytes(a, bb, c * BPV), (__attribute__((address_space(1))) u32x4*)(out));
+                continue;
+            }
+            // clamped x halo voxels, or the brick's last partial item: voxel by voxel
+            int32_t const n = min(V, chunkVox - lv);
+            int32_t rr = r, xx = x, qq = q;
+            uint64_t rbb = rb;
+            for (int32_t k = 0; k < n; ++k)
+            {
+                int32_t const sx = min(max(fx + xx, 0), sdx - 1);
+                uint32_t const a = ldsAt(qq, rbb, sx);
+                uint32_t code;
+                if constexpr (BPV == 1)
+                    code = lds[a];
+                else if constexpr (BPV == 2)
+                    code = static_cast<uint32_t>(lds[a]) | static_cast<uint32_t>(lds[a + 1]) << 8;
+                else
+                    code = static_cast<uint32_t>(lds[a]) | static_cast<uint32_t>(lds[a + 1]) << 8 |
+                           static_cast<uint32_t>(lds[a + 2]) << 16 | static_cast<uint32_t>(lds[a + 3]) << 24;
+                storeCode<BPV>(out, static_cast<uint64_t>(k), code);
+                if (++xx == nx && k + 1 < n)
+                {
+                    xx = 0;
+                    ++rr;
+                    ++qq;
+                    rbb = rowBase(rr);
+                }
+            }
+        }
+    }
+
+    // Dynamic LDS bytes of brickGatherKernel for a grid (0: more than kGatherLdsMax -- the staged
+    // kernel then runs): per class, the rows a 16-KiB chunk can touch x the words per row.
+    constexpr uint32_t kGatherLdsMax = 64u * 1024u;
+
+    uint32_t gatherLdsBytes(BrickGrid const& g, uint32_t bpv)
+    {
+        uint32_t const V = 16u / bpv;
+        uint64_t need = 0;
+        for (int cx = 0; cx < 3; ++cx)
+            for (int cy = 0; cy < 3; ++cy)
+                for (int cz = 0; cz < 3; ++cz)
+                {
+                    uint64_t const nvox = static_cast<uint64_t>(g.nx[cx]) * g.ny[cy] * g.nz[cz];
+                    uint64_t const chunkVox = std::min<uint64_t>(static_cast<uint64_t>(kBrickChunk) * V, nvox);
+                    uint64_t const rows = (chunkVox + g.nx[cx] - 1) / g.nx[cx] + 1;
+                    need = std::max<uint64_t>(need, rows * g.fwpr[cx].d * 16ull);
+                }
+        return need <= kGatherLdsMax ? static_cast<uint32_t>(need) : 0u;
+    }
+
     // Descriptor table: pinned host staging + a grow-only device buffer, uploaded with a
     // stream-ordered H2D copy on the compute stream.  Both are reused only after the previous
     // decomposition's kernel finished (event recorded behind it), so a caller that switches
@@ -610,9 +1021,35 @@ namespace hipk
         // threads per workgroup (knob decompose.block): 128 gives each thread twice the items and
         // staged words of a 256-thread workgroup over the same 16-KiB chunk
         bool const half = rt::knob(rt::Knob::DecomposeBlock) == 128;
+        uint32_t const gatherLds =
+            useGrid && rt::knob(rt::Knob::DecomposeGather) != 0 ? gatherLdsBytes(grid, bpv) : 0u;
+        bool const pipe = useGrid && gatherLds == 0 && !half && rt::knob(rt::Knob::DecomposePipe) != 0;
         auto launch = [&](auto bpvC, auto swC) {
             constexpr int B = decltype(bpvC)::value, W = decltype(swC)::value;
-            if (half)
+            if (pipe)
+            {
+                // resident workgroups only (a persistent walk), a multiple of 8 (XCD grouping)
+                static unsigned const perCU = [] {
+                    int n = 0;
+                    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                            &n, reinterpret_cast<void const*>(brickPipeKernel<B, W, kBlock>), kBlock, 0) != hipSuccess ||
+                        n < 1)
+                    {
+                        (void)hipGetLastError();
+                        n = 2;
+                    }
+                    return static_cast<unsigned>(std::min(n, 8));
+                }();
+                unsigned G = std::min<unsigned>(g, kNumCUs * perCU);
+                if (G >= 8)
+                    G &= ~7u;
+                hipLaunchKernelGGL((brickPipeKernel<B, W, kBlock>), dim3(G), dim3(kBlock), 0, s, grid, fdc, fdg, g,
+                                   source.data, source.dimX, source.dimY, source.dimZ, alignedLds);
+            }
+            else if (gatherLds != 0)
+                hipLaunchKernelGGL((brickGatherKernel<B, W, kBlock>), dim3(g), dim3(kBlock), gatherLds, s, grid, fdc, fdg,
+                                   source.data, source.dimX, source.dimY, source.dimZ);
+            else if (half)
             {
                 if (useGrid)
                     hipLaunchKernelGGL((brickCopyKernel<B, 2 * W, true, 128>), dim3(g), dim3(128), 0, s, dev, grid, fdc,

@@ -100,6 +100,8 @@ namespace rt
         PointwiseDwordShift,           // 0: 4-byte general-path windows keep the byte-align stage (whole-dword offsets)
         AggregatesMomentsPipe,         // integer moments: 0 one buffer x 4 items, 1 (default) / 2 / 4 two buffers x 4 / 8 / 2 items, 3 one buffer x 8
         DecomposeBatch,                // 1: BrickDecompose plans / copies in up to 8 batches of brick planes (measured slower: off)
+        DecomposeGather,               // 1: uniform brick grids stage source rows and gather items (measured no faster: off)
+        DecomposePipe,                 // 1: uniform brick grids on a resident, double-buffered walk (measured slower: off)
         Count
     };
     int64_t knob(Knob k);
