@@ -484,3 +484,36 @@ def test_resample_chain_downsampling_unstaged_rows(g, o, dfmt):
                 out = g.resample(dfmt, dmap, dd, 7, (0.0, 1.0), src, 1)
                 ref = o.resample(dfmt, dmap, dd, 7, (0.0, 1.0), src, 1)
                 assert_codes_equal(out, ref, dfmt, f"down {sd}->{dd} specials={specials} dmap={dmap}")
+
+
+@pytest.mark.parametrize("pinned", [0, 1])
+def test_large_migrations_keep_the_data(g, pinned):
+    """Buffers of >= 64 MiB take the migration fast paths (runtime/Memory.cpp MigrateBuffer): a
+    fresh pageable destination faulted in by the host threads before the D2H copy, the old pageable
+    buffer freed on a background thread after the H2D copy, pinned buffers kept for reuse by the
+    next migration of the same size.  Three round trips of a 128 MiB UInt16 volume with a GPU op in
+    between: the data arrives intact each way; vktHipReleaseCachedMemory then returns the cached
+    pinned buffer."""
+    import ctypes as C
+    from volkit_amd._lib import lib
+    vkt = g.vkt
+    assert lib.vktHipSetPinnedHostAllocation(pinned) == 0
+    try:
+        rng = np.random.default_rng(31 + pinned)
+        codes = rng.integers(0, 60000, (256, 512, 512), dtype=np.uint16)
+        v = g.volume(codes, 5, (0.0, 1.0))
+        for r in range(3):
+            g._gpu()
+            v.migrate()
+            assert vkt.FillRange(v, 7, 3 + r, 2, 9, 5 + r, 4, 1.0 - 1.0 / 65536) == vkt.NoError
+            g._cpu()
+            got = v.to_numpy()
+            codes[2:4, 3 + r:5 + r, 7:9] = 65535
+            np.testing.assert_array_equal(got, codes, err_msg=f"round {r}")
+        del v
+        released = C.c_size_t(0)
+        assert lib.vktHipReleaseCachedMemory(C.byref(released)) == 0
+        if pinned:
+            assert released.value >= codes.nbytes
+    finally:
+        lib.vktHipSetPinnedHostAllocation(0)

@@ -13,8 +13,12 @@
 // reference's cudaMemcpy contract: the caller may free or read host memory right after).
 // Device-to-device copies stay on the compute stream, ordered with the kernels.
 
+#include "HostPool.hpp"
 #include "Runtime.hpp"
 #include "volkit_hip.h"
+
+#include <sys/mman.h>
+#include <thread>
 
 #include <algorithm>
 #include <atomic>
@@ -47,6 +51,66 @@ namespace
     {
         static auto* s = new std::unordered_set<void*>;
         return *s;
+    }
+
+    // ---- host side of a migration (ManagedBuffer::migrate -> MigrateBuffer) ------------------
+    // Measured on the MI355X box for a 2 GiB volume (profiles/r04/migrate_breakdown.txt): the
+    // PCIe copy itself runs at 55-57 GB/s from pageable (pages written) or pinned memory, but a
+    // migrate ran at 9.5-13 GB/s -- the rest was host memory management around it: a D2H copy into
+    // a FRESH pageable buffer faults its pages in during the DMA (10 GB/s), freeing the 2 GiB host
+    // buffer after an H2D copy (munmap) costs more than the copy, and hipHostMalloc / hipHostFree of
+    // 2 GiB pinned take 138 / 78 ms.  So, for large buffers (>= kBigHost):
+    //  * a fresh pageable destination is faulted in by the host pool's threads before the copy
+    //    (transparent huge pages requested: 2-MiB faults);
+    //  * the old pageable buffer is freed on a background thread (the copy has completed: the
+    //    migrate's memcpy is synchronous);
+    //  * freed pinned buffers are kept for reuse by an allocation of the same size (at most
+    //    kPinnedCacheBytes in all), returned by vktHipReleaseCachedMemory or when hipHostMalloc fails.
+    constexpr std::size_t kBigHost = std::size_t(64) << 20;
+    constexpr std::size_t kPinnedCacheBytes = std::size_t(16) << 30;
+    std::vector<std::pair<void*, std::size_t>>& pinnedCache()
+    {
+        static auto* c = new std::vector<std::pair<void*, std::size_t>>;
+        return *c;
+    }
+    std::size_t gPinnedCached = 0;   // under gPinnedMutex
+    std::unordered_map<void*, std::size_t>& pinnedSizes()
+    {
+        static auto* m = new std::unordered_map<void*, std::size_t>;
+        return *m;
+    }
+
+    std::size_t releasePinnedCache()
+    {
+        std::vector<std::pair<void*, std::size_t>> drop;
+        {
+            std::lock_guard<std::mutex> lock(gPinnedMutex);
+            drop.swap(pinnedCache());
+            gPinnedCached = 0;
+        }
+        std::size_t n = 0;
+        for (auto& e : drop)
+        {
+            (void)rt::check(hipHostFree(e.first), "hipHostFree");
+            n += e.second;
+        }
+        return n;
+    }
+
+    void prefaultHost(void* p, std::size_t bytes)
+    {
+        uintptr_t const a = reinterpret_cast<uintptr_t>(p);
+        uintptr_t const h0 = (a + (std::size_t(2) << 20) - 1) & ~((std::size_t(2) << 20) - 1);
+        uintptr_t const h1 = (a + bytes) & ~((std::size_t(2) << 20) - 1);
+        if (h1 > h0)
+            (void)madvise(reinterpret_cast<void*>(h0), h1 - h0, MADV_HUGEPAGE);
+        constexpr std::size_t kPage = 4096;
+        std::size_t const pages = (bytes + kPage - 1) / kPage;
+        volatile uint8_t* const b = static_cast<volatile uint8_t*>(p);
+        rt::parallelFor(pages, 2048, [&](std::size_t i0, std::size_t i1) {
+            for (std::size_t i = i0; i < i1; ++i)
+                b[std::min(i * kPage, bytes - 1)] = 0;
+        });
     }
 
     // ---- device heap: the library's caching allocator for GPU buffers ----------------------
@@ -463,11 +527,32 @@ namespace detail
         }
         if (gPinnedHost.load())
         {
+            {
+                std::lock_guard<std::mutex> lock(gPinnedMutex);
+                auto& c = pinnedCache();
+                for (auto it = c.begin(); it != c.end(); ++it)
+                    if (it->second == bytes)
+                    {
+                        void* const p = it->first;
+                        gPinnedCached -= it->second;
+                        c.erase(it);
+                        pinnedSet().insert(p);
+                        pinnedSizes()[p] = bytes;
+                        return p;
+                    }
+            }
             void* p = nullptr;
-            if (rt::check(hipHostMalloc(&p, bytes, hipHostMallocDefault), "hipHostMalloc") == vktNoError)
+            hipError_t err = hipHostMalloc(&p, bytes, hipHostMallocDefault);
+            if (err != hipSuccess && releasePinnedCache() > 0)
+            {
+                (void)hipGetLastError();
+                err = hipHostMalloc(&p, bytes, hipHostMallocDefault);
+            }
+            if (rt::check(err, "hipHostMalloc") == vktNoError)
             {
                 std::lock_guard<std::mutex> lock(gPinnedMutex);
                 pinnedSet().insert(p);
+                pinnedSizes()[p] = bytes;
                 return p;
             }
         }
@@ -493,11 +578,26 @@ namespace detail
             if (it != pinnedSet().end())
             {
                 pinnedSet().erase(it);
+                std::size_t const bytes = pinnedSizes()[data];
+                pinnedSizes().erase(data);
+                if (bytes >= kBigHost && gPinnedCached + bytes <= kPinnedCacheBytes)
+                {
+                    pinnedCache().emplace_back(data, bytes);   // for the next migration of this size
+                    gPinnedCached += bytes;
+                    return;
+                }
                 (void)rt::check(hipHostFree(data), "hipHostFree");
                 return;
             }
         }
         std::free(data);
+    }
+
+    // A large pageable buffer the caller is done with: freed off the calling thread (munmap of
+    // 2 GiB costs more than its PCIe copy).
+    void freeHostLater(void* data)
+    {
+        std::thread([data] { std::free(data); }).detach();
     }
 
     void CopyOn(void* dst, void const* src, std::size_t bytes, ExecutionPolicy const& owner)
@@ -511,10 +611,22 @@ namespace detail
         if (ep.device == last.device)
             return data;
         void* fresh = AllocateOn(bytes, ep);
+        bool pinnedFresh = false, pinnedOld = false;
+        if (bytes >= kBigHost)
+        {
+            std::lock_guard<std::mutex> lock(gPinnedMutex);
+            pinnedFresh = fresh != nullptr && pinnedSet().count(fresh) != 0;
+            pinnedOld = data != nullptr && pinnedSet().count(data) != 0;
+        }
+        if (bytes >= kBigHost && !onGpu(ep) && fresh != nullptr && !pinnedFresh && data != nullptr)
+            prefaultHost(fresh, bytes);   // (the copy below then writes resident pages)
         if (bytes > 0 && data != nullptr && fresh != nullptr)
             (void)memcpyHip(fresh, data, bytes,
                             onGpu(ep) ? CopyKind::HostToDevice : CopyKind::DeviceToHost);
-        FreeOn(data, last);
+        if (bytes >= kBigHost && !onGpu(last) && !pinnedOld && data != nullptr)
+            freeHostLater(data);   // the copy is complete (memcpyHip synchronises)
+        else
+            FreeOn(data, last);
         last = ep;
         return fresh;
     }
@@ -611,7 +723,7 @@ vktError vktHipFree(void* ptr)
 
 vktError vktHipReleaseCachedMemory(size_t* releasedBytes)
 {
-    std::size_t const n = vkt::heapReleaseCached();
+    std::size_t const n = vkt::heapReleaseCached() + vkt::releasePinnedCache();
     if (releasedBytes != nullptr)
         *releasedBytes = n;
     return vktNoError;
