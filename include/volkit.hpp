@@ -568,6 +568,10 @@ namespace vkt
         virtual bool flush();
         virtual bool good() const;
 
+        //! read(), with large reads split over the library's host threads (pread at the
+        //! stream's position, which then advances as read() would advance it)
+        std::size_t readParallel(char* buf, std::size_t len);
+
         void setDims(Vec3i dims);
         Vec3i getDims() const;
         void setDataFormat(DataFormat dataFormat);

@@ -178,3 +178,36 @@ def test_sv_stream_gpu_policy(tmp_path):
     ref = ob.Volume.zeros((31, 9, 17), 4)
     ob.arith_range("Sum", ref, ob.Volume(codes, 4), ob.Volume(codes, 4), (0, 0, 0), (31, 9, 17))
     np.testing.assert_array_equal(w.to_numpy(), ref.codes)
+
+
+def test_large_host_read_in_parallel_keeps_the_stream_position(tmp_path):
+    """InputStream::read into a host volume of >= 64 MiB reads the file with parallel preads at
+    the stream's position (RawFile::readParallel): the volume's bytes, then a second, small read
+    from the same RawFile continues right after them (the FILE position advanced as fread would);
+    a file shorter than the volume gives ReadError."""
+    dims = (512, 288, 256)                         # 72 MiB of UInt16
+    n = dims[0] * dims[1] * dims[2]
+    rng = np.random.default_rng(5)
+    head = rng.integers(0, 65535, 7, dtype=np.uint16)          # read first, small (fread)
+    big = rng.integers(0, 65535, n, dtype=np.uint16)
+    tail = rng.integers(0, 65535, 2 * 3 * 4, dtype=np.uint16)
+    path = tmp_path / "big.raw"
+    np.concatenate([head, big, tail]).tofile(path)
+    set_device(vkt.ExecutionPolicy.Device_CPU)
+    a = vkt.StructuredVolume(7, 1, 1, 5)
+    v = vkt.StructuredVolume(*dims, 5)
+    w = vkt.StructuredVolume(2, 3, 4, 5)
+    f = vkt.RawFile(str(path), "rb")
+    s = vkt.InputStream(f)
+    assert s.read(a) == vkt.NoError
+    assert s.read(v) == vkt.NoError
+    assert s.read(w) == vkt.NoError
+    f.close()
+    np.testing.assert_array_equal(a.to_numpy().reshape(-1), head)
+    np.testing.assert_array_equal(v.to_numpy().reshape(-1), big)
+    np.testing.assert_array_equal(w.to_numpy().reshape(-1), tail)
+    short = tmp_path / "short.raw"
+    big[: n - 1000].tofile(short)
+    f = vkt.RawFile(str(short), "rb")
+    assert vkt.InputStream(f).read(v) == vkt.ReadError
+    f.close()

@@ -21,17 +21,22 @@
 // the compute stream waits for the copies (later kernels see the data).  Under the CPU policy
 // the bytes go straight to / from host memory, as in the reference.
 
+#include "../runtime/HostPool.hpp"
 #include "../runtime/Runtime.hpp"
 #include "../StructuredVolume_impl.hpp"
 #include "volkit_codec.hpp"
 #include "volkit_hip.h"
 
 #include <algorithm>
+#include <atomic>
+#include <cstdio>
 #include <cstring>
 #include <mutex>
 #include <sstream>
 #include <string>
 #include <vector>
+
+#include <unistd.h>
 
 namespace vkt
 {
@@ -318,6 +323,56 @@ RawFile::~RawFile()
 
 std::size_t RawFile::read(char* buf, std::size_t len) { return good() ? std::fread(buf, 1, len, file_) : 0; }
 
+// A host-resident volume read from a file (InputStream::read under the CPU policy, the
+// reference's flow before a migrate): one fread into fresh pages ran at ~4.5 GB/s on the MI355X
+// box (page-cache copy plus the page faults, one thread); 16 MiB preads spread over the host pool
+// fault and copy in parallel.  Falls back to fread for small reads, unseekable streams, or when
+// the descriptor cannot pread.
+std::size_t RawFile::readParallel(char* buf, std::size_t len)
+{
+    constexpr std::size_t kMin = std::size_t(64) << 20, kChunk = std::size_t(16) << 20;
+    if (!good() || len < kMin || rt::hostThreads() <= 1)
+        return read(buf, len);
+    off_t const pos = ftello(file_);
+    int const fd = fileno(file_);
+    if (pos < 0 || fd < 0)
+        return read(buf, len);
+    std::size_t const chunks = (len + kChunk - 1) / kChunk;
+    std::vector<std::size_t> got(chunks, 0);
+    std::atomic<bool> failed{false};
+    rt::parallelFor(chunks, 1, [&](std::size_t c0, std::size_t c1) {
+        for (std::size_t c = c0; c < c1; ++c)
+        {
+            std::size_t const b = c * kChunk, e = std::min(len, b + kChunk);
+            std::size_t off = b;
+            while (off < e)
+            {
+                ssize_t const r = pread(fd, buf + off, e - off, pos + static_cast<off_t>(off));
+                if (r < 0)
+                    failed.store(true);
+                if (r <= 0)
+                    break;
+                off += static_cast<std::size_t>(r);
+            }
+            got[c] = off - b;
+        }
+    });
+    std::size_t total = 0;   // the contiguous prefix (a short chunk is the end of the file)
+    for (std::size_t c = 0; c < chunks; ++c)
+    {
+        total += got[c];
+        if (got[c] < std::min(len, (c + 1) * kChunk) - c * kChunk)
+            break;
+    }
+    if (failed.load() && total == 0)
+    {
+        (void)fseeko(file_, pos, SEEK_SET);
+        return read(buf, len);
+    }
+    (void)fseeko(file_, pos + static_cast<off_t>(total), SEEK_SET);
+    return total;
+}
+
 std::size_t RawFile::write(char const* buf, std::size_t len) { return good() ? std::fwrite(buf, 1, len, file_) : 0; }
 
 bool RawFile::seek(std::size_t pos) { return good() && std::fseek(file_, static_cast<long>(pos), SEEK_SET) == 0; }
@@ -350,6 +405,8 @@ Error InputStream::read(StructuredVolume& volume)
         if (e != vktNoError)
             return InvalidValue;
     }
+    else if (auto* file = dynamic_cast<RawFile*>(&dataSource_))
+        len = file->readParallel(reinterpret_cast<char*>(volume.getData()), n);
     else
         len = dataSource_.read(reinterpret_cast<char*>(volume.getData()), n);
     return len == n ? NoError : ReadError;
