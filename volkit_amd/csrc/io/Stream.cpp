@@ -164,7 +164,9 @@ namespace
                 if (bytes <= Staging::kChunk)
                 {
                     // one file read for all lines of the chunk (they are consecutive in the file)
-                    got = src.read(reinterpret_cast<char*>(st.buf[b]), bytes);
+                    auto* file = dynamic_cast<RawFile*>(&src);
+                    got = file ? file->readParallel(reinterpret_cast<char*>(st.buf[b]), bytes)
+                               : src.read(reinterpret_cast<char*>(st.buf[b]), bytes);
                     std::size_t const fullLines = got / std::max<std::size_t>(lineBytes, 1);
                     uint8_t* d = dev + run.devOffset + done * pitch;
                     hipError_t he;
@@ -325,12 +327,13 @@ std::size_t RawFile::read(char* buf, std::size_t len) { return good() ? std::fre
 
 // A host-resident volume read from a file (InputStream::read under the CPU policy, the
 // reference's flow before a migrate): one fread into fresh pages ran at ~4.5 GB/s on the MI355X
-// box (page-cache copy plus the page faults, one thread); 16 MiB preads spread over the host pool
-// fault and copy in parallel.  Falls back to fread for small reads, unseekable streams, or when
+// box (page-cache copy plus the page faults, one thread); 4 MiB preads spread over the host pool
+// fault and copy in parallel (and fill InputStream's 64 MiB pinned staging buffers faster than
+// one fread for volumes in HBM).  Falls back to fread for small reads, unseekable streams, or when
 // the descriptor cannot pread.
 std::size_t RawFile::readParallel(char* buf, std::size_t len)
 {
-    constexpr std::size_t kMin = std::size_t(64) << 20, kChunk = std::size_t(16) << 20;
+    constexpr std::size_t kMin = std::size_t(8) << 20, kChunk = std::size_t(4) << 20;
     if (!good() || len < kMin || rt::hostThreads() <= 1)
         return read(buf, len);
     off_t const pos = ftello(file_);
