@@ -979,6 +979,32 @@ def main():
         del V
         ep.device = vkt.ExecutionPolicy.Device_CPU
         vkt.SetThreadExecutionPolicy(ep)
+    if want("u8ab"):
+        # in-process A/B of the UInt8 row-edge knobs on the 800^3 sub-box at x0 = 100 (SumRange and
+        # CopyRange, same offsets): pointwise.u8_pairs x pointwise.merge_sectors x pointwise.u8_wide
+        m = 1024
+        A, B, D = alloc((m,) * 3, 4, seed=1), alloc((m,) * 3, 4, seed=2), alloc((m,) * 3, 4)
+        f0, f1 = Vec3i_t(100, 100, 100), Vec3i_t(900, 900, 900)
+        nv = 800 ** 3
+        cases = (("SumRange", lambda: lib.vktHipArithmeticRange(0, D, A, B, f0, f1, o), 3),
+                 ("CopyRange same offset", lambda: lib.vktHipCopyRange(D, A, f0, f1, f0), 2))
+        kvs = [(p_, mg, w) for p_ in (1, 2, 0) for mg in (1, 2, 0) for w in (1, 0)]
+        ab = {}
+        for rnd in range(3):
+            for kv in kvs:
+                lib.vktHipSetTuningKnob(b"pointwise.u8_pairs", kv[0])
+                lib.vktHipSetTuningKnob(b"pointwise.merge_sectors", kv[1])
+                lib.vktHipSetTuningKnob(b"pointwise.u8_wide", kv[2])
+                for lab, fn, _ in cases:
+                    ab.setdefault((lab, kv), []).append(timed(fn, R))
+        for k in (b"pointwise.u8_pairs", b"pointwise.merge_sectors", b"pointwise.u8_wide"):
+            lib.vktHipSetTuningKnob(k, -1)
+        for lab, fn, streams in cases:
+            for kv in kvs:
+                ts = sorted(ab[(lab, kv)])
+                report(f"u8ab {lab} 800^3 x0=100 UInt8 u8_pairs={kv[0]} merge_sectors={kv[1]} u8_wide={kv[2]} "
+                       f"(median of 3, spread {ts[0]:.4f}-{ts[-1]:.4f})", ts[1], streams * nv, nv)
+        free(A, B, D)
     if want("decbatch"):
         # in-process A/B of BrickDecompose's batched planning (knob decompose.batch: 1 up to 8
         # batches of brick planes, planning batch k + 1 while the GPU copies batch k; 0 one batch)

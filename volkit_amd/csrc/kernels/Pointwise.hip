@@ -15,6 +15,8 @@
 #include "../runtime/Runtime.hpp"
 #include "volkit_hip.h"
 
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 namespace vkt
@@ -347,6 +349,18 @@ namespace hipk
         p.vec = vec;
         p.gen = gen && !vec && rt::knob(rt::Knob::PointwiseGeneral) != 0;
         p.uniform = uniform;
+        static bool const debugPlan = std::getenv("VKT_DEBUG_PLAN") != nullptr;   // diagnostics: the chosen path
+        if (debugPlan)
+            std::fprintf(stderr,
+                         "VKT_PLAN ns=%d bpv=%u box=%lldx%lldx%lld rows=%lldx%lldx%lld bases=%lld/%lld/%lld vec=%d "
+                         "padded=%d merge=%d pair16=%d gen=%d gg.fast=%d gg.merge=%d gg.wide=%d gg.dword=%d "
+                         "gg.cpr=%llu gg.items=%llu\n",
+                         ns, bpv, static_cast<long long>(nx), static_cast<long long>(ny), static_cast<long long>(nz),
+                         static_cast<long long>(vnx), static_cast<long long>(vny), static_cast<long long>(vnz),
+                         static_cast<long long>(p.d.base), static_cast<long long>(p.s1.base),
+                         static_cast<long long>(p.s2.base), p.vec ? 1 : 0, p.g.padded, p.g.merge, p.g.pair16,
+                         p.gen ? 1 : 0, gg.fast, gg.merge, gg.wide, gg.dword, static_cast<unsigned long long>(gg.cpr),
+                         static_cast<unsigned long long>(gg.items));
         return p;
     }
 
