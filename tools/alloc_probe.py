@@ -24,61 +24,7 @@ nb = 2 * n ** 3
 o, last = Vec3i_t(0, 0, 0), Vec3i_t(n, n, n)
 
 
-class _Loc(C.Structure):
-    _fields_ = [("type", C.c_int), ("id", C.c_int)]
-
-
-class _Flags(C.Structure):
-    _fields_ = [("compressionType", C.c_ubyte), ("gpuDirectRDMACapable", C.c_ubyte), ("usage", C.c_ushort)]
-
-
-class _Prop(C.Structure):
-    _fields_ = [("type", C.c_int), ("requestedHandleType", C.c_int), ("location", _Loc),
-                ("win32HandleMetaData", C.c_void_p), ("allocFlags", _Flags)]
-
-
-class _Access(C.Structure):
-    _fields_ = [("location", _Loc), ("flags", C.c_int)]
-
-
-def vmm_alloc(sizes):
-    """Virtual-memory-management allocation: one VA reservation for all volumes, one physical
-    allocation (hipMemCreate) per entry of `sizes`, mapped back to back (hipMemMap)."""
-    prop = _Prop(1, 0, _Loc(1, 0), None, _Flags(0, 0, 0))
-    gran = C.c_size_t(0)
-    assert hip.hipMemGetAllocationGranularity(C.byref(gran), C.byref(prop), 0) == 0
-    g = gran.value
-    total = sum((sz + g - 1) // g * g for sz in sizes)
-    va = C.c_void_p()
-    assert hip.hipMemAddressReserve(C.byref(va), C.c_size_t(total), C.c_size_t(max(g, 1 << 30)), None, C.c_ulonglong(0)) == 0
-    off, handles, ptrs = 0, [], []
-    for sz in sizes:
-        sz = (sz + g - 1) // g * g
-        h = C.c_void_p()
-        assert hip.hipMemCreate(C.byref(h), C.c_size_t(sz), C.byref(prop), C.c_ulonglong(0)) == 0
-        assert hip.hipMemMap(C.c_void_p(va.value + off), C.c_size_t(sz), C.c_size_t(0), h, C.c_ulonglong(0)) == 0
-        handles.append((h, va.value + off, sz))
-        ptrs.append(va.value + off)
-        off += sz
-    acc = _Access(_Loc(1, 0), 3)
-    assert hip.hipMemSetAccess(va, C.c_size_t(total), C.byref(acc), C.c_size_t(1)) == 0
-    return ptrs, [("vmm", va.value, total, handles)]
-
-
-def vmm_free(rec):
-    _, va, total, handles = rec
-    for h, p, sz in handles:
-        hip.hipMemUnmap(C.c_void_p(p), C.c_size_t(sz))
-        hip.hipMemRelease(h)
-    hip.hipMemAddressFree(C.c_void_p(va), C.c_size_t(total))
-
-
 def alloc(mode):
-    if mode == "vmm":      # one physical allocation for the three volumes
-        ptrs, rec = vmm_alloc([3 * nb])
-        return [ptrs[0], ptrs[0] + nb, ptrs[0] + 2 * nb], rec
-    if mode == "vmm3":     # one physical allocation per volume, one VA range
-        return vmm_alloc([nb, nb, nb])
     if mode in ("library", "library0"):   # vktHipAllocate (arena on / off: knob memory.arena)
         lib.vktHipSetTuningKnob(b"memory.arena", 1 if mode == "library" else 0)
         ptrs = []
@@ -124,9 +70,7 @@ for it in range(int(os.environ.get("PROBE_ITERS", "5"))):
         print(it, mode, round(ms, 4), flush=True)
         torch.cuda.synchronize()
         for p in frees:
-            if isinstance(p, tuple) and p[0] == "vmm":
-                vmm_free(p)
-            elif isinstance(p, tuple):
+            if isinstance(p, tuple):
                 lib.vktHipFree(C.c_void_p(p[1]))
             else:
                 hip.hipFree(C.c_void_p(p))

@@ -408,7 +408,7 @@ namespace hipk
 #pragma unroll
                         for (int q = 0; q < 2; ++q)
                         {
-                            u32x4 const v{o[u][4 * q], o[u][4 * q + 1], o[u][4 * q + 2], o[u][4 * q + 3]};
+                            u32x4 v{o[u][4 * q], o[u][4 * q + 1], o[u][4 * q + 2], o[u][4 * q + 3]};
                             uint8_t* const p = d.data + od[u][q] * 4u;
                             if constexpr (MODE != 0)
                             {
@@ -419,13 +419,17 @@ namespace hipk
                                     int const lo = 4 * static_cast<int>(x < 0 ? (x < -4 ? 4 : -x) : 0);
                                     int const hi = 4 * static_cast<int>(g.vnx - x < 4 ? (g.vnx - x < 0 ? 0 : g.vnx - x) : 4);
                                     if (g.merge)
-                                        __builtin_nontemporal_store(mergeBytes16(v, own[u][q], lo, hi),
-                                                                    reinterpret_cast<u32x4*>(p));
-                                    else if (hi > lo)
-                                        storeByteRange16(p, v, lo, hi);
-                                    continue;
+                                        v = mergeBytes16(v, own[u][q], lo, hi);   // (stored below, with the rest)
+                                    else
+                                    {
+                                        if (hi > lo)
+                                            storeByteRange16(p, v, lo, hi);
+                                        continue;
+                                    }
                                 }
                             }
+                            // one store statement for whole and merged halves: a wave holding both
+                            // issues it once (two statements: both, in nearly every wave of a sub-box)
                             __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
                         }
                     }
@@ -439,6 +443,7 @@ namespace hipk
                             w[2 + i] = o[u + 1][4 * i] | o[u + 1][4 * i + 1] << 8 | o[u + 1][4 * i + 2] << 16 |
                                        o[u + 1][4 * i + 3] << 24;
                         }
+                        u32x4 v{w[0], w[1], w[2], w[3]};
                         if constexpr (MODE != 0)
                         {
                             int64_t const x = xr[u][0];
@@ -446,19 +451,19 @@ namespace hipk
                             {
                                 // the pair straddles a row end (or, merging, lies in an end
                                 // sector): the row's bytes only, or the whole 16 B merged with
-                                // the destination's own bytes
+                                // the destination's own bytes (stored below, with the rest)
                                 int const lo = x < 0 ? static_cast<int>(x < -16 ? 16 : -x) : 0;
                                 int const hi = g.vnx - x < 16 ? static_cast<int>(g.vnx - x < 0 ? 0 : g.vnx - x) : 16;
                                 if (g.merge)
-                                    __builtin_nontemporal_store(mergeBytes16(u32x4{w[0], w[1], w[2], w[3]}, own[u][0], lo, hi),
-                                                                reinterpret_cast<u32x4*>(d.data + od[u][0]));
+                                    v = mergeBytes16(v, own[u][0], lo, hi);
                                 else
-                                    storeByteRange16(d.data + od[u][0], u32x4{w[0], w[1], w[2], w[3]}, lo, hi);
-                                continue;
+                                {
+                                    storeByteRange16(d.data + od[u][0], v, lo, hi);
+                                    continue;
+                                }
                             }
                         }
-                        __builtin_nontemporal_store(u32x4{w[0], w[1], w[2], w[3]},
-                                                    reinterpret_cast<u32x4*>(d.data + od[u][0]));
+                        __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(d.data + od[u][0]));
                     }
                 }
                 return;
@@ -1124,38 +1129,34 @@ namespace hipk
                 __builtin_nontemporal_store(u32x4{rd[4], rd[5], rd[6], rd[7]}, reinterpret_cast<u32x4*>(p + 16));
             }
         };
+        // Full items, merged row-end items and sector-completion pads share ONE store statement
+        // (see pointwiseGenSpanFast16: separate statements cost a wave both instruction sets
+        // whenever it holds both kinds of item -- 2.3x the store instructions on a sub-box)
         auto store = [&](int u, uint32_t const (&rd)[2 * BD]) {
-            if (g.merge && !(xs[u] >= 0 && xs[u] + 8 <= vnx))
+            bool const full = xs[u] >= 0 && xs[u] + 8 <= vnx;
+            if (g.merge || full)
             {
-                // the row's voxels from rd, the rest of the chunk from the destination itself: one
-                // whole-chunk store, so every 64-B sector of the row ends is written completely
-                uint32_t oc[8], dc[8];
-                unpack8<BD>(rd, oc);
-                unpack8<BD>(dd[u], dc);
-#pragma unroll
-                for (int v = 0; v < 8; ++v)
-                    oc[v] = xs[u] + v >= 0 && xs[u] + v < vnx ? oc[v] : dc[v];
-                Window<BD> t;
-                packCodes<BD>(oc, t, std::make_index_sequence<2 * BD>{});
                 uint32_t m[2 * BD];
 #pragma unroll
                 for (int i = 0; i < 2 * BD; ++i)
-                    m[i] = t.w[i];
-                storeFull(u, m);
-                return;
-            }
-            if (xs[u] >= 0 && xs[u] + 8 <= vnx)
-            {
-                uint8_t* const p = d.data + od[u] * BD;
-                if constexpr (BD == 1)
-                    *reinterpret_cast<u32x2*>(p) = u32x2{rd[0], rd[1]};
-                else if constexpr (BD == 2)
-                    __builtin_nontemporal_store(u32x4{rd[0], rd[1], rd[2], rd[3]}, reinterpret_cast<u32x4*>(p));
-                else
+                    m[i] = rd[i];
+                if (!full)
                 {
-                    __builtin_nontemporal_store(u32x4{rd[0], rd[1], rd[2], rd[3]}, reinterpret_cast<u32x4*>(p));
-                    __builtin_nontemporal_store(u32x4{rd[4], rd[5], rd[6], rd[7]}, reinterpret_cast<u32x4*>(p + 16));
+                    // the row's voxels from rd, the rest of the chunk from the destination itself:
+                    // one whole-chunk store, so every 64-B sector of the row ends is written completely
+                    uint32_t oc[8], dc[8];
+                    unpack8<BD>(rd, oc);
+                    unpack8<BD>(dd[u], dc);
+#pragma unroll
+                    for (int v = 0; v < 8; ++v)
+                        oc[v] = xs[u] + v >= 0 && xs[u] + v < vnx ? oc[v] : dc[v];
+                    Window<BD> t;
+                    packCodes<BD>(oc, t, std::make_index_sequence<2 * BD>{});
+#pragma unroll
+                    for (int i = 0; i < 2 * BD; ++i)
+                        m[i] = t.w[i];
                 }
+                storeFull(u, m);
             }
             else
             {
@@ -1170,20 +1171,22 @@ namespace hipk
 #pragma unroll
         for (int u = 0; u < U; ++u)
         {
-            if (pad[u])
+            if (!win[u] && !pad[u])
+                continue;
+            uint32_t rd[2 * BD];
+#pragma unroll
+            for (int i = 0; i < 2 * BD; ++i)
+                rd[i] = dd[u][i];   // pad: sector completion, the destination's own bytes
+            if (win[u])
             {
-                storeFull(u, dd[u]);   // sector completion: the destination's own bytes
-                continue;
+                uint32_t a[2 * B1], b[2 * (NS >= 2 ? B2 : 1)];
+                if constexpr (NS >= 1)
+                    shiftWindow<B1>(wa[u], a, g.dword != 0);
+                if constexpr (NS >= 2)
+                    shiftWindow<B2>(wb[u], b, g.dword != 0);
+                result(a, b, rd);
             }
-            if (!win[u])
-                continue;
-            uint32_t a[2 * B1], b[2 * (NS >= 2 ? B2 : 1)], rd[2 * BD];
-            if constexpr (NS >= 1)
-                shiftWindow<B1>(wa[u], a, g.dword != 0);
-            if constexpr (NS >= 2)
-                shiftWindow<B2>(wb[u], b, g.dword != 0);
-            result(a, b, rd);
-            store(u, rd);
+            store(u, rd);   // (a pad lies outside its row: merged, every voxel is the destination's own)
         }
         if (!g.anyClamp)
             return;
@@ -1352,39 +1355,41 @@ namespace hipk
                 rd = u32x4{r[0], r[1], r[2], r[3]};
             }
         };
+        // Whole-item stores (full items, merged row-end items, sector-completion pads) go through
+        // ONE store instruction per item slot: separate store statements per case issue each as
+        // its own wave instruction whenever a wave holds both kinds of item -- nearly every wave of
+        // a sub-box, whose rows end every ~100 items (PMC: 2.3x the store instructions of an
+        // edge-free box).  Only the byte-range stores of unmerged row ends stay apart.
         auto store = [&](int u, u32x4 const& rd) {
             uint8_t* const p = d.data + od[u] * B;
             int32_t const x = xs[u];
-            if (x >= 0 && x + V <= vnx)
-                __builtin_nontemporal_store(rd, reinterpret_cast<u32x4*>(p));
-            else
+            bool const full = x >= 0 && x + V <= vnx;
+            if (full || g.merge)
             {
-                int const lo = B * (x < 0 ? -x : 0);
-                int const hi = B * (x + V > vnx ? vnx - x : V);
-                if (g.merge)
-                    __builtin_nontemporal_store(mergeBytes16(rd, dd[u], lo, hi), reinterpret_cast<u32x4*>(p));
-                else
-                    storeByteRange16(p, rd, lo, hi);
+                u32x4 v = rd;
+                if (!full)
+                    v = mergeBytes16(rd, dd[u], B * (x < 0 ? -x : 0), B * (x + V > vnx ? vnx - x : V));
+                __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
             }
+            else
+                storeByteRange16(p, rd, B * (x < 0 ? -x : 0), B * (x + V > vnx ? vnx - x : V));
         };
 #pragma unroll
         for (int u = 0; u < U; ++u)
         {
-            if (pad[u])
+            if (!win[u] && !pad[u])
+                continue;
+            u32x4 rd = dd[u];   // pad: sector completion with the destination's own bytes
+            if (win[u])
             {
-                __builtin_nontemporal_store(dd[u], reinterpret_cast<u32x4*>(d.data + od[u] * B));   // sector completion
-                continue;
+                uint32_t a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
+                if constexpr (NS >= 1)
+                    shiftWindow16(wa[u], a, B == 4 && g.dword != 0);
+                if constexpr (NS >= 2)
+                    shiftWindow16(wb[u], b, B == 4 && g.dword != 0);
+                result(a, b, rd);
             }
-            if (!win[u])
-                continue;
-            uint32_t a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
-            if constexpr (NS >= 1)
-                shiftWindow16(wa[u], a, B == 4 && g.dword != 0);
-            if constexpr (NS >= 2)
-                shiftWindow16(wb[u], b, B == 4 && g.dword != 0);
-            u32x4 rd;
-            result(a, b, rd);
-            store(u, rd);
+            store(u, rd);   // (a pad lies outside its row: merged, every byte is the destination's own)
         }
         if (!g.anyClamp)
             return;
