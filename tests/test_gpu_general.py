@@ -672,3 +672,32 @@ def test_float32_dword_shift(lib, o, dword, wide):
     finally:
         lib.vktHipSetTuningKnob(b"pointwise.dword_shift", -1)
         lib.vktHipSetTuningKnob(b"pointwise.f32_wide", -1)
+
+
+@pytest.mark.parametrize("dx", [0, 1, 3, 13, 16])
+def test_float32_three_stream_sector_completion(lib, o, dx):
+    """pointwise.merge_sectors = 2 extends 64-B sector completion to the 3-stream Float32 ops on
+    the general path (row-end items merged with the destination's own voxels, pads rewriting
+    them): Sum / SafeDiff with phase-shifting dstOffsets on 192-voxel rows (768-B pitches, gaps
+    >= 64 B between box rows), the destination outside the box intact, vs the oracle; knob 1 (the
+    default: byte-range row ends) alongside."""
+    rng = np.random.default_rng(300 + dx)
+    a = rand_codes(rng, 7, (5, 6, 192))
+    b = rand_codes(rng, 7, (5, 6, 192))
+    dinit = rand_codes(rng, 7, (5, 6, 192))
+    try:
+        for mk in (2, 1):
+            assert lib.vktHipSetTuningKnob(b"pointwise.merge_sectors", mk) == 0
+            for x0, w in ((0, 160), (5, 100), (17, 31), (40, 7), (3, 150)):
+                first, last = (x0, 1, 0), (x0 + w, 5, 4)
+                off = (dx - x0 + 2, 0, 1)   # arithmetic dstOffset: dst x = x + off
+                if x0 + w + off[0] > 192:
+                    continue
+                for op in ("Sum", "SafeDiff"):
+                    da, db, dd = Dev(a, 7), Dev(b, 7), Dev(dinit, 7)
+                    assert lib.vktHipArithmeticRange(OPS.index(op), dd.view, da.view, db.view, vec(first), vec(last),
+                                                     vec(off)) == 0, last_error()
+                    ref = o.arith(op, [7] * 3, [(0.0, 1.0)] * 3, a, b, dinit.copy(), first, last, off)
+                    assert_codes_equal(dd.read(), ref, 7, f"{op} merge={mk} dx={dx} x0={x0} w={w}")
+    finally:
+        lib.vktHipSetTuningKnob(b"pointwise.merge_sectors", -1)
