@@ -676,17 +676,17 @@ def test_float32_dword_shift(lib, o, dword, wide):
 
 @pytest.mark.parametrize("dx", [0, 1, 3, 13, 16])
 def test_float32_three_stream_sector_completion(lib, o, dx):
-    """pointwise.merge_sectors = 2 extends 64-B sector completion to the 3-stream Float32 ops on
-    the general path (row-end items merged with the destination's own voxels, pads rewriting
-    them): Sum / SafeDiff with phase-shifting dstOffsets on 192-voxel rows (768-B pitches, gaps
-    >= 64 B between box rows), the destination outside the box intact, vs the oracle; knob 1 (the
-    default: byte-range row ends) alongside."""
+    """64-B sector completion for the 3-stream Float32 ops on the general path (the default;
+    row-end items merged with the destination's own voxels, pads rewriting them): Sum / SafeDiff
+    with phase-shifting dstOffsets on 192-voxel rows (768-B pitches, gaps >= 64 B between box
+    rows), the destination outside the box intact, vs the oracle; knob pointwise.merge_sectors
+    = 0 (per-voxel row ends) alongside."""
     rng = np.random.default_rng(300 + dx)
     a = rand_codes(rng, 7, (5, 6, 192))
     b = rand_codes(rng, 7, (5, 6, 192))
     dinit = rand_codes(rng, 7, (5, 6, 192))
     try:
-        for mk in (2, 1):
+        for mk in (1, 0):
             assert lib.vktHipSetTuningKnob(b"pointwise.merge_sectors", mk) == 0
             for x0, w in ((0, 160), (5, 100), (17, 31), (40, 7), (3, 150)):
                 first, last = (x0, 1, 0), (x0 + w, 5, 4)

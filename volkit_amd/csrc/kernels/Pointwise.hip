@@ -282,8 +282,11 @@ namespace hipk
             // path completes sectors on its own, above)
             // (3-stream ops on 1-byte voxels: knob value 2, for the A/B of the 16-voxel items)
             bool const u8 = p.d.bpv == 1 && (ns < 1 || p.s1.bpv == 1) && (ns < 2 || p.s2.bpv == 1);
+            // 3-stream Float32 ops complete their sectors too (round 4, with one store statement
+            // per item: 800^3 sub-box at x0 = 100, SumRange dstOffset -97 1.271 -> 1.232 ms,
+            // dstOffset -100 1.204 -> 1.172 ms, profiles/r04/f32m3.jsonl)
             bool const f32 = p.d.bpv == 4 && (ns < 1 || p.s1.bpv == 4) && (ns < 2 || p.s2.bpv == 4);
-            bool merge = (ns <= 1 || ((u8 || f32) && rt::knob(rt::Knob::PointwiseMergeSectors) == 2)) && gg.fast &&
+            bool merge = (ns <= 1 || f32 || (u8 && rt::knob(rt::Knob::PointwiseMergeSectors) == 2)) && gg.fast &&
                          rt::knob(rt::Knob::PointwiseMergeSectors) != 0 &&
                          reinterpret_cast<uintptr_t>(p.d.data) % 64 == 0 && dBytes % 64 == 0;
             if (merge && vny > 1)
