@@ -1026,6 +1026,31 @@ def main():
                 report(f"f32m3 {lab} 800^3 x0=100 Float32 merge_sectors={kv} (median of 3, spread {ts[0]:.4f}-{ts[-1]:.4f})",
                        ts[1], 3 * 4 * 800 ** 3, 800 ** 3)
         free(A, B, D)
+    if want("m3ab"):
+        # in-process A/B: sector completion for 3-stream UInt16 / UInt8 ops (knob
+        # pointwise.merge_sectors = 2) on the 800^3 sub-box at x0 = 100, same offsets (aligned
+        # path) and shifted (general path)
+        m = 1024
+        res = {}
+        for fmt, name in ((5, "UInt16"), (4, "UInt8")):
+            A, B, D = alloc((m,) * 3, fmt, seed=1), alloc((m,) * 3, fmt, seed=2), alloc((m,) * 3, fmt)
+            bpv = BPV[fmt]
+            f0, f1 = Vec3i_t(100, 100, 100), Vec3i_t(900, 900, 900)
+            cases = (("SumRange same offsets", lambda: lib.vktHipArithmeticRange(0, D, A, B, f0, f1, o)),
+                     ("SumRange dstOffset x=-97", lambda: lib.vktHipArithmeticRange(0, D, A, B, f0, f1, Vec3i_t(-97, 0, 0))))
+            ab = {}
+            for rnd in range(3):
+                for kv in (1, 2):
+                    lib.vktHipSetTuningKnob(b"pointwise.merge_sectors", kv)
+                    for lab, fn in cases:
+                        ab.setdefault((lab, kv), []).append(timed(fn, R))
+            lib.vktHipSetTuningKnob(b"pointwise.merge_sectors", -1)
+            for lab, fn in cases:
+                for kv in (1, 2):
+                    ts = sorted(ab[(lab, kv)])
+                    report(f"m3ab {lab} 800^3 x0=100 {name} merge_sectors={kv} (median of 3, spread {ts[0]:.4f}-{ts[-1]:.4f})",
+                           ts[1], 3 * bpv * 800 ** 3, 800 ** 3)
+            free(A, B, D)
     if want("decbatch"):
         # in-process A/B of BrickDecompose's batched planning (knob decompose.batch: 1 up to 8
         # batches of brick planes, planning batch k + 1 while the GPU copies batch k; 0 one batch)

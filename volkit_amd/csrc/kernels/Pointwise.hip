@@ -286,7 +286,7 @@ namespace hipk
             // per item: 800^3 sub-box at x0 = 100, SumRange dstOffset -97 1.271 -> 1.232 ms,
             // dstOffset -100 1.204 -> 1.172 ms, profiles/r04/f32m3.jsonl)
             bool const f32 = p.d.bpv == 4 && (ns < 1 || p.s1.bpv == 4) && (ns < 2 || p.s2.bpv == 4);
-            bool merge = (ns <= 1 || f32 || (u8 && rt::knob(rt::Knob::PointwiseMergeSectors) == 2)) && gg.fast &&
+            bool merge = (ns <= 1 || f32 || rt::knob(rt::Knob::PointwiseMergeSectors) == 2) && gg.fast &&
                          rt::knob(rt::Knob::PointwiseMergeSectors) != 0 &&
                          reinterpret_cast<uintptr_t>(p.d.data) % 64 == 0 && dBytes % 64 == 0;
             if (merge && vny > 1)
