@@ -94,8 +94,9 @@ VKTAPI vktError vktHipKernelScopeEnd(vktHipKernelScope scope);
 /* Tuning knobs (process-wide; a negative value restores the default): "pointwise.padded_rows"
  * (1), "pointwise.max_quanta_per_launch" (2^20), "pointwise.general" (1; 0 sends boxes the
  * aligned vector path cannot take to the per-voxel kernel), "pointwise.merge_sectors" (1; 0 stops
- * the general path from completing the 64-B sectors at the row ends of a box by rewriting the
- * destination's own bytes around it), "pointwise.general_32bit" (1; 0 makes the general path use
+ * the pointwise kernels from completing the 64-B sectors at the row ends of a box by rewriting the
+ * destination's own bytes around it; 2 extends it to the aligned path's 2-byte 3-stream ops),
+ * "pointwise.general_32bit" (1; 0 makes the general path use
  * its 64-bit addressing, otherwise taken only for operands beyond 4 GiB from their 16-B aligned base), "pointwise.u8_pairs"
  * (1; 0 keeps UInt8 multi-row boxes on the 8-voxel per-item loop instead of 16-B accesses on a
  * 16-voxel row grid), "histogram.packed16" (1; 0 makes histograms with more bins than one LDS
@@ -131,8 +132,8 @@ VKTAPI vktError vktHipKernelScopeEnd(vktHipKernelScope scope);
  * For tests and in-process A/B measurements; unknown names return
  * vktInvalidValue.
  *
- * Writes outside a range box: FillRange / CopyRange / convert and device-functor TransformRange
- * may rewrite, with the destination's own unchanged bytes, up to one 64-B sector around each row
+ * Writes outside a range box: FillRange / CopyRange / ArithmeticRange / convert and device-functor
+ * TransformRange may rewrite, with the destination's own unchanged bytes, up to one 64-B sector around each row
  * of the box (64-B sector completion; off with "pointwise.merge_sectors" = 0 for
  * the pointwise ops).  Every call runs on the one compute stream, so the library's own calls
  * never race; a caller that writes bytes within 64 B of a box row from another stream or the

@@ -277,16 +277,12 @@ namespace hipk
             int64_t const sv = 64 / bd;
             uint64_t const dBytes = static_cast<uint64_t>(p.d.dims[0]) * static_cast<uint64_t>(p.d.dims[1]) *
                                     static_cast<uint64_t>(p.d.dims[2]) * bd;
-            // (copies, conversions and fills only: a 3-stream op measured slower on this path, an
-            // 800^3 SafeSumRange sub-box of 1024^3 at x0 = 100: 0.589 -> 0.634 ms; the aligned
-            // path completes sectors on its own, above)
-            // (3-stream ops on 1-byte voxels: knob value 2, for the A/B of the 16-voxel items)
-            bool const u8 = p.d.bpv == 1 && (ns < 1 || p.s1.bpv == 1) && (ns < 2 || p.s2.bpv == 1);
-            // 3-stream Float32 ops complete their sectors too (round 4, with one store statement
-            // per item: 800^3 sub-box at x0 = 100, SumRange dstOffset -97 1.271 -> 1.232 ms,
-            // dstOffset -100 1.204 -> 1.172 ms, profiles/r04/f32m3.jsonl)
-            bool const f32 = p.d.bpv == 4 && (ns < 1 || p.s1.bpv == 4) && (ns < 2 || p.s2.bpv == 4);
-            bool merge = (ns <= 1 || f32 || rt::knob(rt::Knob::PointwiseMergeSectors) == 2) && gg.fast &&
+            // The 3-stream ops complete their sectors too (round 4, with one store statement per
+            // item; round 3 had measured them slower here): 800^3 sub-box at x0 = 100, SumRange
+            // dstOffset -97 Float32 1.271 -> 1.232 ms, UInt16 0.684 -> 0.632 ms, UInt8 0.435 ->
+            // 0.426 ms (profiles/r04/f32m3.jsonl, m3ab.jsonl).  (The aligned path's 3-stream
+            // completion, merge3 above, still loses for UInt16: 0.623 -> 0.644 ms.)
+            bool merge = gg.fast &&
                          rt::knob(rt::Knob::PointwiseMergeSectors) != 0 &&
                          reinterpret_cast<uintptr_t>(p.d.data) % 64 == 0 && dBytes % 64 == 0;
             if (merge && vny > 1)
