@@ -385,3 +385,24 @@ def test_brick_decompose_staged_grid_kernel(fmt, dims, brick, neg, pos):
     ref = ob.brick_decompose(ob.Volume(codes, fmt), brick, neg, pos)
     for idx, v in ref.items():
         np.testing.assert_array_equal(got[idx], v.codes, err_msg=f"brick {idx}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fmt", [4, 5, 7])
+@pytest.mark.parametrize("dims,brick,neg,pos", LAYOUTS + [((70, 33, 21), (16, 16, 16), (1, 1, 1), (1, 1, 1)),
+                                                        ((45, 9, 5), (9, 4, 2), (2, 0, 1), (1, 3, 0))])
+def test_brick_decompose_pair_kernel(fmt, dims, brick, neg, pos):
+    """Knob decompose.pair = 1: two x-neighbour bricks of <= 16 KiB per workgroup, the union of
+    their rows staged once into two LDS tiles (odd last bricks alone; bricks of several chunks and
+    other lists keep the other kernels) -- every layout, bit-exact vs the oracle."""
+    rng = np.random.default_rng(fmt * 100 + sum(dims) + 23)
+    codes = rand_codes(rng, fmt, dims[::-1])
+    assert lib.vktHipSetTuningKnob(b"decompose.pair", 1) == 0
+    try:
+        err, got = gpu_decompose(codes, fmt, (0.0, 1.0), brick, neg, pos)
+    finally:
+        assert lib.vktHipSetTuningKnob(b"decompose.pair", -1) == 0
+    assert err == vkt.NoError, vkt.last_error()
+    ref = ob.brick_decompose(ob.Volume(codes, fmt), brick, neg, pos)
+    for idx, v in ref.items():
+        np.testing.assert_array_equal(got[idx], v.codes, err_msg=f"brick {idx}")

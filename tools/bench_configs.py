@@ -979,6 +979,37 @@ def main():
         del V
         ep.device = vkt.ExecutionPolicy.Device_CPU
         vkt.SetThreadExecutionPolicy(ep)
+    if want("decpair"):
+        # in-process A/B: two x-neighbour small bricks per workgroup (knob decompose.pair)
+        import volkit_amd.volkit as vkt
+        ep = vkt.GetThreadExecutionPolicy()
+        ep.device = vkt.ExecutionPolicy.Device_GPU
+        vkt.SetThreadExecutionPolicy(ep)
+        n = 1024
+        V = vkt.StructuredVolume(n, n, n, vkt.DataFormat_UInt16)
+        vkt.Synthesize(V, 77)
+        ab = {}
+        for bs, halo in ((16, (1, 1, 1)), (16, (0, 0, 0)), (32, (1, 1, 1)), (64, (1, 1, 1)), (256, (1, 1, 1))):
+            arr = vkt.Array3D_StructuredVolume()
+            b3, h3 = vkt.Vec3i(bs, bs, bs), vkt.Vec3i(*halo)
+            vkt.BrickDecomposeResize(arr, V, b3, h3, h3)
+            vox = (n // bs) ** 3 * (bs + 2 * halo[0]) ** 3
+            for rnd in range(3):
+                for kv in (1, 0):
+                    lib.vktHipSetTuningKnob(b"decompose.pair", kv)
+                    ab.setdefault((bs, halo, kv, vox, "back-to-back"), []).append(
+                        pipelined(lambda: vkt.BrickDecompose(arr, V, b3, h3, h3), R))
+                    ab.setdefault((bs, halo, kv, vox, "incl. host planning"), []).append(
+                        timed(lambda: vkt.BrickDecompose(arr, V, b3, h3, h3), R))
+            del arr
+        lib.vktHipSetTuningKnob(b"decompose.pair", -1)
+        for (bs, halo, kv, vox, how), ts in sorted(ab.items()):
+            ts.sort()
+            report(f"decpair BrickDecompose 1024^3 UInt16 -> {bs}^3 bricks halo {halo} pair={kv} ({how}; median of "
+                   f"3 rounds, spread {ts[0]:.4f}-{ts[-1]:.4f})", ts[1], 4 * vox, vox)
+        del V
+        ep.device = vkt.ExecutionPolicy.Device_CPU
+        vkt.SetThreadExecutionPolicy(ep)
     if want("u8ab"):
         # in-process A/B of the UInt8 row-edge knobs on the 800^3 sub-box at x0 = 100 (SumRange and
         # CopyRange, same offsets): pointwise.u8_pairs x pointwise.merge_sectors x pointwise.u8_wide

@@ -629,6 +629,225 @@ namespace hipk
         }
     }
 
+    // ---- Two small bricks per workgroup (knob decompose.pair) --------------------------------
+    // Bricks of one 16-KiB chunk or less (16^3 + halo 1 UInt16: 11.7 KB) made one short-lived
+    // workgroup each: 262 144 workgroups whose load, LDS and store phases run back to back, and
+    // whose rows (36 B, 4 source words of which 2 partial) re-read the neighbour's halo words.
+    // Here a workgroup takes two x-neighbours of a brick row: it stages the UNION of their rows
+    // (34 voxels: 5-6 words, the shared columns read once) into two LDS tiles -- a word lands in
+    // each brick whose box it touches -- and stores both bricks: half the workgroups, ~30 % fewer
+    // source words, twice the bytes per workgroup in flight.  An odd last brick of a row pairs
+    // with nothing.  Pair types (pick by the pair index): 0 first, 1 interior, 2 last, 3 first and
+    // last (one pair per row) -- the words per row of the union differ only by clamping.
+    struct PairGeom
+    {
+        FastDiv fwpr[4];
+        FastDiv fPairs;     // pairs per brick row
+    };
+
+    template <int BPV, int W, int NT>
+    __global__ __launch_bounds__(NT) void brickPairKernel(BrickGrid grid, PairGeom pg, uint8_t const* src, int32_t sdx,
+                                                          int32_t sdy, int32_t sdz, int32_t alignedLds)
+    {
+        constexpr int32_t V = 16 / BPV;
+        __shared__ u32x4 tile[2][kBrickChunk];   // 32 KiB
+        uint64_t const spY = static_cast<uint64_t>(sdx), spZ = spY * static_cast<uint64_t>(sdy);
+        uint64_t const srcBytes = spZ * static_cast<uint64_t>(sdz) * BPV;
+        uint32_t const lb = xcdSwizzle(blockIdx.x, gridDim.x);
+        uint32_t const yz = __builtin_amdgcn_readfirstlane(fdiv(lb, pg.fPairs));
+        uint32_t const px = __builtin_amdgcn_readfirstlane(lb - yz * pg.fPairs.d);
+        uint32_t const izu = fdiv(yz, grid.fnby);
+        int32_t const iy = static_cast<int32_t>(yz - izu * grid.fnby.d), iz = static_cast<int32_t>(izu);
+        int32_t const ix0 = 2 * static_cast<int32_t>(px);
+        bool const two = ix0 + 1 < grid.nbx;
+        int const cy = gridClass(iy, grid.nby), cz = gridClass(iz, grid.nbz);
+        int32_t const fy = grid.fy0 + iy * grid.by, fz = grid.fz0 + iz * grid.bz;
+        int32_t const ny = pick3(grid.ny, cy), nz = pick3(grid.nz, cz);
+        FastDiv const fdy = pick3(grid.fdy, cy);
+        // the two bricks' geometry in scalars (arrays indexed by the brick number went to scratch)
+        struct Brick
+        {
+            int32_t fx, nx, nvox, lo, hi;
+            uint8_t* dst;
+        };
+        auto brick = [&](int32_t ix) -> Brick {
+            Brick b;
+            int const cx = gridClass(ix, grid.nbx);
+            b.fx = grid.fx0 + ix * grid.bx;
+            b.nx = pick3(grid.nx, cx);
+            b.nvox = b.nx * ny * nz;
+            b.lo = max(b.fx, 0);
+            b.hi = min(b.fx + b.nx, sdx);
+            b.dst = grid.dst[(static_cast<uint32_t>(iz) * grid.nby + static_cast<uint32_t>(iy)) * grid.nbx + ix];
+            return b;
+        };
+        Brick const B0 = brick(ix0), B1 = brick(two ? ix0 + 1 : ix0);
+        auto pickB = [&](int k) -> Brick const& { return k == 0 ? B0 : B1; };
+        int const nb = two ? 2 : 1;
+        int const type = px == 0 ? (px + 1 == pg.fPairs.d ? 3 : 0) : (px + 1 == pg.fPairs.d ? 2 : 1);
+        // field-wise selects: a select of whole FastDivs became a dynamic index into a scratch copy
+        auto sel4 = [&](uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+            return type == 0 ? a : type == 1 ? b : type == 2 ? c : d;
+        };
+        FastDiv const fwpr{sel4(pg.fwpr[0].d, pg.fwpr[1].d, pg.fwpr[2].d, pg.fwpr[3].d),
+                           sel4(pg.fwpr[0].m, pg.fwpr[1].m, pg.fwpr[2].m, pg.fwpr[3].m),
+                           sel4(pg.fwpr[0].l, pg.fwpr[1].l, pg.fwpr[2].l, pg.fwpr[3].l)};
+        uint32_t const wpr = fwpr.d;
+        int32_t const ulo = B0.lo, uhi = two ? B1.hi : B0.hi;   // the union's in-volume x span
+        int32_t const nRows = ny * nz;
+        uint32_t const total = static_cast<uint32_t>(nRows) * wpr;
+        auto rowBase = [&](int32_t r) -> uint64_t {
+            uint32_t const z = fdiv(static_cast<uint32_t>(r), fdy);
+            uint32_t const y = static_cast<uint32_t>(r) - z * fdy.d;
+            return static_cast<uint64_t>(clampi(fz + static_cast<int32_t>(z), sdz - 1)) * spZ +
+                   static_cast<uint64_t>(clampi(fy + static_cast<int32_t>(y), sdy - 1)) * spY;
+        };
+        struct Word
+        {
+            uint64_t rb;
+            int32_t x0, r;
+            bool live, whole;
+            u32x4 v;
+        };
+        auto locate = [&](uint32_t t, Word& w) {
+            w.live = t < total;
+            uint32_t const tt = w.live ? t : 0u;
+            uint32_t const q = fdiv(tt, fwpr);
+            w.r = static_cast<int32_t>(q);
+            w.rb = rowBase(w.r);
+            uint64_t const startByte =
+                (((w.rb + static_cast<uint64_t>(ulo)) * BPV) & ~uint64_t(15)) + 16ull * (tt - q * wpr);
+            w.live = w.live && startByte < (w.rb + static_cast<uint64_t>(uhi)) * BPV;
+            w.x0 = static_cast<int32_t>(startByte / BPV - w.rb);
+            w.whole = startByte + 16 <= srcBytes;
+            w.v = u32x4{0u, 0u, 0u, 0u};
+            if (w.live && w.whole)
+                w.v = *reinterpret_cast<u32x4 const*>(src + startByte);
+        };
+        auto place = [&](Word const& w) {
+            if (!w.live)
+                return;
+#pragma unroll
+            for (int k = 0; k < 2; ++k)
+            {
+                Brick const& b = pickB(k);
+                if (k >= nb || w.x0 + V <= b.lo || w.x0 >= b.hi)
+                    continue;   // the word holds no voxel of brick k's in-volume span
+                uint8_t* const lds = reinterpret_cast<uint8_t*>(tile[k]);
+                int32_t const li = w.r * b.nx + (w.x0 - b.fx);   // brick-local voxel of the word's first
+                if (w.whole && w.x0 >= b.lo && w.x0 + V <= b.hi)
+                {
+                    if (alignedLds >= 2)
+                        ldsStoreRange(lds, li * BPV, w.v, 0, 16);
+                    else
+                        reinterpret_cast<Unaligned16*>(lds + li * BPV)->v = w.v;
+                }
+                else if (w.whole && alignedLds >= 1)
+                {
+                    int32_t const k0 = max(b.lo - w.x0, 0), k1 = min(b.hi - w.x0, V);
+                    ldsStoreRange(lds, (li + k0) * BPV, w.v, k0 * BPV, k1 * BPV);
+                }
+                else
+                {
+#pragma unroll
+                    for (int j = 0; j < V; ++j)
+                        if (w.x0 + j >= b.lo && w.x0 + j < b.hi)
+                            ldsStoreCode<BPV>(lds, li + j,
+                                              w.whole ? wordCode<BPV>(w.v, j) : loadCode<BPV>(src, w.rb + w.x0 + j));
+                }
+            }
+        };
+        {
+            Word words[W];
+#pragma unroll
+            for (int k = 0; k < W; ++k)
+                locate(threadIdx.x + k * NT, words[k]);
+#pragma unroll
+            for (int k = 0; k < W; ++k)
+                place(words[k]);
+        }
+        for (uint32_t t = threadIdx.x + W * NT; t < total; t += NT)
+        {
+            Word w;
+            locate(t, w);
+            place(w);
+        }
+        // clamped x halo voxels (the border bricks of a row)
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+        {
+            Brick const& b = pickB(k);
+            if (k >= nb || (b.fx >= 0 && b.fx + b.nx <= sdx))
+                continue;
+            uint8_t* const lds = reinterpret_cast<uint8_t*>(tile[k]);
+            for (int32_t r = threadIdx.x; r < nRows; r += NT)
+            {
+                uint64_t const rb = rowBase(r);
+                int32_t const rowL = r * b.nx - b.fx;   // LDS voxel of x = 0
+                if (b.fx < 0)
+                {
+                    uint32_t const c = loadCode<BPV>(src, rb);
+                    for (int32_t x = b.fx; x < min(0, b.fx + b.nx); ++x)
+                        ldsStoreCode<BPV>(lds, rowL + x, c);
+                }
+                if (b.fx + b.nx > sdx)
+                {
+                    uint32_t const c = loadCode<BPV>(src, rb + static_cast<uint64_t>(sdx - 1));
+                    for (int32_t x = max(sdx, b.fx); x < b.fx + b.nx; ++x)
+                        ldsStoreCode<BPV>(lds, rowL + x, c);
+                }
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+        {
+            Brick const& b = pickB(k);
+            if (k >= nb)
+                continue;
+            uint8_t const* const lds = reinterpret_cast<uint8_t const*>(tile[k]);
+#pragma unroll
+            for (int u = 0; u < static_cast<int>(kBrickChunk) / NT; ++u)
+            {
+                int32_t const it = u * NT + static_cast<int32_t>(threadIdx.x);
+                int32_t const lv = it * V;
+                if (lv >= b.nvox)
+                    continue;
+                uint8_t* const out = b.dst + static_cast<uint64_t>(lv) * BPV;
+                if (lv + V <= b.nvox)
+                    __builtin_nontemporal_store(tile[k][it], (__attribute__((address_space(1))) u32x4*)(out));
+                else
+                {
+                    for (int32_t j = 0; j < V && lv + j < b.nvox; ++j)
+                        storeCode<BPV>(out, j, loadCode<BPV>(lds, lv + j));
+                }
+            }
+        }
+    }
+
+    // The pair kernel's per-type words per row (PairGeom), or false when the grid does not take
+    // it: bricks of more than one chunk, a single brick per row.
+    bool pairGeom(BrickGrid const& g, uint32_t bpv, uint32_t maxItems, int32_t sdx, PairGeom& pg, uint32_t& pairs)
+    {
+        if (maxItems > kBrickChunk || g.nbx < 2)
+            return false;
+        uint32_t const pp = static_cast<uint32_t>((g.nbx + 1) / 2);
+        pg.fPairs = makeFastDiv(pp);
+        auto cls = [&](int32_t ix) { return ix == g.nbx - 1 ? 2 : (ix == 0 ? 0 : 1); };
+        auto words = [&](int32_t ix0) -> uint32_t {
+            int32_t const ix1 = ix0 + 1 < g.nbx ? ix0 + 1 : ix0;
+            int32_t const f0 = g.fx0 + ix0 * g.bx, f1 = g.fx0 + ix1 * g.bx;
+            int64_t const span = std::min<int64_t>(f1 + g.nx[cls(ix1)], sdx) - std::max(f0, 0);
+            return span > 0 ? static_cast<uint32_t>((span * bpv + 15) / 16 + 1) : 1u;
+        };
+        pg.fwpr[0] = makeFastDiv(words(0));
+        pg.fwpr[1] = makeFastDiv(pp > 2 ? words(2) : words(0));
+        pg.fwpr[2] = makeFastDiv(words(2 * static_cast<int32_t>(pp - 1)));
+        pg.fwpr[3] = makeFastDiv(words(0));
+        pairs = pp * static_cast<uint32_t>(g.nby) * static_cast<uint32_t>(g.nbz);
+        return true;
+    }
+
     // ---- Gather form of the uniform-grid copy (knob decompose.gather) ------------------------
     // Phase 1 stages the source rows a chunk touches in LDS as ALIGNED 16-B words -- row q of the
     // chunk at q * P bytes, P = the class's source words per row * 16 -- with aligned LDS writes
@@ -1024,9 +1243,16 @@ namespace hipk
         uint32_t const gatherLds =
             useGrid && rt::knob(rt::Knob::DecomposeGather) != 0 ? gatherLdsBytes(grid, bpv) : 0u;
         bool const pipe = useGrid && gatherLds == 0 && !half && rt::knob(rt::Knob::DecomposePipe) != 0;
+        PairGeom pg{};
+        uint32_t pairs = 0;
+        bool const pair = useGrid && gatherLds == 0 && !pipe && !half && rt::knob(rt::Knob::DecomposePair) != 0 &&
+                          pairGeom(grid, bpv, maxItems, source.dimX, pg, pairs);
         auto launch = [&](auto bpvC, auto swC) {
             constexpr int B = decltype(bpvC)::value, W = decltype(swC)::value;
-            if (pipe)
+            if (pair)
+                hipLaunchKernelGGL((brickPairKernel<B, W + 2, kBlock>), dim3(pairs), dim3(kBlock), 0, s, grid, pg,
+                                   source.data, source.dimX, source.dimY, source.dimZ, alignedLds);
+            else if (pipe)
             {
                 // resident workgroups only (a persistent walk), a multiple of 8 (XCD grouping)
                 static unsigned const perCU = [] {

@@ -218,6 +218,7 @@ namespace rt
             {"decompose.batch", 0},
             {"decompose.gather", 0},
             {"decompose.pipe", 0},
+            {"decompose.pair", 0},
         };
         static_assert(sizeof(kKnobs) / sizeof(kKnobs[0]) == static_cast<size_t>(Knob::Count), "knob table");
         std::atomic<int64_t> gKnobs[static_cast<int>(Knob::Count)] = {{kKnobs[0].def}, {kKnobs[1].def},
@@ -233,7 +234,8 @@ namespace rt
                                                                   {kKnobs[20].def}, {kKnobs[21].def},
                                                                   {kKnobs[22].def}, {kKnobs[23].def},
                                                                   {kKnobs[24].def}, {kKnobs[25].def},
-                                                                  {kKnobs[26].def}, {kKnobs[27].def}};
+                                                                  {kKnobs[26].def}, {kKnobs[27].def},
+                                                                  {kKnobs[28].def}};
     } // namespace
 
     int64_t knob(Knob k) { return gKnobs[static_cast<int>(k)].load(std::memory_order_relaxed); }

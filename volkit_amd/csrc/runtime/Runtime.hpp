@@ -102,6 +102,7 @@ namespace rt
         DecomposeBatch,                // 1: BrickDecompose plans / copies in up to 8 batches of brick planes (measured slower: off)
         DecomposeGather,               // 1: uniform brick grids stage source rows and gather items (measured no faster: off)
         DecomposePipe,                 // 1: uniform brick grids on a resident, double-buffered walk (measured slower: off)
+        DecomposePair,                 // 1: two x-neighbour bricks of <= 16 KiB per workgroup (uniform grids)
         Count
     };
     int64_t knob(Knob k);
