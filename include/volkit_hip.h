@@ -128,7 +128,8 @@ VKTAPI vktError vktHipKernelScopeEnd(vktHipKernelScope scope);
  * "decompose.gather" (0; 1 makes uniform brick grids stage source rows in LDS and gather each
  * output item from them instead of scattering source words into the brick layout),
  * "decompose.pipe" (0; 1 runs uniform brick grids on a resident grid that loads chunk k + 1 while
- * it stores chunk k instead of one workgroup per 16-KiB chunk).
+ * it stores chunk k instead of one workgroup per 16-KiB chunk), "decompose.pair" (0; 1 copies
+ * two x-neighbour bricks of at most 16 KiB per workgroup from one staging of their rows' union).
  * For tests and in-process A/B measurements; unknown names return
  * vktInvalidValue.
  *
