@@ -108,7 +108,8 @@ VKTAPI vktError vktHipKernelScopeEnd(vktHipKernelScope scope);
  * (0; 1 / 2 write the row-end / every staged word to LDS as aligned pieces), "decompose.stage_words"
  * (6; 5 or 8 source words in flight per thread), "pointwise.u8_wide" (1; 0 keeps UInt8 boxes of the
  * general path on 8-voxel items), "pointwise.f32_halves" (1; 0 keeps 4-byte padded multi-row boxes
- * on the per-item loop), "pointwise.f32_wide" (0; 1 gives 4-byte general-path boxes 16-B items),
+ * on the per-item loop), "pointwise.f32_wide" (2; 4-byte general-path boxes with 16-B items: 1 for
+ * every op, 2 for the ops of at most one source (copies), 0 for none),
  * "aggregates.codes" (3; bit 0 UInt8, bit 1 UInt16: ComputeAggregates from one pass of code counts
  * instead of the two float passes), "reduce.u8_rows16" (1; UInt8 code counts over range rows on 16-voxel
  * items, row-end bytes subtracted inside the main loop; 2 subtracts them in a row walk after it;

@@ -324,7 +324,8 @@ def test_uint8_wide_general_path(lib, o, sx, fmt):
     knob_name = b"pointwise.u8_wide" if fmt == 4 else b"pointwise.f32_wide"
     from volkit_amd._lib import lib as L
     try:
-        for on, mk in ((1, -1), (1, 2), (0, -1)):
+        # f32_wide 2 (the default): 16-B items for the copies only, 8-voxel items for SafeSum / Diff
+        for on, mk in ((1, -1), (1, 2), (2, -1), (0, -1)):
             assert L.vktHipSetTuningKnob(knob_name, on) == 0
             assert L.vktHipSetTuningKnob(b"pointwise.merge_sectors", mk) == 0
             for dx in (0, 3, 16, 17, 64):
@@ -641,7 +642,7 @@ def test_uint8_long_edge_free_rows_on_the_general_path(lib, o, k):
 
 
 @pytest.mark.parametrize("dword", [1, 0])
-@pytest.mark.parametrize("wide", [0, 1])
+@pytest.mark.parametrize("wide", [0, 1, 2])
 def test_float32_dword_shift(lib, o, dword, wide):
     """4-byte voxels at 4-B aligned addresses shift their windows by whole dwords (knob
     pointwise.dword_shift: the byte-align stage skipped), on the 8-voxel and the 16-B item layouts

@@ -309,8 +309,14 @@ namespace hipk
         {
             uint32_t const B = p.d.bpv;
             bool const same = (ns < 1 || p.s1.bpv == B) && (ns < 2 || p.s2.bpv == B);
+            // Float32 (knob pointwise.f32_wide: 1 every op, 2 ops of at most one source): after the
+            // round-4 single store statement the 16-B items win for copies (800^3 at x0 = 100 ->
+            // dst 0 0.821 -> 0.768 ms, -> dst x0 = 3 0.884 -> 0.803 ms, 1021 x 1024^2 x0 = 3 -> 0
+            // 1.722 -> 1.470 ms) and still lose for SumRange dstOffset -97 (1.239 -> 1.257 ms),
+            // profiles/r04/configs_bench.jsonl f32gen / f32dw
+            int64_t const f32w = rt::knob(rt::Knob::PointwiseF32Wide);
             bool const on = B == 1 ? rt::knob(rt::Knob::PointwiseU8Wide) != 0
-                                   : B == 4 && rt::knob(rt::Knob::PointwiseF32Wide) != 0;
+                                   : B == 4 && (f32w == 1 || (f32w == 2 && ns < 2));
             if (gg.fast && same && on)
             {
                 int64_t const V = 16 / B, sv = 64 / B;

@@ -204,7 +204,7 @@ namespace rt
             {"decompose.stage_words", 6},
             {"pointwise.u8_wide", 1},
             {"pointwise.f32_halves", 1},
-            {"pointwise.f32_wide", 0},
+            {"pointwise.f32_wide", 2},
             {"aggregates.codes", 3},
             {"reduce.u8_rows16", 1},
             {"decompose.grid", 1},

@@ -88,7 +88,7 @@ namespace rt
         DecomposeStageWords,           // source words per thread in flight in the staged copy (5, 6, 8)
         PointwiseU8Wide,               // 0: UInt8 general-path boxes keep 8-voxel items
         PointwiseF32Halves,            // 0: padded 4-byte rows keep the per-item loop
-        PointwiseF32Wide,              // 1: 4-byte general-path boxes use 16-B items (measured neutral; off)
+        PointwiseF32Wide,              // 4-byte general-path boxes with 16-B items: 1 every op, 2 one-source ops
         AggregatesCodes,               // bit 0 UInt8, bit 1 UInt16: ComputeAggregates from one pass of code counts
         ReduceU8Rows16,                // UInt8 code counts over range rows with 16-voxel items (codeCountsU8RowsKernel)
         DecomposeGrid,                 // 0: uniform brick grids keep the per-brick descriptor table
