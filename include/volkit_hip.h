@@ -124,7 +124,8 @@ VKTAPI vktError vktHipKernelScopeEnd(vktHipKernelScope scope);
  * under other mappings and Float32 from one pass of floating-point moments -- both instead of
  * "aggregates.codes" / the two float passes), "aggregates.moments_pipe" (1; integer-moments kernel
  * variant: 0 one register buffer of 4 items per lane and wave-step, 1 two buffers of 4 (the next
- * step's loads in flight during this step's arithmetic), 2 two of 8, 3 one of 8, 4 two of 2),
+ * step's loads in flight during this step's arithmetic), 2 two of 8, 3 one of 8, 4 two of 2, 5 as 1
+ * bound to 7 waves per SIMD),
  * "decompose.batch" (0; 1 plans and copies BrickDecompose in up to 8 batches of brick planes),
  * "decompose.gather" (0; 1 makes uniform brick grids stage source rows in LDS and gather each
  * output item from them instead of scattering source words into the brick layout),

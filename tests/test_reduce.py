@@ -634,6 +634,25 @@ def test_u8_histogram_over_rows_from_code_counts(rows16):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
+def test_aggregates_uint16_moment_variants(variant):
+    """Every integer-moments kernel variant (knob aggregates.moments_pipe: buffers x items per lane,
+    5 = the two-buffer kernel bound to 7 waves per SIMD) against the oracle over spans, padded
+    rows and extremes first occurring late in a lane's walk."""
+    rng = np.random.default_rng(77 + variant)
+    late = rng.integers(100, 60000, (16, 64, 1024), dtype=np.uint16)
+    late[12, 5, 700] = late[14, 0, 3] = 3
+    late[15, 63, 1000] = late[13, 9, 9] = 65000
+    assert lib.vktHipSetTuningKnob(b"aggregates.moments_pipe", variant) == 0
+    try:
+        for first, last in (((0, 0, 0), (1024, 64, 16)), ((3, 1, 0), (1021, 64, 16)), ((9, 5, 3), (1001, 60, 14))):
+            got = gpu_aggregates(late, 5, 0.0, 1.0, first, last)
+            check_aggregates(got, late, 5, (0.0, 1.0), first, last, f"variant={variant} {first}->{last}")
+    finally:
+        lib.vktHipSetTuningKnob(b"aggregates.moments_pipe", -1)
+
+
+@pytest.mark.gpu
 def test_aggregates_uint16_moments():
     """UInt16 ComputeAggregates under the unit mapping from one pass of exact integer moments
     (knob aggregates.moments) against the oracle and against the code-count path

@@ -1469,8 +1469,11 @@ namespace hipk
         return pipe ? 4 : u <= 4 ? (contig ? 8 : 6) : (contig ? 6 : 4);
     }
 
-    template <bool CONTIG, int U, bool PIPE>
-    __global__ __launch_bounds__(kBlock, momentWaves(CONTIG, U, PIPE)) void aggregatesMomentsU16Kernel(FastHistArgs h, MomentPartialU16* partials)
+    // WAVES: the launch bound's waves per SIMD (0: momentWaves).  The two-buffer 4-item span kernel
+    // takes 76 VGPRs unbounded (6 waves); bound to 7 it fits 72 with 12 B spilled outside the walk
+    // (bound to 8, 64 VGPRs, the spills land inside it).
+    template <bool CONTIG, int U, bool PIPE, int WAVES = 0>
+    __global__ __launch_bounds__(kBlock, WAVES ? WAVES : momentWaves(CONTIG, U, PIPE)) void aggregatesMomentsU16Kernel(FastHistArgs h, MomentPartialU16* partials)
     {
         uint32_t const lane = threadIdx.x & 63;
         MomentPartialU16 p;
@@ -2666,7 +2669,8 @@ namespace hipk
 
     // The integer-moments kernel variant (knob aggregates.moments_pipe: 0 one buffer, 4 items per
     // lane and step; 1 two buffers (next step's loads in flight during this step's arithmetic),
-    // 4 items; 2 two buffers, 8 items; 3 one buffer, 8 items; 4 two buffers, 2 items) and its grid: as many workgroups as the variant keeps
+    // 4 items; 2 two buffers, 8 items; 3 one buffer, 8 items; 4 two buffers, 2 items; 5 as 1, bound to
+    // 7 waves per SIMD for spans) and its grid: as many workgroups as the variant keeps
     // resident on every CU (hipOccupancyMaxActiveBlocksPerMultiprocessor, at most 8) -- a grid-
     // stride walk with more would leave a second partial wave of workgroups running alone.
     using MomentKernelU16 = void (*)(FastHistArgs, MomentPartialU16*);
@@ -2680,6 +2684,7 @@ namespace hipk
         case 2: itemsPerLane = 8; return aggregatesMomentsU16Kernel<CONTIG, 8, true>;
         case 3: itemsPerLane = 8; return aggregatesMomentsU16Kernel<CONTIG, 8, false>;
         case 4: itemsPerLane = 2; return aggregatesMomentsU16Kernel<CONTIG, 2, true>;
+        case 5: itemsPerLane = 4; return aggregatesMomentsU16Kernel<CONTIG, 4, true, CONTIG ? 7 : 0>;
         default: itemsPerLane = 4; return aggregatesMomentsU16Kernel<CONTIG, 4, false>;
         }
     }
