@@ -504,9 +504,11 @@ def migrate_rates(vkt, lib, edge, reps=3):
     thread policy (reference include/cpp/vkt/ManagedBuffer.hpp:168-198 -> runtime/Memory.cpp
     MigrateBuffer: allocate on the new side, one copy on the side copy stream, free the old side).
     Pageable host buffers (malloc, the reference's behaviour) and pinned ones
-    (vktHipSetPinnedHostAllocation).  H2D: the host volume (pages written) to HBM; D2H: back into a
-    FRESH host allocation (its pages are first touched by the copy -- part of the flow's cost).
-    Best of `reps` round trips; GB/s of the volume's bytes."""
+    (vktHipSetPinnedHostAllocation).  H2D: the host volume (pages written) to HBM; D2H: back into
+    the host buffer the H2D released (the library keeps it, pages resident, for the migration
+    back), and `D2H_fresh_*`: one D2H after vktHipReleaseCachedMemory, into a FRESH host
+    allocation whose pages the library faults in first.  Best of `reps` round trips; GB/s of the
+    volume's bytes."""
     import numpy as np
     cpu, gpu = vkt.ExecutionPolicy.Device_CPU, vkt.ExecutionPolicy.Device_GPU
 
@@ -536,12 +538,22 @@ def migrate_rates(vkt, lib, edge, reps=3):
                 t0 = time.perf_counter()
                 v.migrate()
                 d2h.append(time.perf_counter() - t0)
+            # one more round trip with the host caches emptied before the D2H
+            policy(gpu)
+            v.migrate()
+            if lib.vktHipSynchronize() != 0 or lib.vktHipReleaseCachedMemory(None) != 0:
+                raise RuntimeError(vkt.last_error())
+            policy(cpu)
+            t0 = time.perf_counter()
+            v.migrate()
+            d2h_fresh = time.perf_counter() - t0
             if v.getValue(3, 2, 1) != 0x1234 / 65536.0:
                 raise RuntimeError("migrate round trip changed the data")
             del v
             key = "pinned" if pinned else "pageable"
             res[key] = {"H2D_GBs": round(nbytes / min(h2d) / 1e9, 2), "D2H_GBs": round(nbytes / min(d2h) / 1e9, 2),
-                        "H2D_ms": round(min(h2d) * 1e3, 2), "D2H_ms": round(min(d2h) * 1e3, 2)}
+                        "H2D_ms": round(min(h2d) * 1e3, 2), "D2H_ms": round(min(d2h) * 1e3, 2),
+                        "D2H_fresh_GBs": round(nbytes / d2h_fresh / 1e9, 2), "D2H_fresh_ms": round(d2h_fresh * 1e3, 2)}
     finally:
         lib.vktHipSetPinnedHostAllocation(0)
         policy(gpu)

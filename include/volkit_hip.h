@@ -155,7 +155,11 @@ VKTAPI vktError vktHipFree(void* ptr);
  * sized for a group of like buffers -- four times the request, at least 64 MiB -- and returned to
  * HIP as soon as their last buffer is freed).  This call waits for the library's streams, then
  * returns every chunk that holds no live buffer to HIP; *releasedBytes (may be NULL) receives the
- * bytes released.  A device allocation that fails does the same and retries once. */
+ * bytes released.  A device allocation that fails does the same and retries once.  It also frees
+ * the host buffers the migrations keep: pinned buffers of >= 64 MiB freed by the caller (at most
+ * 16 GiB, reused by a pinned allocation of the same size) and pageable buffers of >= 64 MiB a
+ * migration to the GPU released (at most min(8 GiB, physical memory / 8), the destination of the
+ * next migration back of the same size: its pages already resident). */
 VKTAPI vktError vktHipReleaseCachedMemory(size_t* releasedBytes);
 VKTAPI vktError vktHipMemcpy(void* dst, void const* src, size_t size, vktCopyKind ck);
 /* Host buffers allocated under the CPU policy from now on are page-locked (hipHostMalloc),

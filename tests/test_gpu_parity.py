@@ -489,11 +489,12 @@ def test_resample_chain_downsampling_unstaged_rows(g, o, dfmt):
 @pytest.mark.parametrize("pinned", [0, 1])
 def test_large_migrations_keep_the_data(g, pinned):
     """Buffers of >= 64 MiB take the migration fast paths (runtime/Memory.cpp MigrateBuffer): a
-    fresh pageable destination faulted in by the host threads before the D2H copy, the old pageable
-    buffer freed on a background thread after the H2D copy, pinned buffers kept for reuse by the
-    next migration of the same size.  Three round trips of a 128 MiB UInt16 volume with a GPU op in
-    between: the data arrives intact each way; vktHipReleaseCachedMemory then returns the cached
-    pinned buffer."""
+    pageable buffer released by the H2D copy kept (pages resident) as the destination of the next
+    D2H of the same size, pinned buffers kept for reuse by the next migration of the same size.
+    Three round trips of a 128 MiB UInt16 volume with a GPU op in between: the data arrives intact
+    each way (a reused destination still holds the previous round's bytes until the copy);
+    vktHipReleaseCachedMemory then returns the cached pinned buffer, or the pageable one a last
+    H2D released."""
     import ctypes as C
     from volkit_amd._lib import lib
     vkt = g.vkt
@@ -510,10 +511,12 @@ def test_large_migrations_keep_the_data(g, pinned):
             got = v.to_numpy()
             codes[2:4, 3 + r:5 + r, 7:9] = 65535
             np.testing.assert_array_equal(got, codes, err_msg=f"round {r}")
+        if not pinned:
+            g._gpu()
+            v.migrate()   # its pageable host buffer goes to the cache
         del v
         released = C.c_size_t(0)
         assert lib.vktHipReleaseCachedMemory(C.byref(released)) == 0
-        if pinned:
-            assert released.value >= codes.nbytes
+        assert released.value >= codes.nbytes
     finally:
         lib.vktHipSetPinnedHostAllocation(0)
