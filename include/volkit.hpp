@@ -128,6 +128,10 @@ namespace vkt
         VKTAPI void FreeOn(void* data, ExecutionPolicy const& owner);
         VKTAPI void* AllocateOn(std::size_t bytes, ExecutionPolicy const& owner);
         VKTAPI void CopyOn(void* dst, void const* src, std::size_t bytes, ExecutionPolicy const& owner);
+        // Copies between buffers owned by (possibly) different devices -- a source whose
+        // migration failed is still in its old address space.
+        VKTAPI void CopyBetween(void* dst, ExecutionPolicy const& dstOwner, void const* src,
+                                ExecutionPolicy const& srcOwner, std::size_t bytes);
     }
 
     //--- ManagedBuffer<T> (reference include/cpp/vkt/ManagedBuffer.hpp:21-276) -----------
@@ -249,7 +253,7 @@ namespace vkt
             rhs.migrate();
             std::size_t n = (size_ < rhs.size_ ? size_ : rhs.size_) * sizeof(T);
             if (n > 0)
-                detail::CopyOn(data_, rhs.data_, n, lastAllocationPolicy_);
+                detail::CopyBetween(data_, lastAllocationPolicy_, rhs.data_, rhs.lastAllocationPolicy_, n);
         }
 
         T* data_ = nullptr;
@@ -303,7 +307,13 @@ namespace vkt
 
         //! getData() for a caller that runs under `ep` (its thread's policy), without looking the
         //! policy up when the bytes already live there (per-brick walks of BrickDecompose).
-        uint8_t* getDataFor(ExecutionPolicy const& ep) { return residentOn(ep) ? data_ : getData(); }
+        //! nullptr when the bytes could not be migrated there (they stay where they were).
+        uint8_t* getDataFor(ExecutionPolicy const& ep)
+        {
+            if (!residentOn(ep))
+                (void)getData();
+            return residentOn(ep) ? data_ : nullptr;
+        }
 
         Box3f getDomainBounds() const;
         Box3f getObjectBounds() const;

@@ -158,6 +158,10 @@ VKTAPI void vktStructuredVolumeGetBytes(vktStructuredVolume volume, int32_t x, i
 VKTAPI size_t vktStructuredVolumeGetSizeInBytes(vktStructuredVolume volume);
 VKTAPI vktResourceHandle vktStructuredVolumeGetResourceHandle(vktStructuredVolume volume);
 VKTAPI void vktStructuredVolumeMigrate(vktStructuredVolume volume);
+/* extension: migrate() with its outcome -- vktInvalidValue when the bytes could not be moved to
+ * the thread's device (allocation or copy failure; vktHipGetLastErrorString says which).  They
+ * then stay where they were, intact, and the next access tries again. */
+VKTAPI vktError vktStructuredVolumeMigrateChecked(vktStructuredVolume volume);
 
 /* ---- Fill.h (reference include/c/vkt/Fill.h:16-43; HV overloads out of scope) */
 VKTAPI vktError vktFillSV(vktStructuredVolume volume, float value);

@@ -148,7 +148,13 @@ VKTAPI vktError vktHipReportError(const char* message);
 /* ---- memory: replaces Allocate_cuda/Free_cuda/MemsetRange_cuda
  *      (reference src/vkt/Memory_cuda.hpp:16-31) and the cudaMemcpy of src/vkt/Memory.cpp:40-75
  * Device buffers are blocks of pooled / arena chunks (knobs "memory.pool", "memory.arena"): release every pointer
- * from vktHipAllocate / vktAllocate with vktHipFree / vktFree, never with hipFree. */
+ * from vktHipAllocate / vktAllocate with vktHipFree / vktFree, never with hipFree.
+ * Ordering of a free: a block freed through vktHipFree / vktFree / vkt::Free is handed out again
+ * only after a device synchronisation (hipFree's guarantee: work the caller queued on streams
+ * of its own is finished).  Buffers the library frees itself (volumes, bricks, lookup tables,
+ * scratch) wait only for the library's compute and copy streams, which are blocking streams
+ * (ordered with the legacy NULL stream): a caller that used a volume's getData() pointer on a
+ * non-blocking stream of its own synchronises that stream before destroying the volume. */
 VKTAPI vktError vktHipAllocate(void** ptr, size_t size);
 VKTAPI vktError vktHipFree(void* ptr);
 /* The library caches device memory (pool chunks of small buffers; arena chunks of large ones,

@@ -520,3 +520,62 @@ def test_large_migrations_keep_the_data(g, pinned):
         assert released.value >= codes.nbytes
     finally:
         lib.vktHipSetPinnedHostAllocation(0)
+
+
+@pytest.mark.parametrize("shape", [(16, 24, 40), (256, 512, 512)])
+def test_failed_migration_keeps_the_data(g, shape):
+    """A host -> HBM migration whose device allocation fails (test knob memory.fail_next_alloc)
+    keeps the only copy of the data: the buffer stays in host memory (same pointer), the
+    migration and the algorithm that asked for it return InvalidValue naming the failure, and
+    after the knob is spent the next migration succeeds and the op runs bit-exactly.  The
+    128 MiB case takes the large-buffer path whose source the reference-style migrate freed
+    (runtime/Memory.cpp MigrateBuffer; reference include/cpp/vkt/ManagedBuffer.hpp:168-198)."""
+    from volkit_amd._lib import lib
+    vkt = g.vkt
+    rng = np.random.default_rng(41 + shape[0])
+    codes = rng.integers(0, 65536, shape, dtype=np.uint16)
+    v = g.volume(codes, 5, (0.0, 1.0))
+    host_ptr = v.getData()
+    try:
+        assert lib.vktHipSetTuningKnob(b"memory.fail_next_alloc", 2) == 0
+        g._gpu()
+        assert v.migrateChecked() == vkt.InvalidValue
+        assert "allocation failed" in vkt.last_error()
+        assert v.getData() == host_ptr          # (retries and fails again) still the host buffer
+        assert lib.vktHipSetTuningKnob(b"memory.fail_next_alloc", 1) == 0
+        assert vkt.FillRange(v, 1, 1, 1, 3, 3, 3, 1.0) == vkt.InvalidValue
+        assert "FillRange_hip" in vkt.last_error() and "allocation failed" in vkt.last_error()
+        g._cpu()
+        assert v.getData() == host_ptr
+        np.testing.assert_array_equal(v.to_numpy(), codes)
+        # knob spent: the next migration and op succeed
+        g._gpu()
+        assert v.migrateChecked() == vkt.NoError
+        assert v.getData() != host_ptr
+        assert vkt.FillRange(v, 1, 1, 1, 3, 3, 3, 1.0 - 1.0 / 65536) == vkt.NoError
+        g._cpu()
+        codes[1:3, 1:3, 1:3] = 65535
+        np.testing.assert_array_equal(v.to_numpy(), codes)
+    finally:
+        lib.vktHipSetTuningKnob(b"memory.fail_next_alloc", 0)
+        g._cpu()
+
+
+def test_failed_migration_in_a_copy_constructor(g):
+    """CreateCopy under the GPU policy of a host volume whose migration fails: the copy still
+    gets the source's bytes (copied across address spaces, detail::CopyBetween), the source keeps
+    them."""
+    from volkit_amd._lib import lib
+    vkt = g.vkt
+    codes = np.arange(4 * 6 * 10, dtype=np.uint8).reshape(4, 6, 10)
+    v = g.volume(codes, 4, (0.0, 1.0))
+    try:
+        assert lib.vktHipSetTuningKnob(b"memory.fail_next_alloc", 1) == 0
+        g._gpu()
+        w = vkt.StructuredVolume.CreateCopy(v)   # v's migration fails, w's allocation succeeds
+        g._cpu()
+        np.testing.assert_array_equal(v.to_numpy(), codes)
+        np.testing.assert_array_equal(w.to_numpy(), codes)
+    finally:
+        lib.vktHipSetTuningKnob(b"memory.fail_next_alloc", 0)
+        g._cpu()

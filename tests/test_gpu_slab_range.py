@@ -125,6 +125,39 @@ def test_local_halo_exchange_linear_chain(L, nslabs, sdims, ddims, transport):
         assert same_codes(D.read(), ref.codes[d0:d1], 7), f"slab {r}: resample differs from the whole volume"
 
 
+def test_peer_halo_exchange_across_two_devices_waits_for_the_compute_stream(L):
+    """vktHipSlabExchangeHaloPeer with slabs on devices 0 and 1: the slab on device 1 receives
+    its halo plane by a peer copy on a stream of device 1, which must first wait for the work
+    queued on the library's compute stream -- here a FillRange of the source slab (device 0)
+    enqueued right before the exchange, with no host synchronisation in between.  Source depth
+    15 -> dst 30 over two ranks: slab 1 (dst planes [15, 30)) reads source plane 7, owned by
+    slab 0; slab 0 reads planes 8 and 9 from slab 1.  Needs two GPUs (skipped on the one-GPU pool)."""
+    import torch
+    from volkit_amd import _lib
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two GPUs")
+    x, y = 64, 32
+    plane = x * y * 4
+    t0 = torch.zeros(10 * plane, dtype=torch.uint8, device="cuda:0")   # global planes [0, 10)
+    t1 = torch.zeros(8 * plane, dtype=torch.uint8, device="cuda:1")   # global planes [7, 15)
+    t1.view(torch.float32).fill_(0.25)
+    torch.cuda.synchronize(1)
+    torch.cuda.synchronize(0)
+    v0 = _lib.HipVolumeView_t(t0.data_ptr(), x, y, 10, 7, 0.0, 1.0)
+    v1 = _lib.HipVolumeView_t(t1.data_ptr(), x, y, 8, 7, 0.0, 1.0)
+    assert L.vktHipFillRange(v0, _lib.Vec3i_t(0, 0, 0), _lib.Vec3i_t(x, y, 8), C.c_float(0.75)) == 0, err(L)
+    views = (_lib.HipVolumeView_t * 2)(v0, v1)
+    z0s = (C.c_int32 * 2)(0, 7)
+    devs = (C.c_int32 * 2)(0, 1)
+    assert L.vktHipSlabExchangeHaloPeer(2, views, z0s, devs, 30, 15, 1, 1) == 0, err(L)
+    torch.cuda.synchronize(0)
+    torch.cuda.synchronize(1)
+    g0 = t0.cpu().numpy().view(np.float32).reshape(10, y, x)
+    g1 = t1.cpu().numpy().view(np.float32).reshape(8, y, x)
+    assert (g0[:8] == 0.75).all() and (g0[8:] == 0.25).all()
+    assert (g1[0] == 0.75).all() and (g1[1:] == 0.25).all()
+
+
 def test_local_halo_exchange_rejects_short_buffers(L):
     import torch
     from volkit_amd import _lib

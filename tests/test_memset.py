@@ -298,3 +298,70 @@ def test_arena_exhaustion_coalesces_freed_neighbours():
             assert lib.vktHipFree(C.c_void_p(b)) == 0
     finally:
         lib.vktHipSetTuningKnob(b"memory.arena_chunk_mib", -1)
+
+
+@pytest.mark.gpu
+def test_arena_chunk_release_then_fresh_allocation_at_that_va():
+    """DESIGN.md §6 (round-4 VMM probe fault): the library carves three volumes from an arena
+    chunk, runs SumRange and frees them (the chunk goes back to HIP); a plain hipMalloc outside
+    the library then takes the released range (HIP hands the freed virtual addresses out again)
+    and the library runs Synthesize + SumRange on three volumes in it, and on new arena volumes
+    while it lives.  Every return code is checked and the device synchronised after each phase
+    (a fault of any stream shows there); the SumRange bytes equal those of the first run.  A
+    library pointer kept into the released chunk would alias the new buffer and change them."""
+    import torch
+    from volkit_amd._lib import lib, last_error, HipVolumeView_t, Vec3i_t
+
+    hip = C.CDLL("libamdhip64.so")
+    torch.cuda.set_device(0)
+
+    def dev_sync(what):
+        assert hip.hipDeviceSynchronize() == 0, f"device sync after {what}"
+
+    n = (256, 256, 512)                      # UInt16: 64 MiB per volume
+    nb = 2 * n[0] * n[1] * n[2]
+    o, last = Vec3i_t(0, 0, 0), Vec3i_t(*n)
+
+    def sumrange(ptrs, seeds=(11, 12)):
+        A, B, D = (HipVolumeView_t(p, n[0], n[1], n[2], 5, 0.0, 1.0) for p in ptrs)
+        assert lib.vktHipSynthesize(A, C.c_uint64(seeds[0])) == 0, last_error()
+        assert lib.vktHipSynthesize(B, C.c_uint64(seeds[1])) == 0, last_error()
+        for _ in range(3):
+            assert lib.vktHipArithmeticRange(0, D, A, B, o, last, o) == 0, last_error()
+        out = np.empty(nb, np.uint8)
+        assert lib.vktHipMemcpy(out.ctypes.data, C.c_void_p(ptrs[2]), nb, 2) == 0, last_error()
+        return out
+
+    def lib_alloc3():
+        ptrs = []
+        for _ in range(3):
+            p = C.c_void_p()
+            assert lib.vktHipAllocate(C.byref(p), nb) == 0, last_error()
+            ptrs.append(p.value)
+        return ptrs
+
+    lib.vktHipReleaseCachedMemory(None)
+    assert lib.vktHipSetTuningKnob(b"memory.arena_chunk_mib", 256) == 0
+    try:
+        ptrs = lib_alloc3()                          # one fresh 256-MiB chunk
+        base = min(ptrs)
+        want = sumrange(ptrs)
+        for p in ptrs:
+            assert lib.vktHipFree(C.c_void_p(p)) == 0, last_error()   # the last free returns the chunk
+        dev_sync("arena release")
+        raw = C.c_void_p()
+        assert hip.hipMalloc(C.byref(raw), C.c_size_t(256 << 20)) == 0
+        print(f"released chunk at {base:#x}, hipMalloc at {raw.value:#x} (VA reused: {raw.value == base})")
+        try:
+            got = sumrange([raw.value, raw.value + nb, raw.value + 2 * nb])
+            fresh = lib_alloc3()                     # a new arena chunk while the buffer lives
+            got2 = sumrange(fresh)
+            for p in fresh:
+                assert lib.vktHipFree(C.c_void_p(p)) == 0, last_error()
+            dev_sync("SumRange on the reused range")
+        finally:
+            assert hip.hipFree(raw) == 0
+        dev_sync("hipFree")
+        assert np.array_equal(got, want) and np.array_equal(got2, want)
+    finally:
+        lib.vktHipSetTuningKnob(b"memory.arena_chunk_mib", 0)

@@ -97,7 +97,18 @@ def resample_bytes(sdims, ddims, bs, bd, every_row=False):
     return bs * sx * rows + bd * ddims[0] * ddims[1] * ddims[2]
 
 
+def two_float_passes(on):
+    """ComputeAggregates in the reference's two passes (mean, then variance) for every format:
+    no code counts (knob aggregates.codes) and no one-pass moments (knob aggregates.moments)."""
+    for k in (b"aggregates.codes", b"aggregates.moments"):
+        lib.vktHipSetTuningKnob(k, 0 if on else -1)
+
+
 def report(name, ms, nbytes, voxels):
+    # a row above the HBM peak means the bytes credited are not the bytes the call moved (e.g. a
+    # knob that no longer selects the path the label names): fail instead of committing it
+    if nbytes / ms / 1e6 / 8000 > 1.0:
+        raise AssertionError(f"{name}: {nbytes / ms / 1e6:.0f} GB/s is above 8 TB/s -- bytes or label wrong")
     print(json.dumps({"case": name, "ms": round(ms, 4), "GB/s": round(nbytes / ms / 1e6, 1),
                       "frac_of_8TBs": round(nbytes / ms / 1e6 / 8000, 4),
                       "Gvox/s": round(voxels / ms / 1e6, 2)}), flush=True)
@@ -764,9 +775,9 @@ def main():
         ms = timed(lambda: lib.vktHipHistogramRange(V, u0, u1, bins, 256, 0), R)
         report("reduce Histogram UInt16 800^3 sub-box of 1024^3 at x0=100, 256 bins", ms, 2 * 800 ** 3, 800 ** 3)
         agg0 = _lib.Aggregates_t()
-        lib.vktHipSetTuningKnob(b"aggregates.codes", 1)   # UInt16: the two float passes
+        two_float_passes(True)   # UInt16: the two float passes
         ms = timed(lambda: lib.vktHipAggregatesRange(V, u0, u1, C.byref(agg0)), R)
-        lib.vktHipSetTuningKnob(b"aggregates.codes", -1)
+        two_float_passes(False)
         report("reduce Aggregates UInt16 800^3 sub-box of 1024^3 at x0=100 (2 passes)", ms, 2 * 2 * 800 ** 3, 800 ** 3)
         for fmt, bpv, name in ((4, 1, "UInt8"), (7, 4, "Float32")):
             W = alloc((n,) * 3, fmt, seed=12 if fmt != 7 else None)
@@ -779,7 +790,12 @@ def main():
             if fmt == 4:   # one pass of code counts (knob aggregates.codes)
                 report(f"reduce Aggregates 1024^3 {name} (1 pass of code counts, incl. D2H of the result)", ms,
                        bpv * n ** 3, n ** 3)
-            else:
+            else:          # one pass of float moments (knob aggregates.moments bit 1)
+                report(f"reduce Aggregates 1024^3 {name} (1 pass of float moments, incl. D2H of the result)", ms,
+                       bpv * n ** 3, n ** 3)
+                two_float_passes(True)
+                ms = timed(lambda: lib.vktHipAggregatesRange(W, o, last, C.byref(aggW)), R)
+                two_float_passes(False)
                 report(f"reduce Aggregates 1024^3 {name} (2 passes, incl. D2H of the result)", ms, 2 * bpv * n ** 3,
                        n ** 3)
             free(W)
@@ -791,9 +807,9 @@ def main():
             ms = timed(lambda: lib.vktHipHistogramRange(Vc, o, last, bins, nb, 0), R)
             report(f"reduce Histogram 1024^3 UInt16 {nb} bins, constant volume", ms, 2 * n ** 3, n ** 3)
         agg = _lib.Aggregates_t()
-        lib.vktHipSetTuningKnob(b"aggregates.codes", 1)   # UInt16: the two float passes
+        two_float_passes(True)   # UInt16: the two float passes
         ms = timed(lambda: lib.vktHipAggregatesRange(V, o, last, C.byref(agg)), R)
-        lib.vktHipSetTuningKnob(b"aggregates.codes", -1)
+        two_float_passes(False)
         report("reduce Aggregates 1024^3 UInt16 (2 passes, incl. D2H of the result)", ms, 2 * 2 * n ** 3, n ** 3)
         free(V, Vc)
         lib.vktHipFree(bins)
@@ -834,6 +850,7 @@ def main():
         lib.vktHipFree(hb)
         free(W)
         V = alloc((n,) * 3, 5, seed=11)
+        lib.vktHipSetTuningKnob(b"aggregates.moments", 0)   # (moments would take both cases)
         for k in (3, 1):
             lib.vktHipSetTuningKnob(b"aggregates.codes", k)
             passes = 1 if k & 2 else 2
@@ -847,6 +864,7 @@ def main():
             report(f"aggcodes Aggregates UInt16 800^3 sub-box x 0..800 [codes={k}, {passes} pass(es)]", ms,
                    passes * 2 * 800 ** 3, 800 ** 3)
         lib.vktHipSetTuningKnob(b"aggregates.codes", -1)
+        lib.vktHipSetTuningKnob(b"aggregates.moments", -1)
         free(V)
     if want("moments"):
         # UInt16 ComputeAggregates under the unit mapping: one pass of integer moments (knob

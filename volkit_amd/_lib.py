@@ -197,6 +197,7 @@ SIGNATURES = {
     "vktStructuredVolumeGetSizeInBytes": (C.c_size_t, [c_vol]),
     "vktStructuredVolumeGetResourceHandle": (u32, [c_vol]),
     "vktStructuredVolumeMigrate": (None, [c_vol]),
+    "vktStructuredVolumeMigrateChecked": (c_err, [c_vol]),
     # Fill.h / Copy.h
     "vktFillSV": (c_err, [c_vol, f32]),
     "vktFillRangeSV": (c_err, [c_vol, i32, i32, i32, i32, i32, i32, f32]),

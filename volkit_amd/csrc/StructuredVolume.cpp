@@ -17,7 +17,14 @@ namespace vkt
 {
     namespace
     {
-        bool policyIsGpu() { return GetThreadExecutionPolicy().device == ExecutionPolicy::Device::GPU; }
+        // where the bytes are (after migrate(): the thread's device, unless that migration failed
+        // and left them where they were)
+        bool residentOnGpu(ManagedBuffer<uint8_t> const& b)
+        {
+            ExecutionPolicy gpu;
+            gpu.device = ExecutionPolicy::Device::GPU;
+            return b.residentOn(gpu);
+        }
     }
 
     StructuredVolume::StructuredVolume()
@@ -117,7 +124,7 @@ namespace vkt
         migrate();
         std::size_t off = linearIndex(x, y, z);
         uint8_t bpv = getBytesPerVoxel();
-        if (policyIsGpu())
+        if (residentOnGpu(*this))
             (void)detail::memcpyHip(out, data_ + off, bpv, CopyKind::DeviceToHost);
         else
             for (uint8_t i = 0; i < bpv; ++i)
@@ -129,7 +136,7 @@ namespace vkt
         migrate();
         std::size_t off = linearIndex(x, y, z);
         uint8_t bpv = getBytesPerVoxel();
-        if (policyIsGpu())
+        if (residentOnGpu(*this))
             (void)detail::memcpyHip(data_ + off, in, bpv, CopyKind::HostToDevice);
         else
             for (uint8_t i = 0; i < bpv; ++i)
@@ -348,6 +355,18 @@ size_t vktStructuredVolumeGetSizeInBytes(vktStructuredVolume v) { return v->volu
 vktResourceHandle vktStructuredVolumeGetResourceHandle(vktStructuredVolume v) { return v->volume.getResourceHandle(); }
 
 void vktStructuredVolumeMigrate(vktStructuredVolume v) { v->volume.migrate(); }
+
+vktError vktStructuredVolumeMigrateChecked(vktStructuredVolume v)
+{
+    if (v == nullptr)
+        return vkt::rt::fail("vktStructuredVolumeMigrateChecked: null volume");
+    (void)vkt::rt::takeMigrationFailure();
+    v->volume.migrate();
+    std::string const m = vkt::rt::takeMigrationFailure();
+    if (!v->volume.residentOn(vkt::GetThreadExecutionPolicy()))
+        return vkt::rt::fail(m.empty() ? "vktStructuredVolumeMigrateChecked: migration failed" : m.c_str());
+    return vktNoError;
+}
 
 vktError vktMapVoxel(uint8_t* dst, float value, vktDataFormat dataFormat, float mappingLo, float mappingHi)
 {

@@ -24,7 +24,7 @@ namespace
     vktHipVolumeView_t view(StructuredVolume& v)
     {
         vktHipVolumeView_t out;
-        out.data = v.getData();   // migrates to the thread's device first
+        out.data = rt::deviceData(v);   // migrates to the thread's device first (nullptr if that failed)
         Vec3i d = v.getDims();
         out.dimX = d.x;
         out.dimY = d.y;
@@ -51,7 +51,8 @@ namespace
             return InvalidValue;
         }
         rt::ScopedKernelTimer timer(name, ep.printPerformance != False);
-        return static_cast<Error>(fn());
+        (void)rt::takeMigrationFailure();
+        return static_cast<Error>(rt::explainFailure(static_cast<vktError>(fn()), name));
     }
 } // namespace
 
@@ -268,9 +269,10 @@ vktError vktTransformRangeSV2(vktStructuredVolume v1, vktStructuredVolume v2, in
     if (ep.device != vkt::ExecutionPolicy::Device::GPU)
         return vkt::rt::fail("TransformRange_hip: CPU execution policy (volkit-amd implements the GPU backend only)");
     vkt::rt::ScopedKernelTimer timer("TransformRange_hip", ep.printPerformance != vkt::False);
+    (void)vkt::rt::takeMigrationFailure();
     auto mk = [](vkt::StructuredVolume& v) {
         vktHipVolumeView_t o;
-        o.data = v.getData();
+        o.data = vkt::rt::deviceData(v);
         vkt::Vec3i d = v.getDims();
         o.dimX = d.x;
         o.dimY = d.y;
@@ -282,7 +284,9 @@ vktError vktTransformRangeSV2(vktStructuredVolume v1, vktStructuredVolume v2, in
     };
     vktHipVolumeView_t a = mk(v1->volume);
     vktHipVolumeView_t b = mk(v2->volume);
-    return vktHipTransformRange2(a, b, vktVec3i_t{fx, fy, fz}, vktVec3i_t{lx, ly, lz}, vktVec3i_t{ox, oy, oz}, op);
+    return vkt::rt::explainFailure(
+        vktHipTransformRange2(a, b, vktVec3i_t{fx, fy, fz}, vktVec3i_t{lx, ly, lz}, vktVec3i_t{ox, oy, oz}, op),
+        "TransformRange_hip");
 }
 
 vktError vktResampleSV(vktStructuredVolume dst, vktStructuredVolume src, vktFilterMode fm)

@@ -26,7 +26,7 @@ namespace
     vktHipVolumeView_t brickView(StructuredVolume& v)
     {
         vktHipVolumeView_t out;
-        out.data = v.getData();
+        out.data = rt::deviceData(v);
         Vec3i d = v.getDims();
         out.dimX = d.x;
         out.dimY = d.y;
@@ -107,6 +107,7 @@ namespace
                        d.z == ext[2][iz + 1 == static_cast<size_t>(na[2])] && v.getDataFormat() == fmt &&
                        m.x == map.x && m.y == map.y;
                 ptrs[i] = v.getDataFor(ep);
+                good = good && (ptrs[i] != nullptr || d.x * d.y * d.z == 0);   // (a failed migration: the range path reports it)
                 if (++ix == nx)
                 {
                     ix = 0;

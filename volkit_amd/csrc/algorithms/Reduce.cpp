@@ -20,7 +20,7 @@ namespace
     vktHipVolumeView_t viewOf(StructuredVolume& v)
     {
         vktHipVolumeView_t out;
-        out.data = v.getData();
+        out.data = rt::deviceData(v);
         Vec3i d = v.getDims();
         out.dimX = d.x;
         out.dimY = d.y;
@@ -34,6 +34,7 @@ namespace
 
     bool gpuPolicy(char const* name)
     {
+        (void)rt::takeMigrationFailure();   // (only this call's migrations explain its errors)
         if (GetThreadExecutionPolicy().device == ExecutionPolicy::Device::GPU)
             return true;
         rt::setLastError(std::string(name) + ": CPU execution policy");
@@ -64,8 +65,9 @@ Error ComputeAggregatesRange(StructuredVolume& volume, Aggregates& aggregates, V
         return InvalidValue;
     rt::ScopedKernelTimer timer("ComputeAggregatesRange_hip", GetThreadExecutionPolicy().printPerformance != False);
     vktAggregates_t out;
-    vktError e = vktHipAggregatesRange(viewOf(volume), vktVec3i_t{first.x, first.y, first.z},
-                                       vktVec3i_t{last.x, last.y, last.z}, &out);
+    vktError e = rt::explainFailure(vktHipAggregatesRange(viewOf(volume), vktVec3i_t{first.x, first.y, first.z},
+                                                          vktVec3i_t{last.x, last.y, last.z}, &out),
+                                    "ComputeAggregatesRange_hip");
     if (e == vktNoError)
         std::memcpy(&aggregates, &out, sizeof(out));
     return static_cast<Error>(e);
@@ -100,9 +102,15 @@ Error ComputeHistogramRange(StructuredVolume& volume, Histogram& histogram, Vec3
     rt::ScopedKernelTimer timer("ComputeHistogramRange_hip", GetThreadExecutionPolicy().printPerformance != False);
     static_assert(sizeof(std::size_t) == sizeof(uint64_t), "bin counters are 64-bit");
     uint64_t* bins = reinterpret_cast<uint64_t*>(histogram.getBinCounts());   // migrates to HBM
-    return static_cast<Error>(vktHipHistogramRange(viewOf(volume), vktVec3i_t{first.x, first.y, first.z},
-                                                   vktVec3i_t{last.x, last.y, last.z}, bins, histogram.getNumBins(),
-                                                   0));
+    if (!histogram.residentOn(GetThreadExecutionPolicy()))
+    {
+        rt::fail(("ComputeHistogramRange_hip: " + rt::takeMigrationFailure()).c_str());
+        return InvalidValue;
+    }
+    return static_cast<Error>(rt::explainFailure(
+        vktHipHistogramRange(viewOf(volume), vktVec3i_t{first.x, first.y, first.z}, vktVec3i_t{last.x, last.y, last.z},
+                             bins, histogram.getNumBins(), 0),
+        "ComputeHistogramRange_hip"));
 }
 
 } // vkt

@@ -223,11 +223,16 @@ namespace
                 rt::fail("Render: rgbaLookupTable must be an RGBA32F LookupTable");
                 return InvalidValue;
             }
-            p.lut = reinterpret_cast<float const*>(lut->getData());   // migrates to HBM
+            p.lut = reinterpret_cast<float const*>(rt::deviceData(*lut));   // migrates to HBM
+            if (p.lut == nullptr)
+            {
+                rt::fail(("Render: " + rt::takeMigrationFailure()).c_str());
+                return InvalidValue;
+            }
             p.lutSize = lut->getDims().x;
         }
         Vec2f m = volume.getVoxelMapping();
-        vktHipVolumeView_t v{volume.getData(), d.x, d.y, d.z, static_cast<int32_t>(volume.getDataFormat()), m.x, m.y};
+        vktHipVolumeView_t v{rt::deviceData(volume), d.x, d.y, d.z, static_cast<int32_t>(volume.getDataFormat()), m.x, m.y};
         std::size_t const n = static_cast<std::size_t>(p.width) * static_cast<std::size_t>(p.height) * 4;
         float* dev = nullptr;
         if (rt::check(hipMalloc(&dev, 2 * n * sizeof(float)), "hipMalloc(render target)") != vktNoError)

@@ -51,7 +51,16 @@ namespace
         return out;
     }
 
-    bool policyIsGpu() { return GetThreadExecutionPolicy().device == ExecutionPolicy::Device::GPU; }
+    // Migrates v to the thread's device; true when its bytes are then in HBM.  A migration that
+    // failed leaves them in host memory (MigrateBuffer keeps the only copy), where the host path
+    // reads / writes them correctly.
+    bool inHbm(StructuredVolume& v)
+    {
+        (void)v.getData();
+        ExecutionPolicy gpu;
+        gpu.device = ExecutionPolicy::Device::GPU;
+        return v.residentOn(gpu);
+    }
 
     // Two pinned staging buffers + events, shared by all streams of the process.
     struct Staging
@@ -401,7 +410,7 @@ Error InputStream::read(StructuredVolume& volume)
         return InvalidDataSource;
     std::size_t const n = volume.getSizeInBytes();
     std::size_t len;
-    if (policyIsGpu())
+    if (inHbm(volume))
     {
         vktError e;
         len = readToDevice(dataSource_, volume.getData(), {Rows{0, 1}}, n, n, e);
@@ -437,7 +446,7 @@ Error InputStream::readRange(StructuredVolume& dst, Vec3i first, Vec3i last)
     std::size_t const expect = static_cast<std::size_t>(last.z - first.z) * (last.y - first.y) * lineBytes;
     std::vector<Rows> runs = rangeRuns(dims, bpv, first, last);
     std::size_t len = 0;
-    if (policyIsGpu())
+    if (inHbm(dst))
     {
         vktError e;
         len = readToDevice(dataSource_, dst.getData(), runs, lineBytes, pitch, e);
@@ -465,7 +474,7 @@ Error OutputStream::write(StructuredVolume& volume)
         return InvalidDataSource;
     std::size_t const n = volume.getSizeInBytes();
     std::size_t len;
-    if (policyIsGpu())
+    if (inHbm(volume))
     {
         vktError e;
         len = writeFromDevice(dataSource_, volume.getData(), {Rows{0, 1}}, n, n, e);
@@ -499,7 +508,7 @@ Error OutputStream::writeRange(StructuredVolume& dst, Vec3i first, Vec3i last)
     std::size_t const expect = static_cast<std::size_t>(last.z - first.z) * (last.y - first.y) * lineBytes;
     std::vector<Rows> runs = rangeRuns(dims, bpv, first, last);
     std::size_t len = 0;
-    if (policyIsGpu())
+    if (inHbm(dst))
     {
         vktError e;
         len = writeFromDevice(dataSource_, dst.getData(), runs, lineBytes, pitch, e);

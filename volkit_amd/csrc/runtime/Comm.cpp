@@ -422,17 +422,28 @@ vktError vktHipSlabExchangeHaloPeer(int32_t numSlabs, vktHipVolumeView_t const* 
     VKT_HIP_TRY(hipGetDevice(&cur));
     std::vector<hipStream_t> streams(static_cast<size_t>(nDev), nullptr);
     std::vector<char> owned(static_cast<size_t>(nDev), 0);
-    vktError e = vktNoError;
+    // the copies into other devices run on streams of their own: each first waits for the work
+    // already queued on the library's compute stream (a kernel that is still writing a source
+    // slab of the library's device)
+    hipEvent_t queued = nullptr;
+    VKT_HIP_TRY(hipEventCreateWithFlags(&queued, hipEventDisableTiming));
+    vktError e = rt::check(hipEventRecord(queued, rt::computeStream()), "hipEventRecord(compute)");
     auto streamOf = [&](int dev) -> hipStream_t {
         if (dev == libDev)
             return rt::computeStream();
         if (!streams[static_cast<size_t>(dev)])
         {
+            hipStream_t st = nullptr;
             if (rt::check(hipSetDevice(dev), "hipSetDevice") == vktNoError &&
-                rt::check(hipStreamCreateWithFlags(&streams[static_cast<size_t>(dev)], hipStreamNonBlocking),
-                          "hipStreamCreate") == vktNoError)
+                rt::check(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate") == vktNoError)
+            {
+                streams[static_cast<size_t>(dev)] = st;
                 owned[static_cast<size_t>(dev)] = 1;
+                if (rt::check(hipStreamWaitEvent(st, queued, 0), "hipStreamWaitEvent(peer copy)") != vktNoError)
+                    st = nullptr;
+            }
             (void)hipSetDevice(cur);
+            return st;
         }
         return streams[static_cast<size_t>(dev)];
     };
@@ -494,6 +505,7 @@ vktError vktHipSlabExchangeHaloPeer(int32_t numSlabs, vktHipVolumeView_t const* 
     (void)hipSetDevice(cur);
     if (e == vktNoError)
         e = rt::check(hipStreamSynchronize(rt::computeStream()), "hipStreamSynchronize");
+    (void)hipEventDestroy(queued);
     return e != vktNoError ? e : rt::finishLaunch("SlabExchangeHaloPeer_hip");
 }
 

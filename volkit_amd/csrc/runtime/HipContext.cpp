@@ -113,6 +113,32 @@ namespace rt
 
     void setLastError(std::string const& msg) { tlsLastError = msg; }
 
+    namespace
+    {
+        thread_local std::string tlsMigrationFailure;
+    }
+
+    void noteMigrationFailure(std::string const& msg)
+    {
+        tlsMigrationFailure = msg;
+        (void)fail(msg.c_str());
+    }
+
+    std::string takeMigrationFailure()
+    {
+        std::string m;
+        m.swap(tlsMigrationFailure);
+        return m;
+    }
+
+    vktError explainFailure(vktError e, char const* name)
+    {
+        std::string const m = takeMigrationFailure();
+        if (e != vktNoError && !m.empty())
+            setLastError(std::string(name) + ": " + m);
+        return e;
+    }
+
     vktError check(hipError_t err, char const* what)
     {
         if (err == hipSuccess)
@@ -219,6 +245,7 @@ namespace rt
             {"decompose.gather", 0},
             {"decompose.pipe", 0},
             {"decompose.pair", 0},
+            {"memory.fail_next_alloc", 0},
         };
         static_assert(sizeof(kKnobs) / sizeof(kKnobs[0]) == static_cast<size_t>(Knob::Count), "knob table");
         std::atomic<int64_t> gKnobs[static_cast<int>(Knob::Count)] = {{kKnobs[0].def}, {kKnobs[1].def},
@@ -235,10 +262,20 @@ namespace rt
                                                                   {kKnobs[22].def}, {kKnobs[23].def},
                                                                   {kKnobs[24].def}, {kKnobs[25].def},
                                                                   {kKnobs[26].def}, {kKnobs[27].def},
-                                                                  {kKnobs[28].def}};
+                                                                  {kKnobs[28].def}, {kKnobs[29].def}};
     } // namespace
 
     int64_t knob(Knob k) { return gKnobs[static_cast<int>(k)].load(std::memory_order_relaxed); }
+
+    bool takeKnobCount(Knob k)
+    {
+        std::atomic<int64_t>& a = gKnobs[static_cast<int>(k)];
+        int64_t v = a.load();
+        while (v > 0)
+            if (a.compare_exchange_weak(v, v - 1))
+                return true;
+        return false;
+    }
 
     // Every backend call is also a roctx range named after the reference's backend function
     // (e.g. "SumRange_hip"), so `rocprofv3 --marker-trace` attributes kernels to API calls.

@@ -23,6 +23,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
 #include <iterator>
@@ -66,9 +67,20 @@ namespace
     //  * the old pageable buffer is freed on a background thread (the copy has completed: the
     //    migrate's memcpy is synchronous);
     //  * freed pinned buffers are kept for reuse by an allocation of the same size (at most
-    //    kPinnedCacheBytes in all), returned by vktHipReleaseCachedMemory or when hipHostMalloc fails.
+    //    pinnedCacheCap() in all), returned by vktHipReleaseCachedMemory or when hipHostMalloc fails.
     constexpr std::size_t kBigHost = std::size_t(64) << 20;
-    constexpr std::size_t kPinnedCacheBytes = std::size_t(16) << 30;
+    std::size_t physicalBytes()
+    {
+        long const pages = sysconf(_SC_PHYS_PAGES), page = sysconf(_SC_PAGESIZE);
+        return pages > 0 && page > 0 ? static_cast<std::size_t>(pages) * static_cast<std::size_t>(page) : 0;
+    }
+
+    // page-locked memory kept for reuse: at most min(16 GiB, physical memory / 16)
+    std::size_t pinnedCacheCap()
+    {
+        static std::size_t const cap = std::min(std::size_t(16) << 30, physicalBytes() / 16);
+        return cap;
+    }
     std::vector<std::pair<void*, std::size_t>>& pinnedCache()
     {
         static auto* c = new std::vector<std::pair<void*, std::size_t>>;
@@ -111,11 +123,7 @@ namespace
 
     std::size_t hostCacheCap()
     {
-        static std::size_t const cap = [] {
-            long const pages = sysconf(_SC_PHYS_PAGES), page = sysconf(_SC_PAGESIZE);
-            std::size_t const phys = pages > 0 && page > 0 ? static_cast<std::size_t>(pages) * static_cast<std::size_t>(page) : 0;
-            return std::min(std::size_t(8) << 30, phys / 8);
-        }();
+        static std::size_t const cap = std::min(std::size_t(8) << 30, physicalBytes() / 8);
         return cap;
     }
 
@@ -187,7 +195,7 @@ namespace
     // (tools/alloc_probe.py).  An arena chunk is sized for a group of like buffers
     // (kArenaGroup times the request: the src / dst / operand volumes of one pipeline land in one
     // chunk), at least kArenaMin, growing geometrically (twice the newest chunk while it is
-    // allocated, up to kArenaGrowCap) for runs of like-sized smaller buffers, and never more than 3/4 of the device's free
+    // allocated, up to kArenaGrowCap) for runs of like-sized smaller buffers, and never more than 1/4 of the device's free
     // memory beyond the request -- a 5 MiB buffer reserves 64 MiB, not a 16-GiB chunk.
     // Freed blocks are not reusable at once (a queued kernel or copy may still use them): they
     // wait on a pending list until a drain records one event on each of the library's streams
@@ -240,6 +248,7 @@ namespace
         ArenaChunk* lastChunk = nullptr;   // the newest arena chunk while it exists, and its request
         std::size_t lastReq = 0;
         std::vector<void*> pending;   // freed, not yet known idle
+        bool pendingForeign = false;  // a pending block was freed through the public free entry points
         hipEvent_t evCompute = nullptr, evCopy = nullptr;
     };
 
@@ -286,7 +295,7 @@ namespace
         if (d.pending.empty())
             return;
         bool idle = false;
-        if (dev == rt::device())
+        if (dev == rt::device() && !d.pendingForeign)
         {
             if (!d.evCompute && (hipEventCreateWithFlags(&d.evCompute, hipEventDisableTiming) != hipSuccess ||
                                  hipEventCreateWithFlags(&d.evCopy, hipEventDisableTiming) != hipSuccess))
@@ -319,6 +328,7 @@ namespace
         }
         d.pending.clear();
         d.pendingByClass.clear();
+        d.pendingForeign = false;
     }
 
     // Returns arena chunks without carved blocks to HIP; with `pools`, also pool chunks without
@@ -447,8 +457,10 @@ namespace
         if (d.lastChunk && d.lastReq <= 2 * len && 2 * d.lastReq >= len)
             want = std::max(want, std::min(2 * d.lastChunk->size, kArenaGrowCap));
         std::size_t freeB = 0, totalB = 0;
+        // the group's extra room is a cache other allocators in the process (torch, RCCL) cannot
+        // reclaim: at most a quarter of the device's free memory beyond the request
         if (want > len && hipMemGetInfo(&freeB, &totalB) == hipSuccess && freeB > len)
-            want = std::min(want, len + (freeB - len) / 4 * 3);
+            want = std::min(want, len + (freeB - len) / 4);
         else
             (void)hipGetLastError();
         return (std::max(want, len) + kArenaAlign - 1) / kArenaAlign * kArenaAlign;
@@ -488,6 +500,11 @@ namespace
 
     void* heapAllocate(std::size_t bytes)
     {
+        if (rt::takeKnobCount(rt::Knob::MemoryFailNextAlloc))
+        {
+            (void)rt::check(hipErrorOutOfMemory, "hipMalloc (memory.fail_next_alloc)");
+            return nullptr;
+        }
         int const dev = rt::device();
         Heaps& H = heaps();
         std::lock_guard<std::mutex> lock(H.m);
@@ -500,8 +517,11 @@ namespace
         return deviceMalloc(bytes, d, dev, H, false);   // a plain buffer (freed with hipFree)
     }
 
-    // true when p is a heap block (then it is queued for reuse)
-    bool heapFree(void* p)
+    // true when p is a heap block (then it is queued for reuse).  foreign: freed through the
+    // public vktHipFree / vktFree / Free, whose caller may have used the buffer on streams of its
+    // own -- its reuse then waits for a device synchronisation (hipFree's guarantee), not only
+    // for the library's streams.
+    bool heapFree(void* p, bool foreign)
     {
         Heaps& H = heaps();
         std::lock_guard<std::mutex> lock(H.m);
@@ -511,6 +531,7 @@ namespace
         HeapBlock const& b = it->second;
         DeviceHeap& d = H.byDevice[b.dev];
         d.pending.push_back(p);
+        d.pendingForeign = d.pendingForeign || foreign;
         if (b.arena)
         {
             b.ac->live -= b.len;
@@ -626,13 +647,13 @@ namespace detail
         return p;
     }
 
-    void FreeOn(void* data, ExecutionPolicy const& owner)
+    void freeOn(void* data, ExecutionPolicy const& owner, bool foreign)
     {
         if (data == nullptr)
             return;
         if (onGpu(owner))
         {
-            if (!heapFree(data))
+            if (!heapFree(data, foreign))
                 (void)rt::check(hipFree(data), "hipFree");
             return;
         }
@@ -644,7 +665,7 @@ namespace detail
                 pinnedSet().erase(it);
                 std::size_t const bytes = pinnedSizes()[data];
                 pinnedSizes().erase(data);
-                if (bytes >= kBigHost && gPinnedCached + bytes <= kPinnedCacheBytes)
+                if (bytes >= kBigHost && gPinnedCached + bytes <= pinnedCacheCap())
                 {
                     pinnedCache().emplace_back(data, bytes);   // for the next migration of this size
                     gPinnedCached += bytes;
@@ -657,16 +678,114 @@ namespace detail
         std::free(data);
     }
 
-    // A large pageable buffer the caller is done with: freed off the calling thread (munmap of
-    // 2 GiB costs more than its PCIe copy).
-    void freeHostLater(void* data)
+    void FreeOn(void* data, ExecutionPolicy const& owner) { freeOn(data, owner, false); }
+
+}   // detail
+
+namespace
+{
+    // Frees large pageable host buffers off the calling thread (munmap of 2 GiB costs more than
+    // its PCIe copy) on ONE worker thread, started on first use.  At most kReaperQueue buffers
+    // wait; beyond that the caller frees synchronously (back-pressure instead of unbounded
+    // threads or memory).  At process exit (static destruction) shutdown() frees what is queued
+    // and joins the worker; the reaper itself is never destroyed, so a free after that is
+    // well-defined and runs on the caller.
+    class HostReaper
     {
-        std::thread([data] { std::free(data); }).detach();
+    public:
+        static constexpr std::size_t kReaperQueue = 4;
+
+        void shutdown()
+        {
+            {
+                std::lock_guard<std::mutex> g(m_);
+                stopped_ = true;
+            }
+            cv_.notify_all();
+            if (worker_.joinable())
+                worker_.join();
+            std::lock_guard<std::mutex> g(m_);
+            for (void* p : queue_)
+                std::free(p);
+            queue_.clear();
+        }
+
+        void release(void* data)
+        {
+            {
+                std::lock_guard<std::mutex> g(m_);
+                if (!stopped_ && queue_.size() < kReaperQueue)
+                {
+                    queue_.push_back(data);
+                    if (!worker_.joinable())
+                        worker_ = std::thread([this] { loop(); });
+                    cv_.notify_one();
+                    return;
+                }
+            }
+            std::free(data);
+        }
+
+    private:
+        void loop()
+        {
+            std::unique_lock<std::mutex> g(m_);
+            for (;;)
+            {
+                cv_.wait(g, [&] { return stopped_ || !queue_.empty(); });
+                if (queue_.empty())
+                    return;   // stopped
+                void* const p = queue_.front();
+                queue_.erase(queue_.begin());
+                g.unlock();
+                std::free(p);
+                g.lock();
+            }
+        }
+
+        std::mutex m_;
+        std::condition_variable cv_;
+        std::vector<void*> queue_;
+        std::thread worker_;
+        bool stopped_ = false;
+    };
+
+    HostReaper& reaper()
+    {
+        static auto* r = new HostReaper;   // (never destroyed, see above)
+        return *r;
     }
+
+    struct ReaperShutdown
+    {
+        ~ReaperShutdown() { reaper().shutdown(); }
+    } gReaperShutdown;
+} // namespace
+
+namespace detail
+{
+    void freeHostLater(void* data) { reaper().release(data); }
 
     void CopyOn(void* dst, void const* src, std::size_t bytes, ExecutionPolicy const& owner)
     {
         (void)memcpyHip(dst, src, bytes, onGpu(owner) ? CopyKind::DeviceToDevice : CopyKind::HostToHost);
+    }
+
+    // The reference allocates, copies and frees the source unconditionally
+    // (include/cpp/vkt/ManagedBuffer.hpp:168-198, errors dropped by src/vkt/Memory.cpp:70), so a
+    // failed allocation or copy loses the only copy of the data.  Here the source is released
+    // only once the copy has completed: on failure the buffer stays where it was (`last` and
+    // the returned pointer unchanged), the error is recorded (rt::noteMigrationFailure, the
+    // thread's last error), and the algorithm that asked for the bytes fails with InvalidValue
+    // (rt::deviceData).
+    void CopyBetween(void* dst, ExecutionPolicy const& dstOwner, void const* src, ExecutionPolicy const& srcOwner,
+                     std::size_t bytes)
+    {
+        if (dst == nullptr || src == nullptr)
+            return;
+        CopyKind const ck = onGpu(dstOwner) ? (onGpu(srcOwner) ? CopyKind::DeviceToDevice : CopyKind::HostToDevice)
+                                            : (onGpu(srcOwner) ? CopyKind::DeviceToHost : CopyKind::HostToHost);
+        (void)memcpyHip(dst, src, bytes, ck);
     }
 
     void* MigrateBuffer(void* data, std::size_t bytes, ExecutionPolicy& last)
@@ -674,11 +793,18 @@ namespace detail
         ExecutionPolicy ep = GetThreadExecutionPolicy();
         if (ep.device == last.device)
             return data;
+        char const* const dir = onGpu(ep) ? "host -> device" : "device -> host";
         // a pageable destination on the host: a cached buffer of this size first (resident pages)
         void* fresh = !onGpu(ep) && bytes >= kBigHost && !gPinnedHost.load() ? takeHostCached(bytes) : nullptr;
         bool const reused = fresh != nullptr;
         if (!reused)
             fresh = AllocateOn(bytes, ep);
+        if (fresh == nullptr && bytes > 0)
+        {
+            rt::noteMigrationFailure(std::string("migrate (") + dir + ", " + std::to_string(bytes) +
+                                     " bytes): allocation failed; the data stays where it was");
+            return data;
+        }
         bool pinnedFresh = false, pinnedOld = false;
         if (bytes >= kBigHost)
         {
@@ -688,9 +814,25 @@ namespace detail
         }
         if (bytes >= kBigHost && !onGpu(ep) && fresh != nullptr && !pinnedFresh && !reused && data != nullptr)
             prefaultHost(fresh, bytes);   // (the copy below then writes resident pages)
-        if (bytes > 0 && data != nullptr && fresh != nullptr)
-            (void)memcpyHip(fresh, data, bytes,
-                            onGpu(ep) ? CopyKind::HostToDevice : CopyKind::DeviceToHost);
+        if (bytes > 0 && data != nullptr)
+        {
+            vktError const e = memcpyHip(fresh, data, bytes, onGpu(ep) ? CopyKind::HostToDevice : CopyKind::DeviceToHost);
+            if (e != vktNoError)
+            {
+                // the destination never received the bytes: give it back, keep the source
+                if (reused)
+                {
+                    if (!keepHostCached(fresh, bytes))
+                        std::free(fresh);
+                }
+                else
+                    FreeOn(fresh, ep);
+                rt::noteMigrationFailure(std::string("migrate (") + dir + ", " + std::to_string(bytes) +
+                                         " bytes): copy failed (" + vktHipGetLastErrorString() +
+                                         "); the data stays where it was");
+                return data;
+            }
+        }
         if (bytes >= kBigHost && !onGpu(last) && !pinnedOld && data != nullptr)
         {
             if (!keepHostCached(data, bytes))   // the copy is complete (memcpyHip synchronises)
@@ -709,7 +851,7 @@ void Allocate(void** ptr, std::size_t size)
         *ptr = detail::AllocateOn(size, GetThreadExecutionPolicy());
 }
 
-void Free(void* ptr) { detail::FreeOn(ptr, GetThreadExecutionPolicy()); }
+void Free(void* ptr) { detail::freeOn(ptr, GetThreadExecutionPolicy(), true); }
 
 void Memcpy(void* dst, void const* src, std::size_t size, CopyKind ck) { (void)detail::memcpyHip(dst, src, size, ck); }
 
@@ -787,7 +929,7 @@ vktError vktHipFree(void* ptr)
 {
     if (ptr == nullptr)
         return vktNoError;
-    if (vkt::heapFree(ptr))
+    if (vkt::heapFree(ptr, true))
         return vktNoError;
     return vkt::rt::check(hipFree(ptr), "hipFree");
 }

@@ -47,6 +47,26 @@ namespace rt
     vktError fail(char const* what);          // non-HIP failure (bad arguments)
     void setLastError(std::string const& msg);
 
+    // A migration that could not move a buffer (allocation or copy failure) leaves the bytes
+    // where they were (detail::MigrateBuffer keeps the only copy) and records why here, per
+    // thread; takeMigrationFailure() returns and clears it (empty: none since the last take).
+    void noteMigrationFailure(std::string const& msg);
+    std::string takeMigrationFailure();
+    // e unchanged; when e is an error and a migration failed since the last take, the thread's
+    // last error names that failure (the backend's own message would only say "invalid view").
+    vktError explainFailure(vktError e, char const* name);
+
+    // Bytes of a buffer (StructuredVolume, LookupTable, Histogram...) for a backend call on
+    // the thread's device: getData() migrates them there first.  A buffer whose migration
+    // failed is still resident elsewhere and yields nullptr, which every backend rejects
+    // (validView) before it launches anything.
+    template <class Buffer>
+    auto deviceData(Buffer& b) -> decltype(b.getData())
+    {
+        auto* p = b.getData();
+        return b.residentOn(GetThreadExecutionPolicy()) ? p : nullptr;
+    }
+
     // Called by every backend entry point right after its launches: picks up launch
     // errors and, if async execution is off, waits for the compute stream.
     vktError finishLaunch(char const* what);
@@ -103,9 +123,12 @@ namespace rt
         DecomposeGather,               // 1: uniform brick grids stage source rows and gather items (measured no faster: off)
         DecomposePipe,                 // 1: uniform brick grids on a resident, double-buffered walk (measured slower: off)
         DecomposePair,                 // 1: two x-neighbour bricks of <= 16 KiB per workgroup (uniform grids)
+        MemoryFailNextAlloc,           // n > 0: the next n device allocations fail (tests of the failure paths)
         Count
     };
     int64_t knob(Knob k);
+    // A counting knob: true (and the knob decremented) when it was > 0.
+    bool takeKnobCount(Knob k);
 
     // Stream ordering between the compute stream and the side copy stream (event based):
     // the copy stream waits for everything queued on the compute stream so far / the compute

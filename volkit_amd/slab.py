@@ -526,7 +526,7 @@ class GpuMomentFns:
 
 
 def _aggregates_moments(view, global_dims, z0, first, last, rng, group, device, fns):
-    """UInt16 / Float32 slabs in one data pass: every rank's 128-byte moments partial (exact
+    """UInt16 / Float32 slabs in one data pass: every rank's 96-byte moments partial (exact
     integer sums under the UInt16 unit mapping, float moments otherwise), ONE all_gather, combined
     in rank order (deterministic, identical on every rank) and finished on the host.  None when
     the float form says its terms may leave the float range (the caller runs the two passes; every
@@ -580,7 +580,7 @@ def aggregates(view, global_dims, z0: int, first, last, group=None, device=None,
     (pass 1), partials are all-gathered and combined in rank order (deterministic), the
     reference's float mean of the WHOLE volume follows, then pass 2 and a second exchange.
     UInt16 / Float32 volumes whose every slab takes the moments walk use ONE data pass and one
-    all_gather of 128-byte moment partials (_aggregates_moments; `moment_fns` replaces the GPU
+    all_gather of 96-byte moment partials (_aggregates_moments; `moment_fns` replaces the GPU
     steps), UInt8 (and UInt16 when that is off) one pass of code counts (_aggregates_codes;
     `code_fns` replaces the GPU steps, e.g. in CPU tests); a custom `pass_fn` alone keeps the two
     passes.  `view` is this rank's slab (global planes [z0, z0 + view.dimZ)); returns Aggregates_t."""

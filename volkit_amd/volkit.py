@@ -177,6 +177,11 @@ class StructuredVolume:
     def migrate(self):
         lib.vktStructuredVolumeMigrate(self._h)
 
+    def migrateChecked(self):
+        """migrate() with its outcome (extension): InvalidValue when the bytes could not be moved
+        to the thread's device -- they then stay where they were, intact."""
+        return lib.vktStructuredVolumeMigrateChecked(self._h)
+
     def setValue(self, x, y, z, value):
         lib.vktStructuredVolumeSetValue(self._h, int(x), int(y), int(z), float(value))
 
