@@ -243,20 +243,45 @@ VKTAPI vktError vktHipCommGetUniqueId(vktHipCommId_t* id);
 VKTAPI vktError vktHipCommInitRank(vktHipComm_t* comm, int32_t nranks, vktHipCommId_t id, int32_t rank);
 VKTAPI vktError vktHipCommDestroy(vktHipComm_t comm);
 /* Failure detection: every RCCL round the library issues on `comm` (halo
- * exchange, slab Range moves) waits on the host up to `milliseconds` for its transfers, polling
+ * exchange, overlapped slab resample, slab Range moves) returns once enqueued -- the host is
+ * never blocked.  A watcher thread of the communicator times each round from the moment the
+ * work queued ahead of it on its stream has finished, up to `milliseconds`, polling
  * ncclCommGetAsyncError; a peer that never joins, or an asynchronous RCCL error, aborts the
- * communicator and the call returns vktInvalidValue (later calls on it fail at once) instead of
- * hanging every rank.  0: a round returns once enqueued (no host wait).  Default 300 000 ms, or
- * the environment variable VKT_COMM_TIMEOUT_MS at vktHipCommInitRank. */
+ * communicator (its kernels exit instead of hanging every rank) and every later call on it,
+ * and vktHipCommSynchronize, return vktInvalidValue naming the failure.  0: no deadline.
+ * Default 300 000 ms, or the environment variable VKT_COMM_TIMEOUT_MS at vktHipCommInitRank. */
 VKTAPI vktError vktHipCommSetTimeout(vktHipComm_t comm, int64_t milliseconds);
+/* Waits until the watcher has judged every round enqueued so far (complete, or the
+ * communicator aborted); vktInvalidValue if the communicator was aborted. */
+VKTAPI vktError vktHipCommSynchronize(vktHipComm_t comm);
+/* One round on the compute stream: `bytes` of sendBuf to `peer` and as many from `peer` into
+ * recvBuf (device buffers; peer may be this rank).  Returns once enqueued, judged like every
+ * round (vktHipCommSetTimeout). */
+VKTAPI vktError vktHipCommExchange(vktHipComm_t comm, int32_t peer, void const* sendBuf, void* recvBuf, size_t bytes);
 /* `localSrc` holds global source planes [localZ0, localZ0 + localSrc.dimZ) (X/Y dims global).
  * Sends the owned planes the peers' dst slabs read and receives this rank's halo planes into
  * the buffer: one ncclGroupStart .. ncclGroupEnd round of ncclSend / ncclRecv on the compute
- * stream, so a vktHipResampleSlab enqueued next reads the halo.  Returns once the round has
- * completed, or once enqueued with a timeout of 0 (vktHipCommSetTimeout). */
+ * stream, so a vktHipResampleSlab enqueued next reads the halo.  Returns once enqueued. */
 VKTAPI vktError vktHipSlabExchangeHalo(vktHipComm_t comm, vktHipVolumeView_t localSrc, int32_t localZ0,
                                        int32_t dstGlobalDimZ, int32_t srcGlobalDimZ, vktFilterMode fm,
                                        int32_t needsNeighbours);
+/* Halo exchange overlapped with the interior (the compute / copy stream split of the reference's
+ * CudaContext, include/c/vkt/CudaContext.h:41-65; volkit_amd/slab.py:resample_slab_overlapped):
+ * the RCCL round runs on the communicator's own stream after the work queued so far on the
+ * compute stream; meanwhile the dst planes that read only owned source planes resample on the
+ * compute stream; the compute stream then waits for the round and resamples the remaining
+ * planes.  `dst` holds exactly this rank's dst slab (ceil partition of dstGlobalDimZ);
+ * `localSrc` as for vktHipSlabExchangeHalo.  Equal to vktHipSlabExchangeHalo +
+ * vktHipResampleSlab; returns once enqueued. */
+VKTAPI vktError vktHipResampleSlabOverlapped(vktHipComm_t comm, vktHipVolumeView_t dst, vktHipVolumeView_t localSrc,
+                                             int32_t localZ0, int32_t dstGlobalDimZ, int32_t srcGlobalDimZ,
+                                             vktFilterMode fm, int32_t needsNeighbours);
+/* The same for `numSlabs` slabs in this process on the library's device (slab r = rank r):
+ * each slab's receives are device copies on the copy stream, overlapped with its interior. */
+VKTAPI vktError vktHipResampleSlabsOverlappedLocal(int32_t numSlabs, vktHipVolumeView_t const* dst,
+                                                   vktHipVolumeView_t const* localSrc, int32_t const* localZ0,
+                                                   int32_t dstGlobalDimZ, int32_t srcGlobalDimZ, vktFilterMode fm,
+                                                   int32_t needsNeighbours);
 /* The same exchange for a partition whose `numSlabs` slabs all live in this process on the
  * library's device (slab r = rank r of numSlabs; localSrc[r] holds global source planes
  * [localZ0[r], localZ0[r] + localSrc[r].dimZ)): every receive of the plan is a device-to-device

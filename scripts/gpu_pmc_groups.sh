@@ -14,6 +14,8 @@ for g in "$@"; do
   i=0
   PASSES=("FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_BUSY_CYCLES SQ_WAIT_INST_ANY")
   [ -n "${PMC_EXTRA:-}" ] && PASSES+=("$PMC_EXTRA")   # one more pass (<= 8 SQ counters)
+  # PMC_PASSES="a b;c d": replaces the passes (each within the per-block limits)
+  [ -n "${PMC_PASSES:-}" ] && IFS=';' read -r -a PASSES <<< "$PMC_PASSES"
   for pass in "${PASSES[@]}"; do
     timeout -s KILL 120 rocprofv3 --pmc $pass -d $O/$g/p$i -o run --output-format csv -- $B > $O/$g.p$i.log 2>&1 || { tail -20 $O/$g.p$i.log; exit 1; }
     i=$((i+1))

@@ -59,6 +59,14 @@ def main():
                 else:
                     out[i][name] = v
     for o in out:
+        # calibrated read bytes: the L2 -> fabric read requests by size (gfx950 counts 32-, 64- and
+        # 128-B requests separately; FETCH_SIZE tallies the 128-B ones at 64 B -- the "doubling")
+        if all(k in o for k in ("TCC_EA0_RDREQ_32B_sum", "TCC_EA0_RDREQ_64B_sum", "TCC_EA0_RDREQ_128B_sum")):
+            o["read_bytes_by_req"] = (32 * o["TCC_EA0_RDREQ_32B_sum"] + 64 * o["TCC_EA0_RDREQ_64B_sum"] +
+                                      128 * o["TCC_EA0_RDREQ_128B_sum"])
+        if "TCC_EA0_WRREQ_sum" in o and "TCC_EA0_WRREQ_64B_sum" in o:
+            o["write_bytes_by_req"] = 32 * (o["TCC_EA0_WRREQ_sum"] - o["TCC_EA0_WRREQ_64B_sum"]) + \
+                64 * o["TCC_EA0_WRREQ_64B_sum"]
         print(json.dumps(o))
 
 

@@ -141,3 +141,54 @@ def test_two_rank_exchange():
     for rank, err, lo, got in res:
         assert err == 0
         assert got == [lo + i + 1 for i in range(len(got))], (rank, got)
+
+
+@pytest.mark.gpu
+def test_round_deadline_aborts_without_blocking_the_host():
+    """Failure detection on one GPU: a one-rank communicator exchanges with itself
+    (vktHipCommExchange, peer = own rank).  A plain round completes and vktHipCommSynchronize
+    returns 0.  Then knob comm.test_stall_ms keeps the round's stream busy for 4 s after its
+    transfers, under a 300 ms deadline: the call returns at once (enqueued, the host is not
+    blocked), the watcher times the round from its start and aborts the communicator, so
+    vktHipCommSynchronize returns vktInvalidValue well before the stall ends, naming the
+    deadline, and the next round is refused."""
+    import time
+    import torch
+    torch.cuda.init()
+    uid = HipCommId_t()
+    assert lib.vktHipCommGetUniqueId(C.byref(uid)) == 0, _lib.last_error()
+    comm = C.c_void_p()
+    assert lib.vktHipCommInitRank(C.byref(comm), 1, uid, 0) == 0, _lib.last_error()
+    n = 1 << 20
+    a = torch.arange(n, dtype=torch.int32, device="cuda").view(torch.uint8)
+    b = torch.zeros_like(a)
+    torch.cuda.synchronize()
+    try:
+        assert lib.vktHipCommSetTimeout(comm, 5000) == 0
+        assert lib.vktHipCommExchange(comm, 0, C.c_void_p(a.data_ptr()), C.c_void_p(b.data_ptr()), a.numel()) == 0, \
+            _lib.last_error()
+        assert lib.vktHipCommSynchronize(comm) == 0, _lib.last_error()
+        torch.cuda.synchronize()
+        assert torch.equal(a, b)
+        assert lib.vktHipCommExchange(comm, 1, C.c_void_p(a.data_ptr()), C.c_void_p(b.data_ptr()), 16) != 0  # no rank 1
+
+        assert lib.vktHipSetTuningKnob(b"comm.test_stall_ms", 4000) == 0
+        assert lib.vktHipCommSetTimeout(comm, 300) == 0
+        t0 = time.monotonic()
+        assert lib.vktHipCommExchange(comm, 0, C.c_void_p(a.data_ptr()), C.c_void_p(b.data_ptr()), a.numel()) == 0, \
+            _lib.last_error()
+        enqueue_s = time.monotonic() - t0
+        lib.vktHipSetTuningKnob(b"comm.test_stall_ms", 0)
+        err = lib.vktHipCommSynchronize(comm)
+        judged_s = time.monotonic() - t0
+        msg = _lib.last_error()
+        assert err != 0 and "within 300 ms" in msg, msg
+        assert enqueue_s < 0.2, enqueue_s
+        assert judged_s < 3.0, judged_s          # the deadline fired; the 4-s stall had not ended
+        # later rounds are refused at once
+        assert lib.vktHipCommExchange(comm, 0, C.c_void_p(a.data_ptr()), C.c_void_p(b.data_ptr()), 16) != 0
+        assert "aborted" in _lib.last_error()
+    finally:
+        lib.vktHipSetTuningKnob(b"comm.test_stall_ms", 0)
+        torch.cuda.synchronize()                 # (the stall kernel leaves after its 4 s)
+        assert lib.vktHipCommDestroy(comm) == 0, _lib.last_error()

@@ -80,7 +80,7 @@ def same_codes(got, want, fmt):
     return np.array_equal(got, want)
 
 
-@pytest.mark.parametrize("transport", ["local", "peer"])
+@pytest.mark.parametrize("transport", ["local", "peer", "overlapped"])
 @pytest.mark.parametrize("nslabs", [4, 8])
 @pytest.mark.parametrize("sdims,ddims", [((40, 24, 32), (80, 48, 64)), ((37, 19, 29), (64, 40, 53)),
                                          ((32, 16, 64), (16, 16, 21))])
@@ -109,6 +109,19 @@ def test_local_halo_exchange_linear_chain(L, nslabs, sdims, ddims, transport):
     assert moved > 0, "the chain must exchange planes"
     views = (_lib.HipVolumeView_t * nslabs)(*[s.view for s in srcs])
     z0s = (C.c_int32 * nslabs)(*[s.z0 for s in srcs])
+    if transport == "overlapped":
+        # vktHipResampleSlabsOverlappedLocal: each slab's receives on the copy stream while its
+        # interior planes resample, then the rest -- equal to the whole-volume resample
+        dsts = [DevSlab(np.zeros((max(p.dst[1] - p.dst[0], 0), dy, dx), np.uint32), 7, 1, 0) for p in plans]
+        dviews = (_lib.HipVolumeView_t * nslabs)(*[d.view for d in dsts])
+        assert L.vktHipResampleSlabsOverlappedLocal(nslabs, dviews, views, z0s, dz, sz, 1, 1) == 0, err(L)
+        for r, (p, s, d) in enumerate(zip(plans, srcs, dsts)):
+            l0, l1 = p.local_src
+            assert np.array_equal(s.read(), glob[l0:l1]), f"slab {r}: halo planes not delivered"
+            d0, d1 = p.dst
+            if d1 > d0:
+                assert same_codes(d.read(), ref.codes[d0:d1], 7), f"slab {r}: overlapped resample differs"
+        return
     if transport == "local":
         assert L.vktHipSlabExchangeHaloLocal(nslabs, views, z0s, dz, sz, 1, 1) == 0, err(L)
     else:

@@ -222,6 +222,35 @@ def main():
                 report(f"{grp} SumRange {lab} {name}",
                        timed(lambda: lib.vktHipArithmeticRange(0, D, A, B, f0, f1, o), R), 3 * bpv * nv, nv)
             free(A, B, D)
+    if want("u8cal"):
+        # FETCH_SIZE calibration for the UInt8 access shapes and the
+        # whole-volume UInt8 ops against UInt16 (item 4); one launch per case for PMC passes.
+        # Known byte counts: whole volumes, whole planes (rows merged into one run per plane),
+        # 768-B rows on 128-B lines (x 128..896); then the 800-B rows at x0 = 100 / 64 with and
+        # without sector completion (knob pointwise.merge_sectors).
+        m = 1024
+        for fmt, bpv, name in ((4, 1, "UInt8"), (5, 2, "UInt16")):
+            A, B, D = alloc((m,) * 3, fmt, seed=1), alloc((m,) * 3, fmt, seed=2), alloc((m,) * 3, fmt)
+            last = Vec3i_t(m, m, m)
+            report(f"u8cal Copy 1024^3 {name}", timed(lambda: lib.vktHipCopyRange(D, A, o, last, o), R),
+                   2 * bpv * m ** 3, m ** 3)
+            report(f"u8cal SumRange 1024^3 {name}", timed(lambda: lib.vktHipArithmeticRange(0, D, A, B, o, last, o), R),
+                   3 * bpv * m ** 3, m ** 3)
+            if fmt == 4:
+                for lab, f0, f1, mg in (("planes x 0..1024", Vec3i_t(0, 100, 100), Vec3i_t(1024, 900, 900), 1),
+                                        ("x 128..896 (128-B lines)", Vec3i_t(128, 100, 100), Vec3i_t(896, 900, 900), 1),
+                                        ("x 100..900", Vec3i_t(100, 100, 100), Vec3i_t(900, 900, 900), 1),
+                                        ("x 100..900 [merge 0]", Vec3i_t(100, 100, 100), Vec3i_t(900, 900, 900), 0),
+                                        ("x 64..864", Vec3i_t(64, 100, 100), Vec3i_t(864, 900, 900), 1),
+                                        ("x 64..864 [merge 0]", Vec3i_t(64, 100, 100), Vec3i_t(864, 900, 900), 0)):
+                    lib.vktHipSetTuningKnob(b"pointwise.merge_sectors", mg)
+                    nv = (f1.x - f0.x) * (f1.y - f0.y) * (f1.z - f0.z)
+                    report(f"u8cal CopyRange {lab} same offset UInt8",
+                           timed(lambda: lib.vktHipCopyRange(D, A, f0, f1, f0), R), 2 * nv, nv)
+                    report(f"u8cal SumRange {lab} UInt8",
+                           timed(lambda: lib.vktHipArithmeticRange(0, D, A, B, f0, f1, o), R), 3 * nv, nv)
+                lib.vktHipSetTuningKnob(b"pointwise.merge_sectors", -1)
+            free(A, B, D)
     if want("f32shift"):
         # one launch per case (PMC passes): the Float32 general path with a
         # phase shift, and UInt8 SumRange on the 800^3 sub-box at x0 = 100, default knobs

@@ -4,6 +4,9 @@ prints before it runs, so a crash names its step.
 
   python tools/vmm_probe.py reuse   # hipMalloc + hipFree a block, then map at that VA
   python tools/vmm_probe.py fresh   # map at a VA the runtime picks (no prior allocation)
+  python tools/vmm_probe.py fresh torch   # the same under PyTorch's bundled HIP runtime
+  python tools/vmm_probe.py lib torch     # libvolkit arena chunk released, mapping at its VA,
+                                          # library kernels + vktHipMemcpy on the mapping
 """
 import ctypes as C
 import faulthandler
@@ -13,7 +16,14 @@ import numpy as np
 
 faulthandler.enable()
 mode = sys.argv[1] if len(sys.argv) > 1 else "fresh"
+if "torch" in sys.argv[2:]:
+    # PyTorch's wheel bundles its own HIP runtime (torch/lib/libamdhip64.so, torch.version.hip);
+    # once torch is imported, "libamdhip64.so" resolves to that copy for every library in the
+    # process (libvolkit's libamdhip64.so.7 included) instead of /opt/rocm's
+    import torch  # noqa: F401
+    mode += f" (torch {torch.version.hip} runtime)"
 hip = C.CDLL("libamdhip64.so")
+print(mode, "runtime:", sorted({ln.split()[-1] for ln in open("/proc/self/maps") if "amdhip64" in ln}), flush=True)
 SIZE = 256 << 20
 
 
@@ -46,7 +56,39 @@ def say(name):
 
 step("hipSetDevice", hip.hipSetDevice(0))
 hint = None
-if mode == "reuse":
+lib = None
+N = (256, 256, 512)                                  # UInt16: 64 MiB per volume (lib mode)
+NB = 2 * N[0] * N[1] * N[2]
+if sys.argv[1:2] == ["lib"]:
+    # the round-5 test's sequence through libvolkit: three arena volumes carved from one
+    # 256-MiB chunk, Synthesize + SumRange, freed (the chunk goes back to HIP); the mapping below
+    # asks for the chunk's VA and the library runs the same kernels and its D2H copy on it
+    import os
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from volkit_amd._lib import lib, last_error, HipVolumeView_t, Vec3i_t   # noqa: E402
+    step("arena_chunk_mib", lib.vktHipSetTuningKnob(b"memory.arena_chunk_mib", 256))
+
+    def lib_sumrange(ptrs, tag):
+        A, B, D = (HipVolumeView_t(p, N[0], N[1], N[2], 5, 0.0, 1.0) for p in ptrs)
+        o, last = Vec3i_t(0, 0, 0), Vec3i_t(*N)
+        step(f"{tag} Synthesize", lib.vktHipSynthesize(A, C.c_uint64(11)) or lib.vktHipSynthesize(B, C.c_uint64(12)))
+        step(f"{tag} SumRange", lib.vktHipArithmeticRange(0, D, A, B, o, last, o))
+        step(f"{tag} device sync", hip.hipDeviceSynchronize())
+        out = np.empty(NB, np.uint8)
+        say(f"{tag} vktHipMemcpy D2H 64 MiB from the third volume")
+        step(f"{tag} vktHipMemcpy", lib.vktHipMemcpy(out.ctypes.data, C.c_void_p(ptrs[2]), NB, 2))
+        return out
+
+    ptrs = []
+    for _ in range(3):
+        q = C.c_void_p()
+        step("vktHipAllocate", lib.vktHipAllocate(C.byref(q), NB))
+        ptrs.append(q.value)
+    want = lib_sumrange(ptrs, "arena")
+    for q in ptrs:
+        step("vktHipFree", lib.vktHipFree(C.c_void_p(q)))
+    hint = min(ptrs)
+elif mode == "reuse":
     p = C.c_void_p()
     step("hipMalloc", hip.hipMalloc(C.byref(p), C.c_size_t(SIZE)))
     step("hipMemset", hip.hipMemset(p, 1, C.c_size_t(SIZE)))
@@ -67,6 +109,9 @@ acc = Access(Loc(1, 0), 3)
 step("hipMemSetAccess", hip.hipMemSetAccess(va, C.c_size_t(SIZE), C.byref(acc), C.c_size_t(1)))
 step("hipMemset(vmm)", hip.hipMemset(va, 7, C.c_size_t(SIZE)))
 step("hipDeviceSynchronize", hip.hipDeviceSynchronize())
+if lib is not None:
+    got = lib_sumrange([va.value, va.value + NB, va.value + 2 * NB], "mapping")
+    print(f"{mode}: SumRange on the mapping equals the arena run: {np.array_equal(got, want)}", flush=True)
 s = C.c_void_p()
 step("hipStreamCreate", hip.hipStreamCreate(C.byref(s)))
 # D2H copies into pageable memory: 1 MiB / 64 MiB, from the mapping's first byte and from an

@@ -260,6 +260,11 @@ SIGNATURES = {
     "vktHipCommInitRank": (c_err, [P(c_comm), i32, HipCommId_t, i32]),
     "vktHipCommDestroy": (c_err, [c_comm]),
     "vktHipCommSetTimeout": (c_err, [c_comm, C.c_int64]),
+    "vktHipCommSynchronize": (c_err, [c_comm]),
+    "vktHipCommExchange": (c_err, [c_comm, i32, C.c_void_p, C.c_void_p, C.c_size_t]),
+    "vktHipResampleSlabOverlapped": (c_err, [c_comm, HipVolumeView_t, HipVolumeView_t, i32, i32, i32, C.c_int, i32]),
+    "vktHipResampleSlabsOverlappedLocal": (c_err, [i32, P(HipVolumeView_t), P(HipVolumeView_t), P(i32), i32, i32,
+                                                   C.c_int, i32]),
     "vktHipSlabExchangeHalo": (c_err, [c_comm, HipVolumeView_t, i32, i32, i32, C.c_int, i32]),
     "vktHipSlabExchangeHaloLocal": (c_err, [i32, P(HipVolumeView_t), P(i32), i32, i32, C.c_int, i32]),
     "vktHipSlabExchangeHaloPeer": (c_err, [i32, P(HipVolumeView_t), P(i32), P(i32), i32, i32, C.c_int, i32]),

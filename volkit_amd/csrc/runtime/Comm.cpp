@@ -172,53 +172,117 @@ namespace comm
     }
 
     // Aborts the communicator after a failed / timed-out round (its kernels exit; every later
-    // call on it fails fast).
-    vktError abortComm(vktHipComm_t c, std::string const& why)
+    // call on it fails fast).  c->m held.
+    void abortLocked(vktHipComm_t c, std::string const& why)
     {
-        if (!c->aborted && c->comm != nullptr)
+        if (!c->aborted.load() && c->comm != nullptr)
             (void)rccl().abort(c->comm);
-        c->aborted = true;
         c->comm = nullptr;
-        return rt::fail((why + " (communicator aborted)").c_str());
+        if (c->failure.empty())
+            c->failure = why + " (communicator aborted)";
+        c->aborted.store(true);
     }
 
-    // Host wait for the round just enqueued on `stream`, under c->timeoutMs.
-    vktError waitRound(vktHipComm_t c, hipStream_t stream, char const* what)
+    // A kernel that keeps one wave busy for `ms` milliseconds of wall clock (knob
+    // comm.test_stall_ms: a round that outlives its deadline, for the watcher's test); every
+    // wave leaves once the time is up.
+    __global__ void stallKernel(uint64_t ticks)
     {
-        hipEvent_t ev = nullptr;
-        VKT_HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        vktError e = rt::check(hipEventRecord(ev, stream), "hipEventRecord(rcclRound)");
+        uint64_t const t0 = wall_clock64();
+        while (wall_clock64() - t0 < ticks)
+            __builtin_amdgcn_s_sleep(64);
+    }
+
+    vktError stall(hipStream_t stream, int64_t ms)
+    {
+        int khz = 0;
+        VKT_HIP_TRY(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, rt::device()));
+        hipLaunchKernelGGL(stallKernel, dim3(1), dim3(64), 0, stream, static_cast<uint64_t>(ms) * static_cast<uint64_t>(khz));
+        return rt::check(hipGetLastError(), "stallKernel");
+    }
+
+    // Polls an event until it completes; false (and *err set) on an error of the event, an
+    // asynchronous RCCL error or, with a deadline (ms > 0, counted from the call), a timeout.
+    bool pollEvent(vktHipComm_t c, hipEvent_t ev, int64_t ms, std::string& err)
+    {
         auto const t0 = std::chrono::steady_clock::now();
-        for (uint32_t polls = 0; e == vktNoError; ++polls)
+        for (uint32_t polls = 0;; ++polls)
         {
             hipError_t const q = hipEventQuery(ev);
             if (q == hipSuccess)
-                break;
+                return true;
             if (q != hipErrorNotReady)
             {
-                e = rt::check(q, what);
-                break;
+                err = std::string("hipEventQuery: ") + hipGetErrorString(q);
+                return false;
+            }
+            ncclComm_t nc = nullptr;
+            {
+                std::lock_guard<std::mutex> g(c->m);
+                nc = c->comm;
             }
             ncclResult_t as = ncclSuccess;
-            if (rccl().getAsyncError != nullptr && rccl().getAsyncError(c->comm, &as) == ncclSuccess &&
+            if (nc != nullptr && rccl().getAsyncError != nullptr && rccl().getAsyncError(nc, &as) == ncclSuccess &&
                 as != ncclSuccess && as != ncclInProgress)
             {
-                e = abortComm(c, std::string(what) + ": RCCL asynchronous error: " + rccl().errorString(as));
-                break;
+                err = std::string("RCCL asynchronous error: ") + rccl().errorString(as);
+                return false;
             }
-            auto const ms = std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0);
-            if (ms.count() >= c->timeoutMs)
+            if (ms > 0 && std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0)
+                                  .count() >= ms)
             {
-                e = abortComm(c, std::string(what) + ": a peer did not complete its side of the round within " +
-                                     std::to_string(c->timeoutMs) + " ms");
-                break;
+                err = "a peer did not complete its side of the round within " + std::to_string(ms) + " ms";
+                return false;
             }
             // spin briefly (a halo round on xGMI takes tens of microseconds), then back off
             if (polls > 256)
                 std::this_thread::sleep_for(std::chrono::microseconds(polls > 4096 ? 1000 : 50));
         }
-        (void)hipEventDestroy(ev);
-        return e;
+    }
+
+    // The watcher thread of a communicator: judges its rounds in order (comm/Comm.hpp).
+    void watch(vktHipComm_t c)
+    {
+        (void)hipSetDevice(c->device);
+        for (;;)
+        {
+            vktHipComm_impl::Round r;
+            {
+                std::unique_lock<std::mutex> g(c->m);
+                c->cv.wait(g, [&] { return c->stop || !c->rounds.empty(); });
+                if (c->rounds.empty())
+                    return;
+                r = c->rounds.front();
+            }
+            std::string err;
+            // the round starts when the work queued ahead of it has finished: that wait has no
+            // deadline of the round's (it is not the round's time) ...
+            bool ok = pollEvent(c, r.start, 0, err);
+            // ... its transfers have one, counted from their start
+            ok = ok && pollEvent(c, r.end, r.timeoutMs, err);
+            ncclComm_t dead = nullptr;
+            {
+                std::lock_guard<std::mutex> g(c->m);
+                if (!ok)
+                {
+                    // the failure is known now: record it and refuse later rounds before the
+                    // abort, which returns only once the communicator's queued work has left
+                    // the GPU (its kernels exit on the abort flag)
+                    if (c->failure.empty())
+                        c->failure = r.what + ": " + err + " (communicator aborted)";
+                    dead = c->aborted.load() ? nullptr : c->comm;
+                    c->comm = nullptr;
+                    c->aborted.store(true);
+                    VKT_LOG(rt::LogLevel::Error) << c->failure;
+                }
+                c->rounds.pop_front();
+            }
+            c->cv.notify_all();
+            if (dead != nullptr)
+                (void)rccl().abort(dead);
+            (void)hipEventDestroy(r.start);
+            (void)hipEventDestroy(r.end);
+        }
     }
 
     vktError rcclRound(vktHipComm_t c, std::vector<Xfer> const& xs, hipStream_t stream, char const* what)
@@ -227,25 +291,137 @@ namespace comm
             return vktNoError;
         if (!rccl().ok)
             return noRccl(what);
-        if (c->aborted)
-            return rt::fail((std::string(what) + ": the communicator was aborted after an earlier failure").c_str());
-        ncclResult_t r = rccl().groupStart();
-        if (r != ncclSuccess)
-            return ncclFail((std::string(what) + ": ncclGroupStart").c_str(), r);
-        for (Xfer const& x : xs)
+        std::unique_lock<std::mutex> g(c->m);
+        if (c->aborted.load())
+            return rt::fail((std::string(what) + ": the communicator was aborted after an earlier failure: " + c->failure)
+                                .c_str());
+        int64_t const deadline = c->timeoutMs;
+        vktHipComm_impl::Round r;
+        if (deadline > 0)
         {
-            r = x.send ? rccl().send(x.ptr, x.bytes, ncclUint8, x.peer, c->comm, stream)
-                       : rccl().recv(x.ptr, x.bytes, ncclUint8, x.peer, c->comm, stream);
-            if (r != ncclSuccess)
+            if (rt::check(hipEventCreateWithFlags(&r.start, hipEventDisableTiming), "hipEventCreate") != vktNoError ||
+                rt::check(hipEventCreateWithFlags(&r.end, hipEventDisableTiming), "hipEventCreate") != vktNoError ||
+                rt::check(hipEventRecord(r.start, stream), "hipEventRecord(round start)") != vktNoError)
             {
-                (void)rccl().groupEnd();
-                return ncclFail((std::string(what) + ": ncclSend/ncclRecv").c_str(), r);
+                (void)hipEventDestroy(r.start);
+                (void)hipEventDestroy(r.end);
+                return vktInvalidValue;
             }
         }
-        r = rccl().groupEnd();
-        if (r != ncclSuccess)
-            return abortComm(c, std::string(what) + ": ncclGroupEnd: " + rccl().errorString(r));
-        return c->timeoutMs > 0 ? waitRound(c, stream, what) : vktNoError;
+        ncclResult_t res = rccl().groupStart();
+        if (res != ncclSuccess)
+            return ncclFail((std::string(what) + ": ncclGroupStart").c_str(), res);
+        for (Xfer const& x : xs)
+        {
+            res = x.send ? rccl().send(x.ptr, x.bytes, ncclUint8, x.peer, c->comm, stream)
+                         : rccl().recv(x.ptr, x.bytes, ncclUint8, x.peer, c->comm, stream);
+            if (res != ncclSuccess)
+            {
+                (void)rccl().groupEnd();
+                return ncclFail((std::string(what) + ": ncclSend/ncclRecv").c_str(), res);
+            }
+        }
+        res = rccl().groupEnd();
+        if (res != ncclSuccess)
+        {
+            abortLocked(c, std::string(what) + ": ncclGroupEnd: " + rccl().errorString(res));
+            return rt::fail(c->failure.c_str());
+        }
+        if (deadline <= 0)
+            return vktNoError;
+        // (test knob comm.test_stall_ms: the round outlives its deadline after its transfers)
+        int64_t const stallMs = rt::knob(rt::Knob::CommTestStallMs);
+        if (stallMs > 0)
+            (void)stall(stream, stallMs);
+        if (rt::check(hipEventRecord(r.end, stream), "hipEventRecord(round end)") != vktNoError)
+        {
+            (void)hipEventDestroy(r.start);
+            (void)hipEventDestroy(r.end);
+            return vktInvalidValue;
+        }
+        r.timeoutMs = deadline;
+        r.what = what;
+        c->rounds.push_back(r);
+        if (!c->watcher.joinable())
+            c->watcher = std::thread(watch, c);
+        g.unlock();
+        c->cv.notify_all();
+        return vktNoError;
+    }
+
+    // Planes [a, b) of a view holding global planes [z0, z0 + v.dimZ).
+    vktHipVolumeView_t planesOf(vktHipVolumeView_t v, int32_t z0, int32_t a, int32_t b)
+    {
+        v.data += static_cast<size_t>(a - z0) * planeBytes(v);
+        v.dimZ = b - a;
+        return v;
+    }
+
+    // The halo exchange of one rank overlapped with its interior (slab.py:resample_slab_overlapped):
+    // `transport(side)` enqueues the rank's moves on the side stream after the work queued so far
+    // on the compute stream; the dst planes that read only owned source planes resample on the
+    // compute stream meanwhile (a source sub-view of exactly those planes, so nothing reads the
+    // planes in flight); the compute stream then waits for the moves and resamples the rest.
+    // Every part is a slab resample of its own (the same exact index tables): the result equals
+    // exchange + vktHipResampleSlab.
+    template <class Transport>
+    vktError overlappedResample(vktHipVolumeView_t dst, vktHipVolumeView_t src, int32_t localZ0, int32_t rank,
+                                int32_t world, int32_t dstG, int32_t srcG, vktFilterMode fm, int32_t chain,
+                                bool receives, hipStream_t side, Transport&& transport, char const* what)
+    {
+        int32_t d0, d1, o0, o1;
+        slabBounds(dstG, world, rank, d0, d1);
+        slabBounds(srcG, world, rank, o0, o1);
+        if (dst.dimZ != d1 - d0)
+            return rt::fail((std::string(what) + ": dst must hold exactly the rank's dst slab").c_str());
+        // dk: [d0, dk) reads only owned planes (binary search, slab.py:interior_split)
+        int32_t dk = d1;
+        if (receives && d1 > d0)
+        {
+            int32_t lo = d0, hi = d1;
+            while (lo < hi)
+            {
+                int32_t const mid = lo + (hi - lo + 1) / 2;
+                int32_t b = 0, en = 0;
+                vktError const err = vktHipResampleSlabSourceRange(dstG, d0, mid, srcG, fm, chain, &b, &en);
+                if (err != vktNoError)
+                    return err;
+                if (b >= o0 && en <= o1)
+                    lo = mid;
+                else
+                    hi = mid - 1;
+            }
+            dk = lo;
+        }
+        hipStream_t const cs = rt::computeStream();
+        hipEvent_t ready = nullptr, moved = nullptr;
+        VKT_HIP_TRY(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+        vktError e = rt::check(hipEventCreateWithFlags(&moved, hipEventDisableTiming), "hipEventCreate");
+        if (e == vktNoError)
+            e = rt::check(hipEventRecord(ready, cs), "hipEventRecord(compute)");
+        if (e == vktNoError)
+            e = rt::check(hipStreamWaitEvent(side, ready, 0), "hipStreamWaitEvent(side)");
+        if (e == vktNoError)
+            e = transport(side);
+        if (e == vktNoError)
+            e = rt::check(hipEventRecord(moved, side), "hipEventRecord(side)");
+        for (int part = 0; part < 2 && e == vktNoError; ++part)
+        {
+            int32_t const a = part == 0 ? d0 : dk, b = part == 0 ? dk : d1;
+            if (part == 1)
+                e = rt::check(hipStreamWaitEvent(cs, moved, 0), "hipStreamWaitEvent(compute)");
+            if (e != vktNoError || b <= a)
+                continue;
+            int32_t s0 = 0, s1 = 0;
+            e = vktHipResampleSlabSourceRange(dstG, a, b, srcG, fm, chain, &s0, &s1);
+            if (e == vktNoError && (s0 < localZ0 || s1 > localZ0 + src.dimZ))
+                e = rt::fail((std::string(what) + ": the source slab does not hold the planes the dst slab reads").c_str());
+            if (e == vktNoError)
+                e = vktHipResampleSlab(planesOf(dst, d0, a, b), planesOf(src, localZ0, s0, s1), fm, dstG, a, srcG, s0);
+        }
+        (void)hipEventDestroy(ready);
+        (void)hipEventDestroy(moved);
+        return e;
     }
 
     vktError localMove(uint8_t* dst, uint8_t const* src, size_t bytes, hipStream_t stream, char const* what)
@@ -316,7 +492,8 @@ vktError vktHipCommInitRank(vktHipComm_t* comm, int32_t nranks, vktHipCommId_t i
     }
     c->rank = rank;
     c->nranks = nranks;
-    // default round deadline: VKT_COMM_TIMEOUT_MS (0 = rounds return once enqueued), else 300 s
+    c->device = rt::device();
+    // default round deadline: VKT_COMM_TIMEOUT_MS (0 = no deadline), else 300 s
     char const* env = std::getenv("VKT_COMM_TIMEOUT_MS");
     c->timeoutMs = env != nullptr ? std::max<int64_t>(0, std::strtoll(env, nullptr, 10)) : 300000;
     *comm = c;
@@ -327,7 +504,19 @@ vktError vktHipCommSetTimeout(vktHipComm_t comm, int64_t milliseconds)
 {
     if (comm == nullptr || milliseconds < 0)
         return rt::fail("vktHipCommSetTimeout: null communicator or negative timeout");
+    std::lock_guard<std::mutex> g(comm->m);
     comm->timeoutMs = milliseconds;
+    return vktNoError;
+}
+
+vktError vktHipCommSynchronize(vktHipComm_t comm)
+{
+    if (comm == nullptr)
+        return rt::fail("vktHipCommSynchronize: null communicator");
+    std::unique_lock<std::mutex> g(comm->m);
+    comm->cv.wait(g, [&] { return comm->rounds.empty(); });
+    if (comm->aborted.load())
+        return rt::fail(comm->failure.c_str());
     return vktNoError;
 }
 
@@ -335,7 +524,16 @@ vktError vktHipCommDestroy(vktHipComm_t comm)
 {
     if (comm == nullptr)
         return vktNoError;
-    ncclResult_t const r = comm->aborted ? ncclSuccess : rccl().commDestroy(comm->comm);
+    {
+        std::lock_guard<std::mutex> g(comm->m);
+        comm->stop = true;   // the watcher judges the rounds still queued, then leaves
+    }
+    comm->cv.notify_all();
+    if (comm->watcher.joinable())
+        comm->watcher.join();
+    ncclResult_t const r = comm->aborted.load() || comm->comm == nullptr ? ncclSuccess : rccl().commDestroy(comm->comm);
+    if (comm->stream != nullptr)
+        (void)hipStreamDestroy(comm->stream);
     delete comm;
     return r == ncclSuccess ? vktNoError : ncclFail("vktHipCommDestroy", r);
 }
@@ -507,6 +705,104 @@ vktError vktHipSlabExchangeHaloPeer(int32_t numSlabs, vktHipVolumeView_t const* 
         e = rt::check(hipStreamSynchronize(rt::computeStream()), "hipStreamSynchronize");
     (void)hipEventDestroy(queued);
     return e != vktNoError ? e : rt::finishLaunch("SlabExchangeHaloPeer_hip");
+}
+
+vktError vktHipCommExchange(vktHipComm_t comm, int32_t peer, void const* sendBuf, void* recvBuf, size_t bytes)
+{
+    if (comm == nullptr || peer < 0 || peer >= comm->nranks || (bytes > 0 && (sendBuf == nullptr || recvBuf == nullptr)))
+        return rt::fail("vktHipCommExchange: null communicator / buffer or peer out of range");
+    std::vector<comm::Xfer> xs;
+    if (bytes > 0)
+    {
+        xs.push_back(comm::Xfer{peer, 1, static_cast<uint8_t*>(const_cast<void*>(sendBuf)), bytes});
+        xs.push_back(comm::Xfer{peer, 0, static_cast<uint8_t*>(recvBuf), bytes});
+    }
+    vktError const e = comm::rcclRound(comm, xs, rt::computeStream(), "vktHipCommExchange");
+    return e != vktNoError ? e : rt::finishLaunch("CommExchange_hip");
+}
+
+vktError vktHipResampleSlabOverlapped(vktHipComm_t comm, vktHipVolumeView_t dst, vktHipVolumeView_t localSrc,
+                                      int32_t localZ0, int32_t dstGlobalDimZ, int32_t srcGlobalDimZ, vktFilterMode fm,
+                                      int32_t needsNeighbours)
+{
+    char const* const what = "vktHipResampleSlabOverlapped";
+    if (comm == nullptr)
+        return rt::fail("vktHipResampleSlabOverlapped: null communicator");
+    int32_t lo, hi;
+    std::vector<vktHipSlabTransfer_t> xs;
+    vktError e = plan(dstGlobalDimZ, srcGlobalDimZ, comm->nranks, comm->rank, fm, needsNeighbours, lo, hi, xs);
+    if (e != vktNoError)
+        return e;
+    std::vector<comm::Xfer> moves;
+    bool receives = false;
+    for (vktHipSlabTransfer_t const& x : xs)
+    {
+        comm::Xfer m{x.peer, x.send, nullptr, 0};
+        e = comm::planeSpan(localSrc, localZ0, x.z0, x.z1, what, m.ptr, m.bytes);
+        if (e != vktNoError)
+            return e;
+        receives = receives || !x.send;
+        moves.push_back(m);
+    }
+    {
+        std::lock_guard<std::mutex> g(comm->m);
+        if (comm->stream == nullptr &&
+            rt::check(hipStreamCreateWithFlags(&comm->stream, hipStreamNonBlocking), "hipStreamCreate(comm)") != vktNoError)
+            return vktInvalidValue;
+    }
+    e = comm::overlappedResample(dst, localSrc, localZ0, comm->rank, comm->nranks, dstGlobalDimZ, srcGlobalDimZ, fm,
+                                 needsNeighbours, receives, comm->stream,
+                                 [&](hipStream_t side) { return comm::rcclRound(comm, moves, side, what); }, what);
+    return e != vktNoError ? e : rt::finishLaunch("ResampleSlabOverlapped_hip");
+}
+
+vktError vktHipResampleSlabsOverlappedLocal(int32_t numSlabs, vktHipVolumeView_t const* dst,
+                                            vktHipVolumeView_t const* localSrc, int32_t const* localZ0,
+                                            int32_t dstGlobalDimZ, int32_t srcGlobalDimZ, vktFilterMode fm,
+                                            int32_t needsNeighbours)
+{
+    char const* const what = "vktHipResampleSlabsOverlappedLocal";
+    if (numSlabs <= 0 || dst == nullptr || localSrc == nullptr || localZ0 == nullptr)
+        return rt::fail("vktHipResampleSlabsOverlappedLocal: invalid slab arrays");
+    for (int32_t r = 0; r < numSlabs; ++r)
+    {
+        int32_t lo, hi;
+        std::vector<vktHipSlabTransfer_t> xs;
+        vktError e = plan(dstGlobalDimZ, srcGlobalDimZ, numSlabs, r, fm, needsNeighbours, lo, hi, xs);
+        if (e != vktNoError)
+            return e;
+        // the receives of slab r: device copies from the owning slabs' buffers (the sends are
+        // the other side of the same moves)
+        std::vector<std::pair<uint8_t*, uint8_t const*>> to;
+        std::vector<size_t> bytes;
+        for (vktHipSlabTransfer_t const& x : xs)
+        {
+            if (x.send)
+                continue;
+            uint8_t *t, *f;
+            size_t n, m;
+            e = comm::planeSpan(localSrc[r], localZ0[r], x.z0, x.z1, what, t, n);
+            if (e == vktNoError)
+                e = comm::planeSpan(localSrc[x.peer], localZ0[x.peer], x.z0, x.z1, what, f, m);
+            if (e == vktNoError && n != m)
+                e = rt::fail("vktHipResampleSlabsOverlappedLocal: slabs of different plane sizes");
+            if (e != vktNoError)
+                return e;
+            to.emplace_back(t, f);
+            bytes.push_back(n);
+        }
+        auto copies = [&](hipStream_t side) {
+            for (size_t k = 0; k < to.size(); ++k)
+                if (vktError const ce = comm::localMove(to[k].first, to[k].second, bytes[k], side, what); ce != vktNoError)
+                    return ce;
+            return vktNoError;
+        };
+        e = comm::overlappedResample(dst[r], localSrc[r], localZ0[r], r, numSlabs, dstGlobalDimZ, srcGlobalDimZ, fm,
+                                     needsNeighbours, !to.empty(), rt::copyStream(), copies, what);
+        if (e != vktNoError)
+            return e;
+    }
+    return rt::finishLaunch("ResampleSlabsOverlappedLocal_hip");
 }
 
 } // extern "C"

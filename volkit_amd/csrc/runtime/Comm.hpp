@@ -7,18 +7,43 @@
 
 #include <rccl/rccl.h>
 
+#include <atomic>
+#include <condition_variable>
 #include <cstddef>
 #include <cstdint>
+#include <deque>
+#include <mutex>
+#include <string>
+#include <thread>
 #include <vector>
 
+// A communicator and its round watcher.  Every RCCL round returns once enqueued; with a
+// deadline (timeoutMs > 0) the round's start / end events go to the watcher thread, which times
+// the round from the moment its start event completes (work queued ahead of it is not the
+// round's), polls ncclCommGetAsyncError, and on a timeout or an asynchronous error aborts the
+// communicator: its kernels exit, and every later call on it -- and vktHipCommSynchronize --
+// returns vktInvalidValue naming the failure.
 struct vktHipComm_impl
 {
+    struct Round
+    {
+        hipEvent_t start = nullptr, end = nullptr;
+        int64_t timeoutMs = 0;
+        std::string what;
+    };
+
     ncclComm_t comm = nullptr;
     int32_t rank = 0, nranks = 0;
-    // rcclRound waits (host) up to timeoutMs for each round, polling ncclCommGetAsyncError;
-    // 0: returns once the round is enqueued (vktHipCommSetTimeout, VKT_COMM_TIMEOUT_MS)
-    int64_t timeoutMs = 0;
-    bool aborted = false;   // a round failed or timed out: the communicator was aborted
+    int device = 0;
+    int64_t timeoutMs = 0;            // vktHipCommSetTimeout, VKT_COMM_TIMEOUT_MS; 0: no deadline
+    hipStream_t stream = nullptr;     // the communicator's own stream (overlapped rounds), lazily
+    std::mutex m;                     // comm use (enqueue / abort), rounds, failure
+    std::condition_variable cv;
+    std::deque<Round> rounds;         // enqueued, not yet judged (front: being judged)
+    std::thread watcher;
+    bool stop = false;
+    std::atomic<bool> aborted{false}; // a round failed or timed out: the communicator was aborted
+    std::string failure;              // why (the first failure)
 };
 
 namespace vkt
@@ -46,10 +71,11 @@ namespace comm
     };
 
     // The moves as ONE ncclGroupStart .. ncclGroupEnd round of ncclSend / ncclRecv on `stream`
-    // (pairs of ranks match their moves in issue order).  With comm->timeoutMs > 0 the host then
-    // waits for the round under that deadline, polling ncclCommGetAsyncError: a peer that never
-    // joins, or an asynchronous RCCL error, aborts the communicator and returns vktInvalidValue
-    // instead of leaving every later call on the stream hanging (SURVEY §5 failure detection).
+    // (pairs of ranks match their moves in issue order); returns once enqueued.  With
+    // comm->timeoutMs > 0 the watcher judges the round under that deadline (see above): a peer
+    // that never joins, or an asynchronous RCCL error, aborts the communicator instead of leaving
+    // every later call on the stream hanging (SURVEY §5 failure detection).  A call on an
+    // aborted communicator fails at once.
     vktError rcclRound(vktHipComm_t comm, std::vector<Xfer> const& xs, hipStream_t stream, char const* what);
 
     // A device-to-device copy on `stream` (the in-process transport: every slab of a

@@ -246,6 +246,7 @@ namespace rt
             {"decompose.pipe", 0},
             {"decompose.pair", 0},
             {"memory.fail_next_alloc", 0},
+            {"comm.test_stall_ms", 0},
         };
         static_assert(sizeof(kKnobs) / sizeof(kKnobs[0]) == static_cast<size_t>(Knob::Count), "knob table");
         std::atomic<int64_t> gKnobs[static_cast<int>(Knob::Count)] = {{kKnobs[0].def}, {kKnobs[1].def},
@@ -262,7 +263,8 @@ namespace rt
                                                                   {kKnobs[22].def}, {kKnobs[23].def},
                                                                   {kKnobs[24].def}, {kKnobs[25].def},
                                                                   {kKnobs[26].def}, {kKnobs[27].def},
-                                                                  {kKnobs[28].def}, {kKnobs[29].def}};
+                                                                  {kKnobs[28].def}, {kKnobs[29].def},
+                                                                  {kKnobs[30].def}};
     } // namespace
 
     int64_t knob(Knob k) { return gKnobs[static_cast<int>(k)].load(std::memory_order_relaxed); }

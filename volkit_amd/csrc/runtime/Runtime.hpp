@@ -124,6 +124,7 @@ namespace rt
         DecomposePipe,                 // 1: uniform brick grids on a resident, double-buffered walk (measured slower: off)
         DecomposePair,                 // 1: two x-neighbour bricks of <= 16 KiB per workgroup (uniform grids)
         MemoryFailNextAlloc,           // n > 0: the next n device allocations fail (tests of the failure paths)
+        CommTestStallMs,               // > 0: every RCCL round with a deadline also stalls its stream this long (watcher test)
         Count
     };
     int64_t knob(Knob k);
