@@ -177,13 +177,14 @@ def test_brick_decompose_128_thread_workgroups(fmt, dims, brick, neg, pos, grid)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("aligned", [1, 2])
+@pytest.mark.parametrize("aligned", [0, 1, 2, 3])
 @pytest.mark.parametrize("fmt", [4, 5, 7])
 @pytest.mark.parametrize("dims,brick,neg,pos", LAYOUTS[1:4] + LAYOUTS[6:])
 def test_brick_decompose_aligned_lds_pieces(fmt, dims, brick, neg, pos, aligned):
-    """The staged copy with its row-end words (knob decompose.aligned_lds = 1) or every word
-    (= 2) written to LDS as naturally aligned pieces instead of unaligned 16-B writes / per-voxel
-    loops: the same bricks as the oracle."""
+    """The staged copy's LDS writes of the words cut by a row end or the chunk, per knob
+    decompose.aligned_lds: 0 per-voxel loop, 1 naturally aligned pieces (2: every word so), 3 all
+    voxels written with the ones outside sent to the tile's unused tail (chunks that leave 16 B
+    free; full chunks keep the loop): the same bricks as the oracle."""
     rng = np.random.default_rng(fmt * 100 + sum(dims) + aligned)
     codes = rand_codes(rng, fmt, dims[::-1])
     assert lib.vktHipSetTuningKnob(b"decompose.aligned_lds", aligned) == 0

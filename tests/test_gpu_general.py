@@ -182,6 +182,46 @@ def test_collapsed_row_contiguous_lanes(lib, o, fmt, pad):
     assert_codes_equal(d.read(), ref, fmt, f"fill fmt={fmt} pad={pad}")
 
 
+@pytest.mark.parametrize("fmt", [4, 5, 7])
+@pytest.mark.parametrize("knobs", [(1, 4, 8192), (1, 2, 0), (1, 8, 6656), (0, 4, 0), (3, 1, 0), (3, 2, 5632)])
+def test_row_kernel(lib, o, fmt, knobs):
+    """The MODE-0-only kernel for one collapsed row (pointwiseRowKernel: UInt8 / UInt16 copies and
+    arithmetic, knob pointwise.row_kernel bits 0 / 1, with the items per lane of
+    pointwise.u8_unroll / u16_unroll and the occupancy cap pointwise.row_lds; Float32 keeps the
+    general kernel): voxel counts
+    that are whole 8-voxel items (no scalar edges -- the condition for the kernel), full and
+    partial quanta, 16-B and 8-B aligned views.  Sum / SafeDiff / Prod, Copy and Fill vs the
+    oracle."""
+    from volkit_amd._lib import lib as L
+    rk, unroll, lds = knobs
+    rng = np.random.default_rng(fmt * 100 + unroll)
+    try:
+        for k, v in ((b"pointwise.row_kernel", rk), (b"pointwise.u8_unroll", unroll if fmt == 4 else 2),
+                     (b"pointwise.u16_unroll", unroll if fmt == 5 and unroll <= 2 else 2), (b"pointwise.row_lds", lds),
+                     (b"pointwise.row_lds_u8", lds)):
+            assert L.vktHipSetTuningKnob(k, v) == 0
+        for dims in ((3, 7, 616), (1, 1, 4096), (2, 5, 1032)):
+            a, b, dinit = (rand_codes(rng, fmt, dims) for _ in range(3))
+            first, last = (0, 0, 0), (dims[2], dims[1], dims[0])
+            for pad in (0, 8):
+                for op in ("Sum", "SafeDiff", "Prod"):
+                    da, db, dd = Dev(a, fmt, pad=pad), Dev(b, fmt, pad=pad), Dev(dinit, fmt, pad=pad)
+                    assert L.vktHipArithmeticRange(OPS.index(op), dd.view, da.view, db.view, vec(first), vec(last),
+                                                   vec((0, 0, 0))) == 0, last_error()
+                    ref = o.arith(op, [fmt] * 3, [(0.0, 1.0)] * 3, a, b, dinit.copy(), first, last, (0, 0, 0))
+                    assert_codes_equal(dd.read(), ref, fmt, f"{op} fmt={fmt} dims={dims} pad={pad} knobs={knobs}")
+                copy_case(lib, o, fmt, fmt, (0.0, 1.0), (0.0, 1.0), a, dinit, first, last, (0, 0, 0), pad, pad,
+                          f"copy fmt={fmt} dims={dims} pad={pad} knobs={knobs}")
+                d = Dev(dinit, fmt, pad=pad)
+                assert L.vktHipFillRange(d.view, vec(first), vec(last), C.c_float(0.375)) == 0, last_error()
+                ref = o.fill_range(fmt, (0.0, 1.0), (dims[2], dims[1], dims[0]), dinit.copy(), first, last, 0.375)
+                assert_codes_equal(d.read(), ref, fmt, f"fill fmt={fmt} dims={dims} pad={pad} knobs={knobs}")
+    finally:
+        for k in (b"pointwise.row_kernel", b"pointwise.u8_unroll", b"pointwise.u16_unroll", b"pointwise.row_lds",
+                  b"pointwise.row_lds_u8"):
+            L.vktHipSetTuningKnob(k, -1)
+
+
 @pytest.mark.parametrize("fmt", [4, 7, 6])
 @pytest.mark.parametrize("box", [((0, 1, 1), (256, 30, 6)),      # rows of 32 items (even)
                                  ((16, 2, 0), (136, 29, 7)),     # 15 items per row

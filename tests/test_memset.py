@@ -365,3 +365,48 @@ def test_arena_chunk_release_then_fresh_allocation_at_that_va():
         assert np.array_equal(got, want) and np.array_equal(got2, want)
     finally:
         lib.vktHipSetTuningKnob(b"memory.arena_chunk_mib", 0)
+
+
+@pytest.mark.gpu
+def test_public_free_waits_for_foreign_streams():
+    """A buffer from vktHipAllocate that the caller keeps busy on a non-blocking stream of its own
+    (torch's), freed with vktHipFree while that work is queued: the next allocation of the size
+    (a full 64-MiB arena chunk: it must reuse that block) gets it back only after a device
+    synchronisation, so the library's Fill into it lands after the foreign writes and the buffer
+    reads back the Fill's codes."""
+    import torch
+    from volkit_amd._lib import lib, last_error, HipVolumeView_t, Vec3i_t
+    torch.cuda.set_device(0)
+    n = 256                                           # UInt16 256^3: 32 MiB, an arena block
+    nb = 2 * n ** 3
+    lib.vktHipReleaseCachedMemory(None)
+    assert lib.vktHipSetTuningKnob(b"memory.arena_chunk_mib", 64) == 0   # two blocks fill a chunk
+    keep, p = C.c_void_p(), C.c_void_p()
+    assert lib.vktHipAllocate(C.byref(keep), nb) == 0, last_error()
+    assert lib.vktHipAllocate(C.byref(p), nb) == 0, last_error()
+    side = torch.cuda.Stream()                        # non-blocking: not ordered with the library
+    raw = torch.as_tensor(_DevBytes(p.value, nb), device="cuda")
+    with torch.cuda.stream(side):
+        big = torch.empty(1 << 28, dtype=torch.float32, device="cuda")
+        for _ in range(20):                           # keep the side stream busy, then overwrite
+            big.mul_(1.0001)
+        raw.fill_(0xAB)
+    assert lib.vktHipFree(p) == 0, last_error()
+    q = C.c_void_p()
+    assert lib.vktHipAllocate(C.byref(q), nb) == 0, last_error()
+    v = HipVolumeView_t(q.value, n, n, n, 5, 0.0, 1.0)
+    assert lib.vktHipFillRange(v, Vec3i_t(0, 0, 0), Vec3i_t(n, n, n), C.c_float(0.5)) == 0, last_error()
+    torch.cuda.synchronize()
+    got = torch.as_tensor(_DevBytes(q.value, nb), device="cuda").view(torch.int16).cpu().numpy().view(np.uint16)
+    want = int(np.frombuffer(__import__("volkit_amd.volkit", fromlist=["MapVoxel"]).MapVoxel(0.5, 5), np.uint16)[0])
+    assert q.value == p.value                         # the freed block, reused after the drain
+    assert (got == want).all(), np.unique(got)[:4]
+    assert lib.vktHipFree(q) == 0 and lib.vktHipFree(keep) == 0
+    lib.vktHipSetTuningKnob(b"memory.arena_chunk_mib", 0)
+    del big
+
+
+class _DevBytes:
+    def __init__(self, ptr, nbytes):
+        self.__cuda_array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (ptr, False),
+                                         "version": 3, "strides": None}

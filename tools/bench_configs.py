@@ -222,55 +222,6 @@ def main():
                 report(f"{grp} SumRange {lab} {name}",
                        timed(lambda: lib.vktHipArithmeticRange(0, D, A, B, f0, f1, o), R), 3 * bpv * nv, nv)
             free(A, B, D)
-    if want("rowk"):
-        # in-process A/B of the MODE-0-only kernel for one collapsed row (knob
-        # pointwise.row_kernel): whole-volume Copy / SumRange / SafeSum / Fill per format, the
-        # knob alternated three times on the same allocations
-        m = 1024
-        for fmt, bpv, name in ((5, 2, "UInt16"), (4, 1, "UInt8"), (7, 4, "Float32")):
-            A, B, D = alloc((m,) * 3, fmt, seed=1), alloc((m,) * 3, fmt, seed=2), alloc((m,) * 3, fmt)
-            if fmt == 7:
-                rng_fill(A, m ** 3)
-                rng_fill(B, m ** 3)
-            last = Vec3i_t(m, m, m)
-            for rep in range(3):
-                for k in (1, 0):
-                    lib.vktHipSetTuningKnob(b"pointwise.row_kernel", k)
-                    report(f"rowk Copy 1024^3 {name} [row_kernel={k}]",
-                           timed(lambda: lib.vktHipCopyRange(D, A, o, last, o), R), 2 * bpv * m ** 3, m ** 3)
-                    report(f"rowk SumRange 1024^3 {name} [row_kernel={k}]",
-                           timed(lambda: lib.vktHipArithmeticRange(0, D, A, B, o, last, o), R), 3 * bpv * m ** 3, m ** 3)
-                    report(f"rowk SafeSum 1024^3 {name} [row_kernel={k}]",
-                           timed(lambda: lib.vktHipArithmeticRange(5, D, A, B, o, last, o), R), 3 * bpv * m ** 3, m ** 3)
-                    report(f"rowk Fill 1024^3 {name} [row_kernel={k}]",
-                           timed(lambda: lib.vktHipFillRange(D, o, last, C.c_float(0.5)), R), bpv * m ** 3, m ** 3)
-            lib.vktHipSetTuningKnob(b"pointwise.row_kernel", -1)
-            free(A, B, D)
-    if want("rowlds"):
-        # occupancy sweep of the one-row kernel: dynamic LDS per one-wave workgroup caps the
-        # waves per CU at 160 KiB / lds (knob pointwise.row_lds); row_kernel=0 is the general kernel
-        m = 1024
-        settings = [(0, 0), (1, 0), (1, 5632), (1, 6656), (1, 7168), (1, 8192), (1, 9216), (1, 10240)]
-        for fmt, bpv, name in ((5, 2, "UInt16"), (4, 1, "UInt8"), (7, 4, "Float32")):
-            A, B, D = alloc((m,) * 3, fmt, seed=1), alloc((m,) * 3, fmt, seed=2), alloc((m,) * 3, fmt)
-            if fmt == 7:
-                rng_fill(A, m ** 3)
-                rng_fill(B, m ** 3)
-            last = Vec3i_t(m, m, m)
-            for rep in range(2):
-                for rk, lds in settings:
-                    lib.vktHipSetTuningKnob(b"pointwise.row_kernel", rk)
-                    lib.vktHipSetTuningKnob(b"pointwise.row_lds", lds)
-                    tag = f"[row_kernel={rk} lds={lds}]"
-                    report(f"rowlds Copy 1024^3 {name} {tag}",
-                           timed(lambda: lib.vktHipCopyRange(D, A, o, last, o), R), 2 * bpv * m ** 3, m ** 3)
-                    report(f"rowlds SumRange 1024^3 {name} {tag}",
-                           timed(lambda: lib.vktHipArithmeticRange(0, D, A, B, o, last, o), R), 3 * bpv * m ** 3, m ** 3)
-                    report(f"rowlds Fill 1024^3 {name} {tag}",
-                           timed(lambda: lib.vktHipFillRange(D, o, last, C.c_float(0.5)), R), bpv * m ** 3, m ** 3)
-            lib.vktHipSetTuningKnob(b"pointwise.row_kernel", -1)
-            lib.vktHipSetTuningKnob(b"pointwise.row_lds", -1)
-            free(A, B, D)
     if want("u8row"):
         # UInt8 whole-volume ops on the row kernel: items per lane (knob pointwise.u8_unroll) x
         # occupancy cap (pointwise.row_lds), against the general kernel (row_kernel 0)
@@ -280,7 +231,7 @@ def main():
         settings = [(0, 4, 0), (1, 4, 8192), (1, 2, 8192), (1, 8, 8192), (1, 2, 0), (1, 8, 0), (1, 2, 10240)]
         for rep in range(2):
             for rk, un, lds in settings:
-                for k, v in ((b"pointwise.row_kernel", rk), (b"pointwise.u8_unroll", un), (b"pointwise.row_lds", lds)):
+                for k, v in ((b"pointwise.row_kernel", rk), (b"pointwise.u8_unroll", un), (b"pointwise.row_lds_u8", lds)):
                     lib.vktHipSetTuningKnob(k, v)
                 tag = f"[row_kernel={rk} unroll={un} lds={lds}]"
                 report(f"u8row Copy 1024^3 UInt8 {tag}", timed(lambda: lib.vktHipCopyRange(D, A, o, last, o), R),
@@ -289,7 +240,29 @@ def main():
                        timed(lambda: lib.vktHipArithmeticRange(0, D, A, B, o, last, o), R), 3 * m ** 3, m ** 3)
                 report(f"u8row SafeSum 1024^3 UInt8 {tag}",
                        timed(lambda: lib.vktHipArithmeticRange(5, D, A, B, o, last, o), R), 3 * m ** 3, m ** 3)
-        for k in (b"pointwise.row_kernel", b"pointwise.u8_unroll", b"pointwise.row_lds"):
+        for k in (b"pointwise.row_kernel", b"pointwise.u8_unroll", b"pointwise.row_lds_u8"):
+            lib.vktHipSetTuningKnob(k, -1)
+        free(A, B, D)
+    if want("u16row"):
+        # UInt16 whole-volume ops: the row kernel (knob pointwise.row_kernel bit 1) at 1 or 2 KiB
+        # per stream per workgroup (pointwise.u16_unroll) and occupancy caps (pointwise.row_lds),
+        # against the general kernel; alternated on the same allocations
+        m = 1024
+        A, B, D = alloc((m,) * 3, 5, seed=1), alloc((m,) * 3, 5, seed=2), alloc((m,) * 3, 5)
+        last = Vec3i_t(m, m, m)
+        settings = [(1, 2, 0), (3, 1, 0), (3, 1, 5376), (3, 1, 5632), (3, 1, 5888), (3, 1, 6144), (3, 2, 5632)]
+        for rep in range(3):
+            for rk, un, lds in settings:
+                for k, v in ((b"pointwise.row_kernel", rk), (b"pointwise.u16_unroll", un), (b"pointwise.row_lds", lds)):
+                    lib.vktHipSetTuningKnob(k, v)
+                tag = f"[row_kernel={rk} unroll={un} lds={lds}]"
+                report(f"u16row Copy 1024^3 UInt16 {tag}", timed(lambda: lib.vktHipCopyRange(D, A, o, last, o), R),
+                       4 * m ** 3, m ** 3)
+                report(f"u16row SumRange 1024^3 UInt16 {tag}",
+                       timed(lambda: lib.vktHipArithmeticRange(0, D, A, B, o, last, o), R), 6 * m ** 3, m ** 3)
+                report(f"u16row SafeDiff 1024^3 UInt16 {tag}",
+                       timed(lambda: lib.vktHipArithmeticRange(6, D, A, B, o, last, o), R), 6 * m ** 3, m ** 3)
+        for k in (b"pointwise.row_kernel", b"pointwise.u16_unroll", b"pointwise.row_lds"):
             lib.vktHipSetTuningKnob(k, -1)
         free(A, B, D)
     if want("u8cal"):

@@ -203,17 +203,35 @@ namespace hipk
             if (w.live && w.whole)
                 w.v = *reinterpret_cast<u32x4 const*>(src + startByte);
         };
+        // (knob decompose.aligned_lds 3) the tile's bytes past the chunk's voxels, when 16 of
+        // them are free: a partial word writes its voxels outside the row span / chunk there
+        int32_t const dumpB = chunkVox * BPV;
+        bool const dumpable = alignedLds == 3 && dumpB + 16 <= static_cast<int32_t>(kBrickChunk) * 16;
         auto place = [&](Word const& w) {
             if (!w.live)
                 return;
             if (w.whole && w.x0 >= lo && w.x0 + V <= hi && w.li >= 0 && w.li + V <= chunkVox)
             {
-                if (alignedLds >= 2)
+                if (alignedLds == 2)
                     ldsStoreRange(lds, w.li * BPV, w.v, 0, 16);
                 else
                     reinterpret_cast<Unaligned16*>(lds + w.li * BPV)->v = w.v;
             }
-            else if (w.whole && alignedLds >= 1)
+            else if (w.whole && dumpable)
+            {
+                // a word cut by a row end or the chunk: all V voxels written, the ones outside to
+                // the dump bytes -- a select per voxel instead of a divergent branch (the
+                // per-voxel ifs below cost ~30 scalar exec-mask instructions per word: SQ_INSTS_SALU
+                // was as high as SQ_INSTS_VALU on 16^3 bricks, profiles/r04/dec16.pmc.jsonl)
+#pragma unroll
+                for (int k = 0; k < V; ++k)
+                {
+                    bool const in = w.x0 + k >= lo && w.x0 + k < hi && w.li + k >= 0 && w.li + k < chunkVox;
+                    int32_t const b = in ? (w.li + k) * BPV : dumpB;
+                    ldsStoreCode<BPV>(lds + b, 0, wordCode<BPV>(w.v, k));
+                }
+            }
+            else if (w.whole && alignedLds == 1)
             {
                 // the voxels of the word inside the row span and the chunk, as aligned pieces
                 int32_t const k0 = max(max(lo - w.x0, -w.li), 0);
@@ -509,12 +527,12 @@ namespace hipk
                 return;
             if (w.whole && w.x0 >= g.lo && w.x0 + V <= g.hi && w.li >= 0 && w.li + V <= g.chunkVox)
             {
-                if (alignedLds >= 2)
+                if (alignedLds == 2)
                     ldsStoreRange(lds, w.li * BPV, w.v, 0, 16);
                 else
                     reinterpret_cast<Unaligned16*>(lds + w.li * BPV)->v = w.v;
             }
-            else if (w.whole && alignedLds >= 1)
+            else if (w.whole && (alignedLds == 1 || alignedLds == 2))
             {
                 int32_t const k0 = max(max(g.lo - w.x0, -w.li), 0);
                 int32_t const k1 = min(min(g.hi - w.x0, g.chunkVox - w.li), V);
@@ -737,12 +755,12 @@ namespace hipk
                 int32_t const li = w.r * b.nx + (w.x0 - b.fx);   // brick-local voxel of the word's first
                 if (w.whole && w.x0 >= b.lo && w.x0 + V <= b.hi)
                 {
-                    if (alignedLds >= 2)
+                    if (alignedLds == 2)
                         ldsStoreRange(lds, li * BPV, w.v, 0, 16);
                     else
                         reinterpret_cast<Unaligned16*>(lds + li * BPV)->v = w.v;
                 }
-                else if (w.whole && alignedLds >= 1)
+                else if (w.whole && (alignedLds == 1 || alignedLds == 2))
                 {
                     int32_t const k0 = max(b.lo - w.x0, 0), k1 = min(b.hi - w.x0, V);
                     ldsStoreRange(lds, (li + k0) * BPV, w.v, k0 * BPV, k1 * BPV);

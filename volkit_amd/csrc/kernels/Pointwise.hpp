@@ -535,6 +535,26 @@ namespace hipk
         }
     }
 
+    // One collapsed row (whole-volume ops: every operand contiguous, no row edges, no scalar
+    // head / tail): the same span code instantiated for MODE 0 alone.  The general kernel below
+    // carries the multi-row, padded-row and sector-completion paths in one body, so its VGPR
+    // count (85 for UInt16 SumRange, 118 for UInt8) is set by code a collapsed row never runs
+    // and caps the waves per SIMD (5 / 4) -- the bytes each SIMD keeps in flight.
+    template <int NS, int BPV, int U, class F>
+    __global__ __launch_bounds__(kVecBlock) void pointwiseRowKernel(Operand d, Operand s1, Operand s2, Geom g, F f,
+                                                                   uint64_t qBase, uint64_t qEnd)
+    {
+        uint64_t const items = static_cast<uint64_t>(g.vnx8 - g.vhead) >> 3;
+        constexpr uint64_t kQ = static_cast<uint64_t>(kVecBlock) * U;
+        for (uint64_t q = qBase + blockIdx.x; q < qEnd; q += gridDim.x)
+        {
+            uint64_t const beg = q * kQ;
+            if (beg >= items)
+                break;
+            pointwiseVecSpan<NS, BPV, 0, U>(d, s1, s2, g, beg, beg + kQ < items ? beg + kQ : items, f);
+        }
+    }
+
     // Work distribution: workgroup q handles the q-th quantum of kVecBlock*kUnroll items and
     // the grid holds one workgroup per quantum (grid-stride only beyond 2^30 quanta).  Short
     // one-shot workgroups dispatched in order make the whole chip sweep memory as one
@@ -1546,8 +1566,24 @@ namespace hipk
                 uint64_t edgeItems = p.g.padded ? 0 : rows * static_cast<uint64_t>(p.g.vhead + (p.g.vnx - p.g.vnx8));
                 uint64_t edgeBlocks = (edgeItems + kVecBlock - 1) / kVecBlock;
                 edgeBlocks = edgeBlocks < 4096 ? edgeBlocks : 4096;
-                auto launch = [&](auto unroll) {
+                // one collapsed row without scalar edges -- UInt8 copies and arithmetic, UInt16
+                // arithmetic: the MODE-0-only kernel (knob pointwise.row_kernel bits 0 / 1), with
+                // 1 KiB per stream per one-wave workgroup and the waves per CU capped by dynamic
+                // LDS (knobs pointwise.u8_unroll / u16_unroll, row_lds_u8 / row_lds).  In-process
+                // A/Bs on the same 1024^3 allocations (profiles/r05/u8row.jsonl, u16row.jsonl):
+                // UInt8 Copy 0.368 -> 0.326 ms, SumRange 0.540 -> 0.495 ms; UInt16 SumRange
+                // 0.995 -> 0.968 ms (29 workgroups per CU; 32 -- no cap -- 0.986, 24: 0.986).
+                // UInt16 copies (0.650 vs 0.660 ms), fills and Float32 stay on the general kernel.
+                constexpr bool kRowCapable = (BPV == 1 && NS >= 1) || (BPV == 2 && NS == 2);   // (the only instantiations)
+                bool const rowOnly = kRowCapable && rows == 1 && edgeItems == 0 &&
+                                     (rt::knob(rt::Knob::PointwiseRowKernel) & (BPV == 1 ? 1 : 2)) != 0;
+                // dynamic LDS per one-wave workgroup: caps the waves per CU at 160 KiB / rowLds
+                // (knob pointwise.row_lds; the kernel does not touch it)
+                unsigned const rowLds =
+                    static_cast<unsigned>(rt::knob(BPV == 1 ? rt::Knob::PointwiseRowLdsU8 : rt::Knob::PointwiseRowLds));
+                auto launch = [&](auto unroll, auto rowKernelOnly) {
                     constexpr int U = decltype(unroll)::value;
+                    constexpr bool kRowOnly = decltype(rowKernelOnly)::value;
                     constexpr uint64_t kQ = static_cast<uint64_t>(kVecBlock) * U;
                     // (row-aligned quanta -- no 128-B line of a row shared by two workgroups --
                     // measured no better in an in-process A/B: 800^3 sub-box of 1024^3 at x0 = 100
@@ -1562,15 +1598,52 @@ namespace hipk
                     {
                         uint64_t const n = quanta - q0 < maxQ ? quanta - q0 : maxQ;
                         uint64_t const g = q0 == 0 && n < edgeBlocks ? edgeBlocks : n;
-                        hipLaunchKernelGGL((pointwiseVecKernel<NS, BPV, U, F>), dim3(static_cast<unsigned>(g > 0 ? g : 1)),
-                                           dim3(kVecBlock), 0, stream, p.d, p.s1, p.s2, p.g, f, q0, q0 + n,
-                                           static_cast<int32_t>(q0 == 0));
+                        if constexpr (kRowCapable)
+                        {
+                            if (kRowOnly || rowOnly)
+                            {
+                                hipLaunchKernelGGL((pointwiseRowKernel<NS, BPV, U, F>),
+                                                   dim3(static_cast<unsigned>(n > 0 ? n : 1)), dim3(kVecBlock), rowLds,
+                                                   stream, p.d, p.s1, p.s2, p.g, f, q0, q0 + n);
+                                q0 += n;
+                                continue;
+                            }
+                        }
+                        if constexpr (!kRowOnly)
+                            hipLaunchKernelGGL((pointwiseVecKernel<NS, BPV, U, F>), dim3(static_cast<unsigned>(g > 0 ? g : 1)),
+                                               dim3(kVecBlock), 0, stream, p.d, p.s1, p.s2, p.g, f, q0, q0 + n,
+                                               static_cast<int32_t>(q0 == 0));
                         q0 += n;
                     } while (q0 < quanta);
                 };
                 // (a 1-KiB quantum for the one-row 3-stream UInt16 ops measured the same as 2 KiB
                 // in an in-process A/B, 0.985 vs 0.986 ms for 1024^3 SumRange: one unroll for all)
-                launch(std::integral_constant<int, vecUnroll<NS, BPV>()>{});
+                if constexpr (BPV == 1 && NS >= 1)
+                {
+                    // UInt8 row kernel: items per lane (knob pointwise.u8_unroll: 2 / 4 / 8 =
+                    // 1 / 2 / 4 KiB per stream per workgroup)
+                    int64_t const u = rt::knob(rt::Knob::PointwiseU8Unroll);
+                    if (rowOnly && u == 2)
+                    {
+                        launch(std::integral_constant<int, 2>{}, std::true_type{});
+                        return vktNoError;
+                    }
+                    if (rowOnly && u == 8)
+                    {
+                        launch(std::integral_constant<int, 8>{}, std::true_type{});
+                        return vktNoError;
+                    }
+                }
+                if constexpr (BPV == 2 && NS == 2)
+                {
+                    // UInt16 row kernel with 1 KiB per stream per workgroup (knob pointwise.u16_unroll 1)
+                    if (rowOnly && rt::knob(rt::Knob::PointwiseU16Unroll) == 1)
+                    {
+                        launch(std::integral_constant<int, 1>{}, std::true_type{});
+                        return vktNoError;
+                    }
+                }
+                launch(std::integral_constant<int, vecUnroll<NS, BPV>()>{}, std::false_type{});
                 return vktNoError;
             }
             if (p.gen && p.uniform && p.bpv == BPV)

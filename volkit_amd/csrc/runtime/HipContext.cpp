@@ -247,6 +247,11 @@ namespace rt
             {"decompose.pair", 0},
             {"memory.fail_next_alloc", 0},
             {"comm.test_stall_ms", 0},
+            {"pointwise.row_kernel", 3},
+            {"pointwise.row_lds", 5632},
+            {"pointwise.u8_unroll", 2},
+            {"pointwise.u16_unroll", 1},
+            {"pointwise.row_lds_u8", 0},
         };
         static_assert(sizeof(kKnobs) / sizeof(kKnobs[0]) == static_cast<size_t>(Knob::Count), "knob table");
         std::atomic<int64_t> gKnobs[static_cast<int>(Knob::Count)] = {{kKnobs[0].def}, {kKnobs[1].def},
@@ -264,7 +269,9 @@ namespace rt
                                                                   {kKnobs[24].def}, {kKnobs[25].def},
                                                                   {kKnobs[26].def}, {kKnobs[27].def},
                                                                   {kKnobs[28].def}, {kKnobs[29].def},
-                                                                  {kKnobs[30].def}};
+                                                                  {kKnobs[30].def}, {kKnobs[31].def},
+                                                                  {kKnobs[32].def}, {kKnobs[33].def},
+                                                                  {kKnobs[34].def}, {kKnobs[35].def}};
     } // namespace
 
     int64_t knob(Knob k) { return gKnobs[static_cast<int>(k)].load(std::memory_order_relaxed); }

@@ -104,7 +104,7 @@ namespace rt
         HistogramP16Step,              // 0: P16 threshold tests after each item, not each wave-step
         PointwiseU8Pairs,              // 0: UInt8 multi-row boxes keep the 8-voxel per-item loop
         RenderBricks,                  // 0: multi-scattering samples the dense volume, not an 8^3-brick copy
-        DecomposeAlignedLds,           // 1: partial words as aligned LDS pieces; 2: every word
+        DecomposeAlignedLds,           // 1: partial words as aligned LDS pieces; 2: every word; 3: partial words branch-free (dump bytes)
         DecomposeStageWords,           // source words per thread in flight in the staged copy (5, 6, 8)
         PointwiseU8Wide,               // 0: UInt8 general-path boxes keep 8-voxel items
         PointwiseF32Halves,            // 0: padded 4-byte rows keep the per-item loop
@@ -125,6 +125,11 @@ namespace rt
         DecomposePair,                 // 1: two x-neighbour bricks of <= 16 KiB per workgroup (uniform grids)
         MemoryFailNextAlloc,           // n > 0: the next n device allocations fail (tests of the failure paths)
         CommTestStallMs,               // > 0: every RCCL round with a deadline also stalls its stream this long (watcher test)
+        PointwiseRowKernel,            // one-row (whole-volume) copies / arithmetic on the MODE-0 kernel: bit 0 UInt8, bit 1 UInt16
+        PointwiseRowLds,               // bytes of dynamic LDS per UInt16 row-kernel workgroup (occupancy cap; 0 = none)
+        PointwiseU8Unroll,             // items per lane of the UInt8 row kernel (2, 4, 8)
+        PointwiseU16Unroll,            // items per lane of the UInt16 row kernel (1, 2)
+        PointwiseRowLdsU8,             // the same occupancy cap for the UInt8 row kernel
         Count
     };
     int64_t knob(Knob k);
