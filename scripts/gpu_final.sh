@@ -6,7 +6,7 @@
 set -u
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
-O=gpurun_out/final
+O=gpurun_out/${1:-final}
 mkdir -p $O
 step() {  # name, limit, command...
     local name=$1 limit=$2; shift 2

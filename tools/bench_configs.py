@@ -318,6 +318,22 @@ def main():
                 report(f"f32shift CopyRange 800^3 x0=100 same offset {name}",
                        timed(lambda: lib.vktHipCopyRange(D, A, f0, f1, f0), R), 2 * bpv * nv, nv)
             free(A, B, D)
+    if want("f32s3"):
+        # Float32 SumRange on the 800^3 sub-box at x0 = 100: same offset (aligned path) vs
+        # dstOffset x = -97 (general path) with 8-voxel items (knob pointwise.f32_wide 2, the
+        # default) and 16-B items (f32_wide 1); one launch per case for PMC passes
+        m = 1024
+        A, B, D = alloc((m,) * 3, 7, seed=1), alloc((m,) * 3, 7, seed=2), alloc((m,) * 3, 7)
+        f0, f1 = Vec3i_t(100, 100, 100), Vec3i_t(900, 900, 900)
+        nv = 800 ** 3
+        report("f32s3 SumRange 800^3 x0=100 same offset Float32",
+               timed(lambda: lib.vktHipArithmeticRange(0, D, A, B, f0, f1, o), R), 12 * nv, nv)
+        for wide in (2, 1):
+            lib.vktHipSetTuningKnob(b"pointwise.f32_wide", wide)
+            report(f"f32s3 SumRange 800^3 x0=100 dstOffset x=-97 Float32 [f32_wide={wide}]",
+                   timed(lambda: lib.vktHipArithmeticRange(0, D, A, B, f0, f1, Vec3i_t(-97, 0, 0)), R), 12 * nv, nv)
+        lib.vktHipSetTuningKnob(b"pointwise.f32_wide", -1)
+        free(A, B, D)
     if want("f32dw"):
         # in-process A/B: whole-dword window shifts (knob pointwise.dword_shift) x 16-B items
         # (pointwise.f32_wide) on the Float32 general path, 800^3 sub-box of 1024^3
