@@ -222,6 +222,36 @@ def test_row_kernel(lib, o, fmt, knobs):
             L.vktHipSetTuningKnob(k, -1)
 
 
+@pytest.mark.parametrize("fmt", [4, 5])
+@pytest.mark.parametrize("u", [2, 4])
+def test_rows_kernel(lib, o, fmt, u):
+    """Multi-row boxes on the MODE-1-only kernel (knob pointwise.rows_kernel; 32-bit row math,
+    no scalar edges: padded rows, with and without sector completion, or rows of whole items):
+    Copy, SumRange, SafeSum vs the oracle, at 1 and 2 KiB per stream."""
+    from volkit_amd._lib import lib as L
+    rng = np.random.default_rng(fmt * 7 + u)
+    dims = (9, 40, 272)
+    a, b, dinit = (rand_codes(rng, fmt, dims) for _ in range(3))
+    try:
+        for k, v in ((b"pointwise.rows_kernel", 3), (b"pointwise.u8_unroll", u), (b"pointwise.u16_unroll", u // 2)):
+            assert L.vktHipSetTuningKnob(k, v) == 0
+        for merge in (1, 0):
+            assert L.vktHipSetTuningKnob(b"pointwise.merge_sectors", merge) == 0
+            for first, last in (((100, 3, 1), (200, 37, 8)), ((0, 1, 1), (256, 39, 9)), ((16, 2, 0), (144, 40, 9)),
+                                ((3, 0, 2), (269, 40, 7))):
+                for op in ("Sum", "SafeSum"):
+                    da, db, dd = Dev(a, fmt), Dev(b, fmt), Dev(dinit, fmt)
+                    assert L.vktHipArithmeticRange(OPS.index(op), dd.view, da.view, db.view, vec(first), vec(last),
+                                                   vec((0, 0, 0))) == 0, last_error()
+                    ref = o.arith(op, [fmt] * 3, [(0.0, 1.0)] * 3, a, b, dinit.copy(), first, last, (0, 0, 0))
+                    assert_codes_equal(dd.read(), ref, fmt, f"{op} fmt={fmt} u={u} {first}->{last} merge={merge}")
+                copy_case(lib, o, fmt, fmt, (0.0, 1.0), (0.0, 1.0), a, dinit, first, last, first, 0, 0,
+                          f"copy fmt={fmt} u={u} {first}->{last} merge={merge}")
+    finally:
+        for k in (b"pointwise.rows_kernel", b"pointwise.u8_unroll", b"pointwise.u16_unroll", b"pointwise.merge_sectors"):
+            L.vktHipSetTuningKnob(k, -1)
+
+
 @pytest.mark.parametrize("fmt", [4, 7, 6])
 @pytest.mark.parametrize("box", [((0, 1, 1), (256, 30, 6)),      # rows of 32 items (even)
                                  ((16, 2, 0), (136, 29, 7)),     # 15 items per row

@@ -265,6 +265,48 @@ def main():
         for k in (b"pointwise.row_kernel", b"pointwise.u16_unroll", b"pointwise.row_lds"):
             lib.vktHipSetTuningKnob(k, -1)
         free(A, B, D)
+    if want("rowswz"):
+        # XCD mapping of the row kernel's quanta (knob pointwise.row_swizzle: 0 every 8th quantum
+        # per XCD, r > 0 runs of r consecutive quanta), UInt16 SumRange / UInt8 SumRange + Copy
+        m = 1024
+        for fmt, bpv, name in ((5, 2, "UInt16"), (4, 1, "UInt8")):
+            A, B, D = alloc((m,) * 3, fmt, seed=1), alloc((m,) * 3, fmt, seed=2), alloc((m,) * 3, fmt)
+            last = Vec3i_t(m, m, m)
+            for rep in range(3):
+                for r in (0, 2, 8, 64, 4096):
+                    lib.vktHipSetTuningKnob(b"pointwise.row_swizzle", r)
+                    report(f"rowswz SumRange 1024^3 {name} [row_swizzle={r}]",
+                           timed(lambda: lib.vktHipArithmeticRange(0, D, A, B, o, last, o), R), 3 * bpv * m ** 3, m ** 3)
+                    if fmt == 4:
+                        report(f"rowswz Copy 1024^3 {name} [row_swizzle={r}]",
+                               timed(lambda: lib.vktHipCopyRange(D, A, o, last, o), R), 2 * bpv * m ** 3, m ** 3)
+            lib.vktHipSetTuningKnob(b"pointwise.row_swizzle", -1)
+            free(A, B, D)
+    if want("rowsk"):
+        # multi-row sub-boxes of 1024^3 on the MODE-1-only kernel (knob pointwise.rows_kernel),
+        # with 1 / 2 KiB per stream (u8_unroll / u16_unroll), against the general kernel
+        m = 1024
+        boxes = (("x0=100", Vec3i_t(100, 100, 100), Vec3i_t(900, 900, 900)),
+                 ("x 0..800", Vec3i_t(0, 100, 100), Vec3i_t(800, 900, 900)))
+        settings = ((0, 2, 1), (3, 2, 1), (3, 4, 2))
+        for fmt, bpv, name in ((4, 1, "UInt8"), (5, 2, "UInt16")):
+            A, B, D = alloc((m,) * 3, fmt, seed=1), alloc((m,) * 3, fmt, seed=2), alloc((m,) * 3, fmt)
+            for rep in range(2):
+                for rk, u8, u16 in settings:
+                    for k, v in ((b"pointwise.rows_kernel", rk), (b"pointwise.u8_unroll", u8),
+                                 (b"pointwise.u16_unroll", u16)):
+                        lib.vktHipSetTuningKnob(k, v)
+                    tag = f"[rows_kernel={rk} u8_unroll={u8} u16_unroll={u16}]"
+                    for lab, f0, f1 in boxes:
+                        nv = (f1.x - f0.x) * (f1.y - f0.y) * (f1.z - f0.z)
+                        if fmt == 4:
+                            report(f"rowsk CopyRange {lab} same offset {name} {tag}",
+                                   timed(lambda: lib.vktHipCopyRange(D, A, f0, f1, f0), R), 2 * bpv * nv, nv)
+                        report(f"rowsk SumRange {lab} {name} {tag}",
+                               timed(lambda: lib.vktHipArithmeticRange(0, D, A, B, f0, f1, o), R), 3 * bpv * nv, nv)
+            for k in (b"pointwise.rows_kernel", b"pointwise.u8_unroll", b"pointwise.u16_unroll"):
+                lib.vktHipSetTuningKnob(k, -1)
+            free(A, B, D)
     if want("u8cal"):
         # FETCH_SIZE calibration for the UInt8 access shapes and the
         # whole-volume UInt8 ops against UInt16 (item 4); one launch per case for PMC passes.

@@ -540,18 +540,33 @@ namespace hipk
     // carries the multi-row, padded-row and sector-completion paths in one body, so its VGPR
     // count (85 for UInt16 SumRange, 118 for UInt8) is set by code a collapsed row never runs
     // and caps the waves per SIMD (5 / 4) -- the bytes each SIMD keeps in flight.
-    template <int NS, int BPV, int U, class F>
+    // MODE 1 (knob pointwise.rows_kernel): the same for multi-row boxes on 32-bit row math
+    // without scalar edges (padded rows or rows of whole items).
+    template <int NS, int BPV, int MODE, int U, class F>
     __global__ __launch_bounds__(kVecBlock) void pointwiseRowKernel(Operand d, Operand s1, Operand s2, Geom g, F f,
-                                                                   uint64_t qBase, uint64_t qEnd)
+                                                                   uint64_t qBase, uint64_t qEnd, uint32_t runs)
     {
-        uint64_t const items = static_cast<uint64_t>(g.vnx8 - g.vhead) >> 3;
+        uint64_t const items = (static_cast<uint64_t>(g.vnx8 - g.vhead) >> 3) * static_cast<uint64_t>(g.vny) *
+                               static_cast<uint64_t>(g.vnz);
         constexpr uint64_t kQ = static_cast<uint64_t>(kVecBlock) * U;
-        for (uint64_t q = qBase + blockIdx.x; q < qEnd; q += gridDim.x)
+        // workgroup b runs on XCD b mod 8; runs > 0 (knob pointwise.row_swizzle) gives each XCD
+        // runs of `runs` consecutive quanta instead of every 8th one
+        uint32_t b = blockIdx.x;
+        if (runs > 0u)
+        {
+            uint32_t const span = 8u * runs, whole = gridDim.x / span * span;
+            if (b < whole)
+            {
+                uint32_t const l = b >> 3;
+                b = (l / runs) * span + (b & 7u) * runs + l % runs;
+            }
+        }
+        for (uint64_t q = qBase + b; q < qEnd; q += gridDim.x)
         {
             uint64_t const beg = q * kQ;
             if (beg >= items)
                 break;
-            pointwiseVecSpan<NS, BPV, 0, U>(d, s1, s2, g, beg, beg + kQ < items ? beg + kQ : items, f);
+            pointwiseVecSpan<NS, BPV, MODE, U>(d, s1, s2, g, beg, beg + kQ < items ? beg + kQ : items, f);
         }
     }
 
@@ -1577,8 +1592,12 @@ namespace hipk
                 constexpr bool kRowCapable = (BPV == 1 && NS >= 1) || (BPV == 2 && NS == 2);   // (the only instantiations)
                 bool const rowOnly = kRowCapable && rows == 1 && edgeItems == 0 &&
                                      (rt::knob(rt::Knob::PointwiseRowKernel) & (BPV == 1 ? 1 : 2)) != 0;
+                // multi-row boxes on the MODE-1-only kernel (knob pointwise.rows_kernel, same bits)
+                bool const rowsOnly = kRowCapable && rows > 1 && p.g.fast32 && edgeItems == 0 &&
+                                      (rt::knob(rt::Knob::PointwiseRowsKernel) & (BPV == 1 ? 1 : 2)) != 0;
                 // dynamic LDS per one-wave workgroup: caps the waves per CU at 160 KiB / rowLds
                 // (knob pointwise.row_lds; the kernel does not touch it)
+                uint32_t const rowRuns = static_cast<uint32_t>(rt::knob(rt::Knob::PointwiseRowSwizzle));
                 unsigned const rowLds =
                     static_cast<unsigned>(rt::knob(BPV == 1 ? rt::Knob::PointwiseRowLdsU8 : rt::Knob::PointwiseRowLds));
                 auto launch = [&](auto unroll, auto rowKernelOnly) {
@@ -1600,11 +1619,19 @@ namespace hipk
                         uint64_t const g = q0 == 0 && n < edgeBlocks ? edgeBlocks : n;
                         if constexpr (kRowCapable)
                         {
+                            if (rowsOnly)
+                            {
+                                hipLaunchKernelGGL((pointwiseRowKernel<NS, BPV, 1, U, F>),
+                                                   dim3(static_cast<unsigned>(n > 0 ? n : 1)), dim3(kVecBlock), rowLds,
+                                                   stream, p.d, p.s1, p.s2, p.g, f, q0, q0 + n, rowRuns);
+                                q0 += n;
+                                continue;
+                            }
                             if (kRowOnly || rowOnly)
                             {
-                                hipLaunchKernelGGL((pointwiseRowKernel<NS, BPV, U, F>),
+                                hipLaunchKernelGGL((pointwiseRowKernel<NS, BPV, 0, U, F>),
                                                    dim3(static_cast<unsigned>(n > 0 ? n : 1)), dim3(kVecBlock), rowLds,
-                                                   stream, p.d, p.s1, p.s2, p.g, f, q0, q0 + n);
+                                                   stream, p.d, p.s1, p.s2, p.g, f, q0, q0 + n, rowRuns);
                                 q0 += n;
                                 continue;
                             }
@@ -1623,12 +1650,12 @@ namespace hipk
                     // UInt8 row kernel: items per lane (knob pointwise.u8_unroll: 2 / 4 / 8 =
                     // 1 / 2 / 4 KiB per stream per workgroup)
                     int64_t const u = rt::knob(rt::Knob::PointwiseU8Unroll);
-                    if (rowOnly && u == 2)
+                    if ((rowOnly || rowsOnly) && u == 2)
                     {
                         launch(std::integral_constant<int, 2>{}, std::true_type{});
                         return vktNoError;
                     }
-                    if (rowOnly && u == 8)
+                    if ((rowOnly || rowsOnly) && u == 8)
                     {
                         launch(std::integral_constant<int, 8>{}, std::true_type{});
                         return vktNoError;
@@ -1637,7 +1664,7 @@ namespace hipk
                 if constexpr (BPV == 2 && NS == 2)
                 {
                     // UInt16 row kernel with 1 KiB per stream per workgroup (knob pointwise.u16_unroll 1)
-                    if (rowOnly && rt::knob(rt::Knob::PointwiseU16Unroll) == 1)
+                    if ((rowOnly || rowsOnly) && rt::knob(rt::Knob::PointwiseU16Unroll) == 1)
                     {
                         launch(std::integral_constant<int, 1>{}, std::true_type{});
                         return vktNoError;

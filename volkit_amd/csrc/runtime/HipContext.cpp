@@ -252,6 +252,8 @@ namespace rt
             {"pointwise.u8_unroll", 2},
             {"pointwise.u16_unroll", 1},
             {"pointwise.row_lds_u8", 0},
+            {"pointwise.row_swizzle", 0},
+            {"pointwise.rows_kernel", 0},
         };
         static_assert(sizeof(kKnobs) / sizeof(kKnobs[0]) == static_cast<size_t>(Knob::Count), "knob table");
         std::atomic<int64_t> gKnobs[static_cast<int>(Knob::Count)] = {{kKnobs[0].def}, {kKnobs[1].def},
@@ -271,7 +273,8 @@ namespace rt
                                                                   {kKnobs[28].def}, {kKnobs[29].def},
                                                                   {kKnobs[30].def}, {kKnobs[31].def},
                                                                   {kKnobs[32].def}, {kKnobs[33].def},
-                                                                  {kKnobs[34].def}, {kKnobs[35].def}};
+                                                                  {kKnobs[34].def}, {kKnobs[35].def},
+                                                                  {kKnobs[36].def}, {kKnobs[37].def}};
     } // namespace
 
     int64_t knob(Knob k) { return gKnobs[static_cast<int>(k)].load(std::memory_order_relaxed); }

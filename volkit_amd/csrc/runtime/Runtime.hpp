@@ -130,6 +130,8 @@ namespace rt
         PointwiseU8Unroll,             // items per lane of the UInt8 row kernel (2, 4, 8)
         PointwiseU16Unroll,            // items per lane of the UInt16 row kernel (1, 2)
         PointwiseRowLdsU8,             // the same occupancy cap for the UInt8 row kernel
+        PointwiseRowSwizzle,           // > 0: the row kernel gives each XCD runs of this many consecutive quanta
+        PointwiseRowsKernel,           // multi-row boxes (32-bit rows, no scalar edges) on the MODE-1 kernel: bit 0 UInt8, bit 1 UInt16
         Count
     };
     int64_t knob(Knob k);
