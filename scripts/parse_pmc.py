@@ -49,6 +49,16 @@ def main():
             "read_bytes": fb, "write_bytes": wb,
             "total_bytes": (fb or 0) + (wb or 0),
         }
+    # calibrated reads (when a request-size pass exists): 32 / 64 / 128-B L2 -> fabric requests
+    req = {c: load(os.path.join(root, "req", "**", "*counter_collection.csv"), c)
+           for c in ("TCC_EA0_RDREQ_32B_sum", "TCC_EA0_RDREQ_64B_sum", "TCC_EA0_RDREQ_128B_sum")}
+    for name in req["TCC_EA0_RDREQ_128B_sum"]:
+        k = out["kernels"].get(short(name))
+        if k is None:
+            continue
+        mean = lambda c: sum(req[c].get(name, [0.0])) / max(1, len(req[c].get(name, [])))  # noqa: E731
+        k["read_bytes_by_request_size"] = (32 * mean("TCC_EA0_RDREQ_32B_sum") + 64 * mean("TCC_EA0_RDREQ_64B_sum") +
+                                           128 * mean("TCC_EA0_RDREQ_128B_sum"))
     s = out["kernels"].get("SumRange(UInt16)")
     if s:
         out["SumRange_bytes_per_launch"] = s["total_bytes"]

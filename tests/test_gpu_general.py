@@ -223,17 +223,18 @@ def test_row_kernel(lib, o, fmt, knobs):
 
 
 @pytest.mark.parametrize("fmt", [4, 5])
-@pytest.mark.parametrize("u", [2, 4])
-def test_rows_kernel(lib, o, fmt, u):
-    """Multi-row boxes on the MODE-1-only kernel (knob pointwise.rows_kernel; 32-bit row math,
-    no scalar edges: padded rows, with and without sector completion, or rows of whole items):
-    Copy, SumRange, SafeSum vs the oracle, at 1 and 2 KiB per stream."""
+@pytest.mark.parametrize("rk", [3, 0])
+def test_rows_kernel(lib, o, fmt, rk):
+    """Multi-row boxes on the MODE-1-only kernel (knob pointwise.rows_kernel 3, the default: UInt8
+    copies at 1 KiB per stream, UInt8 / UInt16 arithmetic at 2 KiB; 32-bit row math, no scalar
+    edges: padded rows, with and without sector completion, or rows of whole items) and on the
+    general kernel (0): Copy, SumRange, SafeSum vs the oracle."""
     from volkit_amd._lib import lib as L
-    rng = np.random.default_rng(fmt * 7 + u)
+    rng = np.random.default_rng(fmt * 7 + rk)
     dims = (9, 40, 272)
     a, b, dinit = (rand_codes(rng, fmt, dims) for _ in range(3))
     try:
-        for k, v in ((b"pointwise.rows_kernel", 3), (b"pointwise.u8_unroll", u), (b"pointwise.u16_unroll", u // 2)):
+        for k, v in ((b"pointwise.rows_kernel", rk),):
             assert L.vktHipSetTuningKnob(k, v) == 0
         for merge in (1, 0):
             assert L.vktHipSetTuningKnob(b"pointwise.merge_sectors", merge) == 0
@@ -244,11 +245,11 @@ def test_rows_kernel(lib, o, fmt, u):
                     assert L.vktHipArithmeticRange(OPS.index(op), dd.view, da.view, db.view, vec(first), vec(last),
                                                    vec((0, 0, 0))) == 0, last_error()
                     ref = o.arith(op, [fmt] * 3, [(0.0, 1.0)] * 3, a, b, dinit.copy(), first, last, (0, 0, 0))
-                    assert_codes_equal(dd.read(), ref, fmt, f"{op} fmt={fmt} u={u} {first}->{last} merge={merge}")
+                    assert_codes_equal(dd.read(), ref, fmt, f"{op} fmt={fmt} rk={rk} {first}->{last} merge={merge}")
                 copy_case(lib, o, fmt, fmt, (0.0, 1.0), (0.0, 1.0), a, dinit, first, last, first, 0, 0,
-                          f"copy fmt={fmt} u={u} {first}->{last} merge={merge}")
+                          f"copy fmt={fmt} rk={rk} {first}->{last} merge={merge}")
     finally:
-        for k in (b"pointwise.rows_kernel", b"pointwise.u8_unroll", b"pointwise.u16_unroll", b"pointwise.merge_sectors"):
+        for k in (b"pointwise.rows_kernel", b"pointwise.merge_sectors"):
             L.vktHipSetTuningKnob(k, -1)
 
 

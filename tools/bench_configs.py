@@ -288,7 +288,7 @@ def main():
         m = 1024
         boxes = (("x0=100", Vec3i_t(100, 100, 100), Vec3i_t(900, 900, 900)),
                  ("x 0..800", Vec3i_t(0, 100, 100), Vec3i_t(800, 900, 900)))
-        settings = ((0, 2, 1), (3, 2, 1), (3, 4, 2))
+        settings = ((0, 2, 1), (3, 2, 1))   # (u8_unroll / u16_unroll: the whole-volume kernel's)
         for fmt, bpv, name in ((4, 1, "UInt8"), (5, 2, "UInt16")):
             A, B, D = alloc((m,) * 3, fmt, seed=1), alloc((m,) * 3, fmt, seed=2), alloc((m,) * 3, fmt)
             for rep in range(2):

@@ -1645,12 +1645,17 @@ namespace hipk
                 };
                 // (a 1-KiB quantum for the one-row 3-stream UInt16 ops measured the same as 2 KiB
                 // in an in-process A/B, 0.985 vs 0.986 ms for 1024^3 SumRange: one unroll for all)
+                // items per lane: the whole-volume kernel per knob (pointwise.u8_unroll / u16_unroll:
+                // 1 KiB per stream measured best); the multi-row kernel 1 KiB per stream for UInt8
+                // copies, the default 2 KiB otherwise (profiles/r05/rowsk.jsonl)
+                int64_t u = vecUnroll<NS, BPV>();
+                if (rowOnly)
+                    u = rt::knob(BPV == 1 ? rt::Knob::PointwiseU8Unroll : rt::Knob::PointwiseU16Unroll);
+                else if (rowsOnly && BPV == 1 && NS == 1)
+                    u = 2;
                 if constexpr (BPV == 1 && NS >= 1)
                 {
-                    // UInt8 row kernel: items per lane (knob pointwise.u8_unroll: 2 / 4 / 8 =
-                    // 1 / 2 / 4 KiB per stream per workgroup)
-                    int64_t const u = rt::knob(rt::Knob::PointwiseU8Unroll);
-                    if ((rowOnly || rowsOnly) && u == 2)
+                    if ((rowOnly || rowsOnly) && u == 2 && vecUnroll<NS, BPV>() != 2)
                     {
                         launch(std::integral_constant<int, 2>{}, std::true_type{});
                         return vktNoError;
@@ -1663,8 +1668,7 @@ namespace hipk
                 }
                 if constexpr (BPV == 2 && NS == 2)
                 {
-                    // UInt16 row kernel with 1 KiB per stream per workgroup (knob pointwise.u16_unroll 1)
-                    if ((rowOnly || rowsOnly) && rt::knob(rt::Knob::PointwiseU16Unroll) == 1)
+                    if ((rowOnly || rowsOnly) && u == 1)
                     {
                         launch(std::integral_constant<int, 1>{}, std::true_type{});
                         return vktNoError;

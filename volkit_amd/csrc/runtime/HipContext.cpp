@@ -253,7 +253,7 @@ namespace rt
             {"pointwise.u16_unroll", 1},
             {"pointwise.row_lds_u8", 0},
             {"pointwise.row_swizzle", 0},
-            {"pointwise.rows_kernel", 0},
+            {"pointwise.rows_kernel", 3},
         };
         static_assert(sizeof(kKnobs) / sizeof(kKnobs[0]) == static_cast<size_t>(Knob::Count), "knob table");
         std::atomic<int64_t> gKnobs[static_cast<int>(Knob::Count)] = {{kKnobs[0].def}, {kKnobs[1].def},
