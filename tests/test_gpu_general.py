@@ -446,32 +446,29 @@ def test_general_knob_matches_scalar_kernel(lib, o):
 
 @pytest.mark.parametrize("fmt", [4, 5, 7])
 def test_general_path_kernels(lib, o, fmt):
-    """The general vector path as one combined kernel (knob pointwise.gen_split 0) and as one
-    kernel per span path (1): wide 16-B items (1- and 4-byte voxels), 32-bit addressing, and the
-    64-bit row paths (knob pointwise.general_32bit 0) -- phase-shifted copies, clamped halos and a
-    shifted SafeSum, every one vs the oracle."""
+    """The general vector path's kernels -- one per span path for 1- and 4-byte destinations
+    (wide 16-B items, 32-bit addressing, and with knob pointwise.general_32bit 0 the 64-bit row
+    paths), the combined kernel for 2-byte ones: phase-shifted copies, clamped halos and a shifted
+    SafeSum, every one vs the oracle."""
     rng = np.random.default_rng(fmt + 77)
     src = rand_codes(rng, fmt, (7, 12, 150))
     src2 = rand_codes(rng, fmt, (7, 12, 150))
     dinit = rand_codes(rng, fmt, (7, 12, 150))
     from volkit_amd._lib import lib as L
     try:
-        for split in (0, 1):
-            for g32 in (1, 0):
-                assert L.vktHipSetTuningKnob(b"pointwise.gen_split", split) == 0
-                assert L.vktHipSetTuningKnob(b"pointwise.general_32bit", g32) == 0
-                for first, last, off in (((3, 0, 0), (150, 12, 7), (0, 0, 0)), ((-4, -3, -2), (146, 14, 8), (0, 0, 0)),
-                                         ((5, 2, 1), (141, 11, 6), (2, 1, 0))):
-                    copy_case(lib, o, fmt, fmt, (0.0, 1.0), (0.0, 1.0), src, dinit, first, last, off,
-                              what=f"split={split} g32={g32} {first}->{last}+{off}")
-                first, last, off = (9, 1, 1), (140, 11, 6), (-7, 1, 0)
-                da, db, dd = Dev(src, fmt), Dev(src2, fmt), Dev(dinit, fmt)
-                assert L.vktHipArithmeticRange(OPS.index("SafeSum"), dd.view, da.view, db.view, vec(first), vec(last),
-                                               vec(off)) == 0, last_error()
-                ref = o.arith("SafeSum", [fmt] * 3, [(0.0, 1.0)] * 3, src, src2, dinit.copy(), first, last, off)
-                assert_codes_equal(dd.read(), ref, fmt, f"SafeSum split={split} g32={g32}")
+        for g32 in (1, 0):
+            assert L.vktHipSetTuningKnob(b"pointwise.general_32bit", g32) == 0
+            for first, last, off in (((3, 0, 0), (150, 12, 7), (0, 0, 0)), ((-4, -3, -2), (146, 9, 5), (0, 0, 0)),
+                                     ((5, 2, 1), (141, 11, 6), (2, 1, 0))):
+                copy_case(lib, o, fmt, fmt, (0.0, 1.0), (0.0, 1.0), src, dinit, first, last, off,
+                          what=f"g32={g32} {first}->{last}+{off}")
+            first, last, off = (9, 1, 1), (140, 11, 6), (-7, 1, 0)
+            da, db, dd = Dev(src, fmt), Dev(src2, fmt), Dev(dinit, fmt)
+            assert L.vktHipArithmeticRange(OPS.index("SafeSum"), dd.view, da.view, db.view, vec(first), vec(last),
+                                           vec(off)) == 0, last_error()
+            ref = o.arith("SafeSum", [fmt] * 3, [(0.0, 1.0)] * 3, src, src2, dinit.copy(), first, last, off)
+            assert_codes_equal(dd.read(), ref, fmt, f"SafeSum g32={g32}")
     finally:
-        L.vktHipSetTuningKnob(b"pointwise.gen_split", -1)
         L.vktHipSetTuningKnob(b"pointwise.general_32bit", -1)
 
 

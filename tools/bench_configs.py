@@ -307,33 +307,6 @@ def main():
             for k in (b"pointwise.rows_kernel", b"pointwise.u8_unroll", b"pointwise.u16_unroll"):
                 lib.vktHipSetTuningKnob(k, -1)
             free(A, B, D)
-    if want("gensplit"):
-        # the general vector path, combined kernel vs one kernel per span path (knob
-        # pointwise.gen_split), alternated: phase-shifted and clamped boxes of 1024^3
-        m = 1024
-        for fmt, bpv, name in ((4, 1, "UInt8"), (5, 2, "UInt16"), (7, 4, "Float32")):
-            A, B, D = alloc((m,) * 3, fmt, seed=1), alloc((m,) * 3, fmt, seed=2), alloc((m,) * 3, fmt)
-            f0, f1 = Vec3i_t(100, 100, 100), Vec3i_t(900, 900, 900)
-            nv = 800 ** 3
-            for rep in range(2):
-                for k in (0, 1):
-                    lib.vktHipSetTuningKnob(b"pointwise.gen_split", k)
-                    tag = f"[gen_split={k}]"
-                    report(f"gensplit SumRange 800^3 x0=100 dstOffset x=-97 {name} {tag}",
-                           timed(lambda: lib.vktHipArithmeticRange(0, D, A, B, f0, f1, Vec3i_t(-97, 0, 0)), R),
-                           3 * bpv * nv, nv)
-                    report(f"gensplit CopyRange 800^3 x0=100 -> dst 0 {name} {tag}",
-                           timed(lambda: lib.vktHipCopyRange(D, A, f0, f1, o), R), 2 * bpv * nv, nv)
-                    n1 = 1021 * m * m
-                    report(f"gensplit CopyRange 1021x1024^2 x0=3 -> 0 {name} {tag}",
-                           timed(lambda: lib.vktHipCopyRange(D, A, Vec3i_t(3, 0, 0), Vec3i_t(m, m, m), o), R),
-                           2 * bpv * n1, n1)
-                    nh = 1022 ** 3
-                    report(f"gensplit CopyRange 1022^3 halo from -1 {name} {tag}",
-                           timed(lambda: lib.vktHipCopyRange(D, A, Vec3i_t(-1, -1, -1), Vec3i_t(1021, 1021, 1021), o), R),
-                           2 * bpv * nh, nh)
-            lib.vktHipSetTuningKnob(b"pointwise.gen_split", -1)
-            free(A, B, D)
     if want("u8cal"):
         # FETCH_SIZE calibration for the UInt8 access shapes and the
         # whole-volume UInt8 ops against UInt16 (item 4); one launch per case for PMC passes.

@@ -1484,6 +1484,31 @@ namespace hipk
         }
     }
 
+    // One span path of the general kernel per instantiation (PATH 0 wide 16-B items, 1 32-bit
+    // addressing, 2 64-bit rows on 32-bit division, 3 64-bit division), chosen on the host from the
+    // same GenGeom flags: the combined kernel's register count is set by its largest path (152
+    // VGPRs for UInt8 SumRange) whichever one a launch takes.
+    template <int NS, int BD, int B1, int B2, int U, int PATH, class F>
+    __global__ __launch_bounds__(kVecBlock) void pointwiseGenPathKernel(Operand d, Operand s1, Operand s2, GenGeom g,
+                                                                       F f, uint64_t qBase, uint64_t qEnd)
+    {
+        constexpr uint64_t kQ = static_cast<uint64_t>(kVecBlock) * U;
+        for (uint64_t q = qBase + blockIdx.x; q < qEnd; q += gridDim.x)
+        {
+            uint64_t const beg = q * kQ;
+            if (beg >= g.items)
+                break;
+            uint64_t const end = beg + kQ < g.items ? beg + kQ : g.items;
+            if constexpr (PATH == 0)
+                pointwiseGenSpanFast16<NS, BD, U>(d, s1, s2, g, static_cast<uint32_t>(beg), static_cast<uint32_t>(end), f);
+            else if constexpr (PATH == 1)
+                pointwiseGenSpanFast<NS, BD, B1, B2, U>(d, s1, s2, g, static_cast<uint32_t>(beg),
+                                                        static_cast<uint32_t>(end), f);
+            else
+                pointwiseGenSpan<NS, BD, B1, B2, PATH - 1, U>(d, s1, s2, g, beg, end, f);
+        }
+    }
+
     template <int NS, class F>
     __global__ __launch_bounds__(kBlock) void pointwiseScalarKernel(Operand d, Operand s1, Operand s2, Geom g, F f)
     {
@@ -1541,12 +1566,37 @@ namespace hipk
         GenGeom const& gg = p.gg;
         uint64_t const quanta = (gg.items + kQ - 1) / kQ;
         uint64_t const maxQ = static_cast<uint64_t>(rt::knob(rt::Knob::PointwiseMaxQuanta));
+        // 1- and 4-byte destinations: one kernel per span path (pointwiseGenPathKernel); 2-byte:
+        // the combined kernel.  In-process A/B on 1024^3-class boxes (profiles/r05/gensplit.jsonl):
+        // UInt8 SumRange dstOffset -97 0.431-0.516 -> 0.393-0.396 ms, UInt8 shifted copies -3 ..
+        // -5 %, Float32 SumRange -1 %, copies -2 % (one +2 %); UInt16 +1 .. +2 % (the clamped
+        // halo copy -6 %), so UInt16 keeps the combined kernel.
+        constexpr bool kSplit = BD == 1 || BD == 4;
+        constexpr bool kWideOk = (BD == 1 || BD == 4) && B1 == BD && (NS < 2 || B2 == BD);
+        int const path = kWideOk && gg.wide ? 0 : gg.fast ? 1 : gg.fast32 ? 2 : 3;
         uint64_t q0 = 0;
         do
         {
             uint64_t const n = quanta - q0 < maxQ ? quanta - q0 : maxQ;
-            hipLaunchKernelGGL((pointwiseGenKernel<NS, BD, B1, B2, U, F>), dim3(static_cast<unsigned>(n > 0 ? n : 1)),
-                               dim3(kVecBlock), 0, stream, p.d, p.s1, p.s2, gg, f, q0, q0 + n);
+            dim3 const grid(static_cast<unsigned>(n > 0 ? n : 1));
+            if constexpr (!kSplit)
+                hipLaunchKernelGGL((pointwiseGenKernel<NS, BD, B1, B2, U, F>), grid, dim3(kVecBlock), 0, stream, p.d,
+                                   p.s1, p.s2, gg, f, q0, q0 + n);
+            else if (path == 0)
+            {
+                if constexpr (kWideOk)
+                    hipLaunchKernelGGL((pointwiseGenPathKernel<NS, BD, B1, B2, U, 0, F>), grid, dim3(kVecBlock), 0,
+                                       stream, p.d, p.s1, p.s2, gg, f, q0, q0 + n);
+            }
+            else if (path == 1)
+                hipLaunchKernelGGL((pointwiseGenPathKernel<NS, BD, B1, B2, U, 1, F>), grid, dim3(kVecBlock), 0, stream,
+                                   p.d, p.s1, p.s2, gg, f, q0, q0 + n);
+            else if (path == 2)
+                hipLaunchKernelGGL((pointwiseGenPathKernel<NS, BD, B1, B2, U, 2, F>), grid, dim3(kVecBlock), 0, stream,
+                                   p.d, p.s1, p.s2, gg, f, q0, q0 + n);
+            else
+                hipLaunchKernelGGL((pointwiseGenPathKernel<NS, BD, B1, B2, U, 3, F>), grid, dim3(kVecBlock), 0, stream,
+                                   p.d, p.s1, p.s2, gg, f, q0, q0 + n);
             q0 += n;
         } while (q0 < quanta);
         return vktNoError;
