@@ -142,6 +142,9 @@ VKTAPI vktError vktHipKernelScopeEnd(vktHipKernelScope scope);
  * never race; a caller that writes bytes within 64 B of a box row from another stream or the
  * host while such a call runs must order the two itself. */
 VKTAPI vktError vktHipSetTuningKnob(const char* name, int64_t value);
+/* The current value of a tuning knob (read by the header-only Transform templates of
+ * volkit_transform.hpp, e.g. "transform.shape"); vktInvalidValue for an unknown name. */
+VKTAPI vktError vktHipGetTuningKnob(const char* name, int64_t* value);
 /* Record `message` as the calling thread's last error, log it; returns vktInvalidValue. */
 VKTAPI vktError vktHipReportError(const char* message);
 

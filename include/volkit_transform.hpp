@@ -215,11 +215,13 @@ namespace transform_detail
     // the one at or above its end (16-B, or 64-B sectors where the rows allow: a partly written
     // 64-B sector costs HBM a read-modify-write); voxels outside [rx0, rx1) are stored back as
     // they were loaded, without calling the functor.
-    template <int BPV, bool GUARD, bool PAD, class Op>
-    __global__ void __launch_bounds__(kBlock) unaryVecKernel(Vol v, Rows g, uint32_t itemBase, Op op)
+    // Workgroup shape (NT threads x U 16-B items per lane): knob transform.shape (vecShape below).
+    template <int BPV, bool GUARD, bool PAD, int NT, int U, class Op>
+    __global__ void __launch_bounds__(NT) unaryVecKernel(Vol v, Rows g, uint32_t itemBase, Op op)
     {
         constexpr int V = 16 / BPV;
-        uint32_t base = itemBase + blockIdx.x * (kBlock * kUnroll) + threadIdx.x;
+        constexpr int kUnroll = U;
+        uint32_t base = itemBase + blockIdx.x * (NT * kUnroll) + threadIdx.x;
         u32x4 w[kUnroll];
         uint64_t at[kUnroll];
         int32_t xs[kUnroll], ys[kUnroll], zs[kUnroll];
@@ -227,7 +229,7 @@ namespace transform_detail
 #pragma unroll
         for (int u = 0; u < kUnroll; ++u)
         {
-            uint32_t local = base + u * kBlock;
+            uint32_t local = base + u * NT;
             ok[u] = !GUARD || local < g.items;
             if (GUARD && !ok[u])
                 local = 0;
@@ -281,11 +283,12 @@ namespace transform_detail
     // ALIAS: both handles name one buffer with one layout: the voxel is loaded once, both
     // scratches start from it, and volume2's bytes are stored (the serial loop stores
     // volume1's, then volume2's, to the same address).
-    template <int BPV, bool GUARD, bool ALIAS, bool PAD, class Op>
-    __global__ void __launch_bounds__(kBlock) binaryVecKernel(Vol v1, Vol v2, Rows g, uint32_t itemBase, Op op)
+    template <int BPV, bool GUARD, bool ALIAS, bool PAD, int NT, int U, class Op>
+    __global__ void __launch_bounds__(NT) binaryVecKernel(Vol v1, Vol v2, Rows g, uint32_t itemBase, Op op)
     {
         constexpr int V = 16 / BPV;
-        uint32_t base = itemBase + blockIdx.x * (kBlock * kUnroll) + threadIdx.x;
+        constexpr int kUnroll = U;
+        uint32_t base = itemBase + blockIdx.x * (NT * kUnroll) + threadIdx.x;
         u32x4 w1[kUnroll], w2[kUnroll];
         uint64_t at1[kUnroll], at2[kUnroll];
         int32_t xs[kUnroll], ys[kUnroll], zs[kUnroll];
@@ -293,7 +296,7 @@ namespace transform_detail
 #pragma unroll
         for (int u = 0; u < kUnroll; ++u)
         {
-            uint32_t local = base + u * kBlock;
+            uint32_t local = base + u * NT;
             ok[u] = !GUARD || local < g.items;
             if (GUARD && !ok[u])
                 local = 0;
@@ -378,7 +381,8 @@ namespace transform_detail
     inline Vol volOf(StructuredVolume& s)
     {
         Vol v;
-        v.data = s.getData();   // migrates to the device first (GPU policy)
+        // migrates to the device first (GPU policy); nullptr when that failed (bytes stay on the host)
+        v.data = s.getDataFor(GetThreadExecutionPolicy());
         Vec3i d = s.getDims();
         v.dimX = static_cast<uint64_t>(d.x);
         v.dimY = static_cast<uint64_t>(d.y);
@@ -399,6 +403,17 @@ namespace transform_detail
     {
         return (reinterpret_cast<uintptr_t>(v.data) & 15u) == 0 && (static_cast<uint64_t>(x0) * bpv) % 16 == 0 &&
                (static_cast<uint64_t>(nx) * bpv) % 16 == 0 && (v.dimX * bpv) % 16 == 0;
+    }
+
+    // A 16-B-aligned range whose rows do not start and end on 64-B sectors still takes the
+    // padded launch when the layout allows sectors: a partly written sector costs HBM a
+    // read-modify-write (measured, TransformRange x 16..1008 of 1024^3 UInt8: 0.51 of peak on
+    // 16-B items vs 0.74 for the sector-padded 2..1022).
+    inline int padUnit(Vol const& v, int bpv);
+    inline bool sectorAligned(Vol const& v, int32_t x0, uint32_t nx, int bpv)
+    {
+        return padUnit(v, bpv) != 64 ||
+               ((static_cast<uint64_t>(x0) * bpv) % 64 == 0 && (static_cast<uint64_t>(nx) * bpv) % 64 == 0);
     }
 
     // Padding unit for a range that vec16 refuses: rows start on 16-B (64-B) boundaries, so a
@@ -452,18 +467,39 @@ namespace transform_detail
         return hipSuccess;
     }
 
+    // Workgroup shape of the 16-B vector kernels, knob transform.shape: 0 = 256 threads x 4 items
+    // (16 KiB per stream per workgroup), 1 = one wave x 2 items (2 KiB), 2 = one wave x 1 item
+    // (1 KiB) -- the pointwise engine's measured sweet spot for streaming ops is one-wave
+    // workgroups of 1-2 KiB per stream.
+    inline int vecShape()
+    {
+        int64_t k = 0;
+        if (vktHipGetTuningKnob("transform.shape", &k) != vktNoError || k < 0 || k > 2)
+            k = 0;
+        return static_cast<int>(k);
+    }
+
     // Whole workgroups without guards, then the remainder with guards:
-    // launch(guarded, itemBase, blocks) enqueues one kernel.
+    // launch(guarded, itemBase, blocks, NT, U) enqueues one kernel (NT / U as integral constants).
     template <class Launch>
     void launchVec(Rows const& g, Launch&& launch)
     {
-        constexpr uint64_t perBlock = uint64_t(kBlock) * kUnroll;
-        uint64_t full = g.items / perBlock;
-        if (full > 0)
-            launch(false, 0u, static_cast<uint32_t>(full));
-        uint64_t done = full * perBlock;
-        if (done < g.items)
-            launch(true, static_cast<uint32_t>(done), static_cast<uint32_t>((g.items - done + perBlock - 1) / perBlock));
+        auto run = [&](auto nt, auto u) {
+            constexpr uint64_t perBlock = uint64_t(decltype(nt)::value) * decltype(u)::value;
+            uint64_t full = g.items / perBlock;
+            if (full > 0)
+                launch(false, 0u, static_cast<uint32_t>(full), nt, u);
+            uint64_t done = full * perBlock;
+            if (done < g.items)
+                launch(true, static_cast<uint32_t>(done), static_cast<uint32_t>((g.items - done + perBlock - 1) / perBlock),
+                       nt, u);
+        };
+        switch (vecShape())
+        {
+        case 1: run(std::integral_constant<int, 64>{}, std::integral_constant<int, 2>{}); break;
+        case 2: run(std::integral_constant<int, 64>{}, std::integral_constant<int, 1>{}); break;
+        default: run(std::integral_constant<int, kBlock>{}, std::integral_constant<int, kUnroll>{}); break;
+        }
     }
 
     struct Scope
@@ -506,6 +542,11 @@ namespace transform_detail
         if (last.x <= first.x || last.y <= first.y || last.z <= first.z)
             return scope.end();
         Vol v = volOf(volume);
+        if (v.data == nullptr)
+        {
+            scope.end();
+            return static_cast<Error>(vktHipReportError("TransformRange_hip: the volume is not in HBM (its migration failed)"));
+        }
         int bpv = bytesPerVoxel(v.format);
         if (bpv != 1 && bpv != 2 && bpv != 4)
         {
@@ -515,7 +556,7 @@ namespace transform_detail
         uint32_t nx = static_cast<uint32_t>(last.x - first.x);
         hipStream_t s = scope.stream;
         hipError_t err = hipSuccess;
-        bool const aligned = vec16(v, first.x, nx, bpv);
+        bool const aligned = vec16(v, first.x, nx, bpv) && sectorAligned(v, first.x, nx, bpv);
         int const unit = aligned ? 0 : padUnit(v, bpv);
         if (aligned || unit != 0)
         {
@@ -527,9 +568,10 @@ namespace transform_detail
                 Rows g = gp;
                 g.rx0 = first.x;
                 g.rx1 = last.x;
-                launchVec(g, [&](bool guard, uint32_t base, uint32_t blocks) {
-                    dim3 grid(blocks), block(kBlock);
-#define VKT_UN_VEC_(B, G, P) unaryVecKernel<B, G, P><<<grid, block, 0, s>>>(v, g, base, op)
+                launchVec(g, [&](bool guard, uint32_t base, uint32_t blocks, auto ntc, auto uc) {
+                    constexpr int NT = decltype(ntc)::value, U = decltype(uc)::value;
+                    dim3 grid(blocks), block(NT);
+#define VKT_UN_VEC_(B, G, P) unaryVecKernel<B, G, P, NT, U><<<grid, block, 0, s>>>(v, g, base, op)
 #define VKT_UN_VEC_B_(B)                                                               \
     (aligned ? (guard ? VKT_UN_VEC_(B, true, false) : VKT_UN_VEC_(B, false, false))    \
              : (guard ? VKT_UN_VEC_(B, true, true) : VKT_UN_VEC_(B, false, true)))
@@ -595,6 +637,11 @@ namespace transform_detail
             return scope.end();
         Vol a = volOf(volume1);
         Vol b = volOf(volume2);
+        if (a.data == nullptr || b.data == nullptr)
+        {
+            scope.end();
+            return static_cast<Error>(vktHipReportError("TransformRange_hip: a volume is not in HBM (its migration failed)"));
+        }
         int b1 = bytesPerVoxel(a.format), b2 = bytesPerVoxel(b.format);
         if ((b1 != 1 && b1 != 2 && b1 != 4) || (b2 != 1 && b2 != 2 && b2 != 4))
         {
@@ -609,7 +656,8 @@ namespace transform_detail
         }
         uint32_t nx = static_cast<uint32_t>(last.x - first.x);
         hipStream_t s = scope.stream;
-        bool const aligned = b1 == b2 && vec16(a, first.x, nx, b1) && vec16(b, first.x, nx, b2);
+        bool const aligned = b1 == b2 && vec16(a, first.x, nx, b1) && vec16(b, first.x, nx, b2) &&
+                             sectorAligned(a, first.x, nx, b1) && sectorAligned(b, first.x, nx, b2);
         int const ua = b1 == b2 && !aligned ? padUnit(a, b1) : 0, ub = b1 == b2 && !aligned ? padUnit(b, b2) : 0;
         int const unit = ua < ub ? ua : ub;
         if (aligned || unit != 0)
@@ -622,9 +670,10 @@ namespace transform_detail
                 Rows g = gp;
                 g.rx0 = first.x;
                 g.rx1 = last.x;
-                launchVec(g, [&](bool guard, uint32_t base, uint32_t blocks) {
-                    dim3 grid(blocks), block(kBlock);
-#define VKT_BIN_VEC_(B, G, A, P) binaryVecKernel<B, G, A, P><<<grid, block, 0, s>>>(a, b, g, base, op)
+                launchVec(g, [&](bool guard, uint32_t base, uint32_t blocks, auto ntc, auto uc) {
+                    constexpr int NT = decltype(ntc)::value, U = decltype(uc)::value;
+                    dim3 grid(blocks), block(NT);
+#define VKT_BIN_VEC_(B, G, A, P) binaryVecKernel<B, G, A, P, NT, U><<<grid, block, 0, s>>>(a, b, g, base, op)
 #define VKT_BIN_VEC_P_(B, P)                                                                    \
     (alias ? (guard ? VKT_BIN_VEC_(B, true, true, P) : VKT_BIN_VEC_(B, false, true, P))         \
            : (guard ? VKT_BIN_VEC_(B, true, false, P) : VKT_BIN_VEC_(B, false, false, P)))

@@ -208,6 +208,35 @@ int vktt_run_unary_slab(int op, void* data, int dx, int dy, int dz, int fmt, flo
     return 0;
 }
 
+// Whole-volume Transform of a volume created in HOST memory (CPU policy), run under the GPU
+// policy so the bytes migrate to HBM first.  failAlloc > 0 makes that many device allocations
+// fail (knob memory.fail_next_alloc): Transform must then return an error and leave the bytes,
+// still in host memory, untouched.  data is updated in place either way.
+int vktt_run_unary_migrating(int op, void* data, int dx, int dy, int dz, int fmt, int failAlloc)
+{
+    vkt::ExecutionPolicy const saved = vkt::GetThreadExecutionPolicy();
+    vkt::ExecutionPolicy cpu = saved;
+    cpu.device = vkt::ExecutionPolicy::Device::CPU;
+    vkt::SetThreadExecutionPolicy(cpu);
+    int rc = 0;
+    {
+        vkt::StructuredVolume v(dx, dy, dz, static_cast<vkt::DataFormat>(fmt));
+        std::memcpy(v.getData(), data, v.getSizeInBytes());
+        {
+            GpuPolicy gpu;
+            vktHipSetTuningKnob("memory.fail_next_alloc", failAlloc);
+            rc = withUnary(op, [&](auto f) { return static_cast<int>(vkt::Transform(v, f)); });
+            vktHipSetTuningKnob("memory.fail_next_alloc", 0);
+            if (rc == 0)
+                download(data, v);
+        }
+        if (rc != 0)   // CPU policy again: the host bytes, no migration
+            std::memcpy(data, v.getData(), v.getSizeInBytes());
+    }
+    vkt::SetThreadExecutionPolicy(saved);
+    return rc;
+}
+
 // Whole-volume Transform (the reference's vkt::Transform(volume, op) entry).
 int vktt_run_unary_whole(int op, void* data, int dx, int dy, int dz, int fmt, float lo, float hi)
 {

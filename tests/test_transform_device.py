@@ -42,6 +42,7 @@ def t():
     lib.vktt_host_binary.argtypes = [i]
     lib.vktt_bench_unary.argtypes = [i, i, i, i, i, i, C.POINTER(f)]
     lib.vktt_lambda_or.argtypes = [p, p, i, i, i]
+    lib.vktt_run_unary_migrating.argtypes = [i, p, i, i, i, i, i]
     return lib
 
 
@@ -225,3 +226,65 @@ def test_device_lambda(t):
     r1, r2 = oracle_binary(t, 0, a, 4, (0.0, 1.0), b, 4, (0.0, 1.0), (0, 0, 0), (48, 17, 9))
     np.testing.assert_array_equal(ga, r1)
     np.testing.assert_array_equal(gb, r2)
+
+
+@pytest.fixture
+def shape_knob():
+    """Set the vector kernels' workgroup shape (knob transform.shape) for one test."""
+    from volkit_amd._lib import lib
+    shapes = []
+
+    def set_shape(k):
+        assert lib.vktHipSetTuningKnob(b"transform.shape", k) == 0
+        got = C.c_int64(-1)
+        assert lib.vktHipGetTuningKnob(b"transform.shape", C.byref(got)) == 0 and got.value == k
+        shapes.append(k)
+
+    yield set_shape
+    lib.vktHipSetTuningKnob(b"transform.shape", -1)
+
+
+@pytest.mark.parametrize("shape", [0, 1, 2])
+def test_vector_kernel_shapes(t, shape_knob, shape):
+    """Every workgroup shape of the 16-B vector kernels (256x4, one wave x 2, one wave x 1
+    items per lane): unguarded whole workgroups plus the guarded tail, padded sector rows,
+    unary and binary (incl. aliased) functors, against the oracle."""
+    shape_knob(shape)
+    rng = np.random.default_rng(900 + shape)
+    for fmt in (4, 5, 7):
+        for dims, first, last in RANGES:
+            codes = rand_codes(rng, fmt, dims[::-1])
+            for op in (0, 3):
+                out = gpu_unary(t, op, codes, fmt, (-1.0, 3.0), first, last)
+                ref = oracle_unary(t, op, codes, fmt, (-1.0, 3.0), first, last)
+                assert_codes_equal(out, ref, fmt, f"shape={shape} {UNARY_OPS[op]} fmt={fmt} {dims} {first}->{last}")
+            c2 = rand_codes(rng, 4, dims[::-1])
+            o1, o2 = gpu_binary(t, 1, codes, fmt, (0.0, 1.0), c2, 4, (0.0, 1.0), first, last)
+            r1, r2 = oracle_binary(t, 1, codes, fmt, (0.0, 1.0), c2, 4, (0.0, 1.0), first, last)
+            assert_codes_equal(o1, r1, fmt, f"shape={shape} MixFormats {dims} volume1")
+            assert_codes_equal(o2, r2, 4, f"shape={shape} MixFormats {dims} volume2")
+            o1, _ = gpu_binary(t, 0, codes, fmt, (0.0, 1.0), codes, fmt, (0.0, 1.0), first, last, alias=True)
+            r1, _ = oracle_binary(t, 0, codes, fmt, (0.0, 1.0), codes, fmt, (0.0, 1.0), first, last, alias=True)
+            assert_codes_equal(o1, r1, fmt, f"shape={shape} aliased Or fmt={fmt} {dims}")
+    for fmt, dims in ((4, (96, 70, 9)), (5, (64, 40, 33)), (7, (32, 33, 17)), (4, (256, 129, 7))):
+        codes = rand_codes(rng, fmt, dims[::-1])
+        out = gpu_unary(t, 2, codes, fmt, (0.0, 1.0), None, None, whole=True)
+        ref = oracle_unary(t, 2, codes, fmt, (0.0, 1.0), (0, 0, 0), dims)
+        assert_codes_equal(out, ref, fmt, f"shape={shape} whole Diagonal fmt={fmt} {dims}")
+
+
+def test_failed_migration_is_an_error(t):
+    """Transform of a host-resident volume whose migration to HBM fails: an error, the bytes
+    (still in host memory) untouched; with the allocation allowed the same call migrates and
+    matches the oracle."""
+    from volkit_amd._lib import lib
+    rng = np.random.default_rng(12)
+    codes = rand_codes(rng, 5, (33, 40, 64))
+    out = np.ascontiguousarray(codes.copy())
+    z, y, x = out.shape
+    assert t.vktt_run_unary_migrating(2, out.ctypes.data, x, y, z, 5, 1) != 0
+    assert b"migration failed" in lib.vktHipGetLastErrorString()
+    np.testing.assert_array_equal(out, codes)
+    assert t.vktt_run_unary_migrating(2, out.ctypes.data, x, y, z, 5, 0) == 0
+    ref = oracle_unary(t, 2, codes, 5, (0.0, 1.0), (0, 0, 0), (x, y, z))
+    assert_codes_equal(out, ref, 5, "migrated Diagonal")

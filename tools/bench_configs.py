@@ -182,6 +182,35 @@ def main():
                 raise RuntimeError(_lib.last_error())
             nv = (m - 4) ** 3
             report(f"TransformRange Diagonal 2..{m - 2} of 1024^3 fmt={fmt}", ms.value, 2 * b * nv, nv)
+    if want("tshape"):
+        # Transform vector-kernel workgroup shape A/B (knob transform.shape: 0 256x4, 1 64x2, 2 64x1)
+        t = C.CDLL(os.path.join(ROOT, "tests", "native", "libfixtures.so"))
+        t.vktt_bench_unary.argtypes = [C.c_int] * 6 + [C.POINTER(C.c_float)]
+        t.vktt_bench_unary_range.argtypes = [C.c_int] * 12 + [C.POINTER(C.c_float)]
+        ms = C.c_float(0.0)
+        m = 1024
+        try:
+            for shape in (0, 1, 2):
+                lib.vktHipSetTuningKnob(b"transform.shape", shape)
+                for fmt, b in ((4, 1), (5, 2), (7, 4)):
+                    if t.vktt_bench_unary(2, m, m, m, fmt, R, C.byref(ms)) != 0:
+                        raise RuntimeError(_lib.last_error())
+                    report(f"Transform Diagonal 1024^3 fmt={fmt} shape={shape}", ms.value, 2 * b * m ** 3, m ** 3)
+                    if t.vktt_bench_unary_range(2, m, m, m, fmt, 2, 2, 2, m - 2, m - 2, m - 2, R, C.byref(ms)) != 0:
+                        raise RuntimeError(_lib.last_error())
+                    nv = (m - 4) ** 3
+                    report(f"TransformRange Diagonal 2..{m - 2} fmt={fmt} shape={shape}", ms.value, 2 * b * nv, nv)
+                    if t.vktt_bench_unary_range(2, m, m, m, fmt, 16, 3, 5, m - 16, m - 3, m - 5, R, C.byref(ms)) != 0:
+                        raise RuntimeError(_lib.last_error())
+                    nv = (m - 32) * (m - 6) * (m - 10)
+                    report(f"TransformRange Diagonal x16..{m - 16} fmt={fmt} shape={shape}", ms.value, 2 * b * nv, nv)
+                    if t.vktt_bench_unary_range(2, m, m, m, fmt, 0, 2, 2, m, m - 2, m - 2, R, C.byref(ms)) != 0:
+                        raise RuntimeError(_lib.last_error())
+                    nv = m * (m - 4) * (m - 4)
+                    report(f"TransformRange Diagonal full rows y,z 2..{m - 2} fmt={fmt} shape={shape}", ms.value,
+                           2 * b * nv, nv)
+        finally:
+            lib.vktHipSetTuningKnob(b"transform.shape", -1)
     if want("memset"):
         # MemsetRange / ManagedBuffer::fill at 1024^3-UInt16 scale (2 GiB), write-only bytes
         nb = 2 << 30

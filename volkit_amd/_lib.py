@@ -240,6 +240,7 @@ SIGNATURES = {
     "vktHipKernelScopeEnd": (c_err, [C.c_void_p]),
     "vktHipReportError": (c_err, [C.c_char_p]),
     "vktHipSetTuningKnob": (c_err, [C.c_char_p, C.c_int64]),
+    "vktHipGetTuningKnob": (c_err, [C.c_char_p, C.POINTER(C.c_int64)]),
     "vktHipAllocate": (c_err, [P(C.c_void_p), C.c_size_t]),
     "vktHipFree": (c_err, [C.c_void_p]),
     "vktHipReleaseCachedMemory": (c_err, [P(C.c_size_t)]),

@@ -254,6 +254,7 @@ namespace rt
             {"pointwise.row_lds_u8", 0},
             {"pointwise.row_swizzle", 0},
             {"pointwise.rows_kernel", 3},
+            {"transform.shape", 0},
         };
         static_assert(sizeof(kKnobs) / sizeof(kKnobs[0]) == static_cast<size_t>(Knob::Count), "knob table");
         std::atomic<int64_t> gKnobs[static_cast<int>(Knob::Count)] = {{kKnobs[0].def}, {kKnobs[1].def},
@@ -274,7 +275,8 @@ namespace rt
                                                                   {kKnobs[30].def}, {kKnobs[31].def},
                                                                   {kKnobs[32].def}, {kKnobs[33].def},
                                                                   {kKnobs[34].def}, {kKnobs[35].def},
-                                                                  {kKnobs[36].def}, {kKnobs[37].def}};
+                                                                  {kKnobs[36].def}, {kKnobs[37].def},
+                                                                  {kKnobs[38].def}};
     } // namespace
 
     int64_t knob(Knob k) { return gKnobs[static_cast<int>(k)].load(std::memory_order_relaxed); }
@@ -496,6 +498,19 @@ vktError vktHipSetTuningKnob(char const* name, int64_t value)
             return vktNoError;
         }
     return rt::fail((std::string("vktHipSetTuningKnob: unknown knob ") + name).c_str());
+}
+
+vktError vktHipGetTuningKnob(char const* name, int64_t* value)
+{
+    if (name == nullptr || value == nullptr)
+        return rt::fail("vktHipGetTuningKnob: null pointer");
+    for (size_t i = 0; i < static_cast<size_t>(rt::Knob::Count); ++i)
+        if (std::strcmp(name, rt::kKnobs[i].name) == 0)
+        {
+            *value = rt::gKnobs[i].load(std::memory_order_relaxed);
+            return vktNoError;
+        }
+    return rt::fail((std::string("vktHipGetTuningKnob: unknown knob ") + name).c_str());
 }
 
 vktError vktHipReportError(char const* message)
