@@ -322,6 +322,28 @@ def test_histogram_packed16_matches_tiled_passes(fmt):
     np.testing.assert_array_equal(runs[0], ref)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("fmt,mapping", [(5, (0.0, 1.0)), (5, (-1.0, 3.0)), (7, (0.0, 1.0))])
+@pytest.mark.parametrize("nbins", [65536, 50001, 100000, 150000])
+def test_histogram_pair_tiles(fmt, mapping, nbins):
+    """Knob histogram.pair_tiles = 2: 2-4 tiles of 32-bit counters counted side by side in one
+    launch (workgroup groups on one XCD; the default 1 takes it where P16 does not apply), vs the
+    oracle: whole volume (integer / mul-shift /
+    float bins), a padded sub-box, and a constant region (the per-wave run register)."""
+    rng = np.random.default_rng(nbins + fmt)
+    codes = rand_codes(rng, fmt, (40, 100, 256), specials=True)
+    codes[5:9] = codes[5, 0, 0]      # constant planes: wave-uniform items
+    vol = ob.Volume(codes, fmt, *mapping)
+    lib.vktHipSetTuningKnob(b"histogram.pair_tiles", 2)   # also where P16 would take the bins
+    try:
+        for first, last in (((0, 0, 0), (256, 100, 40)), ((3, 1, 2), (250, 99, 37))):
+            got = gpu_histogram(codes, fmt, *mapping, first, last, nbins)
+            ref, _ = ob.histogram_range(vol, first, last, nbins)
+            np.testing.assert_array_equal(got, ref, err_msg=f"{first}->{last}")
+    finally:
+        lib.vktHipSetTuningKnob(b"histogram.pair_tiles", -1)
+
+
 def takes_moments(fmt, mapping):
     """UInt16 (integer moments under the unit mapping, float moments otherwise) and Float32 (float
     moments) take the one-pass moments paths (aggregates.moments)."""

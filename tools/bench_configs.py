@@ -897,6 +897,35 @@ def main():
         del arr, V
         ep.device = vkt.ExecutionPolicy.Device_CPU
         vkt.SetThreadExecutionPolicy(ep)
+    if want("pairtiles"):
+        # knob histogram.pair_tiles: the tiles of a > 40 704-bin histogram side by side in one
+        # launch (XCD-grouped workgroups) vs P16 (65 536 bins) / one pass per tile (more bins)
+        n = 1024
+        bins = C.c_void_p()
+        lib.vktHipAllocate(C.byref(bins), 150000 * 8)
+        last = Vec3i_t(n, n, n)
+        try:
+            for fmt, b in ((5, 2), (7, 4)):
+                V = alloc((n,) * 3, fmt, seed=11 if fmt == 5 else None)
+                if fmt == 7:
+                    rng_fill(V, n ** 3)
+                for nb in ((65536, 50000, 100000, 150000) if fmt == 5 else (65536, 100000)):
+                    for rep in range(2):
+                        for k in (0, 2):
+                            lib.vktHipSetTuningKnob(b"histogram.pair_tiles", k)
+                            ms = timed(lambda: lib.vktHipHistogramRange(V, o, last, bins, nb, 0), R)
+                            report(f"pairtiles Histogram 1024^3 fmt={fmt} {nb} bins [pair_tiles={k}]", ms,
+                                   b * n ** 3, n ** 3)
+                u0, u1 = Vec3i_t(100, 100, 100), Vec3i_t(900, 900, 900)
+                for k in (0, 2):
+                    lib.vktHipSetTuningKnob(b"histogram.pair_tiles", k)
+                    ms = timed(lambda: lib.vktHipHistogramRange(V, u0, u1, bins, 65536, 0), R)
+                    report(f"pairtiles Histogram 800^3 at x0=100 fmt={fmt} 65536 bins [pair_tiles={k}]", ms,
+                           b * 800 ** 3, 800 ** 3)
+                free(V)
+        finally:
+            lib.vktHipSetTuningKnob(b"histogram.pair_tiles", -1)
+            lib.vktHipFree(bins)
     if want("reduce"):
         # ComputeHistogram / ComputeAggregates on a device-resident 1024^3 UInt16
         n = 1024

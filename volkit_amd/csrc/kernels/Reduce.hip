@@ -362,6 +362,7 @@ namespace hipk
     constexpr uint32_t kReplicatedMaxBins = 10240;
     constexpr uint32_t kP16Flush = 0x4000u;   // packed 16-bit counters: moved to HBM at 2^14
     constexpr uint32_t kFastMaxTiles = 8;
+    constexpr uint32_t kPairMaxTiles = 4;   // PAIR: tiles side by side in one launch
     constexpr int kTileBlock = 1024;
 
     struct FastHistArgs
@@ -384,6 +385,7 @@ namespace hipk
         int32_t px0, rx0, rx1;
         uint32_t padded;
         uint32_t rows;              // codeCountsU8RowsKernel: range rows (ny * nz)
+        uint32_t pairTiles;         // PAIR: tiles counted side by side in one launch (tileBins each)
     };
 
     typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -493,9 +495,28 @@ namespace hipk
     // for ~100 000 cycles while the other waves of the workgroup keep issuing; a context save
     // stops the whole workgroup.  (A first version flushed on exactly kP16Flush - 1 returned:
     // 60 moves went missing on 64 Mi voxels alternating between the two halves of one word.)
-    template <int FMT, bool CONTIG, bool TILED, int BLOCK, bool SHIFT = false, bool P16 = false>
-    __global__ __launch_bounds__(BLOCK) void histogramFastKernel(FastHistArgs h)
+    //
+    // PAIR (TILED, not P16; knob histogram.pair_tiles): the T = h.pairTiles tiles of 32-bit
+    // counters in ONE launch instead of one launch per tile.  Workgroups b and b + 8 run on the
+    // same XCD (workgroups are dealt to the 8 XCDs round robin), so the T workgroups of a group
+    // -- same XCD, one tile each -- walk the same items side by side: the first read of an item
+    // comes from HBM, the others from that XCD's L2.  Each voxel is decoded T times but added
+    // once, with non-returning LDS adds (no 16-bit halves to watch).
+    template <int FMT, bool CONTIG, bool TILED, int BLOCK, bool SHIFT = false, bool P16 = false, bool PAIR = false>
+    __global__ __launch_bounds__(BLOCK) void histogramFastKernel(FastHistArgs hArg)
     {
+        static_assert(!PAIR || (TILED && !P16), "PAIR: tiles of 32-bit counters");
+        FastHistArgs h = hArg;
+        uint32_t group = blockIdx.x, groups = gridDim.x;
+        if constexpr (PAIR)
+        {
+            uint32_t const T = h.pairTiles;
+            uint32_t const tile = (blockIdx.x >> 3) % T;
+            group = (blockIdx.x / (8u * T)) * 8u + (blockIdx.x & 7u);
+            groups = gridDim.x / T;
+            h.tileBase = tile * h.tileBins;
+            h.tileBins = min(h.tileBins, h.nb - h.tileBase);
+        }
         constexpr int BPV = FMT == codec::FmtUInt8 ? 1 : FMT == codec::FmtUInt16 ? 2 : 4;
         constexpr int U = 4;
         constexpr uint32_t kOff = ~0u;   // UInt8 table: code outside the tile
@@ -716,8 +737,8 @@ namespace hipk
             }
         };
 
-        uint64_t const wave = static_cast<uint64_t>(blockIdx.x) * (BLOCK / 64) + (threadIdx.x >> 6);
-        uint64_t const waves = static_cast<uint64_t>(gridDim.x) * (BLOCK / 64);
+        uint64_t const wave = static_cast<uint64_t>(group) * (BLOCK / 64) + (threadIdx.x >> 6);
+        uint64_t const waves = static_cast<uint64_t>(groups) * (BLOCK / 64);
         uint64_t const steps = h.items / (64 * U);
         // Float32 spans: lane l's "item" of a 64-item block is the 4-voxel halves at 4l and
         // 256 + 4l, so each 16-B load instruction of the wave reads one contiguous KiB (a
@@ -2453,6 +2474,38 @@ namespace hipk
             unsigned const perCU = static_cast<unsigned>(std::min<size_t>(8, (160u * 1024u) / (lds + 1024u)));
             unsigned const g = streamingGrid(items, 64u * 4u * (kBlock / 64), std::max(1u, perCU));
             VKT_FAST_HIST_FMT(false, kBlock, g, lds);
+        }
+        else if (tiles > 1 && tiles <= kPairMaxTiles && fmt != codec::FmtUInt8 &&
+                 (rt::knob(rt::Knob::HistogramPairTiles) == 2 ||
+                  (rt::knob(rt::Knob::HistogramPairTiles) == 1 &&
+                   !((hh.numBins + 1) / 2 <= tileCap && rt::knob(rt::Knob::HistogramPacked16) != 0))))
+        {
+            // PAIR: the tiles side by side in one launch, workgroups of one group on one XCD
+            uint32_t const T = static_cast<uint32_t>(tiles);
+            h.rShift = 0;
+            h.tileBase = 0;
+            h.pairTiles = T;
+            h.tileBins = (h.nb + T - 1) / T;
+            unsigned const g0 = streamingGrid(items, 64u * 4u * (kTileBlock / 64), 1);
+            unsigned const groups = std::max(8u, g0 / T / 8u * 8u);
+            unsigned const g = groups * T;
+            size_t const lds = static_cast<size_t>(h.tileBins) * 4u;
+#define VKT_PAIR(FMT, SH)                                                                                          \
+    do {                                                                                                           \
+        if (contig)                                                                                                \
+            hipLaunchKernelGGL((histogramFastKernel<FMT, true, true, kTileBlock, SH, false, true>), dim3(g),        \
+                               dim3(kTileBlock), lds, s, h);                                                       \
+        else                                                                                                       \
+            hipLaunchKernelGGL((histogramFastKernel<FMT, false, true, kTileBlock, SH, false, true>), dim3(g),       \
+                               dim3(kTileBlock), lds, s, h);                                                       \
+    } while (0)
+            if (shift)
+                VKT_PAIR(codec::FmtUInt16, true);
+            else if (fmt == codec::FmtUInt16)
+                VKT_PAIR(codec::FmtUInt16, false);
+            else
+                VKT_PAIR(codec::FmtFloat32, false);
+#undef VKT_PAIR
         }
         else if (tiles > 1 && fmt != codec::FmtUInt8 && (hh.numBins + 1) / 2 <= tileCap &&
                  rt::knob(rt::Knob::HistogramPacked16) != 0)

@@ -132,7 +132,8 @@ namespace rt
         PointwiseRowLdsU8,             // the same occupancy cap for the UInt8 row kernel
         PointwiseRowSwizzle,           // > 0: the row kernel gives each XCD runs of this many consecutive quanta
         PointwiseRowsKernel,           // multi-row boxes (32-bit rows, no scalar edges) on the MODE-1 kernel: bit 0 UInt8, bit 1 UInt16
-        TransformShape,                // device-functor Transform vector kernels: 0 256x4, 1 64x2, 2 64x1 (read via vktHipGetTuningKnob)
+        TransformShape,
+        HistogramPairTiles,            // histograms of 2..4 tiles side by side in one launch (PAIR): 1 where P16 does not apply, 2 always, 0 never                // device-functor Transform vector kernels: 0 256x4, 1 64x2, 2 64x1 (read via vktHipGetTuningKnob)
         Count
     };
     int64_t knob(Knob k);
