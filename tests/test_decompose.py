@@ -407,3 +407,38 @@ def test_brick_decompose_pair_kernel(fmt, dims, brick, neg, pos):
     ref = ob.brick_decompose(ob.Volume(codes, fmt), brick, neg, pos)
     for idx, v in ref.items():
         np.testing.assert_array_equal(got[idx], v.codes, err_msg=f"brick {idx}")
+
+
+DIRECT_LAYOUTS = [
+    ((64, 64, 64), (64, 64, 64), (0, 0, 0), (0, 0, 0)),
+    ((128, 40, 33), (16, 8, 5), (0, 0, 0), (0, 0, 0)),     # border bricks along y and z
+    ((96, 20, 12), (32, 7, 5), (0, 0, 0), (0, 0, 0)),
+    ((160, 9, 130), (32, 9, 64), (0, 0, 0), (0, 0, 0)),    # one brick along y, bricks of several chunks
+    ((100, 20, 12), (20, 7, 5), (0, 0, 0), (0, 0, 0)),     # rows not whole 16-B words: staged kernel
+    ((64, 24, 16), (16, 8, 8), (0, 0, 0), (0, 1, 0)),      # a halo: staged kernel
+    ((176, 48, 40), (16, 16, 16), (0, 0, 0), (0, 0, 0)),   # 16^3: 2 (UInt16) / 4 (UInt8) bricks per workgroup,
+    ((144, 20, 24), (16, 8, 8), (0, 0, 0), (0, 0, 0)),     # odd brick counts (a partial last workgroup)
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("direct", [1, 2, 0])
+@pytest.mark.parametrize("fmt", [4, 5, 7])
+@pytest.mark.parametrize("dims,brick,neg,pos", DIRECT_LAYOUTS)
+def test_brick_decompose_direct_kernel(fmt, dims, brick, neg, pos, direct):
+    """Knob decompose.direct: halo-free grids whose box rows are whole 16-B words at aligned
+    source offsets copy each word with one load and one store (brickDirect, no LDS tile; 1:
+    small bricks 2 or 4 per workgroup, 2: one per workgroup); the other layouts and direct = 0
+    keep the staged kernel -- bit-exact vs the oracle either way."""
+    rng = np.random.default_rng(fmt * 100 + sum(dims) + 31)
+    codes = rand_codes(rng, fmt, dims[::-1])
+    assert lib.vktHipSetTuningKnob(b"decompose.direct", direct) == 0
+    try:
+        err, got = gpu_decompose(codes, fmt, (0.0, 1.0), brick, neg, pos)
+    finally:
+        assert lib.vktHipSetTuningKnob(b"decompose.direct", -1) == 0
+    assert err == vkt.NoError, vkt.last_error()
+    ref = ob.brick_decompose(ob.Volume(codes, fmt), brick, neg, pos)
+    assert set(got) == set(ref)
+    for idx, v in ref.items():
+        np.testing.assert_array_equal(got[idx], v.codes, err_msg=f"brick {idx}")

@@ -1153,6 +1153,39 @@ def main():
         del V
         ep.device = vkt.ExecutionPolicy.Device_CPU
         vkt.SetThreadExecutionPolicy(ep)
+    if want("decdirect"):
+        # in-process A/B of the direct halo-free brick copy (knob decompose.direct: 1 one load +
+        # one store per 16-B word, 0 the LDS-staged kernel), alternated, on the same bricks
+        import volkit_amd.volkit as vkt
+        ep = vkt.GetThreadExecutionPolicy()
+        ep.device = vkt.ExecutionPolicy.Device_GPU
+        vkt.SetThreadExecutionPolicy(ep)
+        n = 1024
+        for fmt, b in ((vkt.DataFormat_UInt16, 2), (vkt.DataFormat_UInt8, 1)):
+            V = vkt.StructuredVolume(n, n, n, fmt)
+            vkt.Synthesize(V, 77)
+            ab = {}
+            for bs in ((16, 32, 64) if b == 2 else (16, 32)):
+                arr = vkt.Array3D_StructuredVolume()
+                b3, h3 = vkt.Vec3i(bs, bs, bs), vkt.Vec3i(0, 0, 0)
+                vkt.BrickDecomposeResize(arr, V, b3, h3, h3)
+                for rnd in range(3):
+                    for kv in (1, 2, 0):
+                        lib.vktHipSetTuningKnob(b"decompose.direct", kv)
+                        ab.setdefault((b, bs, kv, "back-to-back"), []).append(
+                            pipelined(lambda: vkt.BrickDecompose(arr, V, b3, h3, h3), R))
+                        ab.setdefault((b, bs, kv, "incl. host planning"), []).append(
+                            timed(lambda: vkt.BrickDecompose(arr, V, b3, h3, h3), R))
+                del arr
+            lib.vktHipSetTuningKnob(b"decompose.direct", -1)
+            for (bb, bs, kv, how), ts in sorted(ab.items()):
+                ts.sort()
+                report(f"decdirect BrickDecompose 1024^3 {'UInt16' if bb == 2 else 'UInt8'} -> {bs}^3 bricks halo 0 "
+                       f"direct={kv} ({how}; median of 3 rounds, spread {ts[0]:.4f}-{ts[-1]:.4f})", ts[1],
+                       2 * bb * n ** 3, n ** 3)
+            del V
+        ep.device = vkt.ExecutionPolicy.Device_CPU
+        vkt.SetThreadExecutionPolicy(ep)
     if want("decdump"):
         # in-process A/B of the staged copy's partial-word writes (knob decompose.aligned_lds:
         # 0 per-voxel branches, 3 branch-free with dump bytes), alternated, on the same bricks

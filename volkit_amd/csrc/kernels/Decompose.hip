@@ -306,6 +306,45 @@ namespace hipk
         }
     }
 
+    // Direct copy of one chunk (knob decompose.direct): the brick grid has no clamped voxel and
+    // every box row is whole 16-B words at 16-B aligned source offsets (halo-free bricks whose x
+    // size is a multiple of 16 / BPV), so dst word i of a brick is ONE aligned 16-B source word:
+    // a load and a store per item, no LDS tile, no barrier.  Items past the brick load its last
+    // word again (every address stays valid) and do not store.
+    // NT threads of the workgroup (tid = 0 .. NT - 1) copy items [base, base + kPer NT) of the brick.
+    template <int BPV, int NT, int kPer = 4>
+    __device__ __forceinline__ void brickDirect(BrickDesc const& d, uint32_t base, uint8_t const* src, int32_t sdx,
+                                                int32_t sdy, uint32_t tid)
+    {
+        constexpr int32_t V = 16 / BPV;
+        uint64_t const spY = static_cast<uint64_t>(sdx), spZ = spY * static_cast<uint64_t>(sdy);
+        uint32_t const end = min(base + static_cast<uint32_t>(kPer * NT), d.nitems);
+        u32x4 v[kPer];
+#pragma unroll
+        for (int u = 0; u < kPer; ++u)
+        {
+            uint32_t const i = min(base + static_cast<uint32_t>(u * NT) + tid, end - 1u);
+            uint32_t const vox = i * V;
+            uint32_t const r = fdiv(vox, d.fdx);
+            uint32_t const x = vox - r * d.fdx.d;
+            uint32_t const z = fdiv(r, d.fdy);
+            uint32_t const y = r - z * d.fdy.d;
+            uint64_t const off = (static_cast<uint64_t>(d.fz + static_cast<int32_t>(z)) * spZ +
+                                  static_cast<uint64_t>(d.fy + static_cast<int32_t>(y)) * spY +
+                                  static_cast<uint64_t>(d.fx + static_cast<int32_t>(x))) * BPV;
+            // a plain (cached) load: the 128-B line of a row is shared by the x-neighbour bricks
+            // when rows are shorter than a line
+            v[u] = *reinterpret_cast<u32x4 const*>(src + off);
+        }
+#pragma unroll
+        for (int u = 0; u < kPer; ++u)
+        {
+            uint32_t const i = base + static_cast<uint32_t>(u * NT) + tid;
+            if (i < end)
+                __builtin_nontemporal_store(v[u], (__attribute__((address_space(1))) u32x4*)(d.dst + 16ull * i));
+        }
+    }
+
     // A uniform brick grid (what BrickDecompose builds: brick (ix, iy, iz) at index ix + nbx * (iy
     // + nby * iz), box = the grid cell extended by the halo, every brick linear): descriptors are
     // derived from the brick index and three classes per axis (first, interior, last brick), so a
@@ -333,25 +372,12 @@ namespace hipk
         return c == 0 ? a[0] : (c == 1 ? a[1] : a[2]);
     }
 
-    template <int BPV, int kStageWords, bool GRID, int NT = kBlock>
-    __global__ __launch_bounds__(NT) void brickCopyKernel(BrickDesc const* bricks, BrickGrid grid,
-                                                             FastDiv chunksPerBrick, FastDiv groupSize,
-                                                             uint8_t const* src, int32_t sdx, int32_t sdy, int32_t sdz,
-                                                             int32_t alignedLds)
+    // The descriptor of brick b of a uniform grid (class per axis: first, interior, last brick).
+    template <int BPV>
+    __device__ __forceinline__ BrickDesc gridDesc(BrickGrid const& grid, uint32_t b)
     {
         constexpr int32_t V = 16 / BPV;
-        // blockIdx = (group, chunk, brick in group): consecutive workgroups copy the same rows
-        // of neighbouring bricks along x, i.e. adjacent pieces of the same source rows, so the
-        // 128-B lines two bricks share (unaligned brick starts, halos) are fetched from HBM once
-        // and hit the Infinity Cache the second time.
-        uint32_t const lb = xcdSwizzle(blockIdx.x, gridDim.x);
-        uint32_t const rest = fdiv(lb, groupSize);
-        uint32_t const ig = lb - rest * groupSize.d;
-        uint32_t const grp = fdiv(rest, chunksPerBrick);
-        uint32_t const chunk = __builtin_amdgcn_readfirstlane(rest - grp * chunksPerBrick.d);
-        uint32_t const b = __builtin_amdgcn_readfirstlane(grp * groupSize.d + ig);
         BrickDesc d;
-        if constexpr (GRID)
         {
             uint32_t const yz = fdiv(b, grid.fnbx);
             int32_t const ix = static_cast<int32_t>(b - yz * grid.fnbx.d);
@@ -373,16 +399,15 @@ namespace hipk
             d.fwpr = pick3(grid.fwpr, cx);
             d.fdy = pick3(grid.fdy, cy);
         }
-        else
-            d = bricks[b];
-        uint32_t const base = chunk * kBrickChunk;
-        if (base >= d.nitems)
-            return;   // border bricks are smaller than the largest one
-        if (GRID || d.linear)
-        {
-            brickStaged<BPV, kStageWords, NT>(d, base, src, sdx, sdy, sdz, alignedLds);
-            return;
-        }
+        return d;
+    }
+
+    // Row mode (a brick larger than its range): one 16-B segment of a box row per item.
+    template <int BPV, int NT>
+    __device__ __forceinline__ void brickRows(BrickDesc const& d, uint32_t base, uint8_t const* src, int32_t sdx,
+                                              int32_t sdy, int32_t sdz)
+    {
+        constexpr int32_t V = 16 / BPV;
         uint64_t const pitchY = static_cast<uint64_t>(d.dimX);
         uint64_t const pitchZ = pitchY * static_cast<uint64_t>(d.dimY);
         uint64_t const spY = static_cast<uint64_t>(sdx), spZ = spY * static_cast<uint64_t>(sdy);
@@ -431,6 +456,63 @@ namespace hipk
             }
         }
     }
+
+    template <int BPV, int kStageWords, bool GRID, int NT = kBlock, bool DIRECT = false>
+    __global__ __launch_bounds__(NT) void brickCopyKernel(BrickDesc const* bricks, BrickGrid grid,
+                                                             FastDiv chunksPerBrick, FastDiv groupSize,
+                                                             uint8_t const* src, int32_t sdx, int32_t sdy, int32_t sdz,
+                                                             int32_t alignedLds)
+    {
+        // blockIdx = (group, chunk, brick in group): consecutive workgroups copy the same rows
+        // of neighbouring bricks along x, i.e. adjacent pieces of the same source rows, so the
+        // 128-B lines two bricks share (unaligned brick starts, halos) are fetched from HBM once
+        // and hit the Infinity Cache the second time.
+        uint32_t const lb = xcdSwizzle(blockIdx.x, gridDim.x);
+        uint32_t const rest = fdiv(lb, groupSize);
+        uint32_t const ig = lb - rest * groupSize.d;
+        uint32_t const grp = fdiv(rest, chunksPerBrick);
+        uint32_t const chunk = __builtin_amdgcn_readfirstlane(rest - grp * chunksPerBrick.d);
+        uint32_t const b = __builtin_amdgcn_readfirstlane(grp * groupSize.d + ig);
+        BrickDesc d;
+        if constexpr (GRID)
+            d = gridDesc<BPV>(grid, b);
+        else
+            d = bricks[b];
+        uint32_t const base = chunk * kBrickChunk;
+        if (base >= d.nitems)
+            return;   // border bricks are smaller than the largest one
+        if constexpr (DIRECT)
+        {
+            static_assert(kBrickChunk == 4 * NT, "brickDirect: 4 items per thread");
+            brickDirect<BPV, NT>(d, base, src, sdx, sdy, threadIdx.x);
+            return;
+        }
+        if (GRID || d.linear)
+        {
+            brickStaged<BPV, kStageWords, NT>(d, base, src, sdx, sdy, sdz, alignedLds);
+            return;
+        }
+        brickRows<BPV, NT>(d, base, src, sdx, sdy, sdz);
+    }
+
+    // Direct copy of P small bricks per workgroup (every brick one chunk of <= 4 NT / P items):
+    // NT / P threads -- whole waves -- per brick, the P bricks consecutive along x (a 16^3 UInt16
+    // brick is 512 items: one workgroup per brick left half of its loads clamped duplicates).
+    template <int BPV, int P, int KPER = 4, int NT = kBlock>
+    __global__ __launch_bounds__(NT) void brickDirectKernel(BrickGrid grid, uint32_t nBricks, uint8_t const* src,
+                                                            int32_t sdx, int32_t sdy)
+    {
+        constexpr int kTpb = NT / P;
+        static_assert(kTpb % 64 == 0, "whole waves per brick");
+        uint32_t const lb = xcdSwizzle(blockIdx.x, gridDim.x);
+        uint32_t const sub = threadIdx.x / kTpb;
+        uint32_t const b = __builtin_amdgcn_readfirstlane(lb * P + sub);
+        if (b >= nBricks)
+            return;
+        BrickDesc const d = gridDesc<BPV>(grid, b);
+        brickDirect<BPV, kTpb, KPER>(d, 0u, src, sdx, sdy, threadIdx.x - sub * kTpb);
+    }
+
 
     // ---- Persistent, software-pipelined staged copy of a uniform grid (knob decompose.pipe) ----
     // The staged kernel above runs one workgroup per 16-KiB chunk: a small brick (16^3 + halo 1 =
@@ -1265,9 +1347,55 @@ namespace hipk
         uint32_t pairs = 0;
         bool const pair = useGrid && gatherLds == 0 && !pipe && !half && rt::knob(rt::Knob::DecomposePair) != 0 &&
                           pairGeom(grid, bpv, maxItems, source.dimX, pg, pairs);
+        // direct copy (brickDirect): no clamped voxel anywhere in the grid, every box row whole
+        // 16-B words at 16-B aligned source offsets
+        auto directGrid = [&] {
+            if (!useGrid || rt::knob(rt::Knob::DecomposeDirect) == 0 || (source.dimX * bpv) % 16 != 0 ||
+                (static_cast<int64_t>(grid.fx0) * bpv) % 16 != 0 || (static_cast<int64_t>(grid.bx) * bpv) % 16 != 0 ||
+                grid.fx0 < 0 || grid.fy0 < 0 || grid.fz0 < 0)
+                return false;
+            int32_t const sdim[3] = {source.dimX, source.dimY, source.dimZ};
+            int32_t const f0[3] = {grid.fx0, grid.fy0, grid.fz0}, step[3] = {grid.bx, grid.by, grid.bz};
+            int32_t const nb[3] = {grid.nbx, grid.nby, grid.nbz};
+            int32_t const* ext[3] = {grid.nx, grid.ny, grid.nz};
+            for (int a = 0; a < 3; ++a)
+                for (int c = 0; c < 3; ++c)
+                {
+                    // classes in use (gridClass): 0 with >= 2 bricks, 1 with >= 3, 2 always; the
+                    // last brick of class c: brick 0, nb - 2, nb - 1
+                    if ((c == 0 && nb[a] < 2) || (c == 1 && nb[a] < 3))
+                        continue;
+                    int64_t const i = c == 0 ? 0 : (c == 1 ? nb[a] - 2 : nb[a] - 1);
+                    if (f0[a] + i * step[a] + ext[a][c] > sdim[a])
+                        return false;
+                    if (a == 0 && (static_cast<int64_t>(ext[0][c]) * bpv) % 16 != 0)
+                        return false;
+                }
+            return true;
+        };
+        bool const direct = !half && gatherLds == 0 && !pipe && !pair && directGrid();
+        // small bricks: P per workgroup (knob decompose.direct 1; 2 keeps one per workgroup).
+        // Measured and rejected: 4 bricks of <= 512 items per workgroup at 8 items per thread
+        // (16^3 UInt16 0.858 vs 0.862 ms, within the spread)
+        uint32_t const perWg = !direct || chunks != 1 || rt::knob(rt::Knob::DecomposeDirect) != 1
+                                   ? 1u
+                                   : (maxItems <= kBrickChunk / 4 ? 4u : (maxItems <= kBrickChunk / 2 ? 2u : 1u));
         auto launch = [&](auto bpvC, auto swC) {
             constexpr int B = decltype(bpvC)::value, W = decltype(swC)::value;
-            if (pair)
+            if (direct && perWg > 1)
+            {
+                unsigned const gw = static_cast<unsigned>((nFast + perWg - 1) / perWg);
+                if (perWg == 4)
+                    hipLaunchKernelGGL((brickDirectKernel<B, 4>), dim3(gw), dim3(kBlock), 0, s, grid,
+                                       static_cast<uint32_t>(nFast), source.data, source.dimX, source.dimY);
+                else
+                    hipLaunchKernelGGL((brickDirectKernel<B, 2>), dim3(gw), dim3(kBlock), 0, s, grid,
+                                       static_cast<uint32_t>(nFast), source.data, source.dimX, source.dimY);
+            }
+            else if (direct)
+                hipLaunchKernelGGL((brickCopyKernel<B, W, true, kBlock, true>), dim3(g), dim3(kBlock), 0, s, dev, grid,
+                                   fdc, fdg, source.data, source.dimX, source.dimY, source.dimZ, alignedLds);
+            else if (pair)
                 hipLaunchKernelGGL((brickPairKernel<B, W + 2, kBlock>), dim3(pairs), dim3(kBlock), 0, s, grid, pg,
                                    source.data, source.dimX, source.dimY, source.dimZ, alignedLds);
             else if (pipe)

@@ -132,8 +132,9 @@ namespace rt
         PointwiseRowLdsU8,             // the same occupancy cap for the UInt8 row kernel
         PointwiseRowSwizzle,           // > 0: the row kernel gives each XCD runs of this many consecutive quanta
         PointwiseRowsKernel,           // multi-row boxes (32-bit rows, no scalar edges) on the MODE-1 kernel: bit 0 UInt8, bit 1 UInt16
-        TransformShape,
-        HistogramPairTiles,            // histograms of 2..4 tiles side by side in one launch (PAIR): 1 where P16 does not apply, 2 always, 0 never                // device-functor Transform vector kernels: 0 256x4, 1 64x2, 2 64x1 (read via vktHipGetTuningKnob)
+        TransformShape,                // device-functor Transform vector kernels: 0 256x4, 1 64x2, 2 64x1 (read via vktHipGetTuningKnob)
+        DecomposeDirect,               // halo-free aligned brick grids: 1 direct copy (small bricks P per workgroup), 2 one brick per workgroup, 0 LDS-staged
+        HistogramPairTiles,            // histograms of 2..4 tiles side by side in one launch (PAIR): 1 where P16 does not apply, 2 always, 0 never
         Count
     };
     int64_t knob(Knob k);
