@@ -336,6 +336,29 @@ def main():
             for k in (b"pointwise.rows_kernel", b"pointwise.u8_unroll", b"pointwise.u16_unroll"):
                 lib.vktHipSetTuningKnob(k, -1)
             free(A, B, D)
+    if want("rowslds"):
+        # occupancy cap (dynamic LDS per one-wave workgroup, knob pointwise.row_lds_u8) for the
+        # UInt8 row / rows kernels: the x0 = 100 sub-boxes (MODE 1) and the whole volume (MODE 0)
+        m = 1024
+        A, B, D = alloc((m,) * 3, 4, seed=1), alloc((m,) * 3, 4, seed=2), alloc((m,) * 3, 4)
+        f0, f1, last = Vec3i_t(100, 100, 100), Vec3i_t(900, 900, 900), Vec3i_t(m, m, m)
+        nv = 800 ** 3
+        try:
+            for rep in range(2):
+                for lds in (0, 4096, 5120, 5632, 6656, 8192):
+                    lib.vktHipSetTuningKnob(b"pointwise.row_lds_u8", lds)
+                    tag = f"[row_lds_u8={lds}]"
+                    report(f"rowslds CopyRange x0=100 same offset UInt8 {tag}",
+                           timed(lambda: lib.vktHipCopyRange(D, A, f0, f1, f0), R), 2 * nv, nv)
+                    report(f"rowslds SumRange x0=100 UInt8 {tag}",
+                           timed(lambda: lib.vktHipArithmeticRange(0, D, A, B, f0, f1, o), R), 3 * nv, nv)
+                    report(f"rowslds Copy 1024^3 UInt8 {tag}",
+                           timed(lambda: lib.vktHipCopyRange(D, A, o, last, o), R), 2 * m ** 3, m ** 3)
+                    report(f"rowslds SumRange 1024^3 UInt8 {tag}",
+                           timed(lambda: lib.vktHipArithmeticRange(0, D, A, B, o, last, o), R), 3 * m ** 3, m ** 3)
+        finally:
+            lib.vktHipSetTuningKnob(b"pointwise.row_lds_u8", -1)
+            free(A, B, D)
     if want("u8cal"):
         # FETCH_SIZE calibration for the UInt8 access shapes and the
         # whole-volume UInt8 ops against UInt16 (item 4); one launch per case for PMC passes.
