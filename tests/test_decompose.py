@@ -442,28 +442,3 @@ def test_brick_decompose_direct_kernel(fmt, dims, brick, neg, pos, direct):
     assert set(got) == set(ref)
     for idx, v in ref.items():
         np.testing.assert_array_equal(got[idx], v.codes, err_msg=f"brick {idx}")
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("fmt", [4, 5, 7])
-@pytest.mark.parametrize("dims,brick,neg,pos", LAYOUTS + [((70, 40, 33), (16, 16, 16), (1, 1, 1), (1, 1, 1)),
-                                                        ((64, 48, 40), (8, 8, 8), (1, 1, 1), (1, 1, 1)),
-                                                        ((96, 30, 20), (14, 9, 7), (2, 1, 0), (0, 2, 1)),
-                                                        ((200, 20, 10), (30, 10, 10), (1, 0, 0), (1, 0, 0))])
-def test_brick_decompose_rows_kernel(fmt, dims, brick, neg, pos):
-    """Knob decompose.rows = 1: one box row per lane for bricks whose rows are <= 64 B (the
-    aligned source words, one funnel shift by the brick's phase, 16-B pieces + a byte-granular
-    tail at any alignment); bricks with clamped x voxels and other layouts keep the staged /
-    direct kernels -- bit-exact vs the oracle."""
-    rng = np.random.default_rng(fmt * 100 + sum(dims) + 41)
-    codes = rand_codes(rng, fmt, dims[::-1])
-    assert lib.vktHipSetTuningKnob(b"decompose.rows", 1) == 0
-    try:
-        err, got = gpu_decompose(codes, fmt, (0.0, 1.0), brick, neg, pos)
-    finally:
-        assert lib.vktHipSetTuningKnob(b"decompose.rows", -1) == 0
-    assert err == vkt.NoError, vkt.last_error()
-    ref = ob.brick_decompose(ob.Volume(codes, fmt), brick, neg, pos)
-    assert set(got) == set(ref)
-    for idx, v in ref.items():
-        np.testing.assert_array_equal(got[idx], v.codes, err_msg=f"brick {idx}")

@@ -1209,40 +1209,6 @@ def main():
             del V
         ep.device = vkt.ExecutionPolicy.Device_CPU
         vkt.SetThreadExecutionPolicy(ep)
-    if want("decrows"):
-        # in-process A/B of the row copy for small bricks with halos (knob decompose.rows: 1 one
-        # box row per lane, 0 the LDS-staged kernel), alternated, on the same bricks
-        import volkit_amd.volkit as vkt
-        ep = vkt.GetThreadExecutionPolicy()
-        ep.device = vkt.ExecutionPolicy.Device_GPU
-        vkt.SetThreadExecutionPolicy(ep)
-        n = 1024
-        for fmt, b, name in ((vkt.DataFormat_UInt16, 2, "UInt16"), (vkt.DataFormat_UInt8, 1, "UInt8"),
-                             (vkt.DataFormat_Float32, 4, "Float32")):
-            V = vkt.StructuredVolume(n, n, n, fmt)
-            vkt.Synthesize(V, 77)
-            ab = {}
-            for bs in ((16, 8) if b == 2 else (16, 32) if b == 1 else (8,)):
-                arr = vkt.Array3D_StructuredVolume()
-                b3, h3 = vkt.Vec3i(bs, bs, bs), vkt.Vec3i(1, 1, 1)
-                vkt.BrickDecomposeResize(arr, V, b3, h3, h3)
-                vox = (n // bs) ** 3 * (bs + 2) ** 3
-                for rnd in range(3):
-                    for kv in (1, 0):
-                        lib.vktHipSetTuningKnob(b"decompose.rows", kv)
-                        ab.setdefault((bs, kv, vox, "back-to-back"), []).append(
-                            pipelined(lambda: vkt.BrickDecompose(arr, V, b3, h3, h3), R))
-                        ab.setdefault((bs, kv, vox, "incl. host planning"), []).append(
-                            timed(lambda: vkt.BrickDecompose(arr, V, b3, h3, h3), R))
-                del arr
-            lib.vktHipSetTuningKnob(b"decompose.rows", -1)
-            for (bs, kv, vox, how), ts in sorted(ab.items()):
-                ts.sort()
-                report(f"decrows BrickDecompose 1024^3 {name} -> {bs}^3 bricks halo 1 rows={kv} ({how}; median of 3 "
-                       f"rounds, spread {ts[0]:.4f}-{ts[-1]:.4f})", ts[1], 2 * b * vox, vox)
-            del V
-        ep.device = vkt.ExecutionPolicy.Device_CPU
-        vkt.SetThreadExecutionPolicy(ep)
     if want("decdump"):
         # in-process A/B of the staged copy's partial-word writes (knob decompose.aligned_lds:
         # 0 per-voxel branches, 3 branch-free with dump bytes), alternated, on the same bricks

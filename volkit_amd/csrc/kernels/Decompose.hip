@@ -62,14 +62,6 @@ namespace hipk
     {
         u32x4 v;
     };
-    struct __attribute__((packed, aligned(1))) Unaligned4
-    {
-        uint32_t v;
-    };
-    struct __attribute__((packed, aligned(1))) Unaligned2
-    {
-        uint16_t v;
-    };
 
     __device__ __forceinline__ int32_t clampi(int32_t v, int32_t hi)
     {
@@ -521,116 +513,6 @@ namespace hipk
         brickDirect<BPV, kTpb, KPER>(d, 0u, src, sdx, sdy, threadIdx.x - sub * kTpb);
     }
 
-
-    // Row copy of small bricks with halos (knob decompose.rows; the reference's own example shape,
-    // src/examples/Decompose.c: 16^3 bricks + halo 1).  Every box row of a brick whose x range is
-    // inside the volume is ONE contiguous source span, and its byte phase within a 16-B word is
-    // the same for every row of the brick (16-B aligned source and row pitch), so a lane copies a
-    // whole row: the aligned source words covering it, one funnel shift by the brick's phase
-    // (dword selects fixed per kernel instance PD, v_alignbyte by a wave-uniform count), and the
-    // row's bytes stored at r * rowBytes in the brick (16-B pieces + a tail; rows <= 4 ND bytes).  No
-    // LDS tile and no cut words -- the staged kernel's per-voxel writes of the words a row end
-    // cuts cost a wave its exec-mask bookkeeping whenever one lane held one (§4.7).  Bricks with
-    // clamped x voxels (the x borders) take the staged path inside the same kernel.
-    template <int BPV, int ND, int PD, int NT>
-    __device__ __forceinline__ void brickRowsCopy(BrickDesc const& d, uint8_t const* src, int32_t sdx, int32_t sdy,
-                                                  int32_t sdz, uint32_t phase)
-    {
-        constexpr int NWD = ND + PD + 1;                 // source dwords one row needs at most
-        constexpr int NW = (NWD + 3) / 4;                // 16-B source words
-        uint64_t const spY = static_cast<uint64_t>(sdx), spZ = spY * static_cast<uint64_t>(sdy);
-        uint32_t const rowBytes = static_cast<uint32_t>(d.nx) * BPV;
-        uint32_t const nw = (phase + rowBytes + 15u) >> 4;
-        uint32_t const sub = phase & 3u;
-        uint32_t const nRows = fdiv(d.nvox, d.fdx);
-        for (uint32_t r = threadIdx.x; r < nRows; r += NT)
-        {
-            uint32_t const z = fdiv(r, d.fdy);
-            uint32_t const y = r - z * d.fdy.d;
-            uint64_t const rb = static_cast<uint64_t>(clampi(d.fz + static_cast<int32_t>(z), sdz - 1)) * spZ +
-                                static_cast<uint64_t>(clampi(d.fy + static_cast<int32_t>(y), sdy - 1)) * spY;
-            uint8_t const* const w0 = src + (rb + static_cast<uint64_t>(d.fx)) * BPV - phase;
-            uint32_t w[4 * NW + 1];
-#pragma unroll
-            for (int k = 0; k < NW; ++k)
-            {
-                u32x4 v = {0u, 0u, 0u, 0u};
-                if (static_cast<uint32_t>(k) < nw)   // wave-uniform
-                    v = *reinterpret_cast<u32x4 const*>(w0 + 16 * k);
-                w[4 * k] = v.x;
-                w[4 * k + 1] = v.y;
-                w[4 * k + 2] = v.z;
-                w[4 * k + 3] = v.w;
-            }
-            w[4 * NW] = 0u;
-            uint32_t o[ND];
-#pragma unroll
-            for (int i = 0; i < ND; ++i)
-                o[i] = __builtin_amdgcn_alignbyte(w[i + PD + 1], w[i + PD], sub);
-            // whole 16-B pieces, then the row's last rowBytes % 16 bytes as dword / halfword / byte
-            // stores (any alignment: a brick row starts at r * rowBytes)
-            uint8_t* const out = d.dst + static_cast<uint64_t>(r) * rowBytes;
-            uint32_t const nb16 = rowBytes >> 4, t = rowBytes & 15u;
-#pragma unroll
-            for (int c = 0; c < ND / 4; ++c)
-                if (static_cast<uint32_t>(c) < nb16)
-                    reinterpret_cast<Unaligned16*>(out + 16 * c)->v = u32x4{o[4 * c], o[4 * c + 1], o[4 * c + 2], o[4 * c + 3]};
-            auto tailAt = [&](auto c0) {
-                constexpr int C0 = decltype(c0)::value;
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-                {
-                    if (4 * C0 + j < ND)
-                    {
-                        uint32_t const v = o[4 * C0 + j < ND ? 4 * C0 + j : ND - 1];
-                        uint8_t* const q = out + 16 * C0 + 4 * j;
-                        if (4u * j + 4u <= t)
-                            reinterpret_cast<Unaligned4*>(q)->v = v;
-                        else if (4u * j < t)
-                        {
-                            uint32_t const rem = t - 4u * j;
-                            if (rem >= 2u)
-                                reinterpret_cast<Unaligned2*>(q)->v = static_cast<uint16_t>(v);
-                            if (rem & 1u)
-                                q[rem & 2u] = static_cast<uint8_t>(v >> (8u * (rem & 2u)));
-                        }
-                    }
-                }
-            };
-            if (t != 0u)
-            {
-                switch (nb16)
-                {
-                case 0: tailAt(std::integral_constant<int, 0>{}); break;
-                case 1: tailAt(std::integral_constant<int, 1>{}); break;
-                case 2: tailAt(std::integral_constant<int, 2>{}); break;
-                default: tailAt(std::integral_constant<int, 3>{}); break;   // (ND <= 16: rows < 64 B)
-                }
-            }
-        }
-    }
-
-    template <int BPV, int ND, int NT = kBlock>
-    __global__ __launch_bounds__(NT) void brickRowKernel(BrickGrid grid, uint8_t const* src, int32_t sdx, int32_t sdy,
-                                                         int32_t sdz, int32_t alignedLds)
-    {
-        // one chunk per brick: the (group, chunk, brick) order of brickCopyKernel is the identity
-        uint32_t const b = __builtin_amdgcn_readfirstlane(xcdSwizzle(blockIdx.x, gridDim.x));
-        BrickDesc const d = gridDesc<BPV>(grid, b);
-        if (d.fx < 0 || d.fx + d.nx > sdx)
-        {
-            brickStaged<BPV, 6, NT>(d, 0u, src, sdx, sdy, sdz, alignedLds);
-            return;
-        }
-        uint32_t const phase = (static_cast<uint32_t>(d.fx) * BPV) & 15u;
-        switch (phase >> 2)
-        {
-        case 0: brickRowsCopy<BPV, ND, 0, NT>(d, src, sdx, sdy, sdz, phase); break;
-        case 1: brickRowsCopy<BPV, ND, 1, NT>(d, src, sdx, sdy, sdz, phase); break;
-        case 2: brickRowsCopy<BPV, ND, 2, NT>(d, src, sdx, sdy, sdz, phase); break;
-        default: brickRowsCopy<BPV, ND, 3, NT>(d, src, sdx, sdy, sdz, phase); break;
-        }
-    }
 
     // ---- Persistent, software-pipelined staged copy of a uniform grid (knob decompose.pipe) ----
     // The staged kernel above runs one workgroup per 16-KiB chunk: a small brick (16^3 + halo 1 =
@@ -1492,18 +1374,6 @@ namespace hipk
             return true;
         };
         bool const direct = !half && gatherLds == 0 && !pipe && !pair && directGrid();
-        // row copy (brickRowKernel): one chunk per brick, rows of <= 64 B in every x class
-        auto rowsGrid = [&] {
-            if (!useGrid || direct || half || gatherLds != 0 || pipe || pair || chunks != 1 ||
-                rt::knob(rt::Knob::DecomposeRows) == 0 || (source.dimX * bpv) % 16 != 0)
-                return false;
-            for (int c = 0; c < 3; ++c)
-                if (static_cast<int64_t>(grid.nx[c]) * bpv > 64)
-                    return false;
-            return true;
-        };
-        bool const rowsCopy = rowsGrid();
-        bool const rowsNarrow = rowsCopy && static_cast<int64_t>(std::max({grid.nx[0], grid.nx[1], grid.nx[2]})) * bpv <= 48;
         // small bricks: P per workgroup (knob decompose.direct 1; 2 keeps one per workgroup).
         // Measured and rejected: 4 bricks of <= 512 items per workgroup at 8 items per thread
         // (16^3 UInt16 0.858 vs 0.862 ms, within the spread)
@@ -1512,16 +1382,7 @@ namespace hipk
                                    : (maxItems <= kBrickChunk / 4 ? 4u : (maxItems <= kBrickChunk / 2 ? 2u : 1u));
         auto launch = [&](auto bpvC, auto swC) {
             constexpr int B = decltype(bpvC)::value, W = decltype(swC)::value;
-            if (rowsCopy)
-            {
-                if (rowsNarrow)
-                    hipLaunchKernelGGL((brickRowKernel<B, 12>), dim3(g), dim3(kBlock), 0, s, grid, source.data,
-                                       source.dimX, source.dimY, source.dimZ, alignedLds);
-                else
-                    hipLaunchKernelGGL((brickRowKernel<B, 16>), dim3(g), dim3(kBlock), 0, s, grid, source.data,
-                                       source.dimX, source.dimY, source.dimZ, alignedLds);
-            }
-            else if (direct && perWg > 1)
+            if (direct && perWg > 1)
             {
                 unsigned const gw = static_cast<unsigned>((nFast + perWg - 1) / perWg);
                 if (perWg == 4)
