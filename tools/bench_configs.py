@@ -1211,8 +1211,7 @@ def main():
         vkt.SetThreadExecutionPolicy(ep)
     if want("decdump"):
         # in-process A/B of the staged copy's partial-word writes (knob decompose.aligned_lds:
-        # 0 per-voxel branches, 4 the row-end voxels in a loop of their own; 3, branch-free with
-        # dump bytes, measured in profiles/r05/decdump_calls.jsonl), alternated, on the same bricks
+        # 0 per-voxel branches, 3 branch-free with dump bytes), alternated, on the same bricks
         import volkit_amd.volkit as vkt
         ep = vkt.GetThreadExecutionPolicy()
         ep.device = vkt.ExecutionPolicy.Device_GPU
@@ -1226,10 +1225,10 @@ def main():
             vkt.BrickDecomposeResize(arr, V, b3, h3, h3)
             vox = (n // bs) ** 3 * (bs + halo[0] + halo[0]) ** 3
             for rep in range(3):
-                for k in (0, 4):
+                for k in (0, 3):
                     lib.vktHipSetTuningKnob(b"decompose.aligned_lds", k)
-                    report(f"decdump BrickDecompose 1024^3 UInt16 -> {bs}^3 bricks halo {halo} [aligned_lds={k}] "
-                           f"(back-to-back)", pipelined(lambda: vkt.BrickDecompose(arr, V, b3, h3, h3), R), 4 * vox, vox)
+                    report(f"decdump BrickDecompose 1024^3 UInt16 -> {bs}^3 bricks halo {halo} [aligned_lds={k}]",
+                           timed(lambda: vkt.BrickDecompose(arr, V, b3, h3, h3), R), 4 * vox, vox)
             lib.vktHipSetTuningKnob(b"decompose.aligned_lds", -1)
             del arr
         del V
