@@ -177,14 +177,19 @@ def test_brick_decompose_128_thread_workgroups(fmt, dims, brick, neg, pos, grid)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("aligned", [0, 1, 2, 3])
+@pytest.mark.parametrize("aligned", [0, 1, 2, 3, 4, 5])
 @pytest.mark.parametrize("fmt", [4, 5, 7])
-@pytest.mark.parametrize("dims,brick,neg,pos", LAYOUTS[1:4] + LAYOUTS[6:])
+@pytest.mark.parametrize("dims,brick,neg,pos", LAYOUTS[1:4] + LAYOUTS[6:] + [
+    ((96, 40, 33), (16, 16, 16), (1, 1, 1), (1, 1, 1)),     # 16-B row pitch: the edge mode (4) applies
+    ((64, 24, 20), (5, 7, 6), (2, 1, 0), (1, 0, 2)),        # rows shorter than a word: all edge voxels
+    ((128, 12, 10), (40, 6, 5), (3, 1, 1), (0, 1, 1))])
 def test_brick_decompose_aligned_lds_pieces(fmt, dims, brick, neg, pos, aligned):
     """The staged copy's LDS writes of the words cut by a row end or the chunk, per knob
     decompose.aligned_lds: 0 per-voxel loop, 1 naturally aligned pieces (2: every word so), 3 all
     voxels written with the ones outside sent to the tile's unused tail (chunks that leave 16 B
-    free; full chunks keep the loop): the same bricks as the oracle."""
+    free; full chunks keep the loop), 4 the voxels at each row end in a loop of their own (one
+    chunk per brick, 16-B row pitch; otherwise 0), 5 (default) 4 for UInt8 and 0 for the wider
+    formats: the same bricks as the oracle."""
     rng = np.random.default_rng(fmt * 100 + sum(dims) + aligned)
     codes = rand_codes(rng, fmt, dims[::-1])
     assert lib.vktHipSetTuningKnob(b"decompose.aligned_lds", aligned) == 0

@@ -1209,6 +1209,31 @@ def main():
             del V
         ep.device = vkt.ExecutionPolicy.Device_CPU
         vkt.SetThreadExecutionPolicy(ep)
+    if want("decedge"):
+        # in-process A/B of the staged copy's row-end handling for UInt8 / Float32 bricks with halos
+        # (knob decompose.aligned_lds: 0 per-voxel branches, 4 the row-end voxels in a loop of their
+        # own, 3 branch-free with dump bytes), back-to-back calls, alternated
+        import volkit_amd.volkit as vkt
+        ep = vkt.GetThreadExecutionPolicy()
+        ep.device = vkt.ExecutionPolicy.Device_GPU
+        vkt.SetThreadExecutionPolicy(ep)
+        n = 1024
+        for fmt, b, name in ((vkt.DataFormat_UInt8, 1, "UInt8"), (vkt.DataFormat_Float32, 4, "Float32")):
+            V = vkt.StructuredVolume(n, n, n, fmt)
+            vkt.Synthesize(V, 77)
+            arr = vkt.Array3D_StructuredVolume()
+            b3, h3 = vkt.Vec3i(16, 16, 16), vkt.Vec3i(1, 1, 1)
+            vkt.BrickDecomposeResize(arr, V, b3, h3, h3)
+            vox = (n // 16) ** 3 * 18 ** 3
+            for rep in range(3):
+                for k in (0, 4, 3):
+                    lib.vktHipSetTuningKnob(b"decompose.aligned_lds", k)
+                    report(f"decedge BrickDecompose 1024^3 {name} -> 16^3 bricks halo 1 [aligned_lds={k}] (back-to-back)",
+                           pipelined(lambda: vkt.BrickDecompose(arr, V, b3, h3, h3), R), 2 * b * vox, vox)
+            lib.vktHipSetTuningKnob(b"decompose.aligned_lds", -1)
+            del arr, V
+        ep.device = vkt.ExecutionPolicy.Device_CPU
+        vkt.SetThreadExecutionPolicy(ep)
     if want("decdump"):
         # in-process A/B of the staged copy's partial-word writes (knob decompose.aligned_lds:
         # 0 per-voxel branches, 3 branch-free with dump bytes), alternated, on the same bricks

@@ -180,6 +180,11 @@ namespace hipk
                    static_cast<uint64_t>(clampi(d.fy + static_cast<int32_t>(y), sdy - 1)) * spY;
         };
         uint32_t const total = static_cast<uint32_t>(nRows) * wpr;
+        // alignedLds 4 (edge mode; host: one chunk per brick, 16-B row pitch): the words a row end
+        // cuts are not placed word by word -- the <= V - 1 voxels at each end of a row's span are
+        // copied voxel by voxel in a loop of their own, the same count for every row of the brick,
+        // so no wave runs the per-voxel branches of a cut word
+        bool const edges = alignedLds == 4;
         // one aligned source word: where it comes from and where it lands in LDS
         struct Word
         {
@@ -200,7 +205,9 @@ namespace hipk
             w.li = r * d.nx + (w.x0 - d.fx) - vStart;              // its LDS voxel index
             w.whole = startByte + 16 <= srcBytes;
             w.v = u32x4{0u, 0u, 0u, 0u};
-            if (w.live && w.whole)
+            // (edge mode: only the words inside the row span are loaded and placed)
+            bool const need = !edges || (w.x0 >= lo && w.x0 + V <= hi);
+            if (w.live && w.whole && need)
                 w.v = *reinterpret_cast<u32x4 const*>(src + startByte);
         };
         // (knob decompose.aligned_lds 3) the tile's bytes past the chunk's voxels, when 16 of
@@ -217,6 +224,8 @@ namespace hipk
                 else
                     reinterpret_cast<Unaligned16*>(lds + w.li * BPV)->v = w.v;
             }
+            else if (edges)
+                return;   // its voxels come from the edge loop
             else if (w.whole && dumpable)
             {
                 // a word cut by a row end or the chunk: all V voxels written, the ones outside to
@@ -263,6 +272,42 @@ namespace hipk
             Word w;
             locate(t, w);
             place(w);
+        }
+        if (edges && hi > lo)
+        {
+            // per row: h head voxels [lo, lo + h) before the first whole word and t tail voxels
+            // [hi - t, hi) after the last (the row phase is the same for every row)
+            int32_t const ph = (lo * BPV) & 15;
+            int32_t const headB = (16 - ph) & 15, spanB = (hi - lo) * BPV;
+            int32_t const h = spanB <= headB ? hi - lo : headB / BPV;
+            int32_t const t = spanB <= headB ? 0 : ((spanB - headB) & 15) / BPV;
+            int32_t const e = h + t;
+            if (e > 0)
+            {
+                FastDiv const fe = makeFastDiv(static_cast<uint32_t>(e));
+                uint32_t const n = static_cast<uint32_t>(nRows) * static_cast<uint32_t>(e);
+                for (uint32_t q0 = 0; q0 < n; q0 += 4u * NT)
+                {
+                    uint32_t code[4];
+                    int32_t at[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                    {
+                        uint32_t const q = q0 + static_cast<uint32_t>(u * NT) + threadIdx.x;
+                        uint32_t const qq = q < n ? q : 0u;
+                        uint32_t const rq = fdiv(qq, fe);
+                        int32_t const k = static_cast<int32_t>(qq - rq * fe.d);
+                        int32_t const x = k < h ? lo + k : hi - t + (k - h);
+                        int32_t const r = rA + static_cast<int32_t>(rq);
+                        at[u] = q < n ? r * d.nx + (x - d.fx) - vStart : -1;
+                        code[u] = loadCode<BPV>(src, rowBase(r) + static_cast<uint64_t>(x));
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                        if (at[u] >= 0 && at[u] < chunkVox)
+                            ldsStoreCode<BPV>(lds, at[u], code[u]);
+                }
+            }
         }
         if (d.fx < 0 || d.fx + d.nx > sdx)   // clamped halo voxels (border bricks only)
         {
@@ -1330,7 +1375,17 @@ namespace hipk
         FastDiv const fdc = makeFastDiv(static_cast<uint32_t>(chunks));
         FastDiv const fdg = makeFastDiv(static_cast<uint32_t>(nFast % run == 0 ? run : 1));
         unsigned const g = static_cast<unsigned>(blocks);
-        int32_t const alignedLds = static_cast<int32_t>(rt::knob(rt::Knob::DecomposeAlignedLds));
+        // (knob value 4, the edge mode of brickStaged, needs one chunk per brick and a 16-B row
+        // pitch; elsewhere it runs as 0)
+        // 5 (default): the edge mode for UInt8 -- a cut word is up to 15 voxels of per-voxel
+        // branches there (16^3 + halo 1 back-to-back 1.38-1.50 -> 1.30 ms), the per-voxel loop for
+        // the wider formats (UInt16 16^3 + halo 1.52-1.68 -> 1.82 ms in the edge mode;
+        // profiles/r05/decedge.jsonl, decedge_u8.jsonl)
+        int32_t alignedLds = static_cast<int32_t>(rt::knob(rt::Knob::DecomposeAlignedLds));
+        if (alignedLds == 5)
+            alignedLds = bpv == 1 ? 4 : 0;
+        if (alignedLds == 4 && (chunks != 1 || (static_cast<int64_t>(source.dimX) * bpv) % 16 != 0))
+            alignedLds = 0;
         // words staged per thread: enough that a chunk's source words are all in flight at once
         // (one memory latency per workgroup): a 16-KiB chunk of 32^3 bricks + halo 1 (68-B rows)
         // reads ~1450 aligned words = 5.7 per thread.  In-process A/B (profiles/r03/decompose_ab.jsonl,

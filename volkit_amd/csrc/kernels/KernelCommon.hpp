@@ -39,7 +39,7 @@ namespace hipk
         uint32_t d, m, l;
     };
 
-    inline FastDiv makeFastDiv(uint32_t d)
+    __host__ __device__ inline FastDiv makeFastDiv(uint32_t d)
     {
         FastDiv f{d, 0u, 0u};
         if (d == 0)

@@ -226,7 +226,7 @@ namespace rt
             {"histogram.p16_step", 1},
             {"pointwise.u8_pairs", 1},
             {"render.bricks", 1},
-            {"decompose.aligned_lds", 0},
+            {"decompose.aligned_lds", 5},
             {"decompose.stage_words", 6},
             {"pointwise.u8_wide", 1},
             {"pointwise.f32_halves", 1},

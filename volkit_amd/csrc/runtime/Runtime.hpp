@@ -104,7 +104,7 @@ namespace rt
         HistogramP16Step,              // 0: P16 threshold tests after each item, not each wave-step
         PointwiseU8Pairs,              // 0: UInt8 multi-row boxes keep the 8-voxel per-item loop
         RenderBricks,                  // 0: multi-scattering samples the dense volume, not an 8^3-brick copy
-        DecomposeAlignedLds,           // 1: partial words as aligned LDS pieces; 2: every word; 3: partial words branch-free (dump bytes)
+        DecomposeAlignedLds,           // cut words: 0 per-voxel, 1 aligned LDS pieces, 2 every word so, 3 branch-free (dump bytes), 4 row-end voxel loop, 5 (default) 4 for UInt8 else 0
         DecomposeStageWords,           // source words per thread in flight in the staged copy (5, 6, 8)
         PointwiseU8Wide,               // 0: UInt8 general-path boxes keep 8-voxel items
         PointwiseF32Halves,            // 0: padded 4-byte rows keep the per-item loop
