@@ -1210,7 +1210,7 @@ def main():
         ep.device = vkt.ExecutionPolicy.Device_CPU
         vkt.SetThreadExecutionPolicy(ep)
     if want("decedge"):
-        # in-process A/B of the staged copy's row-end handling for UInt8 / Float32 bricks with halos
+        # in-process A/B of the staged copy's row-end handling for UInt8 / UInt16 bricks with halos
         # (knob decompose.aligned_lds: 0 per-voxel branches, 4 the row-end voxels in a loop of their
         # own, 3 branch-free with dump bytes), back-to-back calls, alternated
         import volkit_amd.volkit as vkt
@@ -1218,7 +1218,7 @@ def main():
         ep.device = vkt.ExecutionPolicy.Device_GPU
         vkt.SetThreadExecutionPolicy(ep)
         n = 1024
-        for fmt, b, name in ((vkt.DataFormat_UInt8, 1, "UInt8"), (vkt.DataFormat_Float32, 4, "Float32")):
+        for fmt, b, name in ((vkt.DataFormat_UInt8, 1, "UInt8"), (vkt.DataFormat_UInt16, 2, "UInt16")):
             V = vkt.StructuredVolume(n, n, n, fmt)
             vkt.Synthesize(V, 77)
             arr = vkt.Array3D_StructuredVolume()

@@ -264,6 +264,49 @@ namespace hipk
 #pragma unroll
         for (int k = 0; k < kStageWords; ++k)
             locate(threadIdx.x + k * NT, words[k]);
+        // edge mode: per row, h head voxels [lo, lo + h) before the first whole word and t tail
+        // voxels [hi - t, hi) after the last (the row phase is the same for every row); their
+        // first round of loads goes out right behind the word loads, so the two round trips
+        // overlap
+        int32_t eh = 0, et = 0;
+        uint32_t en = 0;
+        FastDiv fe{1u, 0u, 0u};
+        if (edges && hi > lo)
+        {
+            int32_t const ph = (lo * BPV) & 15;
+            int32_t const headB = (16 - ph) & 15, spanB = (hi - lo) * BPV;
+            eh = spanB <= headB ? hi - lo : headB / BPV;
+            et = spanB <= headB ? 0 : ((spanB - headB) & 15) / BPV;
+            if (eh + et > 0)
+            {
+                fe = makeFastDiv(static_cast<uint32_t>(eh + et));
+                en = static_cast<uint32_t>(nRows) * static_cast<uint32_t>(eh + et);
+            }
+        }
+        auto edgeIssue = [&](uint32_t q0, uint32_t (&code)[4], int32_t (&at)[4]) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+            {
+                uint32_t const q = q0 + static_cast<uint32_t>(u * NT) + threadIdx.x;
+                uint32_t const qq = q < en ? q : 0u;
+                uint32_t const rq = fdiv(qq, fe);
+                int32_t const k = static_cast<int32_t>(qq - rq * fe.d);
+                int32_t const x = k < eh ? lo + k : hi - et + (k - eh);
+                int32_t const r = rA + static_cast<int32_t>(rq);
+                at[u] = q < en ? r * d.nx + (x - d.fx) - vStart : -1;
+                code[u] = q < en ? loadCode<BPV>(src, rowBase(r) + static_cast<uint64_t>(x)) : 0u;
+            }
+        };
+        auto edgeWrite = [&](uint32_t const (&code)[4], int32_t const (&at)[4]) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (at[u] >= 0 && at[u] < chunkVox)
+                    ldsStoreCode<BPV>(lds, at[u], code[u]);
+        };
+        uint32_t ecode[4] = {0u, 0u, 0u, 0u};
+        int32_t eat[4] = {-1, -1, -1, -1};
+        if (en > 0)
+            edgeIssue(0u, ecode, eat);
 #pragma unroll
         for (int k = 0; k < kStageWords; ++k)
             place(words[k]);
@@ -273,40 +316,13 @@ namespace hipk
             locate(t, w);
             place(w);
         }
-        if (edges && hi > lo)
+        if (en > 0)
         {
-            // per row: h head voxels [lo, lo + h) before the first whole word and t tail voxels
-            // [hi - t, hi) after the last (the row phase is the same for every row)
-            int32_t const ph = (lo * BPV) & 15;
-            int32_t const headB = (16 - ph) & 15, spanB = (hi - lo) * BPV;
-            int32_t const h = spanB <= headB ? hi - lo : headB / BPV;
-            int32_t const t = spanB <= headB ? 0 : ((spanB - headB) & 15) / BPV;
-            int32_t const e = h + t;
-            if (e > 0)
+            edgeWrite(ecode, eat);
+            for (uint32_t q0 = 4u * NT; q0 < en; q0 += 4u * NT)
             {
-                FastDiv const fe = makeFastDiv(static_cast<uint32_t>(e));
-                uint32_t const n = static_cast<uint32_t>(nRows) * static_cast<uint32_t>(e);
-                for (uint32_t q0 = 0; q0 < n; q0 += 4u * NT)
-                {
-                    uint32_t code[4];
-                    int32_t at[4];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u)
-                    {
-                        uint32_t const q = q0 + static_cast<uint32_t>(u * NT) + threadIdx.x;
-                        uint32_t const qq = q < n ? q : 0u;
-                        uint32_t const rq = fdiv(qq, fe);
-                        int32_t const k = static_cast<int32_t>(qq - rq * fe.d);
-                        int32_t const x = k < h ? lo + k : hi - t + (k - h);
-                        int32_t const r = rA + static_cast<int32_t>(rq);
-                        at[u] = q < n ? r * d.nx + (x - d.fx) - vStart : -1;
-                        code[u] = loadCode<BPV>(src, rowBase(r) + static_cast<uint64_t>(x));
-                    }
-#pragma unroll
-                    for (int u = 0; u < 4; ++u)
-                        if (at[u] >= 0 && at[u] < chunkVox)
-                            ldsStoreCode<BPV>(lds, at[u], code[u]);
-                }
+                edgeIssue(q0, ecode, eat);
+                edgeWrite(ecode, eat);
             }
         }
         if (d.fx < 0 || d.fx + d.nx > sdx)   // clamped halo voxels (border bricks only)
