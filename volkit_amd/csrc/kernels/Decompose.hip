@@ -156,7 +156,7 @@ namespace hipk
     // reads, one aligned 16-byte global store per item.  The byte shifting is done by LDS
     // addressing instead of VALU funnel shifts (a 128-bit shift per lane made the kernel VALU
     // bound: 256^3 bricks + halo 1 took 1.15 ms vs 0.75 ms without halo; staged: 0.83 ms).
-    template <int BPV, int kStageWords, int NT>
+    template <int BPV, int kStageWords, int NT, bool EDGE = false>
     __device__ __forceinline__ void brickStaged(BrickDesc const& d, uint32_t base, uint8_t const* src, int32_t sdx,
                                                 int32_t sdy, int32_t sdz, int32_t alignedLds)
     {
@@ -184,7 +184,9 @@ namespace hipk
         // cuts are not placed word by word -- the <= V - 1 voxels at each end of a row's span are
         // copied voxel by voxel in a loop of their own, the same count for every row of the brick,
         // so no wave runs the per-voxel branches of a cut word
-        bool const edges = alignedLds == 4;
+        // (a template parameter: the edge code in every instance cost the others 15 VGPRs --
+        // brickCopyKernel<2, 6> 66 -> 81, 7 -> 5 waves per SIMD)
+        constexpr bool edges = EDGE;
         // one aligned source word: where it comes from and where it lands in LDS
         struct Word
         {
@@ -518,7 +520,7 @@ namespace hipk
         }
     }
 
-    template <int BPV, int kStageWords, bool GRID, int NT = kBlock, bool DIRECT = false>
+    template <int BPV, int kStageWords, bool GRID, int NT = kBlock, bool DIRECT = false, bool EDGE = false>
     __global__ __launch_bounds__(NT) void brickCopyKernel(BrickDesc const* bricks, BrickGrid grid,
                                                              FastDiv chunksPerBrick, FastDiv groupSize,
                                                              uint8_t const* src, int32_t sdx, int32_t sdy, int32_t sdz,
@@ -550,7 +552,7 @@ namespace hipk
         }
         if (GRID || d.linear)
         {
-            brickStaged<BPV, kStageWords, NT>(d, base, src, sdx, sdy, sdz, alignedLds);
+            brickStaged<BPV, kStageWords, NT, EDGE>(d, base, src, sdx, sdy, sdz, alignedLds);
             return;
         }
         brickRows<BPV, NT>(d, base, src, sdx, sdy, sdz);
@@ -1501,9 +1503,15 @@ namespace hipk
                     hipLaunchKernelGGL((brickCopyKernel<B, 2 * W, false, 128>), dim3(g), dim3(128), 0, s, dev, grid, fdc,
                                        fdg, source.data, source.dimX, source.dimY, source.dimZ, alignedLds);
             }
+            else if (useGrid && alignedLds == 4)
+                hipLaunchKernelGGL((brickCopyKernel<B, W, true, kBlock, false, true>), dim3(g), dim3(kBlock), 0, s, dev,
+                                   grid, fdc, fdg, source.data, source.dimX, source.dimY, source.dimZ, alignedLds);
             else if (useGrid)
                 hipLaunchKernelGGL((brickCopyKernel<B, W, true>), dim3(g), dim3(kBlock), 0, s, dev, grid, fdc, fdg,
                                    source.data, source.dimX, source.dimY, source.dimZ, alignedLds);
+            else if (alignedLds == 4)
+                hipLaunchKernelGGL((brickCopyKernel<B, W, false, kBlock, false, true>), dim3(g), dim3(kBlock), 0, s, dev,
+                                   grid, fdc, fdg, source.data, source.dimX, source.dimY, source.dimZ, alignedLds);
             else
                 hipLaunchKernelGGL((brickCopyKernel<B, W, false>), dim3(g), dim3(kBlock), 0, s, dev, grid, fdc, fdg,
                                    source.data, source.dimX, source.dimY, source.dimZ, alignedLds);
