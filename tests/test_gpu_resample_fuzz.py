@@ -56,24 +56,3 @@ def test_resample_random_geometry(g, o, seed):
             out = g.resample(df, dmap, dd, sf, smap, src, fm)
             ref = o.resample(df, dmap, dd, sf, smap, src, fm)
             assert_codes_equal(out, ref, df, f"fuzz{seed}.{case} {sd}->{dd} {sf}->{df} {smap}->{dmap} fm={fm}")
-
-
-@pytest.mark.parametrize("xreg", [1, 0])
-@pytest.mark.parametrize("sd,dd,sf,df", [((48, 20, 10), (64, 27, 13), 5, 5), ((64, 30, 20), (48, 17, 9), 4, 4),
-                                         ((32, 16, 8), (48, 20, 12), 7, 7), ((96, 11, 7), (128, 5, 9), 5, 4),
-                                         ((160, 9, 6), (96, 14, 6), 4, 5)])
-def test_resample_gather_xtab_regs(g, o, sd, dd, sf, df, xreg):
-    """Knob resample.xtab_regs: the LDS-staged gather with the x table loaded per lane from the
-    device table (1) or staged in LDS (0) -- non-integer ratios with 16-B rows, vs the oracle."""
-    from volkit_amd._lib import lib
-    rng = np.random.default_rng(sum(sd) + 7 * sum(dd) + sf + df)
-    src = rand_codes(rng, sf, sd[::-1], floats="mixed")
-    assert lib.vktHipSetTuningKnob(b"resample.xtab_regs", xreg) == 0
-    try:
-        for fm in (0, 1):
-            for dmap in ((0.0, 1.0), (-1.0, 3.0)):
-                out = g.resample(df, dmap, dd, sf, (0.0, 1.0), src, fm)
-                ref = o.resample(df, dmap, dd, sf, (0.0, 1.0), src, fm)
-                assert_codes_equal(out, ref, df, f"xreg={xreg} {sd}->{dd} {sf}->{df} {dmap} fm={fm}")
-    finally:
-        lib.vktHipSetTuningKnob(b"resample.xtab_regs", -1)

@@ -193,25 +193,20 @@ namespace hipk
     // DETECT (Float32 "Linear", optimistic): every staged source row is also checked for values
     // that can make the lerp chain differ from v000 (chainSensitive); such a row's flag is set
     // in a.rowDirtyOut and resampleGatherFixupKernel later re-evaluates the affected tasks.
-    // XREG (knob resample.xtab_regs): the x table is not staged in LDS -- each lane loads its own
-    // entries from the (L1/L2-resident) device table, no workgroup barrier before the first task.
-    template <int BPVS, int BPVD, bool CONV, bool CHAIN, bool DETECT = false, bool XREG = false>
+    template <int BPVS, int BPVD, bool CONV, bool CHAIN, bool DETECT = false>
     __global__ __launch_bounds__(kBlock) void resampleGatherLdsKernel(ResampleArgs a, uint32_t slotBytes)
     {
         constexpr int V = 16 / BPVD;
         extern __shared__ u32x4 ldsRaw[];
         uint8_t* const lds = reinterpret_cast<uint8_t*>(ldsRaw);
         int32_t* const xt = reinterpret_cast<int32_t*>(lds);                  // ddx entries (padded)
-        uint32_t const xtBytes = XREG ? 0u : (static_cast<uint32_t>(a.ddx) * 4u + 15u) & ~15u;
+        uint32_t const xtBytes = (static_cast<uint32_t>(a.ddx) * 4u + 15u) & ~15u;
         int const lane = threadIdx.x & 63;
         uint32_t const wib = threadIdx.x >> 6;
         uint8_t* const slot = lds + xtBytes + wib * slotBytes;
-        if constexpr (!XREG)
-        {
-            for (uint32_t i = threadIdx.x * 4; i < static_cast<uint32_t>(a.ddx); i += kBlock * 4)
-                *reinterpret_cast<u32x4*>(xt + i) = *reinterpret_cast<u32x4 const*>(a.xtab + i);
-            __syncthreads();
-        }
+        for (uint32_t i = threadIdx.x * 4; i < static_cast<uint32_t>(a.ddx); i += kBlock * 4)
+            *reinterpret_cast<u32x4*>(xt + i) = *reinterpret_cast<u32x4 const*>(a.xtab + i);
+        __syncthreads();
 
         uint32_t const wavesPerBlock = blockDim.x >> 6;
         uint32_t const wave = __builtin_amdgcn_readfirstlane(xcdSwizzle(blockIdx.x, gridDim.x) * wavesPerBlock + wib);
@@ -266,8 +261,7 @@ namespace hipk
 #pragma unroll
                 for (int i = 0; i < V; i += 4)
                 {
-                    u32x4 const q = XREG ? *reinterpret_cast<u32x4 const*>(a.xtab + dx + i)
-                                         : *reinterpret_cast<u32x4 const*>(xt + dx + i);
+                    u32x4 const q = *reinterpret_cast<u32x4 const*>(xt + dx + i);
                     int32_t const xs[4] = {static_cast<int32_t>(q.x), static_cast<int32_t>(q.y),
                                            static_cast<int32_t>(q.z), static_cast<int32_t>(q.w)};
 #pragma unroll
@@ -762,9 +756,8 @@ namespace hipk
             return false;
         uint64_t const rowBytes = static_cast<uint64_t>(b.sdx) * bs;
         uint64_t const xtBytes = (static_cast<uint64_t>(b.ddx) * 4 + 15) & ~uint64_t(15);
-        bool const xreg = rt::knob(rt::Knob::ResampleXtabRegs) != 0 && !detect && !chain;
-        uint64_t const lds = (xreg ? 0 : xtBytes) + (kBlock / 64) * rowBytes;
-        if (rowBytes % 16 != 0 || reinterpret_cast<uintptr_t>(b.src) % 16 != 0 || xtBytes + (kBlock / 64) * rowBytes > 65536)
+        uint64_t const lds = xtBytes + (kBlock / 64) * rowBytes;
+        if (rowBytes % 16 != 0 || reinterpret_cast<uintptr_t>(b.src) % 16 != 0 || lds > 65536)
             return false;
         // one task per wave; for 1-byte destinations a task writes so little (one 1-KiB store
         // per dst row) that staging the x table per workgroup dominates: there the grid is
@@ -775,14 +768,7 @@ namespace hipk
             blocks = 16384;
         unsigned const g = static_cast<unsigned>(blocks < (1u << 30) ? blocks : (1u << 30));
         uint32_t const slot = static_cast<uint32_t>(rowBytes);
-#define VKT_GL(S, D, C, H)                                                                                         \
-    do {                                                                                                           \
-        if (xreg && !(H))                                                                                          \
-            hipLaunchKernelGGL((resampleGatherLdsKernel<S, D, C, H, false, true>), dim3(g), dim3(kBlock), lds, s, b, \
-                               slot);                                                                              \
-        else                                                                                                       \
-            hipLaunchKernelGGL((resampleGatherLdsKernel<S, D, C, H>), dim3(g), dim3(kBlock), lds, s, b, slot);     \
-    } while (0)
+#define VKT_GL(S, D, C, H) hipLaunchKernelGGL((resampleGatherLdsKernel<S, D, C, H>), dim3(g), dim3(kBlock), lds, s, b, slot)
 #define VKT_GL_D(S, C, H) do { if (bd == 1) VKT_GL(S, 1, C, H); else if (bd == 2) VKT_GL(S, 2, C, H); else VKT_GL(S, 4, C, H); } while (0)
 #define VKT_GLX(D, C) hipLaunchKernelGGL((resampleGatherLdsKernel<4, D, C, false, true>), dim3(g), dim3(kBlock), lds, s, b, slot)
         if (detect)

@@ -134,7 +134,6 @@ namespace rt
         PointwiseRowsKernel,           // multi-row boxes (32-bit rows, no scalar edges) on the MODE-1 kernel: bit 0 UInt8, bit 1 UInt16
         TransformShape,                // device-functor Transform vector kernels: 0 256x4, 1 64x2, 2 64x1 (read via vktHipGetTuningKnob)
         DecomposeDirect,               // halo-free aligned brick grids: 1 direct copy (small bricks P per workgroup), 2 one brick per workgroup, 0 LDS-staged
-        ResampleXtabRegs,              // 1: the LDS gather loads the x table per lane from global memory (no LDS copy, no barrier)
         HistogramPairTiles,            // histograms of 2..4 tiles side by side in one launch (PAIR): 1 where P16 does not apply, 2 always, 0 never
         Count
     };
