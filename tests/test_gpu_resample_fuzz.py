@@ -56,3 +56,23 @@ def test_resample_random_geometry(g, o, seed):
             out = g.resample(df, dmap, dd, sf, smap, src, fm)
             ref = o.resample(df, dmap, dd, sf, smap, src, fm)
             assert_codes_equal(out, ref, df, f"fuzz{seed}.{case} {sd}->{dd} {sf}->{df} {smap}->{dmap} fm={fm}")
+
+
+@pytest.mark.parametrize("prefetch", [2, 1, 0])
+def test_resample_gather_prefetch_multi_task_waves(g, o, prefetch):
+    """Knob resample.prefetch: UInt8 destinations cap the LDS gather's grid, so with more source
+    rows than waves (260 x 260 rows here, 65 536 waves) a wave runs several tasks and loads the
+    next task's row while it gathers the current one (knob 2; the default 1 prefetches for 2-byte
+    destinations only) -- UInt8 and UInt8 -> UInt16 vs the oracle, every knob value."""
+    from volkit_amd._lib import lib
+    rng = np.random.default_rng(77)
+    src = rand_codes(rng, 4, (260, 260, 32))
+    assert lib.vktHipSetTuningKnob(b"resample.prefetch", prefetch) == 0
+    try:
+        for fm in (0, 1):
+            for df in (4, 5):
+                out = g.resample(df, (0.0, 1.0), (48, 300, 300), 4, (0.0, 1.0), src, fm)
+                ref = o.resample(df, (0.0, 1.0), (48, 300, 300), 4, (0.0, 1.0), src, fm)
+                assert_codes_equal(out, ref, df, f"prefetch={prefetch} df={df} fm={fm}")
+    finally:
+        lib.vktHipSetTuningKnob(b"resample.prefetch", -1)

@@ -713,6 +713,23 @@ def main():
             report(f"gather Resample {se}^3->{de}^3 fmt{fmt} {'Linear' if fm else 'Nearest'}", ms,
                    resample_bytes((se,) * 3, (de,) * 3, b, b, every_row=fmt == 7 and fm == 1), de ** 3)
             free(S, Rv)
+    if want("gatherp"):
+        # in-process A/B of the LDS gather's next-row prefetch (knob resample.prefetch), alternated
+        cases = [(768, 1024, 4, 1), (1000, 1024, 4, 1), (1024, 768, 4, 1), (768, 1024, 5, 1), (1024, 768, 5, 1)]
+        try:
+            for se, de, fmt, fm in cases:
+                b = {4: 1, 5: 2, 7: 4}[fmt]
+                S = alloc((se,) * 3, fmt, seed=21)
+                Rv = alloc((de,) * 3, fmt)
+                for rep in range(2):
+                    for k in (0, 2):
+                        lib.vktHipSetTuningKnob(b"resample.prefetch", k)
+                        ms = timed(lambda: lib.vktHipResample(Rv, S, fm), max(3, R // 2))
+                        report(f"gatherp Resample {se}^3->{de}^3 fmt{fmt} {'Linear' if fm else 'Nearest'} "
+                               f"[prefetch={k}]", ms, resample_bytes((se,) * 3, (de,) * 3, b, b), de ** 3)
+                free(S, Rv)
+        finally:
+            lib.vktHipSetTuningKnob(b"resample.prefetch", -1)
     if want("gpmc"):
         # one launch per case for FETCH / WRITE passes: the downsampling gathers whose bytes the
         # table image decides (UInt16: staged rows only; Float32 Linear: every source row)

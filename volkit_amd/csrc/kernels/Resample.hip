@@ -193,9 +193,13 @@ namespace hipk
     // DETECT (Float32 "Linear", optimistic): every staged source row is also checked for values
     // that can make the lerp chain differ from v000 (chainSensitive); such a row's flag is set
     // in a.rowDirtyOut and resampleGatherFixupKernel later re-evaluates the affected tasks.
-    template <int BPVS, int BPVD, bool CONV, bool CHAIN, bool DETECT = false>
+    // PREFETCH (knob resample.prefetch; rows <= 4 KiB, no chain / detect): a wave that loops over
+    // tasks (the capped UInt8 grid) loads the NEXT task's source row into registers while it
+    // gathers and stores the current one, instead of one load -> wait -> gather round trip per task.
+    template <int BPVS, int BPVD, bool CONV, bool CHAIN, bool DETECT = false, bool PREFETCH = false>
     __global__ __launch_bounds__(kBlock) void resampleGatherLdsKernel(ResampleArgs a, uint32_t slotBytes)
     {
+        constexpr bool kPre = PREFETCH && !CHAIN && !DETECT;   // plain gathers only
         constexpr int V = 16 / BPVD;
         extern __shared__ u32x4 ldsRaw[];
         uint8_t* const lds = reinterpret_cast<uint8_t*>(ldsRaw);
@@ -213,11 +217,37 @@ namespace hipk
         uint32_t const totalWaves = gridDim.x * wavesPerBlock;
         uint32_t const tasks = static_cast<uint32_t>(a.nRunsY) * static_cast<uint32_t>(a.nRunsZ);
         uint32_t const rowBytes = static_cast<uint32_t>(a.sdx) * BPVS;
+        constexpr int kStage = 4;
+        u32x4 pre[kStage];   // PREFETCH: the next task's row (lane l holds bytes 16 l + 1024 j)
+        auto loadRow = [&](uint32_t tt) {
+            Run const ny = runY(a, tt % static_cast<uint32_t>(a.nRunsY));
+            Run const nz = runZ(a, tt / static_cast<uint32_t>(a.nRunsY));
+            uint8_t const* const np = a.src + srcRowIndex(a, ny.s, nz.s) * BPVS;
+#pragma unroll
+            for (int j = 0; j < kStage; ++j)
+                if (16u * lane + 1024u * j < rowBytes)
+                    pre[j] = __builtin_nontemporal_load(reinterpret_cast<u32x4 const*>(np + 16u * lane + 1024u * j));
+        };
+        if constexpr (kPre)
+        {
+            if (wave < tasks)
+                loadRow(wave);
+        }
         for (uint32_t t = wave; t < tasks; t += totalWaves)
         {
             Run const ry = runY(a, t % static_cast<uint32_t>(a.nRunsY));
             Run const rz = runZ(a, t / static_cast<uint32_t>(a.nRunsY));
             uint64_t const srow = srcRowIndex(a, ry.s, rz.s);
+            if constexpr (kPre)
+            {
+                // this task's row is in registers: to the slot, then the next row goes out
+#pragma unroll
+                for (int j = 0; j < kStage; ++j)
+                    if (16u * lane + 1024u * j < rowBytes)
+                        *reinterpret_cast<u32x4*>(slot + 16u * lane + 1024u * j) = pre[j];
+                if (t + totalWaves < tasks)
+                    loadRow(t + totalWaves);
+            }
             if constexpr (CHAIN)
             {
                 if (a.rowChain[srow / static_cast<uint64_t>(a.sdx)])   // wave-uniform
@@ -228,8 +258,7 @@ namespace hipk
             }
             uint8_t const* sp = a.src + srow * BPVS;
             // stage: all of a lane's loads in flight before the first LDS write
-            constexpr int kStage = 4;
-            for (uint32_t o0 = 16u * lane; o0 < rowBytes; o0 += 1024u * kStage)
+            for (uint32_t o0 = 16u * lane; !kPre && o0 < rowBytes; o0 += 1024u * kStage)
             {
                 u32x4 w[kStage];
 #pragma unroll
@@ -759,6 +788,12 @@ namespace hipk
         uint64_t const lds = xtBytes + (kBlock / 64) * rowBytes;
         if (rowBytes % 16 != 0 || reinterpret_cast<uintptr_t>(b.src) % 16 != 0 || lds > 65536)
             return false;
+        // next-row prefetch (knob resample.prefetch): 1 (default) for 2-byte destinations, 2 for
+        // every destination, 0 off.  Measured (profiles/r05/gatherp.jsonl, in-process A/B): UInt16
+        // 1024^3 -> 768^3 0.378 -> 0.358 ms, 768^3 -> 1024^3 0.520 -> 0.517; UInt8 (the capped grid,
+        // waves over several tasks) LOST: 768^3 -> 1024^3 0.306 -> 0.38 ms, 1024^3 -> 768^3 0.244 -> 0.293
+        int64_t const pk = rt::knob(rt::Knob::ResamplePrefetch);
+        bool const prefetch = (pk == 2 || (pk == 1 && bd == 2)) && !detect && !chain && rowBytes <= 4096;
         // one task per wave; for 1-byte destinations a task writes so little (one 1-KiB store
         // per dst row) that staging the x table per workgroup dominates: there the grid is
         // capped and waves loop over tasks (768^3 -> 1024^3 UInt8: 0.38 -> 0.29 ms; 2- and
@@ -768,7 +803,14 @@ namespace hipk
             blocks = 16384;
         unsigned const g = static_cast<unsigned>(blocks < (1u << 30) ? blocks : (1u << 30));
         uint32_t const slot = static_cast<uint32_t>(rowBytes);
-#define VKT_GL(S, D, C, H) hipLaunchKernelGGL((resampleGatherLdsKernel<S, D, C, H>), dim3(g), dim3(kBlock), lds, s, b, slot)
+#define VKT_GL(S, D, C, H)                                                                                         \
+    do {                                                                                                           \
+        if (prefetch && !(H))   /* (a chain instance with PREFETCH compiles as the plain one) */                  \
+            hipLaunchKernelGGL((resampleGatherLdsKernel<S, D, C, H, false, true>), dim3(g), dim3(kBlock), lds, s, b, \
+                               slot);                                                                              \
+        else                                                                                                       \
+            hipLaunchKernelGGL((resampleGatherLdsKernel<S, D, C, H>), dim3(g), dim3(kBlock), lds, s, b, slot);     \
+    } while (0)
 #define VKT_GL_D(S, C, H) do { if (bd == 1) VKT_GL(S, 1, C, H); else if (bd == 2) VKT_GL(S, 2, C, H); else VKT_GL(S, 4, C, H); } while (0)
 #define VKT_GLX(D, C) hipLaunchKernelGGL((resampleGatherLdsKernel<4, D, C, false, true>), dim3(g), dim3(kBlock), lds, s, b, slot)
         if (detect)
