@@ -76,3 +76,25 @@ def test_resample_gather_prefetch_multi_task_waves(g, o, prefetch):
                 assert_codes_equal(out, ref, df, f"prefetch={prefetch} df={df} fm={fm}")
     finally:
         lib.vktHipSetTuningKnob(b"resample.prefetch", -1)
+
+
+@pytest.mark.parametrize("anyrows", [1, 0])
+@pytest.mark.parametrize("sd,dd,sf,df", [((37, 20, 10), (64, 30, 14), 4, 4), ((21, 13, 9), (40, 20, 11), 5, 5),
+                                         ((13, 9, 7), (20, 11, 9), 7, 7), ((100, 8, 6), (128, 9, 7), 4, 4),
+                                         ((250, 12, 5), (176, 7, 9), 4, 5), ((19, 33, 4), (32, 17, 6), 7, 4)])
+def test_resample_gather_rows_not_16_byte_multiples(g, o, sd, dd, sf, df, anyrows):
+    """Knob resample.any_rows: source rows that are not 16-B multiples are staged in LDS too (the
+    chunk past the row end taken at rowBytes - 16, overlapping its neighbour), Float32 Linear
+    with specials included -- vs the oracle, knob on and off."""
+    from volkit_amd._lib import lib
+    rng = np.random.default_rng(sum(sd) * 3 + sum(dd) + sf * 11 + df)
+    src = rand_codes(rng, sf, sd[::-1], floats="mixed")
+    assert lib.vktHipSetTuningKnob(b"resample.any_rows", anyrows) == 0
+    try:
+        for fm in (0, 1):
+            for dmap in ((0.0, 1.0), (-1.0, 3.0)):
+                out = g.resample(df, dmap, dd, sf, (0.0, 1.0), src, fm)
+                ref = o.resample(df, dmap, dd, sf, (0.0, 1.0), src, fm)
+                assert_codes_equal(out, ref, df, f"anyrows={anyrows} {sd}->{dd} {sf}->{df} {dmap} fm={fm}")
+    finally:
+        lib.vktHipSetTuningKnob(b"resample.any_rows", -1)

@@ -730,6 +730,26 @@ def main():
                 free(S, Rv)
         finally:
             lib.vktHipSetTuningKnob(b"resample.prefetch", -1)
+    if want("gathera"):
+        # in-process A/B: source rows that are not 16-B multiples staged in LDS (knob
+        # resample.any_rows 1) vs the per-voxel gather (0)
+        cases = [(1000, 1024, 4, 1), (1000, 768, 4, 1), (1000, 1024, 7, 0), (1001, 1024, 5, 1)]
+        try:
+            for se, de, fmt, fm in cases:
+                b = {4: 1, 5: 2, 7: 4}[fmt]
+                S = alloc((se,) * 3, fmt, seed=21)
+                if fmt == 7:
+                    rng_fill(S, se ** 3)
+                Rv = alloc((de,) * 3, fmt)
+                for rep in range(2):
+                    for k in (0, 1):
+                        lib.vktHipSetTuningKnob(b"resample.any_rows", k)
+                        ms = timed(lambda: lib.vktHipResample(Rv, S, fm), max(3, R // 2))
+                        report(f"gathera Resample {se}^3->{de}^3 fmt{fmt} {'Linear' if fm else 'Nearest'} "
+                               f"[any_rows={k}]", ms, resample_bytes((se,) * 3, (de,) * 3, b, b), de ** 3)
+                free(S, Rv)
+        finally:
+            lib.vktHipSetTuningKnob(b"resample.any_rows", -1)
     if want("gpmc"):
         # one launch per case for FETCH / WRITE passes: the downsampling gathers whose bytes the
         # table image decides (UInt16: staged rows only; Float32 Linear: every source row)

@@ -193,6 +193,20 @@ namespace hipk
     // DETECT (Float32 "Linear", optimistic): every staged source row is also checked for values
     // that can make the lerp chain differ from v000 (chainSensitive); such a row's flag is set
     // in a.rowDirtyOut and resampleGatherFixupKernel later re-evaluates the affected tasks.
+    // A 16-B vector at any byte address (source rows that are not 16-B multiples start anywhere).
+    struct __attribute__((packed, aligned(1))) RowVec16
+    {
+        u32x4 v;
+    };
+
+    // Offset of a row's 16-B chunk starting at byte o (< rowBytes): rows of a whole number of
+    // chunks keep o; otherwise the chunk that would run past the row end is taken at rowBytes - 16
+    // instead (it overlaps its neighbour with the same bytes), so no load leaves the row.
+    __device__ __forceinline__ uint32_t rowChunk(uint32_t o, uint32_t rowBytes)
+    {
+        return o + 16u <= rowBytes ? o : rowBytes - 16u;
+    }
+
     // PREFETCH (knob resample.prefetch; rows <= 4 KiB, no chain / detect): a wave that loops over
     // tasks (the capped UInt8 grid) loads the NEXT task's source row into registers while it
     // gathers and stores the current one, instead of one load -> wait -> gather round trip per task.
@@ -226,7 +240,7 @@ namespace hipk
 #pragma unroll
             for (int j = 0; j < kStage; ++j)
                 if (16u * lane + 1024u * j < rowBytes)
-                    pre[j] = __builtin_nontemporal_load(reinterpret_cast<u32x4 const*>(np + 16u * lane + 1024u * j));
+                    pre[j] = reinterpret_cast<RowVec16 const*>(np + rowChunk(16u * lane + 1024u * j, rowBytes))->v;
         };
         if constexpr (kPre)
         {
@@ -244,7 +258,7 @@ namespace hipk
 #pragma unroll
                 for (int j = 0; j < kStage; ++j)
                     if (16u * lane + 1024u * j < rowBytes)
-                        *reinterpret_cast<u32x4*>(slot + 16u * lane + 1024u * j) = pre[j];
+                        reinterpret_cast<RowVec16*>(slot + rowChunk(16u * lane + 1024u * j, rowBytes))->v = pre[j];
                 if (t + totalWaves < tasks)
                     loadRow(t + totalWaves);
             }
@@ -264,11 +278,17 @@ namespace hipk
 #pragma unroll
                 for (int j = 0; j < kStage; ++j)
                     if (o0 + 1024u * j < rowBytes)
-                        w[j] = __builtin_nontemporal_load(reinterpret_cast<u32x4 const*>(sp + o0 + 1024u * j));
+                    {
+                        uint32_t const oc = rowChunk(o0 + 1024u * j, rowBytes);
+                        if (rowBytes % 16u == 0u)   // (wave-uniform) aligned rows: nontemporal vector loads
+                            w[j] = __builtin_nontemporal_load(reinterpret_cast<u32x4 const*>(sp + oc));
+                        else
+                            w[j] = reinterpret_cast<RowVec16 const*>(sp + oc)->v;
+                    }
 #pragma unroll
                 for (int j = 0; j < kStage; ++j)
                     if (o0 + 1024u * j < rowBytes)
-                        *reinterpret_cast<u32x4*>(slot + o0 + 1024u * j) = w[j];
+                        reinterpret_cast<RowVec16*>(slot + rowChunk(o0 + 1024u * j, rowBytes))->v = w[j];
                 if constexpr (DETECT)
                 {
                     bool sens = false;
@@ -785,8 +805,11 @@ namespace hipk
             return false;
         uint64_t const rowBytes = static_cast<uint64_t>(b.sdx) * bs;
         uint64_t const xtBytes = (static_cast<uint64_t>(b.ddx) * 4 + 15) & ~uint64_t(15);
-        uint64_t const lds = xtBytes + (kBlock / 64) * rowBytes;
-        if (rowBytes % 16 != 0 || reinterpret_cast<uintptr_t>(b.src) % 16 != 0 || lds > 65536)
+        // rows that are not 16-B multiples (>= 16 B) stage through rowChunk; slots stay 16-B aligned
+        uint64_t const slotBytes = (rowBytes + 15) & ~uint64_t(15);
+        uint64_t const lds = xtBytes + (kBlock / 64) * slotBytes;
+        if (rowBytes < 16 || (rowBytes % 16 != 0 && rt::knob(rt::Knob::ResampleAnyRows) == 0) ||
+            reinterpret_cast<uintptr_t>(b.src) % 16 != 0 || lds > 65536)
             return false;
         // next-row prefetch (knob resample.prefetch): 1 (default) for 2-byte destinations, 2 for
         // every destination, 0 off.  Measured (profiles/r05/gatherp.jsonl, in-process A/B): UInt16
@@ -802,7 +825,7 @@ namespace hipk
         if (bd == 1 && blocks > 16384)
             blocks = 16384;
         unsigned const g = static_cast<unsigned>(blocks < (1u << 30) ? blocks : (1u << 30));
-        uint32_t const slot = static_cast<uint32_t>(rowBytes);
+        uint32_t const slot = static_cast<uint32_t>(slotBytes);
 #define VKT_GL(S, D, C, H)                                                                                         \
     do {                                                                                                           \
         if (prefetch && !(H))   /* (a chain instance with PREFETCH compiles as the plain one) */                  \

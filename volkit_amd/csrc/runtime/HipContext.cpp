@@ -257,6 +257,7 @@ namespace rt
             {"transform.shape", 0},
             {"decompose.direct", 1},
             {"resample.prefetch", 1},
+            {"resample.any_rows", 1},
             {"histogram.pair_tiles", 1},
         };
         static_assert(sizeof(kKnobs) / sizeof(kKnobs[0]) == static_cast<size_t>(Knob::Count), "knob table");
@@ -280,7 +281,8 @@ namespace rt
                                                                   {kKnobs[34].def}, {kKnobs[35].def},
                                                                   {kKnobs[36].def}, {kKnobs[37].def},
                                                                   {kKnobs[38].def}, {kKnobs[39].def},
-                                                                  {kKnobs[40].def}, {kKnobs[41].def}};
+                                                                  {kKnobs[40].def}, {kKnobs[41].def},
+                                                                  {kKnobs[42].def}};
     } // namespace
 
     int64_t knob(Knob k) { return gKnobs[static_cast<int>(k)].load(std::memory_order_relaxed); }
