@@ -21,6 +21,11 @@ them is `value`):
   * f32_linear     -- Float32 "Linear" Resample with the z+1 halo plane exchanged between
                       neighbour ranks over torch.distributed on device tensors (RCCL over
                       xGMI at N>1): per rank 512^3 -> 1024^3 of the same global layout;
+  * f32_linear_native -- the same leg through the library's own C-ABI communicator
+                      (vktHipCommGetUniqueId broadcast over the process group ->
+                      vktHipCommInitRank -> vktHipSlabExchangeHalo + vktHipResampleSlab, and
+                      vktHipResampleSlabOverlapped): at N>1 with the nccl backend, or with
+                      --native-comm on a one-rank communicator; its dst equals the torch path's;
   * config4_2048   -- BASELINE config 4 in its STRONG-scaling form: the fixed global volume
                       1024^3 -> 2048^3 Resample + SumRange 2048^3 UInt16 Z-slab partitioned over
                       the N GPUs launched (at N=1 the whole 2048^3 on one GPU, ~50 GiB of
@@ -69,6 +74,9 @@ def parse():
                    help="torch.distributed backend for N>1 (nccl = RCCL over xGMI; gloo only for rehearsal)")
     p.add_argument("--rehearse-one-device", action="store_true",
                    help="put every rank on device 0 (multi-rank rehearsal on a 1-GPU box, with --dist-backend gloo)")
+    p.add_argument("--native-comm", action="store_true",
+                   help="run the f32_linear_native leg also at N=1 (a one-rank communicator; at N>1 with the "
+                        "nccl backend it always runs)")
     p.add_argument("--dist-timeout", type=float, default=300.0,
                    help="seconds: torch.distributed process-group timeout (collectives and p2p waits)")
     p.add_argument("--secondary-timeout", type=float, default=120.0,
@@ -325,6 +333,12 @@ def main():
         out["f32_linear"] = guarded(out, "f32_linear",
                                     lambda: f32_linear(ctx, vkt, slab, lib, args, layout_n, stream),
                                     args.secondary_timeout, rank)
+        # the library's own RCCL transport (C ABI): where a real exchange runs, or on request
+        if layout_n == world and (args.native_comm or (world > 1 and args.dist_backend == "nccl")):
+            want = out["f32_linear"].get("dst_checksum") if isinstance(out["f32_linear"], dict) else None
+            out["f32_linear_native"] = guarded(out, "f32_linear_native",
+                                               lambda: f32_linear_native(ctx, vkt, slab, lib, args, stream, want),
+                                               args.secondary_timeout, rank)
     if not args.no_config4:
         out["config4_2048"] = guarded(out, "config4_2048",
                                       lambda: config4_strong(ctx, vkt, slab, lib, args, layout_n, stream),
@@ -477,7 +491,9 @@ def f32_linear(ctx, vkt, slab, lib, args, layout_n, stream):
         ms = elapsed_o * 1e3 / steps
     vox = DX * DY * (dz1 - dz0)
     nbytes = 4 * SX * SY * (o1 - o0) + 4 * vox
+    checksum = dst_checksum(torch, rv)
     out = {
+        "dst_checksum": checksum,
         "workload": f"Resample {SX}x{SY}x{sgz}->{DX}x{DY}x{dgz} Float32 Linear (source uniform [0,1)), "
                     f"Z-slab over {layout_n} GPU(s), z+1 halo exchanged on device tensors "
                     f"({'RCCL' if ctx.backend == 'nccl' and world > 1 else ctx.backend if world > 1 else 'none'})",
@@ -493,6 +509,105 @@ def f32_linear(ctx, vkt, slab, lib, args, layout_n, stream):
     }
     del S, R
     return out
+
+
+def dst_checksum(torch, view):
+    """Sum of the dst slab's 32-bit words (int64): the bytes of one leg against another's."""
+    from volkit_amd import slab
+    words = slab.device_tensor(view.data, view.dimX * view.dimY * view.dimZ * 4).view(torch.int32)
+    return int(words.sum(dtype=torch.int64).item())
+
+
+def f32_linear_native(ctx, vkt, slab, lib, args, stream, want_checksum):
+    """f32_linear's workload with the halo moved by the library's own communicator (the C-ABI
+    multi-GPU surface, include/volkit_hip.h; design intent reference include/c/vkt/CudaContext.h:
+    41-65): rank 0's vktHipCommGetUniqueId broadcast over the process group, vktHipCommInitRank,
+    then per step (a) vktHipSlabExchangeHalo + vktHipResampleSlab (one RCCL group round on the
+    library's compute stream, then the resample) and (b) vktHipResampleSlabOverlapped (the round
+    on the communicator's stream under the interior planes).  Both legs' dst bytes are checked
+    against the torch-transport leg's checksum."""
+    import torch
+    from volkit_amd._lib import HipCommId_t
+    rank, world = ctx.rank, ctx.world
+    LINEAR, FLOAT32 = vkt.FilterMode_Linear, vkt.DataFormat_Float32
+    DX, DY, dgz = global_dims(args.dst, world)
+    SX, SY, sgz = DX // 2, DY // 2, dgz // 2
+    plan = slab.plan_resample(dgz, sgz, world, rank, LINEAR, chain=True)
+    ls0, ls1 = plan.local_src
+    dz0, dz1 = plan.dst
+    uid = HipCommId_t()
+    if rank == 0 and lib.vktHipCommGetUniqueId(C.byref(uid)) != 0:
+        raise RuntimeError(vkt.last_error())
+    if world > 1:
+        dev = "cuda" if ctx.backend == "nccl" else "cpu"
+        t = torch.frombuffer(bytearray(C.string_at(C.addressof(uid), C.sizeof(uid))), dtype=torch.uint8).to(dev)
+        ctx.dist.broadcast(t, src=0)
+        C.memmove(C.addressof(uid), bytes(t.cpu().numpy().tobytes()), C.sizeof(uid))
+    comm = C.c_void_p()
+    if lib.vktHipCommInitRank(C.byref(comm), world, uid, rank) != 0:
+        raise RuntimeError(vkt.last_error())
+    S = R = None
+    try:
+        if lib.vktHipCommSetTimeout(comm, int(args.dist_timeout * 1000)) != 0:
+            raise RuntimeError(vkt.last_error())
+        S = vkt.StructuredVolume(SX, SY, ls1 - ls0, FLOAT32)
+        R = vkt.StructuredVolume(DX, DY, dz1 - dz0, FLOAT32)
+        sv, rv = S.hip_view(), R.hip_view()
+        src_t = slab.device_tensor(sv.data, (ls1 - ls0) * SX * SY * 4).view(torch.float32)
+        gen = torch.Generator(device="cuda")
+        gen.manual_seed(0x5EED + rank)              # the f32_linear leg's source, bit for bit
+        src_t.uniform_(0.0, 1.0, generator=gen)
+        torch.cuda.synchronize()
+
+        def step(ev):
+            if ev:
+                ev[0].record(stream)
+            if lib.vktHipSlabExchangeHalo(comm, sv, ls0, dgz, sgz, LINEAR, 1) != 0:
+                raise RuntimeError(vkt.last_error())
+            if ev:
+                ev[1].record(stream)
+            if lib.vktHipResampleSlab(rv, sv, LINEAR, dgz, dz0, sgz, ls0) != 0:
+                raise RuntimeError(vkt.last_error())
+            if ev:
+                ev[2].record(stream)
+
+        def step_overlapped(ev):
+            if ev:
+                ev[0].record(stream)
+            if lib.vktHipResampleSlabOverlapped(comm, rv, sv, ls0, dgz, sgz, LINEAR, 1) != 0:
+                raise RuntimeError(vkt.last_error())
+            if ev:
+                ev[1].record(stream)
+
+        steps = max(5, args.steps // 2)
+        elapsed, (ex_ms, res_ms) = ctx.timed(step, steps, 3, 2)
+        if lib.vktHipCommSynchronize(comm) != 0:
+            raise RuntimeError(vkt.last_error())
+        serial_sum = dst_checksum(torch, rv)
+        R_bytes = slab.device_tensor(rv.data, DX * DY * (dz1 - dz0) * 4)
+        R_bytes.fill_(0)
+        elapsed_o, (ov_ms,) = ctx.timed(step_overlapped, steps, 3, 1)
+        if lib.vktHipCommSynchronize(comm) != 0:
+            raise RuntimeError(vkt.last_error())
+        overlapped_sum = dst_checksum(torch, rv)
+        vox = DX * DY * (dz1 - dz0)
+        ms = elapsed_o * 1e3 / steps
+        return {
+            "workload": f"Resample {SX}x{SY}x{sgz}->{DX}x{DY}x{dgz} Float32 Linear, Z-slab over {world} GPU(s), "
+                        f"z+1 halo moved by libvolkit's communicator (RCCL, C ABI)",
+            "transport": "vktHipCommInitRank + vktHipSlabExchangeHalo / vktHipResampleSlabOverlapped "
+                         f"({'RCCL over xGMI' if world > 1 else 'one-rank communicator: no plane moves'})",
+            "value": round(vox * world / (ms / 1e3) / 1e9, 3), "unit": "Gvoxels/s", "ms_per_step": round(ms, 4),
+            "ms_per_step_serial_exchange": round(elapsed * 1e3 / steps, 4),
+            "exchange_ms": round(ex_ms, 4), "resample_ms": round(res_ms, 4), "overlapped_ms": round(ov_ms, 4),
+            "halo_planes_per_rank": plan.halo_planes,
+            "matches_torch_transport": (want_checksum is not None and serial_sum == want_checksum
+                                        and overlapped_sum == want_checksum),
+            "dst_checksum": overlapped_sum,
+        }
+    finally:
+        del S, R
+        lib.vktHipCommDestroy(comm)
 
 
 PCIE_PEAK_GBS = 63.0   # MI355X host link, PCIe Gen5 x16 per direction (MI355X_MICROARCH.md)

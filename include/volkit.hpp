@@ -132,6 +132,11 @@ namespace vkt
         // migration failed is still in its old address space.
         VKTAPI void CopyBetween(void* dst, ExecutionPolicy const& dstOwner, void const* src,
                                 ExecutionPolicy const& srcOwner, std::size_t bytes);
+        // MemsetRange where the bytes live (`owner`: the buffer's last allocation policy), not
+        // where the thread's policy points -- a buffer whose migration failed is still in host
+        // memory and gets the host pattern loop.
+        VKTAPI void MemsetRangeOn(void* dst, void const* src, std::size_t dstSize, std::size_t srcSize,
+                                  ExecutionPolicy const& owner);
     }
 
     //--- ManagedBuffer<T> (reference include/cpp/vkt/ManagedBuffer.hpp:21-276) -----------
@@ -243,7 +248,7 @@ namespace vkt
         void fill(T& value)
         {
             migrate();
-            MemsetRange(data_, &value, size_ * sizeof(T), sizeof(T));
+            detail::MemsetRangeOn(data_, &value, size_ * sizeof(T), sizeof(T), lastAllocationPolicy_);
         }
 
         void fill(T const& value) { fill(const_cast<T&>(value)); }

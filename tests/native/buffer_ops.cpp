@@ -4,6 +4,7 @@
 // policy fill() migrates the buffer to HBM and calls MemsetRange (vktHipMemsetRange's
 // kernels), which repeats the element bytes over the buffer.
 #include "volkit.hpp"
+#include "volkit_hip.h"
 
 #include <cstdint>
 #include <cstring>
@@ -68,6 +69,41 @@ int vktt_managed_fill(int elemBytes, size_t count, uint8_t const* pattern, uint8
     case 300: return fillAndRead<300>(count, pattern, out);
     default: return -100;
     }
+}
+
+// ManagedBuffer<uint32_t>::fill under the GPU policy on a buffer allocated under the CPU policy
+// whose migration to HBM fails (test knob memory.fail_next_alloc): the buffer stays in host
+// memory (the same pointer), and fill() must write the pattern there -- the host pattern loop
+// of MemsetRange_serial (reference src/vkt/Memory_serial.hpp:24-37) -- not launch the pattern
+// kernel on the pageable pointer.  Copies the host bytes to `out` (count * 4 bytes).
+// Returns 0, or -1 when the buffer moved (the knob did not fail the allocation), -2 when the
+// buffer is not host-resident after fill().
+int vktt_fill_after_failed_migration(size_t count, uint32_t pattern, uint8_t* out)
+{
+    vkt::ExecutionPolicy saved = vkt::GetThreadExecutionPolicy();
+    vkt::ExecutionPolicy cpu = saved, gpu = saved;
+    cpu.device = vkt::ExecutionPolicy::Device::CPU;
+    gpu.device = vkt::ExecutionPolicy::Device::GPU;
+    vkt::SetThreadExecutionPolicy(cpu);
+    int rc = 0;
+    {
+        FillableBuffer<uint32_t> buf(count);   // host memory (CPU policy)
+        uint32_t* const host = buf.raw();
+        std::memset(host, 0xEE, count * 4);
+        vktHipSetTuningKnob("memory.fail_next_alloc", 1);
+        vkt::SetThreadExecutionPolicy(gpu);
+        buf.fill(pattern);                     // migrate() fails: the bytes stay on the host
+        vkt::SetThreadExecutionPolicy(cpu);
+        vktHipSetTuningKnob("memory.fail_next_alloc", 0);
+        if (!buf.residentOn(cpu))
+            rc = -2;
+        else if (buf.raw() != host)
+            rc = -1;
+        else
+            std::memcpy(out, host, count * 4);
+    }
+    vkt::SetThreadExecutionPolicy(saved);
+    return rc;
 }
 
 } // extern "C"

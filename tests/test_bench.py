@@ -83,3 +83,23 @@ def test_bench_small_run_prints_one_contract_line():
         assert mig[kind]["H2D_GBs"] > 0 and mig[kind]["D2H_GBs"] > 0, mig
     cpu = out["cpu_baseline"]
     assert cpu["kind"] == "port" and cpu["cores"] == 1 and cpu["value"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_native_comm_leg_on_one_rank():
+    """the f32_linear_native leg (libvolkit's own C-ABI communicator:
+    vktHipCommGetUniqueId -> vktHipCommInitRank -> vktHipSlabExchangeHalo + vktHipResampleSlab
+    and vktHipResampleSlabOverlapped) end to end on a one-rank communicator; its dst bytes equal
+    the torch-transport leg's.  At N>1 with the nccl backend the same leg moves the halo over
+    RCCL between GPUs (the driver's 8-GPU run)."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dst", "128", "--steps", "4",
+                        "--warmup", "1", "--no-cpu-baseline", "--no-copy-peak", "--no-config4", "--no-migrate",
+                        "--native-comm"], capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    nat = out["f32_linear_native"]
+    assert "error" not in nat, nat
+    assert nat["value"] > 0 and nat["exchange_ms"] >= 0 and nat["overlapped_ms"] > 0
+    assert nat["matches_torch_transport"] is True, (nat, out["f32_linear"])
+    assert nat["dst_checksum"] == out["f32_linear"]["dst_checksum"]
+    assert "one-rank communicator" in nat["transport"]

@@ -192,3 +192,143 @@ def test_round_deadline_aborts_without_blocking_the_host():
         lib.vktHipSetTuningKnob(b"comm.test_stall_ms", 0)
         torch.cuda.synchronize()                 # (the stall kernel leaves after its 4 s)
         assert lib.vktHipCommDestroy(comm) == 0, _lib.last_error()
+
+
+@pytest.mark.gpu
+def test_round_deadline_fails_the_issuing_call_when_synchronous():
+    """with async execution off (vktHipSetAsyncExecution(0)) every call
+    synchronises, so the call whose round outlived its deadline returns vktInvalidValue itself,
+    naming the deadline (comm::finishRound -> vktHipCommSynchronize after the stream drained) --
+    not vktNoError with garbage in the halo and the failure surfacing on a later call."""
+    import torch
+    torch.cuda.init()
+    was = C.c_int32()
+    assert lib.vktHipGetAsyncExecution(C.byref(was)) == 0
+    uid = HipCommId_t()
+    assert lib.vktHipCommGetUniqueId(C.byref(uid)) == 0, _lib.last_error()
+    comm = C.c_void_p()
+    assert lib.vktHipCommInitRank(C.byref(comm), 1, uid, 0) == 0, _lib.last_error()
+    a = torch.arange(1 << 18, dtype=torch.int32, device="cuda").view(torch.uint8)
+    b = torch.zeros_like(a)
+    torch.cuda.synchronize()
+    try:
+        assert lib.vktHipSetAsyncExecution(0) == 0
+        assert lib.vktHipCommSetTimeout(comm, 5000) == 0
+        # a clean round: the synchronous call judges it and returns 0, the bytes have landed
+        assert lib.vktHipCommExchange(comm, 0, C.c_void_p(a.data_ptr()), C.c_void_p(b.data_ptr()), a.numel()) == 0, \
+            _lib.last_error()
+        assert torch.equal(a, b)
+        assert lib.vktHipSetTuningKnob(b"comm.test_stall_ms", 1500) == 0
+        assert lib.vktHipCommSetTimeout(comm, 300) == 0
+        err = lib.vktHipCommExchange(comm, 0, C.c_void_p(a.data_ptr()), C.c_void_p(b.data_ptr()), a.numel())
+        msg = _lib.last_error()
+        assert err != 0 and "within 300 ms" in msg, (err, msg)
+    finally:
+        lib.vktHipSetTuningKnob(b"comm.test_stall_ms", 0)
+        lib.vktHipSetAsyncExecution(was.value)
+        torch.cuda.synchronize()
+        assert lib.vktHipCommDestroy(comm) == 0, _lib.last_error()
+
+
+@pytest.mark.gpu
+def test_overlapped_resample_on_one_rank_matches_resample_slab():
+    """vktHipResampleSlabOverlapped on a one-rank communicator (the C entry had no
+    test): the whole volume is the rank's slab, nothing moves, the interior split covers every
+    dst plane -- bytes equal one vktHipResampleSlab of the same volume (Float32 Linear, the
+    z+1 chain, with non-finite voxels), in async and synchronous mode."""
+    import numpy as np
+    import torch
+    torch.cuda.init()
+    rng = np.random.default_rng(77)
+    vals = rng.uniform(-1, 2, (24, 20, 36)).astype(np.float32)
+    vals[7, 3, 5], vals[23, 19, 35], vals[0, 0, 0] = np.inf, np.nan, -0.0
+    src = torch.from_numpy(vals).cuda()
+    dd = (50, 31, 40)                                     # dst (x, y, z)
+    want = torch.zeros((dd[2], dd[1], dd[0]), dtype=torch.float32, device="cuda")
+    got = torch.full_like(want, 7.0)
+    sv = HipVolumeView_t(src.data_ptr(), 36, 20, 24, 7, 0.0, 1.0)
+    wv = HipVolumeView_t(want.data_ptr(), dd[0], dd[1], dd[2], 7, 0.0, 1.0)
+    gv = HipVolumeView_t(got.data_ptr(), dd[0], dd[1], dd[2], 7, 0.0, 1.0)
+    assert lib.vktHipResampleSlab(wv, sv, LINEAR, dd[2], 0, 24, 0) == 0, _lib.last_error()
+    was = C.c_int32()
+    assert lib.vktHipGetAsyncExecution(C.byref(was)) == 0
+    uid = HipCommId_t()
+    assert lib.vktHipCommGetUniqueId(C.byref(uid)) == 0, _lib.last_error()
+    comm = C.c_void_p()
+    assert lib.vktHipCommInitRank(C.byref(comm), 1, uid, 0) == 0, _lib.last_error()
+    try:
+        for mode in (1, 0):
+            assert lib.vktHipSetAsyncExecution(mode) == 0
+            got.fill_(7.0)
+            torch.cuda.synchronize()
+            assert lib.vktHipResampleSlabOverlapped(comm, gv, sv, 0, dd[2], 24, LINEAR, 1) == 0, _lib.last_error()
+            torch.cuda.synchronize()
+            assert torch.equal(got.view(torch.int32), want.view(torch.int32)), mode
+        # a dst view that is not the rank's slab is refused
+        bad = HipVolumeView_t(got.data_ptr(), dd[0], dd[1], dd[2] - 1, 7, 0.0, 1.0)
+        assert lib.vktHipResampleSlabOverlapped(comm, bad, sv, 0, dd[2], 24, LINEAR, 1) != 0
+        assert "dst slab" in _lib.last_error()
+    finally:
+        lib.vktHipSetAsyncExecution(was.value)
+        assert lib.vktHipCommDestroy(comm) == 0, _lib.last_error()
+
+
+def _two_rank_overlapped_worker(rank, uid_bytes, result_q):
+    """One rank of test_two_rank_overlapped_resample (one GPU per rank)."""
+    import numpy as np
+    import torch
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    torch.cuda.set_device(rank)
+    assert lib.vktHipSetDevice(rank) == 0
+    uid = HipCommId_t()
+    C.memmove(C.addressof(uid), uid_bytes, 128)
+    comm = C.c_void_p()
+    assert lib.vktHipCommInitRank(C.byref(comm), 2, uid, rank) == 0, _lib.last_error()
+    dst_gdz, src_gdz, dx, dy, sx, sy = 64, 32, 40, 12, 24, 10
+    rng = np.random.default_rng(5)
+    vals = rng.uniform(-1, 2, (src_gdz, sy, sx)).astype(np.float32)
+    (lo, hi), recvs, _ = c_plan(dst_gdz, src_gdz, 2, rank, LINEAR, True)
+    o0, o1 = slab.slab_bounds(src_gdz, 2, rank)
+    d0, d1 = slab.slab_bounds(dst_gdz, 2, rank)
+    out = []
+    for path in ("overlapped", "exchange"):
+        src = torch.zeros((hi - lo, sy, sx), dtype=torch.float32, device="cuda")
+        src[o0 - lo:o1 - lo] = torch.from_numpy(vals[o0:o1]).cuda()     # halo planes start at 0
+        dst = torch.zeros((d1 - d0, dy, dx), dtype=torch.float32, device="cuda")
+        sv = HipVolumeView_t(src.data_ptr(), sx, sy, hi - lo, 7, 0.0, 1.0)
+        dv = HipVolumeView_t(dst.data_ptr(), dx, dy, d1 - d0, 7, 0.0, 1.0)
+        if path == "overlapped":
+            err = lib.vktHipResampleSlabOverlapped(comm, dv, sv, lo, dst_gdz, src_gdz, LINEAR, 1)
+        else:
+            err = lib.vktHipSlabExchangeHalo(comm, sv, lo, dst_gdz, src_gdz, LINEAR, 1)
+            if err == 0:
+                err = lib.vktHipResampleSlab(dv, sv, LINEAR, dst_gdz, d0, src_gdz, lo)
+        torch.cuda.synchronize()
+        out.append((err, dst.cpu().numpy().view(np.uint32).copy()))
+    lib.vktHipCommDestroy(comm)
+    result_q.put((rank, len(recvs), out[0][0], out[1][0], bool(np.array_equal(out[0][1], out[1][1]))))
+
+
+@pytest.mark.gpu
+def test_two_rank_overlapped_resample():
+    """vktHipResampleSlabOverlapped between two processes (one GPU each) equals
+    vktHipSlabExchangeHalo + vktHipResampleSlab on the same slabs; rank 0 receives the z+1 halo
+    plane, rank 1 receives nothing (its interior split covers its whole slab)."""
+    import torch
+    import torch.multiprocessing as mp
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two GPUs (RCCL refuses two ranks on one device)")
+    uid = HipCommId_t()
+    assert lib.vktHipCommGetUniqueId(C.byref(uid)) == 0
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_two_rank_overlapped_worker, args=(r, C.string_at(C.addressof(uid), 128), q))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert [r[1] > 0 for r in res] == [True, False]
+    for rank, _, e_ov, e_ex, same in res:
+        assert e_ov == 0 and e_ex == 0 and same, rank

@@ -750,6 +750,30 @@ def main():
                 free(S, Rv)
         finally:
             lib.vktHipSetTuningKnob(b"resample.any_rows", -1)
+    if want("u8gather"):
+        # the UInt8 LDS gather beside UInt16 on the same ratios (Linear = Nearest
+        # for integer formats), one case per launch group for the counter passes
+        cases = [(1024, 768, 4), (768, 1024, 4), (1000, 1024, 4), (1024, 768, 5), (768, 1024, 5), (1000, 1024, 5)]
+        for se, de, fmt in cases:
+            b = {4: 1, 5: 2}[fmt]
+            S = alloc((se,) * 3, fmt, seed=21)
+            Rv = alloc((de,) * 3, fmt)
+            ms = timed(lambda: lib.vktHipResample(Rv, S, 1), R)
+            report(f"u8gather Resample {se}^3->{de}^3 fmt{fmt} Linear", ms,
+                   resample_bytes((se,) * 3, (de,) * 3, b, b), de ** 3)
+            free(S, Rv)
+    if want("f32lin"):
+        # Float32 "Linear" (optimistic gather + fix-up) against Nearest on the
+        # gather ratios; Linear's bytes: every source row (the chain's neighbours are classified)
+        for se, de in ((768, 1024), (1024, 768)):
+            S = alloc((se,) * 3, 7)
+            rng_fill(S, se ** 3)
+            Rv = alloc((de,) * 3, 7)
+            for fm, lab in ((0, "Nearest"), (1, "Linear")):
+                ms = timed(lambda: lib.vktHipResample(Rv, S, fm), R)
+                report(f"f32lin Resample {se}^3->{de}^3 Float32 {lab}", ms,
+                       resample_bytes((se,) * 3, (de,) * 3, 4, 4, every_row=fm == 1), de ** 3)
+            free(S, Rv)
     if want("gpmc"):
         # one launch per case for FETCH / WRITE passes: the downsampling gathers whose bytes the
         # table image decides (UInt16: staged rows only; Float32 Linear: every source row)

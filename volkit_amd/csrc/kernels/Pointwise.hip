@@ -562,8 +562,12 @@ namespace hipk
             return rt::fail("MemsetRange: null pointer");
         if (patternSize > (1u << 30))
             return rt::fail("MemsetRange: pattern larger than 1 GiB");
-        hipStream_t s = rt::computeStream();
         uint64_t const nbytes = (dstSize / patternSize) * patternSize;   // whole patterns only
+        // a pageable host destination would fault the kernel (no XNACK): refused, nothing launched
+        vktError const where = rt::requireDevicePointer(dst, nbytes, "MemsetRange: destination is not device memory");
+        if (where != vktNoError)
+            return where;
+        hipStream_t s = rt::computeStream();
         uint8_t const* pb = static_cast<uint8_t const*>(pattern);
         uint32_t const psize = static_cast<uint32_t>(patternSize);
         uint32_t const elen = psize + 15;

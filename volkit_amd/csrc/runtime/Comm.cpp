@@ -171,17 +171,41 @@ namespace comm
         return vktNoError;
     }
 
-    // Aborts the communicator after a failed / timed-out round (its kernels exit; every later
-    // call on it fails fast).  c->m held.
-    void abortLocked(vktHipComm_t c, std::string const& why)
+    // Aborts the communicator after a failed round enqueue (its kernels exit; every later call
+    // on it fails fast) and returns the failure.  c->em held by the caller (the enqueue), c->m not.
+    vktError abortAfterEnqueue(vktHipComm_t c, std::string const& why)
     {
-        if (!c->aborted.load() && c->comm != nullptr)
-            (void)rccl().abort(c->comm);
-        c->comm = nullptr;
-        if (c->failure.empty())
-            c->failure = why + " (communicator aborted)";
-        c->aborted.store(true);
+        std::string msg;
+        {
+            std::lock_guard<std::mutex> g(c->m);
+            if (c->failure.empty())
+                c->failure = why + " (communicator aborted)";
+            c->aborted.store(true);
+            msg = c->failure;
+        }
+        if (ncclComm_t const dead = c->comm.exchange(nullptr))
+            (void)rccl().abort(dead);
+        return rt::fail(msg.c_str());
     }
+
+    // A round enqueue that does not let go of c->em within this long is taken to be stuck in
+    // RCCL (a blocking ncclGroupEnd waiting for a dead peer): the watcher aborts without it.
+    constexpr int64_t kEnqueueGraceMs = 2000;
+
+    // The two events of a round with a deadline; destroyed on every early return of the enqueue
+    // (the watcher destroys them once the round is handed over: release()).
+    struct RoundEvents
+    {
+        hipEvent_t start = nullptr, end = nullptr;
+        ~RoundEvents()
+        {
+            if (start != nullptr)
+                (void)hipEventDestroy(start);
+            if (end != nullptr)
+                (void)hipEventDestroy(end);
+        }
+        void release() { start = end = nullptr; }
+    };
 
     // A kernel that keeps one wave busy for `ms` milliseconds of wall clock (knob
     // comm.test_stall_ms: a round that outlives its deadline, for the watcher's test); every
@@ -216,11 +240,8 @@ namespace comm
                 err = std::string("hipEventQuery: ") + hipGetErrorString(q);
                 return false;
             }
-            ncclComm_t nc = nullptr;
-            {
-                std::lock_guard<std::mutex> g(c->m);
-                nc = c->comm;
-            }
+            // (no lock: the comm pointer is atomic, and an enqueue may be blocked inside RCCL)
+            ncclComm_t const nc = c->comm.load();
             ncclResult_t as = ncclSuccess;
             if (nc != nullptr && rccl().getAsyncError != nullptr && rccl().getAsyncError(nc, &as) == ncclSuccess &&
                 as != ncclSuccess && as != ncclInProgress)
@@ -260,26 +281,32 @@ namespace comm
             bool ok = pollEvent(c, r.start, 0, err);
             // ... its transfers have one, counted from their start
             ok = ok && pollEvent(c, r.end, r.timeoutMs, err);
-            ncclComm_t dead = nullptr;
+            if (!ok)
             {
-                std::lock_guard<std::mutex> g(c->m);
-                if (!ok)
+                // the failure is known now: record it and refuse later rounds before the abort,
+                // which returns only once the communicator's queued work has left the GPU (its
+                // kernels exit on the abort flag)
                 {
-                    // the failure is known now: record it and refuse later rounds before the
-                    // abort, which returns only once the communicator's queued work has left
-                    // the GPU (its kernels exit on the abort flag)
+                    std::lock_guard<std::mutex> g(c->m);
                     if (c->failure.empty())
                         c->failure = r.what + ": " + err + " (communicator aborted)";
-                    dead = c->aborted.load() ? nullptr : c->comm;
-                    c->comm = nullptr;
                     c->aborted.store(true);
                     VKT_LOG(rt::LogLevel::Error) << c->failure;
                 }
+                // An enqueue in flight finishes its RCCL calls on the comm before it goes (no
+                // use after the abort frees it) -- unless it is stuck in RCCL, when only the
+                // abort releases it.
+                bool const quiet = c->em.try_lock_for(std::chrono::milliseconds(kEnqueueGraceMs));
+                if (ncclComm_t const dead = c->comm.exchange(nullptr))
+                    (void)rccl().abort(dead);
+                if (quiet)
+                    c->em.unlock();
+            }
+            {
+                std::lock_guard<std::mutex> g(c->m);
                 c->rounds.pop_front();
             }
             c->cv.notify_all();
-            if (dead != nullptr)
-                (void)rccl().abort(dead);
             (void)hipEventDestroy(r.start);
             (void)hipEventDestroy(r.end);
         }
@@ -291,30 +318,35 @@ namespace comm
             return vktNoError;
         if (!rccl().ok)
             return noRccl(what);
-        std::unique_lock<std::mutex> g(c->m);
-        if (c->aborted.load())
+        std::lock_guard<std::timed_mutex> enqueue(c->em);
+        auto refused = [&]() {
+            std::lock_guard<std::mutex> g(c->m);
             return rt::fail((std::string(what) + ": the communicator was aborted after an earlier failure: " + c->failure)
                                 .c_str());
-        int64_t const deadline = c->timeoutMs;
-        vktHipComm_impl::Round r;
+        };
+        int64_t deadline = 0;
+        {
+            std::lock_guard<std::mutex> g(c->m);
+            deadline = c->timeoutMs;
+        }
+        ncclComm_t const nc = c->comm.load();
+        if (c->aborted.load() || nc == nullptr)
+            return refused();
+        RoundEvents ev;
         if (deadline > 0)
         {
-            if (rt::check(hipEventCreateWithFlags(&r.start, hipEventDisableTiming), "hipEventCreate") != vktNoError ||
-                rt::check(hipEventCreateWithFlags(&r.end, hipEventDisableTiming), "hipEventCreate") != vktNoError ||
-                rt::check(hipEventRecord(r.start, stream), "hipEventRecord(round start)") != vktNoError)
-            {
-                (void)hipEventDestroy(r.start);
-                (void)hipEventDestroy(r.end);
+            if (rt::check(hipEventCreateWithFlags(&ev.start, hipEventDisableTiming), "hipEventCreate") != vktNoError ||
+                rt::check(hipEventCreateWithFlags(&ev.end, hipEventDisableTiming), "hipEventCreate") != vktNoError ||
+                rt::check(hipEventRecord(ev.start, stream), "hipEventRecord(round start)") != vktNoError)
                 return vktInvalidValue;
-            }
         }
         ncclResult_t res = rccl().groupStart();
         if (res != ncclSuccess)
             return ncclFail((std::string(what) + ": ncclGroupStart").c_str(), res);
         for (Xfer const& x : xs)
         {
-            res = x.send ? rccl().send(x.ptr, x.bytes, ncclUint8, x.peer, c->comm, stream)
-                         : rccl().recv(x.ptr, x.bytes, ncclUint8, x.peer, c->comm, stream);
+            res = x.send ? rccl().send(x.ptr, x.bytes, ncclUint8, x.peer, nc, stream)
+                         : rccl().recv(x.ptr, x.bytes, ncclUint8, x.peer, nc, stream);
             if (res != ncclSuccess)
             {
                 (void)rccl().groupEnd();
@@ -322,31 +354,44 @@ namespace comm
             }
         }
         res = rccl().groupEnd();
+        if (c->aborted.load())   // the watcher aborted the communicator meanwhile (an earlier round)
+            return refused();
         if (res != ncclSuccess)
-        {
-            abortLocked(c, std::string(what) + ": ncclGroupEnd: " + rccl().errorString(res));
-            return rt::fail(c->failure.c_str());
-        }
+            return abortAfterEnqueue(c, std::string(what) + ": ncclGroupEnd: " + rccl().errorString(res));
         if (deadline <= 0)
             return vktNoError;
         // (test knob comm.test_stall_ms: the round outlives its deadline after its transfers)
         int64_t const stallMs = rt::knob(rt::Knob::CommTestStallMs);
         if (stallMs > 0)
             (void)stall(stream, stallMs);
-        if (rt::check(hipEventRecord(r.end, stream), "hipEventRecord(round end)") != vktNoError)
-        {
-            (void)hipEventDestroy(r.start);
-            (void)hipEventDestroy(r.end);
+        if (rt::check(hipEventRecord(ev.end, stream), "hipEventRecord(round end)") != vktNoError)
             return vktInvalidValue;
-        }
+        vktHipComm_impl::Round r;
+        r.start = ev.start;
+        r.end = ev.end;
         r.timeoutMs = deadline;
         r.what = what;
-        c->rounds.push_back(r);
-        if (!c->watcher.joinable())
-            c->watcher = std::thread(watch, c);
-        g.unlock();
+        {
+            std::lock_guard<std::mutex> g(c->m);
+            c->rounds.push_back(r);
+            ev.release();   // the watcher destroys them
+            if (!c->watcher.joinable())
+                c->watcher = std::thread(watch, c);
+        }
         c->cv.notify_all();
         return vktNoError;
+    }
+
+    // Entry points that enqueue a round return after finishLaunch; with async execution off
+    // that is the compute stream drained, and the rounds are judged too (vktHipCommSynchronize),
+    // so a round that timed out or failed asynchronously fails the call that issued it, as the
+    // synchronous mode promises -- not a later comm call.
+    vktError finishRound(vktHipComm_t c, char const* name)
+    {
+        vktError const e = rt::finishLaunch(name);
+        if (e != vktNoError || rt::asyncExecution())
+            return e;
+        return vktHipCommSynchronize(c);
     }
 
     // Planes [a, b) of a view holding global planes [z0, z0 + v.dimZ).
@@ -483,13 +528,12 @@ vktError vktHipCommInitRank(vktHipComm_t* comm, int32_t nranks, vktHipCommId_t i
     VKT_HIP_TRY(hipSetDevice(rt::device()));   // the communicator lives on the library's device
     ncclUniqueId u;
     std::memcpy(u.internal, id.internal, sizeof(u.internal));
-    auto* c = new vktHipComm_impl;
-    ncclResult_t const r = rccl().commInitRank(&c->comm, nranks, u, rank);
+    ncclComm_t nc = nullptr;
+    ncclResult_t const r = rccl().commInitRank(&nc, nranks, u, rank);
     if (r != ncclSuccess)
-    {
-        delete c;
         return ncclFail("vktHipCommInitRank", r);
-    }
+    auto* c = new vktHipComm_impl;
+    c->comm.store(nc);
     c->rank = rank;
     c->nranks = nranks;
     c->device = rt::device();
@@ -531,7 +575,8 @@ vktError vktHipCommDestroy(vktHipComm_t comm)
     comm->cv.notify_all();
     if (comm->watcher.joinable())
         comm->watcher.join();
-    ncclResult_t const r = comm->aborted.load() || comm->comm == nullptr ? ncclSuccess : rccl().commDestroy(comm->comm);
+    ncclComm_t const nc = comm->comm.exchange(nullptr);
+    ncclResult_t const r = comm->aborted.load() || nc == nullptr ? ncclSuccess : rccl().commDestroy(nc);
     if (comm->stream != nullptr)
         (void)hipStreamDestroy(comm->stream);
     delete comm;
@@ -560,7 +605,7 @@ vktError vktHipSlabExchangeHalo(vktHipComm_t comm, vktHipVolumeView_t localSrc, 
         moves.push_back(m);
     }
     e = comm::rcclRound(comm, moves, rt::computeStream(), "vktHipSlabExchangeHalo");
-    return e != vktNoError ? e : rt::finishLaunch("SlabExchangeHalo_hip");
+    return e != vktNoError ? e : comm::finishRound(comm, "SlabExchangeHalo_hip");
 }
 
 vktError vktHipSlabExchangeHaloLocal(int32_t numSlabs, vktHipVolumeView_t const* localSrc, int32_t const* localZ0,
@@ -631,14 +676,22 @@ vktError vktHipSlabExchangeHaloPeer(int32_t numSlabs, vktHipVolumeView_t const* 
             return rt::computeStream();
         if (!streams[static_cast<size_t>(dev)])
         {
+            // cached only once it waits for the compute stream: a stream that could not be
+            // ordered after the kernels writing the source slabs is destroyed, never reused
             hipStream_t st = nullptr;
             if (rt::check(hipSetDevice(dev), "hipSetDevice") == vktNoError &&
                 rt::check(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate") == vktNoError)
             {
-                streams[static_cast<size_t>(dev)] = st;
-                owned[static_cast<size_t>(dev)] = 1;
-                if (rt::check(hipStreamWaitEvent(st, queued, 0), "hipStreamWaitEvent(peer copy)") != vktNoError)
+                if (rt::check(hipStreamWaitEvent(st, queued, 0), "hipStreamWaitEvent(peer copy)") == vktNoError)
+                {
+                    streams[static_cast<size_t>(dev)] = st;
+                    owned[static_cast<size_t>(dev)] = 1;
+                }
+                else
+                {
+                    (void)hipStreamDestroy(st);
                     st = nullptr;
+                }
             }
             (void)hipSetDevice(cur);
             return st;
@@ -718,7 +771,7 @@ vktError vktHipCommExchange(vktHipComm_t comm, int32_t peer, void const* sendBuf
         xs.push_back(comm::Xfer{peer, 0, static_cast<uint8_t*>(recvBuf), bytes});
     }
     vktError const e = comm::rcclRound(comm, xs, rt::computeStream(), "vktHipCommExchange");
-    return e != vktNoError ? e : rt::finishLaunch("CommExchange_hip");
+    return e != vktNoError ? e : comm::finishRound(comm, "CommExchange_hip");
 }
 
 vktError vktHipResampleSlabOverlapped(vktHipComm_t comm, vktHipVolumeView_t dst, vktHipVolumeView_t localSrc,
@@ -753,7 +806,7 @@ vktError vktHipResampleSlabOverlapped(vktHipComm_t comm, vktHipVolumeView_t dst,
     e = comm::overlappedResample(dst, localSrc, localZ0, comm->rank, comm->nranks, dstGlobalDimZ, srcGlobalDimZ, fm,
                                  needsNeighbours, receives, comm->stream,
                                  [&](hipStream_t side) { return comm::rcclRound(comm, moves, side, what); }, what);
-    return e != vktNoError ? e : rt::finishLaunch("ResampleSlabOverlapped_hip");
+    return e != vktNoError ? e : comm::finishRound(comm, "ResampleSlabOverlapped_hip");
 }
 
 vktError vktHipResampleSlabsOverlappedLocal(int32_t numSlabs, vktHipVolumeView_t const* dst,

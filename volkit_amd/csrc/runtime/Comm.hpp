@@ -32,12 +32,18 @@ struct vktHipComm_impl
         std::string what;
     };
 
-    ncclComm_t comm = nullptr;
+    std::atomic<ncclComm_t> comm{nullptr};   // nullptr once aborted
     int32_t rank = 0, nranks = 0;
     int device = 0;
     int64_t timeoutMs = 0;            // vktHipCommSetTimeout, VKT_COMM_TIMEOUT_MS; 0: no deadline
     hipStream_t stream = nullptr;     // the communicator's own stream (overlapped rounds), lazily
-    std::mutex m;                     // comm use (enqueue / abort), rounds, failure
+    // em: one enqueue (ncclGroupStart .. ncclGroupEnd + the round's bookkeeping) at a time, so
+    // rounds are issued and judged in order.  The watcher never blocks on it: a blocking
+    // ncclGroupEnd may wait for a peer that died, and the abort is what releases it -- the
+    // watcher aborts under em when the enqueue in flight lets go within kEnqueueGraceMs, and
+    // without it otherwise (comm.cpp watch()).
+    std::timed_mutex em;
+    std::mutex m;                     // rounds, failure, timeoutMs (never held across an RCCL call)
     std::condition_variable cv;
     std::deque<Round> rounds;         // enqueued, not yet judged (front: being judged)
     std::thread watcher;
@@ -77,6 +83,10 @@ namespace comm
     // every later call on the stream hanging (SURVEY §5 failure detection).  A call on an
     // aborted communicator fails at once.
     vktError rcclRound(vktHipComm_t comm, std::vector<Xfer> const& xs, hipStream_t stream, char const* what);
+
+    // rt::finishLaunch, then -- with async execution off -- vktHipCommSynchronize: a call that
+    // enqueued a round returns that round's failure (timeout, asynchronous RCCL error).
+    vktError finishRound(vktHipComm_t comm, char const* name);
 
     // A device-to-device copy on `stream` (the in-process transport: every slab of a
     // partition held by this process on the library's device).

@@ -601,6 +601,34 @@ namespace detail
         return rt::fail("Memcpy: unknown CopyKind");
     }
 
+    // The public copies (vktHipMemcpy, vkt::Memcpy / vktMemcpy) take caller pointers: the device
+    // side of each copy kind must be memory the device can address.  memcpyHip itself trusts its
+    // (library-allocated) pointers.  A pointer the HIP runtime does not track is refused here
+    // rather than handed to hipMemcpyAsync, which treats an untracked address as host memory
+    // and reads or writes it on the CPU (the r5a SIGSEGV).
+    vktError memcpyChecked(void* dst, void const* src, std::size_t size, CopyKind ck)
+    {
+        if (size == 0)
+            return vktNoError;
+        if (dst == nullptr || src == nullptr)
+            return rt::fail("Memcpy: null pointer");
+        bool const devDst = ck == CopyKind::HostToDevice || ck == CopyKind::DeviceToDevice;
+        bool const devSrc = ck == CopyKind::DeviceToHost || ck == CopyKind::DeviceToDevice;
+        if (devDst)
+        {
+            vktError const e = rt::requireDevicePointer(dst, size, "Memcpy: destination is not device memory");
+            if (e != vktNoError)
+                return e;
+        }
+        if (devSrc)
+        {
+            vktError const e = rt::requireDevicePointer(src, size, "Memcpy: source is not device memory");
+            if (e != vktNoError)
+                return e;
+        }
+        return memcpyHip(dst, src, size, ck);
+    }
+
     void* AllocateOn(std::size_t bytes, ExecutionPolicy const& owner)
     {
         if (bytes == 0)
@@ -853,8 +881,26 @@ void Allocate(void** ptr, std::size_t size)
 
 void Free(void* ptr) { detail::freeOn(ptr, GetThreadExecutionPolicy(), true); }
 
-void Memcpy(void* dst, void const* src, std::size_t size, CopyKind ck) { (void)detail::memcpyHip(dst, src, size, ck); }
+void Memcpy(void* dst, void const* src, std::size_t size, CopyKind ck) { (void)detail::memcpyChecked(dst, src, size, ck); }
 
+namespace
+{
+    // Host-resident buffers: a plain pattern copy, as MemsetRange_serial (reference
+    // src/vkt/Memory_serial.hpp:24-37).  This is buffer housekeeping of ManagedBuffer::fill,
+    // not one of the StructuredVolume algorithms.
+    void hostMemsetRange(void* dst, void const* src, std::size_t dstSize, std::size_t srcSize)
+    {
+        if (srcSize == 0 || dst == nullptr || src == nullptr)
+            return;
+        std::size_t n = dstSize / srcSize;
+        for (std::size_t i = 0; i < n; ++i)
+            std::memcpy(static_cast<char*>(dst) + i * srcSize, src, srcSize);
+    }
+} // namespace
+
+// The reference dispatches on the thread policy (src/vkt/Memory.cpp:77-80).  Under the GPU
+// policy the pattern kernel refuses a pointer the device cannot address (hipk::memsetRange ->
+// rt::requireDevicePointer) instead of faulting on it.
 void MemsetRange(void* dst, void const* src, std::size_t dstSize, std::size_t srcSize)
 {
     if (onGpu(GetThreadExecutionPolicy()))
@@ -862,15 +908,23 @@ void MemsetRange(void* dst, void const* src, std::size_t dstSize, std::size_t sr
         (void)hipk::memsetRange(dst, src, dstSize, srcSize);
         return;
     }
-    // Host-resident buffers (CPU policy): a plain pattern copy, as MemsetRange_serial
-    // (reference src/vkt/Memory_serial.hpp:24-37).  This is buffer housekeeping of
-    // ManagedBuffer::fill, not one of the StructuredVolume algorithms.
-    if (srcSize == 0)
-        return;
-    std::size_t n = dstSize / srcSize;
-    for (std::size_t i = 0; i < n; ++i)
-        std::memcpy(static_cast<char*>(dst) + i * srcSize, src, srcSize);
+    hostMemsetRange(dst, src, dstSize, srcSize);
 }
+
+namespace detail
+{
+    // ManagedBuffer<T>::fill (reference include/cpp/vkt/ManagedBuffer.hpp:252-258): the bytes
+    // are filled where they live.  After a failed migration (MigrateBuffer keeps the buffer in
+    // host memory under the GPU policy) that is the host pattern loop, not the pattern kernel.
+    void MemsetRangeOn(void* dst, void const* src, std::size_t dstSize, std::size_t srcSize,
+                       ExecutionPolicy const& owner)
+    {
+        if (onGpu(owner))
+            (void)hipk::memsetRange(dst, src, dstSize, srcSize);
+        else
+            hostMemsetRange(dst, src, dstSize, srcSize);
+    }
+} // detail
 
 } // vkt
 
@@ -900,6 +954,34 @@ namespace rt
             e = check(hipStreamWaitEvent(computeStream(), ev, 0), "hipStreamWaitEvent(compute)");
         (void)hipEventDestroy(ev);
         return e;
+    }
+
+    vktError requireDevicePointer(void const* p, std::size_t bytes, char const* what)
+    {
+        hipPointerAttribute_t a{};
+        hipError_t const err = hipPointerGetAttributes(&a, p);
+        if (err != hipSuccess)
+            (void)hipGetLastError();   // (untracked pointers: an error, not a sticky one)
+        bool const ok = err == hipSuccess &&
+                        (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged ||
+                         a.type == hipMemoryTypeUnified ||
+                         (a.type == hipMemoryTypeHost && a.devicePointer == p));
+        if (!ok)
+            return fail(what);
+        if (bytes > 0 && a.type == hipMemoryTypeDevice)
+        {
+            hipDeviceptr_t base = nullptr;
+            std::size_t size = 0;
+            if (hipMemGetAddressRange(&base, &size, const_cast<void*>(p)) == hipSuccess && base != nullptr)
+            {
+                auto const b = reinterpret_cast<uintptr_t>(base), q = reinterpret_cast<uintptr_t>(p);
+                if (q - b > size || bytes > size - (q - b))
+                    return fail(what);
+            }
+            else
+                (void)hipGetLastError();   // (VMM mappings: no range to check against)
+        }
+        return vktNoError;
     }
 } // rt
 } // vkt
@@ -944,7 +1026,7 @@ vktError vktHipReleaseCachedMemory(size_t* releasedBytes)
 
 vktError vktHipMemcpy(void* dst, void const* src, size_t size, vktCopyKind ck)
 {
-    return vkt::detail::memcpyHip(dst, src, size, static_cast<vkt::CopyKind>(ck));
+    return vkt::detail::memcpyChecked(dst, src, size, static_cast<vkt::CopyKind>(ck));
 }
 
 vktError vktHipSetPinnedHostAllocation(int32_t enable)

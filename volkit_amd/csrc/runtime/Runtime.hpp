@@ -149,6 +149,14 @@ namespace rt
     vktError copyStreamAfterCompute();
     vktError computeStreamAfterCopy();
 
+    // vktNoError when the device can address [p, p + bytes): HBM (hipMalloc, VMM, managed) or
+    // pinned host memory mapped at the same address.  Anything else -- pageable host memory, or
+    // an address the runtime does not track -- records `what` as the thread's last error and
+    // returns vktInvalidValue, before any kernel or copy is queued on it (no XNACK on this pool:
+    // a kernel on a pageable pointer is a memory-access fault).  A device range that runs past
+    // its allocation is refused the same way.
+    vktError requireDevicePointer(void const* p, std::size_t bytes, char const* what);
+
     // Device scratch for one backend call site, reused across calls (no per-call hipMalloc,
     // and no stream-ordered pool: hipMallocAsync blocks filled by an H2D copy were
     // intermittently seen stale by the next kernel on gfx950/ROCm 7.2 -- DESIGN.md §4.6).
@@ -179,6 +187,9 @@ namespace detail
 {
     // Copy with the stream ordering described in runtime/Memory.cpp.
     vktError memcpyHip(void* dst, void const* src, std::size_t size, CopyKind ck);
+    // memcpyHip after checking that the device side(s) of `ck` are device-addressable
+    // (rt::requireDevicePointer): the public copy entry points, which take caller pointers.
+    vktError memcpyChecked(void* dst, void const* src, std::size_t size, CopyKind ck);
 }
 } // vkt
 

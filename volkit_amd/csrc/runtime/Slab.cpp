@@ -376,7 +376,9 @@ namespace
             e = runPieces(a, op, dst[i], src, buf, pieces[i], first, last, off, value);
         }
         release();
-        return e != vktNoError ? e : rt::finishLaunch(what);
+        if (e != vktNoError)
+            return e;
+        return comm != nullptr ? comm::finishRound(comm, what) : rt::finishLaunch(what);
     }
 } // namespace
 } // namespace vkt
