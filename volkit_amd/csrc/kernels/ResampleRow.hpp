@@ -72,6 +72,11 @@ namespace hipk
         // optimistic gather: nonzero iff any rowChain byte is set (written by rowChainKernel);
         // the fix-up pass returns at once when it is 0 (the common case).  nullptr = scan.
         uint32_t const* anyChain;
+        // optimistic LDS gather (Float32 "Linear", any ratio): the passes that classify source
+        // rows write this call's `epoch` here when they flag one; the fix-up runs only if the word
+        // holds the epoch (no per-call zeroing: a stale equal value only costs a scan).
+        uint32_t* anyDirtyOut;
+        uint32_t epoch;
     };
 
     // Plane-layout launches are split into at most kMaxPlaneTasksPerLaunch one-wave workgroups
@@ -100,6 +105,16 @@ namespace hipk
         return (bits & 0x7F800000u) == 0x7F800000u || bits == 0x80000000u;
     }
 
+    // Run tables are read through the constant address space: with a wave-uniform index they
+    // become scalar loads (lgkmcnt), not vector loads whose s_waitcnt vmcnt(0) would also wait
+    // for every store the wave still has in flight (gfx950's vmcnt counts loads AND stores).
+    typedef __attribute__((address_space(4))) int32_t const ConstI32;
+    __device__ __forceinline__ Run loadRun(Run const* table, uint32_t i)
+    {
+        ConstI32* const p = (ConstI32*)table + 3u * i;
+        return Run{p[0], p[1], p[2]};
+    }
+
     __device__ __forceinline__ Run runY(ResampleArgs const& a, uint32_t i)
     {
         if (a.affY)
@@ -107,7 +122,7 @@ namespace hipk
             int32_t d0 = a.d0Y + a.daY * static_cast<int32_t>(i);
             return Run{a.s0Y + a.saY * static_cast<int32_t>(i), d0, d0 + a.dlY};
         }
-        return a.runsY[i];
+        return loadRun(a.runsY, i);
     }
 
     __device__ __forceinline__ Run runZ(ResampleArgs const& a, uint32_t i)
@@ -117,7 +132,7 @@ namespace hipk
             int32_t d0 = a.d0Z + a.daZ * static_cast<int32_t>(i);
             return Run{a.s0Z + a.saZ * static_cast<int32_t>(i), d0, d0 + a.dlZ};
         }
-        return a.runsZ[i];
+        return loadRun(a.runsZ, i);
     }
 
     template <int FS, int FD>

@@ -281,18 +281,23 @@ namespace comm
             bool ok = pollEvent(c, r.start, 0, err);
             // ... its transfers have one, counted from their start
             ok = ok && pollEvent(c, r.end, r.timeoutMs, err);
-            if (!ok)
             {
-                // the failure is known now: record it and refuse later rounds before the abort,
-                // which returns only once the communicator's queued work has left the GPU (its
-                // kernels exit on the abort flag)
+                // the failure is known now: record it, refuse later rounds and release the
+                // waiters (vktHipCommSynchronize) before the abort, which returns only once the
+                // communicator's queued work has left the GPU (its kernels exit on the abort flag)
+                std::lock_guard<std::mutex> g(c->m);
+                if (!ok)
                 {
-                    std::lock_guard<std::mutex> g(c->m);
                     if (c->failure.empty())
                         c->failure = r.what + ": " + err + " (communicator aborted)";
                     c->aborted.store(true);
                     VKT_LOG(rt::LogLevel::Error) << c->failure;
                 }
+                c->rounds.pop_front();
+            }
+            c->cv.notify_all();
+            if (!ok)
+            {
                 // An enqueue in flight finishes its RCCL calls on the comm before it goes (no
                 // use after the abort frees it) -- unless it is stuck in RCCL, when only the
                 // abort releases it.
@@ -302,11 +307,6 @@ namespace comm
                 if (quiet)
                     c->em.unlock();
             }
-            {
-                std::lock_guard<std::mutex> g(c->m);
-                c->rounds.pop_front();
-            }
-            c->cv.notify_all();
             (void)hipEventDestroy(r.start);
             (void)hipEventDestroy(r.end);
         }
