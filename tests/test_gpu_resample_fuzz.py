@@ -187,3 +187,25 @@ def test_resample_wide_workgroup_gather(g, o, block):
                 assert_codes_equal(out, ref, df, f"block={block} {sd}->{dd} {sf}->{df} fm={fm}")
     finally:
         lib.vktHipSetTuningKnob(b"resample.gather_block", -1)
+
+
+@pytest.mark.parametrize("pad", [1, 2])
+@pytest.mark.parametrize("prefetch", [0, 2])
+def test_resample_padded_lds_rows(g, o, pad, prefetch):
+    """Knob resample.lds_pad (round 6): staged rows with 16 B of padding after every 256 B
+    (UInt8 sources: 1; every format: 2), with and without the next-row prefetch -- the
+    PC_SHAPES cases (rows of 48 B to 4 KiB, 16-B multiples padded, others not) vs the oracle."""
+    from volkit_amd._lib import lib
+    rng = np.random.default_rng(500 + pad + prefetch)
+    assert lib.vktHipSetTuningKnob(b"resample.lds_pad", pad) == 0
+    assert lib.vktHipSetTuningKnob(b"resample.prefetch", prefetch) == 0
+    try:
+        for sd, dd, sf, df in PC_SHAPES + [((1024, 20, 9), (768, 25, 7), 4, 4), ((512, 9, 9), (700, 9, 9), 4, 4)]:
+            src = rand_codes(rng, sf, sd[::-1])
+            for fm in (0, 1):
+                out = g.resample(df, (0.0, 1.0), dd, sf, (0.0, 1.0), src, fm)
+                ref = o.resample(df, (0.0, 1.0), dd, sf, (0.0, 1.0), src, fm)
+                assert_codes_equal(out, ref, df, f"pad={pad} {sd}->{dd} {sf}->{df} fm={fm}")
+    finally:
+        lib.vktHipSetTuningKnob(b"resample.lds_pad", -1)
+        lib.vktHipSetTuningKnob(b"resample.prefetch", -1)

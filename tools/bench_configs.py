@@ -820,6 +820,23 @@ def main():
                 free(S, Rv)
         finally:
             lib.vktHipSetTuningKnob(b"resample.gather_block", -1)
+    if want("padab"):
+        # in-process A/B: padded LDS rows (knob resample.lds_pad 0 / 2) on the gather shapes
+        try:
+            for se, de, fmt in ((1024, 768, 4), (768, 1024, 4), (1000, 1024, 4), (1024, 768, 5), (768, 1024, 5),
+                                (768, 1024, 7), (1024, 768, 7)):
+                b = {4: 1, 5: 2, 7: 4}[fmt]
+                S = alloc((se,) * 3, fmt, seed=21)
+                Rv = alloc((de,) * 3, fmt)
+                for rep in range(2):
+                    for pad in (0, 2):
+                        lib.vktHipSetTuningKnob(b"resample.lds_pad", pad)
+                        ms = timed(lambda: lib.vktHipResample(Rv, S, 0), R)
+                        report(f"padab Resample {se}^3->{de}^3 fmt{fmt} Nearest [pad={pad}]", ms,
+                               resample_bytes((se,) * 3, (de,) * 3, b, b), de ** 3)
+                free(S, Rv)
+        finally:
+            lib.vktHipSetTuningKnob(b"resample.lds_pad", -1)
     if want("f32lin"):
         # Float32 "Linear" (optimistic gather + fix-up) against Nearest on the
         # gather ratios; Linear's bytes: every source row (the chain's neighbours are classified)

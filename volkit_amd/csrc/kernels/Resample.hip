@@ -212,7 +212,19 @@ namespace hipk
     // PREFETCH (knob resample.prefetch; rows <= 4 KiB, no chain / detect): a wave that loops over
     // tasks (the capped UInt8 grid) loads the NEXT task's source row into registers while it
     // gathers and stores the current one, instead of one load -> wait -> gather round trip per task.
-    template <int BPVS, int BPVD, bool CONV, bool CHAIN, bool DETECT = false, bool PREFETCH = false, int NT = kBlock>
+    // PAD (knob resample.lds_pad; 16-B multiple rows): 16 bytes of padding after every 256 bytes
+    // of a staged row, so the gather's per-lane reads -- lane l at source byte ~16 l r for a
+    // ratio r -- spread over the LDS banks (UInt8 1024 -> 768: a 5.33-dword lane stride hit
+    // each bank ~5 times per wave read; SQ_LDS_BANK_CONFLICT 85 M cycles per launch, 34 % of the
+    // wave cycles waiting on LDS, profiles/r06/u8gather.pmc.jsonl).
+    template <bool PAD>
+    __device__ __forceinline__ uint32_t padOff(uint32_t o)
+    {
+        return PAD ? o + ((o >> 8) << 4) : o;
+    }
+
+    template <int BPVS, int BPVD, bool CONV, bool CHAIN, bool DETECT = false, bool PREFETCH = false, int NT = kBlock,
+              bool PAD = false>
     __global__ __launch_bounds__(NT) void resampleGatherLdsKernel(ResampleArgs a, uint32_t slotBytes)
     {
         constexpr bool kPre = PREFETCH && !CHAIN && !DETECT;   // plain gathers only
@@ -260,7 +272,8 @@ namespace hipk
 #pragma unroll
                 for (int j = 0; j < kStage; ++j)
                     if (16u * lane + 1024u * j < rowBytes)
-                        reinterpret_cast<RowVec16*>(slot + rowChunk(16u * lane + 1024u * j, rowBytes))->v = pre[j];
+                        reinterpret_cast<RowVec16*>(slot + padOff<PAD>(rowChunk(16u * lane + 1024u * j, rowBytes)))->v =
+                            pre[j];
                 if (t + totalWaves < tasks)
                     loadRow(t + totalWaves);
             }
@@ -291,7 +304,7 @@ namespace hipk
 #pragma unroll
                 for (int j = 0; j < kStage; ++j)
                     if (o0 + 1024u * j < rowBytes)
-                        reinterpret_cast<RowVec16*>(slot + rowChunk(o0 + 1024u * j, rowBytes))->v = w[j];
+                        reinterpret_cast<RowVec16*>(slot + padOff<PAD>(rowChunk(o0 + 1024u * j, rowBytes)))->v = w[j];
                 if constexpr (DETECT)
                 {
 #pragma unroll
@@ -327,7 +340,9 @@ namespace hipk
 #pragma unroll
                     for (int j = 0; j < 4 && i + j < V; ++j)
                     {
-                        uint32_t const c = loadCode<BPVS>(slot, static_cast<uint64_t>(xs[j]));
+                        uint32_t const c =
+                            PAD ? loadCode<BPVS>(slot + padOff<true>(static_cast<uint32_t>(xs[j]) * BPVS), 0)
+                                : loadCode<BPVS>(slot, static_cast<uint64_t>(xs[j]));
                         code[i + j] = CONV ? convertCode<-1, -1>(c, a) : c;
                     }
                 }
@@ -1108,7 +1123,9 @@ namespace hipk
         uint64_t const rowBytes = static_cast<uint64_t>(b.sdx) * bs;
         uint64_t const xtBytes = (static_cast<uint64_t>(b.ddx) * 4 + 15) & ~uint64_t(15);
         // rows that are not 16-B multiples (>= 16 B) stage through rowChunk; slots stay 16-B aligned
-        uint64_t const slotBytes = (rowBytes + 15) & ~uint64_t(15);
+        int64_t const padKnob = rt::knob(rt::Knob::ResampleLdsPad);
+        bool const pad = rowBytes % 16 == 0 && (padKnob == 2 || (padKnob == 1 && bs == 1));
+        uint64_t const slotBytes = pad ? rowBytes + (rowBytes >> 8) * 16 : (rowBytes + 15) & ~uint64_t(15);
         uint64_t const lds = xtBytes + (kBlock / 64) * slotBytes;
         // wide workgroups (knob resample.gather_block = 512 / 1024 threads): one task per wave,
         // the x table staged once per 8 / 16 tasks, grid not capped -- no wave loops over tasks,
@@ -1146,31 +1163,13 @@ namespace hipk
         if (rowBytes < 16 || (rowBytes % 16 != 0 && rt::knob(rt::Knob::ResampleAnyRows) == 0) ||
             reinterpret_cast<uintptr_t>(b.src) % 16 != 0 || lds > 65536)
             return false;
-        // next-row prefetch (knob resample.prefetch): 1 (default) for 2-byte destinations, 2 for
-        // every destination, 0 off.  Measured (profiles/r05/gatherp.jsonl, in-process A/B): UInt16
-        // 1024^3 -> 768^3 0.378 -> 0.358 ms, 768^3 -> 1024^3 0.520 -> 0.517; UInt8 (the capped grid,
-        // waves over several tasks) LOST: 768^3 -> 1024^3 0.306 -> 0.38 ms, 1024^3 -> 768^3 0.244 -> 0.293
-        int64_t const pc = rt::knob(rt::Knob::ResamplePc);
-        if (pc > 0 && !detect && !chain && rowBytes <= 4096)
-        {
-            constexpr uint64_t kS = kBlock / 64 - 1;
-            uint64_t const ldsPc = xtBytes + 2 * kS * slotBytes;
-            if (ldsPc <= 65536)
-            {
-                uint64_t groups = (tasks + kS - 1) / kS;
-                uint64_t const cap = static_cast<uint64_t>(pc) * 1024;
-                unsigned const gp = static_cast<unsigned>(groups < cap ? groups : cap);
-                uint32_t const slotp = static_cast<uint32_t>(slotBytes);
-#define VKT_PC(S, D, C) hipLaunchKernelGGL((resampleGatherPcKernel<S, D, C>), dim3(gp), dim3(kBlock), ldsPc, s, b, slotp)
-#define VKT_PC_D(S, C) do { if (bd == 1) VKT_PC(S, 1, C); else if (bd == 2) VKT_PC(S, 2, C); else VKT_PC(S, 4, C); } while (0)
-#define VKT_PC_S(C) do { if (bs == 1) VKT_PC_D(1, C); else if (bs == 2) VKT_PC_D(2, C); else VKT_PC_D(4, C); } while (0)
-                if (identity) VKT_PC_S(false); else VKT_PC_S(true);
-#undef VKT_PC_S
-#undef VKT_PC_D
-#undef VKT_PC
-                return true;
-            }
-        }
+        // next-row prefetch (knob resample.prefetch): 1 for 2-byte destinations, 2 for every
+        // destination, 0 (default since round 6) off.  Round 5 (profiles/r05/gatherp.jsonl): UInt16
+        // 1024^3 -> 768^3 0.378 -> 0.358 ms with it, UInt8 lost.  Round 6, after the run tables
+        // moved to scalar loads (profiles/r06/gatherp.jsonl): UInt16 1024^3 -> 768^3 0.343-0.346 ms
+        // without vs 0.354-0.356 with, 768^3 -> 1024^3 0.500-0.503 vs 0.507-0.508; UInt8 equal.
+        // The prefetched row's wait is a vmcnt(0) behind the task's stores either way (the store
+        // count per task is not a compile-time constant).
         int64_t const pk = rt::knob(rt::Knob::ResamplePrefetch);
         bool const prefetch = (pk == 2 || (pk == 1 && bd == 2)) && !detect && !chain && rowBytes <= 4096;
         // one task per wave; for 1-byte destinations a task writes so little (one 1-KiB store
@@ -1184,7 +1183,16 @@ namespace hipk
         uint32_t const slot = static_cast<uint32_t>(slotBytes);
 #define VKT_GL(S, D, C, H)                                                                                         \
     do {                                                                                                           \
-        if (prefetch && !(H))   /* (a chain instance with PREFETCH compiles as the plain one) */                  \
+        if (pad && !(H))                                                                                           \
+        {                                                                                                          \
+            if (prefetch)                                                                                          \
+                hipLaunchKernelGGL((resampleGatherLdsKernel<S, D, C, false, false, true, kBlock, true>), dim3(g),  \
+                                   dim3(kBlock), lds, s, b, slot);                                                \
+            else                                                                                                   \
+                hipLaunchKernelGGL((resampleGatherLdsKernel<S, D, C, false, false, false, kBlock, true>), dim3(g), \
+                                   dim3(kBlock), lds, s, b, slot);                                                \
+        }                                                                                                          \
+        else if (prefetch && !(H))   /* (a chain instance with PREFETCH compiles as the plain one) */             \
             hipLaunchKernelGGL((resampleGatherLdsKernel<S, D, C, H, false, true>), dim3(g), dim3(kBlock), lds, s, b, \
                                slot);                                                                              \
         else                                                                                                       \
