@@ -209,3 +209,22 @@ def test_resample_padded_lds_rows(g, o, pad, prefetch):
     finally:
         lib.vktHipSetTuningKnob(b"resample.lds_pad", -1)
         lib.vktHipSetTuningKnob(b"resample.prefetch", -1)
+
+
+@pytest.mark.parametrize("rpw", [2, 4])
+def test_resample_rows_per_wave_gather(g, o, rpw):
+    """Knob resample.rows_per_wave (round 6): the LDS gather staging 2 / 4 tasks' rows per wave
+    iteration (resampleGatherLdsMultiKernel), padded UInt8 rows included -- the PC_SHAPES cases plus
+    task counts that are not multiples of the group size, vs the oracle."""
+    from volkit_amd._lib import lib
+    rng = np.random.default_rng(600 + rpw)
+    assert lib.vktHipSetTuningKnob(b"resample.rows_per_wave", rpw) == 0
+    try:
+        for sd, dd, sf, df in PC_SHAPES + [((1024, 7, 3), (768, 9, 5), 4, 4), ((256, 5, 7), (300, 7, 9), 4, 4)]:
+            src = rand_codes(rng, sf, sd[::-1])
+            for fm in (0, 1):
+                out = g.resample(df, (0.0, 1.0), dd, sf, (0.0, 1.0), src, fm)
+                ref = o.resample(df, (0.0, 1.0), dd, sf, (0.0, 1.0), src, fm)
+                assert_codes_equal(out, ref, df, f"rpw={rpw} {sd}->{dd} {sf}->{df} fm={fm}")
+    finally:
+        lib.vktHipSetTuningKnob(b"resample.rows_per_wave", -1)

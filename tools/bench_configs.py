@@ -837,6 +837,23 @@ def main():
                 free(S, Rv)
         finally:
             lib.vktHipSetTuningKnob(b"resample.lds_pad", -1)
+    if want("rpwab"):
+        # in-process A/B: rows staged per wave iteration (knob resample.rows_per_wave 0 / 2 / 4)
+        try:
+            for se, de, fmt in ((1024, 768, 4), (768, 1024, 4), (1000, 1024, 4), (1024, 768, 5), (768, 1024, 5),
+                                (1000, 1024, 5), (768, 1024, 7)):
+                b = {4: 1, 5: 2, 7: 4}[fmt]
+                S = alloc((se,) * 3, fmt, seed=21)
+                Rv = alloc((de,) * 3, fmt)
+                for rep in range(2):
+                    for rpw in (0, 2, 4):
+                        lib.vktHipSetTuningKnob(b"resample.rows_per_wave", rpw)
+                        ms = timed(lambda: lib.vktHipResample(Rv, S, 0), R)
+                        report(f"rpwab Resample {se}^3->{de}^3 fmt{fmt} Nearest [rpw={rpw}]", ms,
+                               resample_bytes((se,) * 3, (de,) * 3, b, b), de ** 3)
+                free(S, Rv)
+        finally:
+            lib.vktHipSetTuningKnob(b"resample.rows_per_wave", -1)
     if want("f32lin"):
         # Float32 "Linear" (optimistic gather + fix-up) against Nearest on the
         # gather ratios; Linear's bytes: every source row (the chain's neighbours are classified)

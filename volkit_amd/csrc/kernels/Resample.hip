@@ -357,6 +357,99 @@ namespace hipk
         }
     }
 
+    // ---- LDS gather, R rows per wave iteration (round 6, knob resample.rows_per_wave) ------------
+    // resampleGatherLdsKernel's plain gather with R consecutive tasks staged per iteration: all R
+    // rows' loads in flight before the first LDS write, so a wave that loops over tasks pays one
+    // load round trip -- and one wait behind its previous stores (vmcnt counts both) -- per R
+    // tasks instead of per task.  Rows <= 4 KiB.
+    template <int BPVS, int BPVD, bool CONV, int R, bool PAD>
+    __global__ __launch_bounds__(kBlock) void resampleGatherLdsMultiKernel(ResampleArgs a, uint32_t slotBytes)
+    {
+        constexpr int V = 16 / BPVD;
+        constexpr int kStage = 4;
+        extern __shared__ u32x4 ldsRaw[];
+        uint8_t* const lds = reinterpret_cast<uint8_t*>(ldsRaw);
+        int32_t* const xt = reinterpret_cast<int32_t*>(lds);
+        uint32_t const xtBytes = (static_cast<uint32_t>(a.ddx) * 4u + 15u) & ~15u;
+        int const lane = threadIdx.x & 63;
+        uint32_t const wib = threadIdx.x >> 6;
+        uint8_t* const slots = lds + xtBytes + wib * R * slotBytes;
+        for (uint32_t i = threadIdx.x * 4; i < static_cast<uint32_t>(a.ddx); i += kBlock * 4)
+            *reinterpret_cast<u32x4*>(xt + i) = *reinterpret_cast<u32x4 const*>(a.xtab + i);
+        __syncthreads();
+
+        uint32_t const wave = __builtin_amdgcn_readfirstlane(xcdSwizzle(blockIdx.x, gridDim.x) * (kBlock / 64) + wib);
+        uint32_t const totalWaves = gridDim.x * (kBlock / 64);
+        uint32_t const nY = static_cast<uint32_t>(a.nRunsY);
+        uint32_t const tasks = nY * static_cast<uint32_t>(a.nRunsZ);
+        uint32_t const groups = (tasks + R - 1) / R;
+        uint32_t const rowBytes = static_cast<uint32_t>(a.sdx) * BPVS;
+        bool const aligned = rowBytes % 16u == 0u;
+        for (uint32_t g = wave; g < groups; g += totalWaves)
+        {
+            Run ry[R], rz[R];
+            u32x4 w[R][kStage];
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+            {
+                uint32_t const t = g * R + r < tasks ? g * R + r : g * R;
+                ry[r] = runY(a, t % nY);
+                rz[r] = runZ(a, t / nY);
+                uint8_t const* const p = a.src + srcRowIndex(a, ry[r].s, rz[r].s) * BPVS;
+#pragma unroll
+                for (int j = 0; j < kStage; ++j)
+                    if (16u * lane + 1024u * j < rowBytes)
+                    {
+                        uint32_t const oc = rowChunk(16u * lane + 1024u * j, rowBytes);
+                        w[r][j] = aligned ? __builtin_nontemporal_load(reinterpret_cast<u32x4 const*>(p + oc))
+                                          : reinterpret_cast<RowVec16 const*>(p + oc)->v;
+                    }
+            }
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+#pragma unroll
+                for (int j = 0; j < kStage; ++j)
+                    if (16u * lane + 1024u * j < rowBytes)
+                        reinterpret_cast<RowVec16*>(slots + r * slotBytes +
+                                                    padOff<PAD>(rowChunk(16u * lane + 1024u * j, rowBytes)))->v = w[r][j];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+            {
+                if (g * R + r >= tasks)
+                    break;
+                uint8_t const* const slot = slots + r * slotBytes;
+                for (int32_t dx = V * lane; dx < a.ddx; dx += 64 * V)
+                {
+                    uint32_t code[V];
+#pragma unroll
+                    for (int i = 0; i < V; i += 4)
+                    {
+                        u32x4 const q = *reinterpret_cast<u32x4 const*>(xt + dx + i);
+                        int32_t const xs[4] = {static_cast<int32_t>(q.x), static_cast<int32_t>(q.y),
+                                               static_cast<int32_t>(q.z), static_cast<int32_t>(q.w)};
+#pragma unroll
+                        for (int j = 0; j < 4 && i + j < V; ++j)
+                        {
+                            uint32_t const c =
+                                PAD ? loadCode<BPVS>(slot + padOff<true>(static_cast<uint32_t>(xs[j]) * BPVS), 0)
+                                    : loadCode<BPVS>(slot, static_cast<uint64_t>(xs[j]));
+                            code[i + j] = CONV ? convertCode<-1, -1>(c, a) : c;
+                        }
+                    }
+                    for (int32_t zd = rz[r].d0; zd < rz[r].d1; ++zd)
+                        for (int32_t yd = ry[r].d0; yd < ry[r].d1; ++yd)
+                            store16<BPVD>(a.dst, dstRowIndex(a, yd, zd) + static_cast<uint64_t>(dx), code);
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+    }
+
     // ---- LDS gather with a loader wave (round 6, knob resample.pc) --------------------------
     // gfx950's vmcnt counts a wave's loads AND stores, so in resampleGatherLdsKernel every task's
     // row load -- `s_waitcnt vmcnt(0)` before its LDS write -- also waits until the PREVIOUS
@@ -1170,6 +1263,38 @@ namespace hipk
         // without vs 0.354-0.356 with, 768^3 -> 1024^3 0.500-0.503 vs 0.507-0.508; UInt8 equal.
         // The prefetched row's wait is a vmcnt(0) behind the task's stores either way (the store
         // count per task is not a compile-time constant).
+        int64_t const rpw = rt::knob(rt::Knob::ResampleRowsPerWave);
+        if ((rpw == 2 || rpw == 4) && !detect && !chain && rowBytes <= 4096)
+        {
+            uint64_t const ldsM = xtBytes + (kBlock / 64) * static_cast<uint64_t>(rpw) * slotBytes;
+            if (ldsM <= 65536)
+            {
+                uint64_t const groups = (tasks + rpw - 1) / rpw;
+                uint64_t blocksM = (groups + 3) / 4;
+                if (bd == 1 && blocksM > 16384)
+                    blocksM = 16384;
+                unsigned const gm = static_cast<unsigned>(blocksM < (1u << 30) ? blocksM : (1u << 30));
+                uint32_t const slotm = static_cast<uint32_t>(slotBytes);
+#define VKT_GM(S, D, C, RR)                                                                                      \
+    do {                                                                                                         \
+        if (pad)                                                                                                 \
+            hipLaunchKernelGGL((resampleGatherLdsMultiKernel<S, D, C, RR, true>), dim3(gm), dim3(kBlock), ldsM, s, b, \
+                               slotm);                                                                           \
+        else                                                                                                     \
+            hipLaunchKernelGGL((resampleGatherLdsMultiKernel<S, D, C, RR, false>), dim3(gm), dim3(kBlock), ldsM, s, \
+                               b, slotm);                                                                        \
+    } while (0)
+#define VKT_GM_R(S, D, C) do { if (rpw == 2) VKT_GM(S, D, C, 2); else VKT_GM(S, D, C, 4); } while (0)
+#define VKT_GM_D(S, C) do { if (bd == 1) VKT_GM_R(S, 1, C); else if (bd == 2) VKT_GM_R(S, 2, C); else VKT_GM_R(S, 4, C); } while (0)
+#define VKT_GM_S(C) do { if (bs == 1) VKT_GM_D(1, C); else if (bs == 2) VKT_GM_D(2, C); else VKT_GM_D(4, C); } while (0)
+                if (identity) VKT_GM_S(false); else VKT_GM_S(true);
+#undef VKT_GM_S
+#undef VKT_GM_D
+#undef VKT_GM_R
+#undef VKT_GM
+                return true;
+            }
+        }
         int64_t const pk = rt::knob(rt::Knob::ResamplePrefetch);
         bool const prefetch = (pk == 2 || (pk == 1 && bd == 2)) && !detect && !chain && rowBytes <= 4096;
         // one task per wave; for 1-byte destinations a task writes so little (one 1-KiB store

@@ -141,6 +141,7 @@ namespace rt
         ResamplePc,                    // LDS gathers: > 0 the loader-wave kernel (resampleGatherPcKernel; grid cap in 1024s of workgroups)
         ResampleGatherBlock,           // LDS gathers: 512 / 1024 = threads per workgroup, one task per wave, grid not capped (0: 256, UInt8 capped)
         ResampleLdsPad,                // LDS gathers: 16 B of padding per 256 B of a staged row (bank spread): 1 UInt8 sources, 2 all, 0 none
+        ResampleRowsPerWave,           // LDS gathers: 2 / 4 = tasks staged per wave iteration (resampleGatherLdsMultiKernel), 0 = one
         Count
     };
     int64_t knob(Knob k);
