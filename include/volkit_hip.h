@@ -131,7 +131,12 @@ VKTAPI vktError vktHipKernelScopeEnd(vktHipKernelScope scope);
  * output item from them instead of scattering source words into the brick layout),
  * "decompose.pipe" (0; 1 runs uniform brick grids on a resident grid that loads chunk k + 1 while
  * it stores chunk k instead of one workgroup per 16-KiB chunk), "decompose.pair" (0; 1 copies
- * two x-neighbour bricks of at most 16 KiB per workgroup from one staging of their rows' union).
+ * two x-neighbour bricks of at most 16 KiB per workgroup from one staging of their rows' union),
+ * "resample.prefetch" (0; 1 / 2: the LDS gather loads the next task's source row during the current
+ * one for 2-byte / every destination), "resample.any_rows" (1; 0 sends source rows that are not
+ * 16-B multiples to the per-voxel gather), "resample.lds_pad" (1; staged LDS rows get 16 B of
+ * padding per 256 B -- LDS bank spread -- for UInt8 sources; 2 for every format, 0 none).
+ * The full list with defaults: volkit_amd/csrc/runtime/HipContext.cpp (kKnobs).
  * For tests and in-process A/B measurements; unknown names return
  * vktInvalidValue.
  *

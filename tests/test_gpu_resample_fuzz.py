@@ -100,44 +100,6 @@ def test_resample_gather_rows_not_16_byte_multiples(g, o, sd, dd, sf, df, anyrow
         lib.vktHipSetTuningKnob(b"resample.any_rows", -1)
 
 
-U8_WINDOW_SHAPES = [
-    ((48, 40, 24), (64, 52, 30)),      # up 4/3: two-dword windows, 4 of 64 lanes store
-    ((64, 40, 24), (48, 30, 20)),      # down 4/3
-    ((1000, 6, 5), (1024, 7, 6)),      # one full group, odd ratio
-    ((700, 5, 4), (1536, 6, 5)),       # two groups (G = 2), the second partial
-    ((100, 7, 9), (80, 9, 7)),         # down 5/4
-    ((36, 4, 4), (16, 5, 3)),          # down 9/4: three-dword windows or the LDS fallback
-    ((8, 3, 3), (16, 5, 5)),           # the shortest row the window takes (2 dwords, clamped)
-    ((12, 3, 3), (32, 4, 4)),
-]
-
-
-@pytest.mark.parametrize("cap", [1, 16])
-@pytest.mark.parametrize("pre", [1, 0])
-def test_resample_u8_register_window_gather(g, o, cap, pre):
-    """Knob resample.u8_direct (round 6): UInt8 -> UInt8 gathers without LDS -- each lane's x
-    windows and v_perm selectors derived once, per task dword-aligned window loads from the
-    source row, 16-B stores -- vs the oracle: up / down ratios, one and two 1024-voxel groups,
-    inactive lanes, rows of 8 and 12 bytes (windows clamped into the row), identity and a
-    mapping conversion (CONV), a 1024-workgroup grid (waves loop over many tasks, cap 1) and the
-    16 K grid, with and without the next-task prefetch (knob resample.prefetch)."""
-    from volkit_amd._lib import lib
-    rng = np.random.default_rng(90 + cap + pre)
-    assert lib.vktHipSetTuningKnob(b"resample.u8_direct", cap) == 0
-    assert lib.vktHipSetTuningKnob(b"resample.prefetch", pre) == 0
-    try:
-        for sd, dd in U8_WINDOW_SHAPES:
-            src = rand_codes(rng, 4, sd[::-1])
-            for dmap in ((0.0, 1.0), (-1.0, 3.0)):
-                for fm in (0, 1):
-                    out = g.resample(4, dmap, dd, 4, (0.0, 1.0), src, fm)
-                    ref = o.resample(4, dmap, dd, 4, (0.0, 1.0), src, fm)
-                    assert_codes_equal(out, ref, 4, f"u8 window {sd}->{dd} dmap={dmap} fm={fm}")
-    finally:
-        lib.vktHipSetTuningKnob(b"resample.u8_direct", -1)
-        lib.vktHipSetTuningKnob(b"resample.prefetch", -1)
-
-
 PC_SHAPES = [
     ((48, 40, 24), (64, 52, 30), 4, 4),
     ((64, 40, 24), (48, 30, 20), 4, 4),
@@ -149,44 +111,6 @@ PC_SHAPES = [
     ((1024, 3, 4), (768, 5, 3), 5, 5),         # 2-KiB rows, several chunks per lane
     ((1024, 3, 4), (1500, 5, 3), 7, 7),        # 4-KiB rows
 ]
-
-
-@pytest.mark.parametrize("cap", [1, 64])
-def test_resample_loader_wave_gather(g, o, cap):
-    """Knob resample.pc (round 6): the LDS gather with one loader wave and three storer waves per
-    workgroup over a double-buffered LDS ring (resampleGatherPcKernel) vs the oracle -- UInt8 /
-    UInt16 / Float32 and a conversion, up / down ratios, rows that are not 16-B multiples, rows of
-    up to 4 KiB, a small grid (cap 1: workgroups loop over many stages) and a large one."""
-    from volkit_amd._lib import lib
-    rng = np.random.default_rng(300 + cap)
-    assert lib.vktHipSetTuningKnob(b"resample.pc", cap) == 0
-    try:
-        for sd, dd, sf, df in PC_SHAPES:
-            src = rand_codes(rng, sf, sd[::-1])
-            for fm in (0, 1):
-                out = g.resample(df, (0.0, 1.0), dd, sf, (0.0, 1.0), src, fm)
-                ref = o.resample(df, (0.0, 1.0), dd, sf, (0.0, 1.0), src, fm)
-                assert_codes_equal(out, ref, df, f"pc {sd}->{dd} {sf}->{df} fm={fm}")
-    finally:
-        lib.vktHipSetTuningKnob(b"resample.pc", -1)
-
-
-@pytest.mark.parametrize("block", [512, 1024])
-def test_resample_wide_workgroup_gather(g, o, block):
-    """Knob resample.gather_block (round 6): the LDS gather in 512 / 1024-thread workgroups, one
-    task per wave, grid not capped -- the PC_SHAPES cases vs the oracle."""
-    from volkit_amd._lib import lib
-    rng = np.random.default_rng(400 + block)
-    assert lib.vktHipSetTuningKnob(b"resample.gather_block", block) == 0
-    try:
-        for sd, dd, sf, df in PC_SHAPES:
-            src = rand_codes(rng, sf, sd[::-1])
-            for fm in (0, 1):
-                out = g.resample(df, (0.0, 1.0), dd, sf, (0.0, 1.0), src, fm)
-                ref = o.resample(df, (0.0, 1.0), dd, sf, (0.0, 1.0), src, fm)
-                assert_codes_equal(out, ref, df, f"block={block} {sd}->{dd} {sf}->{df} fm={fm}")
-    finally:
-        lib.vktHipSetTuningKnob(b"resample.gather_block", -1)
 
 
 @pytest.mark.parametrize("pad", [1, 2])
@@ -209,22 +133,3 @@ def test_resample_padded_lds_rows(g, o, pad, prefetch):
     finally:
         lib.vktHipSetTuningKnob(b"resample.lds_pad", -1)
         lib.vktHipSetTuningKnob(b"resample.prefetch", -1)
-
-
-@pytest.mark.parametrize("rpw", [2, 4])
-def test_resample_rows_per_wave_gather(g, o, rpw):
-    """Knob resample.rows_per_wave (round 6): the LDS gather staging 2 / 4 tasks' rows per wave
-    iteration (resampleGatherLdsMultiKernel), padded UInt8 rows included -- the PC_SHAPES cases plus
-    task counts that are not multiples of the group size, vs the oracle."""
-    from volkit_amd._lib import lib
-    rng = np.random.default_rng(600 + rpw)
-    assert lib.vktHipSetTuningKnob(b"resample.rows_per_wave", rpw) == 0
-    try:
-        for sd, dd, sf, df in PC_SHAPES + [((1024, 7, 3), (768, 9, 5), 4, 4), ((256, 5, 7), (300, 7, 9), 4, 4)]:
-            src = rand_codes(rng, sf, sd[::-1])
-            for fm in (0, 1):
-                out = g.resample(df, (0.0, 1.0), dd, sf, (0.0, 1.0), src, fm)
-                ref = o.resample(df, (0.0, 1.0), dd, sf, (0.0, 1.0), src, fm)
-                assert_codes_equal(out, ref, df, f"rpw={rpw} {sd}->{dd} {sf}->{df} fm={fm}")
-    finally:
-        lib.vktHipSetTuningKnob(b"resample.rows_per_wave", -1)

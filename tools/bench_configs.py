@@ -762,64 +762,6 @@ def main():
             report(f"u8gather Resample {se}^3->{de}^3 fmt{fmt} Linear", ms,
                    resample_bytes((se,) * 3, (de,) * 3, b, b), de ** 3)
             free(S, Rv)
-    if want("u8win"):
-        # in-process A/B of the UInt8 register-window gather (knob resample.u8_direct = grid cap
-        # in 1024s of workgroups, 0 = the LDS gather) x next-task prefetch (resample.prefetch)
-        variants = [(0, 1), (16, 0), (16, 1), (4, 1), (64, 1), (1024, 1)]
-        if os.environ.get("VKT_U8WIN"):   # "cap:pre;..."
-            variants = [tuple(int(x) for x in v.split(":")) for v in os.environ["VKT_U8WIN"].split(";")]
-        try:
-            for se, de in ((1024, 768), (768, 1024), (1000, 1024)):
-                S = alloc((se,) * 3, 4, seed=21)
-                Rv = alloc((de,) * 3, 4)
-                for rep in range(2):
-                    for cap, pre in variants:
-                        lib.vktHipSetTuningKnob(b"resample.u8_direct", cap)
-                        lib.vktHipSetTuningKnob(b"resample.prefetch", pre if cap else -1)
-                        ms = timed(lambda: lib.vktHipResample(Rv, S, 1), R)
-                        report(f"u8win Resample {se}^3->{de}^3 UInt8 Linear [direct={cap} pre={pre}]", ms,
-                               resample_bytes((se,) * 3, (de,) * 3, 1, 1), de ** 3)
-                free(S, Rv)
-        finally:
-            lib.vktHipSetTuningKnob(b"resample.u8_direct", -1)
-            lib.vktHipSetTuningKnob(b"resample.prefetch", -1)
-    if want("pcab"):
-        # in-process A/B of the loader-wave LDS gather (knob resample.pc = grid cap in 1024s of
-        # workgroups, 0 = resampleGatherLdsKernel)
-        caps = [int(c) for c in os.environ.get("VKT_PC_CAPS", "0,2,4,8,16").split(",")]
-        try:
-            for se, de, fmt in ((1024, 768, 4), (768, 1024, 4), (1000, 1024, 4), (1024, 768, 5), (768, 1024, 5),
-                                (768, 1024, 7)):
-                b = {4: 1, 5: 2, 7: 4}[fmt]
-                S = alloc((se,) * 3, fmt, seed=21)
-                Rv = alloc((de,) * 3, fmt)
-                for rep in range(2):
-                    for cap in caps:
-                        lib.vktHipSetTuningKnob(b"resample.pc", cap)
-                        ms = timed(lambda: lib.vktHipResample(Rv, S, 0), R)
-                        report(f"pcab Resample {se}^3->{de}^3 fmt{fmt} Nearest [pc={cap}]", ms,
-                               resample_bytes((se,) * 3, (de,) * 3, b, b), de ** 3)
-                free(S, Rv)
-        finally:
-            lib.vktHipSetTuningKnob(b"resample.pc", -1)
-    if want("wgab"):
-        # in-process A/B: the LDS gather with 256-thread workgroups (UInt8: capped grid, waves loop
-        # over tasks) vs 512 / 1024-thread ones (one task per wave, knob resample.gather_block)
-        try:
-            for se, de, fmt in ((1024, 768, 4), (768, 1024, 4), (1000, 1024, 4), (1024, 768, 5), (768, 1024, 5),
-                                (1000, 1024, 5), (768, 1024, 7)):
-                b = {4: 1, 5: 2, 7: 4}[fmt]
-                S = alloc((se,) * 3, fmt, seed=21)
-                Rv = alloc((de,) * 3, fmt)
-                for rep in range(2):
-                    for wb in (0, 512, 1024):
-                        lib.vktHipSetTuningKnob(b"resample.gather_block", wb)
-                        ms = timed(lambda: lib.vktHipResample(Rv, S, 0), R)
-                        report(f"wgab Resample {se}^3->{de}^3 fmt{fmt} Nearest [block={wb}]", ms,
-                               resample_bytes((se,) * 3, (de,) * 3, b, b), de ** 3)
-                free(S, Rv)
-        finally:
-            lib.vktHipSetTuningKnob(b"resample.gather_block", -1)
     if want("padab"):
         # in-process A/B: padded LDS rows (knob resample.lds_pad 0 / 2) on the gather shapes
         try:
@@ -837,23 +779,6 @@ def main():
                 free(S, Rv)
         finally:
             lib.vktHipSetTuningKnob(b"resample.lds_pad", -1)
-    if want("rpwab"):
-        # in-process A/B: rows staged per wave iteration (knob resample.rows_per_wave 0 / 2 / 4)
-        try:
-            for se, de, fmt in ((1024, 768, 4), (768, 1024, 4), (1000, 1024, 4), (1024, 768, 5), (768, 1024, 5),
-                                (1000, 1024, 5), (768, 1024, 7)):
-                b = {4: 1, 5: 2, 7: 4}[fmt]
-                S = alloc((se,) * 3, fmt, seed=21)
-                Rv = alloc((de,) * 3, fmt)
-                for rep in range(2):
-                    for rpw in (0, 2, 4):
-                        lib.vktHipSetTuningKnob(b"resample.rows_per_wave", rpw)
-                        ms = timed(lambda: lib.vktHipResample(Rv, S, 0), R)
-                        report(f"rpwab Resample {se}^3->{de}^3 fmt{fmt} Nearest [rpw={rpw}]", ms,
-                               resample_bytes((se,) * 3, (de,) * 3, b, b), de ** 3)
-                free(S, Rv)
-        finally:
-            lib.vktHipSetTuningKnob(b"resample.rows_per_wave", -1)
     if want("f32lin"):
         # Float32 "Linear" (optimistic gather + fix-up) against Nearest on the
         # gather ratios; Linear's bytes: every source row (the chain's neighbours are classified)

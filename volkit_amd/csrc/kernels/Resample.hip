@@ -357,364 +357,6 @@ namespace hipk
         }
     }
 
-    // ---- LDS gather, R rows per wave iteration (round 6, knob resample.rows_per_wave) ------------
-    // resampleGatherLdsKernel's plain gather with R consecutive tasks staged per iteration: all R
-    // rows' loads in flight before the first LDS write, so a wave that loops over tasks pays one
-    // load round trip -- and one wait behind its previous stores (vmcnt counts both) -- per R
-    // tasks instead of per task.  Rows <= 4 KiB.
-    template <int BPVS, int BPVD, bool CONV, int R, bool PAD>
-    __global__ __launch_bounds__(kBlock) void resampleGatherLdsMultiKernel(ResampleArgs a, uint32_t slotBytes)
-    {
-        constexpr int V = 16 / BPVD;
-        constexpr int kStage = 4;
-        extern __shared__ u32x4 ldsRaw[];
-        uint8_t* const lds = reinterpret_cast<uint8_t*>(ldsRaw);
-        int32_t* const xt = reinterpret_cast<int32_t*>(lds);
-        uint32_t const xtBytes = (static_cast<uint32_t>(a.ddx) * 4u + 15u) & ~15u;
-        int const lane = threadIdx.x & 63;
-        uint32_t const wib = threadIdx.x >> 6;
-        uint8_t* const slots = lds + xtBytes + wib * R * slotBytes;
-        for (uint32_t i = threadIdx.x * 4; i < static_cast<uint32_t>(a.ddx); i += kBlock * 4)
-            *reinterpret_cast<u32x4*>(xt + i) = *reinterpret_cast<u32x4 const*>(a.xtab + i);
-        __syncthreads();
-
-        uint32_t const wave = __builtin_amdgcn_readfirstlane(xcdSwizzle(blockIdx.x, gridDim.x) * (kBlock / 64) + wib);
-        uint32_t const totalWaves = gridDim.x * (kBlock / 64);
-        uint32_t const nY = static_cast<uint32_t>(a.nRunsY);
-        uint32_t const tasks = nY * static_cast<uint32_t>(a.nRunsZ);
-        uint32_t const groups = (tasks + R - 1) / R;
-        uint32_t const rowBytes = static_cast<uint32_t>(a.sdx) * BPVS;
-        bool const aligned = rowBytes % 16u == 0u;
-        for (uint32_t g = wave; g < groups; g += totalWaves)
-        {
-            Run ry[R], rz[R];
-            u32x4 w[R][kStage];
-#pragma unroll
-            for (int r = 0; r < R; ++r)
-            {
-                uint32_t const t = g * R + r < tasks ? g * R + r : g * R;
-                ry[r] = runY(a, t % nY);
-                rz[r] = runZ(a, t / nY);
-                uint8_t const* const p = a.src + srcRowIndex(a, ry[r].s, rz[r].s) * BPVS;
-#pragma unroll
-                for (int j = 0; j < kStage; ++j)
-                    if (16u * lane + 1024u * j < rowBytes)
-                    {
-                        uint32_t const oc = rowChunk(16u * lane + 1024u * j, rowBytes);
-                        w[r][j] = aligned ? __builtin_nontemporal_load(reinterpret_cast<u32x4 const*>(p + oc))
-                                          : reinterpret_cast<RowVec16 const*>(p + oc)->v;
-                    }
-            }
-#pragma unroll
-            for (int r = 0; r < R; ++r)
-#pragma unroll
-                for (int j = 0; j < kStage; ++j)
-                    if (16u * lane + 1024u * j < rowBytes)
-                        reinterpret_cast<RowVec16*>(slots + r * slotBytes +
-                                                    padOff<PAD>(rowChunk(16u * lane + 1024u * j, rowBytes)))->v = w[r][j];
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-            for (int r = 0; r < R; ++r)
-            {
-                if (g * R + r >= tasks)
-                    break;
-                uint8_t const* const slot = slots + r * slotBytes;
-                for (int32_t dx = V * lane; dx < a.ddx; dx += 64 * V)
-                {
-                    uint32_t code[V];
-#pragma unroll
-                    for (int i = 0; i < V; i += 4)
-                    {
-                        u32x4 const q = *reinterpret_cast<u32x4 const*>(xt + dx + i);
-                        int32_t const xs[4] = {static_cast<int32_t>(q.x), static_cast<int32_t>(q.y),
-                                               static_cast<int32_t>(q.z), static_cast<int32_t>(q.w)};
-#pragma unroll
-                        for (int j = 0; j < 4 && i + j < V; ++j)
-                        {
-                            uint32_t const c =
-                                PAD ? loadCode<BPVS>(slot + padOff<true>(static_cast<uint32_t>(xs[j]) * BPVS), 0)
-                                    : loadCode<BPVS>(slot, static_cast<uint64_t>(xs[j]));
-                            code[i + j] = CONV ? convertCode<-1, -1>(c, a) : c;
-                        }
-                    }
-                    for (int32_t zd = rz[r].d0; zd < rz[r].d1; ++zd)
-                        for (int32_t yd = ry[r].d0; yd < ry[r].d1; ++yd)
-                            store16<BPVD>(a.dst, dstRowIndex(a, yd, zd) + static_cast<uint64_t>(dx), code);
-                }
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        }
-    }
-
-    // ---- LDS gather with a loader wave (round 6, knob resample.pc) --------------------------
-    // gfx950's vmcnt counts a wave's loads AND stores, so in resampleGatherLdsKernel every task's
-    // row load -- `s_waitcnt vmcnt(0)` before its LDS write -- also waits until the PREVIOUS
-    // task's nontemporal stores are acknowledged: a wave that loops over tasks (the capped UInt8
-    // grid) serialises store latency + load latency per task.  Here the roles are split inside
-    // the workgroup: wave 0 only loads -- the S = kBlock/64 - 1 source rows of the next stage,
-    // all loads in flight, one wait that covers nothing but its own loads, then the rows into
-    // the other half of a double-buffered LDS ring -- while waves 1..S only gather from LDS and
-    // store (they never wait on vmcnt).  One workgroup barrier per stage; the x table is staged
-    // once per workgroup and the workgroups loop over stages (grid capped).
-    template <int BPVS, int BPVD, bool CONV>
-    __global__ __launch_bounds__(kBlock) void resampleGatherPcKernel(ResampleArgs a, uint32_t slotBytes)
-    {
-        constexpr int S = kBlock / 64 - 1;   // storer waves = rows per stage
-        constexpr int V = 16 / BPVD;
-        constexpr int kChunks = 4;           // rows <= 4 KiB: <= 4 x 16 B per lane
-        extern __shared__ u32x4 ldsRaw[];
-        uint8_t* const lds = reinterpret_cast<uint8_t*>(ldsRaw);
-        int32_t* const xt = reinterpret_cast<int32_t*>(lds);
-        uint32_t const xtBytes = (static_cast<uint32_t>(a.ddx) * 4u + 15u) & ~15u;
-        uint8_t* const ring = lds + xtBytes;   // [2][S] slots
-        int const lane = threadIdx.x & 63;
-        uint32_t const wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-        for (uint32_t i = threadIdx.x * 4; i < static_cast<uint32_t>(a.ddx); i += kBlock * 4)
-            *reinterpret_cast<u32x4*>(xt + i) = *reinterpret_cast<u32x4 const*>(a.xtab + i);
-        uint32_t const nY = static_cast<uint32_t>(a.nRunsY);
-        uint32_t const tasks = nY * static_cast<uint32_t>(a.nRunsZ);
-        uint32_t const rowBytes = static_cast<uint32_t>(a.sdx) * BPVS;
-        bool const aligned = rowBytes % 16u == 0u;
-
-        // loader: the rows of stage group q into ring half h
-        auto loadStage = [&](uint32_t q, uint32_t h) {
-            u32x4 w[S][kChunks];
-#pragma unroll
-            for (int i = 0; i < S; ++i)
-            {
-                uint32_t const t = q * S + i;
-                if (t >= tasks)
-                    continue;
-                Run const ry = runY(a, t % nY);
-                Run const rz = runZ(a, t / nY);
-                uint8_t const* const p = a.src + srcRowIndex(a, ry.s, rz.s) * BPVS;
-#pragma unroll
-                for (int j = 0; j < kChunks; ++j)
-                    if (16u * lane + 1024u * j < rowBytes)
-                    {
-                        uint32_t const oc = rowChunk(16u * lane + 1024u * j, rowBytes);
-                        w[i][j] = aligned ? __builtin_nontemporal_load(reinterpret_cast<u32x4 const*>(p + oc))
-                                          : reinterpret_cast<RowVec16 const*>(p + oc)->v;
-                    }
-            }
-#pragma unroll
-            for (int i = 0; i < S; ++i)
-            {
-                if (q * S + i >= tasks)
-                    continue;
-                uint8_t* const slot = ring + (h * S + i) * slotBytes;
-#pragma unroll
-                for (int j = 0; j < kChunks; ++j)
-                    if (16u * lane + 1024u * j < rowBytes)
-                        reinterpret_cast<RowVec16*>(slot + rowChunk(16u * lane + 1024u * j, rowBytes))->v = w[i][j];
-            }
-        };
-        auto barrier = [] {
-            // LDS writes / reads of this stage done, then the workgroup barrier: no vmcnt wait
-            // (the storers' stores stay in flight across it)
-            __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0); vmcnt, expcnt untouched
-            __builtin_amdgcn_s_barrier();
-        };
-
-        // Two loops, one per role, with the same number of barriers: the storers' loop issues
-        // no global load, so the compiler's waits there never involve vmcnt (a shared loop body
-        // merged the loader's pending loads into the storers' path as an s_waitcnt vmcnt(0)).
-        uint32_t const q0 = blockIdx.x;
-        if (wib == 0)
-        {
-            if (q0 * S < tasks)
-                loadStage(q0, 0);
-            barrier();
-            uint32_t k = 0;
-            for (uint32_t q = q0; q * S < tasks; ++k, q += gridDim.x)
-            {
-                if ((q + gridDim.x) * S < tasks)
-                    loadStage(q + gridDim.x, (k & 1u) ^ 1u);
-                barrier();
-            }
-        }
-        else
-        {
-            barrier();
-            uint32_t k = 0;
-            for (uint32_t q = q0; q * S < tasks; ++k, q += gridDim.x)
-            {
-                uint32_t const t = q * S + (wib - 1);
-                if (t < tasks)
-                {
-                    Run const ry = runY(a, t % nY);
-                    Run const rz = runZ(a, t / nY);
-                    uint8_t const* const slot = ring + ((k & 1u) * S + (wib - 1)) * slotBytes;
-                    for (int32_t dx = V * lane; dx < a.ddx; dx += 64 * V)
-                    {
-                        uint32_t code[V];
-#pragma unroll
-                        for (int i = 0; i < V; i += 4)
-                        {
-                            u32x4 const xq = *reinterpret_cast<u32x4 const*>(xt + dx + i);
-                            int32_t const xs[4] = {static_cast<int32_t>(xq.x), static_cast<int32_t>(xq.y),
-                                                   static_cast<int32_t>(xq.z), static_cast<int32_t>(xq.w)};
-#pragma unroll
-                            for (int j = 0; j < 4 && i + j < V; ++j)
-                            {
-                                uint32_t const c = loadCode<BPVS>(slot, static_cast<uint64_t>(xs[j]));
-                                code[i + j] = CONV ? convertCode<-1, -1>(c, a) : c;
-                            }
-                        }
-                        for (int32_t zd = rz.d0; zd < rz.d1; ++zd)
-                            for (int32_t yd = ry.d0; yd < ry.d1; ++yd)
-                                store16<BPVD>(a.dst, dstRowIndex(a, yd, zd) + static_cast<uint64_t>(dx), code);
-                    }
-                }
-                barrier();
-            }
-        }
-    }
-
-    // ---- UInt8 gather without LDS (round 6, knob resample.u8_direct) ------------------------
-    // Lane l owns dst voxels [16 l + 1024 g, +16) of every dst row (g < G).  Output dword j of
-    // that 16-B store holds dst voxels 4j..4j+3, whose source bytes xs[4j..4j+3] (exact x
-    // table) lie within SPAN consecutive dwords of the source row starting at the dword-aligned
-    // byte offset base_j (host-checked, clamped into the row).  base_j and the v_perm selectors
-    // are the same for every task, so each lane derives them ONCE from the x table; per task a
-    // lane issues 4 dword-aligned SPAN-dword loads per group straight from the task's source row
-    // (the wave's loads share the row's lines in L1 / L2), assembles each output dword with one
-    // or two v_perm_b32, and stores 16 B per dst row: no LDS staging, no x-table reads, no
-    // per-byte LDS gathers.  (The LDS gather issues 16 ds_read_u8 + 4 ds_read_b128 per lane per
-    // 16 stored bytes, twice the UInt16 kernel's LDS instructions per byte.)  PRE: the next
-    // task's loads are issued before the current task's stores.
-    struct __attribute__((packed, aligned(4))) Dw2
-    {
-        uint32_t v[2];
-    };
-    struct __attribute__((packed, aligned(4))) Dw3
-    {
-        uint32_t v[3];
-    };
-
-    template <int SPAN, int G, bool CONV, bool PRE>
-    __global__ __launch_bounds__(kBlock) void resampleGatherU8Kernel(ResampleArgs a)
-    {
-        static_assert(SPAN == 2 || SPAN == 3, "two or three source dwords per output dword");
-        int const lane = threadIdx.x & 63;
-        uint32_t const wave = __builtin_amdgcn_readfirstlane(xcdSwizzle(blockIdx.x, gridDim.x) * (kBlock / 64) +
-                                                             (threadIdx.x >> 6));
-        uint32_t const totalWaves = gridDim.x * (kBlock / 64);
-        uint32_t const nY = static_cast<uint32_t>(a.nRunsY);
-        uint32_t const tasks = nY * static_cast<uint32_t>(a.nRunsZ);
-        if (wave >= tasks)
-            return;
-        uint32_t const sdx = static_cast<uint32_t>(a.sdx);
-        // per lane, once: dword offsets and selectors of the 4 output dwords of each group
-        uint32_t base[G][4], selA[G][4], selB[G][4];
-        bool act[G];
-#pragma unroll
-        for (int g = 0; g < G; ++g)
-        {
-            int32_t const dx = 16 * lane + 1024 * g;
-            act[g] = dx < a.ddx;
-            int32_t const dxc = act[g] ? dx : a.ddx - 16;
-            uint32_t xs[16];
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-            {
-                u32x4 const t = *reinterpret_cast<u32x4 const*>(a.xtab + dxc + 4 * q);
-                xs[4 * q] = t.x; xs[4 * q + 1] = t.y; xs[4 * q + 2] = t.z; xs[4 * q + 3] = t.w;
-            }
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-            {
-                uint32_t b = xs[4 * j] & ~3u;
-                uint32_t const lim = sdx - 4u * SPAN;
-                b = b < lim ? b : lim;
-                base[g][j] = b;
-                uint32_t sa = 0, sb = 0;
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-                {
-                    uint32_t const r = xs[4 * j + i] - b;   // < 4 SPAN (host-checked)
-                    uint32_t const va = r < 8u ? r : 0x0Cu;              // perm: 0x0C = zero byte
-                    uint32_t const vb = r >= 8u ? r - 4u : 0x0Cu;
-                    sa |= va << (8 * i);
-                    sb |= vb << (8 * i);
-                }
-                selA[g][j] = sa;
-                selB[g][j] = sb;
-            }
-        }
-        uint32_t w[G][4][SPAN];
-        auto load = [&](uint32_t t) {
-            Run const ry = runY(a, t % nY);
-            Run const rz = runZ(a, t / nY);
-            uint8_t const* const p = a.src + srcRowIndex(a, ry.s, rz.s);
-#pragma unroll
-            for (int g = 0; g < G; ++g)
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-                {
-                    if constexpr (SPAN == 2)
-                    {
-                        Dw2 const d = *reinterpret_cast<Dw2 const*>(p + base[g][j]);
-                        w[g][j][0] = d.v[0]; w[g][j][1] = d.v[1];
-                    }
-                    else
-                    {
-                        Dw3 const d = *reinterpret_cast<Dw3 const*>(p + base[g][j]);
-                        w[g][j][0] = d.v[0]; w[g][j][1] = d.v[1]; w[g][j][2] = d.v[2];
-                    }
-                }
-        };
-        load(wave);
-        for (uint32_t t = wave; t < tasks; t += totalWaves)
-        {
-            uint32_t out[G][4];
-#pragma unroll
-            for (int g = 0; g < G; ++g)
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-                {
-                    uint32_t v = __builtin_amdgcn_perm(w[g][j][1], w[g][j][0], selA[g][j]);
-                    if constexpr (SPAN == 3)
-                        v |= __builtin_amdgcn_perm(w[g][j][2], w[g][j][1], selB[g][j]);
-                    if constexpr (CONV)
-                    {
-                        uint32_t c = 0;
-#pragma unroll
-                        for (int i = 0; i < 4; ++i)
-                            c |= (convertCode<-1, -1>((v >> (8 * i)) & 0xFFu, a) & 0xFFu) << (8 * i);
-                        v = c;
-                    }
-                    out[g][j] = v;
-                }
-            Run const ry = runY(a, t % nY);
-            Run const rz = runZ(a, t / nY);
-            if constexpr (PRE)
-            {
-                if (t + totalWaves < tasks)
-                    load(t + totalWaves);
-            }
-            for (int32_t zd = rz.d0; zd < rz.d1; ++zd)
-                for (int32_t yd = ry.d0; yd < ry.d1; ++yd)
-                {
-                    uint8_t* const row = a.dst + dstRowIndex(a, yd, zd);
-#pragma unroll
-                    for (int g = 0; g < G; ++g)
-                        if (act[g])
-                            __builtin_nontemporal_store(u32x4{out[g][0], out[g][1], out[g][2], out[g][3]},
-                                                        reinterpret_cast<u32x4*>(row + 16 * lane + 1024 * g));
-                }
-            if constexpr (!PRE)
-            {
-                if (t + totalWaves < tasks)
-                    load(t + totalWaves);
-            }
-        }
-    }
-
     // Fix-up of the optimistic Float32 "Linear" gather: one wave per task; tasks whose source
     // row's chain neighbourhood holds a flagged row (a.rowChain, from rowChainKernel) rewrite
     // their destination rectangle with the full sampleLinear chain.
@@ -890,7 +532,6 @@ namespace hipk
         uint8_t const* staged = nullptr; // sdy bytes (y) then sgz bytes (global z): 1 = a task reads it
         bool yAllRows = false;           // the y runs read every source row 0..sdy-1, in order
         bool zContiguous = false;        // the z runs read consecutive source planes
-        int32_t u8span = 0;              // resampleGatherU8Kernel's SPAN for this x table (0: n/a)
         int32_t aff[2][6] = {{0, 0, 0, 0, 0, 0}, {0, 0, 0, 0, 0, 0}};   // {aff, sa, da, dl, s0, d0}
     };
 
@@ -963,21 +604,6 @@ namespace hipk
         t.zContiguous = true;
         for (size_t i = 1; i < rz.size(); ++i)
             t.zContiguous = t.zContiguous && rz[i].s == rz[i - 1].s + 1;
-        // the UInt8 register-window gather: every output dword's 4 source bytes within SPAN
-        // dwords at a dword-aligned offset clamped into the row (resampleGatherU8Kernel)
-        auto spanFits = [&](int32_t span) {
-            if (ddx % 16 != 0 || sdx % 4 != 0 || sdx < 4 * span)
-                return false;
-            for (int32_t dx = 0; dx < ddx; dx += 4)
-            {
-                int32_t const b = std::min(xt[dx] & ~3, sdx - 4 * span);
-                for (int32_t i = 0; i < 4; ++i)
-                    if (xt[dx + i] - b < 0 || xt[dx + i] - b >= 4 * span)
-                        return false;
-            }
-            return true;
-        };
-        t.u8span = spanFits(2) ? 2 : spanFits(3) ? 3 : 0;
         t.minSz = rz.empty() ? 0 : rz.front().s;
         t.maxSz = rz.empty() ? -1 : rz.back().s;
         // layout: x table first (16-byte aligned for vector reads, padded to 4 entries), runs after
@@ -1220,42 +846,6 @@ namespace hipk
         bool const pad = rowBytes % 16 == 0 && (padKnob == 2 || (padKnob == 1 && bs == 1));
         uint64_t const slotBytes = pad ? rowBytes + (rowBytes >> 8) * 16 : (rowBytes + 15) & ~uint64_t(15);
         uint64_t const lds = xtBytes + (kBlock / 64) * slotBytes;
-        // wide workgroups (knob resample.gather_block = 512 / 1024 threads): one task per wave,
-        // the x table staged once per 8 / 16 tasks, grid not capped -- no wave loops over tasks,
-        // so no task's row load waits behind the previous task's stores (vmcnt counts both)
-        int64_t const wb = rt::knob(rt::Knob::ResampleGatherBlock);
-        if ((wb == 512 || wb == 1024) && !detect && !chain && rowBytes >= 16 &&
-            (rowBytes % 16 == 0 || rt::knob(rt::Knob::ResampleAnyRows) != 0) &&
-            reinterpret_cast<uintptr_t>(b.src) % 16 == 0)
-        {
-            uint64_t const waves = static_cast<uint64_t>(wb) / 64;
-            uint64_t const ldsW = xtBytes + waves * slotBytes;
-            if (ldsW <= 65536)
-            {
-                uint64_t const blocksW = (tasks + waves - 1) / waves;
-                unsigned const gw = static_cast<unsigned>(blocksW < (1u << 30) ? blocksW : (1u << 30));
-                uint32_t const slotw = static_cast<uint32_t>(slotBytes);
-#define VKT_GW(S, D, C)                                                                                           \
-    do {                                                                                                          \
-        if (wb == 512)                                                                                            \
-            hipLaunchKernelGGL((resampleGatherLdsKernel<S, D, C, false, false, false, 512>), dim3(gw), dim3(512),  \
-                               ldsW, s, b, slotw);                                                               \
-        else                                                                                                      \
-            hipLaunchKernelGGL((resampleGatherLdsKernel<S, D, C, false, false, false, 1024>), dim3(gw), dim3(1024), \
-                               ldsW, s, b, slotw);                                                               \
-    } while (0)
-#define VKT_GW_D(S, C) do { if (bd == 1) VKT_GW(S, 1, C); else if (bd == 2) VKT_GW(S, 2, C); else VKT_GW(S, 4, C); } while (0)
-#define VKT_GW_S(C) do { if (bs == 1) VKT_GW_D(1, C); else if (bs == 2) VKT_GW_D(2, C); else VKT_GW_D(4, C); } while (0)
-                if (identity) VKT_GW_S(false); else VKT_GW_S(true);
-#undef VKT_GW_S
-#undef VKT_GW_D
-#undef VKT_GW
-                return true;
-            }
-        }
-        if (rowBytes < 16 || (rowBytes % 16 != 0 && rt::knob(rt::Knob::ResampleAnyRows) == 0) ||
-            reinterpret_cast<uintptr_t>(b.src) % 16 != 0 || lds > 65536)
-            return false;
         // next-row prefetch (knob resample.prefetch): 1 for 2-byte destinations, 2 for every
         // destination, 0 (default since round 6) off.  Round 5 (profiles/r05/gatherp.jsonl): UInt16
         // 1024^3 -> 768^3 0.378 -> 0.358 ms with it, UInt8 lost.  Round 6, after the run tables
@@ -1263,38 +853,6 @@ namespace hipk
         // without vs 0.354-0.356 with, 768^3 -> 1024^3 0.500-0.503 vs 0.507-0.508; UInt8 equal.
         // The prefetched row's wait is a vmcnt(0) behind the task's stores either way (the store
         // count per task is not a compile-time constant).
-        int64_t const rpw = rt::knob(rt::Knob::ResampleRowsPerWave);
-        if ((rpw == 2 || rpw == 4) && !detect && !chain && rowBytes <= 4096)
-        {
-            uint64_t const ldsM = xtBytes + (kBlock / 64) * static_cast<uint64_t>(rpw) * slotBytes;
-            if (ldsM <= 65536)
-            {
-                uint64_t const groups = (tasks + rpw - 1) / rpw;
-                uint64_t blocksM = (groups + 3) / 4;
-                if (bd == 1 && blocksM > 16384)
-                    blocksM = 16384;
-                unsigned const gm = static_cast<unsigned>(blocksM < (1u << 30) ? blocksM : (1u << 30));
-                uint32_t const slotm = static_cast<uint32_t>(slotBytes);
-#define VKT_GM(S, D, C, RR)                                                                                      \
-    do {                                                                                                         \
-        if (pad)                                                                                                 \
-            hipLaunchKernelGGL((resampleGatherLdsMultiKernel<S, D, C, RR, true>), dim3(gm), dim3(kBlock), ldsM, s, b, \
-                               slotm);                                                                           \
-        else                                                                                                     \
-            hipLaunchKernelGGL((resampleGatherLdsMultiKernel<S, D, C, RR, false>), dim3(gm), dim3(kBlock), ldsM, s, \
-                               b, slotm);                                                                        \
-    } while (0)
-#define VKT_GM_R(S, D, C) do { if (rpw == 2) VKT_GM(S, D, C, 2); else VKT_GM(S, D, C, 4); } while (0)
-#define VKT_GM_D(S, C) do { if (bd == 1) VKT_GM_R(S, 1, C); else if (bd == 2) VKT_GM_R(S, 2, C); else VKT_GM_R(S, 4, C); } while (0)
-#define VKT_GM_S(C) do { if (bs == 1) VKT_GM_D(1, C); else if (bs == 2) VKT_GM_D(2, C); else VKT_GM_D(4, C); } while (0)
-                if (identity) VKT_GM_S(false); else VKT_GM_S(true);
-#undef VKT_GM_S
-#undef VKT_GM_D
-#undef VKT_GM_R
-#undef VKT_GM
-                return true;
-            }
-        }
         int64_t const pk = rt::knob(rt::Knob::ResamplePrefetch);
         bool const prefetch = (pk == 2 || (pk == 1 && bd == 2)) && !detect && !chain && rowBytes <= 4096;
         // one task per wave; for 1-byte destinations a task writes so little (one 1-KiB store
@@ -1553,28 +1111,6 @@ namespace hipk
         {
             hipLaunchKernelGGL(resampleChainKernel, dim3(grid), dim3(kBlock), 0, s, a);
             return rt::finishLaunch("Resample_hip(linear chain, gather)");
-        }
-        int64_t const u8direct = rt::knob(rt::Knob::ResampleU8Direct);
-        if (vecDst && bs == 1 && bd == 1 && u8direct > 0 && t.u8span != 0 && dst.dimX <= 2048 &&
-            reinterpret_cast<uintptr_t>(src.data) % 4 == 0)
-        {
-            uint64_t blocks = (tasks + kBlock / 64 - 1) / (kBlock / 64);
-            uint64_t const cap = static_cast<uint64_t>(u8direct) * 1024;
-            unsigned const g = static_cast<unsigned>(blocks < cap ? blocks : cap);
-            bool const pre = rt::knob(rt::Knob::ResamplePrefetch) != 0;
-#define VKT_U8(SP, G, C)                                                                                        \
-    do {                                                                                                        \
-        if (pre)                                                                                                \
-            hipLaunchKernelGGL((resampleGatherU8Kernel<SP, G, C, true>), dim3(g), dim3(kBlock), 0, s, a);       \
-        else                                                                                                    \
-            hipLaunchKernelGGL((resampleGatherU8Kernel<SP, G, C, false>), dim3(g), dim3(kBlock), 0, s, a);      \
-    } while (0)
-#define VKT_U8_G(SP, C) do { if (dst.dimX <= 1024) VKT_U8(SP, 1, C); else VKT_U8(SP, 2, C); } while (0)
-            if (t.u8span == 2) { if (identity) VKT_U8_G(2, false); else VKT_U8_G(2, true); }
-            else { if (identity) VKT_U8_G(3, false); else VKT_U8_G(3, true); }
-#undef VKT_U8_G
-#undef VKT_U8
-            return rt::finishLaunch("Resample_hip(gather, UInt8 register window)");
         }
         if (vecDst && gatherLdsEnabled() && launchGatherLds(a, bs, bd, identity, false, tasks, s))
             return rt::finishLaunch("Resample_hip(gather, LDS)");

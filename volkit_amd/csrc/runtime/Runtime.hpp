@@ -137,11 +137,7 @@ namespace rt
         ResamplePrefetch,              // LDS gather loads the next task's row during the current one: 1 (default) 2-byte destinations, 2 all, 0 off
         ResampleAnyRows,               // 1: the LDS gather also stages source rows that are not 16-B multiples (rowChunk)
         HistogramPairTiles,            // histograms of 2..4 tiles side by side in one launch (PAIR): 1 where P16 does not apply, 2 always, 0 never
-        ResampleU8Direct,              // UInt8 gathers: > 0 the register-window kernel (no LDS; the value caps its grid in 1024s of workgroups)
-        ResamplePc,                    // LDS gathers: > 0 the loader-wave kernel (resampleGatherPcKernel; grid cap in 1024s of workgroups)
-        ResampleGatherBlock,           // LDS gathers: 512 / 1024 = threads per workgroup, one task per wave, grid not capped (0: 256, UInt8 capped)
         ResampleLdsPad,                // LDS gathers: 16 B of padding per 256 B of a staged row (bank spread): 1 UInt8 sources, 2 all, 0 none
-        ResampleRowsPerWave,           // LDS gathers: 2 / 4 = tasks staged per wave iteration (resampleGatherLdsMultiKernel), 0 = one
         Count
     };
     int64_t knob(Knob k);
