@@ -447,3 +447,36 @@ def test_brick_decompose_direct_kernel(fmt, dims, brick, neg, pos, direct):
     assert set(got) == set(ref)
     for idx, v in ref.items():
         np.testing.assert_array_equal(got[idx], v.codes, err_msg=f"brick {idx}")
+
+
+ROW_IMAGE_LAYOUTS = [
+    ((64, 40, 36), (16, 16, 16), (1, 1, 1), (1, 1, 1)),    # 16^3 + halo 1: clamped voxels at every border
+    ((70, 33, 21), (16, 8, 8), (1, 0, 2), (0, 1, 1)),      # asymmetric halos, partial last bricks
+    ((96, 20, 18), (32, 8, 8), (2, 1, 0), (3, 0, 1)),      # wider halos (<= 16 B of the left halo)
+    ((64, 24, 16), (16, 8, 8), (0, 0, 0), (0, 1, 0)),      # halo in y only
+    ((48, 16, 16), (8, 8, 8), (1, 1, 1), (1, 1, 1)),       # 8^3 + halo: rows of 10 voxels
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("knob", [1, 0])
+@pytest.mark.parametrize("fmt", [4, 5, 7])
+@pytest.mark.parametrize("dims,brick,neg,pos", ROW_IMAGE_LAYOUTS)
+def test_brick_decompose_row_image_kernel(fmt, dims, brick, neg, pos, knob):
+    """Knob decompose.row_image (round 6): one brick per workgroup through per-row LDS images --
+    aligned source words in, one 16-B piece per 16 B of a destination row out (the last piece
+    overlapping), clamped border voxels beside the span -- bit-exact vs the oracle for every format
+    (layouts whose rows are under 16 B, UInt8 8^3 + halo, fall back to the staged kernel); knob 0
+    is the staged kernel on the same layouts (the default, 2, takes the row image for UInt8 only)."""
+    rng = np.random.default_rng(fmt * 10 + sum(dims) + 77)
+    codes = rand_codes(rng, fmt, dims[::-1])
+    assert lib.vktHipSetTuningKnob(b"decompose.row_image", knob) == 0
+    try:
+        err, got = gpu_decompose(codes, fmt, (0.0, 1.0), brick, neg, pos)
+    finally:
+        assert lib.vktHipSetTuningKnob(b"decompose.row_image", -1) == 0
+    assert err == vkt.NoError, vkt.last_error()
+    ref = ob.brick_decompose(ob.Volume(codes, fmt), brick, neg, pos)
+    assert set(got) == set(ref)
+    for idx, v in ref.items():
+        np.testing.assert_array_equal(got[idx], v.codes, err_msg=f"brick {idx}")

@@ -803,6 +803,31 @@ def main():
             report(f"gpmc Resample 1024^3->768^3 fmt{fmt} Linear", ms,
                    resample_bytes((1024,) * 3, (768,) * 3, b, b, every_row=fmt == 7), 768 ** 3)
             free(S, Rv)
+    if want("decrow"):
+        # in-process A/B of the row-image BrickDecompose (knob decompose.row_image), back-to-back
+        import volkit_amd.volkit as vkt
+        ep = vkt.GetThreadExecutionPolicy()
+        ep.device = vkt.ExecutionPolicy.Device_GPU
+        vkt.SetThreadExecutionPolicy(ep)
+        n = 1024
+        try:
+            for fmt, bs in ((vkt.DataFormat_UInt16, 16), (vkt.DataFormat_UInt8, 16), (vkt.DataFormat_UInt16, 8)):
+                V = vkt.StructuredVolume(n, n, n, fmt)
+                vkt.Synthesize(V, 77)
+                arr = vkt.Array3D_StructuredVolume()
+                b3, h3 = vkt.Vec3i(bs, bs, bs), vkt.Vec3i(1, 1, 1)
+                vkt.BrickDecomposeResize(arr, V, b3, h3, h3)
+                bpv = 1 if fmt == vkt.DataFormat_UInt8 else 2
+                vox = (bs + 2) ** 3 * (n // bs) ** 3
+                for rep in range(2):
+                    for k in (0, 1):
+                        lib.vktHipSetTuningKnob(b"decompose.row_image", 1 if k else 0)
+                        ms = pipelined(lambda: vkt.BrickDecompose(arr, V, b3, h3, h3), R)
+                        report(f"decrow BrickDecompose 1024^3 bpv{bpv} -> {bs}^3 bricks halo 1 back-to-back "
+                               f"[row_image={k}]", ms, 2 * bpv * vox, vox)
+                del arr, V
+        finally:
+            lib.vktHipSetTuningKnob(b"decompose.row_image", -1)
     if want("decompose"):
         # BrickDecompose: 1024^3 UInt16 into 64^3 bricks with a 1-voxel halo
         import volkit_amd.volkit as vkt

@@ -577,6 +577,115 @@ namespace hipk
     }
 
 
+    // ---- Row-image copy of a uniform grid (round 6, knob decompose.row_image) ------------------
+    // No cut words anywhere.  Phase 1: the 16-B ALIGNED source words covering each box row's
+    // in-volume span go, coalesced (consecutive threads = consecutive words of a row, then the
+    // next row), to ALIGNED places of a per-row LDS image (row r at r * IMG, IMG an odd number of
+    // 16-B words so phase 2's per-row reads spread over the banks); border bricks then write
+    // their clamped voxels next to the span.  Phase 2: one thread per destination row reads the
+    // row's bytes from the image (unaligned ds_read_b128 at the row's phase, the same for every
+    // row of the brick: source rows are 16-B multiples) and stores them as 16-B pieces at
+    // r * rowBytes in the brick -- the last piece taken at rowBytes - 16, overlapping its
+    // neighbour with the same bytes, so a row end costs one store, not per-voxel masks.  One brick
+    // (<= 16 KiB, rows >= 16 B) per workgroup; dynamic LDS = rows * IMG.
+    template <int BPV, int NT>
+    __global__ __launch_bounds__(NT) void brickRowImageKernel(BrickGrid grid, uint8_t const* src, int32_t sdx,
+                                                              int32_t sdy, int32_t sdz)
+    {
+        constexpr uint32_t kHead = 16;   // room for the left clamped halo voxels
+        constexpr int kBatch = 4;
+        extern __shared__ u32x4 imgRaw[];
+        uint8_t* const img = reinterpret_cast<uint8_t*>(imgRaw);
+        uint32_t const b = __builtin_amdgcn_readfirstlane(xcdSwizzle(blockIdx.x, gridDim.x));
+        BrickDesc const d = gridDesc<BPV>(grid, b);
+        int32_t const nRows = static_cast<int32_t>(fdiv(d.nvox, d.fdx));
+        int32_t const lo = max(d.fx, 0), hi = min(d.fx + d.nx, sdx);
+        uint64_t const spY = static_cast<uint64_t>(sdx), spZ = spY * static_cast<uint64_t>(sdy);
+        uint64_t const srcBytes = spZ * static_cast<uint64_t>(sdz) * BPV;
+        auto rowBase = [&](int32_t r) -> uint64_t {
+            uint32_t const z = fdiv(static_cast<uint32_t>(r), d.fdy);
+            uint32_t const y = static_cast<uint32_t>(r) - z * d.fdy.d;
+            return static_cast<uint64_t>(clampi(d.fz + static_cast<int32_t>(z), sdz - 1)) * spZ +
+                   static_cast<uint64_t>(clampi(d.fy + static_cast<int32_t>(y), sdy - 1)) * spY;
+        };
+        uint32_t const ph = (static_cast<uint32_t>(lo) * BPV) & 15u;
+        uint32_t const alignLo = static_cast<uint32_t>(lo) * BPV - ph;   // in-row byte of word 0
+        uint32_t const spanB = ph + static_cast<uint32_t>(hi - lo) * BPV;
+        uint32_t const wpr = (spanB + 15u) / 16u;
+        uint32_t const tailB = static_cast<uint32_t>(d.fx + d.nx - hi) * BPV;
+        uint32_t const imgW = ((kHead + spanB + tailB + 15u) / 16u) | 1u;
+        uint32_t const IMG = imgW * 16u;
+        FastDiv const fw = makeFastDiv(wpr);
+        uint32_t const total = static_cast<uint32_t>(nRows) * wpr;
+        for (uint32_t t0 = threadIdx.x; t0 < total; t0 += kBatch * NT)
+        {
+            u32x4 w[kBatch];
+            uint32_t at[kBatch];
+#pragma unroll
+            for (int u = 0; u < kBatch; ++u)
+            {
+                uint32_t const t = t0 + static_cast<uint32_t>(u * NT);
+                uint32_t const tt = t < total ? t : 0u;
+                uint32_t const r = fdiv(tt, fw);
+                uint32_t const k = tt - r * wpr;
+                uint64_t const byte = rowBase(static_cast<int32_t>(r)) * BPV + alignLo + 16ull * k;
+                at[u] = t < total ? r * IMG + kHead + 16u * k : ~0u;
+                if (byte + 16 <= srcBytes)
+                    w[u] = *reinterpret_cast<u32x4 const*>(src + byte);
+                else
+                {
+                    // the volume's last word: only the bytes inside the buffer
+                    uint32_t q[4] = {0u, 0u, 0u, 0u};
+                    for (uint32_t i = 0; i < 16u && byte + i < srcBytes; ++i)
+                        q[i / 4] |= static_cast<uint32_t>(src[byte + i]) << (8 * (i % 4));
+                    w[u] = u32x4{q[0], q[1], q[2], q[3]};
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kBatch; ++u)
+                if (at[u] != ~0u)
+                    *reinterpret_cast<u32x4*>(img + at[u]) = w[u];
+        }
+        if (d.fx < 0 || d.fx + d.nx > sdx)   // border brick: clamped voxels beside the span
+        {
+            __syncthreads();
+            for (int32_t r = threadIdx.x; r < nRows; r += NT)
+            {
+                uint64_t const rb = rowBase(r);
+                uint8_t* const row = img + static_cast<uint32_t>(r) * IMG + kHead + ph;   // x = lo
+                if (d.fx < 0)
+                {
+                    uint32_t const c = loadCode<BPV>(src, rb);
+                    for (int32_t x = d.fx; x < min(0, d.fx + d.nx); ++x)
+                        storeCode<BPV>(row + (x - lo) * BPV, 0, c);
+                }
+                if (d.fx + d.nx > sdx)
+                {
+                    uint32_t const c = loadCode<BPV>(src, rb + static_cast<uint64_t>(sdx - 1));
+                    for (int32_t x = max(sdx, d.fx); x < d.fx + d.nx; ++x)
+                        storeCode<BPV>(row + (x - lo) * BPV, 0, c);
+                }
+            }
+        }
+        __syncthreads();
+        uint32_t const rowB = static_cast<uint32_t>(d.nx) * BPV;
+        uint32_t const pieces = (rowB + 15u) / 16u;
+        int32_t const first = static_cast<int32_t>(kHead + ph) + (d.fx - lo) * BPV;   // image byte of x = fx
+        for (int32_t r = threadIdx.x; r < nRows; r += NT)
+        {
+            uint8_t const* const in = img + static_cast<uint32_t>(r) * IMG + first;
+            uint8_t* const out = d.dst + static_cast<uint64_t>(r) * rowB;
+            for (uint32_t p = 0; p < pieces; ++p)
+            {
+                uint32_t const off = 16u * p + 16u <= rowB ? 16u * p : rowB - 16u;
+                u32x4 const v = reinterpret_cast<Unaligned16 const*>(in + off)->v;
+                // (global address space named: a flat store would also count on lgkmcnt and make the
+                // next row's LDS reads wait for it)
+                __builtin_nontemporal_store(v, (__attribute__((address_space(1))) u32x4*)(out + off));
+            }
+        }
+    }
+
     // ---- Persistent, software-pipelined staged copy of a uniform grid (knob decompose.pipe) ----
     // The staged kernel above runs one workgroup per 16-KiB chunk: a small brick (16^3 + halo 1 =
     // 11.7 KB) is one short-lived workgroup whose loads, LDS pass and stores run back to back, so
@@ -1447,6 +1556,33 @@ namespace hipk
             return true;
         };
         bool const direct = !half && gatherLds == 0 && !pipe && !pair && directGrid();
+        // row-image copy (knob decompose.row_image: 2 (default) UInt8, 1 every format, 0 off): one
+        // brick of <= 16 KiB per workgroup, rows >= 16 B, 16-B multiple source rows, halos <= 16 B.
+        // Measured (profiles/r06/decrow.jsonl, 1024^3 -> 16^3 bricks + halo 1, back-to-back): UInt8
+        // 1.27-1.32 -> 1.04 ms, UInt16 1.46-1.60 -> 2.55 ms (a 36-B row's three 16-B pieces per lane
+        // scatter each store instruction over ~2.3 KB), UInt16 8^3 + halo 5.85-6.32 -> 5.05 ms
+        int64_t const rowImageKnob = rt::knob(rt::Knob::DecomposeRowImage);
+        uint32_t rowImageLds = 0;
+        if (!direct && useGrid && chunks == 1 && gatherLds == 0 && !pipe && !pair && !half &&
+            (rowImageKnob == 1 || (rowImageKnob == 2 && bpv == 1)) &&
+            (static_cast<int64_t>(source.dimX) * bpv) % 16 == 0)
+        {
+            int32_t minNx = grid.nx[2], maxNx = grid.nx[2], maxRows = 0;
+            for (int c = 0; c < 3; ++c)
+            {
+                if ((c == 0 && grid.nbx < 2) || (c == 1 && grid.nbx < 3))
+                    continue;
+                minNx = std::min(minNx, grid.nx[c]);
+                maxNx = std::max(maxNx, grid.nx[c]);
+            }
+            for (int cy = 0; cy < 3; ++cy)
+                for (int cz = 0; cz < 3; ++cz)
+                    maxRows = std::max(maxRows, grid.ny[cy] * grid.nz[cz]);
+            int64_t const img = ((16 + 15 + static_cast<int64_t>(maxNx) * bpv + 16 + 15) / 16 | 1) * 16;
+            if (static_cast<int64_t>(minNx) * bpv >= 16 && -grid.fx0 * static_cast<int64_t>(bpv) <= 16 &&
+                img * maxRows <= 65536)
+                rowImageLds = static_cast<uint32_t>(img * maxRows);
+        }
         // small bricks: P per workgroup (knob decompose.direct 1; 2 keeps one per workgroup).
         // Measured and rejected: 4 bricks of <= 512 items per workgroup at 8 items per thread
         // (16^3 UInt16 0.858 vs 0.862 ms, within the spread)
@@ -1455,7 +1591,10 @@ namespace hipk
                                    : (maxItems <= kBrickChunk / 4 ? 4u : (maxItems <= kBrickChunk / 2 ? 2u : 1u));
         auto launch = [&](auto bpvC, auto swC) {
             constexpr int B = decltype(bpvC)::value, W = decltype(swC)::value;
-            if (direct && perWg > 1)
+            if (rowImageLds != 0)
+                hipLaunchKernelGGL((brickRowImageKernel<B, kBlock>), dim3(static_cast<unsigned>(nFast)), dim3(kBlock),
+                                   rowImageLds, s, grid, source.data, source.dimX, source.dimY, source.dimZ);
+            else if (direct && perWg > 1)
             {
                 unsigned const gw = static_cast<unsigned>((nFast + perWg - 1) / perWg);
                 if (perWg == 4)

@@ -260,6 +260,7 @@ namespace rt
             {"resample.any_rows", 1},
             {"histogram.pair_tiles", 1},
             {"resample.lds_pad", 1},
+            {"decompose.row_image", 2},
         };
         static_assert(sizeof(kKnobs) / sizeof(kKnobs[0]) == static_cast<size_t>(Knob::Count), "knob table");
         std::atomic<int64_t> gKnobs[static_cast<int>(Knob::Count)] = {{kKnobs[0].def}, {kKnobs[1].def},
@@ -283,7 +284,8 @@ namespace rt
                                                                   {kKnobs[36].def}, {kKnobs[37].def},
                                                                   {kKnobs[38].def}, {kKnobs[39].def},
                                                                   {kKnobs[40].def}, {kKnobs[41].def},
-                                                                  {kKnobs[42].def}, {kKnobs[43].def}};
+                                                                  {kKnobs[42].def}, {kKnobs[43].def},
+                                                                  {kKnobs[44].def}};
     } // namespace
 
     int64_t knob(Knob k) { return gKnobs[static_cast<int>(k)].load(std::memory_order_relaxed); }

@@ -138,6 +138,7 @@ namespace rt
         ResampleAnyRows,               // 1: the LDS gather also stages source rows that are not 16-B multiples (rowChunk)
         HistogramPairTiles,            // histograms of 2..4 tiles side by side in one launch (PAIR): 1 where P16 does not apply, 2 always, 0 never
         ResampleLdsPad,                // LDS gathers: 16 B of padding per 256 B of a staged row (bank spread): 1 UInt8 sources, 2 all, 0 none
+        DecomposeRowImage,             // uniform grids of <= 16-KiB bricks through per-row LDS images (brickRowImageKernel): 2 UInt8, 1 all, 0 off
         Count
     };
     int64_t knob(Knob k);
