@@ -133,3 +133,28 @@ def test_resample_padded_lds_rows(g, o, pad, prefetch):
     finally:
         lib.vktHipSetTuningKnob(b"resample.lds_pad", -1)
         lib.vktHipSetTuningKnob(b"resample.prefetch", -1)
+
+
+@pytest.mark.parametrize("cap", [1, 64])
+def test_resample_dst_row_gather(g, o, cap):
+    """Knob resample.dst_rows (round 6): the LDS gather over destination-row tasks -- a fixed number
+    of loads and stores per task, the next row's loads in flight across this task's stores
+    (resampleGatherDstRowKernel) -- vs the oracle: UInt8 (padded and unpadded rows, a conversion)
+    and UInt16, one and two store groups and source chunks, destination rows that are not whole
+    store groups (lanes repeat the last lane's store), a small grid (cap 1: waves loop over many
+    tasks) and a large one.  Rows beyond the kernel's limits take the source-row gather."""
+    from volkit_amd._lib import lib
+    rng = np.random.default_rng(700 + cap)
+    assert lib.vktHipSetTuningKnob(b"resample.dst_rows", cap) == 0
+    shapes = PC_SHAPES + [((1024, 9, 7), (768, 11, 5), 4, 4), ((768, 7, 6), (1024, 9, 8), 4, 4),
+                          ((1000, 5, 6), (1024, 7, 5), 4, 4), ((768, 6, 5), (1024, 8, 7), 5, 5),
+                          ((1001, 4, 5), (1000, 6, 4), 5, 5), ((40, 30, 20), (24, 40, 30), 4, 4)]
+    try:
+        for sd, dd, sf, df in shapes:
+            src = rand_codes(rng, sf, sd[::-1])
+            for dmap in ((0.0, 1.0), (-1.0, 3.0)):
+                out = g.resample(df, dmap, dd, sf, (0.0, 1.0), src, 0)
+                ref = o.resample(df, dmap, dd, sf, (0.0, 1.0), src, 0)
+                assert_codes_equal(out, ref, df, f"dst_rows={cap} {sd}->{dd} {sf}->{df} dmap={dmap}")
+    finally:
+        lib.vktHipSetTuningKnob(b"resample.dst_rows", -1)

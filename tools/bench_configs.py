@@ -779,6 +779,25 @@ def main():
                 free(S, Rv)
         finally:
             lib.vktHipSetTuningKnob(b"resample.lds_pad", -1)
+    if want("dstab"):
+        # in-process A/B: destination-row gather (knob resample.dst_rows = grid cap in 1024s of
+        # workgroups; 0 = the source-row LDS gather)
+        caps = [int(c) for c in os.environ.get("VKT_DST_CAPS", "0,4,16,64,1024").split(",")]
+        try:
+            for se, de, fmt in ((768, 1024, 4), (1000, 1024, 4), (1024, 768, 4), (768, 1024, 5), (1024, 768, 5),
+                                (1000, 1024, 5)):
+                b = {4: 1, 5: 2}[fmt]
+                S = alloc((se,) * 3, fmt, seed=21)
+                Rv = alloc((de,) * 3, fmt)
+                for rep in range(2):
+                    for cap in caps:
+                        lib.vktHipSetTuningKnob(b"resample.dst_rows", cap)
+                        ms = timed(lambda: lib.vktHipResample(Rv, S, 1), R)
+                        report(f"dstab Resample {se}^3->{de}^3 fmt{fmt} Linear [dst_rows={cap}]", ms,
+                               resample_bytes((se,) * 3, (de,) * 3, b, b), de ** 3)
+                free(S, Rv)
+        finally:
+            lib.vktHipSetTuningKnob(b"resample.dst_rows", -1)
     if want("f32lin"):
         # Float32 "Linear" (optimistic gather + fix-up) against Nearest on the
         # gather ratios; Linear's bytes: every source row (the chain's neighbours are classified)

@@ -357,6 +357,112 @@ namespace hipk
         }
     }
 
+    // ---- LDS gather over DESTINATION rows (round 6, knob resample.dst_rows) ---------------------
+    // gfx950's vmcnt counts loads and stores in one in-order counter, and the compiler can wait for
+    // a load without also waiting for the stores issued after it only when it knows how many were
+    // issued.  A source-row task stores to 1..4 destination rows (its run rectangle): a dynamic
+    // count, so resampleGatherLdsKernel's next row load always waited for the previous task's
+    // stores.  Here a task is ONE destination row (plane-linear order: consecutive tasks share or
+    // neighbour a source row, which the L2 serves again): exactly G 16-B store instructions per
+    // task, every lane storing (lanes past the row end repeat the last lane's store: same address,
+    // same bytes), and exactly KS 16-B loads per lane for the source row (clamped to its last 16 B).
+    // The next task's row is loaded into registers before this task's gather and stores, and its
+    // wait at the next iteration is vmcnt(G): the stores stay in flight.  Rows <= 64 G V voxels
+    // (destination) and <= 1 KiB KS (source).
+    template <int BPVS, int BPVD, bool CONV, bool PAD, int G, int KS>
+    __global__ __launch_bounds__(kBlock) void resampleGatherDstRowKernel(ResampleArgs a, uint32_t slotBytes)
+    {
+        constexpr int V = 16 / BPVD;
+        extern __shared__ u32x4 ldsRaw[];
+        uint8_t* const lds = reinterpret_cast<uint8_t*>(ldsRaw);
+        int32_t* const xt = reinterpret_cast<int32_t*>(lds);
+        uint32_t const xtBytes = (static_cast<uint32_t>(a.ddx) * 4u + 15u) & ~15u;
+        int const lane = threadIdx.x & 63;
+        uint32_t const wib = threadIdx.x >> 6;
+        uint8_t* const slot = lds + xtBytes + wib * slotBytes;
+        for (uint32_t i = threadIdx.x * 4; i < static_cast<uint32_t>(a.ddx); i += kBlock * 4)
+            *reinterpret_cast<u32x4*>(xt + i) = *reinterpret_cast<u32x4 const*>(a.xtab + i);
+        __syncthreads();
+
+        uint32_t const wave = __builtin_amdgcn_readfirstlane(xcdSwizzle(blockIdx.x, gridDim.x) * (kBlock / 64) + wib);
+        uint32_t const totalWaves = gridDim.x * (kBlock / 64);
+        uint32_t const ddy = static_cast<uint32_t>(a.ddy);
+        uint32_t const tasks = ddy * static_cast<uint32_t>(a.dnz);
+        uint32_t const rowBytes = static_cast<uint32_t>(a.sdx) * BPVS;
+        bool const aligned = rowBytes % 16u == 0u;
+        uint32_t off[KS];
+#pragma unroll
+        for (int j = 0; j < KS; ++j)
+            off[j] = rowChunk(min(16u * lane + 1024u * j, rowBytes - 16u), rowBytes);
+        int32_t dxs[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+            dxs[g] = min(V * lane + 64 * V * g, a.ddx - V);
+        typedef __attribute__((address_space(4))) int32_t const CI32;
+        auto srcRow = [&](uint32_t t) -> uint8_t const* {
+            uint32_t const zl = fdiv(t, a.fdDdy);
+            uint32_t const yd = t - zl * ddy;
+            int32_t const ys = ((CI32*)a.ysrc)[yd];
+            int32_t const zs = ((CI32*)a.zsrc)[zl];
+            return a.src + srcRowIndex(a, ys, zs) * BPVS;
+        };
+        u32x4 w[KS];
+        auto load = [&](uint32_t t) {
+            uint8_t const* const p = srcRow(t);
+#pragma unroll
+            for (int j = 0; j < KS; ++j)
+                w[j] = aligned ? *reinterpret_cast<u32x4 const*>(p + off[j]) : reinterpret_cast<RowVec16 const*>(p + off[j])->v;
+        };
+        // one task: this row into the slot, the next row's loads out, gather, G stores.  The first
+        // task is peeled so that every path into the loop issues the loads and then the stores,
+        // and the wait at the top of the next task counts G younger stores: vmcnt(G), not 0.
+        auto step = [&](uint32_t t) {
+#pragma unroll
+            for (int j = 0; j < KS; ++j)
+                reinterpret_cast<RowVec16*>(slot + padOff<PAD>(off[j]))->v = w[j];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // the next task's row, in flight during this task's gather and stores
+            load(t + totalWaves < tasks ? t + totalWaves : t);
+            uint32_t const zl = fdiv(t, a.fdDdy);
+            uint32_t const yd = t - zl * ddy;
+            uint8_t* const drow = a.dst + dstRowIndex(a, static_cast<int32_t>(yd), a.dstZ0 + static_cast<int32_t>(zl)) * BPVD;
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+            {
+                int32_t const dx = dxs[g];
+                uint32_t code[V];
+#pragma unroll
+                for (int i = 0; i < V; i += 4)
+                {
+                    u32x4 const q = *reinterpret_cast<u32x4 const*>(xt + dx + i);
+                    int32_t const xs[4] = {static_cast<int32_t>(q.x), static_cast<int32_t>(q.y),
+                                           static_cast<int32_t>(q.z), static_cast<int32_t>(q.w)};
+#pragma unroll
+                    for (int j = 0; j < 4 && i + j < V; ++j)
+                    {
+                        uint32_t const c =
+                            PAD ? loadCode<BPVS>(slot + padOff<true>(static_cast<uint32_t>(xs[j]) * BPVS), 0)
+                                : loadCode<BPVS>(slot, static_cast<uint64_t>(xs[j]));
+                        code[i + j] = CONV ? convertCode<-1, -1>(c, a) : c;
+                    }
+                }
+                store16<BPVD>(drow, static_cast<uint64_t>(dx), code);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        };
+        if (wave < tasks)
+        {
+            load(wave);
+            step(wave);
+            for (uint32_t t = wave + totalWaves; t < tasks; t += totalWaves)
+                step(t);
+        }
+    }
+
     // Fix-up of the optimistic Float32 "Linear" gather: one wave per task; tasks whose source
     // row's chain neighbourhood holds a flagged row (a.rowChain, from rowChainKernel) rewrite
     // their destination rectangle with the full sampleLinear chain.
@@ -529,6 +635,7 @@ namespace hipk
         Run const* runsZ = nullptr;
         int32_t const* xtab = nullptr;
         int32_t const* zsrc = nullptr;   // source plane of every local dst plane
+        int32_t const* ysrc = nullptr;   // source row of every dst row (ddy entries)
         uint8_t const* staged = nullptr; // sdy bytes (y) then sgz bytes (global z): 1 = a task reads it
         bool yAllRows = false;           // the y runs read every source row 0..sdy-1, in order
         bool zContiguous = false;        // the z runs read consecutive source planes
@@ -608,12 +715,15 @@ namespace hipk
         t.maxSz = rz.empty() ? -1 : rz.back().s;
         // layout: x table first (16-byte aligned for vector reads, padded to 4 entries), runs after
         size_t xwords = (xt.size() + 3) / 4 * 4;
-        size_t words = xwords + 3 * ry.size() + 3 * rz.size() + static_cast<size_t>(dnz);
+        size_t words = xwords + 3 * ry.size() + 3 * rz.size() + static_cast<size_t>(dnz) + static_cast<size_t>(ddy);
         std::vector<int32_t> host(xt.begin(), xt.end());
         host.resize(xwords, 0);
         for (Run const& r : ry) host.insert(host.end(), {r.s, r.d0, r.d1});
         for (Run const& r : rz) host.insert(host.end(), {r.s, r.d0, r.d1});
         for (Run const& r : rz)
+            for (int32_t d = r.d0; d < r.d1; ++d)
+                host.push_back(r.s);
+        for (Run const& r : ry)
             for (int32_t d = r.d0; d < r.d1; ++d)
                 host.push_back(r.s);
         VKT_HIP_TRY(hipMalloc(&t.dev, words * sizeof(int32_t) + 16));
@@ -622,6 +732,7 @@ namespace hipk
         t.runsY = reinterpret_cast<Run const*>(t.dev + xwords);
         t.runsZ = reinterpret_cast<Run const*>(t.dev + xwords + 3 * ry.size());
         t.zsrc = t.dev + xwords + 3 * ry.size() + 3 * rz.size();
+        t.ysrc = t.zsrc + dnz;
         {
             // rows the tasks stage (the optimistic Float32 Linear gather flags those itself)
             std::vector<uint8_t> st(static_cast<size_t>(sdy) + static_cast<size_t>(sgz), 0);
@@ -853,6 +964,37 @@ namespace hipk
         // without vs 0.354-0.356 with, 768^3 -> 1024^3 0.500-0.503 vs 0.507-0.508; UInt8 equal.
         // The prefetched row's wait is a vmcnt(0) behind the task's stores either way (the store
         // count per task is not a compile-time constant).
+        // destination-row tasks (knob resample.dst_rows = grid cap in 1024s of workgroups, 0 off)
+        int64_t const dr = rt::knob(rt::Knob::ResampleDstRows);
+        if (dr > 0 && !detect && !chain && bs == bd && bs <= 2 && rowBytes >= 16)
+        {
+            uint32_t const vd = 16 / bd;
+            uint32_t const G = (static_cast<uint32_t>(b.ddx) + 64 * vd - 1) / (64 * vd);
+            uint32_t const KS = static_cast<uint32_t>((rowBytes + 1023) / 1024);
+            uint64_t const dtasks = static_cast<uint64_t>(b.ddy) * static_cast<uint64_t>(b.dnz);
+            if (G <= 2 && KS <= 2 && b.ddx >= static_cast<int32_t>(vd) && dtasks < (1ull << 32))
+            {
+                uint64_t blocksD = (dtasks + 3) / 4;
+                uint64_t const cap = static_cast<uint64_t>(dr) * 1024;
+                unsigned const gd = static_cast<unsigned>(blocksD < cap ? blocksD : cap);
+                uint32_t const slotd = static_cast<uint32_t>(slotBytes);
+#define VKT_DR(S, C, P, GG, KK) hipLaunchKernelGGL((resampleGatherDstRowKernel<S, S, C, P, GG, KK>), dim3(gd), dim3(kBlock), lds, s, b, slotd)
+#define VKT_DR_GK(S, C, P) do { if (G == 1) { if (KS == 1) VKT_DR(S, C, P, 1, 1); else VKT_DR(S, C, P, 1, 2); } \
+                                else { if (KS == 1) VKT_DR(S, C, P, 2, 1); else VKT_DR(S, C, P, 2, 2); } } while (0)
+                if (bs == 1)
+                {
+                    if (pad) { if (identity) VKT_DR_GK(1, false, true); else VKT_DR_GK(1, true, true); }
+                    else { if (identity) VKT_DR_GK(1, false, false); else VKT_DR_GK(1, true, false); }
+                }
+                else
+                {
+                    if (identity) VKT_DR_GK(2, false, false); else VKT_DR_GK(2, true, false);
+                }
+#undef VKT_DR_GK
+#undef VKT_DR
+                return true;
+            }
+        }
         int64_t const pk = rt::knob(rt::Knob::ResamplePrefetch);
         bool const prefetch = (pk == 2 || (pk == 1 && bd == 2)) && !detect && !chain && rowBytes <= 4096;
         // one task per wave; for 1-byte destinations a task writes so little (one 1-KiB store
@@ -987,6 +1129,8 @@ namespace hipk
         a.s0Z = t.aff[1][4]; a.d0Z = t.aff[1][5];
         a.k = t.k;
         a.zsrc = t.zsrc;
+        a.ysrc = t.ysrc;
+        a.fdDdy = makeFastDiv(static_cast<uint32_t>(dst.dimY));
         a.dnz = dst.dimZ;
         {
             static int const layout = [] {

@@ -77,6 +77,10 @@ namespace hipk
         // holds the epoch (no per-call zeroing: a stale equal value only costs a scan).
         uint32_t* anyDirtyOut;
         uint32_t epoch;
+        // dst-row gather (resampleGatherDstRowKernel): source row y of every dst row y (ddy
+        // entries) and a fast divisor by ddy
+        int32_t const* ysrc;
+        FastDiv fdDdy;
     };
 
     // Plane-layout launches are split into at most kMaxPlaneTasksPerLaunch one-wave workgroups
