@@ -135,7 +135,9 @@ VKTAPI vktError vktHipKernelScopeEnd(vktHipKernelScope scope);
  * "resample.prefetch" (0; 1 / 2: the LDS gather loads the next task's source row during the current
  * one for 2-byte / every destination), "resample.any_rows" (1; 0 sends source rows that are not
  * 16-B multiples to the per-voxel gather), "resample.lds_pad" (1; staged LDS rows get 16 B of
- * padding per 256 B -- LDS bank spread -- for UInt8 sources; 2 for every format, 0 none).
+ * padding per 256 B -- LDS bank spread -- for UInt8 sources; 2 for every format, 0 none),
+ * "resample.dst_rows" (1; the gather over destination-row tasks for UInt8 source rows that are not
+ * 16-B multiples; 0 off; >= 2 for every eligible 1- / 2-byte gather, grid cap in 1024s of workgroups).
  * The full list with defaults: volkit_amd/csrc/runtime/HipContext.cpp (kKnobs).
  * For tests and in-process A/B measurements; unknown names return
  * vktInvalidValue.

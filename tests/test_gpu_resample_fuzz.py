@@ -135,14 +135,15 @@ def test_resample_padded_lds_rows(g, o, pad, prefetch):
         lib.vktHipSetTuningKnob(b"resample.prefetch", -1)
 
 
-@pytest.mark.parametrize("cap", [1, 64])
+@pytest.mark.parametrize("cap", [2, 64, 1, 0])
 def test_resample_dst_row_gather(g, o, cap):
     """Knob resample.dst_rows (round 6): the LDS gather over destination-row tasks -- a fixed number
     of loads and stores per task, the next row's loads in flight across this task's stores
     (resampleGatherDstRowKernel) -- vs the oracle: UInt8 (padded and unpadded rows, a conversion)
     and UInt16, one and two store groups and source chunks, destination rows that are not whole
-    store groups (lanes repeat the last lane's store), a small grid (cap 1: waves loop over many
-    tasks) and a large one.  Rows beyond the kernel's limits take the source-row gather."""
+    store groups (lanes repeat the last lane's store), a small grid (cap 2: waves loop over many
+    tasks) and a large one, the default (1: UInt8 rows that are not 16-B multiples) and off (0).
+    Rows beyond the kernel's limits take the source-row gather."""
     from volkit_amd._lib import lib
     rng = np.random.default_rng(700 + cap)
     assert lib.vktHipSetTuningKnob(b"resample.dst_rows", cap) == 0

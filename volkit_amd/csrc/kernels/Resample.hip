@@ -964,8 +964,14 @@ namespace hipk
         // without vs 0.354-0.356 with, 768^3 -> 1024^3 0.500-0.503 vs 0.507-0.508; UInt8 equal.
         // The prefetched row's wait is a vmcnt(0) behind the task's stores either way (the store
         // count per task is not a compile-time constant).
-        // destination-row tasks (knob resample.dst_rows = grid cap in 1024s of workgroups, 0 off)
-        int64_t const dr = rt::knob(rt::Knob::ResampleDstRows);
+        // destination-row tasks (knob resample.dst_rows: 0 off, 1 (default) UInt8 rows that are not
+        // 16-B multiples with a 64 K-workgroup grid, >= 2 every eligible gather with a grid cap of
+        // that many 1024s of workgroups).  In-process A/B (profiles/r06/dstab.jsonl): UInt8
+        // 1000^3 -> 1024^3 0.407 -> 0.381 ms at cap 64; 768^3 -> 1024^3 and 1024^3 -> 768^3 UInt8
+        // equal (0.305-0.318 / 0.201-0.216 vs 0.308 / 0.201), UInt16 15-25 % slower
+        int64_t dr = rt::knob(rt::Knob::ResampleDstRows);
+        if (dr == 1)
+            dr = bs == 1 && bd == 1 && rowBytes % 16 != 0 ? 64 : 0;
         if (dr > 0 && !detect && !chain && bs == bd && bs <= 2 && rowBytes >= 16)
         {
             uint32_t const vd = 16 / bd;

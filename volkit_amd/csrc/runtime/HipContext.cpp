@@ -261,7 +261,7 @@ namespace rt
             {"histogram.pair_tiles", 1},
             {"resample.lds_pad", 1},
             {"decompose.row_image", 2},
-            {"resample.dst_rows", 0},
+            {"resample.dst_rows", 1},
         };
         static_assert(sizeof(kKnobs) / sizeof(kKnobs[0]) == static_cast<size_t>(Knob::Count), "knob table");
         std::atomic<int64_t> gKnobs[static_cast<int>(Knob::Count)] = {{kKnobs[0].def}, {kKnobs[1].def},

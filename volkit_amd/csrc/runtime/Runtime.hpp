@@ -139,7 +139,7 @@ namespace rt
         HistogramPairTiles,            // histograms of 2..4 tiles side by side in one launch (PAIR): 1 where P16 does not apply, 2 always, 0 never
         ResampleLdsPad,                // LDS gathers: 16 B of padding per 256 B of a staged row (bank spread): 1 UInt8 sources, 2 all, 0 none
         DecomposeRowImage,             // uniform grids of <= 16-KiB bricks through per-row LDS images (brickRowImageKernel): 2 UInt8, 1 all, 0 off
-        ResampleDstRows,               // > 0: LDS gathers over destination-row tasks (resampleGatherDstRowKernel), grid cap in 1024s of workgroups
+        ResampleDstRows,               // LDS gathers over destination-row tasks (resampleGatherDstRowKernel): 0 off, 1 UInt8 rows not 16-B multiples, >= 2 all (grid cap in 1024s of workgroups)
         Count
     };
     int64_t knob(Knob k);
