@@ -957,6 +957,9 @@ namespace hipk
         bool const pad = rowBytes % 16 == 0 && (padKnob == 2 || (padKnob == 1 && bs == 1));
         uint64_t const slotBytes = pad ? rowBytes + (rowBytes >> 8) * 16 : (rowBytes + 15) & ~uint64_t(15);
         uint64_t const lds = xtBytes + (kBlock / 64) * slotBytes;
+        if (rowBytes < 16 || (rowBytes % 16 != 0 && rt::knob(rt::Knob::ResampleAnyRows) == 0) ||
+            reinterpret_cast<uintptr_t>(b.src) % 16 != 0 || lds > 65536)
+            return false;
         // next-row prefetch (knob resample.prefetch): 1 for 2-byte destinations, 2 for every
         // destination, 0 (default since round 6) off.  Round 5 (profiles/r05/gatherp.jsonl): UInt16
         // 1024^3 -> 768^3 0.378 -> 0.358 ms with it, UInt8 lost.  Round 6, after the run tables
