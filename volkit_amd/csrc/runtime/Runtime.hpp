@@ -134,7 +134,7 @@ namespace rt
         PointwiseRowsKernel,           // multi-row boxes (32-bit rows, no scalar edges) on the MODE-1 kernel: bit 0 UInt8, bit 1 UInt16
         TransformShape,                // device-functor Transform vector kernels: 0 256x4, 1 64x2, 2 64x1 (read via vktHipGetTuningKnob)
         DecomposeDirect,               // halo-free aligned brick grids: 1 direct copy (small bricks P per workgroup), 2 one brick per workgroup, 0 LDS-staged
-        ResamplePrefetch,              // LDS gather loads the next task's row during the current one: 1 (default) 2-byte destinations, 2 all, 0 off
+        ResamplePrefetch,              // LDS gather loads the next task's row during the current one: 1 2-byte destinations, 2 all, 0 (default) off
         ResampleAnyRows,               // 1: the LDS gather also stages source rows that are not 16-B multiples (rowChunk)
         HistogramPairTiles,            // histograms of 2..4 tiles side by side in one launch (PAIR): 1 where P16 does not apply, 2 always, 0 never
         ResampleLdsPad,                // LDS gathers: 16 B of padding per 256 B of a staged row (bank spread): 1 UInt8 sources, 2 all, 0 none
