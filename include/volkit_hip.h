@@ -137,7 +137,10 @@ VKTAPI vktError vktHipKernelScopeEnd(vktHipKernelScope scope);
  * 16-B multiples to the per-voxel gather), "resample.lds_pad" (1; staged LDS rows get 16 B of
  * padding per 256 B -- LDS bank spread -- for UInt8 sources; 2 for every format, 0 none),
  * "resample.dst_rows" (1; the gather over destination-row tasks for UInt8 source rows that are not
- * 16-B multiples; 0 off; >= 2 for every eligible 1- / 2-byte gather, grid cap in 1024s of workgroups).
+ * 16-B multiples; 0 off; >= 2 for every eligible 1- / 2-byte gather, grid cap in 1024s of workgroups),
+ * "histogram.u16_codes" (1; UInt16 histograms whose bins are not integer functions of the code and
+ * exceed one LDS tile count the 65 536 codes in one pass and fold the counts into the bins; 2 also
+ * for bins beyond the replicated counters; 0 one pass per LDS tile / the global-atomic kernel).
  * The full list with defaults: volkit_amd/csrc/runtime/HipContext.cpp (kKnobs).
  * For tests and in-process A/B measurements; unknown names return
  * vktInvalidValue.

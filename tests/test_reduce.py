@@ -292,7 +292,11 @@ def test_histogram_packed16_counter_wraps(fmt, mapping, nbins, fill):
     idx = rng.choice(flat.size, 100000, replace=False)
     flat[idx] = rand_codes(rng, fmt, (100000,))
     full = ((0, 0, 0), (1024, 1024, 64))
-    got = gpu_histogram(codes, fmt, *mapping, *full, nbins)
+    lib.vktHipSetTuningKnob(b"histogram.u16_codes", 0)   # (UInt16 float bins: the P16 float path)
+    try:
+        got = gpu_histogram(codes, fmt, *mapping, *full, nbins)
+    finally:
+        lib.vktHipSetTuningKnob(b"histogram.u16_codes", -1)
     ref, _ = ob.histogram_range(ob.Volume(codes, fmt, *mapping), *full, nbins)
     np.testing.assert_array_equal(got, ref)
     # a padded sub-box (masked end items) through the same path
@@ -335,6 +339,7 @@ def test_histogram_pair_tiles(fmt, mapping, nbins):
     codes[5:9] = codes[5, 0, 0]      # constant planes: wave-uniform items
     vol = ob.Volume(codes, fmt, *mapping)
     lib.vktHipSetTuningKnob(b"histogram.pair_tiles", 2)   # also where P16 would take the bins
+    lib.vktHipSetTuningKnob(b"histogram.u16_codes", 0)    # (UInt16 float bins: not the code counts)
     try:
         for first, last in (((0, 0, 0), (256, 100, 40)), ((3, 1, 2), (250, 99, 37))):
             got = gpu_histogram(codes, fmt, *mapping, first, last, nbins)
@@ -342,6 +347,34 @@ def test_histogram_pair_tiles(fmt, mapping, nbins):
             np.testing.assert_array_equal(got, ref, err_msg=f"{first}->{last}")
     finally:
         lib.vktHipSetTuningKnob(b"histogram.pair_tiles", -1)
+        lib.vktHipSetTuningKnob(b"histogram.u16_codes", -1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mapping,nbins", [((-1.0, 3.0), 20000), ((-1.0, 3.0), 50000), ((0.0, 1.0), 100000),
+                                           ((0.25, 7.5), 150000), ((3.0, -1.0), 70000), ((0.0, 1e-3), 90000),
+                                           ((0.0, 1.0), 3000000), ((-1.0, 3.0), 65536)])
+def test_histogram_uint16_code_counts(mapping, nbins):
+    """Knob histogram.u16_codes (round 6): UInt16 bins that are not integer functions of the code
+    count the 65 536 codes in one pass (the packed-16 kernel with the identity bin) and fold the
+    counts into the bins with the reference's bin of the decoded value -- vs the oracle and vs the
+    per-voxel kernels (knob 0): float bins inside one tile (knob 2) and across 2-4 tiles, a
+    decreasing mapping and one that sends most codes out of range, 3 M bins (more tiles than the
+    streaming kernels take: the global-atomic kernel at knob 0), whole volume, padded sub-box, and
+    a constant region (one code, counts past the 16-bit counters' flush)."""
+    rng = np.random.default_rng(nbins)
+    codes = rand_codes(rng, 5, (40, 100, 256))
+    codes[5:30] = 40000                       # 640 000 voxels of one code
+    vol = ob.Volume(codes, 5, *mapping)
+    try:
+        for first, last in (((0, 0, 0), (256, 100, 40)), ((3, 1, 2), (250, 99, 37))):
+            ref, _ = ob.histogram_range(vol, first, last, nbins)
+            for k in (1, 2, 0):
+                lib.vktHipSetTuningKnob(b"histogram.u16_codes", k)
+                got = gpu_histogram(codes, 5, *mapping, first, last, nbins)
+                np.testing.assert_array_equal(got, ref, err_msg=f"knob={k} {first}->{last}")
+    finally:
+        lib.vktHipSetTuningKnob(b"histogram.u16_codes", -1)
 
 
 def takes_moments(fmt, mapping):

@@ -1042,6 +1042,34 @@ def main():
         del arr, V
         ep.device = vkt.ExecutionPolicy.Device_CPU
         vkt.SetThreadExecutionPolicy(ep)
+    if want("u16codes"):
+        # knob histogram.u16_codes: UInt16 float-formula bins through one pass of code counts and a
+        # fold (1: beyond one LDS tile, 2: also single-tile bins) vs the per-voxel kernels (0)
+        n = 1024
+        bins = C.c_void_p()
+        lib.vktHipAllocate(C.byref(bins), 1000000 * 8)
+        last = Vec3i_t(n, n, n)
+        try:
+            for lo, hi in ((0.0, 1.0), (-1.0, 3.0)):
+                V = alloc((n,) * 3, 5, lo, hi, seed=11)
+                cases = (20000, 100000, 150000, 1000000) if lo == 0.0 else (20000, 50000, 65536)
+                for nb in cases:
+                    for rep in range(2):
+                        for k in (0, 1, 2):
+                            lib.vktHipSetTuningKnob(b"histogram.u16_codes", k)
+                            ms = timed(lambda: lib.vktHipHistogramRange(V, o, last, bins, nb, 0), R)
+                            report(f"u16codes Histogram 1024^3 UInt16 map=({lo},{hi}) {nb} bins [u16_codes={k}]", ms,
+                                   2 * n ** 3, n ** 3)
+                u0, u1 = Vec3i_t(100, 100, 100), Vec3i_t(900, 900, 900)
+                for k in (0, 1):
+                    lib.vktHipSetTuningKnob(b"histogram.u16_codes", k)
+                    ms = timed(lambda: lib.vktHipHistogramRange(V, u0, u1, bins, 100000, 0), R)
+                    report(f"u16codes Histogram 800^3 at x0=100 UInt16 map=({lo},{hi}) 100000 bins [u16_codes={k}]",
+                           ms, 2 * 800 ** 3, 800 ** 3)
+                free(V)
+        finally:
+            lib.vktHipSetTuningKnob(b"histogram.u16_codes", -1)
+            lib.vktHipFree(bins)
     if want("pairtiles"):
         # knob histogram.pair_tiles: the tiles of a > 40 704-bin histogram side by side in one
         # launch (XCD-grouped workgroups) vs P16 (65 536 bins) / one pass per tile (more bins)
@@ -1049,6 +1077,7 @@ def main():
         bins = C.c_void_p()
         lib.vktHipAllocate(C.byref(bins), 150000 * 8)
         last = Vec3i_t(n, n, n)
+        lib.vktHipSetTuningKnob(b"histogram.u16_codes", 0)   # (the tiled kernels, not the code counts)
         try:
             for fmt, b in ((5, 2), (7, 4)):
                 V = alloc((n,) * 3, fmt, seed=11 if fmt == 5 else None)
@@ -1070,6 +1099,7 @@ def main():
                 free(V)
         finally:
             lib.vktHipSetTuningKnob(b"histogram.pair_tiles", -1)
+            lib.vktHipSetTuningKnob(b"histogram.u16_codes", -1)
             lib.vktHipFree(bins)
     if want("reduce"):
         # ComputeHistogram / ComputeAggregates on a device-resident 1024^3 UInt16

@@ -2366,6 +2366,66 @@ namespace hipk
             atomicAdd(&bins[b], counts[c]);
     }
 
+    // UInt16 histogram from code counts: bins[bin(c)] += counts[c] for the 65 536 codes, with the
+    // reference's bin of the decoded value (binOf: any bin count, out-of-range and NaN dropped)
+    __global__ __launch_bounds__(256) void histogramFromCodesU16Kernel(unsigned long long const* counts, float lo,
+                                                                     float hi, float scale, uint64_t numBins,
+                                                                     unsigned long long* bins)
+    {
+        uint32_t const c = blockIdx.x * 256u + threadIdx.x;
+        unsigned long long const n = counts[c];
+        if (n == 0ull)
+            return;
+        uint64_t const b = binOf(codec::decode(c, codec::FmtUInt16, lo, hi), lo, scale, numBins);
+        if (b < numBins)
+            atomicAdd(&bins[b], n);
+    }
+
+    // UInt16 bins that are not a function of code >> s / (code * n) >> 16 and do not fit one LDS
+    // tile (knob histogram.u16_codes): a UInt16 voxel holds one of 65 536
+    // codes and its bin depends on the code alone, so the data pass counts codes -- the P16
+    // kernel with the identity bin (SHIFT, code >> 0), one pass whatever the bin count -- and a
+    // 65 536-thread kernel folds the counts into the bins.  Same counts as the per-voxel bin, by
+    // construction.
+    bool launchU16CodeHistogram(FastHistArgs const& h, bool contig, uint32_t tileCap, BoxArgs const& a,
+                                HistArgs const& hh, hipStream_t s)
+    {
+        if (32768u > tileCap)   // 65 536 packed 16-bit counters in one workgroup's LDS
+            return false;
+        static rt::StreamScratch scratch;
+        auto* const counts = static_cast<unsigned long long*>(scratch.acquire(65536 * sizeof(unsigned long long), s));
+        if (!counts)
+            return false;
+        FastHistArgs c = h;
+        c.bins = counts;
+        c.nb = 65536u;
+        c.nbf = 65536.0f;
+        c.binShift = 0u;
+        c.binMul = 1u;
+        c.rShift = 0u;
+        c.tileBase = 0u;
+        c.tileBins = 65536u;
+        c.pairTiles = 0u;
+        c.p16Step = rt::knob(rt::Knob::HistogramP16Step) != 0 ? 1u : 0u;
+        bool ok = hipMemsetAsync(counts, 0, 65536 * sizeof(unsigned long long), s) == hipSuccess;
+        if (ok)
+        {
+            unsigned const g = streamingGrid(c.items, 64u * 4u * (kTileBlock / 64), 1);
+            size_t const lds = 32768u * 4u;
+            if (contig)
+                hipLaunchKernelGGL((histogramFastKernel<codec::FmtUInt16, true, true, kTileBlock, true, true>), dim3(g),
+                                   dim3(kTileBlock), lds, s, c);
+            else
+                hipLaunchKernelGGL((histogramFastKernel<codec::FmtUInt16, false, true, kTileBlock, true, true>), dim3(g),
+                                   dim3(kTileBlock), lds, s, c);
+            hipLaunchKernelGGL(histogramFromCodesU16Kernel, dim3(256), dim3(256), 0, s, counts, a.lo, a.hi, hh.scale,
+                               hh.numBins, hh.bins);
+            ok = hipGetLastError() == hipSuccess;
+        }
+        scratch.release(s);
+        return ok;
+    }
+
     // Launches histogramFastKernel when the range qualifies (see its comment); false otherwise.
     bool launchFastHistogram(BoxArgs const& a, HistArgs const& hh, hipStream_t s)
     {
@@ -2373,11 +2433,24 @@ namespace hipk
         // LDS counters of one 1024-thread workgroup (the device limit minus the static table)
         uint32_t const tileCap = (ldsBinCapacity() * 4u - 1024u) / 4u;
         uint64_t const tiles = (hh.numBins + tileCap - 1) / tileCap;
-        if (tiles > kFastMaxTiles)
-            return false;
         FastHistArgs h;
         bool contig;
         if (!makeSpanArgs(a, h, contig))
+            return false;
+        // UInt16 code counts (knob histogram.u16_codes: 1 (default) bins beyond one LDS tile, 2
+        // also single-tile bins beyond the replicated counters, 0 off); integer bins keep the
+        // streaming kernels below
+        int64_t const u16k = rt::knob(rt::Knob::HistogramU16Codes);
+        if (fmt == codec::FmtUInt16 && u16k > 0 && (tiles > 1 || (u16k == 2 && hh.numBins > kReplicatedMaxBins)))
+        {
+            bool integerBins = codec::isUnitMapping(a.lo, a.hi) && hh.numBins <= 65536u &&
+                               (hh.numBins & (hh.numBins - 1)) == 0 && hh.scale == static_cast<float>(hh.numBins);
+            if (!integerBins && rt::knob(rt::Knob::HistogramMulShift) != 0)
+                integerBins = mulShiftBinsU16(a.lo, a.hi, hh.scale, hh.numBins);
+            if (!integerBins && launchU16CodeHistogram(h, contig, tileCap, a, hh, s))
+                return true;
+        }
+        if (tiles > kFastMaxTiles)
             return false;
         uint64_t const items = h.items;
         h.scale = hh.scale;

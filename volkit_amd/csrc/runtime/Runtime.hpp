@@ -140,6 +140,7 @@ namespace rt
         ResampleLdsPad,                // LDS gathers: 16 B of padding per 256 B of a staged row (bank spread): 1 UInt8 sources, 2 all, 0 none
         DecomposeRowImage,             // uniform grids of <= 16-KiB bricks through per-row LDS images (brickRowImageKernel): 2 UInt8, 1 all, 0 off
         ResampleDstRows,               // LDS gathers over destination-row tasks (resampleGatherDstRowKernel): 0 off, 1 UInt8 rows not 16-B multiples, >= 2 all (grid cap in 1024s of workgroups)
+        HistogramU16Codes,             // UInt16 float-formula bins through code counts + fold: 1 (default) beyond one LDS tile, 2 also beyond the replicated counters, 0 off
         Count
     };
     int64_t knob(Knob k);
