@@ -353,25 +353,27 @@ def test_histogram_pair_tiles(fmt, mapping, nbins):
 @pytest.mark.gpu
 @pytest.mark.parametrize("mapping,nbins", [((-1.0, 3.0), 20000), ((-1.0, 3.0), 50000), ((0.0, 1.0), 100000),
                                            ((0.25, 7.5), 150000), ((3.0, -1.0), 70000), ((0.0, 1e-3), 90000),
-                                           ((0.0, 1.0), 3000000), ((-1.0, 3.0), 65536)])
-def test_histogram_uint16_code_counts(mapping, nbins):
+                                           ((0.0, 1.0), 3000000), ((-1.0, 3.0), 65536), ((0.0, 1.0), 256)])
+@pytest.mark.parametrize("fmt", [5, 2])
+def test_histogram_uint16_code_counts(fmt, mapping, nbins):
     """Knob histogram.u16_codes (round 6): UInt16 bins that are not integer functions of the code
     count the 65 536 codes in one pass (the packed-16 kernel with the identity bin) and fold the
     counts into the bins with the reference's bin of the decoded value -- vs the oracle and vs the
     per-voxel kernels (knob 0): float bins inside one tile (knob 2) and across 2-4 tiles, a
     decreasing mapping and one that sends most codes out of range, 3 M bins (more tiles than the
     streaming kernels take: the global-atomic kernel at knob 0), whole volume, padded sub-box, and
-    a constant region (one code, counts past the 16-bit counters' flush)."""
-    rng = np.random.default_rng(nbins)
-    codes = rand_codes(rng, 5, (40, 100, 256))
+    a constant region (one code, counts past the 16-bit counters' flush).  Int16 (fmt 2) volumes
+    take the counts of their raw codes for every bin count (knob 0: the per-row kernel)."""
+    rng = np.random.default_rng(nbins + fmt)
+    codes = rand_codes(rng, fmt, (40, 100, 256))
     codes[5:30] = 40000                       # 640 000 voxels of one code
-    vol = ob.Volume(codes, 5, *mapping)
+    vol = ob.Volume(codes, fmt, *mapping)
     try:
         for first, last in (((0, 0, 0), (256, 100, 40)), ((3, 1, 2), (250, 99, 37))):
             ref, _ = ob.histogram_range(vol, first, last, nbins)
             for k in (1, 2, 0):
                 lib.vktHipSetTuningKnob(b"histogram.u16_codes", k)
-                got = gpu_histogram(codes, 5, *mapping, first, last, nbins)
+                got = gpu_histogram(codes, fmt, *mapping, first, last, nbins)
                 np.testing.assert_array_equal(got, ref, err_msg=f"knob={k} {first}->{last}")
     finally:
         lib.vktHipSetTuningKnob(b"histogram.u16_codes", -1)

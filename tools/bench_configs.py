@@ -1067,6 +1067,14 @@ def main():
                     report(f"u16codes Histogram 800^3 at x0=100 UInt16 map=({lo},{hi}) 100000 bins [u16_codes={k}]",
                            ms, 2 * 800 ** 3, 800 ** 3)
                 free(V)
+            V = alloc((n,) * 3, 2, seed=11)   # Int16: the per-row kernel (0) vs the code counts (1)
+            for nb in (256, 100000):
+                for rep in range(2):
+                    for k in (0, 1):
+                        lib.vktHipSetTuningKnob(b"histogram.u16_codes", k)
+                        ms = timed(lambda: lib.vktHipHistogramRange(V, o, last, bins, nb, 0), R)
+                        report(f"u16codes Histogram 1024^3 Int16 {nb} bins [u16_codes={k}]", ms, 2 * n ** 3, n ** 3)
+            free(V)
         finally:
             lib.vktHipSetTuningKnob(b"histogram.u16_codes", -1)
             lib.vktHipFree(bins)

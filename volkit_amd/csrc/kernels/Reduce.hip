@@ -2366,17 +2366,18 @@ namespace hipk
             atomicAdd(&bins[b], counts[c]);
     }
 
-    // UInt16 histogram from code counts: bins[bin(c)] += counts[c] for the 65 536 codes, with the
-    // reference's bin of the decoded value (binOf: any bin count, out-of-range and NaN dropped)
-    __global__ __launch_bounds__(256) void histogramFromCodesU16Kernel(unsigned long long const* counts, float lo,
-                                                                     float hi, float scale, uint64_t numBins,
-                                                                     unsigned long long* bins)
+    // 16-bit histogram from code counts: bins[bin(c)] += counts[c] for the 65 536 codes (UInt16 or
+    // Int16 `fmt`), with the reference's bin of the decoded value (binOf: any bin count,
+    // out-of-range and NaN dropped)
+    __global__ __launch_bounds__(256) void histogramFromCodesU16Kernel(unsigned long long const* counts, int32_t fmt,
+                                                                     float lo, float hi, float scale,
+                                                                     uint64_t numBins, unsigned long long* bins)
     {
         uint32_t const c = blockIdx.x * 256u + threadIdx.x;
         unsigned long long const n = counts[c];
         if (n == 0ull)
             return;
-        uint64_t const b = binOf(codec::decode(c, codec::FmtUInt16, lo, hi), lo, scale, numBins);
+        uint64_t const b = binOf(codec::decode(c, fmt, lo, hi), lo, scale, numBins);
         if (b < numBins)
             atomicAdd(&bins[b], n);
     }
@@ -2386,7 +2387,8 @@ namespace hipk
     // codes and its bin depends on the code alone, so the data pass counts codes -- the P16
     // kernel with the identity bin (SHIFT, code >> 0), one pass whatever the bin count -- and a
     // 65 536-thread kernel folds the counts into the bins.  Same counts as the per-voxel bin, by
-    // construction.
+    // construction.  Int16 volumes take the same counts of their raw 16-bit codes (the streaming
+    // kernels below read only UInt8 / UInt16 / Float32).
     bool launchU16CodeHistogram(FastHistArgs const& h, bool contig, uint32_t tileCap, BoxArgs const& a,
                                 HistArgs const& hh, hipStream_t s)
     {
@@ -2418,8 +2420,8 @@ namespace hipk
             else
                 hipLaunchKernelGGL((histogramFastKernel<codec::FmtUInt16, false, true, kTileBlock, true, true>), dim3(g),
                                    dim3(kTileBlock), lds, s, c);
-            hipLaunchKernelGGL(histogramFromCodesU16Kernel, dim3(256), dim3(256), 0, s, counts, a.lo, a.hi, hh.scale,
-                               hh.numBins, hh.bins);
+            hipLaunchKernelGGL(histogramFromCodesU16Kernel, dim3(256), dim3(256), 0, s, counts, a.fmt, a.lo, a.hi,
+                               hh.scale, hh.numBins, hh.bins);
             ok = hipGetLastError() == hipSuccess;
         }
         scratch.release(s);
@@ -2435,12 +2437,17 @@ namespace hipk
         uint64_t const tiles = (hh.numBins + tileCap - 1) / tileCap;
         FastHistArgs h;
         bool contig;
-        if (!makeSpanArgs(a, h, contig))
+        BoxArgs a16 = a;   // (Int16: the span of its raw 16-bit codes)
+        if (fmt == codec::FmtInt16)
+            a16.fmt = codec::FmtUInt16;
+        if (!makeSpanArgs(a16, h, contig))
             return false;
-        // UInt16 code counts (knob histogram.u16_codes: 1 (default) bins beyond one LDS tile, 2
-        // also single-tile bins beyond the replicated counters, 0 off); integer bins keep the
-        // streaming kernels below
+        // 16-bit code counts (knob histogram.u16_codes: 1 (default) UInt16 bins beyond one LDS
+        // tile and every Int16 histogram, 2 also UInt16 single-tile bins beyond the replicated
+        // counters, 0 off); integer UInt16 bins keep the streaming kernels below
         int64_t const u16k = rt::knob(rt::Knob::HistogramU16Codes);
+        if (fmt == codec::FmtInt16)
+            return u16k > 0 && launchU16CodeHistogram(h, contig, tileCap, a, hh, s);
         if (fmt == codec::FmtUInt16 && u16k > 0 && (tiles > 1 || (u16k == 2 && hh.numBins > kReplicatedMaxBins)))
         {
             bool integerBins = codec::isUnitMapping(a.lo, a.hi) && hh.numBins <= 65536u &&
