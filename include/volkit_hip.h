@@ -138,9 +138,11 @@ VKTAPI vktError vktHipKernelScopeEnd(vktHipKernelScope scope);
  * padding per 256 B -- LDS bank spread -- for UInt8 sources; 2 for every format, 0 none),
  * "resample.dst_rows" (1; the gather over destination-row tasks for UInt8 source rows that are not
  * 16-B multiples; 0 off; >= 2 for every eligible 1- / 2-byte gather, grid cap in 1024s of workgroups),
- * "histogram.u16_codes" (1; UInt16 histograms whose bins are not integer functions of the code and
- * exceed one LDS tile count the 65 536 codes in one pass and fold the counts into the bins; 2 also
- * for bins beyond the replicated counters; 0 one pass per LDS tile / the global-atomic kernel).
+ * "histogram.u16_codes" (2; UInt16 histograms whose bins are not integer functions of the code and
+ * exceed the replicated LDS counters, and every Int16 histogram, count the 65 536 codes in one pass
+ * and fold the counts into the bins; 1 only UInt16 bins beyond one LDS tile; 0 the per-voxel
+ * kernels), "histogram.partials" (1; packed-16 histogram workgroups store their counter words and
+ * one kernel sums them instead of a 64-bit atomic per counter; 2 every tiled launch; 0 atomics).
  * The full list with defaults: volkit_amd/csrc/runtime/HipContext.cpp (kKnobs).
  * For tests and in-process A/B measurements; unknown names return
  * vktInvalidValue.

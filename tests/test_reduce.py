@@ -379,6 +379,45 @@ def test_histogram_uint16_code_counts(fmt, mapping, nbins):
         lib.vktHipSetTuningKnob(b"histogram.u16_codes", -1)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("partials", [1, 2, 0])
+def test_histogram_partials(partials):
+    """Knob histogram.partials (round 6): tiled histogram launches store per-workgroup counter words
+    that one kernel sums (1: packed-16 launches, 2: every tiled launch) instead of 64-bit atomics
+    per counter (0) -- vs the oracle on every tiled
+    path: packed-16 integer bins (with the in-run 2^14 flushes of a constant region), packed-16
+    float bins, single-tile and multi-tile (one launch per tile) 32-bit counters, the 16-bit code
+    counts (UInt16 float bins, Int16), whole volumes, a padded sub-box and a one-plane volume
+    (fewer workgroups than the grid cap)."""
+    rng = np.random.default_rng(31 + partials)
+    assert lib.vktHipSetTuningKnob(b"histogram.partials", partials) == 0
+    try:
+        for fmt, mapping, nbins, knobs in ((5, (0.0, 1.0), 65536, ()), (5, (-1.0, 3.0), 20000, ()),
+                                           (7, (0.0, 1.0), 65536, ()), (7, (0.0, 1.0), 100000, ()),
+                                           (7, (0.0, 1.0), 150000, ((b"histogram.pair_tiles", 0),)),
+                                           (5, (0.0, 1.0), 100000, ()), (2, (-1.0, 3.0), 256, ()),
+                                           (5, (-1.0, 3.0), 50000, ((b"histogram.u16_codes", 0),))):
+            for dims in ((256, 100, 40), (512, 64, 1)):
+                codes = rand_codes(rng, fmt, dims[::-1], specials=True)
+                codes[:, 10:30] = codes[0, 0, 0]      # a constant slab (run registers, flushes)
+                vol = ob.Volume(codes, fmt, *mapping)
+                boxes = [((0, 0, 0), dims)]
+                if dims[2] > 1:
+                    boxes.append(((3, 1, 2), (dims[0] - 5, dims[1] - 1, dims[2] - 3)))
+                for k, v in knobs:
+                    lib.vktHipSetTuningKnob(k, v)
+                try:
+                    for first, last in boxes:
+                        got = gpu_histogram(codes, fmt, *mapping, first, last, nbins)
+                        ref, _ = ob.histogram_range(vol, first, last, nbins)
+                        np.testing.assert_array_equal(got, ref, err_msg=f"fmt={fmt} nb={nbins} {first}->{last}")
+                finally:
+                    for k, _ in knobs:
+                        lib.vktHipSetTuningKnob(k, -1)
+    finally:
+        lib.vktHipSetTuningKnob(b"histogram.partials", -1)
+
+
 def takes_moments(fmt, mapping):
     """UInt16 (integer moments under the unit mapping, float moments otherwise) and Float32 (float
     moments) take the one-pass moments paths (aggregates.moments)."""

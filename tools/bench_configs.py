@@ -18,7 +18,7 @@ import torch  # noqa: E402
 from volkit_amd import _lib  # noqa: E402
 from volkit_amd._lib import lib, HipVolumeView_t, Vec3i_t  # noqa: E402
 
-BPV = {4: 1, 5: 2, 7: 4, 2: 2, 6: 4}
+BPV = {4: 1, 5: 2, 7: 4, 2: 2, 6: 4, 1: 1, 3: 4}
 
 
 def alloc(dims, fmt, lo=0.0, hi=1.0, seed=None):
@@ -1042,6 +1042,83 @@ def main():
         del arr, V
         ep.device = vkt.ExecutionPolicy.Device_CPU
         vkt.SetThreadExecutionPolicy(ep)
+    if want("fmts"):
+        # every data format through each hot-path call at 512^3 (per-format fall-backs show up as
+        # outliers): Fill, Copy, SumRange, SafeSum, Resample up (integer ratio) / down (gather),
+        # Aggregates, Histogram 256 bins
+        m = 512
+        lastm = Vec3i_t(m, m, m)
+        bins = C.c_void_p()
+        lib.vktHipAllocate(C.byref(bins), 256 * 8)
+        names = {1: "Int8", 2: "Int16", 3: "Int32", 4: "UInt8", 5: "UInt16", 6: "UInt32", 7: "Float32"}
+        try:
+            for fmt in (4, 5, 7, 2, 6):   # (Int8 / Int32: the reference's codec leaves them untouched)
+                b = BPV[fmt]
+                A, B2, D = alloc((m,) * 3, fmt, seed=1), alloc((m,) * 3, fmt, seed=2), alloc((m,) * 3, fmt)
+                if fmt == 7:
+                    rng_fill(A, m ** 3)
+                    rng_fill(B2, m ** 3)
+                nv = m ** 3
+                nm = names[fmt]
+                report(f"fmts FillRange 512^3 {nm}", timed(lambda: lib.vktHipFillRange(D, o, lastm, C.c_float(0.3)), R),
+                       b * nv, nv)
+                report(f"fmts CopyRange 512^3 {nm}", timed(lambda: lib.vktHipCopyRange(D, A, o, lastm, o), R), 2 * b * nv, nv)
+                report(f"fmts SumRange 512^3 {nm}", timed(lambda: lib.vktHipArithmeticRange(0, D, A, B2, o, lastm, o), R),
+                       3 * b * nv, nv)
+                report(f"fmts SafeSumRange 512^3 {nm}",
+                       timed(lambda: lib.vktHipArithmeticRange(5, D, A, B2, o, lastm, o), R), 3 * b * nv, nv)
+                S = alloc((256,) * 3, fmt, seed=3)
+                report(f"fmts Resample 256^3->512^3 {nm} Linear", timed(lambda: lib.vktHipResample(D, S, 1), R),
+                       b * 256 ** 3 + b * nv, nv)
+                Rd = alloc((384,) * 3, fmt)
+                report(f"fmts Resample 512^3->384^3 {nm} Nearest", timed(lambda: lib.vktHipResample(Rd, A, 0), R),
+                       resample_bytes((m,) * 3, (384,) * 3, b, b), 384 ** 3)
+                agg = _lib.Aggregates_t()
+                report(f"fmts Aggregates 512^3 {nm}", timed(lambda: lib.vktHipAggregatesRange(A, o, lastm, C.byref(agg)), R),
+                       b * nv, nv)
+                report(f"fmts Histogram 512^3 {nm} 256 bins",
+                       timed(lambda: lib.vktHipHistogramRange(A, o, lastm, bins, 256, 0), R), b * nv, nv)
+                free(A, B2, D, S, Rd)
+        finally:
+            lib.vktHipFree(bins)
+    if want("p16size"):
+        # the packed-16 histogram (UInt16, 65 536 integer bins) over volume sizes: time vs voxels
+        bins = C.c_void_p()
+        lib.vktHipAllocate(C.byref(bins), 65536 * 8)
+        try:
+            for n in (256, 512, 768, 1024):
+                last = Vec3i_t(n, n, n)
+                V = alloc((n,) * 3, 5, seed=11)
+                ms = timed(lambda: lib.vktHipHistogramRange(V, o, last, bins, 65536, 0), R)
+                report(f"p16size Histogram {n}^3 UInt16 65536 bins", ms, 2 * n ** 3, n ** 3)
+                free(V)
+        finally:
+            lib.vktHipFree(bins)
+    if want("partials"):
+        # knob histogram.partials: tiled histogram launches store per-workgroup counts summed by
+        # one kernel (1) vs global 64-bit atomics per counter (0)
+        bins = C.c_void_p()
+        lib.vktHipAllocate(C.byref(bins), 200000 * 8)
+        try:
+            for n in (1024, 512):
+                last = Vec3i_t(n, n, n)
+                for fmt, lo, hi, nbs in ((5, 0.0, 1.0, (65536, 100000)), (5, -1.0, 3.0, (20000, 65536)),
+                                         (7, 0.0, 1.0, (20000, 65536, 150000)), (2, 0.0, 1.0, (256,))):
+                    b = BPV[fmt]
+                    V = alloc((n,) * 3, fmt, lo, hi, seed=11 if fmt != 7 else None)
+                    if fmt == 7:
+                        rng_fill(V, n ** 3)
+                    for nb in nbs:
+                        for rep in range(2):
+                            for k in (0, 1, 2):
+                                lib.vktHipSetTuningKnob(b"histogram.partials", k)
+                                ms = timed(lambda: lib.vktHipHistogramRange(V, o, last, bins, nb, 0), R)
+                                report(f"partials Histogram {n}^3 fmt={fmt} map=({lo},{hi}) {nb} bins [partials={k}]",
+                                       ms, b * n ** 3, n ** 3)
+                    free(V)
+        finally:
+            lib.vktHipSetTuningKnob(b"histogram.partials", -1)
+            lib.vktHipFree(bins)
     if want("u16codes"):
         # knob histogram.u16_codes: UInt16 float-formula bins through one pass of code counts and a
         # fold (1: beyond one LDS tile, 2: also single-tile bins) vs the per-voxel kernels (0)

@@ -386,6 +386,7 @@ namespace hipk
         uint32_t padded;
         uint32_t rows;              // codeCountsU8RowsKernel: range rows (ny * nz)
         uint32_t pairTiles;         // PAIR: tiles counted side by side in one launch (tileBins each)
+        uint32_t* partials;         // TILED, not PAIR: per-workgroup counts [blockIdx.x][tileBins] (no atomics)
     };
 
     typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -789,11 +790,23 @@ namespace hipk
         __syncthreads();
         if constexpr (TILED)
         {
-            for (uint32_t t = threadIdx.x; t < h.tileBins; t += BLOCK)
+            if (!PAIR && h.partials != nullptr)
             {
-                uint32_t const c = P16 ? (cnt[t >> 1] >> ((t & 1u) << 4)) & 0xFFFFu : cnt[t];
-                if (c)
-                    atomicAdd(&h.bins[h.tileBase + t], static_cast<unsigned long long>(c));
+                // this workgroup's counter words as they are (P16: two 16-bit counts per word),
+                // every one written; histogramPartialsKernel sums them
+                uint32_t const words = P16 ? (h.tileBins + 1) / 2 : h.tileBins;
+                uint32_t* const out = h.partials + static_cast<uint64_t>(blockIdx.x) * words;
+                for (uint32_t t = threadIdx.x; t < words; t += BLOCK)
+                    __builtin_nontemporal_store(cnt[t], out + t);
+            }
+            else
+            {
+                for (uint32_t t = threadIdx.x; t < h.tileBins; t += BLOCK)
+                {
+                    uint32_t const c = P16 ? (cnt[t >> 1] >> ((t & 1u) << 4)) & 0xFFFFu : cnt[t];
+                    if (c)
+                        atomicAdd(&h.bins[h.tileBase + t], static_cast<unsigned long long>(c));
+                }
             }
         }
         else
@@ -2366,20 +2379,103 @@ namespace hipk
             atomicAdd(&bins[b], counts[c]);
     }
 
+    // bins += the workgroups' partial counter words (tiled histogram launches with
+    // FastHistArgs::partials): one thread per word and slice of
+    // kPartialRows workgroup rows (loads coalesced along the row, all of a thread's in flight),
+    // one 64-bit atomic per nonzero count and slice; PACKED words hold two 16-bit counts.  The
+    // data kernel's in-run flushes reached bins first (same stream).
+    constexpr uint32_t kPartialRows = 32;
+    template <bool PACKED>
+    __global__ __launch_bounds__(256) void histogramPartialsKernel(uint32_t const* partials, uint32_t groups,
+                                                                 uint32_t words, uint32_t tileBins,
+                                                                 unsigned long long* bins)
+    {
+        uint32_t const w = blockIdx.x * 256u + threadIdx.x;
+        if (w >= words)
+            return;
+        uint32_t const r0 = blockIdx.y * kPartialRows;
+        uint32_t const r1 = min(groups, r0 + kPartialRows);
+        uint32_t lo = 0, hi = 0;   // (<= 32 rows of < 2^16 / 2^32 - per-workgroup counts: no overflow for PACKED)
+        unsigned long long wide = 0ull;
+#pragma unroll 8
+        for (uint32_t r = r0; r < r1; ++r)
+        {
+            uint32_t const v = __builtin_nontemporal_load(partials + static_cast<uint64_t>(r) * words + w);
+            if constexpr (PACKED)
+            {
+                lo += v & 0xFFFFu;
+                hi += v >> 16;
+            }
+            else
+                wide += v;
+        }
+        if constexpr (PACKED)
+        {
+            if (lo != 0u)
+                atomicAdd(&bins[2 * w], static_cast<unsigned long long>(lo));
+            if (hi != 0u && 2 * w + 1 < tileBins)
+                atomicAdd(&bins[2 * w + 1], static_cast<unsigned long long>(hi));
+        }
+        else if (wide != 0ull)
+            atomicAdd(&bins[w], wide);
+    }
+
+    // A tiled (not PAIR) histogram launch of g workgroups over tileBins bins starting at
+    // h.bins + h.tileBase: with knob histogram.partials (1, default: packed-16 launches; 2: every
+    // tiled launch) the workgroups store their counter words and histogramPartialsKernel sums
+    // them, instead of one global 64-bit atomic per nonzero counter and workgroup (256 x 65 536
+    // for a packed-16 histogram: ~70 us of its ~0.5 ms at 1024^3, most of its time at 256^3).
+    template <bool P16, typename Launch>
+    void tiledWithPartials(FastHistArgs& h, unsigned g, hipStream_t s, Launch&& launch)
+    {
+        static rt::StreamScratch scratch;
+        uint32_t* parts = nullptr;
+        int64_t const k = rt::knob(rt::Knob::HistogramPartials);
+        uint32_t const words = P16 ? (h.tileBins + 1) / 2 : h.tileBins;
+        if (k == 2 || (k == 1 && P16))
+            parts = static_cast<uint32_t*>(scratch.acquire(static_cast<size_t>(g) * words * sizeof(uint32_t), s));
+        h.partials = parts;
+        launch();
+        if (parts != nullptr)
+        {
+            dim3 const grid((words + 255) / 256, (g + kPartialRows - 1) / kPartialRows);
+            hipLaunchKernelGGL((histogramPartialsKernel<P16>), grid, dim3(256), 0, s, parts, g, words, h.tileBins,
+                               h.bins + h.tileBase);
+            scratch.release(s);
+        }
+        h.partials = nullptr;
+    }
+
     // 16-bit histogram from code counts: bins[bin(c)] += counts[c] for the 65 536 codes (UInt16 or
     // Int16 `fmt`), with the reference's bin of the decoded value (binOf: any bin count,
-    // out-of-range and NaN dropped)
+    // out-of-range and NaN dropped).  A thread folds kFoldCodes consecutive codes, adding a run of
+    // codes on one bin with one atomic (the decode is monotonic along a run of codes, so few bins
+    // hold many codes: one atomic per code put ~256 adds on each of 256 bins, serialised).
+    constexpr uint32_t kFoldCodes = 16;
     __global__ __launch_bounds__(256) void histogramFromCodesU16Kernel(unsigned long long const* counts, int32_t fmt,
                                                                      float lo, float hi, float scale,
                                                                      uint64_t numBins, unsigned long long* bins)
     {
-        uint32_t const c = blockIdx.x * 256u + threadIdx.x;
-        unsigned long long const n = counts[c];
-        if (n == 0ull)
-            return;
-        uint64_t const b = binOf(codec::decode(c, fmt, lo, hi), lo, scale, numBins);
-        if (b < numBins)
-            atomicAdd(&bins[b], n);
+        uint32_t const c0 = (blockIdx.x * 256u + threadIdx.x) * kFoldCodes;
+        uint64_t runBin = ~0ull;
+        unsigned long long run = 0ull;
+        for (uint32_t c = c0; c < c0 + kFoldCodes; ++c)
+        {
+            unsigned long long const n = counts[c];
+            if (n == 0ull)
+                continue;
+            uint64_t const b = binOf(codec::decode(c, fmt, lo, hi), lo, scale, numBins);
+            if (b != runBin)
+            {
+                if (run != 0ull && runBin < numBins)
+                    atomicAdd(&bins[runBin], run);
+                runBin = b;
+                run = 0ull;
+            }
+            run += n;
+        }
+        if (run != 0ull && runBin < numBins)
+            atomicAdd(&bins[runBin], run);
     }
 
     // UInt16 bins that are not a function of code >> s / (code * n) >> 16 and do not fit one LDS
@@ -2414,18 +2510,20 @@ namespace hipk
         {
             unsigned const g = streamingGrid(c.items, 64u * 4u * (kTileBlock / 64), 1);
             size_t const lds = 32768u * 4u;
-            if (contig)
-                hipLaunchKernelGGL((histogramFastKernel<codec::FmtUInt16, true, true, kTileBlock, true, true>), dim3(g),
-                                   dim3(kTileBlock), lds, s, c);
-            else
-                hipLaunchKernelGGL((histogramFastKernel<codec::FmtUInt16, false, true, kTileBlock, true, true>), dim3(g),
-                                   dim3(kTileBlock), lds, s, c);
-            hipLaunchKernelGGL(histogramFromCodesU16Kernel, dim3(256), dim3(256), 0, s, counts, a.fmt, a.lo, a.hi,
+            tiledWithPartials<true>(c, g, s, [&] {
+                if (contig)
+                    hipLaunchKernelGGL((histogramFastKernel<codec::FmtUInt16, true, true, kTileBlock, true, true>),
+                                       dim3(g), dim3(kTileBlock), lds, s, c);
+                else
+                    hipLaunchKernelGGL((histogramFastKernel<codec::FmtUInt16, false, true, kTileBlock, true, true>),
+                                       dim3(g), dim3(kTileBlock), lds, s, c);
+            });
+            hipLaunchKernelGGL(histogramFromCodesU16Kernel, dim3(65536 / (256 * kFoldCodes)), dim3(256), 0, s, counts,
+                               a.fmt, a.lo, a.hi,
                                hh.scale, hh.numBins, hh.bins);
-            ok = hipGetLastError() == hipSuccess;
         }
         scratch.release(s);
-        return ok;
+        return ok;   // (a failed launch surfaces in the caller's finishLaunch)
     }
 
     // Launches histogramFastKernel when the range qualifies (see its comment); false otherwise.
@@ -2442,9 +2540,9 @@ namespace hipk
             a16.fmt = codec::FmtUInt16;
         if (!makeSpanArgs(a16, h, contig))
             return false;
-        // 16-bit code counts (knob histogram.u16_codes: 1 (default) UInt16 bins beyond one LDS
-        // tile and every Int16 histogram, 2 also UInt16 single-tile bins beyond the replicated
-        // counters, 0 off); integer UInt16 bins keep the streaming kernels below
+        // 16-bit code counts (knob histogram.u16_codes: 2 (default) UInt16 bins beyond the
+        // replicated counters and every Int16 histogram, 1 only UInt16 bins beyond one LDS tile,
+        // 0 off); integer UInt16 bins keep the streaming kernels below
         int64_t const u16k = rt::knob(rt::Knob::HistogramU16Codes);
         if (fmt == codec::FmtInt16)
             return u16k > 0 && launchU16CodeHistogram(h, contig, tileCap, a, hh, s);
@@ -2605,12 +2703,14 @@ namespace hipk
             hipLaunchKernelGGL((histogramFastKernel<FMT, false, true, kTileBlock, SH, true>), dim3(g),             \
                                dim3(kTileBlock), lds, s, h);                                                       \
     } while (0)
-            if (shift)
-                VKT_P16(codec::FmtUInt16, true);
-            else if (fmt == codec::FmtUInt16)
-                VKT_P16(codec::FmtUInt16, false);
-            else
-                VKT_P16(codec::FmtFloat32, false);
+            tiledWithPartials<true>(h, g, s, [&] {
+                if (shift)
+                    VKT_P16(codec::FmtUInt16, true);
+                else if (fmt == codec::FmtUInt16)
+                    VKT_P16(codec::FmtUInt16, false);
+                else
+                    VKT_P16(codec::FmtFloat32, false);
+            });
 #undef VKT_P16
         }
         else
@@ -2621,7 +2721,7 @@ namespace hipk
             {
                 h.tileBase = static_cast<uint32_t>(t * tileCap);
                 h.tileBins = static_cast<uint32_t>(std::min<uint64_t>(tileCap, hh.numBins - h.tileBase));
-                VKT_FAST_HIST_FMT(true, kTileBlock, g, static_cast<size_t>(h.tileBins) * 4u);
+                tiledWithPartials<false>(h, g, s, [&] { VKT_FAST_HIST_FMT(true, kTileBlock, g, static_cast<size_t>(h.tileBins) * 4u); });
             }
         }
 #undef VKT_FAST_HIST_FMT

@@ -262,7 +262,8 @@ namespace rt
             {"resample.lds_pad", 1},
             {"decompose.row_image", 2},
             {"resample.dst_rows", 1},
-            {"histogram.u16_codes", 1},
+            {"histogram.u16_codes", 2},
+            {"histogram.partials", 1},
         };
         static_assert(sizeof(kKnobs) / sizeof(kKnobs[0]) == static_cast<size_t>(Knob::Count), "knob table");
         std::atomic<int64_t> gKnobs[static_cast<int>(Knob::Count)] = {{kKnobs[0].def}, {kKnobs[1].def},
@@ -288,7 +289,7 @@ namespace rt
                                                                   {kKnobs[40].def}, {kKnobs[41].def},
                                                                   {kKnobs[42].def}, {kKnobs[43].def},
                                                                   {kKnobs[44].def}, {kKnobs[45].def},
-                                                                  {kKnobs[46].def}};
+                                                                  {kKnobs[46].def}, {kKnobs[47].def}};
     } // namespace
 
     int64_t knob(Knob k) { return gKnobs[static_cast<int>(k)].load(std::memory_order_relaxed); }

@@ -140,7 +140,8 @@ namespace rt
         ResampleLdsPad,                // LDS gathers: 16 B of padding per 256 B of a staged row (bank spread): 1 UInt8 sources, 2 all, 0 none
         DecomposeRowImage,             // uniform grids of <= 16-KiB bricks through per-row LDS images (brickRowImageKernel): 2 UInt8, 1 all, 0 off
         ResampleDstRows,               // LDS gathers over destination-row tasks (resampleGatherDstRowKernel): 0 off, 1 UInt8 rows not 16-B multiples, >= 2 all (grid cap in 1024s of workgroups)
-        HistogramU16Codes,             // UInt16 float-formula bins through code counts + fold: 1 (default) beyond one LDS tile, 2 also beyond the replicated counters, 0 off
+        HistogramU16Codes,             // 16-bit float-formula bins through code counts + fold: 2 (default) beyond the replicated counters, 1 beyond one LDS tile, 0 off (Int16: always unless 0)
+        HistogramPartials,             // tiled histogram launches store per-workgroup counter words summed by one kernel: 1 (default) packed-16 launches, 2 every tiled launch, 0 global atomics per counter
         Count
     };
     int64_t knob(Knob k);
