@@ -99,9 +99,9 @@ VKTAPI vktError vktHipKernelScopeEnd(vktHipKernelScope scope);
  * "pointwise.general_32bit" (1; 0 makes the general path use
  * its 64-bit addressing, otherwise taken only for operands beyond 4 GiB from their 16-B aligned base), "pointwise.u8_pairs"
  * (1; 0 keeps UInt8 multi-row boxes on the 8-voxel per-item loop instead of 16-B accesses on a
- * 16-voxel row grid), "histogram.packed16" (1; 0 makes histograms with more bins than one LDS
- * tile of 32-bit counters take one pass per tile instead of one pass over packed 16-bit
- * counters), "histogram.mulshift" (1; 0 makes UInt16 histograms whose bins are (code * numBins)
+ * 16-voxel row grid), "histogram.packed16" (2; histograms with more bins than one LDS tile of
+ * 32-bit counters count in packed 16-bit counters, one pass per tile of twice as many bins; 1 only
+ * when one such tile holds every bin; 0 one pass per tile of 32-bit counters), "histogram.mulshift" (1; 0 makes UInt16 histograms whose bins are (code * numBins)
  * >> 16 keep the float bin formula), "histogram.p16_step" (1; 0 runs the packed-16 counters'
  * threshold tests after every item instead of once per wave-step), "render.bricks" (1; 0 makes
  * MultiScattering sample the dense volume instead of its 8^3-brick copy), "decompose.aligned_lds"

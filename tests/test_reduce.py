@@ -328,6 +328,30 @@ def test_histogram_packed16_matches_tiled_passes(fmt):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("fmt,mapping", [(5, (0.0, 1.0)), (5, (-1.0, 3.0)), (7, (0.0, 1.0))])
+@pytest.mark.parametrize("nbins", [100000, 150001, 300000])
+def test_histogram_packed16_tiles(fmt, mapping, nbins):
+    """Knob histogram.packed16 = 2 (round 6): more bins than one packed-16 launch holds, in
+    packed-16 tiles (one pass each, the tile boundary at an even bin) -- vs the oracle: whole
+    volume, padded sub-box, a constant region (flushes inside one tile); UInt16 with the code
+    counts off."""
+    rng = np.random.default_rng(nbins + 3 * fmt)
+    codes = rand_codes(rng, fmt, (40, 100, 256), specials=True)
+    codes[5:9] = codes[5, 0, 0]
+    vol = ob.Volume(codes, fmt, *mapping)
+    lib.vktHipSetTuningKnob(b"histogram.packed16", 2)
+    lib.vktHipSetTuningKnob(b"histogram.u16_codes", 0)
+    try:
+        for first, last in (((0, 0, 0), (256, 100, 40)), ((3, 1, 2), (250, 99, 37))):
+            got = gpu_histogram(codes, fmt, *mapping, first, last, nbins)
+            ref, _ = ob.histogram_range(vol, first, last, nbins)
+            np.testing.assert_array_equal(got, ref, err_msg=f"{first}->{last}")
+    finally:
+        lib.vktHipSetTuningKnob(b"histogram.packed16", -1)
+        lib.vktHipSetTuningKnob(b"histogram.u16_codes", -1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fmt,mapping", [(5, (0.0, 1.0)), (5, (-1.0, 3.0)), (7, (0.0, 1.0))])
 @pytest.mark.parametrize("nbins", [65536, 50001, 100000, 150000])
 def test_histogram_pair_tiles(fmt, mapping, nbins):
     """Knob histogram.pair_tiles = 2: 2-4 tiles of 32-bit counters counted side by side in one
@@ -340,6 +364,7 @@ def test_histogram_pair_tiles(fmt, mapping, nbins):
     vol = ob.Volume(codes, fmt, *mapping)
     lib.vktHipSetTuningKnob(b"histogram.pair_tiles", 2)   # also where P16 would take the bins
     lib.vktHipSetTuningKnob(b"histogram.u16_codes", 0)    # (UInt16 float bins: not the code counts)
+    lib.vktHipSetTuningKnob(b"histogram.packed16", 1)     # (> 81 408 bins: not packed-16 tiles)
     try:
         for first, last in (((0, 0, 0), (256, 100, 40)), ((3, 1, 2), (250, 99, 37))):
             got = gpu_histogram(codes, fmt, *mapping, first, last, nbins)
@@ -348,6 +373,7 @@ def test_histogram_pair_tiles(fmt, mapping, nbins):
     finally:
         lib.vktHipSetTuningKnob(b"histogram.pair_tiles", -1)
         lib.vktHipSetTuningKnob(b"histogram.u16_codes", -1)
+        lib.vktHipSetTuningKnob(b"histogram.packed16", -1)
 
 
 @pytest.mark.gpu

@@ -1094,6 +1094,31 @@ def main():
                 free(V)
         finally:
             lib.vktHipFree(bins)
+    if want("p16tiles"):
+        # knob histogram.packed16 = 2: more bins than one packed-16 launch holds (Float32; UInt16
+        # with the code counts off) in packed-16 tiles, one pass per tile, vs PAIR / 32-bit tiles (1)
+        n = 1024
+        last = Vec3i_t(n, n, n)
+        bins = C.c_void_p()
+        lib.vktHipAllocate(C.byref(bins), 300000 * 8)
+        lib.vktHipSetTuningKnob(b"histogram.u16_codes", 0)
+        try:
+            for fmt, b in ((7, 4), (5, 2)):
+                V = alloc((n,) * 3, fmt, -1.0, 3.0, seed=11 if fmt == 5 else None)
+                if fmt == 7:
+                    rng_fill(V, n ** 3)
+                for nb in (100000, 150000, 300000):
+                    for rep in range(2):
+                        for k in (1, 2):
+                            lib.vktHipSetTuningKnob(b"histogram.packed16", k)
+                            ms = timed(lambda: lib.vktHipHistogramRange(V, o, last, bins, nb, 0), R)
+                            report(f"p16tiles Histogram 1024^3 fmt={fmt} {nb} bins [packed16={k}]", ms, b * n ** 3,
+                                   n ** 3)
+                free(V)
+        finally:
+            lib.vktHipSetTuningKnob(b"histogram.packed16", -1)
+            lib.vktHipSetTuningKnob(b"histogram.u16_codes", -1)
+            lib.vktHipFree(bins)
     if want("partials"):
         # knob histogram.partials: tiled histogram launches store per-workgroup counts summed by
         # one kernel (1) vs global 64-bit atomics per counter (0)
@@ -1163,6 +1188,7 @@ def main():
         lib.vktHipAllocate(C.byref(bins), 150000 * 8)
         last = Vec3i_t(n, n, n)
         lib.vktHipSetTuningKnob(b"histogram.u16_codes", 0)   # (the tiled kernels, not the code counts)
+        lib.vktHipSetTuningKnob(b"histogram.packed16", 1)    # (PAIR, not packed-16 tiles)
         try:
             for fmt, b in ((5, 2), (7, 4)):
                 V = alloc((n,) * 3, fmt, seed=11 if fmt == 5 else None)
@@ -1185,6 +1211,7 @@ def main():
         finally:
             lib.vktHipSetTuningKnob(b"histogram.pair_tiles", -1)
             lib.vktHipSetTuningKnob(b"histogram.u16_codes", -1)
+            lib.vktHipSetTuningKnob(b"histogram.packed16", -1)
             lib.vktHipFree(bins)
     if want("reduce"):
         # ComputeHistogram / ComputeAggregates on a device-resident 1024^3 UInt16

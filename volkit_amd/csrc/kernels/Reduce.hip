@@ -2653,6 +2653,41 @@ namespace hipk
             unsigned const g = streamingGrid(items, 64u * 4u * (kBlock / 64), std::max(1u, perCU));
             VKT_FAST_HIST_FMT(false, kBlock, g, lds);
         }
+        else if (tiles > 1 && fmt != codec::FmtUInt8 && (hh.numBins + 1) / 2 > tileCap &&
+                 rt::knob(rt::Knob::HistogramPacked16) == 2 &&
+                 (hh.numBins + 2ull * tileCap - 1) / (2ull * tileCap) <= kFastMaxTiles)
+        {
+            // packed 16-bit counters in tiles of up to 2 tileCap bins, one pass per tile (more bins
+            // than one packed-16 launch holds: Float32, UInt16 with the code counts off)
+            uint64_t const t16 = (hh.numBins + 2ull * tileCap - 1) / (2ull * tileCap);
+            uint32_t const per = static_cast<uint32_t>(((hh.numBins + t16 - 1) / t16 + 1) & ~1ull);   // even
+            h.rShift = 0;
+            unsigned const g = streamingGrid(items, 64u * 4u * (kTileBlock / 64), 1);
+            for (uint64_t t = 0; t < t16; ++t)
+            {
+                h.tileBase = static_cast<uint32_t>(t * per);
+                h.tileBins = static_cast<uint32_t>(std::min<uint64_t>(per, hh.numBins - h.tileBase));
+                size_t const lds = static_cast<size_t>((h.tileBins + 1) / 2) * 4u;
+                tiledWithPartials<true>(h, g, s, [&] {
+#define VKT_P16T(FMT, SH)                                                                                          \
+    do {                                                                                                           \
+        if (contig)                                                                                                \
+            hipLaunchKernelGGL((histogramFastKernel<FMT, true, true, kTileBlock, SH, true>), dim3(g),              \
+                               dim3(kTileBlock), lds, s, h);                                                       \
+        else                                                                                                       \
+            hipLaunchKernelGGL((histogramFastKernel<FMT, false, true, kTileBlock, SH, true>), dim3(g),             \
+                               dim3(kTileBlock), lds, s, h);                                                       \
+    } while (0)
+                    if (shift)
+                        VKT_P16T(codec::FmtUInt16, true);
+                    else if (fmt == codec::FmtUInt16)
+                        VKT_P16T(codec::FmtUInt16, false);
+                    else
+                        VKT_P16T(codec::FmtFloat32, false);
+#undef VKT_P16T
+                });
+            }
+        }
         else if (tiles > 1 && tiles <= kPairMaxTiles && fmt != codec::FmtUInt8 &&
                  (rt::knob(rt::Knob::HistogramPairTiles) == 2 ||
                   (rt::knob(rt::Knob::HistogramPairTiles) == 1 &&

@@ -221,7 +221,7 @@ namespace rt
             {"pointwise.general", 1},
             {"pointwise.merge_sectors", 1},
             {"pointwise.general_32bit", 1},
-            {"histogram.packed16", 1},
+            {"histogram.packed16", 2},
             {"histogram.mulshift", 1},
             {"histogram.p16_step", 1},
             {"pointwise.u8_pairs", 1},

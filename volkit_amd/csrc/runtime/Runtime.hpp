@@ -99,7 +99,7 @@ namespace rt
         PointwiseGeneral,              // 0: boxes the aligned path cannot take use the scalar kernel
         PointwiseMergeSectors,         // 0: no 64-B sector completion at row ends
         PointwiseGeneral32,            // 0: the general path uses 64-bit addressing everywhere (tests)
-        HistogramPacked16,             // 0: histograms beyond one LDS tile take one pass per tile
+        HistogramPacked16,             // 2 (default): packed 16-bit counters, in tiles beyond one launch; 1: one launch only (beyond: PAIR / 32-bit tiles); 0: one pass per 32-bit tile
         HistogramMulShift,             // 0: UInt16 bins other than code >> s keep the float formula
         HistogramP16Step,              // 0: P16 threshold tests after each item, not each wave-step
         PointwiseU8Pairs,              // 0: UInt8 multi-row boxes keep the 8-voxel per-item loop
