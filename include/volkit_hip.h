@@ -119,9 +119,10 @@ VKTAPI vktError vktHipKernelScopeEnd(vktHipKernelScope scope);
  * own hipMalloc instead of a 2-MiB aligned block of an arena chunk), "memory.arena_chunk_mib" (0; > 0 makes
  * new arena chunks exactly max(request, value MiB): tests), "decompose.block" (256; 128 copies each
  * 16-KiB BrickDecompose chunk with 128 threads), "pointwise.dword_shift" (1; 0 keeps the byte-align
- * stage of the general path's window shift for 4-byte voxels at 4-B aligned addresses), "aggregates.moments" (3; bit 0: UInt16
+ * stage of the general path's window shift for 4-byte voxels at 4-B aligned addresses), "aggregates.moments" (7; bit 0: UInt16
  * ComputeAggregates under the unit mapping from one pass of exact integer moments, bit 1: UInt16
- * under other mappings and Float32 from one pass of floating-point moments -- both instead of
+ * under other mappings and Float32 from one pass of floating-point moments, bit 2 (with bit 1):
+ * Int16 and UInt32 the same -- all instead of
  * "aggregates.codes" / the two float passes), "aggregates.moments_pipe" (1; integer-moments kernel
  * variant: 0 one register buffer of 4 items per lane and wave-step, 1 two buffers of 4 (the next
  * step's loads in flight during this step's arithmetic), 2 two of 8, 3 one of 8, 4 two of 2, 5 as 1

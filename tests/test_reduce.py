@@ -445,9 +445,10 @@ def test_histogram_partials(partials):
 
 
 def takes_moments(fmt, mapping):
-    """UInt16 (integer moments under the unit mapping, float moments otherwise) and Float32 (float
-    moments) take the one-pass moments paths (aggregates.moments)."""
-    return fmt in (5, 7)
+    """UInt16 (integer moments under the unit mapping, float moments otherwise), Float32, Int16 and
+    UInt32 (float moments; the last two since round 6) take the one-pass moments paths
+    (aggregates.moments)."""
+    return fmt in (5, 7, 2, 6)
 
 
 def check_var(got_var, var_terms, moments, what=""):
@@ -880,7 +881,8 @@ def test_aggregates_float_moments_and_fallbacks():
             lib.vktHipSetTuningKnob(b"aggregates.moments", -1)
         return got, two
 
-    for fmt, mapping in ((5, (-1.0, 3.0)), (5, (1000.0, 1000.001)), (5, (3.0, -1.0)), (7, (0.0, 1.0))):
+    for fmt, mapping in ((5, (-1.0, 3.0)), (5, (1000.0, 1000.001)), (5, (3.0, -1.0)), (7, (0.0, 1.0)),
+                         (2, (-1.0, 3.0)), (2, (1000.0, 1000.001)), (6, (0.25, 7.5)), (6, (3.0, -1.0))):
         codes = rand_codes(rng, fmt, (12, 24, 520))
         if fmt == 7:
             vals = codes.view(np.float32)
@@ -891,7 +893,15 @@ def test_aggregates_float_moments_and_fallbacks():
             check_aggregates(got, codes, fmt, mapping, first, last, what)
             assert (got.min, got.max, tuple(got.argmin), tuple(got.argmax)) == \
                 (two.min, two.max, tuple(two.argmin), tuple(two.argmax)), what
-    # fallbacks: bit-identical to the two passes
+    # fallbacks: bit-identical to the two passes -- Int16 / UInt32 mappings whose values are tiny
+    # (Int16: found per code on the host; UInt32: flagged per voxel)
+    for fmt, mapping in ((2, (-1e-20, 1e-20)), (6, (-1e-20, 1e-20))):
+        codes = rand_codes(rng, fmt, (8, 16, 256))
+        got, two = both(codes, fmt, mapping, (0, 0, 0), (256, 16, 8))
+        for f in ("min", "max", "sum", "mean", "var", "stddev", "prod"):
+            assert np.array_equal(np.float32(getattr(got, f)), np.float32(getattr(two, f)), equal_nan=True), \
+                f"fmt={fmt} {f}"
+        assert tuple(got.argmin) == tuple(two.argmin) and tuple(got.argmax) == tuple(two.argmax)
     base = rng.uniform(-1.0, 1.0, (8, 16, 256)).astype(np.float32)
     specials = {"nan": np.nan, "inf": np.inf, "huge": 3.0e30, "tiny": 1.0e-20, "denormal": 1.0e-40}
     for name, val in specials.items():

@@ -1084,15 +1084,19 @@ def main():
     if want("aggfix"):
         # ComputeAggregates per call at 256^3 / 512^3 for every format (fixed cost vs voxels)
         names = {2: "Int16", 4: "UInt8", 5: "UInt16", 6: "UInt32", 7: "Float32"}
-        for m in (256, 512):
+        for m in (256, 512, 1024):
             lastm = Vec3i_t(m, m, m)
             for fmt in (4, 5, 7, 2, 6):
                 A = alloc((m,) * 3, fmt, seed=1)
                 if fmt == 7:
                     rng_fill(A, m ** 3)
                 agg = _lib.Aggregates_t()
-                report(f"aggfix Aggregates {m}^3 {names[fmt]}",
-                       timed(lambda: lib.vktHipAggregatesRange(A, o, lastm, C.byref(agg)), R), BPV[fmt] * m ** 3, m ** 3)
+                for k in ((3, 7) if fmt in (2, 6) else (-1,)):
+                    lib.vktHipSetTuningKnob(b"aggregates.moments", k)
+                    report(f"aggfix Aggregates {m}^3 {names[fmt]} [moments={k}]",
+                           timed(lambda: lib.vktHipAggregatesRange(A, o, lastm, C.byref(agg)), R), BPV[fmt] * m ** 3,
+                           m ** 3)
+                lib.vktHipSetTuningKnob(b"aggregates.moments", -1)
                 free(A)
     if want("p16size"):
         # the packed-16 histogram (UInt16, 65 536 integer bins) over volume sizes: time vs voxels

@@ -1849,11 +1849,12 @@ namespace hipk
         return p;
     }
 
-    // FMT UInt16 (any mapping but the unit one, which takes the integer kernel) or Float32.
+    // FMT UInt16 (any mapping but the unit one, which takes the integer kernel), Float32, and
+    // (round 6) Int16 / UInt32 under any mapping.
     template <int FMT, bool CONTIG>
     __global__ __launch_bounds__(kBlock) void aggregatesMomentsFKernel(FastHistArgs h, MomentPartialF* partials)
     {
-        constexpr int BPV = FMT == codec::FmtUInt16 ? 2 : 4;
+        constexpr int BPV = FMT == codec::FmtUInt16 || FMT == codec::FmtInt16 ? 2 : 4;
         constexpr int U = 4;
         uint32_t const lane = threadIdx.x & 63;
         MomentPartialF p = emptyMomentF();
@@ -1935,7 +1936,7 @@ namespace hipk
                     p.prod *= x;
                 float const a = fabsf(v[j]);
                 bad = bad || !(a <= FLT_MAX);
-                if constexpr (FMT == codec::FmtFloat32)
+                if constexpr (FMT == codec::FmtFloat32 || FMT == codec::FmtUInt32)   // (per voxel: 2^32 codes)
                     tiny = tiny || (a < kTinyValue && a != 0.f);
             }
             n += static_cast<uint32_t>(__builtin_popcount(m));
@@ -3008,19 +3009,20 @@ namespace hipk
         return momentGridItemsU16(h.items, contig);
     }
 
-    // 1 when some UInt16 code decodes to a nonzero |v| < 2^-40 under (lo, hi): every code once on
-    // the host, the answer kept per thread for the last mapping
-    uint32_t tinyCodesU16(float lo, float hi)
+    // 1 when some UInt16 (Int16) code decodes to a nonzero |v| < 2^-40 under (lo, hi): every code
+    // once on the host, the answer kept per thread for the last mapping
+    uint32_t tinyCodesU16(float lo, float hi, int32_t fmt = codec::FmtUInt16)
     {
         thread_local uint64_t lastKey = ~0ull;
         thread_local uint32_t lastTiny = 0;
-        uint64_t const key = static_cast<uint64_t>(codec::floatToBits(lo)) << 32 | codec::floatToBits(hi);
+        uint64_t const key = (static_cast<uint64_t>(codec::floatToBits(lo)) << 32 | codec::floatToBits(hi)) ^
+                             (fmt == codec::FmtInt16 ? 1ull << 63 | 1ull : 0ull);
         if (key != lastKey)
         {
             uint32_t t = 0;
             for (uint32_t c = 0; c < 65536u && !t; ++c)
             {
-                float const v = std::fabs(codec::decode(c, codec::FmtUInt16, lo, hi));
+                float const v = std::fabs(codec::decode(c, fmt, lo, hi));
                 t = v != 0.f && v < 0x1p-40f ? 1u : 0u;
             }
             lastKey = key;
@@ -3035,29 +3037,40 @@ namespace hipk
     unsigned momentGridF(BoxArgs const& a, FastHistArgs& h, bool& contig, uint32_t& tiny)
     {
         tiny = 0;
-        bool const fmtOk = (a.fmt == codec::FmtUInt16 && !codec::isUnitMapping(a.lo, a.hi)) || a.fmt == codec::FmtFloat32;
-        if (!fmtOk || (rt::knob(rt::Knob::AggregatesMoments) & 2) == 0 || !makeSpanArgs(a, h, contig))
+        bool const fmtOk = (a.fmt == codec::FmtUInt16 && !codec::isUnitMapping(a.lo, a.hi)) || a.fmt == codec::FmtFloat32 ||
+                           ((a.fmt == codec::FmtInt16 || a.fmt == codec::FmtUInt32) &&
+                            (rt::knob(rt::Knob::AggregatesMoments) & 4) != 0);
+        BoxArgs w = a;   // (Int16 / UInt32: the item walk of the 2- / 4-byte span)
+        if (a.fmt == codec::FmtInt16)
+            w.fmt = codec::FmtUInt16;
+        else if (a.fmt == codec::FmtUInt32)
+            w.fmt = codec::FmtFloat32;
+        if (!fmtOk || (rt::knob(rt::Knob::AggregatesMoments) & 2) == 0 || !makeSpanArgs(w, h, contig))
             return 0;
-        if (a.fmt == codec::FmtUInt16)
-            tiny = tinyCodesU16(a.lo, a.hi);
+        if (a.fmt == codec::FmtUInt16 || a.fmt == codec::FmtInt16)
+            tiny = tinyCodesU16(a.lo, a.hi, a.fmt);
         return streamingGrid(h.items, 64u * 4u * (kBlock / 64), 8);
     }
 
     void launchMomentsF(FastHistArgs const& h, bool contig, int32_t fmt, unsigned g, double numElems, uint32_t tiny,
                         MomentPartialF* parts, vktHipAggregatePartial_t* res, hipStream_t s)
     {
+#define VKT_MOMF(FMT)                                                                                            \
+    do {                                                                                                         \
+        if (contig)                                                                                              \
+            hipLaunchKernelGGL((aggregatesMomentsFKernel<FMT, true>), dim3(g), dim3(kBlock), 0, s, h, parts);   \
+        else                                                                                                     \
+            hipLaunchKernelGGL((aggregatesMomentsFKernel<FMT, false>), dim3(g), dim3(kBlock), 0, s, h, parts);  \
+    } while (0)
         if (fmt == codec::FmtUInt16)
-        {
-            if (contig)
-                hipLaunchKernelGGL((aggregatesMomentsFKernel<codec::FmtUInt16, true>), dim3(g), dim3(kBlock), 0, s, h, parts);
-            else
-                hipLaunchKernelGGL((aggregatesMomentsFKernel<codec::FmtUInt16, false>), dim3(g), dim3(kBlock), 0, s, h,
-                                   parts);
-        }
-        else if (contig)
-            hipLaunchKernelGGL((aggregatesMomentsFKernel<codec::FmtFloat32, true>), dim3(g), dim3(kBlock), 0, s, h, parts);
+            VKT_MOMF(codec::FmtUInt16);
+        else if (fmt == codec::FmtInt16)
+            VKT_MOMF(codec::FmtInt16);
+        else if (fmt == codec::FmtUInt32)
+            VKT_MOMF(codec::FmtUInt32);
         else
-            hipLaunchKernelGGL((aggregatesMomentsFKernel<codec::FmtFloat32, false>), dim3(g), dim3(kBlock), 0, s, h, parts);
+            VKT_MOMF(codec::FmtFloat32);
+#undef VKT_MOMF
         hipLaunchKernelGGL(aggregatesMomentsFFinalKernel, dim3(1), dim3(kBlock), 0, s, parts, g, numElems, tiny, res);
     }
 

@@ -236,7 +236,7 @@ namespace rt
             {"decompose.grid", 1},
             {"memory.pool", 1},
             {"memory.arena", 1},
-            {"aggregates.moments", 3},
+            {"aggregates.moments", 7},
             {"memory.arena_chunk_mib", 0},
             {"decompose.block", 256},
             {"pointwise.dword_shift", 1},

@@ -114,7 +114,7 @@ namespace rt
         DecomposeGrid,                 // 0: uniform brick grids keep the per-brick descriptor table
         MemoryPool,                    // 0: every device buffer from its own hipMalloc (no small-block pool)
         MemoryArena,                   // 0: buffers > 4 MiB from their own hipMalloc (no arena chunks)
-        AggregatesMoments,             // ComputeAggregates in one pass of moments: bit 0 UInt16 unit mapping (integer), bit 1 UInt16 other mappings / Float32 (float)
+        AggregatesMoments,             // ComputeAggregates in one pass of moments: bit 0 UInt16 unit mapping (integer), bit 1 UInt16 other mappings / Float32 (float), bit 2 (with bit 1) Int16 / UInt32 (float)
         MemoryArenaChunkMiB,           // > 0: arena chunks of exactly max(request, this many MiB) (tests)
         DecomposeBlock,                // threads per BrickDecompose workgroup over one 16-KiB chunk: 256 or 128
         PointwiseDwordShift,           // 0: 4-byte general-path windows keep the byte-align stage (whole-dword offsets)
