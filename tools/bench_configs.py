@@ -1081,6 +1081,15 @@ def main():
                 free(A, B2, D, S, Rd)
         finally:
             lib.vktHipFree(bins)
+    if want("f32small"):
+        # Float32 Linear Resample at small sizes (fixed cost vs voxels)
+        for se, de in ((256, 512), (512, 1024), (384, 512)):
+            S = alloc((se,) * 3, 7)
+            rng_fill(S, se ** 3)
+            Rv = alloc((de,) * 3, 7)
+            report(f"f32small Resample {se}^3->{de}^3 Float32 Linear", timed(lambda: lib.vktHipResample(Rv, S, 1), R),
+                   4 * se ** 3 + 4 * de ** 3, de ** 3)
+            free(S, Rv)
     if want("aggfix"):
         # ComputeAggregates per call at 256^3 / 512^3 for every format (fixed cost vs voxels)
         names = {2: "Int16", 4: "UInt8", 5: "UInt16", 6: "UInt32", 7: "Float32"}
