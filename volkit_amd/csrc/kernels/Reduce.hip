@@ -2396,7 +2396,7 @@ namespace hipk
             return;
         uint32_t const r0 = blockIdx.y * kPartialRows;
         uint32_t const r1 = min(groups, r0 + kPartialRows);
-        uint32_t lo = 0, hi = 0;   // (<= 32 rows of < 2^16 / 2^32 - per-workgroup counts: no overflow for PACKED)
+        uint32_t lo = 0, hi = 0;   // PACKED: <= 32 rows of 16-bit halves (< 2^16 each, the in-run flush) fit 32 bits
         unsigned long long wide = 0ull;
 #pragma unroll 8
         for (uint32_t r = r0; r < r1; ++r)
@@ -2479,8 +2479,9 @@ namespace hipk
             atomicAdd(&bins[runBin], run);
     }
 
-    // UInt16 bins that are not a function of code >> s / (code * n) >> 16 and do not fit one LDS
-    // tile (knob histogram.u16_codes): a UInt16 voxel holds one of 65 536
+    // UInt16 bins that are not a function of code >> s / (code * n) >> 16 and do not fit the
+    // replicated counters (knob histogram.u16_codes, default 2; 1: only beyond one LDS tile;
+    // DESIGN §4.8 round 6): a UInt16 voxel holds one of 65 536
     // codes and its bin depends on the code alone, so the data pass counts codes -- the P16
     // kernel with the identity bin (SHIFT, code >> 0), one pass whatever the bin count -- and a
     // 65 536-thread kernel folds the counts into the bins.  Same counts as the per-voxel bin, by
